@@ -1,0 +1,198 @@
+"""Headline benchmark: voice-to-intent p50 latency (ms) + ASR RTF, 10 s utterance, Llama-3-8B brain.
+
+One step = one voice command end to end on the on-node engines:
+    10 s PCM16 16 kHz utterance -> pcm16->f32 (HIP) -> Whisper log-mel (HIP) -> encoder -> greedy
+    decode of the transcript (fixed work: 4 text tokens per second of audio) -> ParseRequest
+    {text: transcript, context} -> Llama-3-8B intent parse (prefix-cached prompt, grammar-
+    constrained + jump-forward decoding, <= 512 output chars) -> ParseResponse validation.
+
+This replaces the reference path Deepgram STT -> 1 s debounce -> OpenAI JSON mode
+(apps/voice/src/server.ts:111-231, apps/brain/src/server.ts:89-139).  `value` is the p50
+ENGINE latency (audio fully received -> validated intent); `parity_p50_ms` adds the
+reference's fixed 1000 ms debounce (apps/voice/src/server.ts:229).
+
+Multi-GPU (torchrun, one process per GPU, RCCL): weak scaling -- every rank serves its own
+voice sessions (ASR data-parallel, one LLM replica per rank, or TP groups with --tp);
+the reported p50 is over ALL sessions of all ranks.
+
+Data: synthetic speech-like audio, random-init weights of the named architectures.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from voice_enabled_browser_automation_amd import ops  # noqa: E402
+from voice_enabled_browser_automation_amd.asr.engine import AsrEngine  # noqa: E402
+from voice_enabled_browser_automation_amd.brain.intent_engine import LLMIntentEngine  # noqa: E402
+from voice_enabled_browser_automation_amd.brain.prompt import COMMANDS  # noqa: E402
+from voice_enabled_browser_automation_amd.contracts import ParseResponse, safe_parse  # noqa: E402
+from voice_enabled_browser_automation_amd.models.config import get_config  # noqa: E402
+from voice_enabled_browser_automation_amd.models.llama import LlamaModel  # noqa: E402
+from voice_enabled_browser_automation_amd.models.whisper import WhisperModel  # noqa: E402
+from voice_enabled_browser_automation_amd.parallel.tp import init_distributed  # noqa: E402
+from voice_enabled_browser_automation_amd.runtime.engine import LLMEngine  # noqa: E402
+from voice_enabled_browser_automation_amd.tokenizer import load_tokenizer  # noqa: E402
+
+METRIC = "voice-to-intent p50 latency (ms) + ASR RTF; 10s utterance; Llama-3-8B brain"
+
+
+def synth_speech(seconds: float, seed: int, rate: int = 16000) -> np.ndarray:
+    """Speech-like PCM16: voiced segments (f0 + 3 formants, syllable-rate AM) and pauses."""
+    rng = np.random.default_rng(seed)
+    n = int(seconds * rate)
+    t = np.arange(n) / rate
+    f0 = 110 + 30 * np.sin(2 * np.pi * 0.3 * t + rng.uniform(0, 6))
+    phase = 2 * np.pi * np.cumsum(f0) / rate
+    sig = np.zeros(n)
+    for k, (f, a) in enumerate(((700, 1.0), (1200, 0.5), (2600, 0.25))):
+        sig += a * np.sin(phase * (k + 1) + rng.uniform(0, 6)) * (1 + 0.3 * np.sin(2 * np.pi * f / 400 * t))
+    env = np.clip(np.sin(2 * np.pi * 4.0 * t + rng.uniform(0, 6)), 0, None) ** 0.5
+    words = (np.sin(2 * np.pi * 0.7 * t + rng.uniform(0, 6)) > -0.6).astype(float)
+    sig = sig * env * words + 0.02 * rng.standard_normal(n)
+    sig = sig / (np.abs(sig).max() + 1e-9) * 0.6
+    return (sig * 32767).astype(np.int16)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--asr", default=os.environ.get("VWA_ASR_MODEL", "whisper-tiny"))
+    ap.add_argument("--llm", default=os.environ.get("VWA_LLM_MODEL", "llama3-8b"))
+    ap.add_argument("--tp", type=int, default=int(os.environ.get("VWA_TP", "1")))
+    ap.add_argument("--audio-s", type=float, default=10.0)
+    ap.add_argument("--asr-tokens-per-s", type=float, default=4.0)
+    ap.add_argument("--budget-chars", type=int, default=512)
+    ap.add_argument("--debounce-ms", type=float, default=1000.0, help="reference debounce added for parity_p50_ms")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--verbose", action="store_true")
+    args = ap.parse_args()
+
+    tp = init_distributed(tp_size=args.tp if int(os.environ.get("WORLD_SIZE", "1")) > 1 else None)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (MI355X)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    ops.ext()  # native kernels are mandatory
+    use_graphs = not args.no_graphs
+
+    t_load = time.time()
+    wcfg, lcfg = get_config(args.asr), get_config(args.llm)
+    whisper = WhisperModel(wcfg, device=dev, seed=1)
+    asr = AsrEngine(whisper, load_tokenizer("whisper"), max_sessions=2, use_graphs=use_graphs)
+    llama = LlamaModel(lcfg, device=dev, tp=tp, seed=2)
+    engine = LLMEngine(llama, max_seqs=4, max_model_len=2048, use_graphs=use_graphs)
+    brain = LLMIntentEngine(engine, load_tokenizer("llama3"), budget_chars=args.budget_chars, temperature=0.1,
+                            seed=1234 + rank)
+    engine.capture_all()
+    torch.cuda.synchronize()
+    load_s = time.time() - t_load
+
+    asr_tokens = int(math.ceil(args.audio_s * args.asr_tokens_per_s))
+    utterances = [synth_speech(args.audio_s, seed=100 * rank + i) for i in range(8)]
+
+    def one(i: int):
+        pcm = utterances[i % len(utterances)]
+        t0 = time.perf_counter()
+        audio = asr.pcm_to_audio(pcm)
+        text = asr.transcribe(audio, exact_tokens=asr_tokens)
+        t_asr = time.perf_counter()
+        cmd = COMMANDS[i % len(COMMANDS)]
+        req = {"text": text if text.strip() else cmd, "context": {"url": "https://www.bestbuy.com"}}
+        out = brain.parse(req)
+        ok = safe_parse(ParseResponse, out).success
+        t1 = time.perf_counter()
+        return (t1 - t0) * 1e3, (t_asr - t0) * 1e3, ok
+
+    for i in range(args.warmup):
+        one(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    lat, asr_ms, oks, llm_stats = [], [], [], []
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        l, a, ok = one(args.warmup + i)
+        lat.append(l)
+        asr_ms.append(a)
+        oks.append(ok)
+        llm_stats.append(dict(brain.last_stats))
+        if args.verbose and rank == 0:
+            print(json.dumps({"step": i, "latency_ms": round(l, 2), "asr_ms": round(a, 2), **brain.last_stats}),
+                  flush=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = (time.perf_counter() - t_start) * 1e3
+
+    # gather every session's latency across ranks (weak scaling: p50 over all sessions)
+    local_t = torch.tensor([elapsed] + lat + asr_ms + [float(sum(oks))], dtype=torch.float64, device=dev)
+    if world > 1:
+        allt = [torch.zeros_like(local_t) for _ in range(world)]
+        torch.distributed.all_gather(allt, local_t)
+    else:
+        allt = [local_t]
+    K = args.steps
+    elapsed_max = max(float(t[0]) for t in allt)
+    all_lat = [float(x) for t in allt for x in t[1 : 1 + K]]
+    all_asr = [float(x) for t in allt for x in t[1 + K : 1 + 2 * K]]
+    n_ok = sum(int(t[-1]) for t in allt)
+    if rank == 0:
+        p50 = statistics.median(all_lat)
+        rtf = statistics.median(all_asr) / (args.audio_s * 1e3)
+        dec = [s.get("decode_steps", 0) for s in llm_stats]
+        res = {
+            "metric": METRIC,
+            "value": round(p50, 3),
+            "unit": "ms",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max / K, 3),
+            "higher_is_better": False,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic 16 kHz speech-like audio, random-init weights",
+            "config": {"model": f"{args.asr} + {args.llm}", "global_batch": world // tp.size, "seq_len": None,
+                       "parallelism": f"dp{world // tp.size}" + (f"-tp{tp.size}" if tp.size > 1 else ""),
+                       "audio_s": args.audio_s, "asr_tokens": asr_tokens, "budget_chars": args.budget_chars,
+                       "hipgraph": use_graphs},
+            "asr_rtf": round(rtf, 5),
+            "p90_ms": round(float(np.percentile(all_lat, 90)), 3),
+            "parity_p50_ms": round(p50 + args.debounce_ms, 3),
+            "asr_p50_ms": round(statistics.median(all_asr), 3),
+            "llm_p50_ms": round(statistics.median([a - b for a, b in zip(all_lat, all_asr)]), 3),
+            "llm_decode_steps_mean": round(sum(dec) / max(1, len(dec)), 2),
+            "llm_forced_tokens_mean": round(sum(s.get("forced_tokens", 0) for s in llm_stats) / max(1, K), 2),
+            "llm_prefill_tokens_mean": round(sum(s.get("prefill_tokens", 0) for s in llm_stats) / max(1, K), 2),
+            "valid_intents": f"{n_ok}/{len(all_lat)}",
+            "throughput_utt_per_s": round(len(all_lat) / (elapsed_max / 1e3), 3),
+            "load_s": round(load_s, 1),
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,413 @@
+// PyTorch bindings for the gfx950 kernel library.
+//
+// Every entry point validates shapes/dtypes/devices on the host BEFORE launching (a bad
+// shape must never reach a kernel: an out-of-bounds access can reset the whole node), then
+// launches on the current HIP stream of the tensor's device -- so each op is capturable in a
+// torch.cuda.CUDAGraph (= hipGraph on ROCm).
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "kernels/vwa_kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+// torch-ROCm exposes GPUs as device type "cuda"; the masquerading accessor returns the stream
+// torch itself launches on (including the capture stream inside torch.cuda.graph).
+hipStream_t cur_stream(const Tensor& t) {
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
+}
+
+const uint16_t* bfp(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+uint16_t* bfp_mut(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+const uint16_t* bfp_opt(const c10::optional<Tensor>& t) { return t.has_value() ? bfp(*t) : nullptr; }
+
+void check_bf16(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+}
+void check_contig_rows(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2, name, " must be 2-D");
+  TORCH_CHECK(t.stride(1) == 1, name, " must be row-contiguous");
+  TORCH_CHECK(t.stride(0) % 8 == 0, name, " row stride must be a multiple of 8 elements");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name, " must be 16-byte aligned");
+}
+void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, what, " launch failed with code ", rc); }
+
+SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool fuse_rms, double eps) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_contig_rows(x, "x");
+  TORCH_CHECK(w.is_contiguous() && w.dim() == 2, "w must be contiguous [N, K]");
+  TORCH_CHECK(x.size(1) == w.size(1), "K mismatch: x ", x.sizes(), " w ", w.sizes());
+  TORCH_CHECK(x.size(0) >= 1 && x.size(0) <= 64, "skinny_gemm supports 1..64 rows, got ", x.size(0));
+  TORCH_CHECK(w.size(1) % 128 == 0, "K must be a multiple of 128");
+  if (bias.has_value()) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->numel() == w.size(0) && bias->is_contiguous(), "bias must be [N]");
+  }
+  SkinnyParams p{};
+  p.X = bfp(x);
+  p.ldx = (int)x.stride(0);
+  p.W = bfp(w);
+  p.M = (int)x.size(0);
+  p.N = (int)w.size(0);
+  p.K = (int)w.size(1);
+  p.bias = bfp_opt(bias);
+  p.fuse_rms = fuse_rms ? 1 : 0;
+  p.eps = (float)eps;
+  return p;
+}
+
+// epi: 0 store, 1 residual add, 3 gelu
+void skinny_gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi, bool fuse_rms, double eps,
+                 c10::optional<Tensor> residual) {
+  c10::DeviceGuard g(x.device());
+  SkinnyParams p = base_params(x, w, bias, fuse_rms, eps);
+  TORCH_CHECK(epi == 0 || epi == 1 || epi == 3, "bad epilogue");
+  TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be a 2-D row-contiguous GPU tensor");
+  TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) == w.size(0), "y shape mismatch");
+  TORCH_CHECK(y.scalar_type() == at::kBFloat16 || y.scalar_type() == at::kFloat, "y must be bf16 or f32");
+  p.Y = y.data_ptr();
+  p.ldy = (int)y.stride(0);
+  p.y_f32 = y.scalar_type() == at::kFloat;
+  if (epi == 1) {
+    TORCH_CHECK(residual.has_value(), "residual epilogue needs residual");
+    check_bf16(*residual, "residual");
+    TORCH_CHECK(residual->dim() == 2 && residual->size(0) == x.size(0) && residual->size(1) == w.size(0) &&
+                    residual->stride(1) == 1,
+                "residual shape mismatch");
+    p.R = bfp(*residual);
+    p.ldr = (int)residual->stride(0);
+  }
+  check_rc(vwa_skinny_gemm((int)epi, &p, cur_stream(x)), "skinny_gemm");
+}
+
+void skinny_gemm_swiglu(Tensor x, Tensor w_gu, c10::optional<Tensor> bias, Tensor h, bool fuse_rms, double eps) {
+  c10::DeviceGuard g(x.device());
+  SkinnyParams p = base_params(x, w_gu, bias, fuse_rms, eps);
+  check_bf16(h, "h");
+  TORCH_CHECK(h.dim() == 2 && h.stride(1) == 1 && h.size(0) == x.size(0) && h.size(1) * 2 == w_gu.size(0),
+              "h must be [M, N/2]");
+  TORCH_CHECK(w_gu.size(0) % 32 == 0, "gate/up rows must be a multiple of 32");
+  p.Y = h.data_ptr();
+  p.ldy = (int)h.stride(0);
+  check_rc(vwa_skinny_gemm(2, &p, cur_stream(x)), "skinny_gemm_swiglu");
+}
+
+void check_cache(const Tensor& c, const char* name) {
+  check_bf16(c, name);
+  TORCH_CHECK(c.dim() == 4 && c.is_contiguous(), name, " must be contiguous [blocks, kv_heads, block_size, head_dim]");
+}
+
+void skinny_gemm_qkv(Tensor x, Tensor w_qkv, c10::optional<Tensor> bias, bool fuse_rms, double eps, int64_t n_q_heads,
+                     int64_t n_kv_heads, int64_t head_dim, bool use_rope, Tensor positions, Tensor slots,
+                     c10::optional<Tensor> rope, Tensor q_out, Tensor k_cache, Tensor v_cache) {
+  c10::DeviceGuard g(x.device());
+  SkinnyParams p = base_params(x, w_qkv, bias, fuse_rms, eps);
+  TORCH_CHECK(w_qkv.size(0) == (n_q_heads + 2 * n_kv_heads) * head_dim, "w_qkv rows mismatch");
+  TORCH_CHECK(head_dim % 16 == 0, "head_dim must be a multiple of 16");
+  TORCH_CHECK(positions.scalar_type() == at::kInt && positions.numel() >= x.size(0), "positions int32 [M]");
+  TORCH_CHECK(slots.scalar_type() == at::kLong && slots.numel() >= x.size(0), "slots int64 [M]");
+  check_bf16(q_out, "q_out");
+  TORCH_CHECK(q_out.dim() == 2 && q_out.size(0) >= x.size(0) && q_out.size(1) == n_q_heads * head_dim, "q_out shape");
+  check_cache(k_cache, "k_cache");
+  check_cache(v_cache, "v_cache");
+  TORCH_CHECK(k_cache.size(1) == n_kv_heads && k_cache.size(3) == head_dim, "cache shape mismatch");
+  if (use_rope) {
+    TORCH_CHECK(rope.has_value() && rope->scalar_type() == at::kFloat && rope->is_contiguous(), "rope table f32");
+    TORCH_CHECK(rope->size(-2) == head_dim / 2, "rope table must be [max_pos, head_dim/2, 2]");
+  }
+  p.n_q_heads = (int)n_q_heads;
+  p.n_kv_heads = (int)n_kv_heads;
+  p.head_dim = (int)head_dim;
+  p.use_rope = use_rope ? 1 : 0;
+  p.positions = positions.data_ptr<int>();
+  p.slots = slots.data_ptr<int64_t>();
+  p.rope = use_rope ? rope->data_ptr<float>() : nullptr;
+  p.q_out = bfp_mut(q_out);
+  p.ldq = (int)q_out.stride(0);
+  p.k_cache = bfp_mut(k_cache);
+  p.v_cache = bfp_mut(v_cache);
+  p.block_size = (int)k_cache.size(2);
+  p.cache_stride_block = k_cache.stride(0);
+  p.cache_stride_head = k_cache.stride(1);
+  p.cache_stride_tok = k_cache.stride(2);
+  check_rc(vwa_skinny_gemm(4, &p, cur_stream(x)), "skinny_gemm_qkv");
+}
+
+void rmsnorm(Tensor x, c10::optional<Tensor> residual, c10::optional<Tensor> residual_out, c10::optional<Tensor> w,
+             Tensor y, double eps) {
+  c10::DeviceGuard g(x.device());
+  check_bf16(x, "x");
+  check_contig_rows(x, "x");
+  check_bf16(y, "y");
+  TORCH_CHECK(y.is_contiguous() && y.sizes() == x.sizes(), "y shape");
+  const int rows = (int)x.size(0), D = (int)x.size(1);
+  if (residual.has_value()) {
+    TORCH_CHECK(residual_out.has_value() && residual->is_contiguous() && residual_out->is_contiguous() &&
+                    residual->sizes() == x.sizes() && residual_out->sizes() == x.sizes(),
+                "residual shapes");
+  }
+  if (w.has_value()) TORCH_CHECK(w->numel() == D, "w must be [D]");
+  check_rc(vwa_rmsnorm(bfp(x), bfp_opt(residual), residual_out.has_value() ? bfp_mut(*residual_out) : nullptr,
+                       bfp_opt(w), bfp_mut(y), rows, D, (int)x.stride(0), (float)eps, cur_stream(x)),
+           "rmsnorm");
+}
+
+void layernorm(Tensor x, c10::optional<Tensor> residual, c10::optional<Tensor> residual_out, Tensor w, Tensor b,
+               Tensor y, double eps) {
+  c10::DeviceGuard g(x.device());
+  check_bf16(x, "x");
+  check_contig_rows(x, "x");
+  TORCH_CHECK(y.is_contiguous() && y.sizes() == x.sizes(), "y shape");
+  const int rows = (int)x.size(0), D = (int)x.size(1);
+  TORCH_CHECK(w.numel() == D && b.numel() == D, "w/b must be [D]");
+  if (residual.has_value())
+    TORCH_CHECK(residual_out.has_value() && residual->sizes() == x.sizes() && residual_out->sizes() == x.sizes() &&
+                    residual->is_contiguous() && residual_out->is_contiguous(),
+                "residual shapes");
+  check_rc(vwa_layernorm(bfp(x), bfp_opt(residual), residual_out.has_value() ? bfp_mut(*residual_out) : nullptr,
+                         bfp(w), bfp(b), bfp_mut(y), rows, D, (int)x.stride(0), (float)eps, cur_stream(x)),
+           "layernorm");
+}
+
+void rope_kv_write(Tensor qkv, int64_t n_q_heads, int64_t n_kv_heads, int64_t head_dim, bool use_rope,
+                   Tensor positions, Tensor slots, c10::optional<Tensor> rope, Tensor q_out, Tensor k_cache,
+                   Tensor v_cache) {
+  c10::DeviceGuard g(qkv.device());
+  check_bf16(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.size(1) == (n_q_heads + 2 * n_kv_heads) * head_dim,
+              "qkv shape");
+  const int rows = (int)qkv.size(0);
+  TORCH_CHECK(positions.scalar_type() == at::kInt && positions.numel() >= rows, "positions");
+  TORCH_CHECK(slots.scalar_type() == at::kLong && slots.numel() >= rows, "slots");
+  TORCH_CHECK(q_out.dim() == 2 && q_out.size(0) >= rows && q_out.size(1) == n_q_heads * head_dim, "q_out");
+  check_cache(k_cache, "k_cache");
+  check_cache(v_cache, "v_cache");
+  if (use_rope) TORCH_CHECK(rope.has_value() && rope->scalar_type() == at::kFloat, "rope table");
+  check_rc(vwa_rope_kv_write(bfp(qkv), (int)qkv.stride(0), rows, (int)n_q_heads, (int)n_kv_heads, (int)head_dim,
+                             use_rope ? 1 : 0, positions.data_ptr<int>(), slots.data_ptr<int64_t>(),
+                             use_rope ? rope->data_ptr<float>() : nullptr, bfp_mut(q_out), (int)q_out.stride(0),
+                             bfp_mut(k_cache), bfp_mut(v_cache), (int)k_cache.size(2), k_cache.stride(0),
+                             k_cache.stride(1), k_cache.stride(2), cur_stream(qkv)),
+           "rope_kv_write");
+}
+
+void swiglu(Tensor gu, Tensor h) {
+  c10::DeviceGuard g(gu.device());
+  check_bf16(gu, "gu");
+  TORCH_CHECK(gu.is_contiguous() && h.is_contiguous() && gu.dim() == 2 && h.dim() == 2 && gu.size(0) == h.size(0) &&
+                  gu.size(1) == 2 * h.size(1),
+              "swiglu shapes");
+  check_rc(vwa_swiglu(bfp(gu), bfp_mut(h), (int)h.size(0), (int)h.size(1), cur_stream(gu)), "swiglu");
+}
+
+void bias_act(Tensor x, c10::optional<Tensor> bias, c10::optional<Tensor> residual, Tensor y, int64_t act) {
+  c10::DeviceGuard g(x.device());
+  check_bf16(x, "x");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.dim() == 2 && y.sizes() == x.sizes(), "bias_act shapes");
+  if (bias.has_value()) TORCH_CHECK(bias->numel() == x.size(1), "bias");
+  if (residual.has_value()) TORCH_CHECK(residual->sizes() == x.sizes() && residual->is_contiguous(), "residual");
+  check_rc(vwa_bias_act(bfp(x), bfp_opt(bias), bfp_opt(residual), bfp_mut(y), (int)x.size(0), (int)x.size(1),
+                        (int)act, cur_stream(x)),
+           "bias_act");
+}
+
+KVView make_view(const Tensor& k, const Tensor& v, const Tensor& table, int64_t block_size, int64_t sb, int64_t sh,
+                 int64_t stok) {
+  check_bf16(k, "k");
+  check_bf16(v, "v");
+  TORCH_CHECK(table.scalar_type() == at::kInt && table.dim() == 2 && table.is_contiguous(), "block table int32 2-D");
+  KVView kv{};
+  kv.k = bfp(k);
+  kv.v = bfp(v);
+  kv.block_table = table.data_ptr<int>();
+  kv.table_stride = (int)table.stride(0);
+  kv.block_size = (int)block_size;
+  kv.stride_block = sb;
+  kv.stride_head = sh;
+  kv.stride_tok = stok;
+  return kv;
+}
+
+void decode_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_size, int64_t sb, int64_t sh,
+                      int64_t stok, Tensor ctx_lens, Tensor seq_ids, int64_t n_q_heads, int64_t n_kv_heads,
+                      int64_t head_dim, double scale, int64_t n_splits, Tensor part_o, Tensor part_ml, Tensor out) {
+  c10::DeviceGuard g(q.device());
+  check_bf16(q, "q");
+  TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && q.size(1) == n_q_heads * head_dim, "q shape");
+  const int rows = (int)q.size(0);
+  TORCH_CHECK(ctx_lens.scalar_type() == at::kInt && ctx_lens.numel() >= rows, "ctx_lens");
+  TORCH_CHECK(seq_ids.scalar_type() == at::kInt && seq_ids.numel() >= rows, "seq_ids");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) >= rows && out.size(1) == n_q_heads * head_dim && out.stride(1) == 1,
+              "out shape");
+  TORCH_CHECK(n_splits >= 1, "n_splits");
+  if (n_splits > 1) {
+    TORCH_CHECK(part_o.scalar_type() == at::kFloat && part_o.numel() >= (int64_t)rows * n_splits * n_q_heads * head_dim,
+                "part_o too small");
+    TORCH_CHECK(part_ml.scalar_type() == at::kFloat && part_ml.numel() >= (int64_t)rows * n_splits * n_q_heads * 2,
+                "part_ml too small");
+  }
+  DecodeAttnParams p{};
+  p.q = bfp(q);
+  p.ldq = (int)q.stride(0);
+  p.kv = make_view(k, v, table, block_size, sb, sh, stok);
+  p.ctx_lens = ctx_lens.data_ptr<int>();
+  p.seq_ids = seq_ids.data_ptr<int>();
+  p.rows = rows;
+  p.n_q_heads = (int)n_q_heads;
+  p.n_kv_heads = (int)n_kv_heads;
+  p.head_dim = (int)head_dim;
+  p.scale = (float)scale;
+  p.split_tokens = vwa_attention_split_tokens();
+  p.n_splits = (int)n_splits;
+  p.part_o = part_o.data_ptr<float>();
+  p.part_ml = part_ml.data_ptr<float>();
+  p.out = bfp_mut(out);
+  p.ldo = (int)out.stride(0);
+  check_rc(vwa_decode_attention(&p, cur_stream(q)), "decode_attention");
+}
+
+void flash_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_size, int64_t sb, int64_t sh,
+                     int64_t stok, Tensor out, int64_t Sk, int64_t n_kv_heads, bool causal, int64_t q_offset,
+                     c10::optional<Tensor> q_offsets, c10::optional<Tensor> k_lens, double scale) {
+  c10::DeviceGuard g(q.device());
+  check_bf16(q, "q");
+  TORCH_CHECK(q.dim() == 4, "q must be [B, S, H, D]");
+  TORCH_CHECK(q.stride(3) == 1 && out.stride(3) == 1 && out.sizes() == q.sizes(), "q/out layout");
+  const int64_t D = q.size(3);
+  TORCH_CHECK((q.stride(2) % 8) == 0 && (q.stride(1) % 8) == 0, "q strides must be 16-byte multiples");
+  FlashAttnParams p{};
+  p.q = bfp(q);
+  p.q_stride_b = q.stride(0);
+  p.q_stride_s = q.stride(1);
+  p.q_stride_h = q.stride(2);
+  p.kv = make_view(k, v, table, block_size, sb, sh, stok);
+  p.o = bfp_mut(out);
+  p.o_stride_b = out.stride(0);
+  p.o_stride_s = out.stride(1);
+  p.o_stride_h = out.stride(2);
+  p.B = (int)q.size(0);
+  p.Sq = (int)q.size(1);
+  p.Sk = (int)Sk;
+  p.n_q_heads = (int)q.size(2);
+  p.n_kv_heads = (int)n_kv_heads;
+  p.head_dim = (int)D;
+  p.causal = causal ? 1 : 0;
+  p.q_offset = (int)q_offset;
+  p.q_offsets = q_offsets.has_value() ? q_offsets->data_ptr<int>() : nullptr;
+  p.k_lens = k_lens.has_value() ? k_lens->data_ptr<int>() : nullptr;
+  p.scale = (float)scale;
+  check_rc(vwa_flash_attention(&p, cur_stream(q)), "flash_attention");
+}
+
+void embedding(Tensor ids, Tensor table, c10::optional<Tensor> pos_table, c10::optional<Tensor> positions, Tensor out,
+               int64_t vocab_start) {
+  c10::DeviceGuard g(ids.device());
+  TORCH_CHECK(ids.scalar_type() == at::kInt, "ids int32");
+  check_bf16(table, "table");
+  TORCH_CHECK(table.is_contiguous() && out.is_contiguous() && out.size(1) == table.size(1), "embedding shapes");
+  const int rows = (int)out.size(0);
+  TORCH_CHECK(ids.numel() >= rows, "ids too short");
+  if (pos_table.has_value()) TORCH_CHECK(positions.has_value() && positions->scalar_type() == at::kInt, "positions");
+  check_rc(vwa_embedding(ids.data_ptr<int>(), bfp(table), bfp_opt(pos_table),
+                         positions.has_value() ? positions->data_ptr<int>() : nullptr, bfp_mut(out), rows,
+                         (int)table.size(1), (int)vocab_start, (int)(vocab_start + table.size(0)), cur_stream(ids)),
+           "embedding");
+}
+
+void sample(Tensor logits, c10::optional<Tensor> mask, c10::optional<Tensor> temperature, Tensor seed, Tensor step,
+            Tensor out_tokens, Tensor part_val, Tensor part_idx) {
+  c10::DeviceGuard g(logits.device());
+  TORCH_CHECK(logits.scalar_type() == at::kFloat && logits.dim() == 2 && logits.stride(1) == 1, "logits f32 2-D");
+  const int rows = (int)logits.size(0), V = (int)logits.size(1);
+  int mask_words = 0;
+  if (mask.has_value()) {
+    TORCH_CHECK(mask->scalar_type() == at::kInt && mask->dim() == 2 && mask->is_contiguous() && mask->size(0) >= rows,
+                "mask int32 [rows, words]");
+    mask_words = (int)mask->size(1);
+    TORCH_CHECK(mask_words * 32 >= V, "mask too short");
+  }
+  if (temperature.has_value())
+    TORCH_CHECK(temperature->scalar_type() == at::kFloat && temperature->numel() >= rows, "temperature");
+  TORCH_CHECK(seed.scalar_type() == at::kLong && step.scalar_type() == at::kInt, "seed int64, step int32");
+  TORCH_CHECK(out_tokens.scalar_type() == at::kInt && out_tokens.numel() >= rows, "out_tokens");
+  const int n_chunks = (int)(part_val.numel() / rows);
+  TORCH_CHECK(n_chunks >= 1 && part_idx.numel() >= (int64_t)rows * n_chunks, "partials");
+  check_rc(vwa_sample(logits.data_ptr<float>(), (int)logits.stride(0), rows, V,
+                      mask.has_value() ? reinterpret_cast<const uint32_t*>(mask->data_ptr<int>()) : nullptr,
+                      mask_words, temperature.has_value() ? temperature->data_ptr<float>() : nullptr,
+                      reinterpret_cast<const uint64_t*>(seed.data_ptr<int64_t>()), step.data_ptr<int>(),
+                      out_tokens.data_ptr<int>(), part_val.data_ptr<float>(), part_idx.data_ptr<int>(), n_chunks,
+                      cur_stream(logits)),
+           "sample");
+}
+
+void pcm16_to_f32(Tensor pcm, Tensor out, double ratio) {
+  c10::DeviceGuard g(pcm.device());
+  TORCH_CHECK(pcm.scalar_type() == at::kShort && out.scalar_type() == at::kFloat, "pcm int16 -> f32");
+  TORCH_CHECK(pcm.is_contiguous() && out.is_contiguous(), "contiguous");
+  const int n_in = (int)pcm.numel(), n_out = (int)out.numel();
+  TORCH_CHECK((int64_t)((n_out - 1) * ratio) < (int64_t)n_in + 1, "resample ratio overruns input");
+  check_rc(vwa_pcm16_to_f32(pcm.data_ptr<int16_t>(), out.data_ptr<float>(), n_in, n_out, (float)ratio, cur_stream(pcm)),
+           "pcm16_to_f32");
+}
+
+void log_mel(Tensor audio, int64_t n_frames, Tensor window, Tensor cos_table, Tensor mel_fb, Tensor mel_scratch,
+             Tensor max_buf, Tensor out) {
+  c10::DeviceGuard g(audio.device());
+  TORCH_CHECK(audio.scalar_type() == at::kFloat && audio.is_contiguous(), "audio f32");
+  TORCH_CHECK(window.numel() == 400 && cos_table.numel() == 400, "n_fft=400 tables");
+  const int n_mels = (int)mel_fb.size(0);
+  TORCH_CHECK(mel_fb.size(1) == 201 && mel_fb.is_contiguous() && mel_fb.scalar_type() == at::kFloat, "mel_fb [n_mels,201]");
+  TORCH_CHECK(mel_scratch.numel() >= n_frames * n_mels && max_buf.numel() >= 1, "scratch");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.dim() == 2 && out.size(0) >= n_frames && out.size(1) == n_mels &&
+                  out.stride(1) == 1,
+              "out bf16 [frames, n_mels]");
+  TORCH_CHECK(audio.numel() > 200, "audio too short");
+  check_rc(vwa_log_mel(audio.data_ptr<float>(), (int)audio.numel(), (int)n_frames, window.data_ptr<float>(),
+                       cos_table.data_ptr<float>(), nullptr, mel_fb.data_ptr<float>(), n_mels,
+                       mel_scratch.data_ptr<float>(), max_buf.data_ptr<float>(), bfp_mut(out), (int)out.stride(0),
+                       cur_stream(audio)),
+           "log_mel");
+}
+
+void conv1d_gelu(Tensor x, Tensor w, c10::optional<Tensor> b, c10::optional<Tensor> pos, Tensor y, int64_t stride) {
+  c10::DeviceGuard g(x.device());
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  TORCH_CHECK(x.dim() == 3 && x.is_contiguous(), "x must be [B, T, Cin] contiguous");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) == 3 * x.size(2), "w must be [Cout, 3*Cin] ([co][kk][ci])");
+  TORCH_CHECK(y.dim() == 3 && y.is_contiguous() && y.size(0) == x.size(0) && y.size(2) == w.size(0), "y [B, Tout, Cout]");
+  const int Tin = (int)x.size(1), Tout = (int)y.size(1);
+  TORCH_CHECK(Tout == (Tin + 2 - 3) / stride + 1, "Tout mismatch");
+  if (pos.has_value()) TORCH_CHECK(pos->dim() == 2 && pos->size(0) >= Tout && pos->size(1) == w.size(0), "pos shape");
+  check_rc(vwa_conv1d_gelu_pos(bfp(x), bfp(w), bfp_opt(b), bfp_opt(pos), bfp_mut(y), (int)x.size(0), (int)x.size(2),
+                               Tin, (int)w.size(0), Tout, (int)stride, cur_stream(x)),
+           "conv1d_gelu");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "MI355X (gfx950) HIP kernels for the voice-web-agent inference engine";
+  m.def("skinny_gemm", &skinny_gemm);
+  m.def("skinny_gemm_swiglu", &skinny_gemm_swiglu);
+  m.def("skinny_gemm_qkv", &skinny_gemm_qkv);
+  m.def("rmsnorm", &rmsnorm);
+  m.def("layernorm", &layernorm);
+  m.def("rope_kv_write", &rope_kv_write);
+  m.def("swiglu", &swiglu);
+  m.def("bias_act", &bias_act);
+  m.def("decode_attention", &decode_attention);
+  m.def("flash_attention", &flash_attention);
+  m.def("embedding", &embedding);
+  m.def("sample", &sample);
+  m.def("pcm16_to_f32", &pcm16_to_f32);
+  m.def("log_mel", &log_mel);
+  m.def("conv1d_gelu", &conv1d_gelu);
+  m.def("attention_split_tokens", []() { return vwa_attention_split_tokens(); });
+}

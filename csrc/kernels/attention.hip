@@ -1,0 +1,375 @@
+// Attention kernels for gfx950.
+//
+// 1) decode_attention (K10, K7): one query row per (sequence | forced token), paged KV,
+//    GQA group of G q-heads per kv-head handled by one workgroup so each K/V byte is read
+//    once per group.  Split-K over the context (64 keys per single-wave workgroup; lane = key
+//    for Q.K, lane = (16-byte dim chunk, token group) for P.V), partials merged by
+//    attn_combine (log-sum-exp).  The grid is sized for the maximum context so the launch
+//    shape is static under hipGraph capture; splits past a row's context exit early.
+//    Also serves Whisper cross-attention (contiguous encoder K/V expressed as one block).
+//
+// 2) flash_attention (K5, K6): MFMA (16x16x32 bf16) flash-attention forward for prefill and
+//    for the Whisper encoder.  "Swapped" formulation: each wave computes S^T = K.Q^T for its
+//    16 queries so a query's scores sit in one lane column; P^T is then already the B
+//    operand of O^T += V^T.P^T (no LDS round trip for P), and the online-softmax row
+//    reductions are 2 cross-lane steps.  K is staged XOR-swizzled (conflict-free
+//    ds_read_b128), V is staged transposed with a padded row.  Causal masking with an
+//    absolute query offset supports prefix-cached prefill (queries at positions
+//    q_offset.., keys 0..).
+#include "common.h"
+#include "vwa_kernels.h"
+
+using namespace vwa;
+
+namespace {
+
+VWA_DEVICE int64_t kv_offset(const KVView& kv, int seq, int kvh, int t) {
+  const int blk = kv.block_table[(int64_t)seq * kv.table_stride + t / kv.block_size];
+  return (int64_t)blk * kv.stride_block + (int64_t)kvh * kv.stride_head + (int64_t)(t % kv.block_size) * kv.stride_tok;
+}
+
+constexpr int kSplit = 64;  // keys per decode workgroup (one wave)
+
+// One wave per (row, kv head, 64-key split).  Q.K: lane = key, the key row streamed with
+// D/8 independent 16-byte loads.  P.V: lane = (16-byte dim chunk, token group), every V row
+// chunk is one 16-byte load, all issued before the first FMA; token groups are reduced with
+// two/three xor-shuffles.  No LDS round trip except the tiny q / p broadcast arrays.
+template <int D, int G>
+__global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
+  __shared__ __attribute__((aligned(16))) float qs[G][D];
+  __shared__ float sc[G][kSplit];
+
+  const int nkv = p.n_kv_heads;
+  const int row = blockIdx.x / nkv, kvh = blockIdx.x % nkv;
+  const int split = blockIdx.y;
+  const int ctx = p.ctx_lens[row];
+  const int seq = p.seq_ids[row];
+  const int t0 = split * kSplit;
+  const int lane = threadIdx.x;
+  const bool single = (p.n_splits == 1);
+  const int nq = p.n_q_heads;
+
+  if (t0 >= ctx) {
+    if (!single && lane < G) {
+      float* pm = p.part_ml + (((int64_t)row * p.n_splits + split) * nq + kvh * G + lane) * 2;
+      pm[0] = -INFINITY;
+      pm[1] = 0.f;
+    }
+    return;
+  }
+  const int tend = min(ctx, t0 + kSplit);
+
+  for (int i = lane; i < G * D; i += 64) {
+    const int g = i / D, d = i % D;
+    qs[g][d] = bf2f(p.q[(int64_t)row * p.ldq + (kvh * G + g) * D + d]) * p.scale;
+  }
+  __syncthreads();
+
+  // ---- Q.K (lane = key)
+  const int t = t0 + lane;
+  float s[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) s[g] = 0.f;
+  if (t < tend) {
+    const uint4* kr = reinterpret_cast<const uint4*>(p.kv.k + kv_offset(p.kv, seq, kvh, t));
+    uint4 kv4[D / 8];
+#pragma unroll
+    for (int c = 0; c < D / 8; ++c) kv4[c] = kr[c];
+#pragma unroll
+    for (int c = 0; c < D / 8; ++c) {
+      float kf[8];
+      unpack8(kv4[c], kf);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float4 qa = *reinterpret_cast<const float4*>(&qs[g][c * 8]);
+        const float4 qb = *reinterpret_cast<const float4*>(&qs[g][c * 8 + 4]);
+        s[g] += qa.x * kf[0] + qa.y * kf[1] + qa.z * kf[2] + qa.w * kf[3] + qb.x * kf[4] + qb.y * kf[5] +
+                qb.z * kf[6] + qb.w * kf[7];
+      }
+    }
+  }
+  float mrow[G], lrow[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const float v = (t < tend) ? s[g] : -INFINITY;
+    const float m = wave_max(v);
+    const float e = (t < tend) ? __expf(v - m) : 0.f;
+    lrow[g] = wave_sum(e);
+    mrow[g] = m;
+    sc[g][lane] = e;
+  }
+  __syncthreads();
+
+  // ---- P.V (lane = dim chunk c, token group tg)
+  constexpr int NCH = D / 8;        // 16-byte chunks per row
+  constexpr int TG = 64 / NCH;      // token groups
+  constexpr int NI = kSplit / TG;   // tokens per lane
+  const int c = lane % NCH, tg = lane / NCH;
+  uint4 vv[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int tt = t0 + tg + TG * i;
+    vv[i] = (tt < tend) ? *reinterpret_cast<const uint4*>(p.kv.v + kv_offset(p.kv, seq, kvh, tt) + c * 8)
+                        : make_uint4(0, 0, 0, 0);
+  }
+  float o[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    float vf[8];
+    unpack8(vv[i], vf);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const float pg = sc[g][tg + TG * i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[g][j] += pg * vf[j];
+    }
+  }
+#pragma unroll
+  for (int off = NCH; off < 64; off <<= 1)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[g][j] += __shfl_xor(o[g][j], off, 64);
+
+  if (tg == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int h = kvh * G + g;
+      if (single) {
+        const float inv = 1.f / lrow[g];
+        float ov[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ov[j] = o[g][j] * inv;
+        *reinterpret_cast<uint4*>(p.out + (int64_t)row * p.ldo + h * D + c * 8) = pack8(ov);
+      } else {
+        float* po = p.part_o + (((int64_t)row * p.n_splits + split) * nq + h) * D + c * 8;
+        *reinterpret_cast<float4*>(po) = make_float4(o[g][0], o[g][1], o[g][2], o[g][3]);
+        *reinterpret_cast<float4*>(po + 4) = make_float4(o[g][4], o[g][5], o[g][6], o[g][7]);
+        if (c == 0) {
+          float* pm = p.part_ml + (((int64_t)row * p.n_splits + split) * nq + h) * 2;
+          pm[0] = mrow[g];
+          pm[1] = lrow[g];
+        }
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(D) void attn_combine_kernel(DecodeAttnParams p) {
+  const int row = blockIdx.x / p.n_q_heads, h = blockIdx.x % p.n_q_heads;
+  const int d = threadIdx.x;
+  const int ctx = p.ctx_lens[row];
+  const int ns = min(p.n_splits, (ctx + kSplit - 1) / kSplit);
+  float M = -INFINITY;
+  for (int s = 0; s < ns; ++s) M = fmaxf(M, p.part_ml[(((int64_t)row * p.n_splits + s) * p.n_q_heads + h) * 2]);
+  float acc = 0.f, L = 0.f;
+  for (int s = 0; s < ns; ++s) {
+    const float* pm = p.part_ml + (((int64_t)row * p.n_splits + s) * p.n_q_heads + h) * 2;
+    if (pm[0] == -INFINITY) continue;
+    const float f = __expf(pm[0] - M);
+    L += pm[1] * f;
+    acc += p.part_o[(((int64_t)row * p.n_splits + s) * p.n_q_heads + h) * D + d] * f;
+  }
+  p.out[(int64_t)row * p.ldo + h * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+}
+
+template <int D, int G>
+void launch_decode(const DecodeAttnParams& p, hipStream_t st) {
+  hipLaunchKernelGGL((decode_attn_kernel<D, G>), dim3(p.rows * p.n_kv_heads, p.n_splits), dim3(64), 0, st, p);
+  if (p.n_splits > 1)
+    hipLaunchKernelGGL((attn_combine_kernel<D>), dim3(p.rows * p.n_q_heads), dim3(D), 0, st, p);
+}
+
+template <int D>
+int dispatch_g(const DecodeAttnParams& p, hipStream_t st) {
+  switch (p.n_q_heads / p.n_kv_heads) {
+    case 1: launch_decode<D, 1>(p, st); break;
+    case 2: launch_decode<D, 2>(p, st); break;
+    case 4: launch_decode<D, 4>(p, st); break;
+    case 8: launch_decode<D, 8>(p, st); break;
+    default: return -2;
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// flash attention forward (MFMA)
+// ------------------------------------------------------------------------------------------
+constexpr int kBQ = 64;   // queries per workgroup (4 waves x 16)
+constexpr int kBK = 64;   // keys per tile
+constexpr int kVTP = kBK + 4;  // padded V^T row (elements)
+
+template <int D, bool CAUSAL>
+__global__ __launch_bounds__(256) void flash_attn_kernel(FlashAttnParams p) {
+  constexpr int NCH = D / 8;       // 16-byte chunks per K row
+  constexpr int NDS = D / 32;      // MFMA k-steps over head dim
+  constexpr int NDT = D / 16;      // 16-row d tiles of O^T
+  __shared__ __attribute__((aligned(16))) u16 ks[kBK * D];
+  __shared__ __attribute__((aligned(16))) u16 vt[D * kVTP];
+
+  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int kvh = h / (p.n_q_heads / p.n_kv_heads);
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int ql = lane & 15, g = lane >> 4;
+  const int qoff = p.q_offsets ? p.q_offsets[b] : p.q_offset;
+  const int Sk = p.k_lens ? p.k_lens[b] : p.Sk;
+  const int qi = qb * kBQ + w * 16 + ql;  // query index within the batch row
+  const int qpos = qoff + qi;
+  const float sl2 = p.scale * 1.4426950408889634f;
+
+  // Q^T fragments (B operand): Q[q][ds*32 + 8g + j], pre-scaled by scale*log2(e)
+  bf16x8 qf[NDS];
+  {
+    const u16* qr = p.q + (int64_t)b * p.q_stride_b + (int64_t)qi * p.q_stride_s + (int64_t)h * p.q_stride_h;
+#pragma unroll
+    for (int ds = 0; ds < NDS; ++ds) {
+      float f[8];
+      if (qi < p.Sq) unpack8(*reinterpret_cast<const uint4*>(qr + ds * 32 + 8 * g), f);
+      else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= sl2;
+      qf[ds] = as_bf16x8(pack8(f));
+    }
+  }
+
+  f32x4 oacc[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) oacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  int k_end = Sk;
+  if (CAUSAL) k_end = min(Sk, qoff + qb * kBQ + kBQ);
+  for (int k0 = 0; k0 < k_end; k0 += kBK) {
+    // ---- stage K (swizzled rows) and V^T into LDS
+    for (int c = threadIdx.x; c < kBK * NCH; c += 256) {
+      const int r = c / NCH, ch = c % NCH;
+      const int t = k0 + r;
+      uint4 kv4 = make_uint4(0, 0, 0, 0), vv4 = make_uint4(0, 0, 0, 0);
+      if (t < Sk) {
+        const int64_t off = kv_offset(p.kv, b, kvh, t) + ch * 8;
+        kv4 = *reinterpret_cast<const uint4*>(p.kv.k + off);
+        vv4 = *reinterpret_cast<const uint4*>(p.kv.v + off);
+      }
+      *reinterpret_cast<uint4*>(&ks[r * D + ((ch ^ (r % NCH)) * 8)]) = kv4;
+      const u16* ve = reinterpret_cast<const u16*>(&vv4);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vt[(ch * 8 + j) * kVTP + r] = ve[j];
+    }
+    __syncthreads();
+
+    // ---- S^T = K . Q^T  (4 key blocks of 16)
+    f32x4 s[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int r = kb * 16 + ql;
+#pragma unroll
+      for (int ds = 0; ds < NDS; ++ds) {
+        const int ch = ds * 4 + g;
+        const uint4 a = *reinterpret_cast<const uint4*>(&ks[r * D + ((ch ^ (r % NCH)) * 8)]);
+        s[kb] = mfma16(as_bf16x8(a), qf[ds], s[kb]);
+      }
+    }
+    // ---- mask + online softmax (column = this lane's query)
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int kidx = k0 + kb * 16 + 4 * g + i;
+        const bool ok = (kidx < Sk) && (!CAUSAL || kidx <= qpos);
+        if (!ok) s[kb][i] = -INFINITY;
+        tmax = fmaxf(tmax, s[kb][i]);
+      }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float m_new = fmaxf(m_run, tmax);
+    const float alpha = (m_run == -INFINITY) ? 0.f : exp2f(m_run - m_new);
+    const bool any = (m_new != -INFINITY);
+    float psum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = (any && s[kb][i] != -INFINITY) ? exp2f(s[kb][i] - m_new) : 0.f;
+        s[kb][i] = e;
+        psum += e;
+      }
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) oacc[dt] *= alpha;
+
+    // ---- O^T += V^T . P^T  (2 k-steps of 32 keys)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      float pf[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pf[i] = s[2 * kk][i];
+        pf[4 + i] = s[2 * kk + 1][i];
+      }
+      const bf16x8 pb = as_bf16x8(pack8(pf));
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const int d = dt * 16 + ql;
+        const uint2 lo = *reinterpret_cast<const uint2*>(&vt[d * kVTP + 32 * kk + 4 * g]);
+        const uint2 hi = *reinterpret_cast<const uint2*>(&vt[d * kVTP + 32 * kk + 16 + 4 * g]);
+        const uint4 a = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        oacc[dt] = mfma16(as_bf16x8(a), pb, oacc[dt]);
+      }
+    }
+    __syncthreads();
+  }
+
+  float l_tot = l_run + __shfl_xor(l_run, 16, 64);
+  l_tot += __shfl_xor(l_tot, 32, 64);
+  if (qi < p.Sq) {
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+    u16* orow = p.o + (int64_t)b * p.o_stride_b + (int64_t)qi * p.o_stride_s + (int64_t)h * p.o_stride_h;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      uint2 v;
+      v.x = pack2(oacc[dt][0] * inv, oacc[dt][1] * inv);
+      v.y = pack2(oacc[dt][2] * inv, oacc[dt][3] * inv);
+      *reinterpret_cast<uint2*>(orow + dt * 16 + 4 * g) = v;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int vwa_decode_attention(const DecodeAttnParams* p, hipStream_t st) {
+  if (p->n_kv_heads <= 0 || p->n_q_heads % p->n_kv_heads) return -1;
+  int r;
+  if (p->head_dim == 128) r = dispatch_g<128>(*p, st);
+  else if (p->head_dim == 64) r = dispatch_g<64>(*p, st);
+  else return -3;
+  if (r) return r;
+  return (int)hipGetLastError();
+}
+
+extern "C" int vwa_flash_attention(const FlashAttnParams* p, hipStream_t st) {
+  if (p->n_kv_heads <= 0 || p->n_q_heads % p->n_kv_heads) return -1;
+  dim3 grid((p->Sq + kBQ - 1) / kBQ, p->n_q_heads, p->B);
+  if (p->head_dim == 128) {
+    if (p->causal) hipLaunchKernelGGL((flash_attn_kernel<128, true>), grid, dim3(256), 0, st, *p);
+    else hipLaunchKernelGGL((flash_attn_kernel<128, false>), grid, dim3(256), 0, st, *p);
+  } else if (p->head_dim == 64) {
+    if (p->causal) hipLaunchKernelGGL((flash_attn_kernel<64, true>), grid, dim3(256), 0, st, *p);
+    else hipLaunchKernelGGL((flash_attn_kernel<64, false>), grid, dim3(256), 0, st, *p);
+  } else {
+    return -3;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int vwa_attention_split_tokens() { return kSplit; }

@@ -1,0 +1,95 @@
+// Shared device helpers for the gfx950 (MI355X, CDNA4) kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * activations / weights are bf16 stored as uint16_t bit patterns; math is f32;
+//  * 16-byte vector loads (8 x bf16) everywhere on memory-bound paths;
+//  * wave = 64 lanes; block sizes are multiples of 64;
+//  * MFMA: __builtin_amdgcn_mfma_f32_16x16x32_bf16, lane maps:
+//      A: lane l holds A[row l&15][k 8*(l>>4)+j], j=0..7
+//      B: lane l holds B[k 8*(l>>4)+j][col l&15]
+//      C: lane l holds C[row 4*(l>>4)+i][col l&15], i=0..3
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define VWA_DEVICE __device__ __forceinline__
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t u16;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+namespace vwa {
+
+constexpr int kWave = 64;
+
+VWA_DEVICE float bf2f(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+VWA_DEVICE u16 f2bf(float f) {
+  // round-to-nearest-even via the hardware convert (v_cvt_pk_bf16_f32 on gfx950); keeps NaN a NaN
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(u16, b);
+}
+
+VWA_DEVICE uint32_t pack2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+// unpack a 16-byte vector of 8 bf16 into f32
+VWA_DEVICE void unpack8(const uint4& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+VWA_DEVICE uint4 pack8(const float* f) {
+  uint4 r;
+  r.x = pack2(f[0], f[1]); r.y = pack2(f[2], f[3]);
+  r.z = pack2(f[4], f[5]); r.w = pack2(f[6], f[7]);
+  return r;
+}
+
+// streaming (non-temporal) 16-byte load: weights are read once per decode step
+VWA_DEVICE uint4 load_nt(const void* p) {
+  u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+VWA_DEVICE bf16x8 as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
+
+VWA_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+VWA_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+VWA_DEVICE int lane_id() { return threadIdx.x & 63; }
+
+VWA_DEVICE f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+VWA_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
+
+VWA_DEVICE float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+// Bijective XCD-aware remap of a 1-D block index (8 XCDs, each with a private L2):
+// consecutive logical tiles land on the same XCD so neighbouring tiles share L2 lines.
+VWA_DEVICE int xcd_remap(int bid, int nwg) {
+  const int nx = 8;
+  if (nwg < nx) return bid;
+  int q = nwg / nx, r = nwg % nx;
+  int x = bid % nx, i = bid / nx;
+  int base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + i;
+}
+
+}  // namespace vwa

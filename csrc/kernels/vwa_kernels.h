@@ -1,0 +1,92 @@
+// Host-visible launch interface of the gfx950 kernel library (C ABI, raw pointers + hipStream_t).
+// The torch binding layer (csrc/bindings.cpp) is the only caller; every launcher is
+// graph-capture safe (no allocation, no synchronisation, only the given stream).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct SkinnyParams {
+  const uint16_t* X; int ldx;
+  const uint16_t* W;
+  int M, N, K;
+  const uint16_t* bias;
+  int fuse_rms; float eps;
+  void* Y; int ldy; int y_f32;
+  const uint16_t* R; int ldr;
+  int n_q_heads, n_kv_heads, head_dim, use_rope;
+  const int* positions;
+  const int64_t* slots;
+  const float* rope;
+  uint16_t* q_out; int ldq;
+  uint16_t* k_cache; uint16_t* v_cache;
+  int block_size;
+  int64_t cache_stride_block, cache_stride_head, cache_stride_tok;
+};
+
+// Paged / strided KV addressing shared by the attention kernels:
+//   addr(seq b, kv head h, token t) = base + table[b*table_stride + t/block_size]*stride_block
+//                                     + h*stride_head + (t%block_size)*stride_tok
+struct KVView {
+  const uint16_t* k; const uint16_t* v;
+  const int* block_table; int table_stride;
+  int block_size;
+  int64_t stride_block, stride_head, stride_tok;
+};
+
+struct DecodeAttnParams {
+  const uint16_t* q; int ldq;       // [rows, n_q_heads*D]
+  KVView kv;
+  const int* ctx_lens;              // [rows] number of keys visible to the row
+  const int* seq_ids;               // [rows] row -> block-table row
+  int rows, n_q_heads, n_kv_heads, head_dim;
+  float scale;
+  int split_tokens;                 // keys per split workgroup
+  int n_splits;                     // max splits (grid.y)
+  float* part_o; float* part_ml;    // [rows][n_splits][n_q_heads][D], [rows][n_splits][n_q_heads][2]
+  uint16_t* out; int ldo;           // [rows, n_q_heads*D]
+};
+
+struct FlashAttnParams {
+  const uint16_t* q; int64_t q_stride_b, q_stride_s, q_stride_h;   // q[b][s][h][d]
+  KVView kv;                        // keys of sequence b: table row b
+  uint16_t* o; int64_t o_stride_b, o_stride_s, o_stride_h;
+  int B, Sq, Sk, n_q_heads, n_kv_heads, head_dim;
+  int causal;
+  int q_offset;                     // absolute position of query 0 (causal: key j visible iff j <= q_offset+i)
+  const int* q_offsets;             // optional per-batch q offsets
+  const int* k_lens;                // optional per-batch key counts
+  float scale;
+};
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+int vwa_skinny_gemm(int epi, const SkinnyParams* p, hipStream_t st);
+int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
+                uint16_t* y, int rows, int D, int ldx, float eps, hipStream_t st);
+int vwa_layernorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
+                  const uint16_t* b, uint16_t* y, int rows, int D, int ldx, float eps, hipStream_t st);
+int vwa_rope_kv_write(const uint16_t* qkv, int ldqkv, int rows, int n_q_heads, int n_kv_heads, int head_dim,
+                      int use_rope, const int* positions, const int64_t* slots, const float* rope, uint16_t* q_out,
+                      int ldq, uint16_t* k_cache, uint16_t* v_cache, int block_size, int64_t sb, int64_t sh,
+                      int64_t st_, hipStream_t st);
+int vwa_swiglu(const uint16_t* gu, uint16_t* h, int rows, int F, hipStream_t st);
+int vwa_bias_act(const uint16_t* x, const uint16_t* bias, const uint16_t* residual, uint16_t* y, int rows, int N,
+                 int act, hipStream_t st);
+int vwa_decode_attention(const DecodeAttnParams* p, hipStream_t st);
+int vwa_flash_attention(const FlashAttnParams* p, hipStream_t st);
+int vwa_embedding(const int* ids, const uint16_t* table, const uint16_t* pos_table, const int* positions,
+                  uint16_t* out, int rows, int D, int vocab_start, int vocab_end, hipStream_t st);
+int vwa_sample(const float* logits, int ld, int rows, int V, const uint32_t* mask, int mask_words,
+               const float* temperature, const uint64_t* seed, const int* step, int* out_tokens,
+               float* part_val, int* part_idx, int n_chunks, hipStream_t st);
+int vwa_pcm16_to_f32(const int16_t* pcm, float* out, int n_in, int n_out, float ratio, hipStream_t st);
+int vwa_log_mel(const float* audio, int n_samples, int n_frames, const float* window, const float* dft_cos,
+                const float* dft_sin, const float* mel_fb, int n_mels, float* mel_out, float* max_buf,
+                uint16_t* out_bf16, int ld_out, hipStream_t st);
+int vwa_conv1d_gelu_pos(const uint16_t* x, const uint16_t* w, const uint16_t* b, const uint16_t* pos, uint16_t* y,
+                        int B, int Cin, int Tin, int Cout, int Tout, int stride, hipStream_t st);
+int vwa_attention_split_tokens();
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,251 @@
+"""Numerics of every gfx950 HIP kernel vs the plain-PyTorch f32 reference (ops/reference.py).
+
+All tests run the native kernel path (ops.ext() must load: no fallback) on cuda:0.
+"""
+import math
+
+import pytest
+import torch
+
+import voice_enabled_browser_automation_amd.ops as ops
+from voice_enabled_browser_automation_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    ops.ext()  # fail loudly if the extension is missing
+    torch.manual_seed(0)
+
+
+def rnd(*shape, scale=1.0, dtype=BF):
+    return (torch.randn(*shape, device=DEV) * scale).to(dtype)
+
+
+def close(a, b, atol, rtol=2e-2):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    err = (a - b).abs().max().item()
+    tol = atol + rtol * b.abs().max().item()
+    assert err <= tol, f"max err {err} > tol {tol}"
+
+
+@pytest.mark.parametrize("M", [1, 5, 17, 40])
+@pytest.mark.parametrize("fuse_rms", [False, True])
+def test_skinny_store_resid_gelu(M, fuse_rms):
+    K, N = 1024, 384
+    x = rnd(M, K)
+    w = rnd(N, K, scale=0.05)
+    b = rnd(N, scale=0.1)
+    for act, res in (("none", None), ("none", rnd(M, N)), ("gelu", None)):
+        out = torch.empty(M, N, dtype=BF, device=DEV)
+        ops.linear(x, w, b, out=out, residual=res, act=act, fuse_rms=fuse_rms, eps=1e-5)
+        exp = torch.empty(M, N, dtype=BF)
+        ref.linear(x.cpu(), w.cpu(), b.cpu(), out=exp, residual=None if res is None else res.cpu(), act=act,
+                   fuse_rms=fuse_rms, eps=1e-5)
+        close(out, exp, 2e-2)
+
+
+def test_skinny_f32_out_large_n_and_inplace_residual():
+    M, K, N = 3, 4096, 4096
+    x = rnd(M, K)
+    w = rnd(N, K, scale=0.02)
+    logits = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    ops.linear(x, w, out=logits, fuse_rms=True)
+    exp = torch.empty(M, N, dtype=torch.float32)
+    ref.linear(x.cpu(), w.cpu(), out=exp, fuse_rms=True)
+    close(logits, exp, 1e-2)
+    h = rnd(M, N)
+    h0 = h.clone()
+    ops.linear(x, w, out=h, residual=h)
+    exp = torch.empty(M, N, dtype=BF)
+    ref.linear(x.cpu(), w.cpu(), out=exp, residual=h0.cpu())
+    close(h, exp, 3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 33])
+def test_skinny_swiglu(M):
+    K, F = 512, 256
+    x = rnd(M, K)
+    wg, wu = rnd(F, K, scale=0.05), rnd(F, K, scale=0.05)
+    wgu = ops.interleave_gate_up(wg, wu)
+    out = ops.linear_swiglu(x, wgu, fuse_rms=True)
+    xf = x.float().cpu()
+    xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)
+    exp = torch.nn.functional.silu(xf @ wg.float().cpu().t()) * (xf @ wu.float().cpu().t())
+    close(out, exp, 2e-2)
+    # prefill path (hipBLASLt + swiglu kernel)
+    x2 = rnd(80, K)
+    out2 = ops.linear_swiglu(x2, wgu)
+    exp2 = torch.nn.functional.silu(x2.float().cpu() @ wg.float().cpu().t()) * (x2.float().cpu() @ wu.float().cpu().t())
+    close(out2, exp2, 3e-2)
+
+
+def _kv_setup(nq, nkv, hd, blocks=16, bs=16):
+    kc = torch.zeros(blocks, nkv, bs, hd, dtype=BF, device=DEV)
+    vc = torch.zeros_like(kc)
+    return kc, vc
+
+
+@pytest.mark.parametrize("M", [1, 7, 70])
+def test_qkv_rope_write(M):
+    nq, nkv, hd, K = 8, 2, 128, 512
+    H = nq + 2 * nkv
+    w = rnd(H * hd, K, scale=0.05)
+    wp = ops.permute_qkv_rows(w, H, hd)
+    x = rnd(M, K)
+    rope = ops.rope_table(256, hd, 500000.0, device=DEV)
+    pos = torch.randint(0, 200, (M,), dtype=torch.int32, device=DEV)
+    slots = torch.randperm(16 * 16, device=DEV)[:M].to(torch.int64)
+    kc, vc = _kv_setup(nq, nkv, hd)
+    q = torch.zeros(M, nq * hd, dtype=BF, device=DEV)
+    ops.qkv_rope_write(x, wp, None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd, rope=rope,
+                       positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc)
+    kc2, vc2 = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q2 = torch.zeros(M, nq * hd, dtype=BF)
+    ref.qkv_rope_write(x.cpu(), wp.cpu(), None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
+                       rope=rope.cpu(), positions=pos.cpu(), slots=slots.cpu(), q_out=q2, k_cache=kc2, v_cache=vc2)
+    close(q, q2, 3e-2)
+    close(kc, kc2, 3e-2)
+    close(vc, vc2, 3e-2)
+
+
+def test_norms():
+    for D in (384, 4096):
+        x, r = rnd(9, D), rnd(9, D)
+        w, b = rnd(D), rnd(D)
+        ro = torch.empty_like(x)
+        y = ops.rmsnorm(x, w, eps=1e-5, residual=r, residual_out=ro)
+        ro2 = torch.empty(9, D, dtype=BF)
+        y2 = ref.rmsnorm(x.cpu(), w.cpu(), eps=1e-5, residual=r.cpu(), residual_out=ro2, out=torch.empty(9, D, dtype=BF))
+        close(y, y2, 3e-2)
+        close(ro, ro2, 2e-2)
+        y = ops.layernorm(x, w, b, eps=1e-5)
+        y2 = ref.layernorm(x.cpu(), w.cpu(), b.cpu(), eps=1e-5, out=torch.empty(9, D, dtype=BF))
+        close(y, y2, 3e-2)
+
+
+def test_bias_act_embedding():
+    x, b, r = rnd(5, 64), rnd(64), rnd(5, 64)
+    y = torch.empty_like(x)
+    ops.ext().bias_act(x, b, r, y, 1)
+    exp = torch.nn.functional.gelu(x.float() + b.float()) + r.float()
+    close(y, exp, 2e-2)
+    table = rnd(100, 64)
+    pos_table = rnd(50, 64)
+    ids = torch.tensor([3, 99, 0, 150], dtype=torch.int32, device=DEV)
+    positions = torch.tensor([0, 1, 2, 3], dtype=torch.int32, device=DEV)
+    out = ops.embedding(ids, table, pos_table=pos_table, positions=positions, vocab_start=0)
+    exp = ref.embedding(ids.cpu(), table.cpu(), pos_table=pos_table.cpu(), positions=positions.cpu(),
+                        out=torch.empty(4, 64, dtype=BF))
+    close(out, exp, 1e-2)
+
+
+@pytest.mark.parametrize("hd,nq,nkv", [(128, 32, 8), (64, 6, 6)])
+@pytest.mark.parametrize("ctx", [1, 100, 700])
+def test_decode_attention_paged(hd, nq, nkv, ctx):
+    bs, blocks = 16, 64
+    kc = rnd(blocks, nkv, bs, hd)
+    vc = rnd(blocks, nkv, bs, hd)
+    rows = 3
+    table = torch.stack([torch.randperm(blocks, device=DEV)[:48] for _ in range(2)]).to(torch.int32)
+    seq_ids = torch.tensor([0, 1, 0], dtype=torch.int32, device=DEV)
+    ctx_lens = torch.tensor([ctx, max(1, ctx // 2), min(ctx + 3, 48 * bs)], dtype=torch.int32, device=DEV)
+    q = rnd(rows, nq * hd)
+    kv = ops.KVLayout.paged(kc, vc, table)
+    out = torch.empty_like(q)
+    ops.decode_attention(q, kv, ctx_lens, seq_ids, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd, scale=hd ** -0.5,
+                         max_ctx=48 * bs, out=out)
+    kvc = ops.KVLayout.paged(kc.cpu(), vc.cpu(), table.cpu())
+    exp = ref.decode_attention(q.cpu(), kvc, ctx_lens.cpu(), seq_ids.cpu(), n_q_heads=nq, n_kv_heads=nkv,
+                               head_dim=hd, scale=hd ** -0.5, out=torch.empty(rows, nq * hd, dtype=BF))
+    close(out, exp, 2e-2)
+    out1 = torch.empty_like(q)
+    ops.decode_attention(q, kv, torch.clamp(ctx_lens, max=64), seq_ids, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
+                         scale=hd ** -0.5, max_ctx=64, out=out1)
+    exp1 = ref.decode_attention(q.cpu(), kvc, torch.clamp(ctx_lens.cpu(), max=64), seq_ids.cpu(), n_q_heads=nq,
+                                n_kv_heads=nkv, head_dim=hd, scale=hd ** -0.5,
+                                out=torch.empty(rows, nq * hd, dtype=BF))
+    close(out1, exp1, 2e-2)
+
+
+def test_flash_attention_causal_paged_prefix():
+    hd, nq, nkv, bs = 128, 8, 2, 16
+    blocks = 40
+    kc, vc = rnd(blocks, nkv, bs, hd), rnd(blocks, nkv, bs, hd)
+    table = torch.randperm(blocks, device=DEV)[:32].to(torch.int32)[None]
+    Sk, Sq = 300, 77
+    q = rnd(1, Sq, nq, hd)
+    kv = ops.KVLayout.paged(kc, vc, table)
+    out = ops.flash_attention(q, kv, Sk=Sk, n_kv_heads=nkv, causal=True, scale=hd ** -0.5, q_offset=Sk - Sq)
+    exp = ref.flash_attention(q.cpu(), ops.KVLayout.paged(kc.cpu(), vc.cpu(), table.cpu()), Sk=Sk, n_kv_heads=nkv,
+                              causal=True, scale=hd ** -0.5, q_offset=Sk - Sq, out=torch.empty(1, Sq, nq, hd, dtype=BF))
+    close(out, exp, 2e-2)
+
+
+def test_flash_attention_encoder_contiguous():
+    B, S, H, D = 2, 150, 6, 64
+    q, k, v = rnd(B, S, H, D), rnd(B, S, H, D), rnd(B, S, H, D)
+    table = torch.arange(B, dtype=torch.int32, device=DEV)[:, None]
+    kv = ops.KVLayout.contiguous(k, v, table)
+    out = ops.flash_attention(q, kv, Sk=S, n_kv_heads=H, causal=False, scale=D ** -0.5)
+    exp = torch.nn.functional.scaled_dot_product_attention(q.float().transpose(1, 2), k.float().transpose(1, 2),
+                                                           v.float().transpose(1, 2)).transpose(1, 2)
+    close(out, exp.cpu(), 2e-2)
+
+
+def test_sample_greedy_masked_and_gumbel():
+    rows, V = 3, 128256
+    logits = torch.randn(rows, V, device=DEV)
+    words = (V + 31) // 32
+    mask = torch.zeros(rows, words, dtype=torch.int32, device=DEV)
+    allowed = [torch.randint(0, V, (50,)) for _ in range(rows)]
+    mcpu = torch.zeros(rows, words, dtype=torch.int64)
+    for r in range(rows):
+        for a in allowed[r].tolist():
+            mcpu[r, a // 32] |= 1 << (a % 32)
+    mask.copy_(((mcpu + 2 ** 31) % 2 ** 32 - 2 ** 31).to(torch.int32))
+    seed = torch.tensor([1234], dtype=torch.int64, device=DEV)
+    step = torch.zeros(1, dtype=torch.int32, device=DEV)
+    out = torch.empty(rows, dtype=torch.int32, device=DEV)
+    ops.sample(logits, mask=mask, temperature=None, seed=seed, step=step, out_tokens=out)
+    for r in range(rows):
+        al = allowed[r].to(DEV)
+        assert int(out[r]) == int(al[torch.argmax(logits[r, al])])
+    temp = torch.full((rows,), 0.7, device=DEV)
+    step0 = int(step.item())
+    ops.sample(logits, mask=mask, temperature=temp, seed=seed, step=step, out_tokens=out)
+    exp = torch.empty(rows, dtype=torch.int32)
+    ref.sample(logits.cpu(), mask=mask.cpu(), temperature=temp.cpu(), seed=seed.cpu(),
+               step=torch.tensor([step0], dtype=torch.int32), out_tokens=exp)
+    assert out.cpu().tolist() == exp.tolist()
+
+
+def test_audio_frontend_and_conv():
+    sr = 16000
+    pcm = (torch.sin(torch.arange(sr * 2) * 2 * math.pi * 440 / sr) * 8000).to(torch.int16).to(DEV)
+    f = ops.pcm16_to_f32(pcm)
+    close(f, pcm.float().cpu() / 32768, 1e-6)
+    n_frames = 3000
+    audio = torch.zeros(n_frames * 160, device=DEV)
+    audio[: f.numel()] = f
+    window = torch.hann_window(400, periodic=True, device=DEV)
+    cos_table = torch.cos(torch.arange(400, dtype=torch.float64) * 2 * math.pi / 400).float().to(DEV)
+    fb = ref.mel_filterbank(n_mels=80).to(DEV)
+    out = torch.empty(n_frames, 80, dtype=BF, device=DEV)
+    ops.log_mel(audio, n_frames=n_frames, window=window, cos_table=cos_table, mel_fb=fb, out=out)
+    exp = ref.log_mel(audio.cpu(), n_frames=n_frames, window=window.cpu(), mel_fb=fb.cpu(),
+                      out=torch.empty(n_frames, 80, dtype=BF))
+    close(out, exp, 3e-2)
+    x = rnd(1, 3000, 80)
+    w = rnd(384, 3 * 80, scale=0.05)
+    b = rnd(384, scale=0.1)
+    y = ops.conv1d_gelu(x, w, b, stride=1)
+    y2 = ref.conv1d_gelu(x.cpu(), w.cpu(), b.cpu(), stride=1, out=torch.empty(1, 3000, 384, dtype=BF))
+    close(y, y2, 3e-2)
+    pos = rnd(1500, 384)
+    z = ops.conv1d_gelu(y, rnd(384, 3 * 384, scale=0.02), b, stride=2, pos=pos)
+    assert z.shape == (1, 1500, 384)

@@ -1,0 +1,110 @@
+"""Kernel microbenchmarks on the Llama-3-8B decode shapes (M = 1..32) and attention.
+
+Reports time and effective HBM bandwidth of the MFMA skinny GEMM against torch.matmul
+(hipBLASLt) on identical random data, interleaved in one process (guide §5.4 rule 24).
+Usage: python tools/bench_kernels.py [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import voice_enabled_browser_automation_amd.ops as ops  # noqa: E402
+
+
+def timeit(fn, iters=50, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(iters):
+        fn()
+    ev1.record()
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--json", default=None)
+    args = ap.parse_args()
+    dev = "cuda"
+    torch.manual_seed(0)
+    res = []
+    shapes = [("qkv", 6144, 4096), ("o_proj", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336),
+              ("lm_head", 128256, 4096)]
+    for M in (1, 4, 16, 32):
+        for name, N, K in shapes:
+            x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            # rotate over enough weight copies (>= 1 GiB) that the 256 MiB Infinity Cache cannot
+            # serve them: decode streams 16 GB of distinct weights per token.
+            ncopy = max(1, int(1.0e9 // (N * K * 2)) + 1)
+            ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(ncopy)]
+            y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            it = [0]
+
+            def ours():
+                it[0] = (it[0] + 1) % ncopy
+                ops.ext().skinny_gemm(x, ws[it[0]], None, y, 0, False, 1e-5, None)
+
+            def blas():
+                it[0] = (it[0] + 1) % ncopy
+                torch.matmul(x, ws[it[0]].t())
+
+            t_ours = timeit(ours)
+            t_blas = timeit(blas)
+            del ws
+            gb = N * K * 2 / 1e9
+            r = dict(kernel="skinny_gemm", shape=name, M=M, N=N, K=K, us=round(t_ours, 2),
+                     tbps=round(gb / (t_ours * 1e-6) / 1e3, 3), hipblaslt_us=round(t_blas, 2),
+                     hipblaslt_tbps=round(gb / (t_blas * 1e-6) / 1e3, 3))
+            print(json.dumps(r), flush=True)
+            res.append(r)
+    # decode attention, Llama-3-8B geometry, ctx 1200
+    nq, nkv, hd, bs = 32, 8, 128, 16
+    for rows, ctx in ((1, 1200), (8, 1200), (32, 1200)):
+        blocks = rows * ((ctx + bs - 1) // bs) + 8
+        kc = torch.randn(blocks, nkv, bs, hd, device=dev).to(torch.bfloat16)
+        vc = torch.randn_like(kc)
+        per = (ctx + bs - 1) // bs
+        table = torch.arange(rows * per, device=dev, dtype=torch.int32).view(rows, per)
+        q = torch.randn(rows, nq * hd, device=dev).to(torch.bfloat16)
+        out = torch.empty_like(q)
+        cl = torch.full((rows,), ctx, dtype=torch.int32, device=dev)
+        sid = torch.arange(rows, dtype=torch.int32, device=dev)
+        kv = ops.KVLayout.paged(kc, vc, table)
+        n_splits = ops.decode_n_splits(2048)
+        po = torch.empty(rows * n_splits * nq * hd, device=dev)
+        pm = torch.empty(rows * n_splits * nq * 2, device=dev)
+        t = timeit(lambda: ops.decode_attention(q, kv, cl, sid, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
+                                                scale=hd ** -0.5, max_ctx=2048, out=out, part_o=po, part_ml=pm))
+        gb = rows * ctx * nkv * hd * 2 * 2 / 1e9
+        r = dict(kernel="decode_attention", rows=rows, ctx=ctx, us=round(t, 2), tbps=round(gb / (t * 1e-6) / 1e3, 3))
+        print(json.dumps(r), flush=True)
+        res.append(r)
+    # flash attention: whisper-tiny encoder and llama prefill
+    for name, B, S, H, Hkv, D, causal in (("whisper_tiny_enc", 1, 1500, 6, 6, 64, False),
+                                          ("whisper_large_enc", 1, 1500, 20, 20, 64, False),
+                                          ("llama_prefill_1k", 1, 1024, 32, 8, 128, True)):
+        q = torch.randn(B, S, H, D, device=dev).to(torch.bfloat16)
+        k = torch.randn(B, S, Hkv, D, device=dev).to(torch.bfloat16)
+        v = torch.randn_like(k)
+        table = torch.arange(B, dtype=torch.int32, device=dev)[:, None]
+        kv = ops.KVLayout.contiguous(k, v, table)
+        out = torch.empty_like(q)
+        t = timeit(lambda: ops.flash_attention(q, kv, Sk=S, n_kv_heads=Hkv, causal=causal, scale=D ** -0.5, out=out))
+        fl = 4 * B * H * S * S * D / (2 if causal else 1)
+        r = dict(kernel="flash_attention", shape=name, us=round(t, 2), tflops=round(fl / (t * 1e-6) / 1e12, 2))
+        print(json.dumps(r), flush=True)
+        res.append(r)
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

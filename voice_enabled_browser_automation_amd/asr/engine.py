@@ -1,0 +1,201 @@
+"""ASR engine: on-node Whisper transcription (replaces the Deepgram live socket,
+apps/voice/src/deepgram.ts:21-67).
+
+`WhisperRunner` owns static decoder buffers for up to ``max_sessions`` concurrent utterances
+(one row per session per step -> continuous batching across voice sessions, the DP unit of a
+GPU) and captures one hipGraph per row bucket.  `AsrEngine.transcribe` runs
+PCM16 -> f32 (HIP) -> log-mel (HIP) -> encoder -> cross K/V -> greedy constrained decode.
+"""
+from __future__ import annotations
+
+import time
+from types import SimpleNamespace
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.whisper import WhisperModel
+
+BUCKETS = (1, 2, 4, 8, 16)
+
+
+class WhisperRunner:
+    def __init__(self, model: WhisperModel, *, max_sessions: int = 4, block_size: int = 16,
+                 use_graphs: Optional[bool] = None):
+        cfg = model.cfg
+        self.model = model
+        dev = model.device
+        self.device = dev
+        self.max_sessions = max_sessions
+        self.bs = block_size
+        self.bps = (cfg.n_text_ctx + block_size - 1) // block_size  # blocks per session
+        n_blocks = max_sessions * self.bps + 1
+        H, hd, d = model.H, model.hd, cfg.d_model
+        R = max(BUCKETS)
+        i32 = dict(dtype=torch.int32, device=dev)
+        b = SimpleNamespace()
+        b.tokens = torch.zeros(R, **i32)
+        b.positions = torch.zeros(R, **i32)
+        b.seq_ids = torch.zeros(R, **i32)
+        b.ctx_lens = torch.ones(R, **i32)
+        b.slots = torch.full((R,), -1, dtype=torch.int64, device=dev)
+        b.block_table = torch.zeros(max_sessions, self.bps, **i32)
+        for s in range(max_sessions):
+            b.block_table[s] = torch.arange(1 + s * self.bps, 1 + (s + 1) * self.bps, dtype=torch.int32)
+        L = cfg.n_dec_layers
+        b.k_cache = torch.zeros(L, n_blocks, H, block_size, hd, dtype=model.dtype, device=dev)
+        b.v_cache = torch.zeros_like(b.k_cache)
+        b.max_ctx = self.bps * block_size
+        b.hidden = torch.zeros(R, d, dtype=model.dtype, device=dev)
+        b.h = torch.zeros_like(b.hidden)
+        b.q = torch.zeros(R, d, dtype=model.dtype, device=dev)
+        b.att = torch.zeros_like(b.q)
+        b.f = torch.zeros(R, cfg.ffn, dtype=model.dtype, device=dev)
+        b.logits = torch.zeros(R, model.vocab_padded, dtype=torch.float32, device=dev)
+        ns = max(ops.decode_n_splits(b.max_ctx), ops.decode_n_splits(cfg.n_audio_ctx))
+        b.part_o = torch.zeros(R * ns * H * hd, dtype=torch.float32, device=dev)
+        b.part_ml = torch.zeros(R * ns * H * 2, dtype=torch.float32, device=dev)
+        b.cross = [(torch.zeros(max_sessions, cfg.n_audio_ctx, H, hd, dtype=model.dtype, device=dev),
+                    torch.zeros(max_sessions, cfg.n_audio_ctx, H, hd, dtype=model.dtype, device=dev)) for _ in range(L)]
+        b.cross_table = torch.arange(max_sessions, dtype=torch.int32, device=dev)[:, None].contiguous()
+        b.cross_lens = torch.full((R,), cfg.n_audio_ctx, dtype=torch.int32, device=dev)
+        self.b = b
+        pin = dev.type == "cuda"
+        self.h_i32 = torch.zeros(4, R, dtype=torch.int32, pin_memory=pin)
+        self.h_slots = torch.full((R,), -1, dtype=torch.int64, pin_memory=pin)
+        if use_graphs is None:
+            use_graphs = ops.env_flag("VWA_HIPGRAPH", True)
+        self.use_graphs = bool(use_graphs) and dev.type == "cuda"
+        self.graphs: Dict[int, Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
+        self.pool = None
+
+    def set_cross(self, slot: int, enc_states: torch.Tensor) -> None:
+        """Compute this session's cross-attention K/V from encoder states [1, T, d]."""
+        kvs = self.model.cross_kv(enc_states)
+        for li, (k, v) in enumerate(kvs):
+            self.b.cross[li][0][slot].copy_(k[0])
+            self.b.cross[li][1][slot].copy_(v[0])
+
+    def _fwd(self, M: int) -> torch.Tensor:
+        return self.model.decode_step(self.b, M)
+
+    def _capture(self, M: int):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._fwd(M)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        if self.pool is None:
+            self.pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(g, pool=self.pool):
+            out = self._fwd(M)
+        self.graphs[M] = (g, out)
+        return self.graphs[M]
+
+    def step(self, rows: Sequence[Tuple[int, int, int]]) -> torch.Tensor:
+        """rows: (session slot, token, position). Returns f32 logits [len(rows), vocab_padded]."""
+        n = len(rows)
+        M = next(bk for bk in BUCKETS if bk >= n)
+        hi = self.h_i32
+        for i, (slot, tok, pos) in enumerate(rows):
+            hi[0, i], hi[1, i], hi[2, i], hi[3, i] = tok, pos, slot, pos + 1
+            blk = 1 + slot * self.bps + pos // self.bs
+            self.h_slots[i] = blk * self.bs + pos % self.bs
+        for i in range(n, M):
+            hi[0, i], hi[1, i], hi[2, i], hi[3, i] = 0, 0, 0, 1
+            self.h_slots[i] = -1
+        b = self.b
+        b.tokens.copy_(hi[0], non_blocking=True)
+        b.positions.copy_(hi[1], non_blocking=True)
+        b.seq_ids.copy_(hi[2], non_blocking=True)
+        b.ctx_lens.copy_(hi[3], non_blocking=True)
+        b.slots.copy_(self.h_slots, non_blocking=True)
+        if self.use_graphs:
+            g, out = self.graphs.get(M) or self._capture(M)
+            g.replay()
+        else:
+            out = self._fwd(M)
+        return out[:n]
+
+
+class AsrEngine:
+    """Whisper transcription with fixed-work decoding options for benchmarking."""
+
+    def __init__(self, model: WhisperModel, tokenizer, *, max_sessions: int = 4, use_graphs: Optional[bool] = None):
+        self.model = model
+        self.tok = tokenizer
+        cfg = model.cfg
+        self.runner = WhisperRunner(model, max_sessions=max_sessions, use_graphs=use_graphs)
+        dev = model.device
+        W = (model.vocab_padded + 31) // 32
+        text_ids = np.arange(model.vocab_padded) < cfg.eot
+        self.mask_text = torch.from_numpy(self._pack(text_ids)).to(dev)[None]
+        with_eot = text_ids.copy()
+        with_eot[cfg.eot] = True
+        self.mask_text_eot = torch.from_numpy(self._pack(with_eot)).to(dev)[None]
+        self.d_seed = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.d_step = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.d_tok = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.part_val = torch.zeros(64, dtype=torch.float32, device=dev)
+        self.part_idx = torch.zeros(64, dtype=torch.int32, device=dev)
+        self.prompt = [cfg.sot, cfg.lang_en, cfg.transcribe, cfg.no_timestamps]
+        self.last_stats: Dict[str, float] = {}
+        self.free_slots = list(range(max_sessions - 1, -1, -1))
+
+    @staticmethod
+    def _pack(bits: np.ndarray) -> np.ndarray:
+        n = (len(bits) + 31) // 32 * 32
+        b = np.zeros(n, dtype=np.uint8)
+        b[: len(bits)] = bits
+        return np.packbits(b, bitorder="little").view(np.uint32).view(np.int32).copy()
+
+    def pcm_to_audio(self, pcm: np.ndarray, rate: int = 16000) -> torch.Tensor:
+        t = torch.from_numpy(np.ascontiguousarray(pcm, dtype=np.int16)).to(self.model.device, non_blocking=True)
+        return ops.pcm16_to_f32(t, in_rate=rate)
+
+    def _sample(self, logits, allow_eot: bool) -> int:
+        ops.sample(logits, mask=self.mask_text_eot if allow_eot else self.mask_text, temperature=None,
+                   seed=self.d_seed, step=self.d_step, out_tokens=self.d_tok, part_val=self.part_val,
+                   part_idx=self.part_idx)
+        return int(self.d_tok.item())
+
+    def transcribe(self, audio: torch.Tensor, *, max_tokens: int = 96, min_tokens: int = 0,
+                   exact_tokens: Optional[int] = None) -> str:
+        """audio: f32 16 kHz on the model device (<= 30 s).
+
+        exact_tokens: decode exactly this many text tokens (EOT suppressed) -- fixed-work mode
+        used by the benchmark so random-init weights do the same work as a real transcript.
+        """
+        t0 = time.perf_counter()
+        m = self.model
+        slot = self.free_slots.pop()
+        try:
+            mel = m.log_mel(audio)
+            enc = m.encode(mel[None])
+            self.runner.set_cross(slot, enc)
+            t_enc = time.perf_counter()
+            rows = [(slot, t, p) for p, t in enumerate(self.prompt)]
+            logits = self.runner.step(rows)[-1:]
+            out: List[int] = []
+            n_max = exact_tokens if exact_tokens is not None else max_tokens
+            pos = len(self.prompt)
+            for i in range(n_max):
+                allow_eot = exact_tokens is None and i >= min_tokens
+                tok = self._sample(logits, allow_eot)
+                if tok == m.cfg.eot or tok < 0:
+                    break
+                out.append(tok)
+                if i + 1 < n_max:
+                    logits = self.runner.step([(slot, tok, pos)])
+                    pos += 1
+            text = self.tok.decode(out)
+            t_end = time.perf_counter()
+            self.last_stats = dict(encode_ms=(t_enc - t0) * 1e3, decode_ms=(t_end - t_enc) * 1e3,
+                                   total_ms=(t_end - t0) * 1e3, tokens=len(out))
+            return text
+        finally:
+            self.free_slots.append(slot)

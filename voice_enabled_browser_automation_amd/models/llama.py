@@ -1,0 +1,190 @@
+"""Llama-3 family decoder (the intent-parsing LLM: replaces the hosted chat model called at
+apps/brain/src/llm.ts:22-27).
+
+MI355X-first layout (see ops/__init__.py): fused + row-permuted QKV with the input RMSNorm
+gamma folded in, interleaved gate/up with the post-attention gamma folded in, final-norm
+gamma folded into the LM head.  A decode layer is therefore 5 kernels:
+
+    skinny_gemm_qkv (rms + QKV + RoPE + paged-KV write) -> decode_attention ->
+    skinny_gemm(o_proj, residual epilogue) -> skinny_gemm_swiglu (rms + gate/up + SiLU*up) ->
+    skinny_gemm(down, residual epilogue)
+
+Tensor parallelism (one process per GPU, torch.distributed over RCCL/xGMI):
+column-parallel QKV (heads split) and gate/up, row-parallel o/down with ONE all-reduce each
+(rank 0 adds the residual in its epilogue, the others contribute their partial product, the
+all-reduce then produces h_new = h + sum_r partial_r in place), vocab-parallel LM head with an
+all-gather of the logits.  Weights are generated (or loaded) full-size per layer with a
+deterministic generator and sliced, so a TP model is numerically the same model as TP=1.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+
+from .. import ops
+from ..parallel.tp import TPContext
+from .config import LlamaConfig
+
+
+@dataclass
+class LlamaLayerWeights:
+    qkv: torch.Tensor   # [(nq_l + 2 nkv_l) * hd, d]   permuted rows, input-norm folded
+    o: torch.Tensor     # [d, nq_l * hd]
+    gu: torch.Tensor    # [2 * F_l, d]  interleaved gate/up, post-attn norm folded
+    down: torch.Tensor  # [d, F_l]
+
+
+def _randn(gen: torch.Generator, shape, std: float, device, dtype) -> torch.Tensor:
+    t = torch.empty(shape, device=device, dtype=torch.float32)
+    t.normal_(0.0, std, generator=gen)
+    return t.to(dtype)
+
+
+class LlamaModel:
+    def __init__(self, cfg: LlamaConfig, *, device="cpu", dtype=torch.bfloat16, tp: Optional[TPContext] = None,
+                 seed: int = 0, weights: Optional[dict] = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.tp = tp or TPContext.single()
+        T = self.tp.size
+        assert cfg.n_heads % T == 0 and cfg.n_kv_heads % T == 0, "TP size must divide the head counts"
+        assert cfg.ffn % (16 * T) == 0 and cfg.vocab_size % 1 == 0
+        self.nq = cfg.n_heads // T
+        self.nkv = cfg.n_kv_heads // T
+        self.F = cfg.ffn // T
+        self.hd = cfg.head_dim
+        V = cfg.vocab_size
+        self.v_per = (V + T - 1) // T
+        self.v_start = self.tp.rank * self.v_per
+        self.v_end = min(V, self.v_start + self.v_per)
+        self.rope = ops.rope_table(cfg.max_pos, cfg.head_dim, cfg.rope_theta, device=self.device)
+        self.scale = cfg.head_dim ** -0.5
+        if weights is not None:
+            self._load(weights)
+        else:
+            self._init_random(seed)
+
+    # ------------------------------------------------------------------ weights
+    def _shard_layer(self, q, k, v, o, g, u, dn, in_norm, post_norm):
+        cfg, T, r, hd = self.cfg, self.tp.size, self.tp.rank, self.hd
+        qs = q.view(cfg.n_heads, hd, -1)[r * self.nq : (r + 1) * self.nq].reshape(-1, cfg.hidden)
+        ks = k.view(cfg.n_kv_heads, hd, -1)[r * self.nkv : (r + 1) * self.nkv].reshape(-1, cfg.hidden)
+        vs = v.view(cfg.n_kv_heads, hd, -1)[r * self.nkv : (r + 1) * self.nkv].reshape(-1, cfg.hidden)
+        qkv = torch.cat([qs, ks, vs], 0)
+        qkv = ops.fold_norm(qkv, in_norm)
+        qkv = ops.permute_qkv_rows(qkv, self.nq + 2 * self.nkv, hd)
+        os_ = o[:, r * self.nq * hd : (r + 1) * self.nq * hd].contiguous()
+        F = self.F
+        gs, us = g[r * F : (r + 1) * F], u[r * F : (r + 1) * F]
+        gu = ops.interleave_gate_up(ops.fold_norm(gs, post_norm), ops.fold_norm(us, post_norm))
+        ds = dn[:, r * F : (r + 1) * F].contiguous()
+        return LlamaLayerWeights(qkv=qkv.contiguous(), o=os_, gu=gu, down=ds)
+
+    def _init_random(self, seed: int):
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        gen = torch.Generator(device=dev)
+        std = cfg.init_std
+        gen.manual_seed(seed * 1000003 + 1)
+        self.embed = _randn(gen, (cfg.vocab_size, cfg.hidden), std, dev, dt)
+        ones = torch.ones(cfg.hidden, device=dev, dtype=dt)
+        self.layers: List[LlamaLayerWeights] = []
+        for li in range(cfg.n_layers):
+            gen.manual_seed(seed * 1000003 + 7919 * (li + 2))
+            q = _randn(gen, (cfg.n_heads * cfg.head_dim, cfg.hidden), std, dev, dt)
+            k = _randn(gen, (cfg.n_kv_heads * cfg.head_dim, cfg.hidden), std, dev, dt)
+            v = _randn(gen, (cfg.n_kv_heads * cfg.head_dim, cfg.hidden), std, dev, dt)
+            o = _randn(gen, (cfg.hidden, cfg.n_heads * cfg.head_dim), std, dev, dt)
+            g = _randn(gen, (cfg.ffn, cfg.hidden), std, dev, dt)
+            u = _randn(gen, (cfg.ffn, cfg.hidden), std, dev, dt)
+            dn = _randn(gen, (cfg.hidden, cfg.ffn), std, dev, dt)
+            self.layers.append(self._shard_layer(q, k, v, o, g, u, dn, ones, ones))
+            del q, k, v, o, g, u, dn
+        gen.manual_seed(seed * 1000003 + 3)
+        if cfg.tie_embeddings:
+            lm = self.embed
+        else:
+            lm = _randn(gen, (cfg.vocab_size, cfg.hidden), std, dev, dt)
+        self.lm_head = ops.fold_norm(lm[self.v_start : self.v_end], ones).contiguous()
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
+
+    def _load(self, w: dict):
+        """HF-layout state dict (safetensors names); sharded + fused on load."""
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        get = lambda n: w[n].to(device=dev, dtype=dt)  # noqa: E731
+        self.embed = get("model.embed_tokens.weight")
+        self.layers = []
+        for li in range(cfg.n_layers):
+            p = f"model.layers.{li}."
+            self.layers.append(self._shard_layer(
+                get(p + "self_attn.q_proj.weight"), get(p + "self_attn.k_proj.weight"),
+                get(p + "self_attn.v_proj.weight"), get(p + "self_attn.o_proj.weight"),
+                get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight"), get(p + "mlp.down_proj.weight"),
+                get(p + "input_layernorm.weight"), get(p + "post_attention_layernorm.weight")))
+        lm = get("lm_head.weight") if "lm_head.weight" in w else self.embed
+        self.lm_head = ops.fold_norm(lm[self.v_start : self.v_end], get("model.norm.weight")).contiguous()
+
+    def weight_bytes(self) -> int:
+        n = self.embed.numel() + self.lm_head.numel()
+        for L in self.layers:
+            n += L.qkv.numel() + L.o.numel() + L.gu.numel() + L.down.numel()
+        return n * self.embed.element_size()
+
+    # ------------------------------------------------------------------ forward
+    def _row_parallel(self, x: torch.Tensor, w: torch.Tensor, h: torch.Tensor):
+        """h <- h + x @ w^T summed over TP ranks (one all-reduce, residual folded into rank 0)."""
+        if self.tp.size == 1:
+            ops.linear(x, w, out=h, residual=h)
+        else:
+            if self.tp.rank == 0:
+                ops.linear(x, w, out=h, residual=h)
+            else:
+                ops.linear(x, w, out=h)
+            self.tp.all_reduce(h)
+
+    def forward(self, bufs, M: int, kv, *, prefill_seq: Optional[int] = None, q_offset: int = 0,
+                logits_rows: Optional[slice] = None) -> torch.Tensor:
+        """Run M token rows described by ``bufs`` (runtime.buffers.StepBuffers).
+
+        Decode/ragged mode (M <= 64): each row is one token of some sequence (seq_ids /
+        ctx_lens / positions / slots per row).  Prefill mode (prefill_seq given): the M rows are
+        consecutive tokens of table row ``prefill_seq`` starting at position q_offset.
+        Returns f32 logits [rows, vocab] (all ranks, gathered under TP).
+        """
+        cfg = self.cfg
+        h = bufs.hidden[:M]
+        ops.embedding(bufs.tokens, self.embed, out=h, rows=M)
+        qbuf = bufs.q[:M] if M <= bufs.q.shape[0] else torch.empty((M, self.nq * self.hd), dtype=self.dtype,
+                                                                      device=self.device)
+        for li, L in enumerate(self.layers):
+            kc, vc = kv.k[li], kv.v[li]
+            q = ops.qkv_rope_write(h, L.qkv, None, fuse_rms=True, eps=cfg.rms_eps, n_q_heads=self.nq,
+                                   n_kv_heads=self.nkv, head_dim=self.hd, rope=self.rope,
+                                   positions=bufs.positions, slots=bufs.slots, q_out=qbuf, k_cache=kc, v_cache=vc)
+            if prefill_seq is None:
+                attn = bufs.attn[:M]
+                ops.decode_attention(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens, bufs.seq_ids,
+                                     n_q_heads=self.nq, n_kv_heads=self.nkv, head_dim=self.hd, scale=self.scale,
+                                     max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o, part_ml=bufs.part_ml)
+            else:
+                table = bufs.block_table[prefill_seq : prefill_seq + 1]
+                q4 = q.view(1, M, self.nq, self.hd)
+                attn4 = torch.empty_like(q4)
+                ops.flash_attention(q4, ops.KVLayout.paged(kc, vc, table), Sk=q_offset + M, n_kv_heads=self.nkv,
+                                    causal=True, scale=self.scale, q_offset=q_offset, out=attn4)
+                attn = attn4.view(M, self.nq * self.hd)
+            self._row_parallel(attn, L.o, h)
+            act = bufs.act[:M] if M <= bufs.act.shape[0] else None
+            act = ops.linear_swiglu(h, L.gu, fuse_rms=True, eps=cfg.rms_eps, out=act)
+            self._row_parallel(act, L.down, h)
+        rows = logits_rows if logits_rows is not None else slice(0, M)
+        hs = h[rows]
+        n = hs.shape[0]
+        local = bufs.logits_local[:n] if n <= bufs.logits_local.shape[0] else None
+        local = ops.linear(hs, self.lm_head, out=local, fuse_rms=True, eps=cfg.rms_eps, out_dtype=torch.float32)
+        if self.tp.size == 1:
+            return local
+        return self.tp.all_gather_vocab(local, cfg.vocab_size, out=bufs.logits[:n] if n <= bufs.logits.shape[0] else None)

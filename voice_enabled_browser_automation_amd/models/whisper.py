@@ -1,0 +1,189 @@
+"""Whisper encoder-decoder ASR (replaces Deepgram Nova-3 live STT: apps/voice/src/deepgram.ts:33-45).
+
+Encoder (one pass per 30 s window, batch of sessions = DP):
+    log_mel (HIP, K2) -> conv1d+GELU (HIP MFMA implicit GEMM, K3) -> conv1d/s2+GELU+pos (K3)
+    -> L x [layernorm (K4) -> QKV GEMM (hipBLASLt) + bias -> flash attention (HIP MFMA, K5)
+            -> out-proj + bias + residual (K-epilogue) -> layernorm -> fc1 + bias + GELU -> fc2 + residual]
+    -> layernorm -> cross-attention K/V for every decoder layer (computed once per window).
+Decoder (per token, hipGraph-captured per batch bucket):
+    embedding + learned positions (K14) -> L x [layernorm -> fused QKV skinny GEMM + bias + paged
+    self-KV write (K12 QKV epilogue, no RoPE) -> decode attention (K10) -> out-proj residual epilogue
+    -> layernorm -> q skinny GEMM -> cross attention over the window's K/V (K7) -> out-proj residual
+    -> layernorm -> fc1 GELU epilogue -> fc2 residual epilogue] -> layernorm -> tied LM head (f32)
+    -> masked greedy sampling (K13).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+
+from .. import ops
+from ..ops import reference as ref
+from .config import WhisperConfig
+
+
+def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> torch.Tensor:
+    inc = math.log(max_timescale) / (channels // 2 - 1)
+    inv = torch.exp(-inc * torch.arange(channels // 2, dtype=torch.float32))
+    t = torch.arange(length, dtype=torch.float32)[:, None] * inv[None, :]
+    return torch.cat([torch.sin(t), torch.cos(t)], dim=1)
+
+
+@dataclass
+class EncLayer:
+    ln1_w: torch.Tensor; ln1_b: torch.Tensor
+    qkv: torch.Tensor; qkv_b: torch.Tensor      # [3d, d] natural order (q,k,v)
+    o: torch.Tensor; o_b: torch.Tensor
+    ln2_w: torch.Tensor; ln2_b: torch.Tensor
+    fc1: torch.Tensor; fc1_b: torch.Tensor
+    fc2: torch.Tensor; fc2_b: torch.Tensor
+
+
+@dataclass
+class DecLayer:
+    ln1_w: torch.Tensor; ln1_b: torch.Tensor
+    qkv: torch.Tensor; qkv_b: torch.Tensor      # permuted rows (skinny QKV epilogue layout)
+    o: torch.Tensor; o_b: torch.Tensor
+    lnx_w: torch.Tensor; lnx_b: torch.Tensor
+    xq: torch.Tensor; xq_b: torch.Tensor
+    xk: torch.Tensor; xv: torch.Tensor; xv_b: torch.Tensor
+    xo: torch.Tensor; xo_b: torch.Tensor
+    ln2_w: torch.Tensor; ln2_b: torch.Tensor
+    fc1: torch.Tensor; fc1_b: torch.Tensor
+    fc2: torch.Tensor; fc2_b: torch.Tensor
+
+
+class WhisperModel:
+    def __init__(self, cfg: WhisperConfig, *, device="cpu", dtype=torch.bfloat16, seed: int = 0):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        d, H = cfg.d_model, cfg.n_heads
+        self.H, self.hd = H, cfg.head_dim
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(seed * 7 + 11)
+        std = cfg.init_std
+
+        def rn(*shape, s=std):
+            t = torch.empty(shape, device=self.device, dtype=torch.float32)
+            t.normal_(0.0, s, generator=gen)
+            return t.to(dtype)
+
+        def ones(n):
+            return torch.ones(n, device=self.device, dtype=dtype)
+
+        def zeros(n):
+            return torch.zeros(n, device=self.device, dtype=dtype)
+
+        F = cfg.ffn
+        # conv weights stored [Cout, 3*Cin] in (kk, ci) order for the implicit-GEMM kernel
+        self.conv1_w, self.conv1_b = rn(d, 3 * cfg.n_mels), rn(d, s=0.01)
+        self.conv2_w, self.conv2_b = rn(d, 3 * d), rn(d, s=0.01)
+        self.pos_enc = sinusoids(cfg.n_audio_ctx, d).to(self.device, dtype)
+        self.enc: List[EncLayer] = []
+        for _ in range(cfg.n_enc_layers):
+            self.enc.append(EncLayer(ones(d), zeros(d), rn(3 * d, d), rn(3 * d, s=0.01), rn(d, d), rn(d, s=0.01),
+                                     ones(d), zeros(d), rn(F, d), rn(F, s=0.01), rn(d, F), rn(d, s=0.01)))
+        self.enc_ln_w, self.enc_ln_b = ones(d), zeros(d)
+        self.tok_emb = rn(cfg.vocab_size, d)
+        self.pos_emb = rn(cfg.n_text_ctx, d, s=0.01)
+        self.dec: List[DecLayer] = []
+        for _ in range(cfg.n_dec_layers):
+            qkv = rn(3 * d, d)
+            qkv_b = rn(3 * d, s=0.01)
+            qkv_b[d : 2 * d] = 0  # Whisper's key projection has no bias
+            qkv_p = ops.permute_qkv_rows(qkv, 3 * H, self.hd)
+            qkv_bp = ops.permute_qkv_rows(qkv_b[:, None], 3 * H, self.hd)[:, 0].contiguous()
+            self.dec.append(DecLayer(ones(d), zeros(d), qkv_p, qkv_bp, rn(d, d), rn(d, s=0.01), ones(d), zeros(d),
+                                     rn(d, d), rn(d, s=0.01), rn(d, d), rn(d, d), rn(d, s=0.01), rn(d, d),
+                                     rn(d, s=0.01), ones(d), zeros(d), rn(F, d), rn(F, s=0.01), rn(d, F),
+                                     rn(d, s=0.01)))
+        self.dec_ln_w, self.dec_ln_b = ones(d), zeros(d)
+        # tied LM head padded to a multiple of 16 rows (MFMA column tile); padded ids are masked
+        vp = (cfg.vocab_size + 15) // 16 * 16
+        self.vocab_padded = vp
+        self.lm_head = torch.zeros(vp, d, device=self.device, dtype=dtype)
+        self.lm_head[: cfg.vocab_size] = self.tok_emb
+        # front-end constants
+        self.window = torch.hann_window(400, periodic=True, device=self.device)
+        self.cos_table = torch.cos(torch.arange(400, dtype=torch.float64) * 2 * math.pi / 400).float().to(self.device)
+        self.mel_fb = ref.mel_filterbank(n_mels=cfg.n_mels).to(self.device)
+
+    # ------------------------------------------------------------------ encoder
+    def log_mel(self, audio: torch.Tensor, n_frames: int = 3000) -> torch.Tensor:
+        """audio: f32 samples (<= 30 s). Returns [n_frames, n_mels] bf16 (channels-last)."""
+        pad = torch.zeros(n_frames * 160, dtype=torch.float32, device=self.device)
+        n = min(audio.numel(), pad.numel())
+        pad[:n] = audio[:n]
+        out = torch.empty(n_frames, self.cfg.n_mels, dtype=self.dtype, device=self.device)
+        return ops.log_mel(pad, n_frames=n_frames, window=self.window, cos_table=self.cos_table, mel_fb=self.mel_fb,
+                           out=out)
+
+    def encode(self, mel: torch.Tensor) -> torch.Tensor:
+        """mel [B, 3000, n_mels] -> encoder states [B, 1500, d]."""
+        cfg = self.cfg
+        B = mel.shape[0]
+        x = ops.conv1d_gelu(mel, self.conv1_w, self.conv1_b, stride=1)
+        x = ops.conv1d_gelu(x, self.conv2_w, self.conv2_b, stride=2, pos=self.pos_enc)
+        T, d = x.shape[1], x.shape[2]
+        x = x.reshape(B * T, d)
+        table = torch.arange(B, dtype=torch.int32, device=self.device)[:, None]
+        for L in self.enc:
+            h = ops.layernorm(x, L.ln1_w, L.ln1_b, eps=cfg.ln_eps)
+            qkv = ops.linear(h, L.qkv, L.qkv_b).view(B, T, 3, self.H, self.hd)
+            q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+            q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+            att = ops.flash_attention(q, ops.KVLayout.contiguous(k, v, table), Sk=T, n_kv_heads=self.H, causal=False,
+                                      scale=self.hd ** -0.5)
+            x = ops.linear(att.view(B * T, d), L.o, L.o_b, residual=x)
+            h = ops.layernorm(x, L.ln2_w, L.ln2_b, eps=cfg.ln_eps)
+            h = ops.linear(h, L.fc1, L.fc1_b, act="gelu")
+            x = ops.linear(h, L.fc2, L.fc2_b, residual=x)
+        x = ops.layernorm(x, self.enc_ln_w, self.enc_ln_b, eps=cfg.ln_eps)
+        return x.view(B, T, d)
+
+    def cross_kv(self, enc: torch.Tensor):
+        """Per decoder layer cross-attention K/V [B, T, H, hd] (computed once per window)."""
+        B, T, d = enc.shape
+        x = enc.reshape(B * T, d)
+        out = []
+        for L in self.dec:
+            k = ops.linear(x, L.xk).view(B, T, self.H, self.hd)
+            v = ops.linear(x, L.xv, L.xv_b).view(B, T, self.H, self.hd)
+            out.append((k.contiguous(), v.contiguous()))
+        return out
+
+    # ------------------------------------------------------------------ decoder step
+    def decode_step(self, bufs, M: int) -> torch.Tensor:
+        """M token rows (bufs: tokens/positions/slots/seq_ids/ctx_lens + self cache + cross K/V).
+        Returns f32 logits [M, vocab]."""
+        cfg = self.cfg
+        d = cfg.d_model
+        x = bufs.hidden[:M]
+        ops.embedding(bufs.tokens, self.tok_emb, pos_table=self.pos_emb, positions=bufs.positions, out=x, rows=M)
+        for li, L in enumerate(self.dec):
+            h = ops.layernorm(x, L.ln1_w, L.ln1_b, eps=cfg.ln_eps, out=bufs.h[:M])
+            q = ops.qkv_rope_write(h, L.qkv, L.qkv_b, fuse_rms=False, eps=0.0, n_q_heads=self.H, n_kv_heads=self.H,
+                                   head_dim=self.hd, rope=None, positions=bufs.positions, slots=bufs.slots,
+                                   q_out=bufs.q, k_cache=bufs.k_cache[li], v_cache=bufs.v_cache[li])
+            att = ops.decode_attention(q, ops.KVLayout.paged(bufs.k_cache[li], bufs.v_cache[li], bufs.block_table),
+                                       bufs.ctx_lens, bufs.seq_ids, n_q_heads=self.H, n_kv_heads=self.H,
+                                       head_dim=self.hd, scale=self.hd ** -0.5, max_ctx=bufs.max_ctx,
+                                       out=bufs.att[:M], part_o=bufs.part_o, part_ml=bufs.part_ml)
+            ops.linear(att, L.o, L.o_b, out=x, residual=x)
+            h = ops.layernorm(x, L.lnx_w, L.lnx_b, eps=cfg.ln_eps, out=bufs.h[:M])
+            xq = ops.linear(h, L.xq, L.xq_b, out=bufs.q[:M])
+            ck, cv = bufs.cross[li]
+            att = ops.decode_attention(xq, ops.KVLayout.contiguous(ck, cv, bufs.cross_table), bufs.cross_lens,
+                                       bufs.seq_ids, n_q_heads=self.H, n_kv_heads=self.H, head_dim=self.hd,
+                                       scale=self.hd ** -0.5, max_ctx=ck.shape[1], out=bufs.att[:M],
+                                       part_o=bufs.part_o, part_ml=bufs.part_ml)
+            ops.linear(att, L.xo, L.xo_b, out=x, residual=x)
+            h = ops.layernorm(x, L.ln2_w, L.ln2_b, eps=cfg.ln_eps, out=bufs.h[:M])
+            f = ops.linear(h, L.fc1, L.fc1_b, act="gelu", out=bufs.f[:M])
+            ops.linear(f, L.fc2, L.fc2_b, out=x, residual=x)
+        h = ops.layernorm(x, self.dec_ln_w, self.dec_ln_b, eps=cfg.ln_eps, out=bufs.h[:M])
+        return ops.linear(h, self.lm_head, out=bufs.logits[:M])

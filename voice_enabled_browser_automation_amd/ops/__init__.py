@@ -1,0 +1,361 @@
+"""Op layer: every hot op of the ASR + intent-LLM stack.
+
+On a GPU tensor the op runs the hand-written gfx950 HIP kernel from ``_vwa_kernels.so``
+(csrc/kernels/*.hip); if that library is missing on a GPU host the op raises -- there is no
+silent eager fallback.  On CPU tensors the op runs the torch reference in ``ops.reference``,
+which is also the numerics oracle for the kernel tests (tests/test_kernels_gpu.py).
+
+Layout conventions shared by kernels, reference and models:
+
+* weights are bf16 ``[N, K]`` (out x in) row-major;
+* fused QKV weights are row-permuted per head (``permute_qkv_rows``) so rotary pairs
+  (d, d+hd/2) sit in columns c and c^8 of one 16-column MFMA tile;
+* fused gate/up weights are interleaved per 16 rows (``interleave_gate_up``) so the SwiGLU
+  epilogue sees matching gate/up columns in one workgroup;
+* RMSNorm gammas are folded into the following projection's columns (``fold_norm``); the
+  kernels apply the per-row 1/rms themselves;
+* paged KV cache per layer: ``[num_blocks, n_kv_heads, block_size, head_dim]`` bf16.
+"""
+from __future__ import annotations
+
+import math
+import os
+from typing import Optional
+
+import torch
+
+from . import reference as ref
+
+_EXT = None
+_EXT_ERR: Optional[BaseException] = None
+
+
+def ext():
+    """Load the native kernel library (once). Raises if unavailable."""
+    global _EXT, _EXT_ERR
+    if _EXT is not None:
+        return _EXT
+    if _EXT_ERR is not None:
+        raise RuntimeError(f"native gfx950 kernel library unavailable: {_EXT_ERR}") from _EXT_ERR
+    try:
+        from . import _vwa_kernels as m  # type: ignore
+
+        _EXT = m
+        return m
+    except BaseException as e:  # noqa: BLE001
+        _EXT_ERR = e
+        raise RuntimeError(
+            "native gfx950 kernel library _vwa_kernels.so failed to load; build it with "
+            "`python -m voice_enabled_browser_automation_amd.ops.build`"
+        ) from e
+
+
+def native_available() -> bool:
+    try:
+        ext()
+        return True
+    except RuntimeError:
+        return False
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ----------------------------------------------------------------------------- layout helpers
+def qkv_row_perm(head_dim: int) -> torch.Tensor:
+    half = head_dim // 2
+    idx = []
+    for t in range(head_dim // 16):
+        idx += [8 * t + p for p in range(8)] + [half + 8 * t + p for p in range(8)]
+    return torch.tensor(idx, dtype=torch.long)
+
+
+def permute_qkv_rows(w: torch.Tensor, n_heads_total: int, head_dim: int) -> torch.Tensor:
+    perm = qkv_row_perm(head_dim)
+    full = torch.cat([perm + h * head_dim for h in range(n_heads_total)])
+    return w[full].contiguous()
+
+
+def unpermute_qkv_cols(y: torch.Tensor, n_heads_total: int, head_dim: int) -> torch.Tensor:
+    perm = qkv_row_perm(head_dim).to(y.device)
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.arange(head_dim, device=y.device)
+    full = torch.cat([inv + h * head_dim for h in range(n_heads_total)])
+    return y[..., full]
+
+
+def interleave_gate_up(w_gate: torch.Tensor, w_up: torch.Tensor) -> torch.Tensor:
+    F, K = w_gate.shape
+    assert F % 16 == 0
+    g = w_gate.view(F // 16, 16, K)
+    u = w_up.view(F // 16, 16, K)
+    return torch.stack([g, u], dim=1).reshape(2 * F, K).contiguous()
+
+
+def fold_norm(w: torch.Tensor, gamma: torch.Tensor) -> torch.Tensor:
+    return (w.float() * gamma.float()[None, :]).to(w.dtype)
+
+
+def rope_table(max_pos: int, head_dim: int, theta: float, device=None, scaling: Optional[dict] = None) -> torch.Tensor:
+    half = head_dim // 2
+    inv = 1.0 / (theta ** (torch.arange(0, half, dtype=torch.float64) * 2.0 / head_dim))
+    if scaling:  # Llama-3.1 style frequency scaling
+        factor = scaling.get("factor", 8.0)
+        lo, hi = scaling.get("low_freq_factor", 1.0), scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        wl = 2 * math.pi / inv
+        smooth = ((old / wl) - lo) / (hi - lo)
+        scaled = torch.where(wl > old / lo, inv / factor, inv)
+        mid = (wl <= old / lo) & (wl >= old / hi)
+        inv = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+    pos = torch.arange(max_pos, dtype=torch.float64)[:, None] * inv[None, :]
+    tab = torch.stack([torch.cos(pos), torch.sin(pos)], dim=-1).float()
+    return tab.to(device) if device is not None else tab
+
+
+# ----------------------------------------------------------------------------- GEMM family
+SKINNY_MAX_M = 64
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, out: Optional[torch.Tensor] = None,
+           residual: Optional[torch.Tensor] = None, act: str = "none", fuse_rms: bool = False, eps: float = 1e-5,
+           out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """y = act(rms(x) @ w^T + bias) [+ residual].
+
+    GPU: rows <= 64 -> MFMA skinny GEMM with fused epilogue (decode); otherwise hipBLASLt
+    (torch.matmul) for the plain GEMM + HIP epilogue kernels (prefill).
+    """
+    M = x.shape[0]
+    dt = out_dtype or (x.dtype if out is None else out.dtype)
+    if out is None:
+        out = torch.empty((M, w.shape[0]), dtype=dt, device=x.device)
+    if not _gpu(x):
+        return ref.linear(x, w, bias, out=out, residual=residual, act=act, fuse_rms=fuse_rms, eps=eps)
+    E = ext()
+    if M <= SKINNY_MAX_M and x.shape[1] % 128 == 0:
+        epi = {"none": 0, "gelu": 3}[act]
+        if residual is not None:
+            assert act == "none"
+            epi = 1
+        E.skinny_gemm(x, w, bias, out, epi, fuse_rms, eps, residual)
+        return out
+    xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
+    y = torch.matmul(xin, w.t())
+    if bias is not None or act != "none" or residual is not None:
+        if y.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and y.shape[1] % 8 == 0:
+            E.bias_act(y, bias, residual, out, 1 if act == "gelu" else 0)
+            return out
+        y = y.float()
+        if bias is not None:
+            y = y + bias.float()
+        if act == "gelu":
+            y = torch.nn.functional.gelu(y)
+        if residual is not None:
+            y = y + residual.float()
+    out.copy_(y)
+    return out
+
+
+def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False, eps: float = 1e-5,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    M = x.shape[0]
+    F = w_gu.shape[0] // 2
+    if out is None:
+        out = torch.empty((M, F), dtype=x.dtype, device=x.device)
+    if not _gpu(x):
+        return ref.linear_swiglu(x, w_gu, fuse_rms=fuse_rms, eps=eps, out=out)
+    E = ext()
+    if M <= SKINNY_MAX_M:
+        E.skinny_gemm_swiglu(x, w_gu, None, out, fuse_rms, eps)
+        return out
+    xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
+    gu = torch.matmul(xin, w_gu.t())
+    E.swiglu(gu, out)
+    return out
+
+
+def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Tensor], *, fuse_rms: bool, eps: float,
+                   n_q_heads: int, n_kv_heads: int, head_dim: int, rope: Optional[torch.Tensor],
+                   positions: torch.Tensor, slots: torch.Tensor, q_out: torch.Tensor, k_cache: torch.Tensor,
+                   v_cache: torch.Tensor) -> torch.Tensor:
+    """Fused QKV projection + rotary + paged KV write. Returns q_out[:M] (natural layout)."""
+    M = x.shape[0]
+    if not _gpu(x):
+        ref.qkv_rope_write(x, w_qkv, bias, fuse_rms=fuse_rms, eps=eps, n_q_heads=n_q_heads, n_kv_heads=n_kv_heads,
+                           head_dim=head_dim, rope=rope, positions=positions, slots=slots, q_out=q_out,
+                           k_cache=k_cache, v_cache=v_cache)
+        return q_out[:M]
+    E = ext()
+    use_rope = rope is not None
+    if M <= SKINNY_MAX_M:
+        E.skinny_gemm_qkv(x, w_qkv, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, use_rope, positions, slots,
+                          rope, q_out, k_cache, v_cache)
+        return q_out[:M]
+    xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
+    qkv = torch.matmul(xin, w_qkv.t())
+    if bias is not None:
+        qkv = qkv + bias
+    E.rope_kv_write(qkv, n_q_heads, n_kv_heads, head_dim, use_rope, positions, slots, rope, q_out, k_cache, v_cache)
+    return q_out[:M]
+
+
+# ----------------------------------------------------------------------------- norms / elementwise
+def rmsnorm(x: torch.Tensor, w: Optional[torch.Tensor], *, eps: float = 1e-5, residual: Optional[torch.Tensor] = None,
+            residual_out: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if out is None:
+        out = torch.empty_like(x)
+    if not _gpu(x):
+        return ref.rmsnorm(x, w, eps=eps, residual=residual, residual_out=residual_out, out=out)
+    ext().rmsnorm(x, residual, residual_out, w, out, eps)
+    return out
+
+
+def layernorm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, *, eps: float = 1e-5,
+              residual: Optional[torch.Tensor] = None, residual_out: Optional[torch.Tensor] = None,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if out is None:
+        out = torch.empty_like(x)
+    if not _gpu(x):
+        return ref.layernorm(x, w, b, eps=eps, residual=residual, residual_out=residual_out, out=out)
+    ext().layernorm(x, residual, residual_out, w, b, out, eps)
+    return out
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor, *, pos_table: Optional[torch.Tensor] = None,
+              positions: Optional[torch.Tensor] = None, vocab_start: int = 0,
+              out: Optional[torch.Tensor] = None, rows: Optional[int] = None) -> torch.Tensor:
+    n = rows if rows is not None else ids.shape[0]
+    if out is None:
+        out = torch.empty((n, table.shape[1]), dtype=table.dtype, device=table.device)
+    if not _gpu(table):
+        return ref.embedding(ids[:n], table, pos_table=pos_table, positions=None if positions is None else positions[:n],
+                             vocab_start=vocab_start, out=out)
+    ext().embedding(ids, table, pos_table, positions, out, vocab_start)
+    return out
+
+
+# ----------------------------------------------------------------------------- attention
+class KVLayout:
+    """Addressing for the attention kernels (see csrc/kernels/vwa_kernels.h KVView)."""
+
+    __slots__ = ("k", "v", "table", "block_size", "sb", "sh", "st")
+
+    def __init__(self, k, v, table, block_size, sb, sh, st):
+        self.k, self.v, self.table = k, v, table
+        self.block_size, self.sb, self.sh, self.st = int(block_size), int(sb), int(sh), int(st)
+
+    @staticmethod
+    def paged(k_cache: torch.Tensor, v_cache: torch.Tensor, block_table: torch.Tensor) -> "KVLayout":
+        # [num_blocks, n_kv, bs, hd]
+        return KVLayout(k_cache, v_cache, block_table, k_cache.shape[2], k_cache.stride(0), k_cache.stride(1),
+                        k_cache.stride(2))
+
+    @staticmethod
+    def contiguous(k: torch.Tensor, v: torch.Tensor, table: torch.Tensor) -> "KVLayout":
+        # [B, S, H, D]: one block per sequence
+        return KVLayout(k, v, table, k.shape[1], k.stride(0), k.stride(2), k.stride(1))
+
+
+def decode_split_tokens() -> int:
+    return 64
+
+
+def decode_n_splits(max_ctx: int) -> int:
+    return max(1, -(-int(max_ctx) // decode_split_tokens()))
+
+
+def decode_attention(q: torch.Tensor, kv: KVLayout, ctx_lens: torch.Tensor, seq_ids: torch.Tensor, *,
+                     n_q_heads: int, n_kv_heads: int, head_dim: int, scale: float, max_ctx: int,
+                     out: torch.Tensor, part_o: Optional[torch.Tensor] = None,
+                     part_ml: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One query row per token; ``max_ctx`` bounds every row's context (fixes the grid, so the
+    launch is graph-capturable while contexts grow)."""
+    n_splits = decode_n_splits(max_ctx)
+    if not _gpu(q):
+        return ref.decode_attention(q, kv, ctx_lens, seq_ids, n_q_heads=n_q_heads, n_kv_heads=n_kv_heads,
+                                    head_dim=head_dim, scale=scale, out=out)
+    assert ext().attention_split_tokens() == decode_split_tokens()
+    if part_o is None:
+        rows = q.shape[0]
+        part_o = torch.empty((rows * n_splits * n_q_heads * head_dim,), dtype=torch.float32, device=q.device)
+        part_ml = torch.empty((rows * n_splits * n_q_heads * 2,), dtype=torch.float32, device=q.device)
+    ext().decode_attention(q, kv.k, kv.v, kv.table, kv.block_size, kv.sb, kv.sh, kv.st, ctx_lens, seq_ids, n_q_heads,
+                           n_kv_heads, head_dim, scale, n_splits, part_o, part_ml, out)
+    return out
+
+
+def flash_attention(q: torch.Tensor, kv: KVLayout, *, Sk: int, n_kv_heads: int, causal: bool, scale: float,
+                    q_offset: int = 0, out: Optional[torch.Tensor] = None,
+                    k_lens: Optional[torch.Tensor] = None, q_offsets: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """q: [B, Sq, Hq, D]; keys of batch b through kv (table row b)."""
+    if out is None:
+        out = torch.empty_like(q)
+    if not _gpu(q):
+        return ref.flash_attention(q, kv, Sk=Sk, n_kv_heads=n_kv_heads, causal=causal, scale=scale,
+                                   q_offset=q_offset, out=out, k_lens=k_lens, q_offsets=q_offsets)
+    ext().flash_attention(q, kv.k, kv.v, kv.table, kv.block_size, kv.sb, kv.sh, kv.st, out, Sk, n_kv_heads, causal,
+                          q_offset, q_offsets, k_lens, scale)
+    return out
+
+
+# ----------------------------------------------------------------------------- sampling
+def sample(logits: torch.Tensor, *, mask: Optional[torch.Tensor], temperature: Optional[torch.Tensor],
+           seed: torch.Tensor, step: torch.Tensor, out_tokens: torch.Tensor,
+           part_val: Optional[torch.Tensor] = None, part_idx: Optional[torch.Tensor] = None,
+           n_chunks: int = 64) -> torch.Tensor:
+    rows = logits.shape[0]
+    if not _gpu(logits):
+        return ref.sample(logits, mask=mask, temperature=temperature, seed=seed, step=step, out_tokens=out_tokens)
+    if part_val is None:
+        part_val = torch.empty((rows * n_chunks,), dtype=torch.float32, device=logits.device)
+        part_idx = torch.empty((rows * n_chunks,), dtype=torch.int32, device=logits.device)
+    ext().sample(logits, mask, temperature, seed, step, out_tokens, part_val, part_idx)
+    return out_tokens
+
+
+# ----------------------------------------------------------------------------- audio
+def pcm16_to_f32(pcm: torch.Tensor, in_rate: int = 16000, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    ratio = in_rate / 16000.0
+    n_out = int(pcm.numel() / ratio)
+    if out is None:
+        out = torch.empty((n_out,), dtype=torch.float32, device=pcm.device)
+    if not _gpu(pcm):
+        return ref.pcm16_to_f32(pcm, ratio, out)
+    ext().pcm16_to_f32(pcm, out, ratio)
+    return out
+
+
+def log_mel(audio: torch.Tensor, *, n_frames: int, window: torch.Tensor, cos_table: torch.Tensor,
+            mel_fb: torch.Tensor, out: torch.Tensor, scratch: Optional[torch.Tensor] = None,
+            max_buf: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """audio: padded f32 samples (n_frames*160 for Whisper) -> out bf16 [n_frames, n_mels]."""
+    if not _gpu(audio):
+        return ref.log_mel(audio, n_frames=n_frames, window=window, mel_fb=mel_fb, out=out)
+    n_mels = mel_fb.shape[0]
+    if scratch is None:
+        scratch = torch.empty((n_frames * n_mels,), dtype=torch.float32, device=audio.device)
+    if max_buf is None:
+        max_buf = torch.empty((1,), dtype=torch.float32, device=audio.device)
+    ext().log_mel(audio, n_frames, window, cos_table, mel_fb, scratch, max_buf, out)
+    return out
+
+
+def conv1d_gelu(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], *, stride: int,
+                pos: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x [B, Tin, Cin] channels-last, w [Cout, 3*Cin] ([co][kk][ci]) -> [B, Tout, Cout]."""
+    B, Tin, Cin = x.shape
+    Tout = (Tin + 2 - 3) // stride + 1
+    if out is None:
+        out = torch.empty((B, Tout, w.shape[0]), dtype=x.dtype, device=x.device)
+    if not _gpu(x):
+        return ref.conv1d_gelu(x, w, b, stride=stride, pos=pos, out=out)
+    ext().conv1d_gelu(x, w, b, pos, out, stride)
+    return out
+
+
+def env_flag(name: str, default: bool = False) -> bool:
+    v = os.environ.get(name)
+    if v is None:
+        return default
+    return v.strip().lower() in ("1", "true", "yes", "on")

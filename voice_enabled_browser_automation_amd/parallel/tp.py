@@ -1,0 +1,86 @@
+"""Tensor-parallel / data-parallel process-group plumbing (one process per GPU).
+
+`torch.distributed` with backend "nccl" is RCCL on ROCm; on CPU (tests) the same code runs
+over gloo.  The LLM needs exactly these collectives:
+
+* C1/C2  all-reduce of the row-parallel o_proj / down_proj outputs (decode: d*2 bytes per row,
+         i.e. 8 KiB for Llama-3-8B -- latency bound; the residual is folded into rank 0's
+         GEMM epilogue so the all-reduce result IS the new residual stream);
+* C4     all-gather of the vocab-parallel logits shards (f32);
+* C5     broadcast (weights are generated deterministically on every rank, so only the
+         random seed needs to agree -- no weight traffic at init);
+* C6     all-gather of per-rank metrics (DP router).
+
+Layout of ranks on one 8-GPU node: TP groups are contiguous ranks (xGMI is a full mesh, so
+any contiguous group has direct links), DP replicas are the TP groups.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class TPContext:
+    rank: int = 0
+    size: int = 1
+    group: Optional[object] = None
+    dp_rank: int = 0
+    dp_size: int = 1
+
+    @staticmethod
+    def single() -> "TPContext":
+        return TPContext()
+
+    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.size > 1:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    def all_gather_vocab(self, local: torch.Tensor, vocab: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """[n, V/T] shards -> [n, V] (last shard may be short: shards are padded to V/T)."""
+        n, vp = local.shape
+        per = (vocab + self.size - 1) // self.size
+        if vp != per:
+            pad = torch.zeros((n, per), dtype=local.dtype, device=local.device)
+            pad[:, :vp] = local
+            pad[:, vp:] = float("-inf")
+            local = pad
+        gathered = torch.empty((self.size, n, per), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(gathered, local.contiguous(), group=self.group)
+        full = gathered.permute(1, 0, 2).reshape(n, self.size * per)[:, :vocab]
+        if out is not None:
+            out.copy_(full)
+            return out
+        return full.contiguous()
+
+    def barrier(self):
+        if self.size > 1:
+            dist.barrier(group=self.group)
+
+
+def init_distributed(tp_size: Optional[int] = None, backend: Optional[str] = None) -> TPContext:
+    """Initialise torch.distributed from torchrun env vars and split ranks into TP groups.
+
+    Returns TPContext for this rank. Single-process runs return TPContext.single().
+    """
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1:
+        return TPContext.single()
+    rank = int(os.environ.get("RANK", "0"))
+    if not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            local = int(os.environ.get("LOCAL_RANK", rank))
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    tp = tp_size or world
+    assert world % tp == 0, f"world {world} not divisible by tp {tp}"
+    groups = [dist.new_group(list(range(s, s + tp))) for s in range(0, world, tp)]
+    gi = rank // tp
+    return TPContext(rank=rank % tp, size=tp, group=groups[gi], dp_rank=gi, dp_size=world // tp)

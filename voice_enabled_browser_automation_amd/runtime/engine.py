@@ -1,0 +1,271 @@
+"""LLM execution engine: sequences, paged KV, ragged decode steps, hipGraph capture (N3).
+
+A *step* runs M token rows through the model.  Rows may belong to different sequences
+(continuous batching of concurrent voice sessions) or be consecutive tokens of one sequence
+(jump-forward of grammar-forced tokens, short prompt suffixes).  Every row carries its own
+position, KV slot, block-table row and context length, so one code path -- the MFMA skinny
+GEMMs + paged decode attention -- serves all of them, and its launch shape depends only on
+the row bucket M.  Each bucket (1, 2, 4, ..., 64) is captured once into a hipGraph
+(torch.cuda.CUDAGraph on ROCm) and replayed: the ~165 kernels of a Llama-3-8B step are
+then one graph launch instead of ~165 Python-driven launches.
+
+Longer prompt chunks (> 64 rows) go through the prefill path (hipBLASLt GEMMs + flash
+attention over the paged cache with a causal query offset), eagerly.
+
+Sampling runs after the forward on the same stream so the CPU can compute the grammar mask
+for this step while the GPU is busy with the forward (see brain.intent_engine).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from types import SimpleNamespace
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from .. import ops
+from .kv_cache import BlockManager, PagedKVCache
+
+BUCKETS = (1, 2, 4, 8, 16, 32, 64)
+
+
+def bucket_for(n: int) -> int:
+    for b in BUCKETS:
+        if n <= b:
+            return b
+    raise ValueError(f"{n} rows exceed the largest decode bucket")
+
+
+@dataclass
+class Sequence_:
+    sid: int                     # block-table row
+    tokens: List[int] = field(default_factory=list)
+    blocks: List[int] = field(default_factory=list)
+    n_computed: int = 0          # tokens whose K/V are in the cache
+    n_cached_prefix: int = 0     # tokens served from the prefix cache
+
+
+class StepBuffers:
+    """Device buffers with fixed addresses (graph inputs/outputs) + pinned host staging."""
+
+    def __init__(self, model, max_rows: int, max_seqs: int, max_blocks_per_seq: int, max_ctx: int, device):
+        i32 = dict(dtype=torch.int32, device=device)
+        dt = model.dtype
+        self.max_rows = max_rows
+        self.max_ctx = max_ctx
+        self.tokens = torch.zeros(max_rows, **i32)
+        self.positions = torch.zeros(max_rows, **i32)
+        self.seq_ids = torch.zeros(max_rows, **i32)
+        self.ctx_lens = torch.ones(max_rows, **i32)
+        self.slots = torch.full((max_rows,), -1, dtype=torch.int64, device=device)
+        self.block_table = torch.zeros(max_seqs, max_blocks_per_seq, **i32)
+        d = model.cfg.hidden
+        self.hidden = torch.zeros(max_rows, d, dtype=dt, device=device)
+        self.q = torch.zeros(max_rows, model.nq * model.hd, dtype=dt, device=device)
+        self.attn = torch.zeros_like(self.q)
+        self.act = torch.zeros(max_rows, model.F, dtype=dt, device=device)
+        self.logits_local = torch.zeros(max_rows, model.v_end - model.v_start, dtype=torch.float32, device=device)
+        self.logits = torch.zeros(max_rows, model.cfg.vocab_size, dtype=torch.float32, device=device) \
+            if model.tp.size > 1 else self.logits_local
+        ns = ops.decode_n_splits(max_ctx)
+        self.part_o = torch.zeros(max_rows * ns * model.nq * model.hd, dtype=torch.float32, device=device)
+        self.part_ml = torch.zeros(max_rows * ns * model.nq * 2, dtype=torch.float32, device=device)
+        pin = torch.device(device).type == "cuda"
+        self.h_i32 = torch.zeros(4, max_rows, dtype=torch.int32, pin_memory=pin)
+        self.h_slots = torch.full((max_rows,), -1, dtype=torch.int64, pin_memory=pin)
+        self.h_table = torch.zeros(max_seqs, max_blocks_per_seq, dtype=torch.int32, pin_memory=pin)
+        self.table_dirty = True
+
+    def upload(self, n_rows: int) -> None:
+        nb = True
+        self.tokens.copy_(self.h_i32[0], non_blocking=nb)
+        self.positions.copy_(self.h_i32[1], non_blocking=nb)
+        self.seq_ids.copy_(self.h_i32[2], non_blocking=nb)
+        self.ctx_lens.copy_(self.h_i32[3], non_blocking=nb)
+        self.slots.copy_(self.h_slots, non_blocking=nb)
+        if self.table_dirty:
+            self.block_table.copy_(self.h_table, non_blocking=nb)
+            self.table_dirty = False
+
+
+class LLMEngine:
+    def __init__(self, model, *, max_seqs: int = 8, max_model_len: int = 4096, block_size: int = 16,
+                 kv_blocks: Optional[int] = None, kv_gb: Optional[float] = None, use_graphs: Optional[bool] = None,
+                 max_rows: int = 64):
+        self.model = model
+        self.device = model.device
+        self.block_size = block_size
+        self.max_model_len = max_model_len
+        self.max_seqs = max_seqs
+        cfg = model.cfg
+        if kv_blocks is None:
+            if kv_gb is None:
+                kv_gb = float(os.environ.get("VWA_KV_GB", "0") or 0)
+            if kv_gb > 0:
+                kv_blocks = PagedKVCache.blocks_for_budget(kv_gb * 1e9, cfg.n_layers, model.nkv, model.hd, block_size)
+            else:
+                kv_blocks = max_seqs * (max_model_len // block_size) * 2 + 1
+        self.kv = PagedKVCache(cfg.n_layers, model.nkv, model.hd, block_size, kv_blocks, device=self.device,
+                               dtype=model.dtype)
+        self.blocks = BlockManager(kv_blocks, block_size)
+        self.max_blocks_per_seq = (max_model_len + block_size - 1) // block_size
+        self.bufs = StepBuffers(model, max_rows, max_seqs, self.max_blocks_per_seq, max_model_len, self.device)
+        self.free_sids = list(range(max_seqs - 1, -1, -1))
+        self.seqs: Dict[int, Sequence_] = {}
+        if use_graphs is None:
+            use_graphs = ops.env_flag("VWA_HIPGRAPH", True)
+        self.use_graphs = bool(use_graphs) and self.device.type == "cuda"
+        self.graphs: Dict[int, Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
+        self.graph_pool = None
+        self.stats = dict(steps=0, rows=0, prefill_tokens=0, cached_tokens=0, graph_replays=0)
+
+    # ------------------------------------------------------------------ sequences
+    def new_sequence(self, tokens: Sequence[int], use_prefix_cache: bool = True) -> Sequence_:
+        if not self.free_sids:
+            raise RuntimeError("too many concurrent sequences")
+        sid = self.free_sids.pop()
+        seq = Sequence_(sid=sid, tokens=list(tokens))
+        if use_prefix_cache:
+            blocks, n = self.blocks.match_prefix(seq.tokens)
+            seq.blocks = blocks
+            seq.n_computed = n
+            seq.n_cached_prefix = n
+            self.stats["cached_tokens"] += n
+        self.seqs[sid] = seq
+        self._sync_table(seq)
+        return seq
+
+    def free_sequence(self, seq: Sequence_, publish: bool = True) -> None:
+        if publish:
+            self.blocks.register_prefix(seq.tokens, seq.blocks, seq.n_computed)
+        self.blocks.release(seq.blocks)
+        seq.blocks = []
+        self.seqs.pop(seq.sid, None)
+        self.free_sids.append(seq.sid)
+
+    def _ensure_blocks(self, seq: Sequence_, n_tokens: int) -> None:
+        need = (n_tokens + self.block_size - 1) // self.block_size
+        if need > self.max_blocks_per_seq:
+            raise RuntimeError(f"sequence exceeds max_model_len={self.max_model_len}")
+        if need > len(seq.blocks):
+            seq.blocks += self.blocks.allocate(need - len(seq.blocks))
+            self._sync_table(seq)
+
+    def _sync_table(self, seq: Sequence_) -> None:
+        row = self.bufs.h_table[seq.sid]
+        row.zero_()
+        if seq.blocks:
+            row[: len(seq.blocks)] = torch.tensor(seq.blocks, dtype=torch.int32)
+        self.bufs.table_dirty = True
+
+    def slot_of(self, seq: Sequence_, pos: int) -> int:
+        return seq.blocks[pos // self.block_size] * self.block_size + pos % self.block_size
+
+    # ------------------------------------------------------------------ forward
+    def _forward_rows(self, M: int) -> torch.Tensor:
+        return self.model.forward(self.bufs, M, self.kv)
+
+    def _capture(self, M: int):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._forward_rows(M)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        if self.graph_pool is None:
+            self.graph_pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(g, pool=self.graph_pool):
+            out = self._forward_rows(M)
+        self.graphs[M] = (g, out)
+        return self.graphs[M]
+
+    def capture_all(self, buckets: Sequence[int] = BUCKETS) -> None:
+        if not self.use_graphs:
+            return
+        for M in buckets:
+            if M <= self.bufs.max_rows and M not in self.graphs:
+                self._capture(M)
+        torch.cuda.synchronize()
+
+    def run_rows(self, rows: List[Tuple[Sequence_, int]]) -> torch.Tensor:
+        """Append one token per row (row = (seq, token)), return f32 logits [len(rows), V].
+
+        Rows of the same sequence must be consecutive and in order.
+        """
+        n = len(rows)
+        M = bucket_for(n)
+        b = self.bufs
+        hi = b.h_i32
+        # per-sequence running length (several rows may extend the same sequence)
+        for seq, _tok in rows:
+            pass
+        pending: Dict[int, int] = {}
+        for i, (seq, tok) in enumerate(rows):
+            pos = pending.get(seq.sid, seq.n_computed)
+            self._ensure_blocks(seq, pos + 1)
+            if pos >= len(seq.tokens):
+                seq.tokens.append(tok)
+            hi[0, i] = tok
+            hi[1, i] = pos
+            hi[2, i] = seq.sid
+            hi[3, i] = pos + 1
+            b.h_slots[i] = self.slot_of(seq, pos)
+            pending[seq.sid] = pos + 1
+        for i in range(n, M):  # padded rows: no KV write, 1-token context on scratch block 0
+            hi[0, i] = 0
+            hi[1, i] = 0
+            hi[2, i] = 0
+            hi[3, i] = 1
+            b.h_slots[i] = -1
+        b.upload(M)
+        if self.use_graphs:
+            g, out = self.graphs.get(M) or self._capture(M)
+            g.replay()
+            self.stats["graph_replays"] += 1
+        else:
+            out = self._forward_rows(M)
+        for sid, ln in pending.items():
+            self.seqs[sid].n_computed = ln
+        self.stats["steps"] += 1
+        self.stats["rows"] += n
+        return out[:n]
+
+    def prefill(self, seq: Sequence_, chunk: int = 2048) -> torch.Tensor:
+        """Compute K/V for seq.tokens[n_computed:]; returns f32 logits of the last token [1, V]."""
+        todo = len(seq.tokens) - seq.n_computed
+        assert todo >= 1, "nothing to prefill"
+        self.stats["prefill_tokens"] += todo
+        if todo <= self.bufs.max_rows:
+            toks = seq.tokens[seq.n_computed:]
+            out = self.run_rows([(seq, t) for t in toks])
+            return out[-1:]
+        logits = None
+        while seq.n_computed < len(seq.tokens):
+            start = seq.n_computed
+            n = min(chunk, len(seq.tokens) - start)
+            if n <= self.bufs.max_rows:
+                toks = seq.tokens[start : start + n]
+                logits = self.run_rows([(seq, t) for t in toks])[-1:]
+                continue
+            self._ensure_blocks(seq, start + n)
+            if self.bufs.table_dirty:
+                self.bufs.block_table.copy_(self.bufs.h_table)
+                self.bufs.table_dirty = False
+            dev = self.device
+            pos = torch.arange(start, start + n, dtype=torch.int32)
+            slots = torch.tensor([self.slot_of(seq, int(p)) for p in pos], dtype=torch.int64)
+            m = self.model
+            scratch = SimpleNamespace(
+                tokens=torch.tensor(seq.tokens[start : start + n], dtype=torch.int32, device=dev),
+                positions=pos.to(dev), slots=slots.to(dev), block_table=self.bufs.block_table,
+                hidden=torch.empty(n, m.cfg.hidden, dtype=m.dtype, device=dev),
+                q=torch.empty(n, m.nq * m.hd, dtype=m.dtype, device=dev),
+                act=torch.empty(n, m.F, dtype=m.dtype, device=dev),
+                logits_local=self.bufs.logits_local, logits=self.bufs.logits, max_ctx=self.max_model_len,
+            )
+            logits = m.forward(scratch, n, self.kv, prefill_seq=seq.sid, q_offset=start,
+                               logits_rows=slice(n - 1, n))
+            seq.n_computed = start + n
+        return logits
