@@ -62,6 +62,7 @@ class LLMIntentEngine:
         self.part_idx = torch.zeros(64, dtype=torch.int32, device=dev)
         self.last_stats: Dict[str, Any] = {}
         self._prefix_ids: Dict[str, List[int]] = {}
+        self._head_len = 0
 
     # ------------------------------------------------------------------ helpers
     def _encode_prompt(self, messages) -> List[int]:
@@ -70,6 +71,7 @@ class LLMIntentEngine:
         if ids is None:
             ids = self.tok.encode(head)
             self._prefix_ids = {head: ids}
+        self._head_len = len(ids)
         return ids + self.tok.encode(tail)
 
     def _sample(self, logits: torch.Tensor) -> int:
@@ -137,7 +139,9 @@ class LLMIntentEngine:
                                    decode_ms=(t_end - t_prefill) * 1e3, total_ms=(t_end - t0) * 1e3)
             return out.decode("utf-8")
         finally:
-            eng.free_sequence(seq)
+            # only the static system + few-shot prefix is shared across requests; the request's
+            # own suffix and answer are never served from cache (no replay of repeated commands)
+            eng.free_sequence(seq, publish_upto=self._head_len)
 
     def grammar_bytes(self, tok: int) -> bytes:
         return self.tok.token_bytes()[tok]

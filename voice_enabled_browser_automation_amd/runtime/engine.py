@@ -136,9 +136,12 @@ class LLMEngine:
         self._sync_table(seq)
         return seq
 
-    def free_sequence(self, seq: Sequence_, publish: bool = True) -> None:
+    def free_sequence(self, seq: Sequence_, publish: bool = True, publish_upto: Optional[int] = None) -> None:
+        """Release a sequence; publish its first ``publish_upto`` computed tokens (default all) to the
+        prefix cache."""
         if publish:
-            self.blocks.register_prefix(seq.tokens, seq.blocks, seq.n_computed)
+            n = seq.n_computed if publish_upto is None else min(seq.n_computed, publish_upto)
+            self.blocks.register_prefix(seq.tokens, seq.blocks, n)
         self.blocks.release(seq.blocks)
         seq.blocks = []
         self.seqs.pop(seq.sid, None)
