@@ -36,6 +36,23 @@ void check_contig_rows(const Tensor& t, const char* name) {
 }
 void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, what, " launch failed with code ", rc); }
 
+// skinny GEMM dispatch: 1 = persistent streaming kernel when the shape fits (default), 0 = one-tile kernel
+int g_skinny_mode = 1;
+int g_grid_cap = 256;
+int g_ks = 8;
+void set_skinny_mode(int64_t mode, int64_t grid_cap, int64_t ks) {
+  g_skinny_mode = (int)mode;
+  g_grid_cap = (int)grid_cap;
+  g_ks = (int)ks;
+}
+int run_skinny(int epi, const SkinnyParams& p, hipStream_t st) {
+  if (g_skinny_mode == 1) {
+    const int r = vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
+    if (r != -10) return r;
+  }
+  return vwa_skinny_gemm(epi, &p, st);
+}
+
 SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool fuse_rms, double eps) {
   check_bf16(x, "x");
   check_bf16(w, "w");
@@ -82,7 +99,7 @@ void skinny_gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64
     p.R = bfp(*residual);
     p.ldr = (int)residual->stride(0);
   }
-  check_rc(vwa_skinny_gemm((int)epi, &p, cur_stream(x)), "skinny_gemm");
+  check_rc(run_skinny((int)epi, p, cur_stream(x)), "skinny_gemm");
 }
 
 void skinny_gemm_swiglu(Tensor x, Tensor w_gu, c10::optional<Tensor> bias, Tensor h, bool fuse_rms, double eps) {
@@ -94,7 +111,7 @@ void skinny_gemm_swiglu(Tensor x, Tensor w_gu, c10::optional<Tensor> bias, Tenso
   TORCH_CHECK(w_gu.size(0) % 32 == 0, "gate/up rows must be a multiple of 32");
   p.Y = h.data_ptr();
   p.ldy = (int)h.stride(0);
-  check_rc(vwa_skinny_gemm(2, &p, cur_stream(x)), "skinny_gemm_swiglu");
+  check_rc(run_skinny(2, p, cur_stream(x)), "skinny_gemm_swiglu");
 }
 
 void check_cache(const Tensor& c, const char* name) {
@@ -135,7 +152,7 @@ void skinny_gemm_qkv(Tensor x, Tensor w_qkv, c10::optional<Tensor> bias, bool fu
   p.cache_stride_block = k_cache.stride(0);
   p.cache_stride_head = k_cache.stride(1);
   p.cache_stride_tok = k_cache.stride(2);
-  check_rc(vwa_skinny_gemm(4, &p, cur_stream(x)), "skinny_gemm_qkv");
+  check_rc(run_skinny(4, p, cur_stream(x)), "skinny_gemm_qkv");
 }
 
 void rmsnorm(Tensor x, c10::optional<Tensor> residual, c10::optional<Tensor> residual_out, c10::optional<Tensor> w,
@@ -409,5 +426,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pcm16_to_f32", &pcm16_to_f32);
   m.def("log_mel", &log_mel);
   m.def("conv1d_gelu", &conv1d_gelu);
+  m.def("set_skinny_mode", &set_skinny_mode, py::arg("mode"), py::arg("grid_cap") = 256, py::arg("ks") = 8);
   m.def("attention_split_tokens", []() { return vwa_attention_split_tokens(); });
 }

@@ -65,24 +65,38 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
   }
   __syncthreads();
 
-  // ---- Q.K (lane = key)
+  // ---- Q.K (lane = key); the V chunk loads of the P.V phase are issued right after the K
+  // loads (their addresses do not depend on the scores), so both HBM round trips overlap.
+  constexpr int NCH = D / 8;        // 16-byte chunks per row
+  constexpr int TG = 64 / NCH;      // token groups
+  constexpr int NI = kSplit / TG;   // tokens per lane
+  const int c = lane % NCH, tg = lane / NCH;
   const int t = t0 + lane;
+  uint4 kv4[D / 8];
+  if (t < tend) {
+    const uint4* kr = reinterpret_cast<const uint4*>(p.kv.k + kv_offset(p.kv, seq, kvh, t));
+#pragma unroll
+    for (int cc = 0; cc < D / 8; ++cc) kv4[cc] = kr[cc];
+  }
+  uint4 vv[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int tt = t0 + tg + TG * i;
+    vv[i] = (tt < tend) ? *reinterpret_cast<const uint4*>(p.kv.v + kv_offset(p.kv, seq, kvh, tt) + c * 8)
+                        : make_uint4(0, 0, 0, 0);
+  }
   float s[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) s[g] = 0.f;
   if (t < tend) {
-    const uint4* kr = reinterpret_cast<const uint4*>(p.kv.k + kv_offset(p.kv, seq, kvh, t));
-    uint4 kv4[D / 8];
 #pragma unroll
-    for (int c = 0; c < D / 8; ++c) kv4[c] = kr[c];
-#pragma unroll
-    for (int c = 0; c < D / 8; ++c) {
+    for (int cc = 0; cc < D / 8; ++cc) {
       float kf[8];
-      unpack8(kv4[c], kf);
+      unpack8(kv4[cc], kf);
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const float4 qa = *reinterpret_cast<const float4*>(&qs[g][c * 8]);
-        const float4 qb = *reinterpret_cast<const float4*>(&qs[g][c * 8 + 4]);
+        const float4 qa = *reinterpret_cast<const float4*>(&qs[g][cc * 8]);
+        const float4 qb = *reinterpret_cast<const float4*>(&qs[g][cc * 8 + 4]);
         s[g] += qa.x * kf[0] + qa.y * kf[1] + qa.z * kf[2] + qa.w * kf[3] + qb.x * kf[4] + qb.y * kf[5] +
                 qb.z * kf[6] + qb.w * kf[7];
       }
@@ -100,18 +114,7 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
   }
   __syncthreads();
 
-  // ---- P.V (lane = dim chunk c, token group tg)
-  constexpr int NCH = D / 8;        // 16-byte chunks per row
-  constexpr int TG = 64 / NCH;      // token groups
-  constexpr int NI = kSplit / TG;   // tokens per lane
-  const int c = lane % NCH, tg = lane / NCH;
-  uint4 vv[NI];
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int tt = t0 + tg + TG * i;
-    vv[i] = (tt < tend) ? *reinterpret_cast<const uint4*>(p.kv.v + kv_offset(p.kv, seq, kvh, tt) + c * 8)
-                        : make_uint4(0, 0, 0, 0);
-  }
+  // ---- P.V (lane = dim chunk c, token group tg; V already in registers)
   float o[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g)
@@ -159,30 +162,52 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
   }
 }
 
+// One wave per (row, q-head): split statistics are loaded in parallel (lane = split), the
+// log-sum-exp weights go through LDS, then every lane sums its dims over the splits with
+// independent loads (no serial load->use chain).
 template <int D>
-__global__ __launch_bounds__(D) void attn_combine_kernel(DecodeAttnParams p) {
+__global__ __launch_bounds__(64) void attn_combine_kernel(DecodeAttnParams p) {
+  __shared__ float wts[256];
   const int row = blockIdx.x / p.n_q_heads, h = blockIdx.x % p.n_q_heads;
-  const int d = threadIdx.x;
+  const int lane = threadIdx.x;
   const int ctx = p.ctx_lens[row];
-  const int ns = min(p.n_splits, (ctx + kSplit - 1) / kSplit);
-  float M = -INFINITY;
-  for (int s = 0; s < ns; ++s) M = fmaxf(M, p.part_ml[(((int64_t)row * p.n_splits + s) * p.n_q_heads + h) * 2]);
-  float acc = 0.f, L = 0.f;
-  for (int s = 0; s < ns; ++s) {
-    const float* pm = p.part_ml + (((int64_t)row * p.n_splits + s) * p.n_q_heads + h) * 2;
-    if (pm[0] == -INFINITY) continue;
-    const float f = __expf(pm[0] - M);
-    L += pm[1] * f;
-    acc += p.part_o[(((int64_t)row * p.n_splits + s) * p.n_q_heads + h) * D + d] * f;
+  const int ns = min(min(p.n_splits, (ctx + kSplit - 1) / kSplit), 256);
+  const float* pm = p.part_ml + ((int64_t)row * p.n_splits * p.n_q_heads + h) * 2;
+  const int64_t sstride = (int64_t)p.n_q_heads * 2;
+  float mloc = -INFINITY;
+  for (int s = lane; s < ns; s += 64) mloc = fmaxf(mloc, pm[s * sstride]);
+  const float M = wave_max(mloc);
+  float lsum = 0.f;
+  for (int s = lane; s < ns; s += 64) {
+    const float m = pm[s * sstride];
+    const float f = (m == -INFINITY) ? 0.f : __expf(m - M);
+    wts[s] = f;
+    lsum += pm[s * sstride + 1] * f;
   }
-  p.out[(int64_t)row * p.ldo + h * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+  const float L = wave_sum(lsum);
+  __syncthreads();
+  constexpr int DPL = D / 64;
+  float acc[DPL];
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
+  const float* po = p.part_o + ((int64_t)row * p.n_splits * p.n_q_heads + h) * D + lane * DPL;
+  const int64_t ostride = (int64_t)p.n_q_heads * D;
+#pragma unroll 8
+  for (int s = 0; s < ns; ++s) {
+    const float f = wts[s];
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) acc[j] += po[s * ostride + j] * f;
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+#pragma unroll
+  for (int j = 0; j < DPL; ++j) p.out[(int64_t)row * p.ldo + h * D + lane * DPL + j] = f2bf(acc[j] * inv);
 }
 
 template <int D, int G>
 void launch_decode(const DecodeAttnParams& p, hipStream_t st) {
   hipLaunchKernelGGL((decode_attn_kernel<D, G>), dim3(p.rows * p.n_kv_heads, p.n_splits), dim3(64), 0, st, p);
   if (p.n_splits > 1)
-    hipLaunchKernelGGL((attn_combine_kernel<D>), dim3(p.rows * p.n_q_heads), dim3(D), 0, st, p);
+    hipLaunchKernelGGL((attn_combine_kernel<D>), dim3(p.rows * p.n_q_heads), dim3(64), 0, st, p);
 }
 
 template <int D>

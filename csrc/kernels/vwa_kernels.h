@@ -62,6 +62,7 @@ struct FlashAttnParams {
 extern "C" {
 #endif
 int vwa_skinny_gemm(int epi, const SkinnyParams* p, hipStream_t st);
+int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st);
 int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
                 uint16_t* y, int rows, int D, int ldx, float eps, hipStream_t st);
 int vwa_layernorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,

@@ -33,9 +33,16 @@ def close(a, b, atol, rtol=2e-2):
     assert err <= tol, f"max err {err} > tol {tol}"
 
 
+@pytest.fixture(params=[(0, 256, 8), (1, 256, 8), (1, 768, 4)], ids=["tile", "stream8", "stream4"])
+def skinny_mode(request):
+    ops.ext().set_skinny_mode(*request.param)
+    yield request.param
+    ops.ext().set_skinny_mode(1, 256, 8)
+
+
 @pytest.mark.parametrize("M", [1, 5, 17, 40])
 @pytest.mark.parametrize("fuse_rms", [False, True])
-def test_skinny_store_resid_gelu(M, fuse_rms):
+def test_skinny_store_resid_gelu(M, fuse_rms, skinny_mode):
     K, N = 1024, 384
     x = rnd(M, K)
     w = rnd(N, K, scale=0.05)
@@ -49,7 +56,7 @@ def test_skinny_store_resid_gelu(M, fuse_rms):
         close(out, exp, 2e-2)
 
 
-def test_skinny_f32_out_large_n_and_inplace_residual():
+def test_skinny_f32_out_large_n_and_inplace_residual(skinny_mode):
     M, K, N = 3, 4096, 4096
     x = rnd(M, K)
     w = rnd(N, K, scale=0.02)
@@ -67,7 +74,7 @@ def test_skinny_f32_out_large_n_and_inplace_residual():
 
 
 @pytest.mark.parametrize("M", [1, 33])
-def test_skinny_swiglu(M):
+def test_skinny_swiglu(M, skinny_mode):
     K, F = 512, 256
     x = rnd(M, K)
     wg, wu = rnd(F, K, scale=0.05), rnd(F, K, scale=0.05)
@@ -91,7 +98,7 @@ def _kv_setup(nq, nkv, hd, blocks=16, bs=16):
 
 
 @pytest.mark.parametrize("M", [1, 7, 70])
-def test_qkv_rope_write(M):
+def test_qkv_rope_write(M, skinny_mode):
     nq, nkv, hd, K = 8, 2, 128, 512
     H = nq + 2 * nkv
     w = rnd(H * hd, K, scale=0.05)
@@ -195,6 +202,18 @@ def test_flash_attention_encoder_contiguous():
     exp = torch.nn.functional.scaled_dot_product_attention(q.float().transpose(1, 2), k.float().transpose(1, 2),
                                                            v.float().transpose(1, 2)).transpose(1, 2)
     close(out, exp.cpu(), 2e-2)
+
+
+def test_skinny_stream_many_tiles_and_k_tail(skinny_mode):
+    # K = 384 (3 k-groups: waves with empty ranges), N spanning several persistent tiles per WG
+    for M, K, N in ((1, 384, 51872), (4, 14336, 4096), (16, 1280, 5120)):
+        x = rnd(M, K)
+        w = rnd(N, K, scale=0.03)
+        out = torch.empty(M, N, dtype=torch.float32, device=DEV)
+        ops.linear(x, w, out=out, fuse_rms=True)
+        exp = torch.empty(M, N, dtype=torch.float32)
+        ref.linear(x.cpu(), w.cpu(), out=exp, fuse_rms=True)
+        close(out, exp, 1e-2)
 
 
 def test_sample_greedy_masked_and_gumbel():

@@ -15,17 +15,27 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import voice_enabled_browser_automation_amd.ops as ops  # noqa: E402
 
 
-def timeit(fn, iters=50, warm=5):
-    for _ in range(warm):
+def timeit(fn, iters=40, reps=5):
+    """GPU time per call: `iters` calls captured in one hipGraph, replayed `reps` times
+    (no Python/launch gaps in the measurement)."""
+    for _ in range(3):
         fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for _ in range(iters):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
-    for _ in range(iters):
-        fn()
+    for _ in range(reps):
+        g.replay()
     ev1.record()
     torch.cuda.synchronize()
-    return ev0.elapsed_time(ev1) / iters * 1e3  # us
+    return ev0.elapsed_time(ev1) / (iters * reps) * 1e3  # us
 
 
 def main():
@@ -51,6 +61,12 @@ def main():
                 it[0] = (it[0] + 1) % ncopy
                 ops.ext().skinny_gemm(x, ws[it[0]], None, y, 0, False, 1e-5, None)
 
+            variants = {}
+            for mode, cap, ks in ((0, 256, 8), (1, 256, 8), (1, 512, 4), (1, 768, 4)):
+                ops.ext().set_skinny_mode(mode, cap, ks)
+                variants[f"m{mode}_g{cap}_k{ks}"] = round(timeit(ours), 2)
+            ops.ext().set_skinny_mode(1, 256, 8)
+
             def blas():
                 it[0] = (it[0] + 1) % ncopy
                 torch.matmul(x, ws[it[0]].t())
@@ -59,7 +75,7 @@ def main():
             t_blas = timeit(blas)
             del ws
             gb = N * K * 2 / 1e9
-            r = dict(kernel="skinny_gemm", shape=name, M=M, N=N, K=K, us=round(t_ours, 2),
+            r = dict(kernel="skinny_gemm", shape=name, M=M, N=N, K=K, us=round(t_ours, 2), variants=variants,
                      tbps=round(gb / (t_ours * 1e-6) / 1e3, 3), hipblaslt_us=round(t_blas, 2),
                      hipblaslt_tbps=round(gb / (t_blas * 1e-6) / 1e3, 3))
             print(json.dumps(r), flush=True)

@@ -1,0 +1,131 @@
+"""Brain service: ``GET /health``, ``POST /parse``, ``GET /metrics`` (parity with apps/brain/src/server.ts).
+
+Request flow (apps/brain/src/server.ts:89-139):
+  ParseRequest validation -> 400 {error:"invalid_request", detail}
+  prompt (system + few-shots + user JSON) -> intent engine
+     engine raises            -> 500 {error:"llm_error", detail}
+     reply fails ParseResponse -> ONE repair call with the repair system note
+  final validation fails      -> 422 {error:"schema_validation_failed", detail}
+  200 -> ParseResponse with zod-style defaults filled.
+
+With the LLM engine the grammar makes the first answer schema-valid, so the repair path only
+runs for engines without constrained decoding (or injected faults in tests).
+
+Engines (VWA_BRAIN_ENGINE): ``llm`` (on-GPU Llama + constrained decoding; VWA_LLM_MODEL, VWA_TP),
+``keyword`` (rule-based, CPU), or any object passed to ``build_app(engine=...)``.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import time
+from typing import Any, Optional
+
+from aiohttp import web
+
+from ..contracts import ParseRequest, ParseResponse, safe_parse
+from ..utils.metrics import Metrics
+from .prompt import messages_for
+
+SERVICE_NAME = "brain-ts"  # byte-compatible /health payload (apps/brain/src/server.ts:87)
+
+
+def build_app(engine: Any = None) -> web.Application:
+    if engine is None:
+        engine = make_engine_from_env()
+    app = web.Application()
+    app["engine"] = engine
+    app["lock"] = asyncio.Lock()
+    app["metrics"] = Metrics("brain")
+
+    async def health(_req: web.Request) -> web.Response:
+        return web.json_response({"status": "ok", "service": SERVICE_NAME})
+
+    async def metrics(_req: web.Request) -> web.Response:
+        snap = app["metrics"].snapshot()
+        st = getattr(app["engine"], "last_stats", None)
+        if st:
+            snap["last_request"] = st
+        return web.json_response(snap)
+
+    async def parse(req: web.Request) -> web.Response:
+        m: Metrics = app["metrics"]
+        t0 = time.perf_counter()
+        try:
+            body = await req.json()
+        except Exception:  # noqa: BLE001
+            body = None
+        pr = safe_parse(ParseRequest, body)
+        if not pr.success:
+            m.inc("invalid_request")
+            return web.json_response({"error": "invalid_request", "detail": pr.format_error()}, status=400)
+        request = pr.data
+        eng = app["engine"]
+        loop = asyncio.get_running_loop()
+        try:
+            async with app["lock"]:  # one engine, serial requests (the engine batches internally)
+                out = await loop.run_in_executor(None, eng, messages_for(request))
+                first = safe_parse(ParseResponse, out)
+                if not first.success:
+                    m.inc("repairs")
+                    out = await loop.run_in_executor(None, eng, messages_for(request, repair=True))
+        except Exception as e:  # noqa: BLE001
+            m.inc("llm_error")
+            return web.json_response({"error": "llm_error", "detail": str(e) or e.__class__.__name__}, status=500)
+        final = safe_parse(ParseResponse, out)
+        if not final.success:
+            m.inc("schema_validation_failed")
+            return web.json_response({"error": "schema_validation_failed", "detail": final.format_error()}, status=422)
+        m.observe("parse_ms", (time.perf_counter() - t0) * 1e3)
+        m.inc("ok")
+        return web.json_response(final.data)
+
+    app.router.add_get("/health", health)
+    app.router.add_get("/metrics", metrics)
+    app.router.add_post("/parse", parse)
+    return app
+
+
+def make_engine_from_env():
+    kind = os.environ.get("VWA_BRAIN_ENGINE", "keyword")
+    if kind == "keyword":
+        from .intent_engine import FakeIntentEngine, keyword_intents
+
+        return FakeIntentEngine(fn=keyword_intents)
+    if kind == "llm":
+        return build_llm_engine()
+    raise ValueError(f"unknown VWA_BRAIN_ENGINE={kind!r}")
+
+
+def build_llm_engine(model_name: Optional[str] = None, device: Optional[str] = None):
+    import torch
+
+    from ..models.config import get_config
+    from ..models.llama import LlamaModel
+    from ..parallel.tp import init_distributed
+    from ..runtime.engine import LLMEngine
+    from ..tokenizer import load_tokenizer
+    from .intent_engine import LLMIntentEngine
+
+    name = model_name or os.environ.get("VWA_LLM_MODEL", "llama3-8b")
+    tp = init_distributed(tp_size=int(os.environ.get("VWA_TP", "1") or 1))
+    dev = device or ("cuda" if torch.cuda.is_available() else "cpu")
+    model = LlamaModel(get_config(name), device=dev, tp=tp, seed=int(os.environ.get("VWA_SEED", "0")))
+    eng = LLMEngine(model, max_seqs=int(os.environ.get("VWA_MAX_SESSIONS", "8")), max_model_len=4096)
+    eng.capture_all()
+    return LLMIntentEngine(eng, load_tokenizer("llama3"),
+                           budget_chars=int(os.environ.get("VWA_BUDGET_CHARS", "512")))
+
+
+def main():
+    from ..utils.env import load_dotenv
+
+    load_dotenv()
+    port = int(os.environ.get("BRAIN_PORT", "8090"))
+    print(f"[brain] listening on http://127.0.0.1:{port}", flush=True)
+    web.run_app(build_app(), host="127.0.0.1", port=port, print=None)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,236 @@
+"""Voice service: ``GET /health``, ``GET /metrics``, WebSocket ``/stream`` (parity with
+apps/voice/src/server.ts:60-304).
+
+Per connection:
+  * binary frames = raw PCM16 LE 16 kHz mono -> on-node streaming ASR (asr/streaming.py) ->
+    ``transcript_partial`` / ``transcript_final`` frames carrying Deepgram-shaped payloads;
+  * final transcripts are aggregated and debounced (``VWA_DEBOUNCE_MS``, reference fixed 1000 ms:
+    :229) before ``POST BRAIN_URL`` {text, context};
+  * brain reply -> ``intent`` frame, ``tts`` frame (tts_summary), context merge of
+    ``context_updates``, safe/risky split: safe intents go to ``POST EXECUTOR_URL/execute`` with
+    the connection's executor session id (``execution_result`` / ``execution_error``), risky
+    ones produce ``confirmation_required``;
+  * JSON control frames: ``{"type":"close"}``, ``{"type":"context_update","payload":{...}}``,
+    and ``{"type":"flush"}`` (end of utterance: finalise without waiting for silence).
+
+Races of the reference fixed here: brain calls and executor calls of one
+connection are serialised by a per-connection lock, so the executor session id is assigned in
+order; sends after a client disconnect are dropped.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+import os
+import time
+from concurrent.futures import ThreadPoolExecutor
+from typing import Any, Callable, Dict, Optional
+
+import aiohttp
+from aiohttp import WSMsgType, web
+
+from ..utils.metrics import Metrics
+
+VERSION = "0.1.0"
+
+
+async def post_json_and_return(session: aiohttp.ClientSession, url: str, body: Any) -> Any:
+    """postJsonAndReturn parity (apps/voice/src/server.ts:15-52): non-JSON reply -> {ok: False}."""
+    async with session.post(url, json=body) as resp:
+        text = await resp.text()
+    try:
+        return json.loads(text)
+    except ValueError:
+        return {"ok": False}
+
+
+def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Optional[str] = None,
+              executor_url: Optional[str] = None, debounce_ms: Optional[float] = None) -> web.Application:
+    """asr_factory() -> a StreamingAsrSession-like object (push(bytes)->events, flush()->events);
+    None = passthrough mode (no recognizer, as the reference without DEEPGRAM_API_KEY)."""
+    app = web.Application()
+    app["metrics"] = Metrics("voice")
+    app["asr_pool"] = ThreadPoolExecutor(max_workers=1, thread_name_prefix="asr")  # one GPU stream of work
+    brain_url = brain_url or os.environ.get("BRAIN_URL", "http://127.0.0.1:8090/parse")
+    executor_url = executor_url or os.environ.get("EXECUTOR_URL", "http://127.0.0.1:7081")
+    if debounce_ms is None:
+        debounce_ms = float(os.environ.get("VWA_DEBOUNCE_MS", "1000"))
+
+    async def on_startup(app_):
+        app_["http"] = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=120))
+
+    async def on_cleanup(app_):
+        await app_["http"].close()
+        app_["asr_pool"].shutdown(wait=False)
+
+    app.on_startup.append(on_startup)
+    app.on_cleanup.append(on_cleanup)
+
+    async def health(_req):
+        return web.json_response({"status": "ok", "service": "voice", "version": VERSION})
+
+    async def metrics(_req):
+        return web.json_response(app["metrics"].snapshot())
+
+    async def stream(req: web.Request) -> web.WebSocketResponse:
+        ws = web.WebSocketResponse()
+        await ws.prepare(req)
+        m: Metrics = app["metrics"]
+        m.inc("connections")
+        loop = asyncio.get_running_loop()
+        st: Dict[str, Any] = {"context": {}, "pending": "", "debounce": None, "session_id": None, "closed": False,
+                              "t_final": None}
+        lock = asyncio.Lock()
+
+        async def send(obj):
+            if st["closed"] or ws.closed:
+                return
+            try:
+                await ws.send_str(json.dumps(obj))
+            except (ConnectionResetError, RuntimeError):
+                st["closed"] = True
+
+        asr = asr_factory() if asr_factory is not None else None
+        if asr is not None:
+            await send({"type": "info", "payload": "asr_connected"})
+        else:
+            await send({"type": "warn", "payload": "no_api_key; running in passthrough"})
+
+        async def run_executor(safe):
+            try:
+                resp = await post_json_and_return(app["http"], f"{executor_url}/execute",
+                                                  {**({"session_id": st["session_id"]} if st["session_id"] else {}),
+                                                   "intents": safe})
+                st["session_id"] = resp.get("session_id", st["session_id"]) if isinstance(resp, dict) else st["session_id"]
+                await send({"type": "execution_result",
+                            "payload": f"Executed {len(safe)} actions successfully. Session: {st['session_id']}"})
+                m.inc("executions")
+            except Exception as e:  # noqa: BLE001
+                await send({"type": "execution_error", "payload": f"Execution failed: {e}"})
+                m.inc("execution_errors")
+
+        async def process(combined: str):
+            async with lock:
+                t0 = time.perf_counter()
+                try:
+                    resp = await post_json_and_return(app["http"], brain_url,
+                                                      {"text": combined, "context": st["context"]})
+                except Exception as e:  # noqa: BLE001
+                    m.inc("brain_errors")
+                    print(f"[voice] brain post failed: {e}", flush=True)
+                    return
+                await send({"type": "intent", "payload": resp})
+                if st["t_final"] is not None:
+                    m.observe("final_to_intent_ms", (time.perf_counter() - st["t_final"]) * 1e3)
+                m.observe("brain_ms", (time.perf_counter() - t0) * 1e3)
+                if isinstance(resp, dict) and resp.get("tts_summary"):
+                    await send({"type": "tts", "payload": resp["tts_summary"]})
+                if isinstance(resp, dict) and isinstance(resp.get("context_updates"), dict):
+                    st["context"] = {**st["context"], **resp["context_updates"]}
+                intents = resp.get("intents") if isinstance(resp, dict) else None
+                if isinstance(intents, list):
+                    safe = [i for i in intents if not (isinstance(i, dict) and i.get("requires_confirmation"))]
+                    risky = [i for i in intents if isinstance(i, dict) and i.get("requires_confirmation")]
+                    if safe:
+                        await run_executor(safe)
+                    if risky:
+                        await send({"type": "confirmation_required",
+                                    "payload": f"{len(risky)} risky actions require manual confirmation"})
+
+        async def debounced():
+            try:
+                await asyncio.sleep(debounce_ms / 1000.0)
+            except asyncio.CancelledError:
+                return
+            combined = st["pending"].strip()
+            st["pending"] = ""
+            st["debounce"] = None
+            if combined:
+                await process(combined)
+
+        async def handle_events(events):
+            for ev in events:
+                is_final = bool(ev.get("is_final") or (ev.get("channel") or {}).get("is_final"))
+                await send({"type": "transcript_final" if is_final else "transcript_partial", "payload": ev})
+                if not is_final:
+                    continue
+                alt = ((ev.get("channel") or {}).get("alternatives") or [{}])[0]
+                text = (alt.get("transcript") or "").strip()
+                if not text:
+                    continue
+                m.inc("finals")
+                st["t_final"] = time.perf_counter()
+                st["pending"] = f"{st['pending']} {text}" if st["pending"] else text
+                if st["debounce"] is not None:
+                    st["debounce"].cancel()
+                st["debounce"] = asyncio.ensure_future(debounced())
+
+        try:
+            async for msg in ws:
+                if msg.type == WSMsgType.BINARY:
+                    m.inc("audio_frames")
+                    if asr is not None:
+                        events = await loop.run_in_executor(app["asr_pool"], asr.push, msg.data)
+                        await handle_events(events)
+                elif msg.type == WSMsgType.TEXT:
+                    try:
+                        ctl = json.loads(msg.data)
+                    except ValueError:
+                        continue
+                    if not isinstance(ctl, dict):
+                        continue
+                    if ctl.get("type") == "close":
+                        await ws.close()
+                        break
+                    if ctl.get("type") == "context_update" and isinstance(ctl.get("payload"), dict):
+                        st["context"] = {**st["context"], **ctl["payload"]}
+                    elif ctl.get("type") == "flush" and asr is not None:
+                        events = await loop.run_in_executor(app["asr_pool"], asr.flush)
+                        await handle_events(events)
+                elif msg.type in (WSMsgType.ERROR, WSMsgType.CLOSE):
+                    break
+        finally:
+            st["closed"] = True
+            if st["debounce"] is not None:
+                st["debounce"].cancel()
+        return ws
+
+    app.router.add_get("/health", health)
+    app.router.add_get("/metrics", metrics)
+    app.router.add_get("/stream", stream)
+    return app
+
+
+def asr_factory_from_env() -> Optional[Callable[[], Any]]:
+    kind = os.environ.get("VWA_ASR_ENGINE", "none")
+    if kind == "none":
+        return None
+    import torch
+
+    from ..asr.engine import AsrEngine
+    from ..asr.streaming import StreamingAsrSession, make_asr_transcriber
+    from ..models.config import get_config
+    from ..models.whisper import WhisperModel
+    from ..tokenizer import load_tokenizer
+
+    name = os.environ.get("VWA_ASR_MODEL", "whisper-tiny")
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    eng = AsrEngine(WhisperModel(get_config(name), device=dev), load_tokenizer("whisper"),
+                    max_sessions=int(os.environ.get("VWA_MAX_SESSIONS", "4")))
+    fn = make_asr_transcriber(eng)
+    every = float(os.environ.get("VWA_PARTIAL_EVERY_S", "1.0"))
+    return lambda: StreamingAsrSession(fn, model_name=name, partial_every_s=every)
+
+
+def main():
+    from ..utils.env import load_dotenv
+
+    load_dotenv()
+    port = int(os.environ.get("VOICE_PORT", "7072"))
+    print(f"[voice] http/ws listening on http://127.0.0.1:{port}", flush=True)
+    # binds all interfaces, as the reference (apps/voice/src/server.ts:80)
+    web.run_app(build_app(asr_factory_from_env()), host="0.0.0.0", port=port, print=None)
+
+
+if __name__ == "__main__":
+    main()
