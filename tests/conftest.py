@@ -22,3 +22,12 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+def pytest_sessionstart(session):
+    """Build the CPU runtime library (grammar engine) in-tree if this checkout has no .so yet."""
+    native = os.path.join(ROOT, "voice_enabled_browser_automation_amd", "ops", "_vwa_native.so")
+    if not os.path.exists(native):
+        from voice_enabled_browser_automation_amd.ops.build import build_native
+
+        build_native()

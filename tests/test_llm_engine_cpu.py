@@ -1,0 +1,119 @@
+"""LLM engine on CPU (reference ops): paged KV + ragged decode == full prefill, prefix cache,
+grammar-constrained intent generation, and tensor parallelism over gloo (world size 2)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from voice_enabled_browser_automation_amd.brain.intent_engine import LLMIntentEngine
+from voice_enabled_browser_automation_amd.contracts import ParseResponse, safe_parse
+from voice_enabled_browser_automation_amd.models.config import LLAMA_PRESETS, LlamaConfig
+from voice_enabled_browser_automation_amd.models.llama import LlamaModel
+from voice_enabled_browser_automation_amd.parallel.tp import TPContext
+from voice_enabled_browser_automation_amd.runtime.engine import LLMEngine
+from voice_enabled_browser_automation_amd.runtime.kv_cache import BlockManager
+from voice_enabled_browser_automation_amd.tokenizer import load_tokenizer
+
+SMALL = LlamaConfig(name="t", vocab_size=512, hidden=128, n_layers=2, n_heads=4, n_kv_heads=2, head_dim=32,
+                    ffn=256, max_pos=1024)
+
+
+def test_block_manager_prefix_cache():
+    bm = BlockManager(num_blocks=16, block_size=4)
+    toks = list(range(13))
+    blocks = bm.allocate(4)
+    bm.register_prefix(toks, blocks, 13)
+    bm.release(blocks)
+    hit, n = bm.match_prefix(toks + [99])
+    assert n == 12 and hit == blocks[:3]
+    hit2, n2 = bm.match_prefix([7] + toks)
+    assert n2 == 0 and hit2 == []
+    bm.release(hit)
+    # exhaustion evicts unreferenced cached blocks instead of failing
+    got = bm.allocate(15)
+    assert len(set(got)) == 15 and 0 not in got
+
+
+def test_ragged_decode_matches_full_prefill():
+    torch.manual_seed(0)
+    m = LlamaModel(SMALL, device="cpu", seed=3)
+    toks = torch.randint(0, 512, (90,)).tolist()
+    # A: full prefill (flash path, 90 rows)
+    eA = LLMEngine(m, max_seqs=2, max_model_len=256, kv_blocks=64, block_size=16)
+    sA = eA.new_sequence(toks, use_prefix_cache=False)
+    la = eA.prefill(sA)
+    # B: prefill 60 rows (ragged path) then decode the remaining 30 tokens one by one
+    eB = LLMEngine(m, max_seqs=2, max_model_len=256, kv_blocks=64, block_size=16)
+    sB = eB.new_sequence(toks[:60], use_prefix_cache=False)
+    eB.prefill(sB)
+    lb = None
+    for t in toks[60:]:
+        lb = eB.run_rows([(sB, t)])
+    assert torch.allclose(la.float(), lb.float(), atol=3e-2, rtol=3e-2), (la - lb).abs().max()
+    # C: jump-forward style multi-row step of one sequence
+    eC = LLMEngine(m, max_seqs=2, max_model_len=256, kv_blocks=64, block_size=16)
+    sC = eC.new_sequence(toks[:70], use_prefix_cache=False)
+    eC.prefill(sC)
+    lc = eC.run_rows([(sC, t) for t in toks[70:]])[-1:]
+    assert torch.allclose(la.float(), lc.float(), atol=3e-2, rtol=3e-2)
+
+
+def test_intent_engine_constrained_valid_and_prefix_cached():
+    m = LlamaModel(LLAMA_PRESETS["llama-tiny"], device="cpu", seed=1)
+    eng = LLMEngine(m, max_seqs=2, max_model_len=2048, kv_blocks=400)
+    ie = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=200)
+    for text in ["search wireless earbuds", "open the second result"]:
+        out = ie.parse({"text": text, "context": {}})
+        assert safe_parse(ParseResponse, out).success
+        assert ie.last_stats["output_chars"] <= 200
+    assert ie.last_stats["cached_prefix_tokens"] > 900  # static system + few-shot prefix served from cache
+    assert ie.last_stats["forced_tokens"] > 0  # jump-forward engaged
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _tp_worker(rank, world, port, toks, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        tp = TPContext(rank=rank, size=world, group=dist.group.WORLD)
+        m = LlamaModel(SMALL, device="cpu", seed=3, tp=tp)
+        e = LLMEngine(m, max_seqs=2, max_model_len=256, kv_blocks=64, block_size=16)
+        s = e.new_sequence(toks[:40], use_prefix_cache=False)
+        e.prefill(s)
+        logits = e.run_rows([(s, toks[40]), (s, toks[41])])
+        if rank == 0:
+            q.put(logits.float().clone())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tensor_parallel_gloo_matches_single():
+    torch.manual_seed(0)
+    toks = torch.randint(0, 512, (42,)).tolist()
+    m = LlamaModel(SMALL, device="cpu", seed=3)
+    e = LLMEngine(m, max_seqs=2, max_model_len=256, kv_blocks=64, block_size=16)
+    s = e.new_sequence(toks[:40], use_prefix_cache=False)
+    e.prefill(s)
+    ref = e.run_rows([(s, toks[40]), (s, toks[41])]).float()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, toks, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got.shape == ref.shape
+    assert torch.allclose(got, ref, atol=3e-2, rtol=3e-2), (got - ref).abs().max()

@@ -1,0 +1,135 @@
+"""Voice service: /health, first WS frame (port of apps/voice/test/server.test.ts:8-32), and the
+full transcript -> debounce -> brain -> intent/tts/context -> executor flow with fake services."""
+import asyncio
+import json
+
+from aiohttp import web
+from aiohttp.test_utils import TestClient, TestServer
+
+from voice_enabled_browser_automation_amd.asr.streaming import StreamingAsrSession, results_event
+from voice_enabled_browser_automation_amd.voice.server import build_app
+
+
+class FakeAsr:
+    """Emits a final transcript on flush(), a partial on every binary frame."""
+
+    def __init__(self):
+        self.n = 0
+
+    def push(self, data):
+        self.n += 1
+        return [results_event(f"partial {self.n}", is_final=False, start=0, duration=0.06, model="fake")]
+
+    def flush(self):
+        return [results_event("search wireless earbuds", is_final=True, start=0, duration=1.0, model="fake")]
+
+
+async def _recv_types(ws, want, timeout=5.0):
+    got = []
+    while not all(w in [g["type"] for g in got] for w in want):
+        msg = await asyncio.wait_for(ws.receive(), timeout)
+        got.append(json.loads(msg.data))
+    return got
+
+
+def test_health_and_passthrough_first_frame():
+    async def go():
+        async with TestClient(TestServer(build_app(None, debounce_ms=10))) as c:
+            r = await c.get("/health")
+            assert await r.json() == {"status": "ok", "service": "voice", "version": "0.1.0"}
+            ws = await c.ws_connect("/stream")
+            first = json.loads((await ws.receive()).data)
+            assert first["type"] in ("warn", "info", "error")
+            assert first == {"type": "warn", "payload": "no_api_key; running in passthrough"}
+            await ws.send_bytes(b"\x00\x00" * 960)  # audio is accepted and dropped in passthrough
+            await ws.send_str(json.dumps({"type": "close"}))
+            await ws.close()
+
+    asyncio.run(go())
+
+
+def test_full_flow_with_fake_brain_and_executor():
+    brain_calls, exec_calls = [], []
+
+    async def brain(req):
+        body = await req.json()
+        brain_calls.append(body)
+        return web.json_response({"version": "1.0", "intents": [
+            {"type": "search", "args": {"query": "wireless earbuds"}, "priority": 0, "requires_confirmation": False,
+             "retries": 1},
+            {"type": "upload", "args": {"fileRef": "resume://latest"}, "priority": 1, "requires_confirmation": True,
+             "retries": 1}], "context_updates": {"query": "wireless earbuds"}, "confidence": 0.9,
+            "tts_summary": "Searching for wireless earbuds."})
+
+    async def execute(req):
+        body = await req.json()
+        exec_calls.append(body)
+        return web.json_response({"session_id": "sess-1", "results": [], "artifacts": {"dir": "x"}})
+
+    async def go():
+        bapp = web.Application()
+        bapp.router.add_post("/parse", brain)
+        eapp = web.Application()
+        eapp.router.add_post("/execute", execute)
+        async with TestServer(bapp) as bs, TestServer(eapp) as es:
+            vapp = build_app(lambda: FakeAsr(), brain_url=str(bs.make_url("/parse")),
+                             executor_url=str(es.make_url("")).rstrip("/"), debounce_ms=20)
+            async with TestClient(TestServer(vapp)) as c:
+                ws = await c.ws_connect("/stream")
+                assert json.loads((await ws.receive()).data) == {"type": "info", "payload": "asr_connected"}
+                await ws.send_str(json.dumps({"type": "context_update", "payload": {"url": "https://bestbuy.com"}}))
+                await ws.send_bytes(b"\x01\x00" * 960)
+                p = json.loads((await ws.receive()).data)
+                assert p["type"] == "transcript_partial"
+                assert p["payload"]["channel"]["alternatives"][0]["transcript"] == "partial 1"
+                await ws.send_str(json.dumps({"type": "flush"}))
+                got = await _recv_types(ws, ["transcript_final", "intent", "tts", "execution_result",
+                                             "confirmation_required"])
+                types = [g["type"] for g in got]
+                assert types.index("transcript_final") < types.index("intent")
+                fin = next(g for g in got if g["type"] == "transcript_final")
+                assert fin["payload"]["is_final"] is True
+                assert next(g for g in got if g["type"] == "tts")["payload"] == "Searching for wireless earbuds."
+                assert next(g for g in got if g["type"] == "execution_result")["payload"] == \
+                    "Executed 1 actions successfully. Session: sess-1"
+                assert next(g for g in got if g["type"] == "confirmation_required")["payload"] == \
+                    "1 risky actions require manual confirmation"
+                assert brain_calls[0] == {"text": "search wireless earbuds", "context": {"url": "https://bestbuy.com"}}
+                assert [i["type"] for i in exec_calls[0]["intents"]] == ["search"] and "session_id" not in exec_calls[0]
+                # second utterance: merged context + executor session id reused
+                await ws.send_str(json.dumps({"type": "flush"}))
+                await _recv_types(ws, ["intent", "execution_result"])
+                assert brain_calls[1]["context"] == {"url": "https://bestbuy.com", "query": "wireless earbuds"}
+                assert exec_calls[1]["session_id"] == "sess-1"
+                await ws.close()
+                r = await c.get("/metrics")
+                m = await r.json()
+                assert m["counters"]["finals"] == 2
+
+    asyncio.run(go())
+
+
+def test_streaming_session_vad_partials_finals():
+    calls = []
+
+    def fake_transcribe(pcm):
+        calls.append(len(pcm))
+        return f"utterance of {len(pcm)} samples"
+
+    s = StreamingAsrSession(fake_transcribe, partial_every_s=0.5, endpoint_silence_s=0.3, energy_threshold=500)
+    import numpy as np
+
+    sr = 16000
+    t = np.arange(sr) / sr
+    speech = (np.sin(2 * np.pi * 220 * t) * 8000).astype(np.int16)
+    silence = np.zeros(int(0.5 * sr), dtype=np.int16)
+    evs = []
+    for chunk in np.split(np.concatenate([silence, speech, silence]), 25):
+        evs += s.push(chunk.tobytes())
+    partial = [e for e in evs if not e["is_final"]]
+    final = [e for e in evs if e["is_final"]]
+    assert len(partial) >= 1 and len(final) == 1
+    assert final[0]["channel"]["alternatives"][0]["transcript"].startswith("utterance of")
+    assert final[0]["type"] == "Results" and final[0]["speech_final"] is True
+    assert final[0]["start"] >= 0.25  # leading silence trimmed (endpoint-sized chunks), stream clock kept
+    assert s.flush() == []  # nothing pending

@@ -50,9 +50,9 @@ class TPContext:
             pad[:, :vp] = local
             pad[:, vp:] = float("-inf")
             local = pad
-        gathered = torch.empty((self.size, n, per), dtype=local.dtype, device=local.device)
-        dist.all_gather_into_tensor(gathered, local.contiguous(), group=self.group)
-        full = gathered.permute(1, 0, 2).reshape(n, self.size * per)[:, :vocab]
+        parts = [torch.empty((n, per), dtype=local.dtype, device=local.device) for _ in range(self.size)]
+        dist.all_gather(parts, local.contiguous(), group=self.group)
+        full = torch.cat(parts, dim=1)[:, :vocab]
         if out is not None:
             out.copy_(full)
             return out
