@@ -99,7 +99,7 @@ def main():
     llama = LlamaModel(lcfg, device=dev, tp=tp, seed=2)
     engine = LLMEngine(llama, max_seqs=4, max_model_len=2048, use_graphs=use_graphs)
     brain = LLMIntentEngine(engine, load_tokenizer("llama3"), budget_chars=args.budget_chars, temperature=0.1,
-                            seed=1234 + rank)
+                            seed=1234 + tp.dp_rank)  # identical within a TP group (lockstep decode)
     engine.capture_all()
     torch.cuda.synchronize()
     load_s = time.time() - t_load

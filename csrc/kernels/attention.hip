@@ -49,14 +49,7 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
   const bool single = (p.n_splits == 1);
   const int nq = p.n_q_heads;
 
-  if (t0 >= ctx) {
-    if (!single && lane < G) {
-      float* pm = p.part_ml + (((int64_t)row * p.n_splits + split) * nq + kvh * G + lane) * 2;
-      pm[0] = -INFINITY;
-      pm[1] = 0.f;
-    }
-    return;
-  }
+  if (t0 >= ctx) return;  // split past this row's context (grid is sized for max_ctx)
   const int tend = min(ctx, t0 + kSplit);
 
   for (int i = lane; i < G * D; i += 64) {
@@ -138,27 +131,75 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[g][j] += __shfl_xor(o[g][j], off, 64);
 
-  if (tg == 0) {
+  const int ns = (ctx + kSplit - 1) / kSplit;  // active splits of this row
+  if (single || ns == 1) {
+    if (tg == 0) {
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int h = kvh * G + g;
-      if (single) {
+      for (int g = 0; g < G; ++g) {
+        const int h = kvh * G + g;
         const float inv = 1.f / lrow[g];
         float ov[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) ov[j] = o[g][j] * inv;
         *reinterpret_cast<uint4*>(p.out + (int64_t)row * p.ldo + h * D + c * 8) = pack8(ov);
-      } else {
-        float* po = p.part_o + (((int64_t)row * p.n_splits + split) * nq + h) * D + c * 8;
-        *reinterpret_cast<float4*>(po) = make_float4(o[g][0], o[g][1], o[g][2], o[g][3]);
-        *reinterpret_cast<float4*>(po + 4) = make_float4(o[g][4], o[g][5], o[g][6], o[g][7]);
-        if (c == 0) {
-          float* pm = p.part_ml + (((int64_t)row * p.n_splits + split) * nq + h) * 2;
-          pm[0] = mrow[g];
-          pm[1] = lrow[g];
-        }
       }
     }
+    return;
+  }
+  if (tg == 0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int h = kvh * G + g;
+      float* po = p.part_o + (((int64_t)row * p.n_splits + split) * nq + h) * D + c * 8;
+      *reinterpret_cast<float4*>(po) = make_float4(o[g][0], o[g][1], o[g][2], o[g][3]);
+      *reinterpret_cast<float4*>(po + 4) = make_float4(o[g][4], o[g][5], o[g][6], o[g][7]);
+      if (c == 0) {
+        float* pm = p.part_ml + (((int64_t)row * p.n_splits + split) * nq + h) * 2;
+        pm[0] = mrow[g];
+        pm[1] = lrow[g];
+      }
+    }
+  }
+  // ---- in-launch combine by the last-arriving split (guide G16: plain stores -> vmcnt(0) ->
+  // agent release -> vmcnt(0) -> relaxed agent ticket; the winner: agent acquire -> vmcnt(0) ->
+  // plain loads).  Counters are zeroed by a memset node ahead of the launch every call.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int ticket = 0;
+  if (lane == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ticket = __hip_atomic_fetch_add(p.counters + row * nkv + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  ticket = __shfl(ticket, 0, 64);
+  if (ticket != ns - 1) return;
+  if (lane == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  constexpr int DPL = D / 64;
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int h = kvh * G + g;
+    const float* pmb = p.part_ml + ((int64_t)row * p.n_splits * nq + h) * 2;
+    const int64_t ms = (int64_t)nq * 2;
+    float M = -INFINITY;
+    for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, pmb[sp * ms]);
+    float L = 0.f, acc[DPL];
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
+    const float* pob = p.part_o + ((int64_t)row * p.n_splits * nq + h) * D + lane * DPL;
+    const int64_t os = (int64_t)nq * D;
+#pragma unroll 4
+    for (int sp = 0; sp < ns; ++sp) {
+      const float f = __expf(pmb[sp * ms] - M);
+      L += pmb[sp * ms + 1] * f;
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) acc[j] += pob[sp * os + j] * f;
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) p.out[(int64_t)row * p.ldo + h * D + lane * DPL + j] = f2bf(acc[j] * inv);
   }
 }
 
@@ -205,9 +246,8 @@ __global__ __launch_bounds__(64) void attn_combine_kernel(DecodeAttnParams p) {
 
 template <int D, int G>
 void launch_decode(const DecodeAttnParams& p, hipStream_t st) {
+  if (p.n_splits > 1) (void)hipMemsetAsync(p.counters, 0, sizeof(int) * p.rows * p.n_kv_heads, st);
   hipLaunchKernelGGL((decode_attn_kernel<D, G>), dim3(p.rows * p.n_kv_heads, p.n_splits), dim3(64), 0, st, p);
-  if (p.n_splits > 1)
-    hipLaunchKernelGGL((attn_combine_kernel<D>), dim3(p.rows * p.n_q_heads), dim3(64), 0, st, p);
 }
 
 template <int D>

@@ -97,7 +97,8 @@ def main():
         po = torch.empty(rows * n_splits * nq * hd, device=dev)
         pm = torch.empty(rows * n_splits * nq * 2, device=dev)
         t = timeit(lambda: ops.decode_attention(q, kv, cl, sid, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
-                                                scale=hd ** -0.5, max_ctx=2048, out=out, part_o=po, part_ml=pm))
+                                                scale=hd ** -0.5, max_ctx=2048, out=out, part_o=po, part_ml=pm,
+                                                counters=torch.zeros(rows * nkv, dtype=torch.int32, device=dev)))
         gb = rows * ctx * nkv * hd * 2 * 2 / 1e9
         r = dict(kernel="decode_attention", rows=rows, ctx=ctx, us=round(t, 2), tbps=round(gb / (t * 1e-6) / 1e3, 3))
         print(json.dumps(r), flush=True)

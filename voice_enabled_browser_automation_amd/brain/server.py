@@ -114,8 +114,46 @@ def build_llm_engine(model_name: Optional[str] = None, device: Optional[str] = N
     model = LlamaModel(get_config(name), device=dev, tp=tp, seed=int(os.environ.get("VWA_SEED", "0")))
     eng = LLMEngine(model, max_seqs=int(os.environ.get("VWA_MAX_SESSIONS", "8")), max_model_len=4096)
     eng.capture_all()
-    return LLMIntentEngine(eng, load_tokenizer("llama3"),
-                           budget_chars=int(os.environ.get("VWA_BUDGET_CHARS", "512")))
+    ie = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=int(os.environ.get("VWA_BUDGET_CHARS", "512")))
+    return TPIntentEngine(ie, tp) if tp.size > 1 else ie
+
+
+class TPIntentEngine:
+    """Control plane for a tensor-parallel brain: rank 0 serves HTTP and broadcasts every request
+    (chat messages) to the TP workers over a CPU (gloo) group; all ranks then run the identical,
+    deterministic decode loop in lockstep (identical all-gathered logits + seeds -> identical
+    tokens), so the RCCL collectives inside each step always match up."""
+
+    def __init__(self, inner, tp):
+        import torch.distributed as dist
+
+        self.inner = inner
+        self.tp = tp
+        self.ctl = dist.new_group(backend="gloo")
+        self.last_stats = {}
+
+    def _bcast(self, obj):
+        import torch.distributed as dist
+
+        box = [obj]
+        dist.broadcast_object_list(box, src=0, group=self.ctl)
+        return box[0]
+
+    def __call__(self, messages):
+        self._bcast(messages)
+        out = self.inner(messages)
+        self.last_stats = self.inner.last_stats
+        return out
+
+    def worker_loop(self):
+        while True:
+            messages = self._bcast(None)
+            if messages is None:
+                return
+            try:
+                self.inner(messages)
+            except Exception as e:  # noqa: BLE001  (rank 0 reports the error to the client)
+                print(f"[brain worker {self.tp.rank}] {e}", flush=True)
 
 
 def main():
@@ -123,8 +161,12 @@ def main():
 
     load_dotenv()
     port = int(os.environ.get("BRAIN_PORT", "8090"))
+    engine = make_engine_from_env()
+    if isinstance(engine, TPIntentEngine) and engine.tp.rank != 0:
+        engine.worker_loop()  # TP worker: no HTTP, follows rank 0's requests
+        return
     print(f"[brain] listening on http://127.0.0.1:{port}", flush=True)
-    web.run_app(build_app(), host="127.0.0.1", port=port, print=None)
+    web.run_app(build_app(engine), host="127.0.0.1", port=port, print=None)
 
 
 if __name__ == "__main__":

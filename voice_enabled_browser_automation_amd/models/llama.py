@@ -168,7 +168,8 @@ class LlamaModel:
                 attn = bufs.attn[:M]
                 ops.decode_attention(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens, bufs.seq_ids,
                                      n_q_heads=self.nq, n_kv_heads=self.nkv, head_dim=self.hd, scale=self.scale,
-                                     max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o, part_ml=bufs.part_ml)
+                                     max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o, part_ml=bufs.part_ml,
+                                     counters=bufs.attn_cnt)
             else:
                 table = bufs.block_table[prefill_seq : prefill_seq + 1]
                 q4 = q.view(1, M, self.nq, self.hd)
@@ -188,3 +189,27 @@ class LlamaModel:
         if self.tp.size == 1:
             return local
         return self.tp.all_gather_vocab(local, cfg.vocab_size, out=bufs.logits[:n] if n <= bufs.logits.shape[0] else None)
+
+
+def move_model(model, device) -> None:
+    """Move every tensor attribute (incl. dataclass layer records) of a model to `device` in place."""
+    import dataclasses
+
+    device = torch.device(device)
+
+    def mv(obj):
+        if isinstance(obj, torch.Tensor):
+            return obj.to(device)
+        if dataclasses.is_dataclass(obj) and not isinstance(obj, type):
+            for f in dataclasses.fields(obj):
+                setattr(obj, f.name, mv(getattr(obj, f.name)))
+            return obj
+        if isinstance(obj, list):
+            return [mv(x) for x in obj]
+        return obj
+
+    for k, v in list(vars(model).items()):
+        if k == "cfg":
+            continue
+        setattr(model, k, mv(v))
+    model.device = device

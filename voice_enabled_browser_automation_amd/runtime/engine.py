@@ -54,11 +54,17 @@ class StepBuffers:
         dt = model.dtype
         self.max_rows = max_rows
         self.max_ctx = max_ctx
-        self.tokens = torch.zeros(max_rows, **i32)
-        self.positions = torch.zeros(max_rows, **i32)
-        self.seq_ids = torch.zeros(max_rows, **i32)
-        self.ctx_lens = torch.ones(max_rows, **i32)
-        self.slots = torch.full((max_rows,), -1, dtype=torch.int64, device=device)
+        # all per-row metadata lives in ONE device buffer (and one pinned host mirror) so a step
+        # needs a single H2D copy: [tokens | positions | seq_ids | ctx_lens | slots (int64)]
+        R = max_rows
+        self.meta = torch.zeros(6 * R, **i32)
+        self.tokens = self.meta[0:R]
+        self.positions = self.meta[R : 2 * R]
+        self.seq_ids = self.meta[2 * R : 3 * R]
+        self.ctx_lens = self.meta[3 * R : 4 * R]
+        self.slots = self.meta[4 * R : 6 * R].view(torch.int64)
+        self.ctx_lens.fill_(1)
+        self.slots.fill_(-1)
         self.block_table = torch.zeros(max_seqs, max_blocks_per_seq, **i32)
         d = model.cfg.hidden
         self.hidden = torch.zeros(max_rows, d, dtype=dt, device=device)
@@ -71,19 +77,17 @@ class StepBuffers:
         ns = ops.decode_n_splits(max_ctx)
         self.part_o = torch.zeros(max_rows * ns * model.nq * model.hd, dtype=torch.float32, device=device)
         self.part_ml = torch.zeros(max_rows * ns * model.nq * 2, dtype=torch.float32, device=device)
+        self.attn_cnt = torch.zeros(max_rows * model.nkv, dtype=torch.int32, device=device)
         pin = torch.device(device).type == "cuda"
-        self.h_i32 = torch.zeros(4, max_rows, dtype=torch.int32, pin_memory=pin)
-        self.h_slots = torch.full((max_rows,), -1, dtype=torch.int64, pin_memory=pin)
+        self.h_meta = torch.zeros(6 * R, dtype=torch.int32, pin_memory=pin)
+        self.h_i32 = self.h_meta[: 4 * R].view(4, R)
+        self.h_slots = self.h_meta[4 * R :].view(torch.int64)
         self.h_table = torch.zeros(max_seqs, max_blocks_per_seq, dtype=torch.int32, pin_memory=pin)
         self.table_dirty = True
 
     def upload(self, n_rows: int) -> None:
         nb = True
-        self.tokens.copy_(self.h_i32[0], non_blocking=nb)
-        self.positions.copy_(self.h_i32[1], non_blocking=nb)
-        self.seq_ids.copy_(self.h_i32[2], non_blocking=nb)
-        self.ctx_lens.copy_(self.h_i32[3], non_blocking=nb)
-        self.slots.copy_(self.h_slots, non_blocking=nb)
+        self.meta.copy_(self.h_meta, non_blocking=nb)
         if self.table_dirty:
             self.block_table.copy_(self.h_table, non_blocking=nb)
             self.table_dirty = False
