@@ -65,6 +65,51 @@ def synth_speech(seconds: float, seed: int, rate: int = 16000) -> np.ndarray:
     return (sig * 32767).astype(np.int16)
 
 
+def run_concurrent(args, C, asr, brain, utterances, asr_tokens, world):
+    """C voice sessions arriving together on every rank: one batched ASR pass, then all C intent
+    parses decoded with continuous batching.  Per-session latency = ASR batch + that session's
+    parse completion.  Not part of the headline value."""
+    def round_(k):
+        pcms = [utterances[(k * C + j) % len(utterances)] for j in range(C)]
+        t0 = time.perf_counter()
+        texts = asr.transcribe_many([asr.pcm_to_audio(p) for p in pcms], exact_tokens=asr_tokens)
+        t_asr = (time.perf_counter() - t0) * 1e3
+        reqs = [{"text": t if t.strip() else COMMANDS[j % len(COMMANDS)], "context": {"url": "https://www.bestbuy.com"}}
+                for j, t in enumerate(texts)]
+        outs = brain.parse_many(reqs)
+        ok = sum(safe_parse(ParseResponse, o).success for o in outs)
+        return [t_asr + b["latency_ms"] for b in brain.last_batch], ok
+
+    round_(0)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    lat, ok = [], 0
+    it0 = dict(brain.batch_stats)
+    for k in range(args.steps):
+        l, o = round_(k + 1)
+        lat += l
+        ok += o
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) * 1e3
+    bs = {k: brain.batch_stats[k] - it0.get(k, 0) for k in ("iterations", "rows", "sampled")}
+    t = torch.tensor([el, float(ok)] + lat, dtype=torch.float64, device=torch.device("cuda", torch.cuda.current_device()))
+    if world > 1:
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        torch.distributed.all_gather(allt, t)
+    else:
+        allt = [t]
+    all_lat = [float(x) for a in allt for x in a[2:]]
+    el_max = max(float(a[0]) for a in allt)
+    return {"sessions_per_rank": C, "p50_ms": round(statistics.median(all_lat), 3),
+            "p90_ms": round(float(np.percentile(all_lat, 90)), 3),
+            "throughput_utt_per_s": round(len(all_lat) / (el_max / 1e3), 3),
+            "valid_intents": f"{sum(int(a[1]) for a in allt)}/{len(all_lat)}",
+            "rows_per_iteration": round(bs["rows"] / max(1, bs["iterations"]), 2),
+            "samples_per_iteration": round(bs["sampled"] / max(1, bs["iterations"]), 2)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -77,6 +122,9 @@ def main():
     ap.add_argument("--asr-tokens-per-s", type=float, default=4.0)
     ap.add_argument("--budget-chars", type=int, default=512)
     ap.add_argument("--debounce-ms", type=float, default=1000.0, help="reference debounce added for parity_p50_ms")
+    ap.add_argument("--concurrent", type=int, default=int(os.environ.get("VWA_BENCH_CONCURRENT", "0")),
+                    help="also measure C concurrent voice sessions per rank (batched ASR + continuous-batched "
+                         "intent decoding); reported under 'concurrent', outside the headline value")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
@@ -87,6 +135,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (MI355X)")
+    if os.environ.get("VWA_DIST_BACKEND", "nccl") != "nccl":
+        local = local % torch.cuda.device_count()  # gloo rehearsal on fewer GPUs than ranks
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     ops.ext()  # native kernels are mandatory
@@ -95,9 +145,10 @@ def main():
     t_load = time.time()
     wcfg, lcfg = get_config(args.asr), get_config(args.llm)
     whisper = WhisperModel(wcfg, device=dev, seed=1)
-    asr = AsrEngine(whisper, load_tokenizer("whisper"), max_sessions=2, use_graphs=use_graphs)
+    C = max(0, args.concurrent)
+    asr = AsrEngine(whisper, load_tokenizer("whisper"), max_sessions=max(2, C), use_graphs=use_graphs)
     llama = LlamaModel(lcfg, device=dev, tp=tp, seed=2)
-    engine = LLMEngine(llama, max_seqs=4, max_model_len=2048, use_graphs=use_graphs)
+    engine = LLMEngine(llama, max_seqs=max(4, C), max_model_len=2048, use_graphs=use_graphs)
     brain = LLMIntentEngine(engine, load_tokenizer("llama3"), budget_chars=args.budget_chars, temperature=0.1,
                             seed=1234 + tp.dp_rank)  # identical within a TP group (lockstep decode)
     engine.capture_all()
@@ -105,7 +156,8 @@ def main():
     load_s = time.time() - t_load
 
     asr_tokens = int(math.ceil(args.audio_s * args.asr_tokens_per_s))
-    utterances = [synth_speech(args.audio_s, seed=100 * rank + i) for i in range(8)]
+    # identical audio within a TP group (its ranks decode in lockstep); distinct across DP replicas
+    utterances = [synth_speech(args.audio_s, seed=100 * tp.dp_rank + i) for i in range(8)]
 
     def one(i: int):
         pcm = utterances[i % len(utterances)]
@@ -127,6 +179,7 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     lat, asr_ms, oks, llm_stats = [], [], [], []
+    tm0, it0 = dict(brain.timing), brain.batch_stats["iterations"]
     t_start = time.perf_counter()
     for i in range(args.steps):
         l, a, ok = one(args.warmup + i)
@@ -142,6 +195,10 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = (time.perf_counter() - t_start) * 1e3
+    n_it = max(1, brain.batch_stats["iterations"] - it0)
+    host_us = {k.replace("_ms", "_us"): round((brain.timing[k] - tm0[k]) * 1e3 / n_it, 1) for k in tm0}
+
+    conc = run_concurrent(args, C, asr, brain, utterances, asr_tokens, world) if C > 1 else None
 
     # gather every session's latency across ranks (weak scaling: p50 over all sessions)
     local_t = torch.tensor([elapsed] + lat + asr_ms + [float(sum(oks))], dtype=torch.float64, device=dev)
@@ -185,9 +242,12 @@ def main():
             "llm_forced_tokens_mean": round(sum(s.get("forced_tokens", 0) for s in llm_stats) / max(1, K), 2),
             "llm_prefill_tokens_mean": round(sum(s.get("prefill_tokens", 0) for s in llm_stats) / max(1, K), 2),
             "valid_intents": f"{n_ok}/{len(all_lat)}",
+            "decode_iteration_host_us": host_us,
             "throughput_utt_per_s": round(len(all_lat) / (elapsed_max / 1e3), 3),
             "load_s": round(load_s, 1),
         }
+        if conc is not None:
+            res["concurrent"] = conc
         print(json.dumps(res), flush=True)
     if world > 1:
         torch.distributed.barrier()

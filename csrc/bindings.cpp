@@ -252,7 +252,7 @@ KVView make_view(const Tensor& k, const Tensor& v, const Tensor& table, int64_t 
 
 void decode_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_size, int64_t sb, int64_t sh,
                       int64_t stok, Tensor ctx_lens, Tensor seq_ids, int64_t n_q_heads, int64_t n_kv_heads,
-                      int64_t head_dim, double scale, int64_t n_splits, Tensor part_o, Tensor part_ml, Tensor counters,
+                      int64_t head_dim, double scale, int64_t n_splits, Tensor part_o, Tensor part_ml,
                       Tensor out) {
   c10::DeviceGuard g(q.device());
   check_bf16(q, "q");
@@ -268,8 +268,7 @@ void decode_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_
                 "part_o too small");
     TORCH_CHECK(part_ml.scalar_type() == at::kFloat && part_ml.numel() >= (int64_t)rows * n_splits * n_q_heads * 2,
                 "part_ml too small");
-    TORCH_CHECK(counters.scalar_type() == at::kInt && counters.numel() >= (int64_t)rows * n_kv_heads,
-                "counters too small");
+    TORCH_CHECK(n_splits <= 256, "decode attention merges <= 256 splits (context <= 16384 tokens)");
   }
   DecodeAttnParams p{};
   p.q = bfp(q);
@@ -286,7 +285,6 @@ void decode_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_
   p.n_splits = (int)n_splits;
   p.part_o = part_o.data_ptr<float>();
   p.part_ml = part_ml.data_ptr<float>();
-  p.counters = counters.data_ptr<int>();
   p.out = bfp_mut(out);
   p.ldo = (int)out.stride(0);
   check_rc(vwa_decode_attention(&p, cur_stream(q)), "decode_attention");

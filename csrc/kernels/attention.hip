@@ -4,7 +4,11 @@
 //    GQA group of G q-heads per kv-head handled by one workgroup so each K/V byte is read
 //    once per group.  Split-K over the context (64 keys per single-wave workgroup; lane = key
 //    for Q.K, lane = (16-byte dim chunk, token group) for P.V), partials merged by
-//    attn_combine (log-sum-exp).  The grid is sized for the maximum context so the launch
+//    attn_combine (log-sum-exp, one wave per (row, q head)).  Measured alternatives that lost
+//    to this second tiny launch (profiles/r1_kernel_microbench_v3.json, 1 row, ctx 1200):
+//    in-launch last-arriver merge with agent-scope release/acquire fences (28 us: the fences
+//    write back / invalidate the per-XCD L2 on every workgroup) and with relaxed agent-scope
+//    atomic partials (24 us) vs 14.4 us here.  The grid is sized for the maximum context so the launch
 //    shape is static under hipGraph capture; splits past a row's context exit early.
 //    Also serves Whisper cross-attention (contiguous encoder K/V expressed as one block).
 //
@@ -160,47 +164,6 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
       }
     }
   }
-  // ---- in-launch combine by the last-arriving split (guide G16: plain stores -> vmcnt(0) ->
-  // agent release -> vmcnt(0) -> relaxed agent ticket; the winner: agent acquire -> vmcnt(0) ->
-  // plain loads).  Counters are zeroed by a memset node ahead of the launch every call.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  int ticket = 0;
-  if (lane == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ticket = __hip_atomic_fetch_add(p.counters + row * nkv + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  ticket = __shfl(ticket, 0, 64);
-  if (ticket != ns - 1) return;
-  if (lane == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  constexpr int DPL = D / 64;
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const int h = kvh * G + g;
-    const float* pmb = p.part_ml + ((int64_t)row * p.n_splits * nq + h) * 2;
-    const int64_t ms = (int64_t)nq * 2;
-    float M = -INFINITY;
-    for (int sp = 0; sp < ns; ++sp) M = fmaxf(M, pmb[sp * ms]);
-    float L = 0.f, acc[DPL];
-#pragma unroll
-    for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
-    const float* pob = p.part_o + ((int64_t)row * p.n_splits * nq + h) * D + lane * DPL;
-    const int64_t os = (int64_t)nq * D;
-#pragma unroll 4
-    for (int sp = 0; sp < ns; ++sp) {
-      const float f = __expf(pmb[sp * ms] - M);
-      L += pmb[sp * ms + 1] * f;
-#pragma unroll
-      for (int j = 0; j < DPL; ++j) acc[j] += pob[sp * os + j] * f;
-    }
-    const float inv = L > 0.f ? 1.f / L : 0.f;
-#pragma unroll
-    for (int j = 0; j < DPL; ++j) p.out[(int64_t)row * p.ldo + h * D + lane * DPL + j] = f2bf(acc[j] * inv);
-  }
 }
 
 // One wave per (row, q-head): split statistics are loaded in parallel (lane = split), the
@@ -213,6 +176,7 @@ __global__ __launch_bounds__(64) void attn_combine_kernel(DecodeAttnParams p) {
   const int lane = threadIdx.x;
   const int ctx = p.ctx_lens[row];
   const int ns = min(min(p.n_splits, (ctx + kSplit - 1) / kSplit), 256);
+  if (ns <= 1) return;  // single-split rows were written directly by decode_attn_kernel
   const float* pm = p.part_ml + ((int64_t)row * p.n_splits * p.n_q_heads + h) * 2;
   const int64_t sstride = (int64_t)p.n_q_heads * 2;
   float mloc = -INFINITY;
@@ -246,8 +210,9 @@ __global__ __launch_bounds__(64) void attn_combine_kernel(DecodeAttnParams p) {
 
 template <int D, int G>
 void launch_decode(const DecodeAttnParams& p, hipStream_t st) {
-  if (p.n_splits > 1) (void)hipMemsetAsync(p.counters, 0, sizeof(int) * p.rows * p.n_kv_heads, st);
   hipLaunchKernelGGL((decode_attn_kernel<D, G>), dim3(p.rows * p.n_kv_heads, p.n_splits), dim3(64), 0, st, p);
+  if (p.n_splits > 1)
+    hipLaunchKernelGGL((attn_combine_kernel<D>), dim3(p.rows * p.n_q_heads), dim3(64), 0, st, p);
 }
 
 template <int D>

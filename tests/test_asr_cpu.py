@@ -34,6 +34,17 @@ def test_transcribe_fixed_work_and_decode_consistency():
     assert enc.shape == (1, 1500, w.cfg.d_model) and torch.isfinite(enc.float()).all()
 
 
+def test_transcribe_many_batched_matches_single():
+    w = WhisperModel(get_config("whisper-test"), device="cpu", seed=0)
+    asr = AsrEngine(w, load_tokenizer("whisper"), max_sessions=3)
+    pcms = [(np.sin(np.arange(16000 * 2) * 2 * np.pi * f / 16000) * 6000).astype(np.int16) for f in (200, 330, 510)]
+    audios = [asr.pcm_to_audio(p) for p in pcms]
+    single = [asr.transcribe(a, max_tokens=8) for a in audios]
+    batched = asr.transcribe_many(audios, max_tokens=8)
+    assert batched == single
+    assert asr.last_stats["batch"] == 3 and sorted(asr.free_slots) == [0, 1, 2]
+
+
 def test_streaming_with_real_engine_emits_deepgram_events():
     w = WhisperModel(get_config("whisper-test"), device="cpu", seed=0)
     asr = AsrEngine(w, load_tokenizer("whisper"), max_sessions=1)

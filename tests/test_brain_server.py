@@ -92,3 +92,28 @@ def test_keyword_engine_and_metrics():
                                              "priority": 0, "requires_confirmation": False, "retries": 1}
     st, m = call(eng, "GET", "/metrics")
     assert st == 200 and m["service"] == "brain"
+
+
+def test_concurrent_parse_requests_batch_on_llm_engine():
+    """Real (tiny, CPU) LLM engine behind /parse: concurrent HTTP requests are decoded together by
+    the continuous-batching scheduler and all come back schema-valid."""
+    from voice_enabled_browser_automation_amd.brain.intent_engine import LLMIntentEngine
+    from voice_enabled_browser_automation_amd.models.config import LLAMA_PRESETS
+    from voice_enabled_browser_automation_amd.models.llama import LlamaModel
+    from voice_enabled_browser_automation_amd.runtime.engine import LLMEngine
+    from voice_enabled_browser_automation_amd.tokenizer import load_tokenizer
+
+    m = LlamaModel(LLAMA_PRESETS["llama-tiny"], device="cpu", seed=1)
+    ie = LLMIntentEngine(LLMEngine(m, max_seqs=4, max_model_len=2048, kv_blocks=800), load_tokenizer("llama3"),
+                         budget_chars=200)
+
+    async def go():
+        async with TestClient(TestServer(build_app(ie))) as c:
+            rs = await asyncio.gather(*[c.post("/parse", json={"text": t}) for t in
+                                        ("scroll down", "go back", "search for laptops")])
+            return [(r.status, await r.json()) for r in rs]
+
+    res = asyncio.run(go())
+    assert all(st == 200 and j["version"] == "1.0" and j["intents"] for st, j in res)
+    assert ie.batch_stats["max_active"] >= 2
+    assert ie._thread is None  # scheduler stopped on app cleanup

@@ -41,13 +41,15 @@ def timeit(fn, iters=40, reps=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default="gemm,attn,flash", help="comma list of gemm,attn,flash")
     args = ap.parse_args()
+    only = set(args.only.split(","))
     dev = "cuda"
     torch.manual_seed(0)
     res = []
     shapes = [("qkv", 6144, 4096), ("o_proj", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336),
               ("lm_head", 128256, 4096)]
-    for M in (1, 4, 16, 32):
+    for M in ((1, 4, 16, 32) if "gemm" in only else ()):
         for name, N, K in shapes:
             x = torch.randn(M, K, device=dev).to(torch.bfloat16)
             # rotate over enough weight copies (>= 1 GiB) that the 256 MiB Infinity Cache cannot
@@ -82,7 +84,7 @@ def main():
             res.append(r)
     # decode attention, Llama-3-8B geometry, ctx 1200
     nq, nkv, hd, bs = 32, 8, 128, 16
-    for rows, ctx in ((1, 1200), (8, 1200), (32, 1200)):
+    for rows, ctx in (((1, 1200), (8, 1200), (32, 1200)) if "attn" in only else ()):
         blocks = rows * ((ctx + bs - 1) // bs) + 8
         kc = torch.randn(blocks, nkv, bs, hd, device=dev).to(torch.bfloat16)
         vc = torch.randn_like(kc)
@@ -97,8 +99,7 @@ def main():
         po = torch.empty(rows * n_splits * nq * hd, device=dev)
         pm = torch.empty(rows * n_splits * nq * 2, device=dev)
         t = timeit(lambda: ops.decode_attention(q, kv, cl, sid, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
-                                                scale=hd ** -0.5, max_ctx=2048, out=out, part_o=po, part_ml=pm,
-                                                counters=torch.zeros(rows * nkv, dtype=torch.int32, device=dev)))
+                                                scale=hd ** -0.5, max_ctx=2048, out=out, part_o=po, part_ml=pm))
         gb = rows * ctx * nkv * hd * 2 * 2 / 1e9
         r = dict(kernel="decode_attention", rows=rows, ctx=ctx, us=round(t, 2), tbps=round(gb / (t * 1e-6) / 1e3, 3))
         print(json.dumps(r), flush=True)
@@ -106,7 +107,7 @@ def main():
     # flash attention: whisper-tiny encoder and llama prefill
     for name, B, S, H, Hkv, D, causal in (("whisper_tiny_enc", 1, 1500, 6, 6, 64, False),
                                           ("whisper_large_enc", 1, 1500, 20, 20, 64, False),
-                                          ("llama_prefill_1k", 1, 1024, 32, 8, 128, True)):
+                                          ("llama_prefill_1k", 1, 1024, 32, 8, 128, True)) if "flash" in only else ():
         q = torch.randn(B, S, H, D, device=dev).to(torch.bfloat16)
         k = torch.randn(B, S, Hkv, D, device=dev).to(torch.bfloat16)
         v = torch.randn_like(k)

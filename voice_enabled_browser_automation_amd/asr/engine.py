@@ -18,7 +18,7 @@ import torch
 from .. import ops
 from ..models.whisper import WhisperModel
 
-BUCKETS = (1, 2, 4, 8, 16)
+BUCKETS = (1, 2, 4, 8, 16, 32, 64)
 
 
 class WhisperRunner:
@@ -57,7 +57,6 @@ class WhisperRunner:
         ns = max(ops.decode_n_splits(b.max_ctx), ops.decode_n_splits(cfg.n_audio_ctx))
         b.part_o = torch.zeros(R * ns * H * hd, dtype=torch.float32, device=dev)
         b.part_ml = torch.zeros(R * ns * H * 2, dtype=torch.float32, device=dev)
-        b.attn_cnt = torch.zeros(R * H, dtype=torch.int32, device=dev)
         b.cross = [(torch.zeros(max_sessions, cfg.n_audio_ctx, H, hd, dtype=model.dtype, device=dev),
                     torch.zeros(max_sessions, cfg.n_audio_ctx, H, hd, dtype=model.dtype, device=dev)) for _ in range(L)]
         b.cross_table = torch.arange(max_sessions, dtype=torch.int32, device=dev)[:, None].contiguous()
@@ -164,6 +163,13 @@ class AsrEngine:
                    part_idx=self.part_idx)
         return int(self.d_tok.item())
 
+    def set_cross_batch(self, slots: List[int], enc_states: torch.Tensor) -> None:
+        kvs = self.model.cross_kv(enc_states)
+        for li, (k, v) in enumerate(kvs):
+            for i, slot in enumerate(slots):
+                self.runner.b.cross[li][0][slot].copy_(k[i])
+                self.runner.b.cross[li][1][slot].copy_(v[i])
+
     def transcribe(self, audio: torch.Tensor, *, max_tokens: int = 96, min_tokens: int = 0,
                    exact_tokens: Optional[int] = None) -> str:
         """audio: f32 16 kHz on the model device (<= 30 s).
@@ -171,32 +177,67 @@ class AsrEngine:
         exact_tokens: decode exactly this many text tokens (EOT suppressed) -- fixed-work mode
         used by the benchmark so random-init weights do the same work as a real transcript.
         """
+        return self.transcribe_many([audio], max_tokens=max_tokens, min_tokens=min_tokens,
+                                    exact_tokens=exact_tokens)[0]
+
+    def transcribe_many(self, audios: List[torch.Tensor], *, max_tokens: int = 96, min_tokens: int = 0,
+                        exact_tokens: Optional[int] = None) -> List[str]:
+        """Batch of utterances (concurrent voice sessions on this GPU): one batched encoder pass
+        ([B, 3000, mels] through conv/flash-attention/GEMMs), then every decode step is one
+        ragged row-per-session graph replay with one masked-argmax launch for all sessions."""
         t0 = time.perf_counter()
         m = self.model
-        slot = self.free_slots.pop()
+        B = len(audios)
+        if B > len(self.free_slots):
+            raise RuntimeError(f"{B} utterances exceed the {len(self.free_slots)} free ASR session slots")
+        slots = [self.free_slots.pop() for _ in range(B)]
         try:
-            mel = m.log_mel(audio)
-            enc = m.encode(mel[None])
-            self.runner.set_cross(slot, enc)
+            mel = torch.stack([m.log_mel(a) for a in audios])
+            enc = m.encode(mel)
+            self.set_cross_batch(slots, enc)
             t_enc = time.perf_counter()
-            rows = [(slot, t, p) for p, t in enumerate(self.prompt)]
-            logits = self.runner.step(rows)[-1:]
-            out: List[int] = []
+            P = len(self.prompt)
+            per = max(1, max(BUCKETS) // P)  # sessions per prompt step
+            # (clone: every step's logits live in the replayed graph's static output buffer)
+            logits = torch.cat([self.runner.step([(slot, t, p) for slot in slots[i : i + per]
+                                                  for p, t in enumerate(self.prompt)])[P - 1 :: P].clone()
+                                for i in range(0, B, per)])
+            outs: List[List[int]] = [[] for _ in range(B)]
+            live = list(range(B))
             n_max = exact_tokens if exact_tokens is not None else max_tokens
-            pos = len(self.prompt)
+            pos = P
             for i in range(n_max):
                 allow_eot = exact_tokens is None and i >= min_tokens
-                tok = self._sample(logits, allow_eot)
-                if tok == m.cfg.eot or tok < 0:
+                toks = self._sample_rows(logits, allow_eot)
+                nxt = []
+                for j, tok in zip(live, toks):
+                    if tok == m.cfg.eot or tok < 0:
+                        continue
+                    outs[j].append(tok)
+                    nxt.append(j)
+                live = nxt
+                if not live or i + 1 >= n_max:
                     break
-                out.append(tok)
-                if i + 1 < n_max:
-                    logits = self.runner.step([(slot, tok, pos)])
-                    pos += 1
-            text = self.tok.decode(out)
+                logits = self.runner.step([(slots[j], outs[j][-1], pos) for j in live])
+                pos += 1
+            texts = [self.tok.decode(o) for o in outs]
             t_end = time.perf_counter()
             self.last_stats = dict(encode_ms=(t_enc - t0) * 1e3, decode_ms=(t_end - t_enc) * 1e3,
-                                   total_ms=(t_end - t0) * 1e3, tokens=len(out))
-            return text
+                                   total_ms=(t_end - t0) * 1e3, tokens=sum(len(o) for o in outs), batch=B)
+            return texts
         finally:
-            self.free_slots.append(slot)
+            self.free_slots.extend(slots)
+
+    def _sample_rows(self, logits: torch.Tensor, allow_eot: bool) -> List[int]:
+        n = logits.shape[0]
+        if n == 1:
+            return [self._sample(logits, allow_eot)]
+        logits = logits.contiguous()
+        mask = (self.mask_text_eot if allow_eot else self.mask_text).expand(n, -1).contiguous()
+        if self.d_tok.numel() < n:
+            self.d_tok = torch.zeros(n, dtype=torch.int32, device=self.d_tok.device)
+        part_val = torch.empty(n * 64, dtype=torch.float32, device=logits.device)
+        part_idx = torch.empty(n * 64, dtype=torch.int32, device=logits.device)
+        ops.sample(logits, mask=mask, temperature=None, seed=self.d_seed, step=self.d_step, out_tokens=self.d_tok,
+                   part_val=part_val, part_idx=part_idx)
+        return self.d_tok[:n].tolist()

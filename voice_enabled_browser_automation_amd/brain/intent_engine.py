@@ -12,7 +12,9 @@ grammar-constrained decoding:
 * the token mask for step t is computed on the CPU (native grammar engine, GIL released) while
   the GPU runs step t's forward; the mask upload + sampling kernel follow on the same stream;
 * a character budget (``budget_chars``) guarantees the JSON can always be closed, so every
-  request terminates with a schema-valid ParseResponse.
+  request terminates with a schema-valid ParseResponse;
+* **continuous batching**: concurrent requests (voice sessions) decode together, one ragged
+  forward + one masked-sampling launch per iteration for all of them.
 
 `FakeIntentEngine` is the test double (the reference mocks callLLMJSON with vi.spyOn,
 apps/brain/test/parse.test.ts:7-21).
@@ -20,8 +22,12 @@ apps/brain/test/parse.test.ts:7-21).
 from __future__ import annotations
 
 import json
+import threading
 import time
-from typing import Any, Callable, Dict, List, Optional
+from collections import deque
+from concurrent.futures import Future
+from dataclasses import dataclass, field
+from typing import Any, Callable, Deque, Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -35,38 +41,92 @@ class IntentEngineError(RuntimeError):
     pass
 
 
+@dataclass
+class IntentRequest:
+    """One in-flight parse: prompt -> sequence -> grammar matcher -> JSON bytes."""
+
+    messages: List[Dict[str, str]]
+    ids: List[int] = field(default_factory=list)
+    seq: Any = None
+    matcher: Any = None
+    out: bytearray = field(default_factory=bytearray)
+    feed: List[int] = field(default_factory=list)   # tokens to append before the next sample
+    steps: int = 0
+    forced: int = 0
+    cached: int = 0
+    t_submit: float = 0.0
+    t_start: float = 0.0
+    t_first: float = 0.0
+    t_end: float = 0.0
+    done: bool = False
+    text: Optional[str] = None
+    error: Optional[BaseException] = None
+    future: Any = None
+
+    def stats(self, t_end: float) -> Dict[str, Any]:
+        return dict(prompt_tokens=len(self.ids), cached_prefix_tokens=self.cached,
+                    prefill_tokens=len(self.ids) - self.cached, decode_steps=self.steps, forced_tokens=self.forced,
+                    output_chars=len(self.out), queue_ms=(self.t_start - self.t_submit) * 1e3,
+                    prefill_ms=(self.t_first - self.t_start) * 1e3, decode_ms=(t_end - self.t_first) * 1e3,
+                    total_ms=(t_end - self.t_start) * 1e3)
+
+
 class LLMIntentEngine:
+    """Grammar-constrained intent decoding with continuous batching.
+
+    Every scheduler iteration (``step``) runs ONE ragged forward over all active requests --
+    each contributes its pending rows (last sampled token + jump-forward tokens) and gets its
+    logits row back (the LM head runs on one row per request) -- then one masked sampling
+    launch for all of them.  New requests are admitted between iterations (prefix-cached
+    prompt, prefill of all but the last prompt token, which joins the batched forward), and
+    finished ones leave immediately, so a burst of voice sessions shares every weight read.
+    """
+
     name = "llm"
 
     def __init__(self, engine, tokenizer, grammar: Optional[CompiledGrammar] = None, *, budget_chars: int = 512,
-                 temperature: float = 0.1, max_steps: int = 400, seed: int = 0):
+                 temperature: float = 0.1, max_steps: int = 400, seed: int = 0, max_active: Optional[int] = None,
+                 chat_format: Callable[[List[Dict[str, str]]], Tuple[str, str]] = llama3_chat):
         self.engine = engine
+        self.chat_format = chat_format
         self.tok = tokenizer
         self.grammar = grammar or intent_grammar(tokenizer)
         self.budget_chars = budget_chars
         self.temperature = temperature
         self.max_steps = max_steps
+        self.max_active = max_active or engine.max_seqs
+        self.max_rows = engine.bufs.max_rows
         dev = engine.device
         self.dev = dev
         pin = dev.type == "cuda"
-        W = self.grammar.words
-        self.h_mask = torch.zeros(1, W, dtype=torch.int32, pin_memory=pin)
-        self.h_mask_np = self.h_mask.numpy().reshape(-1)
-        self.d_mask = torch.zeros(1, W, dtype=torch.int32, device=dev)
-        self.d_temp = torch.full((1,), float(temperature), dtype=torch.float32, device=dev)
+        R, W = self.max_active, self.grammar.words
+        self.h_mask = torch.zeros(R, W, dtype=torch.int32, pin_memory=pin)
+        self.h_mask_np = self.h_mask.numpy()
+        self.d_mask = torch.zeros(R, W, dtype=torch.int32, device=dev)
+        self.d_temp = torch.full((R,), float(temperature), dtype=torch.float32, device=dev)
         self.d_seed = torch.tensor([seed], dtype=torch.int64, device=dev)
         self.d_step = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.d_tok = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.h_tok = torch.zeros(1, dtype=torch.int32, pin_memory=pin)
-        self.part_val = torch.zeros(64, dtype=torch.float32, device=dev)
-        self.part_idx = torch.zeros(64, dtype=torch.int32, device=dev)
+        self.d_tok = torch.zeros(R, dtype=torch.int32, device=dev)
+        self.h_tok = torch.zeros(R, dtype=torch.int32, pin_memory=pin)
+        self.part_val = torch.zeros(R * 64, dtype=torch.float32, device=dev)
+        self.part_idx = torch.zeros(R * 64, dtype=torch.int32, device=dev)
         self.last_stats: Dict[str, Any] = {}
+        self.last_batch: List[Dict[str, Any]] = []
+        self.batch_stats = dict(iterations=0, rows=0, sampled=0, max_active=0)
+        # host-side time per scheduler phase (where a decode step's wall time goes)
+        self.timing = dict(build_launch_ms=0.0, mask_ms=0.0, sample_launch_ms=0.0, gpu_wait_ms=0.0, post_ms=0.0)
         self._prefix_ids: Dict[str, List[int]] = {}
         self._head_len = 0
+        self.waiting: Deque[IntentRequest] = deque()
+        self.active: List[IntentRequest] = []
+        self._lock = threading.Lock()
+        self._wake = threading.Condition(self._lock)
+        self._thread: Optional[threading.Thread] = None
+        self._stop = False
 
     # ------------------------------------------------------------------ helpers
     def _encode_prompt(self, messages) -> List[int]:
-        head, tail = llama3_chat(messages)
+        head, tail = self.chat_format(messages)
         ids = self._prefix_ids.get(head)
         if ids is None:
             ids = self.tok.encode(head)
@@ -74,77 +134,167 @@ class LLMIntentEngine:
         self._head_len = len(ids)
         return ids + self.tok.encode(tail)
 
-    def _sample(self, logits: torch.Tensor) -> int:
-        ops.sample(logits, mask=self.d_mask, temperature=self.d_temp if self.temperature > 0 else None,
-                   seed=self.d_seed, step=self.d_step, out_tokens=self.d_tok, part_val=self.part_val,
-                   part_idx=self.part_idx)
-        if self.dev.type == "cuda":
-            self.h_tok.copy_(self.d_tok, non_blocking=True)
-            torch.cuda.current_stream().synchronize()
-            return int(self.h_tok[0])
-        return int(self.d_tok[0])
-
-    def _run(self, seq, toks: List[int]) -> torch.Tensor:
-        logits = None
-        for i in range(0, len(toks), 64):
-            chunk = toks[i : i + 64]
-            logits = self.engine.run_rows([(seq, t) for t in chunk])[-1:]
-        return logits
-
-    # ------------------------------------------------------------------ generation
-    def generate(self, messages: List[Dict[str, str]]) -> str:
-        t0 = time.perf_counter()
-        eng = self.engine
-        ids = self._encode_prompt(messages)
-        seq = eng.new_sequence(ids)
-        cached = seq.n_computed
-        try:
-            logits = eng.prefill(seq)
-            t_prefill = time.perf_counter()
-            m = self.grammar.matcher(self.budget_chars)
-            out = bytearray()
-            steps = forced_toks = 0
-            forced = m.forced_prefix()
-            if forced:
-                m.accept_bytes(forced)
-                out += forced
-                ftoks = self.tok.encode(forced.decode("ascii"))
-                forced_toks += len(ftoks)
-                logits = self._run(seq, ftoks)
-            while not m.is_accept():
-                if steps >= self.max_steps:
-                    raise IntentEngineError("decode step limit reached")
-                m.fill_mask(self.h_mask_np)  # CPU, overlaps the in-flight forward
-                self.d_mask.copy_(self.h_mask, non_blocking=True)
-                tok = self._sample(logits)
-                steps += 1
-                if tok < 0 or not m.accept_token(tok):
-                    raise IntentEngineError(f"sampler returned a token the grammar rejects ({tok})")
-                out += self.grammar_bytes(tok)
-                if m.is_accept():
-                    seq.tokens.append(tok)
-                    break
-                forced = m.forced_prefix()
-                ftoks: List[int] = []
-                if forced:
-                    m.accept_bytes(forced)
-                    out += forced
-                    ftoks = self.tok.encode(forced.decode("ascii"))
-                    forced_toks += len(ftoks)
-                logits = self._run(seq, [tok] + ftoks)
-            t_end = time.perf_counter()
-            self.last_stats = dict(prompt_tokens=len(ids), cached_prefix_tokens=cached,
-                                   prefill_tokens=len(ids) - cached, decode_steps=steps, forced_tokens=forced_toks,
-                                   output_chars=len(out), prefill_ms=(t_prefill - t0) * 1e3,
-                                   decode_ms=(t_end - t_prefill) * 1e3, total_ms=(t_end - t0) * 1e3)
-            return out.decode("utf-8")
-        finally:
-            # only the static system + few-shot prefix is shared across requests; the request's
-            # own suffix and answer are never served from cache (no replay of repeated commands)
-            eng.free_sequence(seq, publish_upto=self._head_len)
-
     def grammar_bytes(self, tok: int) -> bytes:
         return self.tok.token_bytes()[tok]
+
+    def _jump_forward(self, r: IntentRequest) -> None:
+        forced = r.matcher.forced_prefix()
+        if forced:
+            r.matcher.accept_bytes(forced)
+            r.out += forced
+            ftoks = self.tok.encode(forced.decode("ascii"))
+            r.forced += len(ftoks)
+            r.feed += ftoks
+
+    def _admit(self, r: IntentRequest) -> None:
+        eng = self.engine
+        r.t_start = time.perf_counter()
+        r.ids = self._encode_prompt(r.messages)
+        r.seq = eng.new_sequence(r.ids)
+        r.cached = r.seq.n_computed
+        if r.cached >= len(r.ids):  # whole prompt cached: recompute its last token for logits
+            r.seq.n_computed = r.cached = len(r.ids) - 1
+        eng.prefill(r.seq, upto=len(r.ids) - 1)  # the last prompt token joins the batched step
+        r.t_first = time.perf_counter()
+        r.matcher = self.grammar.matcher(self.budget_chars)
+        if r.matcher.min_completion() > self.budget_chars:
+            raise IntentEngineError(f"budget_chars={self.budget_chars} is below the shortest schema-valid "
+                                    f"answer ({r.matcher.min_completion()} chars)")
+        r.feed = [r.ids[-1]]
+        self._jump_forward(r)
+
+    def _finish(self, r: IntentRequest, error: Optional[BaseException] = None) -> None:
+        r.done = True
+        r.error = error
+        if error is None:
+            r.text = r.out.decode("utf-8")
+        if r.seq is not None:
+            # only the static system + few-shot prefix is shared across requests; the request's
+            # own suffix and answer are never served from cache (no replay of repeated commands)
+            self.engine.free_sequence(r.seq, publish_upto=self._head_len)
+            r.seq = None
+        r.t_end = time.perf_counter()
+        self.last_stats = r.stats(r.t_end)
+        if r.future is not None:
+            if error is None:
+                r.future.set_result(r.text)
+            else:
+                r.future.set_exception(error)
+
+    # ------------------------------------------------------------------ scheduler
+    def submit(self, messages: List[Dict[str, str]], future=None) -> IntentRequest:
+        r = IntentRequest(messages=messages, t_submit=time.perf_counter(), future=future)
+        with self._lock:
+            self.waiting.append(r)
+            self._wake.notify()
+        return r
+
+    def has_work(self) -> bool:
+        return bool(self.active or self.waiting)
+
+    def step(self) -> List[IntentRequest]:
+        """One scheduler iteration; returns the requests that finished in it."""
+        finished: List[IntentRequest] = []
+        while len(self.active) < self.max_active:
+            with self._lock:
+                if not self.waiting:
+                    break
+                r = self.waiting.popleft()
+            try:
+                self._admit(r)
+                self.active.append(r)
+            except Exception as e:  # noqa: BLE001
+                self._finish(r, e)
+                finished.append(r)
+        if not self.active:
+            return finished
+        # rows: each request's pending tokens; requests that do not fit wait one iteration, a
+        # feed longer than the row cap is consumed in pieces (sampled once it is exhausted)
+        rows, last, batch, budget = [], [], [], self.max_rows
+        for r in self.active:
+            if not r.feed or budget <= 0:
+                continue
+            take = r.feed[:budget]
+            if len(take) < len(r.feed) and rows:
+                continue
+            rows += [(r.seq, t) for t in take]
+            budget -= len(take)
+            r.feed = r.feed[len(take):]
+            if not r.feed:
+                last.append(len(rows) - 1)
+                batch.append(r)
+        if not rows:
+            return finished
+        tm = self.timing
+        t0 = time.perf_counter()
+        logits = self.engine.run_rows(rows, logits_for=last) if last else None
+        t1 = time.perf_counter()
+        tm["build_launch_ms"] += (t1 - t0) * 1e3
+        self.batch_stats["iterations"] += 1
+        self.batch_stats["rows"] += len(rows)
+        self.batch_stats["max_active"] = max(self.batch_stats["max_active"], len(self.active))
+        if not batch:
+            return finished
+        n = len(batch)
+        for i, r in enumerate(batch):  # CPU grammar masks overlap the in-flight forward
+            r.matcher.fill_mask(self.h_mask_np[i])
+        t2 = time.perf_counter()
+        self.d_mask[:n].copy_(self.h_mask[:n], non_blocking=True)
+        ops.sample(logits, mask=self.d_mask, temperature=self.d_temp if self.temperature > 0 else None,
+                   seed=self.d_seed, step=self.d_step, out_tokens=self.d_tok, part_val=self.part_val[: n * 64],
+                   part_idx=self.part_idx[: n * 64])
+        if self.dev.type == "cuda":
+            self.h_tok[:n].copy_(self.d_tok[:n], non_blocking=True)
+            t3 = time.perf_counter()
+            torch.cuda.current_stream().synchronize()
+            toks = self.h_tok[:n].tolist()
+        else:
+            t3 = time.perf_counter()
+            toks = self.d_tok[:n].tolist()
+        t4 = time.perf_counter()
+        tm["mask_ms"] += (t2 - t1) * 1e3
+        tm["sample_launch_ms"] += (t3 - t2) * 1e3
+        tm["gpu_wait_ms"] += (t4 - t3) * 1e3
+        self.batch_stats["sampled"] += n
+        for r, tok in zip(batch, toks):
+            r.steps += 1
+            m = r.matcher
+            if tok < 0 or not m.accept_token(tok):
+                self._finish(r, IntentEngineError(f"sampler returned a token the grammar rejects ({tok})"))
+            else:
+                r.out += self.grammar_bytes(tok)
+                if m.is_accept():
+                    r.seq.tokens.append(tok)
+                    self._finish(r)
+                elif r.steps >= self.max_steps:
+                    self._finish(r, IntentEngineError("decode step limit reached"))
+                else:
+                    r.feed = [tok]
+                    self._jump_forward(r)
+            if r.done:
+                finished.append(r)
+        if finished:
+            self.active = [r for r in self.active if not r.done]
+        tm["post_ms"] += (time.perf_counter() - t4) * 1e3
+        return finished
+
+    def run_until_idle(self) -> None:
+        while self.has_work():
+            self.step()
+
+    def generate_many(self, messages_list: List[List[Dict[str, str]]]) -> List[str]:
+        """Decode a batch of requests together (continuous batching); raises the first error."""
+        reqs = [self.submit(m) for m in messages_list]
+        while not all(r.done for r in reqs):
+            self.step()
+        self.last_batch = [dict(r.stats(r.t_end), latency_ms=(r.t_end - r.t_submit) * 1e3) for r in reqs]
+        for r in reqs:
+            if r.error is not None:
+                raise r.error
+        return [r.text for r in reqs]
+
+    def generate(self, messages: List[Dict[str, str]]) -> str:
+        return self.generate_many([messages])[0]
 
     def __call__(self, messages: List[Dict[str, str]]) -> Any:
         """callLLMJSON parity: returns the parsed JSON object."""
@@ -152,6 +302,48 @@ class LLMIntentEngine:
 
     def parse(self, request: Dict[str, Any], repair: bool = False) -> Any:
         return self(messages_for(request, repair=repair))
+
+    def parse_many(self, requests: List[Dict[str, Any]]) -> List[Any]:
+        return [json.loads(t) for t in self.generate_many([messages_for(r) for r in requests])]
+
+    # ------------------------------------------------------------------ background serving
+    def start(self) -> None:
+        """Run the scheduler on a background thread (the brain service submits into it)."""
+        if self._thread is not None:
+            return
+        self._stop = False
+        self._thread = threading.Thread(target=self._loop, name="intent-scheduler", daemon=True)
+        self._thread.start()
+
+    def stop(self) -> None:
+        with self._lock:
+            self._stop = True
+            self._wake.notify()
+        if self._thread is not None:
+            self._thread.join(timeout=30)
+            self._thread = None
+
+    def _loop(self) -> None:
+        if self.dev.type == "cuda":
+            torch.cuda.set_device(self.dev)
+        while True:
+            with self._lock:
+                while not self._stop and not self.waiting and not self.active:
+                    self._wake.wait()
+                if self._stop:
+                    return
+            try:
+                self.step()
+            except Exception as e:  # noqa: BLE001  (fail every in-flight request, keep serving)
+                for r in self.active:
+                    self._finish(r, e)
+                self.active = []
+
+    def submit_async(self, messages: List[Dict[str, str]]):
+        """concurrent.futures.Future resolved with the JSON text (requires start())."""
+        fut: Future = Future()
+        self.submit(messages, future=fut)
+        return fut
 
 
 class FakeIntentEngine:

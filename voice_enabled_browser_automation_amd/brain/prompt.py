@@ -125,3 +125,18 @@ def llama3_chat(messages: List[Dict[str, str]]) -> Tuple[str, str]:
         head = "<|begin_of_text|>" + "".join(turn(m) for m in messages[:-2])
         tail = turn(messages[-2]) + turn(last) + "<|start_header_id|>assistant<|end_header_id|>\n\n"
     return head, tail
+
+
+def plain_chat(messages: List[Dict[str, str]]) -> Tuple[str, str]:
+    """(static prefix, dynamic suffix) for base LMs without chat tokens (GPT-2 config): role-tagged
+    paragraphs separated by blank lines, the answer primed after ``Assistant:``."""
+    def turn(m):
+        return f"{m['role'].capitalize()}: {m['content']}\n\n"
+
+    head_msgs, tail_msgs = messages[:-1], messages[-1:]
+    if messages[-1]["role"] == "system":  # repair note after the user turn
+        head_msgs, tail_msgs = messages[:-2], messages[-2:]
+    return "".join(turn(m) for m in head_msgs), "".join(turn(m) for m in tail_msgs) + "Assistant: "
+
+
+CHAT_FORMATS = {"llama3": llama3_chat, "plain": plain_chat}

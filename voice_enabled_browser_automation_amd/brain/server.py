@@ -49,6 +49,18 @@ def build_app(engine: Any = None) -> web.Application:
             snap["last_request"] = st
         return web.json_response(snap)
 
+    async def call(eng, messages):
+        if hasattr(eng, "submit_async"):
+            # continuous batching: concurrent requests decode together on the scheduler thread
+            eng.start()
+            return json.loads(await asyncio.wrap_future(eng.submit_async(messages)))
+        async with app["lock"]:  # engines without a scheduler: serial requests
+            return await asyncio.get_running_loop().run_in_executor(None, eng, messages)
+
+    async def on_cleanup(_app):
+        if hasattr(app["engine"], "stop"):
+            app["engine"].stop()
+
     async def parse(req: web.Request) -> web.Response:
         m: Metrics = app["metrics"]
         t0 = time.perf_counter()
@@ -62,14 +74,12 @@ def build_app(engine: Any = None) -> web.Application:
             return web.json_response({"error": "invalid_request", "detail": pr.format_error()}, status=400)
         request = pr.data
         eng = app["engine"]
-        loop = asyncio.get_running_loop()
         try:
-            async with app["lock"]:  # one engine, serial requests (the engine batches internally)
-                out = await loop.run_in_executor(None, eng, messages_for(request))
-                first = safe_parse(ParseResponse, out)
-                if not first.success:
-                    m.inc("repairs")
-                    out = await loop.run_in_executor(None, eng, messages_for(request, repair=True))
+            out = await call(eng, messages_for(request))
+            first = safe_parse(ParseResponse, out)
+            if not first.success:
+                m.inc("repairs")
+                out = await call(eng, messages_for(request, repair=True))
         except Exception as e:  # noqa: BLE001
             m.inc("llm_error")
             return web.json_response({"error": "llm_error", "detail": str(e) or e.__class__.__name__}, status=500)
@@ -81,6 +91,7 @@ def build_app(engine: Any = None) -> web.Application:
         m.inc("ok")
         return web.json_response(final.data)
 
+    app.on_cleanup.append(on_cleanup)
     app.router.add_get("/health", health)
     app.router.add_get("/metrics", metrics)
     app.router.add_post("/parse", parse)
@@ -99,22 +110,38 @@ def make_engine_from_env():
 
 
 def build_llm_engine(model_name: Optional[str] = None, device: Optional[str] = None):
+    """Intent LLM from env: VWA_LLM_MODEL (llama3-8b | llama3-70b | llama3.2-1b | llama-tiny |
+    gpt2-small | gpt2-tiny), VWA_TP, VWA_MAX_SESSIONS, VWA_BUDGET_CHARS, VWA_SEED.  GPT-2 is the
+    CPU config (BASELINE.json config 1): plain-text prompt layout, GPT-2 vocabulary."""
     import torch
 
-    from ..models.config import get_config
-    from ..models.llama import LlamaModel
+    from ..models.config import GPT2Config, get_config
     from ..parallel.tp import init_distributed
     from ..runtime.engine import LLMEngine
     from ..tokenizer import load_tokenizer
     from .intent_engine import LLMIntentEngine
+    from .prompt import llama3_chat, plain_chat
 
     name = model_name or os.environ.get("VWA_LLM_MODEL", "llama3-8b")
-    tp = init_distributed(tp_size=int(os.environ.get("VWA_TP", "1") or 1))
+    cfg = get_config(name)
+    seed = int(os.environ.get("VWA_SEED", "0"))
     dev = device or ("cuda" if torch.cuda.is_available() else "cpu")
-    model = LlamaModel(get_config(name), device=dev, tp=tp, seed=int(os.environ.get("VWA_SEED", "0")))
-    eng = LLMEngine(model, max_seqs=int(os.environ.get("VWA_MAX_SESSIONS", "8")), max_model_len=4096)
+    sessions = int(os.environ.get("VWA_MAX_SESSIONS", "8"))
+    budget = int(os.environ.get("VWA_BUDGET_CHARS", "512"))
+    if isinstance(cfg, GPT2Config):
+        from ..models.gpt2 import GPT2Model
+
+        model = GPT2Model(cfg, device=dev, seed=seed)
+        eng = LLMEngine(model, max_seqs=sessions, max_model_len=cfg.max_pos)
+        eng.capture_all()
+        return LLMIntentEngine(eng, load_tokenizer("gpt2"), budget_chars=budget, chat_format=plain_chat)
+    from ..models.llama import LlamaModel
+
+    tp = init_distributed(tp_size=int(os.environ.get("VWA_TP", "1") or 1))
+    model = LlamaModel(cfg, device=dev, tp=tp, seed=seed)
+    eng = LLMEngine(model, max_seqs=sessions, max_model_len=4096)
     eng.capture_all()
-    ie = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=int(os.environ.get("VWA_BUDGET_CHARS", "512")))
+    ie = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=budget, chat_format=llama3_chat)
     return TPIntentEngine(ie, tp) if tp.size > 1 else ie
 
 

@@ -146,13 +146,14 @@ class LlamaModel:
             self.tp.all_reduce(h)
 
     def forward(self, bufs, M: int, kv, *, prefill_seq: Optional[int] = None, q_offset: int = 0,
-                logits_rows: Optional[slice] = None) -> torch.Tensor:
+                logits_rows: Optional[slice] = None, n_sel: Optional[int] = None) -> torch.Tensor:
         """Run M token rows described by ``bufs`` (runtime.buffers.StepBuffers).
 
         Decode/ragged mode (M <= 64): each row is one token of some sequence (seq_ids /
         ctx_lens / positions / slots per row).  Prefill mode (prefill_seq given): the M rows are
         consecutive tokens of table row ``prefill_seq`` starting at position q_offset.
-        Returns f32 logits [rows, vocab] (all ranks, gathered under TP).
+        Returns f32 logits [rows, vocab] (all ranks, gathered under TP) for every row, for
+        ``logits_rows``, or (``n_sel``) for the rows listed in ``bufs.sel[:n_sel]``.
         """
         cfg = self.cfg
         h = bufs.hidden[:M]
@@ -168,8 +169,7 @@ class LlamaModel:
                 attn = bufs.attn[:M]
                 ops.decode_attention(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens, bufs.seq_ids,
                                      n_q_heads=self.nq, n_kv_heads=self.nkv, head_dim=self.hd, scale=self.scale,
-                                     max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o, part_ml=bufs.part_ml,
-                                     counters=bufs.attn_cnt)
+                                     max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o, part_ml=bufs.part_ml)
             else:
                 table = bufs.block_table[prefill_seq : prefill_seq + 1]
                 q4 = q.view(1, M, self.nq, self.hd)
@@ -181,8 +181,10 @@ class LlamaModel:
             act = bufs.act[:M] if M <= bufs.act.shape[0] else None
             act = ops.linear_swiglu(h, L.gu, fuse_rms=True, eps=cfg.rms_eps, out=act)
             self._row_parallel(act, L.down, h)
-        rows = logits_rows if logits_rows is not None else slice(0, M)
-        hs = h[rows]
+        if n_sel is not None:
+            hs = torch.index_select(h, 0, bufs.sel[:n_sel], out=bufs.hidden_sel[:n_sel])
+        else:
+            hs = h[logits_rows if logits_rows is not None else slice(0, M)]
         n = hs.shape[0]
         local = bufs.logits_local[:n] if n <= bufs.logits_local.shape[0] else None
         local = ops.linear(hs, self.lm_head, out=local, fuse_rms=True, eps=cfg.rms_eps, out_dtype=torch.float32)

@@ -74,10 +74,11 @@ def init_distributed(tp_size: Optional[int] = None, backend: Optional[str] = Non
     rank = int(os.environ.get("RANK", "0"))
     if not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
+            backend = os.environ.get("VWA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        if torch.cuda.is_available():
             local = int(os.environ.get("LOCAL_RANK", rank))
-            torch.cuda.set_device(local)
+            # gloo rehearsal of a multi-rank run on fewer GPUs: ranks share devices round-robin
+            torch.cuda.set_device(local if backend == "nccl" else local % torch.cuda.device_count())
         dist.init_process_group(backend=backend)
     tp = tp_size or world
     assert world % tp == 0, f"world {world} not divisible by tp {tp}"

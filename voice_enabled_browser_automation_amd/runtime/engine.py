@@ -55,19 +55,22 @@ class StepBuffers:
         self.max_rows = max_rows
         self.max_ctx = max_ctx
         # all per-row metadata lives in ONE device buffer (and one pinned host mirror) so a step
-        # needs a single H2D copy: [tokens | positions | seq_ids | ctx_lens | slots (int64)]
+        # needs a single H2D copy: [tokens | positions | seq_ids | ctx_lens | slots (int64) | sel]
+        # (sel = the rows whose logits the step returns: one per sequence, not one per token row)
         R = max_rows
-        self.meta = torch.zeros(6 * R, **i32)
+        self.meta = torch.zeros(7 * R, **i32)
         self.tokens = self.meta[0:R]
         self.positions = self.meta[R : 2 * R]
         self.seq_ids = self.meta[2 * R : 3 * R]
         self.ctx_lens = self.meta[3 * R : 4 * R]
         self.slots = self.meta[4 * R : 6 * R].view(torch.int64)
+        self.sel = self.meta[6 * R : 7 * R]
         self.ctx_lens.fill_(1)
         self.slots.fill_(-1)
         self.block_table = torch.zeros(max_seqs, max_blocks_per_seq, **i32)
         d = model.cfg.hidden
         self.hidden = torch.zeros(max_rows, d, dtype=dt, device=device)
+        self.hidden_sel = torch.zeros(max_rows, d, dtype=dt, device=device)
         self.q = torch.zeros(max_rows, model.nq * model.hd, dtype=dt, device=device)
         self.attn = torch.zeros_like(self.q)
         self.act = torch.zeros(max_rows, model.F, dtype=dt, device=device)
@@ -77,11 +80,11 @@ class StepBuffers:
         ns = ops.decode_n_splits(max_ctx)
         self.part_o = torch.zeros(max_rows * ns * model.nq * model.hd, dtype=torch.float32, device=device)
         self.part_ml = torch.zeros(max_rows * ns * model.nq * 2, dtype=torch.float32, device=device)
-        self.attn_cnt = torch.zeros(max_rows * model.nkv, dtype=torch.int32, device=device)
         pin = torch.device(device).type == "cuda"
-        self.h_meta = torch.zeros(6 * R, dtype=torch.int32, pin_memory=pin)
+        self.h_meta = torch.zeros(7 * R, dtype=torch.int32, pin_memory=pin)
         self.h_i32 = self.h_meta[: 4 * R].view(4, R)
-        self.h_slots = self.h_meta[4 * R :].view(torch.int64)
+        self.h_slots = self.h_meta[4 * R : 6 * R].view(torch.int64)
+        self.h_sel = self.h_meta[6 * R :]
         self.h_table = torch.zeros(max_seqs, max_blocks_per_seq, dtype=torch.int32, pin_memory=pin)
         self.table_dirty = True
 
@@ -120,7 +123,7 @@ class LLMEngine:
         if use_graphs is None:
             use_graphs = ops.env_flag("VWA_HIPGRAPH", True)
         self.use_graphs = bool(use_graphs) and self.device.type == "cuda"
-        self.graphs: Dict[int, Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
+        self.graphs: Dict[Tuple[int, int], Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
         self.graph_pool = None
         self.stats = dict(steps=0, rows=0, prefill_tokens=0, cached_tokens=0, graph_replays=0)
 
@@ -170,44 +173,62 @@ class LLMEngine:
         return seq.blocks[pos // self.block_size] * self.block_size + pos % self.block_size
 
     # ------------------------------------------------------------------ forward
-    def _forward_rows(self, M: int) -> torch.Tensor:
-        return self.model.forward(self.bufs, M, self.kv)
+    def _forward_rows(self, M: int, L: int) -> torch.Tensor:
+        return self.model.forward(self.bufs, M, self.kv, n_sel=None if L == M else L)
 
-    def _capture(self, M: int):
+    def _capture(self, M: int, L: int):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
-                self._forward_rows(M)
+                self._forward_rows(M, L)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         if self.graph_pool is None:
             self.graph_pool = torch.cuda.graph_pool_handle()
         with torch.cuda.graph(g, pool=self.graph_pool):
-            out = self._forward_rows(M)
-        self.graphs[M] = (g, out)
-        return self.graphs[M]
+            out = self._forward_rows(M, L)
+        self.graphs[(M, L)] = (g, out)
+        return self.graphs[(M, L)]
 
-    def capture_all(self, buckets: Sequence[int] = BUCKETS) -> None:
+    def capture_all(self, buckets: Sequence[int] = BUCKETS, logit_buckets: Sequence[int] = (1,)) -> None:
+        """Capture the (row bucket, logit-row bucket) graphs up front; others are captured on
+        first use.  Default: every row bucket with one logit row (single-session decode with
+        jump-forward) plus the all-rows variant."""
         if not self.use_graphs:
             return
         for M in buckets:
-            if M <= self.bufs.max_rows and M not in self.graphs:
-                self._capture(M)
+            if M > self.bufs.max_rows:
+                continue
+            for L in tuple(logit_buckets) + (M,):
+                if L <= M and (M, L) not in self.graphs:
+                    self._capture(M, L)
         torch.cuda.synchronize()
 
-    def run_rows(self, rows: List[Tuple[Sequence_, int]]) -> torch.Tensor:
-        """Append one token per row (row = (seq, token)), return f32 logits [len(rows), V].
+    def run_rows(self, rows: List[Tuple[Sequence_, int]], logits_for: Optional[List[int]] = None) -> torch.Tensor:
+        """Append one token per row (row = (seq, token)); return f32 logits of the rows listed in
+        ``logits_for`` ([len(logits_for), V], default: every row).
 
-        Rows of the same sequence must be consecutive and in order.
+        Rows of the same sequence must be consecutive and in order.  Selecting rows (typically
+        the last row of each sequence) keeps the LM head -- the largest GEMM of a step -- at one
+        row per sequence when jump-forward appends forced tokens.
         """
         n = len(rows)
         M = bucket_for(n)
         b = self.bufs
         hi = b.h_i32
-        # per-sequence running length (several rows may extend the same sequence)
-        for seq, _tok in rows:
-            pass
+        if logits_for is None or len(logits_for) == n:
+            nl, L = n, M
+        else:
+            nl = len(logits_for)
+            L = min(bucket_for(nl), M)
+            if L == M:  # no saving: compute every row and index on the host side
+                pass
+            else:
+                for j, r in enumerate(logits_for):
+                    b.h_sel[j] = r
+                for j in range(nl, L):
+                    b.h_sel[j] = logits_for[-1]
         pending: Dict[int, int] = {}
         for i, (seq, tok) in enumerate(rows):
             pos = pending.get(seq.sid, seq.n_computed)
@@ -228,33 +249,34 @@ class LLMEngine:
             b.h_slots[i] = -1
         b.upload(M)
         if self.use_graphs:
-            g, out = self.graphs.get(M) or self._capture(M)
+            g, out = self.graphs.get((M, L)) or self._capture(M, L)
             g.replay()
             self.stats["graph_replays"] += 1
         else:
-            out = self._forward_rows(M)
+            out = self._forward_rows(M, L)
         for sid, ln in pending.items():
             self.seqs[sid].n_computed = ln
         self.stats["steps"] += 1
         self.stats["rows"] += n
-        return out[:n]
+        if L == M and nl != n:
+            return out[torch.tensor(logits_for, device=out.device)]
+        return out[:nl]
 
-    def prefill(self, seq: Sequence_, chunk: int = 2048) -> torch.Tensor:
-        """Compute K/V for seq.tokens[n_computed:]; returns f32 logits of the last token [1, V]."""
-        todo = len(seq.tokens) - seq.n_computed
-        assert todo >= 1, "nothing to prefill"
+    def prefill(self, seq: Sequence_, chunk: int = 2048, upto: Optional[int] = None) -> Optional[torch.Tensor]:
+        """Compute K/V for seq.tokens[n_computed:upto] (default: all tokens); returns f32 logits
+        of the last computed token [1, V] (None if there was nothing to compute)."""
+        end = len(seq.tokens) if upto is None else min(upto, len(seq.tokens))
+        todo = end - seq.n_computed
+        if todo <= 0:
+            return None
         self.stats["prefill_tokens"] += todo
-        if todo <= self.bufs.max_rows:
-            toks = seq.tokens[seq.n_computed:]
-            out = self.run_rows([(seq, t) for t in toks])
-            return out[-1:]
         logits = None
-        while seq.n_computed < len(seq.tokens):
+        while seq.n_computed < end:
             start = seq.n_computed
-            n = min(chunk, len(seq.tokens) - start)
+            n = min(chunk, end - start)
             if n <= self.bufs.max_rows:
                 toks = seq.tokens[start : start + n]
-                logits = self.run_rows([(seq, t) for t in toks])[-1:]
+                logits = self.run_rows([(seq, t) for t in toks], logits_for=[n - 1])
                 continue
             self._ensure_blocks(seq, start + n)
             if self.bufs.table_dirty:

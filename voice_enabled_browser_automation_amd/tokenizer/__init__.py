@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import functools
 import gzip
+import json
 import os
 from typing import List, Optional
 
@@ -77,12 +78,37 @@ class Tokenizer:
 def load_tokenizer(kind: str = "llama3") -> Tokenizer:
     from tokenizers import Tokenizer as HFTok
 
-    env = {"llama3": "VWA_LLAMA_TOKENIZER", "whisper": "VWA_WHISPER_TOKENIZER"}.get(kind)
+    env = {"llama3": "VWA_LLAMA_TOKENIZER", "whisper": "VWA_WHISPER_TOKENIZER", "gpt2": "VWA_GPT2_TOKENIZER"}.get(kind)
     path = os.environ.get(env) if env else None
     if path:
         tok = HFTok.from_file(path)
+    elif kind == "gpt2":
+        tok = HFTok.from_str(json.dumps(_gpt2_layout(_asset_json("whisper"))))
     else:
-        p = os.path.join(ASSET_DIR, f"{kind}_tokenizer.json.gz")
-        with gzip.open(p, "rt", encoding="utf-8") as fh:
-            tok = HFTok.from_str(fh.read())
+        tok = HFTok.from_str(json.dumps(_asset_json(kind)))
     return Tokenizer(tok, kind)
+
+
+def _asset_json(kind: str) -> dict:
+    with gzip.open(os.path.join(ASSET_DIR, f"{kind}_tokenizer.json.gz"), "rt", encoding="utf-8") as fh:
+        return json.load(fh)
+
+
+GPT2_PATTERN = r"""'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+"""
+
+
+def _gpt2_layout(d: dict) -> dict:
+    """GPT-2 id layout (50257 ids, <|endoftext|> = 50256) derived from the byte-level BPE shared
+    with the Whisper vocabulary: the last merge is dropped so the BPE part ends at 50255, the
+    Whisper special tokens are removed, and the GPT-2 pre-tokenizer regex is used."""
+    m = d["model"]
+    last = max(m["vocab"].values())
+    m["vocab"] = {t: i for t, i in m["vocab"].items() if i < last}
+    m["merges"] = m["merges"][:-1]
+    d["added_tokens"] = [{"id": last, "content": "<|endoftext|>", "single_word": False, "lstrip": False,
+                          "rstrip": False, "normalized": False, "special": True}]
+    d["pre_tokenizer"] = {"type": "Sequence", "pretokenizers": [
+        {"type": "Split", "pattern": {"Regex": GPT2_PATTERN}, "behavior": "Isolated", "invert": False},
+        {"type": "ByteLevel", "add_prefix_space": False, "trim_offsets": True, "use_regex": False}]}
+    d["post_processor"] = None
+    return d
