@@ -125,6 +125,8 @@ def main():
     ap.add_argument("--concurrent", type=int, default=int(os.environ.get("VWA_BENCH_CONCURRENT", "0")),
                     help="also measure C concurrent voice sessions per rank (batched ASR + continuous-batched "
                          "intent decoding); reported under 'concurrent', outside the headline value")
+    ap.add_argument("--dtype", default=os.environ.get("VWA_DTYPE", "bf16"), choices=("bf16", "fp8"),
+                    help="LLM weight dtype: bf16 (headline config) or fp8 (W8A8 on the fp8 MFMA, config 5)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
@@ -147,7 +149,7 @@ def main():
     whisper = WhisperModel(wcfg, device=dev, seed=1)
     C = max(0, args.concurrent)
     asr = AsrEngine(whisper, load_tokenizer("whisper"), max_sessions=max(2, C), use_graphs=use_graphs)
-    llama = LlamaModel(lcfg, device=dev, tp=tp, seed=2)
+    llama = LlamaModel(lcfg, device=dev, tp=tp, seed=2, wdtype=args.dtype)
     engine = LLMEngine(llama, max_seqs=max(4, C), max_model_len=2048, use_graphs=use_graphs)
     brain = LLMIntentEngine(engine, load_tokenizer("llama3"), budget_chars=args.budget_chars, temperature=0.1,
                             seed=1234 + tp.dp_rank)  # identical within a TP group (lockstep decode)
@@ -227,7 +229,7 @@ def main():
             "higher_is_better": False,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.dtype,
             "data": "synthetic 16 kHz speech-like audio, random-init weights",
             "config": {"model": f"{args.asr} + {args.llm}", "global_batch": world // tp.size, "seq_len": None,
                        "parallelism": f"dp{world // tp.size}" + (f"-tp{tp.size}" if tp.size > 1 else ""),

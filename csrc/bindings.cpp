@@ -53,9 +53,16 @@ int run_skinny(int epi, const SkinnyParams& p, hipStream_t st) {
   return vwa_skinny_gemm(epi, &p, st);
 }
 
-SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool fuse_rms, double eps) {
+SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool fuse_rms, double eps,
+                         const c10::optional<Tensor>& w_scale = c10::nullopt) {
   check_bf16(x, "x");
-  check_bf16(w, "w");
+  if (w_scale.has_value()) {
+    TORCH_CHECK(w.scalar_type() == at::kFloat8_e4m3fn && w.is_cuda(), "fp8 weights must be float8_e4m3fn on the GPU");
+    TORCH_CHECK(w_scale->scalar_type() == at::kFloat && w_scale->is_contiguous() && w_scale->numel() == w.size(0),
+                "w_scale must be f32 [N]");
+  } else {
+    check_bf16(w, "w");
+  }
   check_contig_rows(x, "x");
   TORCH_CHECK(w.is_contiguous() && w.dim() == 2, "w must be contiguous [N, K]");
   TORCH_CHECK(x.size(1) == w.size(1), "K mismatch: x ", x.sizes(), " w ", w.sizes());
@@ -75,14 +82,22 @@ SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<T
   p.bias = bfp_opt(bias);
   p.fuse_rms = fuse_rms ? 1 : 0;
   p.eps = (float)eps;
+  p.w_scale = w_scale.has_value() ? w_scale->data_ptr<float>() : nullptr;
   return p;
+}
+
+// fp8 weights run only on the streaming kernel; a shape it cannot take is an error, never a
+// silent bf16 fallback (the Python layer routes those shapes to the dequantising path).
+int run_skinny_checked(int epi, const SkinnyParams& p, hipStream_t st) {
+  if (p.w_scale) return vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
+  return run_skinny(epi, p, st);
 }
 
 // epi: 0 store, 1 residual add, 3 gelu
 void skinny_gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi, bool fuse_rms, double eps,
-                 c10::optional<Tensor> residual) {
+                 c10::optional<Tensor> residual, c10::optional<Tensor> w_scale) {
   c10::DeviceGuard g(x.device());
-  SkinnyParams p = base_params(x, w, bias, fuse_rms, eps);
+  SkinnyParams p = base_params(x, w, bias, fuse_rms, eps, w_scale);
   TORCH_CHECK(epi == 0 || epi == 1 || epi == 3, "bad epilogue");
   TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be a 2-D row-contiguous GPU tensor");
   TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) == w.size(0), "y shape mismatch");
@@ -99,19 +114,20 @@ void skinny_gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64
     p.R = bfp(*residual);
     p.ldr = (int)residual->stride(0);
   }
-  check_rc(run_skinny((int)epi, p, cur_stream(x)), "skinny_gemm");
+  check_rc(run_skinny_checked((int)epi, p, cur_stream(x)), "skinny_gemm");
 }
 
-void skinny_gemm_swiglu(Tensor x, Tensor w_gu, c10::optional<Tensor> bias, Tensor h, bool fuse_rms, double eps) {
+void skinny_gemm_swiglu(Tensor x, Tensor w_gu, c10::optional<Tensor> bias, Tensor h, bool fuse_rms, double eps,
+                        c10::optional<Tensor> w_scale) {
   c10::DeviceGuard g(x.device());
-  SkinnyParams p = base_params(x, w_gu, bias, fuse_rms, eps);
+  SkinnyParams p = base_params(x, w_gu, bias, fuse_rms, eps, w_scale);
   check_bf16(h, "h");
   TORCH_CHECK(h.dim() == 2 && h.stride(1) == 1 && h.size(0) == x.size(0) && h.size(1) * 2 == w_gu.size(0),
               "h must be [M, N/2]");
   TORCH_CHECK(w_gu.size(0) % 32 == 0, "gate/up rows must be a multiple of 32");
   p.Y = h.data_ptr();
   p.ldy = (int)h.stride(0);
-  check_rc(run_skinny(2, p, cur_stream(x)), "skinny_gemm_swiglu");
+  check_rc(run_skinny_checked(2, p, cur_stream(x)), "skinny_gemm_swiglu");
 }
 
 void check_cache(const Tensor& c, const char* name) {
@@ -121,9 +137,10 @@ void check_cache(const Tensor& c, const char* name) {
 
 void skinny_gemm_qkv(Tensor x, Tensor w_qkv, c10::optional<Tensor> bias, bool fuse_rms, double eps, int64_t n_q_heads,
                      int64_t n_kv_heads, int64_t head_dim, bool use_rope, Tensor positions, Tensor slots,
-                     c10::optional<Tensor> rope, Tensor q_out, Tensor k_cache, Tensor v_cache) {
+                     c10::optional<Tensor> rope, Tensor q_out, Tensor k_cache, Tensor v_cache,
+                     c10::optional<Tensor> w_scale) {
   c10::DeviceGuard g(x.device());
-  SkinnyParams p = base_params(x, w_qkv, bias, fuse_rms, eps);
+  SkinnyParams p = base_params(x, w_qkv, bias, fuse_rms, eps, w_scale);
   TORCH_CHECK(w_qkv.size(0) == (n_q_heads + 2 * n_kv_heads) * head_dim, "w_qkv rows mismatch");
   TORCH_CHECK(head_dim % 16 == 0, "head_dim must be a multiple of 16");
   TORCH_CHECK(positions.scalar_type() == at::kInt && positions.numel() >= x.size(0), "positions int32 [M]");
@@ -152,7 +169,7 @@ void skinny_gemm_qkv(Tensor x, Tensor w_qkv, c10::optional<Tensor> bias, bool fu
   p.cache_stride_block = k_cache.stride(0);
   p.cache_stride_head = k_cache.stride(1);
   p.cache_stride_tok = k_cache.stride(2);
-  check_rc(run_skinny(4, p, cur_stream(x)), "skinny_gemm_qkv");
+  check_rc(run_skinny_checked(4, p, cur_stream(x)), "skinny_gemm_qkv");
 }
 
 void rmsnorm(Tensor x, c10::optional<Tensor> residual, c10::optional<Tensor> residual_out, c10::optional<Tensor> w,
@@ -257,6 +274,8 @@ void decode_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_
   c10::DeviceGuard g(q.device());
   check_bf16(q, "q");
   TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && q.size(1) == n_q_heads * head_dim, "q shape");
+  TORCH_CHECK(q.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0,
+              "q rows must be 16-byte aligned (vector loads)");
   const int rows = (int)q.size(0);
   TORCH_CHECK(ctx_lens.scalar_type() == at::kInt && ctx_lens.numel() >= rows, "ctx_lens");
   TORCH_CHECK(seq_ids.scalar_type() == at::kInt && seq_ids.numel() >= rows, "seq_ids");
@@ -413,9 +432,14 @@ void conv1d_gelu(Tensor x, Tensor w, c10::optional<Tensor> b, c10::optional<Tens
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for the voice-web-agent inference engine";
-  m.def("skinny_gemm", &skinny_gemm);
-  m.def("skinny_gemm_swiglu", &skinny_gemm_swiglu);
-  m.def("skinny_gemm_qkv", &skinny_gemm_qkv);
+  m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
+        py::arg("fuse_rms"), py::arg("eps"), py::arg("residual"), py::arg("w_scale") = py::none());
+  m.def("skinny_gemm_swiglu", &skinny_gemm_swiglu, py::arg("x"), py::arg("w_gu"), py::arg("bias"), py::arg("h"),
+        py::arg("fuse_rms"), py::arg("eps"), py::arg("w_scale") = py::none());
+  m.def("skinny_gemm_qkv", &skinny_gemm_qkv, py::arg("x"), py::arg("w_qkv"), py::arg("bias"), py::arg("fuse_rms"),
+        py::arg("eps"), py::arg("n_q_heads"), py::arg("n_kv_heads"), py::arg("head_dim"), py::arg("use_rope"),
+        py::arg("positions"), py::arg("slots"), py::arg("rope"), py::arg("q_out"), py::arg("k_cache"),
+        py::arg("v_cache"), py::arg("w_scale") = py::none());
   m.def("rmsnorm", &rmsnorm);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);

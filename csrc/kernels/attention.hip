@@ -56,12 +56,6 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
   if (t0 >= ctx) return;  // split past this row's context (grid is sized for max_ctx)
   const int tend = min(ctx, t0 + kSplit);
 
-  for (int i = lane; i < G * D; i += 64) {
-    const int g = i / D, d = i % D;
-    qs[g][d] = bf2f(p.q[(int64_t)row * p.ldq + (kvh * G + g) * D + d]) * p.scale;
-  }
-  __syncthreads();
-
   // ---- Q.K (lane = key); the V chunk loads of the P.V phase are issued right after the K
   // loads (their addresses do not depend on the scores), so both HBM round trips overlap.
   constexpr int NCH = D / 8;        // 16-byte chunks per row
@@ -82,6 +76,15 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
     vv[i] = (tt < tend) ? *reinterpret_cast<const uint4*>(p.kv.v + kv_offset(p.kv, seq, kvh, tt) + c * 8)
                         : make_uint4(0, 0, 0, 0);
   }
+  // q staged after the K/V loads are in flight (its latency hides under theirs)
+  for (int i = lane * 8; i < G * D; i += 64 * 8) {
+    const int g = i / D, d = i % D;
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(p.q + (int64_t)row * p.ldq + (kvh * G + g) * D + d), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qs[g][d + j] = f[j] * p.scale;
+  }
+  __syncthreads();
   float s[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) s[g] = 0.f;

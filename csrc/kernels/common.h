@@ -77,6 +77,16 @@ VWA_DEVICE f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// OCP fp8 e4m3 (gfx950 MFMA/cvt format): 16x16x32 MFMA with 8 fp8 per lane per operand
+VWA_DEVICE f32x4 mfma16_fp8(long a, long b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
+}
+
+// two f32 -> two OCP e4m3 bytes (round to nearest even, saturating at +-448 via the caller's scale)
+VWA_DEVICE uint32_t cvt_pk_fp8(float a, float b) {
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xFFFFu;
+}
+
 VWA_DEVICE float silu(float x) { return x / (1.f + __expf(-x)); }
 
 VWA_DEVICE float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }

@@ -21,6 +21,7 @@ struct SkinnyParams {
   uint16_t* k_cache; uint16_t* v_cache;
   int block_size;
   int64_t cache_stride_block, cache_stride_head, cache_stride_tok;
+  const float* w_scale;  // non-null: W is OCP fp8 e4m3 [N, K] bytes with per-row scales (W8A8 path)
 };
 
 // Paged / strided KV addressing shared by the attention kernels:

@@ -104,3 +104,19 @@ def test_gpt2_gpu_engine_matches_cpu_reference():
     for i, (a, b) in enumerate(zip(got, ref)):
         err = (a - b).abs().max().item()
         assert err < 0.05 * (1 + b.abs().max().item()), (i, err)
+
+
+def test_llama_fp8_gpu_engine_matches_cpu_emulation():
+    """fp8 (W8A8) Llama through the fp8-MFMA decode GEMMs vs the CPU emulation of the same
+    quantisation (same quantised weights)."""
+    ops.ext()
+    torch.manual_seed(0)
+    toks = torch.randint(0, CFG.vocab_size, (140,)).tolist()
+    cpu = LlamaModel(CFG, device="cpu", seed=5, wdtype="fp8")
+    ref = _run(cpu, toks, 120)
+    gpu = LlamaModel(CFG, device="cpu", seed=5, wdtype="fp8")
+    move_model(gpu, "cuda")
+    got = _run(gpu, toks, 120)
+    for i, (a, b) in enumerate(zip(got, ref)):
+        err = (a - b).abs().max().item()
+        assert err < 0.08 * (1 + b.abs().max().item()), (i, err)

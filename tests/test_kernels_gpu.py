@@ -56,6 +56,21 @@ def test_skinny_store_resid_gelu(M, fuse_rms, skinny_mode):
         close(out, exp, 2e-2)
 
 
+@pytest.mark.parametrize("M", [3, 6, 16])
+def test_skinny_large_k_residual(M, skinny_mode):
+    """Down-projection shape (K = 14336): past 5 rows X no longer fits in LDS and the streaming
+    kernel reads X fragments from global memory (XG variant)."""
+    K, N = 14336, 512
+    x = rnd(M, K)
+    w = rnd(N, K, scale=0.02)
+    res = rnd(M, N)
+    out = torch.empty(M, N, dtype=BF, device=DEV)
+    ops.linear(x, w, out=out, residual=res)
+    exp = torch.empty(M, N, dtype=BF)
+    ref.linear(x.cpu(), w.cpu(), None, out=exp, residual=res.cpu())
+    close(out, exp, 3e-2)
+
+
 def test_skinny_f32_out_large_n_and_inplace_residual(skinny_mode):
     M, K, N = 3, 4096, 4096
     x = rnd(M, K)
@@ -268,3 +283,68 @@ def test_audio_frontend_and_conv():
     pos = rnd(1500, 384)
     z = ops.conv1d_gelu(y, rnd(384, 3 * 384, scale=0.02), b, stride=2, pos=pos)
     assert z.shape == (1, 1500, 384)
+
+
+# ----------------------------------------------------------------------------- fp8 (W8A8)
+def _fp8_cpu(w8: "ops.FP8Weight") -> "ops.FP8Weight":
+    return w8.to("cpu")
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 40])
+def test_fp8_linear_epilogues(M):
+    """OCP e4m3 weights x per-row-quantised activations on the fp8 MFMA (decode rows <= 16) or the
+    large-M fp8 path, against the CPU emulation of the same W8A8 rounding."""
+    K, N = 1024, 384
+    x = rnd(M, K)
+    w8 = ops.FP8Weight.quantize(rnd(N, K, scale=0.05))
+    b = rnd(N, scale=0.1)
+    for act, res, rms, odt in (("none", None, False, BF), ("none", rnd(M, N), True, BF), ("gelu", None, False, BF),
+                               ("none", None, True, torch.float32)):
+        out = torch.empty(M, N, dtype=odt, device=DEV)
+        ops.linear(x, w8, b if act == "gelu" else None, out=out, residual=res, act=act, fuse_rms=rms, eps=1e-5)
+        exp = torch.empty(M, N, dtype=odt)
+        ops.linear(x.cpu(), _fp8_cpu(w8), b.cpu() if act == "gelu" else None, out=exp,
+                   residual=None if res is None else res.cpu(), act=act, fuse_rms=rms, eps=1e-5)
+        close(out, exp, 3e-2)
+
+
+def test_fp8_large_k_and_swiglu():
+    M, K, F = 8, 4096, 512
+    x = rnd(M, K)
+    wgu = ops.FP8Weight.quantize(ops.interleave_gate_up(rnd(F, K, scale=0.02), rnd(F, K, scale=0.02)))
+    out = ops.linear_swiglu(x, wgu, fuse_rms=True, eps=1e-5)
+    exp = torch.empty(M, F, dtype=BF)
+    ops.linear_swiglu(x.cpu(), _fp8_cpu(wgu), fuse_rms=True, eps=1e-5, out=exp)
+    close(out, exp, 3e-2)
+    # down-projection shape: K = 14336 fits the fp8 LDS staging up to 10 rows
+    xd = rnd(6, 14336)
+    wd = ops.FP8Weight.quantize(rnd(256, 14336, scale=0.02))
+    res = rnd(6, 256)
+    o = torch.empty(6, 256, dtype=BF, device=DEV)
+    ops.linear(xd, wd, out=o, residual=res)
+    e = torch.empty(6, 256, dtype=BF)
+    ops.linear(xd.cpu(), _fp8_cpu(wd), out=e, residual=res.cpu())
+    close(o, e, 3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 9])
+def test_fp8_qkv_rope_write(M):
+    nq, nkv, hd, K = 8, 2, 128, 512
+    H = nq + 2 * nkv
+    w8 = ops.FP8Weight.quantize(ops.permute_qkv_rows(rnd(H * hd, K, scale=0.05), H, hd))
+    x = rnd(M, K)
+    rope = ops.rope_table(256, hd, 500000.0, device=DEV)
+    pos = torch.randint(0, 200, (M,), dtype=torch.int32, device=DEV)
+    slots = torch.randperm(16 * 16, device=DEV)[:M].to(torch.int64)
+    kc, vc = _kv_setup(nq, nkv, hd)
+    q = torch.zeros(M, nq * hd, dtype=BF, device=DEV)
+    ops.qkv_rope_write(x, w8, None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd, rope=rope,
+                       positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc)
+    kc2, vc2 = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q2 = torch.zeros(M, nq * hd, dtype=BF)
+    ops.qkv_rope_write(x.cpu(), _fp8_cpu(w8), None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv,
+                       head_dim=hd, rope=rope.cpu(), positions=pos.cpu(), slots=slots.cpu(), q_out=q2, k_cache=kc2,
+                       v_cache=vc2)
+    close(q, q2, 3e-2)
+    close(kc, kc2, 3e-2)
+    close(vc, vc2, 3e-2)

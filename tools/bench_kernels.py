@@ -41,7 +41,7 @@ def timeit(fn, iters=40, reps=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
-    ap.add_argument("--only", default="gemm,attn,flash", help="comma list of gemm,attn,flash")
+    ap.add_argument("--only", default="gemm,attn,flash", help="comma list of gemm,attn,flash,mall")
     args = ap.parse_args()
     only = set(args.only.split(","))
     dev = "cuda"
@@ -82,6 +82,35 @@ def main():
                      hipblaslt_tbps=round(gb / (t_blas * 1e-6) / 1e3, 3))
             print(json.dumps(r), flush=True)
             res.append(r)
+    # Infinity-Cache (MALL) experiment: GEMM time when its weights were read by the previous
+    # kernel (prefetched into the 256 MB memory-side cache) vs cold
+    for name, N, K in (shapes[1:3] if "mall" in only else ()):
+        M = 1
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        ncopy = max(1, int(1.0e9 // (N * K * 2)) + 1)
+        ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(ncopy)]
+        y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        acc = torch.empty((), device=dev, dtype=torch.int64)
+        it = [0]
+
+        def pf():
+            it[0] = (it[0] + 1) % ncopy
+            torch.sum(ws[it[0]].view(torch.int32), dim=(0, 1), out=acc)
+
+        def pf_gemm():
+            pf()
+            ops.ext().skinny_gemm(x, ws[it[0]], None, y, 0, False, 1e-5, None)
+
+        def cold():
+            it[0] = (it[0] + 1) % ncopy
+            ops.ext().skinny_gemm(x, ws[it[0]], None, y, 0, False, 1e-5, None)
+
+        t_pf, t_both, t_cold = timeit(pf), timeit(pf_gemm), timeit(cold)
+        r = dict(kernel="mall_prefetch", shape=name, N=N, K=K, cold_us=round(t_cold, 2),
+                 after_prefetch_us=round(t_both - t_pf, 2), prefetch_us=round(t_pf, 2))
+        print(json.dumps(r), flush=True)
+        res.append(r)
+        del ws
     # decode attention, Llama-3-8B geometry, ctx 1200
     nq, nkv, hd, bs = 32, 8, 128, 16
     for rows, ctx in (((1, 1200), (8, 1200), (32, 1200)) if "attn" in only else ()):

@@ -111,13 +111,16 @@ def make_engine_from_env():
 
 def build_llm_engine(model_name: Optional[str] = None, device: Optional[str] = None):
     """Intent LLM from env: VWA_LLM_MODEL (llama3-8b | llama3-70b | llama3.2-1b | llama-tiny |
-    gpt2-small | gpt2-tiny), VWA_TP, VWA_MAX_SESSIONS, VWA_BUDGET_CHARS, VWA_SEED.  GPT-2 is the
+    gpt2-small | gpt2-tiny), VWA_LLM_WEIGHTS (safetensors dir; random init if unset), VWA_DTYPE
+    (bf16 | fp8 weights for Llama), VWA_TP,
+    VWA_MAX_SESSIONS, VWA_BUDGET_CHARS, VWA_SEED.  GPT-2 is the
     CPU config (BASELINE.json config 1): plain-text prompt layout, GPT-2 vocabulary."""
     import torch
 
     from ..models.config import GPT2Config, get_config
     from ..parallel.tp import init_distributed
     from ..runtime.engine import LLMEngine
+    from ..runtime.weights import load_llm
     from ..tokenizer import load_tokenizer
     from .intent_engine import LLMIntentEngine
     from .prompt import llama3_chat, plain_chat
@@ -128,17 +131,15 @@ def build_llm_engine(model_name: Optional[str] = None, device: Optional[str] = N
     dev = device or ("cuda" if torch.cuda.is_available() else "cpu")
     sessions = int(os.environ.get("VWA_MAX_SESSIONS", "8"))
     budget = int(os.environ.get("VWA_BUDGET_CHARS", "512"))
+    wpath = os.environ.get("VWA_LLM_WEIGHTS") or None  # safetensors checkpoint (HF names)
     if isinstance(cfg, GPT2Config):
-        from ..models.gpt2 import GPT2Model
-
-        model = GPT2Model(cfg, device=dev, seed=seed)
+        model = load_llm(name, device=dev, seed=seed, weights_path=wpath)
         eng = LLMEngine(model, max_seqs=sessions, max_model_len=cfg.max_pos)
         eng.capture_all()
         return LLMIntentEngine(eng, load_tokenizer("gpt2"), budget_chars=budget, chat_format=plain_chat)
-    from ..models.llama import LlamaModel
-
     tp = init_distributed(tp_size=int(os.environ.get("VWA_TP", "1") or 1))
-    model = LlamaModel(cfg, device=dev, tp=tp, seed=seed)
+    model = load_llm(name, device=dev, tp=tp, seed=seed, weights_path=wpath,
+                     wdtype=os.environ.get("VWA_DTYPE", "bf16"))
     eng = LLMEngine(model, max_seqs=sessions, max_model_len=4096)
     eng.capture_all()
     ie = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=budget, chat_format=llama3_chat)

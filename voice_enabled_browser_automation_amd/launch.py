@@ -6,7 +6,8 @@ processes, like ``pnpm dev`` in each app of the reference (README.md:83-97).
 
 GPU placement on one node: the brain (LLM) and the voice service (ASR) each pin their own
 GPU via HIP_VISIBLE_DEVICES (VWA_BRAIN_GPUS / VWA_VOICE_GPUS, default "0"); with VWA_TP>1 the
-brain is launched through torch.distributed.run with one process per GPU.
+brain is launched through torch.distributed.run with one process per GPU.  A comma list in
+VWA_VOICE_GPUS (e.g. "4,5,6,7") starts one voice worker per GPU behind the session router.
 """
 from __future__ import annotations
 
@@ -32,12 +33,17 @@ def _spawn(module: str, env_extra: dict, torchrun_nproc: int = 0) -> subprocess.
 
 def main():
     tp = int(os.environ.get("VWA_TP", "1") or 1)
-    procs = [
-        _spawn(f"{PKG}.brain.server", {"HIP_VISIBLE_DEVICES": os.environ.get("VWA_BRAIN_GPUS", "0")}, tp),
-        _spawn(f"{PKG}.voice.server", {"HIP_VISIBLE_DEVICES": os.environ.get("VWA_VOICE_GPUS", "0")}),
-        _spawn(f"{PKG}.executor.server", {}),
-        _spawn(f"{PKG}.web.server", {}),
-    ]
+    voice_gpus = [g for g in os.environ.get("VWA_VOICE_GPUS", "0").split(",") if g.strip()]
+    procs = [_spawn(f"{PKG}.brain.server", {"HIP_VISIBLE_DEVICES": os.environ.get("VWA_BRAIN_GPUS", "0")}, tp)]
+    if len(voice_gpus) > 1:
+        # ASR session-DP: one voice worker per GPU behind the router on VOICE_PORT (voice/router.py)
+        base = int(os.environ.get("VWA_VOICE_BASE_PORT", "7100"))
+        for i, g in enumerate(voice_gpus):
+            procs.append(_spawn(f"{PKG}.voice.server", {"HIP_VISIBLE_DEVICES": g, "VOICE_PORT": str(base + i)}))
+        procs.append(_spawn(f"{PKG}.voice.router", {"VWA_DP": str(len(voice_gpus))}))
+    else:
+        procs.append(_spawn(f"{PKG}.voice.server", {"HIP_VISIBLE_DEVICES": voice_gpus[0] if voice_gpus else "0"}))
+    procs += [_spawn(f"{PKG}.executor.server", {}), _spawn(f"{PKG}.web.server", {})]
 
     def stop(*_a):
         for p in procs:

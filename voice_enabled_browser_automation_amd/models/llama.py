@@ -44,8 +44,11 @@ def _randn(gen: torch.Generator, shape, std: float, device, dtype) -> torch.Tens
 
 class LlamaModel:
     def __init__(self, cfg: LlamaConfig, *, device="cpu", dtype=torch.bfloat16, tp: Optional[TPContext] = None,
-                 seed: int = 0, weights: Optional[dict] = None):
+                 seed: int = 0, weights: Optional[dict] = None, wdtype: str = "bf16"):
+        """wdtype: "bf16", or "fp8" (OCP e4m3 projection + LM-head weights with per-row scales,
+        W8A8 decode GEMMs on the fp8 MFMA; embeddings, norms and the KV cache stay bf16)."""
         self.cfg = cfg
+        self.wdtype = wdtype
         self.device = torch.device(device)
         self.dtype = dtype
         self.tp = tp or TPContext.single()
@@ -66,6 +69,18 @@ class LlamaModel:
             self._load(weights)
         else:
             self._init_random(seed)
+        if wdtype == "fp8":
+            self._quantize_fp8()
+        elif wdtype != "bf16":
+            raise ValueError(f"unsupported weight dtype {wdtype!r} (bf16 | fp8)")
+
+    def _quantize_fp8(self) -> None:
+        q = ops.FP8Weight.quantize
+        for L in self.layers:
+            L.qkv, L.o, L.gu, L.down = q(L.qkv), q(L.o), q(L.gu), q(L.down)
+        self.lm_head = q(self.lm_head)
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
 
     # ------------------------------------------------------------------ weights
     def _shard_layer(self, q, k, v, o, g, u, dn, in_norm, post_norm):
@@ -128,10 +143,9 @@ class LlamaModel:
         self.lm_head = ops.fold_norm(lm[self.v_start : self.v_end], get("model.norm.weight")).contiguous()
 
     def weight_bytes(self) -> int:
-        n = self.embed.numel() + self.lm_head.numel()
-        for L in self.layers:
-            n += L.qkv.numel() + L.o.numel() + L.gu.numel() + L.down.numel()
-        return n * self.embed.element_size()
+        """Bytes streamed per decode step (projections + LM head; one embedding row is noise)."""
+        ts = [self.lm_head] + [t for L in self.layers for t in (L.qkv, L.o, L.gu, L.down)]
+        return sum(t.numel() * t.element_size() for t in ts)
 
     # ------------------------------------------------------------------ forward
     def _row_parallel(self, x: torch.Tensor, w: torch.Tensor, h: torch.Tensor):
@@ -200,7 +214,7 @@ def move_model(model, device) -> None:
     device = torch.device(device)
 
     def mv(obj):
-        if isinstance(obj, torch.Tensor):
+        if isinstance(obj, (torch.Tensor, ops.FP8Weight)):
             return obj.to(device)
         if dataclasses.is_dataclass(obj) and not isinstance(obj, type):
             for f in dataclasses.fields(obj):

@@ -58,7 +58,8 @@ class DecLayer:
 
 
 class WhisperModel:
-    def __init__(self, cfg: WhisperConfig, *, device="cpu", dtype=torch.bfloat16, seed: int = 0):
+    def __init__(self, cfg: WhisperConfig, *, device="cpu", dtype=torch.bfloat16, seed: int = 0,
+                 weights=None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
@@ -103,6 +104,8 @@ class WhisperModel:
                                      rn(d, s=0.01), ones(d), zeros(d), rn(F, d), rn(F, s=0.01), rn(d, F),
                                      rn(d, s=0.01)))
         self.dec_ln_w, self.dec_ln_b = ones(d), zeros(d)
+        if weights is not None:
+            self._load(weights)
         # tied LM head padded to a multiple of 16 rows (MFMA column tile); padded ids are masked
         vp = (cfg.vocab_size + 15) // 16 * 16
         self.vocab_padded = vp
@@ -112,6 +115,55 @@ class WhisperModel:
         self.window = torch.hann_window(400, periodic=True, device=self.device)
         self.cos_table = torch.cos(torch.arange(400, dtype=torch.float64) * 2 * math.pi / 400).float().to(self.device)
         self.mel_fb = ref.mel_filterbank(n_mels=cfg.n_mels).to(self.device)
+
+    def _load(self, w) -> None:
+        """HF WhisperForConditionalGeneration names (safetensors, runtime.weights.LazySafetensors)."""
+        cfg, dev, dt = self.cfg, self.device, self.dtype
+        d, H = cfg.d_model, self.H
+        g = lambda n: w[n].to(device=dev, dtype=dt)  # noqa: E731
+
+        def conv(n):  # [Cout, Cin, 3] -> [Cout, 3*Cin] in (kk, ci) order
+            t = g(n)
+            return t.permute(0, 2, 1).reshape(t.shape[0], -1).contiguous()
+
+        def qkv(pre):
+            wq, wk, wv = g(pre + "q_proj.weight"), g(pre + "k_proj.weight"), g(pre + "v_proj.weight")
+            bq, bv = g(pre + "q_proj.bias"), g(pre + "v_proj.bias")
+            return torch.cat([wq, wk, wv]), torch.cat([bq, torch.zeros_like(bq), bv])
+
+        e, dd = "model.encoder.", "model.decoder."
+        self.conv1_w, self.conv1_b = conv(e + "conv1.weight"), g(e + "conv1.bias")
+        self.conv2_w, self.conv2_b = conv(e + "conv2.weight"), g(e + "conv2.bias")
+        if e + "embed_positions.weight" in w:
+            self.pos_enc = g(e + "embed_positions.weight")
+        self.enc = []
+        for i in range(cfg.n_enc_layers):
+            p = f"{e}layers.{i}."
+            wqkv, bqkv = qkv(p + "self_attn.")
+            self.enc.append(EncLayer(
+                g(p + "self_attn_layer_norm.weight"), g(p + "self_attn_layer_norm.bias"), wqkv, bqkv,
+                g(p + "self_attn.out_proj.weight"), g(p + "self_attn.out_proj.bias"), g(p + "final_layer_norm.weight"),
+                g(p + "final_layer_norm.bias"), g(p + "fc1.weight"), g(p + "fc1.bias"), g(p + "fc2.weight"),
+                g(p + "fc2.bias")))
+        self.enc_ln_w, self.enc_ln_b = g(e + "layer_norm.weight"), g(e + "layer_norm.bias")
+        self.tok_emb = g(dd + "embed_tokens.weight")
+        self.pos_emb = g(dd + "embed_positions.weight")
+        self.dec = []
+        for i in range(cfg.n_dec_layers):
+            p = f"{dd}layers.{i}."
+            wqkv, bqkv = qkv(p + "self_attn.")
+            x = p + "encoder_attn."
+            self.dec.append(DecLayer(
+                g(p + "self_attn_layer_norm.weight"), g(p + "self_attn_layer_norm.bias"),
+                ops.permute_qkv_rows(wqkv, 3 * H, self.hd),
+                ops.permute_qkv_rows(bqkv[:, None], 3 * H, self.hd)[:, 0].contiguous(),
+                g(p + "self_attn.out_proj.weight"), g(p + "self_attn.out_proj.bias"),
+                g(p + "encoder_attn_layer_norm.weight"), g(p + "encoder_attn_layer_norm.bias"),
+                g(x + "q_proj.weight"), g(x + "q_proj.bias"), g(x + "k_proj.weight"), g(x + "v_proj.weight"),
+                g(x + "v_proj.bias"), g(x + "out_proj.weight"), g(x + "out_proj.bias"),
+                g(p + "final_layer_norm.weight"), g(p + "final_layer_norm.bias"), g(p + "fc1.weight"),
+                g(p + "fc1.bias"), g(p + "fc2.weight"), g(p + "fc2.bias")))
+        self.dec_ln_w, self.dec_ln_b = g(dd + "layer_norm.weight"), g(dd + "layer_norm.bias")
 
     # ------------------------------------------------------------------ encoder
     def log_mel(self, audio: torch.Tensor, n_frames: int = 3000) -> torch.Tensor:

@@ -62,6 +62,96 @@ def _gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+# ----------------------------------------------------------------------------- fp8 weights
+FP8_MAX = 448.0  # OCP e4m3fn
+
+
+class FP8Weight:
+    """OCP e4m3 weight [N, K] with a per-output-row f32 scale (VWA_DTYPE=fp8).
+
+    Decode GEMMs (<= 16 rows) run the W8A8 streaming kernel: activations are quantised per row
+    on the fly (dynamic amax/448 scale) and multiplied on the fp8 MFMA.  Larger row counts
+    (prefill chunks) use hipBLASLt's fp8 GEMM with row-wise scales when the torch build exposes
+    it, else dequantise.  The CPU reference emulates the same W8A8 rounding.
+    """
+
+    __slots__ = ("w8", "scale")
+
+    def __init__(self, w8: torch.Tensor, scale: torch.Tensor):
+        self.w8, self.scale = w8, scale
+
+    @staticmethod
+    def quantize(w: torch.Tensor) -> "FP8Weight":
+        wf = w.float()
+        scale = (wf.abs().amax(dim=1) / FP8_MAX).clamp_min(1e-12)
+        w8 = (wf / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+        return FP8Weight(w8.contiguous(), scale.contiguous())
+
+    def dequant(self, dtype=torch.float32) -> torch.Tensor:
+        return (self.w8.float() * self.scale[:, None]).to(dtype)
+
+    @property
+    def shape(self):
+        return self.w8.shape
+
+    @property
+    def device(self):
+        return self.w8.device
+
+    def numel(self) -> int:
+        return self.w8.numel()
+
+    def element_size(self) -> int:
+        return 1
+
+    def to(self, device) -> "FP8Weight":
+        return FP8Weight(self.w8.to(device), self.scale.to(device))
+
+
+def quant_rows_fp8(x: torch.Tensor) -> torch.Tensor:
+    """Per-row dynamic e4m3 quantise -> dequantise (f32), the activation rounding of the W8A8 path."""
+    xf = x.float()
+    s = (xf.abs().amax(dim=1, keepdim=True) / FP8_MAX)
+    s = torch.where(s > 0, s, torch.ones_like(s))
+    return (xf / s).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).float() * s
+
+
+def _ref_w8(x: torch.Tensor, w, fuse_rms: bool, eps: float):
+    """(x, w) for the torch reference: W8A8 emulation when w is fp8 (rms from the unquantised x)."""
+    if not isinstance(w, FP8Weight):
+        return x, w, fuse_rms
+    xf = x.float()
+    if fuse_rms:
+        xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+        # the kernel applies 1/rms after the product; quantising x or x/rms gives the same codes
+    return quant_rows_fp8(xf), w.dequant(), False
+
+
+def _fp8_stream_fits(M: int, K: int, nt: int = 1) -> bool:
+    ks = 8
+    return M <= 16 and M * (K + 16) + (ks * nt * 4 * 64 + 32) * 4 <= 160 * 1024
+
+
+_SCALED_MM_OK: Optional[bool] = None
+
+
+def _fp8_matmul(x: torch.Tensor, w: "FP8Weight") -> torch.Tensor:
+    """x [M, K] bf16 @ W8^T for large M: hipBLASLt fp8 GEMM with row-wise scales, or dequantise."""
+    global _SCALED_MM_OK
+    if _SCALED_MM_OK is not False and hasattr(torch, "_scaled_mm"):
+        try:
+            xf = x.float()
+            sx = (xf.abs().amax(dim=1, keepdim=True) / FP8_MAX).clamp_min(1e-12)
+            x8 = (xf / sx).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
+            y = torch._scaled_mm(x8, w.w8.t(), scale_a=sx, scale_b=w.scale[None, :].contiguous(),
+                                 out_dtype=torch.bfloat16)
+            _SCALED_MM_OK = True
+            return y
+        except (RuntimeError, TypeError):
+            _SCALED_MM_OK = False
+    return torch.matmul(x, w.dequant(x.dtype).t())
+
+
 # ----------------------------------------------------------------------------- layout helpers
 def qkv_row_perm(head_dim: int) -> torch.Tensor:
     half = head_dim // 2
@@ -131,17 +221,23 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if out is None:
         out = torch.empty((M, w.shape[0]), dtype=dt, device=x.device)
     if not _gpu(x):
-        return ref.linear(x, w, bias, out=out, residual=residual, act=act, fuse_rms=fuse_rms, eps=eps)
+        xr, wr, fr = _ref_w8(x, w, fuse_rms, eps)
+        return ref.linear(xr, wr, bias, out=out, residual=residual, act=act, fuse_rms=fr, eps=eps)
     E = ext()
-    if M <= SKINNY_MAX_M and x.shape[1] % 128 == 0:
+    fp8 = isinstance(w, FP8Weight)
+    if (M <= SKINNY_MAX_M and x.shape[1] % 128 == 0 and w.shape[0] % 16 == 0
+            and (not fp8 or _fp8_stream_fits(M, x.shape[1]))):
         epi = {"none": 0, "gelu": 3}[act]
         if residual is not None:
             assert act == "none"
             epi = 1
-        E.skinny_gemm(x, w, bias, out, epi, fuse_rms, eps, residual)
+        if fp8:
+            E.skinny_gemm(x, w.w8, bias, out, epi, fuse_rms, eps, residual, w.scale)
+        else:
+            E.skinny_gemm(x, w, bias, out, epi, fuse_rms, eps, residual)
         return out
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
-    y = torch.matmul(xin, w.t())
+    y = _fp8_matmul(xin, w) if fp8 else torch.matmul(xin, w.t())
     if bias is not None or act != "none" or residual is not None:
         if y.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and y.shape[1] % 8 == 0:
             E.bias_act(y, bias, residual, out, 1 if act == "gelu" else 0)
@@ -164,13 +260,18 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
     if out is None:
         out = torch.empty((M, F), dtype=x.dtype, device=x.device)
     if not _gpu(x):
-        return ref.linear_swiglu(x, w_gu, fuse_rms=fuse_rms, eps=eps, out=out)
+        xr, wr, fr = _ref_w8(x, w_gu, fuse_rms, eps)
+        return ref.linear_swiglu(xr, wr, fuse_rms=fr, eps=eps, out=out)
     E = ext()
-    if M <= SKINNY_MAX_M:
-        E.skinny_gemm_swiglu(x, w_gu, None, out, fuse_rms, eps)
+    fp8 = isinstance(w_gu, FP8Weight)
+    if M <= SKINNY_MAX_M and (not fp8 or _fp8_stream_fits(M, x.shape[1], nt=2)):
+        if fp8:
+            E.skinny_gemm_swiglu(x, w_gu.w8, None, out, fuse_rms, eps, w_gu.scale)
+        else:
+            E.skinny_gemm_swiglu(x, w_gu, None, out, fuse_rms, eps)
         return out
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
-    gu = torch.matmul(xin, w_gu.t())
+    gu = _fp8_matmul(xin, w_gu) if fp8 else torch.matmul(xin, w_gu.t())
     E.swiglu(gu, out)
     return out
 
@@ -182,18 +283,24 @@ def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Te
     """Fused QKV projection + rotary + paged KV write. Returns q_out[:M] (natural layout)."""
     M = x.shape[0]
     if not _gpu(x):
+        x, w_qkv, fuse_rms = _ref_w8(x, w_qkv, fuse_rms, eps)
         ref.qkv_rope_write(x, w_qkv, bias, fuse_rms=fuse_rms, eps=eps, n_q_heads=n_q_heads, n_kv_heads=n_kv_heads,
                            head_dim=head_dim, rope=rope, positions=positions, slots=slots, q_out=q_out,
                            k_cache=k_cache, v_cache=v_cache)
         return q_out[:M]
     E = ext()
     use_rope = rope is not None
-    if M <= SKINNY_MAX_M:
-        E.skinny_gemm_qkv(x, w_qkv, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, use_rope, positions, slots,
-                          rope, q_out, k_cache, v_cache)
+    fp8 = isinstance(w_qkv, FP8Weight)
+    if M <= SKINNY_MAX_M and (not fp8 or _fp8_stream_fits(M, x.shape[1])):
+        if fp8:
+            E.skinny_gemm_qkv(x, w_qkv.w8, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, use_rope, positions,
+                              slots, rope, q_out, k_cache, v_cache, w_qkv.scale)
+        else:
+            E.skinny_gemm_qkv(x, w_qkv, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, use_rope, positions,
+                              slots, rope, q_out, k_cache, v_cache)
         return q_out[:M]
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
-    qkv = torch.matmul(xin, w_qkv.t())
+    qkv = _fp8_matmul(xin, w_qkv) if fp8 else torch.matmul(xin, w_qkv.t())
     if bias is not None:
         qkv = qkv + bias
     E.rope_kv_write(qkv, n_q_heads, n_kv_heads, head_dim, use_rope, positions, slots, rope, q_out, k_cache, v_cache)

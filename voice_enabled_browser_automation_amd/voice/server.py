@@ -215,7 +215,12 @@ def asr_factory_from_env() -> Optional[Callable[[], Any]]:
 
     name = os.environ.get("VWA_ASR_MODEL", "whisper-tiny")
     dev = "cuda" if torch.cuda.is_available() else "cpu"
-    eng = AsrEngine(WhisperModel(get_config(name), device=dev), load_tokenizer("whisper"),
+    wpath = os.environ.get("VWA_ASR_WEIGHTS")
+    if wpath:
+        from ..runtime.weights import LazySafetensors
+
+    model = WhisperModel(get_config(name), device=dev, weights=LazySafetensors(wpath) if wpath else None)
+    eng = AsrEngine(model, load_tokenizer("whisper"),
                     max_sessions=int(os.environ.get("VWA_MAX_SESSIONS", "4")))
     fn = make_asr_transcriber(eng)
     every = float(os.environ.get("VWA_PARTIAL_EVERY_S", "1.0"))
