@@ -430,7 +430,39 @@ void conv1d_gelu(Tensor x, Tensor w, c10::optional<Tensor> b, c10::optional<Tens
 
 }  // namespace
 
+// ---- one-shot all-reduce (opaque state handle as int64)
+int64_t ar_create(int64_t rank, int64_t world, int64_t max_elems) {
+  void* st = vwa_ar_create((int)rank, (int)world, max_elems);
+  TORCH_CHECK(st, "all-reduce buffer allocation failed (world <= 8, max_elems % 512 == 0)");
+  return reinterpret_cast<int64_t>(st);
+}
+Tensor ar_handles(int64_t st) {
+  Tensor t = torch::empty({vwa_ar_handle_bytes()}, torch::dtype(torch::kUInt8));
+  check_rc(vwa_ar_handles(reinterpret_cast<void*>(st), t.data_ptr()), "hipIpcGetMemHandle");
+  return t;
+}
+void ar_open_peer(int64_t st, int64_t p, Tensor h) {
+  TORCH_CHECK(h.scalar_type() == at::kByte && h.numel() == vwa_ar_handle_bytes() && !h.is_cuda(), "ipc handle bytes");
+  check_rc(vwa_ar_open_peer(reinterpret_cast<void*>(st), (int)p, h.contiguous().data_ptr()), "hipIpcOpenMemHandle");
+}
+void ar_allreduce(int64_t st, Tensor in, Tensor out) {
+  c10::DeviceGuard g(in.device());
+  check_bf16(in, "in");
+  check_bf16(out, "out");
+  TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel(), "contiguous, same size");
+  check_rc(vwa_ar_allreduce(reinterpret_cast<void*>(st), bfp(in), bfp_mut(out), in.numel(), cur_stream(in)),
+           "one-shot all-reduce");
+}
+int64_t ar_error(int64_t st) { return vwa_ar_error(reinterpret_cast<void*>(st)); }
+void ar_destroy(int64_t st) { vwa_ar_destroy(reinterpret_cast<void*>(st)); }
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("ar_create", &ar_create);
+  m.def("ar_handles", &ar_handles);
+  m.def("ar_open_peer", &ar_open_peer);
+  m.def("ar_allreduce", &ar_allreduce);
+  m.def("ar_error", &ar_error);
+  m.def("ar_destroy", &ar_destroy);
   m.doc() = "MI355X (gfx950) HIP kernels for the voice-web-agent inference engine";
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
         py::arg("fuse_rms"), py::arg("eps"), py::arg("residual"), py::arg("w_scale") = py::none());

@@ -1,0 +1,187 @@
+// One-shot peer-to-peer all-reduce for decode-sized tensor-parallel messages (SURVEY.md §2.8
+// C1/C2, §5.8).  RCCL's ring all-reduce pays 2(N-1) link hops of latency; a decode step's
+// row-parallel output is only M x d x 2 bytes (8 KiB per row for Llama-3-8B), so here every rank
+// reads all peers' inputs directly over its point-to-point xGMI links and reduces in registers:
+// one hop, one kernel, graph-capturable.
+//
+// The buffer is cut into kMaxBlocks fixed regions of max_elems/kMaxBlocks; workgroup b always
+// owns region b (every call launches all kMaxBlocks workgroups, idle ones just signal), so a
+// region's epoch advances exactly once per call on every rank whatever the message size.
+// Per call (epoch e, per workgroup b so no cross-workgroup ordering is needed):
+//   1. copy this workgroup's chunk of the input into our IPC-shared staging buffer [e & 1]
+//      (double-buffered by epoch parity, so call e+1 never overwrites what a slow peer may
+//      still be reading for call e);
+//   2. release (system-scope fence), then store flag[b][rank] = e into every peer's flag array;
+//   3. wait until our own flag[b][p] == e for every peer p (bounded spin: a missing peer
+//      raises an error word instead of hanging the GPU);
+//   4. acquire (system-scope fence) and sum the chunk of all ranks' staging buffers in rank
+//      order (bit-identical result on every rank) into the output.
+// Buffers come from hipMalloc and are shared with hipIpcGetMemHandle / hipIpcOpenMemHandle.
+#include "common.h"
+
+using namespace vwa;
+
+namespace {
+
+constexpr int kMaxRanks = 8;
+constexpr int kThreads = 512;
+constexpr int kMaxBlocks = 64;
+
+struct ArPeers {
+  uint16_t* staging[kMaxRanks];  // each rank's staging base (2 x max_elems bf16)
+  int* flags[kMaxRanks];         // each rank's flag array [kMaxBlocks][kMaxRanks]
+};
+
+__global__ __launch_bounds__(kThreads) void oneshot_ar_kernel(const uint16_t* __restrict__ in, uint16_t* out,
+                                                              int64_t n, int64_t max_elems,
+                                                              int rank, int world, ArPeers peers, int* epochs,
+                                                              int* error) {
+  const int b = blockIdx.x;
+  const int64_t chunk = max_elems / kMaxBlocks;
+  const int64_t lo = (int64_t)b * chunk, hi = min(n, lo + chunk);
+  __shared__ int s_epoch;
+  if (threadIdx.x == 0) s_epoch = epochs[b] + 1;
+  __syncthreads();
+  const int e = s_epoch;
+  uint16_t* mine = peers.staging[rank] + (int64_t)(e & 1) * max_elems;
+  // 1. stage (16-byte vectors; n is a multiple of 8)
+  for (int64_t i = lo + (int64_t)threadIdx.x * 8; i < hi; i += (int64_t)kThreads * 8)
+    *reinterpret_cast<uint4*>(mine + i) = *reinterpret_cast<const uint4*>(in + i);
+  __syncthreads();
+  // 2. release + signal every peer (flag slot [b][rank] lives in the peer's memory)
+  if (threadIdx.x < world) {
+    __threadfence_system();
+    __hip_atomic_store(peers.flags[threadIdx.x] + b * kMaxRanks + rank, e, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // 3. wait for every peer's signal in our own flag array (bounded)
+  if (threadIdx.x < world) {
+    int* f = peers.flags[rank] + b * kMaxRanks + threadIdx.x;
+    int64_t spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1ll << 24)) {  // ~seconds: a peer never arrived
+        atomicExch(error, 1);
+        break;
+      }
+    }
+    __threadfence_system();
+  }
+  __syncthreads();
+  // 4. reduce in rank order
+  for (int64_t i = lo + (int64_t)threadIdx.x * 8; i < hi; i += (int64_t)kThreads * 8) {
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    for (int p = 0; p < world; ++p) {
+      const uint16_t* src = peers.staging[p] + (int64_t)(e & 1) * max_elems + i;
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(src), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += f[j];
+    }
+    *reinterpret_cast<uint4*>(out + i) = pack8(acc);
+  }
+  if (threadIdx.x == 0) epochs[b] = e;
+}
+
+struct ArState {
+  int rank = 0, world = 1;
+  int64_t max_elems = 0;
+  uint16_t* staging = nullptr;  // local
+  int* flags = nullptr;         // local [kMaxBlocks][kMaxRanks]
+  int* epochs = nullptr;        // local, private [kMaxBlocks]
+  int* error = nullptr;
+  ArPeers peers{};
+  bool opened[kMaxRanks] = {};
+};
+
+}  // namespace
+
+extern "C" {
+
+// Allocate the local IPC-shareable buffers; returns an opaque state pointer (nullptr on error).
+void* vwa_ar_create(int rank, int world, int64_t max_elems) {
+  if (world < 1 || world > kMaxRanks || rank < 0 || rank >= world || max_elems % (8 * kMaxBlocks)) return nullptr;
+  auto* s = new ArState();
+  s->rank = rank;
+  s->world = world;
+  s->max_elems = max_elems;
+  if (hipMalloc(&s->staging, 2 * max_elems * sizeof(uint16_t)) != hipSuccess ||
+      hipMalloc(&s->flags, kMaxBlocks * kMaxRanks * sizeof(int)) != hipSuccess ||
+      hipMalloc(&s->epochs, kMaxBlocks * sizeof(int)) != hipSuccess || hipMalloc(&s->error, sizeof(int)) != hipSuccess) {
+    delete s;
+    return nullptr;
+  }
+  (void)hipMemset(s->flags, 0, kMaxBlocks * kMaxRanks * sizeof(int));
+  (void)hipMemset(s->epochs, 0, kMaxBlocks * sizeof(int));
+  (void)hipMemset(s->error, 0, sizeof(int));
+  (void)hipDeviceSynchronize();
+  s->peers.staging[rank] = s->staging;
+  s->peers.flags[rank] = s->flags;
+  return s;
+}
+
+// IPC handles of the local staging and flag buffers (2 x hipIpcMemHandle_t).
+int vwa_ar_handles(void* st, void* out128) {
+  auto* s = static_cast<ArState*>(st);
+  auto* h = static_cast<hipIpcMemHandle_t*>(out128);
+  if (hipIpcGetMemHandle(&h[0], s->staging) != hipSuccess) return -1;
+  if (hipIpcGetMemHandle(&h[1], s->flags) != hipSuccess) return -2;
+  return 0;
+}
+
+int vwa_ar_handle_bytes() { return (int)(2 * sizeof(hipIpcMemHandle_t)); }
+
+// Map peer p's buffers from its two IPC handles.
+int vwa_ar_open_peer(void* st, int p, const void* in128) {
+  auto* s = static_cast<ArState*>(st);
+  if (p == s->rank) return 0;
+  const auto* h = static_cast<const hipIpcMemHandle_t*>(in128);
+  void* a = nullptr;
+  void* f = nullptr;
+  if (hipIpcOpenMemHandle(&a, h[0], hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -1;
+  if (hipIpcOpenMemHandle(&f, h[1], hipIpcMemLazyEnablePeerAccess) != hipSuccess) return -2;
+  s->peers.staging[p] = static_cast<uint16_t*>(a);
+  s->peers.flags[p] = static_cast<int*>(f);
+  s->opened[p] = true;
+  return 0;
+}
+
+// In-place (in == out allowed) bf16 sum over the group.  n % 8 == 0, n <= max_elems.
+int vwa_ar_allreduce(void* st, const uint16_t* in, uint16_t* out, int64_t n, hipStream_t stream) {
+  auto* s = static_cast<ArState*>(st);
+  if (n % 8 || n > s->max_elems) return -1;
+  for (int p = 0; p < s->world; ++p)
+    if (!s->peers.staging[p] || !s->peers.flags[p]) return -2;
+  hipLaunchKernelGGL(oneshot_ar_kernel, dim3(kMaxBlocks), dim3(kThreads), 0, stream, in, out, n, s->max_elems,
+                     s->rank, s->world, s->peers, s->epochs, s->error);
+  return (int)hipGetLastError();
+}
+
+// Non-zero if a call timed out waiting for a peer (sticky).
+int vwa_ar_error(void* st) {
+  auto* s = static_cast<ArState*>(st);
+  int v = 0;
+  (void)hipMemcpy(&v, s->error, sizeof(int), hipMemcpyDeviceToHost);
+  return v;
+}
+
+void vwa_ar_destroy(void* st) {
+  auto* s = static_cast<ArState*>(st);
+  if (!s) return;
+  (void)hipDeviceSynchronize();
+  for (int p = 0; p < s->world; ++p) {
+    if (s->opened[p]) {
+      (void)hipIpcCloseMemHandle(s->peers.staging[p]);
+      (void)hipIpcCloseMemHandle(s->peers.flags[p]);
+    }
+  }
+  (void)hipFree(s->staging);
+  (void)hipFree(s->flags);
+  (void)hipFree(s->epochs);
+  (void)hipFree(s->error);
+  delete s;
+}
+
+}  // extern "C"

@@ -89,6 +89,14 @@ int vwa_log_mel(const float* audio, int n_samples, int n_frames, const float* wi
 int vwa_conv1d_gelu_pos(const uint16_t* x, const uint16_t* w, const uint16_t* b, const uint16_t* pos, uint16_t* y,
                         int B, int Cin, int Tin, int Cout, int Tout, int stride, hipStream_t st);
 int vwa_attention_split_tokens();
+// one-shot peer-to-peer all-reduce (allreduce.hip)
+void* vwa_ar_create(int rank, int world, int64_t max_elems);
+int vwa_ar_handles(void* st, void* out);
+int vwa_ar_handle_bytes();
+int vwa_ar_open_peer(void* st, int p, const void* in);
+int vwa_ar_allreduce(void* st, const uint16_t* in, uint16_t* out, int64_t n, hipStream_t stream);
+int vwa_ar_error(void* st);
+void vwa_ar_destroy(void* st);
 #ifdef __cplusplus
 }
 #endif

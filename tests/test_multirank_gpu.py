@@ -1,0 +1,39 @@
+"""Multi-process GPU checks (2 ranks sharing the test GPU): the one-shot IPC all-reduce kernel
+(eager and inside a replayed hipGraph) and tensor-parallel Llama (column/row-parallel kernels +
+one-shot all-reduce + vocab-parallel LM head) against TP=1.  Each runs under torchrun in a child
+process with its own timeout."""
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _torchrun(script, extra_env=None, timeout=240):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", **(extra_env or {}))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(_port()), os.path.join(ROOT, "tools", script)]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    return r.returncode, r.stdout + r.stderr
+
+
+def test_oneshot_allreduce_two_ranks():
+    rc, out = _torchrun("ar_check.py")
+    assert rc == 0 and "AR_CHECK PASS" in out, out[-3000:]
+
+
+def test_tensor_parallel_llama_two_ranks():
+    rc, out = _torchrun("tp_check.py", {"VWA_DIST_BACKEND": "gloo"})
+    assert rc == 0 and "TP_CHECK PASS" in out, out[-3000:]

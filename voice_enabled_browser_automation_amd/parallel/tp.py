@@ -31,14 +31,20 @@ class TPContext:
     group: Optional[object] = None
     dp_rank: int = 0
     dp_size: int = 1
+    custom_ar: Optional[object] = None  # parallel.custom_ar.OneShotAllReduce (GPU TP groups)
 
     @staticmethod
     def single() -> "TPContext":
         return TPContext()
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over the TP group: one-shot xGMI kernel for decode-sized bf16 messages,
+        RCCL otherwise."""
         if self.size > 1:
-            dist.all_reduce(t, group=self.group)
+            if self.custom_ar is not None and t.is_cuda and self.custom_ar.fits(t):
+                self.custom_ar(t)
+            else:
+                dist.all_reduce(t, group=self.group)
         return t
 
     def all_gather_vocab(self, local: torch.Tensor, vocab: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -84,4 +90,10 @@ def init_distributed(tp_size: Optional[int] = None, backend: Optional[str] = Non
     assert world % tp == 0, f"world {world} not divisible by tp {tp}"
     groups = [dist.new_group(list(range(s, s + tp))) for s in range(0, world, tp)]
     gi = rank // tp
-    return TPContext(rank=rank % tp, size=tp, group=groups[gi], dp_rank=gi, dp_size=world // tp)
+    ctx = TPContext(rank=rank % tp, size=tp, group=groups[gi], dp_rank=gi, dp_size=world // tp)
+    if tp > 1 and torch.cuda.is_available():
+        from .custom_ar import maybe_custom_ar
+
+        ctl = [dist.new_group(list(range(s, s + tp)), backend="gloo") for s in range(0, world, tp)]
+        ctx.custom_ar = maybe_custom_ar(ctx, ctl[gi])
+    return ctx
