@@ -270,7 +270,7 @@ KVView make_view(const Tensor& k, const Tensor& v, const Tensor& table, int64_t 
 void decode_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_size, int64_t sb, int64_t sh,
                       int64_t stok, Tensor ctx_lens, Tensor seq_ids, int64_t n_q_heads, int64_t n_kv_heads,
                       int64_t head_dim, double scale, int64_t n_splits, Tensor part_o, Tensor part_ml,
-                      Tensor out) {
+                      Tensor counters, Tensor out) {
   c10::DeviceGuard g(q.device());
   check_bf16(q, "q");
   TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && q.size(1) == n_q_heads * head_dim, "q shape");
@@ -287,7 +287,9 @@ void decode_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_
                 "part_o too small");
     TORCH_CHECK(part_ml.scalar_type() == at::kFloat && part_ml.numel() >= (int64_t)rows * n_splits * n_q_heads * 2,
                 "part_ml too small");
-    TORCH_CHECK(n_splits <= 256, "decode attention merges <= 256 splits (context <= 16384 tokens)");
+    TORCH_CHECK(n_splits <= 64, "decode attention merges <= 64 chunks (context <= 16384 tokens)");
+    TORCH_CHECK(counters.scalar_type() == at::kInt && counters.is_cuda() && counters.numel() >= rows * n_kv_heads,
+                "counters: int32 [rows * n_kv_heads], zero-initialised, left zero by the kernel");
   }
   DecodeAttnParams p{};
   p.q = bfp(q);
@@ -304,6 +306,7 @@ void decode_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_
   p.n_splits = (int)n_splits;
   p.part_o = part_o.data_ptr<float>();
   p.part_ml = part_ml.data_ptr<float>();
+  p.counters = counters.data_ptr<int>();
   p.out = bfp_mut(out);
   p.ldo = (int)out.stride(0);
   check_rc(vwa_decode_attention(&p, cur_stream(q)), "decode_attention");

@@ -2,13 +2,12 @@
 //
 // 1) decode_attention (K10, K7): one query row per (sequence | forced token), paged KV,
 //    GQA group of G q-heads per kv-head handled by one workgroup so each K/V byte is read
-//    once per group.  Split-K over the context (64 keys per single-wave workgroup; lane = key
-//    for Q.K, lane = (16-byte dim chunk, token group) for P.V), partials merged by
-//    attn_combine (log-sum-exp, one wave per (row, q head)).  Measured alternatives that lost
-//    to this second tiny launch (profiles/r1_kernel_microbench_v3.json, 1 row, ctx 1200):
-//    in-launch last-arriver merge with agent-scope release/acquire fences (28 us: the fences
-//    write back / invalidate the per-XCD L2 on every workgroup) and with relaxed agent-scope
-//    atomic partials (24 us) vs 14.4 us here.  The grid is sized for the maximum context so the launch
+//    once per group.  Split-K over the context in 256-key chunks (4 waves x 64 keys), the
+//    waves merged in LDS and the chunks merged in-launch by the last-arriving chunk through an
+//    sc1 (write-through) hand-off.  Measured history (1 row, ctx 1200, incl. launch gaps):
+//    64-key single-wave splits + separate combine launch 14.4 us; same with an agent-scope
+//    release/acquire fenced last-arriver merge 28 us (fences write back / invalidate the per-XCD
+//    L2 per workgroup); with per-float relaxed atomics and a head-serial merge 24 us.  The grid is sized for the maximum context so the launch
 //    shape is static under hipGraph capture; splits past a row's context exit early.
 //    Also serves Whisper cross-attention (contiguous encoder K/V expressed as one block).
 //
@@ -32,42 +31,67 @@ VWA_DEVICE int64_t kv_offset(const KVView& kv, int seq, int kvh, int t) {
   return (int64_t)blk * kv.stride_block + (int64_t)kvh * kv.stride_head + (int64_t)(t % kv.block_size) * kv.stride_tok;
 }
 
-constexpr int kSplit = 64;  // keys per decode workgroup (one wave)
+constexpr int kWaves = 4;              // waves per decode workgroup
+constexpr int kKeysPerWave = 64;
+constexpr int kSplit = kWaves * kKeysPerWave;  // keys per decode workgroup (chunk)
 
-// One wave per (row, kv head, 64-key split).  Q.K: lane = key, the key row streamed with
-// D/8 independent 16-byte loads.  P.V: lane = (16-byte dim chunk, token group), every V row
-// chunk is one 16-byte load, all issued before the first FMA; token groups are reduced with
-// two/three xor-shuffles.  No LDS round trip except the tiny q / p broadcast arrays.
+// sc1 (write-through / L2-bypassing) global accesses for the in-launch hand-off (guide G16 R1)
+VWA_DEVICE __amdgpu_buffer_rsrc_t rsrc_f32(float* p, int64_t n) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)(n * 4), 0x00020000);
+}
+VWA_DEVICE void st_sc1_f2(__amdgpu_buffer_rsrc_t r, int64_t idx, float a, float b) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, make_float2(a, b)), r, (int)(idx * 4), 0, 16);
+}
+VWA_DEVICE void st_sc1_f1(__amdgpu_buffer_rsrc_t r, int64_t idx, float a) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(a), r, (int)(idx * 4), 0, 16);
+}
+VWA_DEVICE float2 ld_sc1_f2(__amdgpu_buffer_rsrc_t r, int64_t idx) {
+  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)(idx * 4), 0, 16));
+}
+VWA_DEVICE float ld_sc1_f1(__amdgpu_buffer_rsrc_t r, int64_t idx) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(idx * 4), 0, 16));
+}
+
+// One 4-wave workgroup per (row, kv head, 256-key chunk); each wave owns 64 keys.
+//  Q.K: lane = key, the key row streamed with D/8 independent 16-byte loads (V loads issued
+//  right behind them: their addresses do not depend on the scores).  P.V: lane = (16-byte dim
+//  chunk, token group), token groups reduced with xor-shuffles.  The 4 waves' (m, l, o) are
+//  merged through LDS (wave w merges q-heads g = w, w+4, ...).  A row with one active chunk
+//  writes its output directly; otherwise each chunk publishes (m, l, o) with sc1 stores, draws a
+//  ticket, and the last-arriving chunk merges them with sc1 loads (no release/acquire fences,
+//  no second launch).  Tickets are reset by the last arriver (counters allocated zeroed).
 template <int D, int G>
-__global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
-  __shared__ __attribute__((aligned(16))) float qs[G][D];
-  __shared__ float sc[G][kSplit];
-
-  const int nkv = p.n_kv_heads;
-  const int row = blockIdx.x / nkv, kvh = blockIdx.x % nkv;
-  const int split = blockIdx.y;
-  const int ctx = p.ctx_lens[row];
-  const int seq = p.seq_ids[row];
-  const int t0 = split * kSplit;
-  const int lane = threadIdx.x;
-  const bool single = (p.n_splits == 1);
-  const int nq = p.n_q_heads;
-
-  if (t0 >= ctx) return;  // split past this row's context (grid is sized for max_ctx)
-  const int tend = min(ctx, t0 + kSplit);
-
-  // ---- Q.K (lane = key); the V chunk loads of the P.V phase are issued right after the K
-  // loads (their addresses do not depend on the scores), so both HBM round trips overlap.
+__global__ __launch_bounds__(kWaves * 64) void decode_attn_kernel(DecodeAttnParams p) {
   constexpr int NCH = D / 8;        // 16-byte chunks per row
   constexpr int TG = 64 / NCH;      // token groups
-  constexpr int NI = kSplit / TG;   // tokens per lane
+  constexpr int NI = kKeysPerWave / TG;  // tokens per lane in P.V
+  constexpr int DPL = D / 64;       // output dims per lane in the merges
+  __shared__ __attribute__((aligned(16))) float qs[G][D];
+  __shared__ float sc[kWaves][G][kKeysPerWave];
+  __shared__ float mlw[kWaves][G][2];
+  __shared__ __attribute__((aligned(16))) float ow[kWaves][G][D];
+  __shared__ float wts[kWaves][64];
+  __shared__ int s_last;
+
+  const int nkv = p.n_kv_heads, nq = p.n_q_heads;
+  const int row = blockIdx.x / nkv, kvh = blockIdx.x % nkv;
+  const int chunk = blockIdx.y;
+  const int ctx = p.ctx_lens[row];
+  const int seq = p.seq_ids[row];
+  if (chunk * kSplit >= ctx) return;  // chunk past this row's context (grid sized for max_ctx)
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int t0 = chunk * kSplit + w * kKeysPerWave;
+  const int tend = min(ctx, t0 + kKeysPerWave);  // t0 >= tend: this wave has no keys
+  const int nact = (ctx + kSplit - 1) / kSplit;  // active chunks of this row
+
+  // ---- issue K (lane = key) and V (lane = chunk c, token group tg) loads first
   const int c = lane % NCH, tg = lane / NCH;
   const int t = t0 + lane;
-  uint4 kv4[D / 8];
+  uint4 kv4[NCH];
   if (t < tend) {
     const uint4* kr = reinterpret_cast<const uint4*>(p.kv.k + kv_offset(p.kv, seq, kvh, t));
 #pragma unroll
-    for (int cc = 0; cc < D / 8; ++cc) kv4[cc] = kr[cc];
+    for (int cc = 0; cc < NCH; ++cc) kv4[cc] = kr[cc];
   }
   uint4 vv[NI];
 #pragma unroll
@@ -76,8 +100,8 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
     vv[i] = (tt < tend) ? *reinterpret_cast<const uint4*>(p.kv.v + kv_offset(p.kv, seq, kvh, tt) + c * 8)
                         : make_uint4(0, 0, 0, 0);
   }
-  // q staged after the K/V loads are in flight (its latency hides under theirs)
-  for (int i = lane * 8; i < G * D; i += 64 * 8) {
+  // q (scaled) into LDS while the K/V loads are in flight
+  for (int i = threadIdx.x * 8; i < G * D; i += kWaves * 64 * 8) {
     const int g = i / D, d = i % D;
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(p.q + (int64_t)row * p.ldq + (kvh * G + g) * D + d), f);
@@ -85,12 +109,14 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
     for (int j = 0; j < 8; ++j) qs[g][d + j] = f[j] * p.scale;
   }
   __syncthreads();
+
+  // ---- Q.K and the wave's softmax statistics
   float s[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) s[g] = 0.f;
   if (t < tend) {
 #pragma unroll
-    for (int cc = 0; cc < D / 8; ++cc) {
+    for (int cc = 0; cc < NCH; ++cc) {
       float kf[8];
       unpack8(kv4[cc], kf);
 #pragma unroll
@@ -102,19 +128,22 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
       }
     }
   }
-  float mrow[G], lrow[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const float v = (t < tend) ? s[g] : -INFINITY;
     const float m = wave_max(v);
     const float e = (t < tend) ? __expf(v - m) : 0.f;
-    lrow[g] = wave_sum(e);
-    mrow[g] = m;
-    sc[g][lane] = e;
+    const float l = wave_sum(e);
+    sc[w][g][lane] = e;
+    if (lane == 0) {
+      mlw[w][g][0] = m;  // -inf for a wave without keys
+      mlw[w][g][1] = l;
+    }
   }
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
 
-  // ---- P.V (lane = dim chunk c, token group tg; V already in registers)
+  // ---- P.V (V already in registers)
   float o[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g)
@@ -126,7 +155,7 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
     unpack8(vv[i], vf);
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const float pg = sc[g][tg + TG * i];
+      const float pg = sc[w][g][tg + TG * i];
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[g][j] += pg * vf[j];
     }
@@ -137,85 +166,102 @@ __global__ __launch_bounds__(64) void decode_attn_kernel(DecodeAttnParams p) {
     for (int g = 0; g < G; ++g)
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[g][j] += __shfl_xor(o[g][j], off, 64);
-
-  const int ns = (ctx + kSplit - 1) / kSplit;  // active splits of this row
-  if (single || ns == 1) {
-    if (tg == 0) {
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const int h = kvh * G + g;
-        const float inv = 1.f / lrow[g];
-        float ov[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ov[j] = o[g][j] * inv;
-        *reinterpret_cast<uint4*>(p.out + (int64_t)row * p.ldo + h * D + c * 8) = pack8(ov);
-      }
-    }
-    return;
-  }
   if (tg == 0) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const int h = kvh * G + g;
-      float* po = p.part_o + (((int64_t)row * p.n_splits + split) * nq + h) * D + c * 8;
-      *reinterpret_cast<float4*>(po) = make_float4(o[g][0], o[g][1], o[g][2], o[g][3]);
-      *reinterpret_cast<float4*>(po + 4) = make_float4(o[g][4], o[g][5], o[g][6], o[g][7]);
-      if (c == 0) {
-        float* pm = p.part_ml + (((int64_t)row * p.n_splits + split) * nq + h) * 2;
-        pm[0] = mrow[g];
-        pm[1] = lrow[g];
-      }
+      *reinterpret_cast<float4*>(&ow[w][g][c * 8]) = make_float4(o[g][0], o[g][1], o[g][2], o[g][3]);
+      *reinterpret_cast<float4*>(&ow[w][g][c * 8 + 4]) = make_float4(o[g][4], o[g][5], o[g][6], o[g][7]);
     }
   }
-}
-
-// One wave per (row, q-head): split statistics are loaded in parallel (lane = split), the
-// log-sum-exp weights go through LDS, then every lane sums its dims over the splits with
-// independent loads (no serial load->use chain).
-template <int D>
-__global__ __launch_bounds__(64) void attn_combine_kernel(DecodeAttnParams p) {
-  __shared__ float wts[256];
-  const int row = blockIdx.x / p.n_q_heads, h = blockIdx.x % p.n_q_heads;
-  const int lane = threadIdx.x;
-  const int ctx = p.ctx_lens[row];
-  const int ns = min(min(p.n_splits, (ctx + kSplit - 1) / kSplit), 256);
-  if (ns <= 1) return;  // single-split rows were written directly by decode_attn_kernel
-  const float* pm = p.part_ml + ((int64_t)row * p.n_splits * p.n_q_heads + h) * 2;
-  const int64_t sstride = (int64_t)p.n_q_heads * 2;
-  float mloc = -INFINITY;
-  for (int s = lane; s < ns; s += 64) mloc = fmaxf(mloc, pm[s * sstride]);
-  const float M = wave_max(mloc);
-  float lsum = 0.f;
-  for (int s = lane; s < ns; s += 64) {
-    const float m = pm[s * sstride];
-    const float f = (m == -INFINITY) ? 0.f : __expf(m - M);
-    wts[s] = f;
-    lsum += pm[s * sstride + 1] * f;
-  }
-  const float L = wave_sum(lsum);
   __syncthreads();
-  constexpr int DPL = D / 64;
-  float acc[DPL];
+
+  // ---- merge the 4 waves: wave w takes q-heads g = w, w + 4, ... (lane = DPL dims)
+  const __amdgpu_buffer_rsrc_t r_o = rsrc_f32(p.part_o, (int64_t)p.rows * p.n_splits * nq * D);
+  const __amdgpu_buffer_rsrc_t r_ml = rsrc_f32(p.part_ml, (int64_t)p.rows * p.n_splits * nq * 2);
+  for (int g = w; g < G; g += kWaves) {
+    const int h = kvh * G + g;
+    float M = -INFINITY;
 #pragma unroll
-  for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
-  const float* po = p.part_o + ((int64_t)row * p.n_splits * p.n_q_heads + h) * D + lane * DPL;
-  const int64_t ostride = (int64_t)p.n_q_heads * D;
-#pragma unroll 8
-  for (int s = 0; s < ns; ++s) {
-    const float f = wts[s];
+    for (int ww = 0; ww < kWaves; ++ww) M = fmaxf(M, mlw[ww][g][0]);
+    float L = 0.f, acc[DPL];
 #pragma unroll
-    for (int j = 0; j < DPL; ++j) acc[j] += po[s * ostride + j] * f;
+    for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < kWaves; ++ww) {
+      const float mw = mlw[ww][g][0];
+      const float f = (mw == -INFINITY) ? 0.f : __expf(mw - M);
+      L += mlw[ww][g][1] * f;
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) acc[j] += ow[ww][g][lane * DPL + j] * f;
+    }
+    if (nact == 1) {
+      const float inv = 1.f / L;
+#pragma unroll
+      for (int j = 0; j < DPL; ++j) p.out[(int64_t)row * p.ldo + h * D + lane * DPL + j] = f2bf(acc[j] * inv);
+    } else {
+      const int64_t base = ((int64_t)row * p.n_splits + chunk) * nq + h;
+      if constexpr (DPL == 2) st_sc1_f2(r_o, base * D + lane * 2, acc[0], acc[1]);
+      else st_sc1_f1(r_o, base * D + lane, acc[0]);
+      if (lane == 0) st_sc1_f2(r_ml, base * 2, M, L);
+    }
   }
-  const float inv = L > 0.f ? 1.f / L : 0.f;
+  if (nact == 1) return;
+
+  // ---- ticket: every storing wave drains its sc1 stores, then one lane counts this chunk in
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* cnt = p.counters + row * nkv + kvh;
+    const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (ticket == nact - 1);
+    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // only orders the sc1 loads after the ticket
+
+  // ---- last arriver: merge the nact chunks (lane = chunk for the statistics, lane = dims for o)
+  for (int g = w; g < G; g += kWaves) {
+    const int h = kvh * G + g;
+    const int64_t hb = (int64_t)row * p.n_splits * nq + h;
+    float mloc = -INFINITY, lloc = 0.f;
+    if (lane < nact) {
+      const float2 ml = ld_sc1_f2(r_ml, (hb + (int64_t)lane * nq) * 2);
+      mloc = ml.x;
+      lloc = ml.y;
+    }
+    const float M = wave_max(mloc);
+    const float f = (lane < nact) ? __expf(mloc - M) : 0.f;
+    const float L = wave_sum(lloc * f);
+    wts[w][lane] = f;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    float acc[DPL];
 #pragma unroll
-  for (int j = 0; j < DPL; ++j) p.out[(int64_t)row * p.ldo + h * D + lane * DPL + j] = f2bf(acc[j] * inv);
+    for (int j = 0; j < DPL; ++j) acc[j] = 0.f;
+    for (int sp = 0; sp < nact; ++sp) {
+      const float wt = wts[w][sp];
+      const int64_t idx = (hb + (int64_t)sp * nq) * D + lane * DPL;
+      if constexpr (DPL == 2) {
+        const float2 v = ld_sc1_f2(r_o, idx);
+        acc[0] += wt * v.x;
+        acc[1] += wt * v.y;
+      } else {
+        acc[0] += wt * ld_sc1_f1(r_o, idx);
+      }
+    }
+    const float inv = L > 0.f ? 1.f / L : 0.f;
+#pragma unroll
+    for (int j = 0; j < DPL; ++j) p.out[(int64_t)row * p.ldo + h * D + lane * DPL + j] = f2bf(acc[j] * inv);
+    __builtin_amdgcn_wave_barrier();
+  }
 }
 
 template <int D, int G>
 void launch_decode(const DecodeAttnParams& p, hipStream_t st) {
-  hipLaunchKernelGGL((decode_attn_kernel<D, G>), dim3(p.rows * p.n_kv_heads, p.n_splits), dim3(64), 0, st, p);
-  if (p.n_splits > 1)
-    hipLaunchKernelGGL((attn_combine_kernel<D>), dim3(p.rows * p.n_q_heads), dim3(64), 0, st, p);
+  hipLaunchKernelGGL((decode_attn_kernel<D, G>), dim3(p.rows * p.n_kv_heads, p.n_splits), dim3(kWaves * 64), 0, st,
+                     p);
 }
 
 template <int D>

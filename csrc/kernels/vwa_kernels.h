@@ -44,6 +44,7 @@ struct DecodeAttnParams {
   int split_tokens;                 // keys per split workgroup
   int n_splits;                     // max splits (grid.y)
   float* part_o; float* part_ml;    // [rows][n_splits][n_q_heads][D], [rows][n_splits][n_q_heads][2]
+  int* counters;                    // [rows * n_kv_heads] chunk tickets, zero between launches
   uint16_t* out; int ldo;           // [rows, n_q_heads*D]
 };
 

@@ -115,5 +115,8 @@ def test_concurrent_parse_requests_batch_on_llm_engine():
 
     res = asyncio.run(go())
     assert all(st == 200 and j["version"] == "1.0" and j["intents"] for st, j in res)
+    es = ie.engine_stats()
+    assert es["kv_blocks_total"] == 800 and 0 < es["kv_blocks_used"] < 800  # static prefix stays cached
+    assert es["samples_per_iteration"] > 1 and es["grammar_rejects"] == 0
     assert ie.batch_stats["max_active"] >= 2
     assert ie._thread is None  # scheduler stopped on app cleanup

@@ -57,6 +57,7 @@ class WhisperRunner:
         ns = max(ops.decode_n_splits(b.max_ctx), ops.decode_n_splits(cfg.n_audio_ctx))
         b.part_o = torch.zeros(R * ns * H * hd, dtype=torch.float32, device=dev)
         b.part_ml = torch.zeros(R * ns * H * 2, dtype=torch.float32, device=dev)
+        b.attn_cnt = torch.zeros(R * H, dtype=torch.int32, device=dev)
         b.cross = [(torch.zeros(max_sessions, cfg.n_audio_ctx, H, hd, dtype=model.dtype, device=dev),
                     torch.zeros(max_sessions, cfg.n_audio_ctx, H, hd, dtype=model.dtype, device=dev)) for _ in range(L)]
         b.cross_table = torch.arange(max_sessions, dtype=torch.int32, device=dev)[:, None].contiguous()

@@ -260,6 +260,7 @@ class LLMIntentEngine:
             r.steps += 1
             m = r.matcher
             if tok < 0 or not m.accept_token(tok):
+                self.batch_stats["rejects"] = self.batch_stats.get("rejects", 0) + 1
                 self._finish(r, IntentEngineError(f"sampler returned a token the grammar rejects ({tok})"))
             else:
                 r.out += self.grammar_bytes(tok)
@@ -277,6 +278,23 @@ class LLMIntentEngine:
             self.active = [r for r in self.active if not r.done]
         tm["post_ms"] += (time.perf_counter() - t4) * 1e3
         return finished
+
+    def engine_stats(self) -> Dict[str, Any]:
+        """Scheduler + KV-cache state for /metrics (batch size, KV utilisation, grammar cache)."""
+        eng = self.engine
+        bm = eng.blocks
+        used = bm.num_blocks - bm.n_free()
+        it = max(1, self.batch_stats["iterations"])
+        out = {"active": len(self.active), "waiting": len(self.waiting),
+               "kv_blocks_used": used, "kv_blocks_total": bm.num_blocks,
+               "kv_utilisation": round(used / max(1, bm.num_blocks), 4),
+               "rows_per_iteration": round(self.batch_stats["rows"] / it, 3),
+               "samples_per_iteration": round(self.batch_stats["sampled"] / it, 3),
+               "grammar_rejects": self.batch_stats.get("rejects", 0),
+               "host_ms": {k: round(v, 1) for k, v in self.timing.items()}}
+        out.update(self.grammar.stats())
+        out.update({k: v for k, v in eng.stats.items()})
+        return out
 
     def run_until_idle(self) -> None:
         while self.has_work():

@@ -44,9 +44,12 @@ def build_app(engine: Any = None) -> web.Application:
 
     async def metrics(_req: web.Request) -> web.Response:
         snap = app["metrics"].snapshot()
-        st = getattr(app["engine"], "last_stats", None)
+        eng = app["engine"]
+        st = getattr(eng, "last_stats", None)
         if st:
             snap["last_request"] = st
+        if hasattr(eng, "engine_stats"):
+            snap["engine"] = eng.engine_stats()
         return web.json_response(snap)
 
     async def call(eng, messages):
@@ -89,6 +92,13 @@ def build_app(engine: Any = None) -> web.Application:
             return web.json_response({"error": "schema_validation_failed", "detail": final.format_error()}, status=422)
         m.observe("parse_ms", (time.perf_counter() - t0) * 1e3)
         m.inc("ok")
+        st = getattr(eng, "last_stats", None) or {}
+        if "prefill_ms" in st:  # engine-side request spans (TTFT ~ queue + prefill; decode rate)
+            m.observe("ttft_ms", st.get("queue_ms", 0.0) + st["prefill_ms"])
+            m.observe("decode_ms", st["decode_ms"])
+            if st.get("decode_ms", 0) > 0:
+                toks = st.get("decode_steps", 0) + st.get("forced_tokens", 0)
+                m.observe("decode_tok_per_s", toks / (st["decode_ms"] / 1e3))
         return web.json_response(final.data)
 
     app.on_cleanup.append(on_cleanup)

@@ -151,7 +151,8 @@ class GPT2Model:
                 attn = bufs.attn[:M]
                 ops.decode_attention(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens, bufs.seq_ids,
                                      n_q_heads=self.nq, n_kv_heads=self.nkv, head_dim=self.hd, scale=self.scale,
-                                     max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o, part_ml=bufs.part_ml)
+                                     max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o, part_ml=bufs.part_ml,
+                                     counters=bufs.attn_cnt)
             else:
                 table = bufs.block_table[prefill_seq : prefill_seq + 1]
                 q4 = q.view(1, M, self.nq, self.hd)

@@ -225,7 +225,8 @@ class WhisperModel:
             att = ops.decode_attention(q, ops.KVLayout.paged(bufs.k_cache[li], bufs.v_cache[li], bufs.block_table),
                                        bufs.ctx_lens, bufs.seq_ids, n_q_heads=self.H, n_kv_heads=self.H,
                                        head_dim=self.hd, scale=self.hd ** -0.5, max_ctx=bufs.max_ctx,
-                                       out=bufs.att[:M], part_o=bufs.part_o, part_ml=bufs.part_ml)
+                                       out=bufs.att[:M], part_o=bufs.part_o, part_ml=bufs.part_ml,
+                                       counters=bufs.attn_cnt)
             ops.linear(att, L.o, L.o_b, out=x, residual=x)
             h = ops.layernorm(x, L.lnx_w, L.lnx_b, eps=cfg.ln_eps, out=bufs.h[:M])
             xq = ops.linear(h, L.xq, L.xq_b, out=bufs.q[:M])
@@ -233,7 +234,8 @@ class WhisperModel:
             att = ops.decode_attention(xq, ops.KVLayout.contiguous(ck, cv, bufs.cross_table), bufs.cross_lens,
                                        bufs.seq_ids, n_q_heads=self.H, n_kv_heads=self.H, head_dim=self.hd,
                                        scale=self.hd ** -0.5, max_ctx=ck.shape[1], out=bufs.att[:M],
-                                       part_o=bufs.part_o, part_ml=bufs.part_ml)
+                                       part_o=bufs.part_o, part_ml=bufs.part_ml,
+                                       counters=bufs.attn_cnt)
             ops.linear(att, L.xo, L.xo_b, out=x, residual=x)
             h = ops.layernorm(x, L.ln2_w, L.ln2_b, eps=cfg.ln_eps, out=bufs.h[:M])
             f = ops.linear(h, L.fc1, L.fc1_b, act="gelu", out=bufs.f[:M])

@@ -365,7 +365,20 @@ class KVLayout:
 
 
 def decode_split_tokens() -> int:
-    return 64
+    return 256  # keys per decode-attention workgroup (4 waves x 64)
+
+
+_COUNTERS: dict = {}
+
+
+def split_counters(device, n: int) -> torch.Tensor:
+    """Zeroed int32 chunk tickets for decode attention (the kernel leaves them zero).  Engines
+    that capture hipGraphs allocate their own (StepBuffers.attn_cnt) before capture."""
+    t = _COUNTERS.get(str(device))
+    if t is None or t.numel() < n:
+        t = torch.zeros(max(n, 4096), dtype=torch.int32, device=device)
+        _COUNTERS[str(device)] = t
+    return t
 
 
 def decode_n_splits(max_ctx: int) -> int:
@@ -375,7 +388,7 @@ def decode_n_splits(max_ctx: int) -> int:
 def decode_attention(q: torch.Tensor, kv: KVLayout, ctx_lens: torch.Tensor, seq_ids: torch.Tensor, *,
                      n_q_heads: int, n_kv_heads: int, head_dim: int, scale: float, max_ctx: int,
                      out: torch.Tensor, part_o: Optional[torch.Tensor] = None,
-                     part_ml: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     part_ml: Optional[torch.Tensor] = None, counters: Optional[torch.Tensor] = None) -> torch.Tensor:
     """One query row per token; ``max_ctx`` bounds every row's context (fixes the grid, so the
     launch is graph-capturable while contexts grow)."""
     n_splits = decode_n_splits(max_ctx)
@@ -387,8 +400,10 @@ def decode_attention(q: torch.Tensor, kv: KVLayout, ctx_lens: torch.Tensor, seq_
         rows = q.shape[0]
         part_o = torch.empty((rows * n_splits * n_q_heads * head_dim,), dtype=torch.float32, device=q.device)
         part_ml = torch.empty((rows * n_splits * n_q_heads * 2,), dtype=torch.float32, device=q.device)
+    if counters is None:
+        counters = split_counters(q.device, q.shape[0] * n_kv_heads)
     ext().decode_attention(q, kv.k, kv.v, kv.table, kv.block_size, kv.sb, kv.sh, kv.st, ctx_lens, seq_ids, n_q_heads,
-                           n_kv_heads, head_dim, scale, n_splits, part_o, part_ml, out)
+                           n_kv_heads, head_dim, scale, n_splits, part_o, part_ml, counters, out)
     return out
 
 

@@ -80,6 +80,7 @@ class StepBuffers:
         ns = ops.decode_n_splits(max_ctx)
         self.part_o = torch.zeros(max_rows * ns * model.nq * model.hd, dtype=torch.float32, device=device)
         self.part_ml = torch.zeros(max_rows * ns * model.nq * 2, dtype=torch.float32, device=device)
+        self.attn_cnt = torch.zeros(max_rows * model.nkv, dtype=torch.int32, device=device)  # chunk tickets
         pin = torch.device(device).type == "cuda"
         self.h_meta = torch.zeros(7 * R, dtype=torch.int32, pin_memory=pin)
         self.h_i32 = self.h_meta[: 4 * R].view(4, R)
