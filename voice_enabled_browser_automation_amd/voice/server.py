@@ -78,8 +78,9 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
         m: Metrics = app["metrics"]
         m.inc("connections")
         loop = asyncio.get_running_loop()
+        # per-utterance span (monotonic): first audio -> final transcript -> brain reply
         st: Dict[str, Any] = {"context": {}, "pending": "", "debounce": None, "session_id": None, "closed": False,
-                              "t_final": None}
+                              "t_final": None, "t_utt": None}
         lock = asyncio.Lock()
 
         async def send(obj):
@@ -120,8 +121,12 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                     print(f"[voice] brain post failed: {e}", flush=True)
                     return
                 await send({"type": "intent", "payload": resp})
+                now = time.perf_counter()
                 if st["t_final"] is not None:
-                    m.observe("final_to_intent_ms", (time.perf_counter() - st["t_final"]) * 1e3)
+                    m.observe("final_to_intent_ms", (now - st["t_final"]) * 1e3)
+                if st["t_utt"] is not None:
+                    m.observe("utterance_to_intent_ms", (now - st["t_utt"]) * 1e3)
+                    st["t_utt"] = None
                 m.observe("brain_ms", (time.perf_counter() - t0) * 1e3)
                 if isinstance(resp, dict) and resp.get("tts_summary"):
                     await send({"type": "tts", "payload": resp["tts_summary"]})
@@ -160,6 +165,8 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                     continue
                 m.inc("finals")
                 st["t_final"] = time.perf_counter()
+                if st["t_utt"] is not None:
+                    m.observe("speech_to_final_ms", (st["t_final"] - st["t_utt"]) * 1e3)
                 st["pending"] = f"{st['pending']} {text}" if st["pending"] else text
                 if st["debounce"] is not None:
                     st["debounce"].cancel()
@@ -169,8 +176,15 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
             async for msg in ws:
                 if msg.type == WSMsgType.BINARY:
                     m.inc("audio_frames")
+                    if st["t_utt"] is None:
+                        st["t_utt"] = time.perf_counter()
                     if asr is not None:
+                        t_push = time.perf_counter()
                         events = await loop.run_in_executor(app["asr_pool"], asr.push, msg.data)
+                        dt = time.perf_counter() - t_push
+                        m.observe("asr_push_ms", dt * 1e3)
+                        if events:  # a recognition pass ran: real-time factor of this packet's work
+                            m.observe("asr_rtf", dt / max(1e-6, len(msg.data) / 2 / 16000.0))
                         await handle_events(events)
                 elif msg.type == WSMsgType.TEXT:
                     try:
