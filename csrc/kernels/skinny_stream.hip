@@ -132,6 +132,34 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nl = lane & 15, g = lane >> 4;
 
+  // ---- stage X rows into LDS
+  const int k8 = K / 8;
+  if constexpr (!XG) {
+    for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
+      const int m = c / k8, kk = c % k8;
+      *reinterpret_cast<uint4*>(xs + m * xstride + kk * 8) =
+          *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8);
+    }
+  }
+  __syncthreads();
+  for (int m = w; m < 16; m += KS) {
+    float sc = 1.f;
+    if (p.fuse_rms && m < M) {
+      float s = 0.f;
+      for (int kk = lane; kk < k8; kk += 64) {
+        float f[8];
+        unpack8(XG ? *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8)
+                   : *reinterpret_cast<const uint4*>(xs + m * xstride + kk * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += f[j] * f[j];
+      }
+      s = wave_sum(s);
+      sc = rsqrtf(s / (float)K + p.eps);
+    }
+    if (lane == 0) rs[m] = sc;
+  }
+  __syncthreads();
+
   const int G = K / 128;
   const int gb = (G * w) / KS, ge = (G * (w + 1)) / KS;
   const __amdgpu_buffer_rsrc_t rw =
@@ -202,36 +230,6 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
   uint4 XA[U][4], XB[U][4];  // XG only (dead otherwise)
   load_item(A, 0);
   if constexpr (XG) load_x(XA, 0);
-  // X staging + row statistics run while the first weight item is in flight (weights do not
-  // depend on X): the two HBM/L2 round trips of the prologue overlap
-  // ---- stage X rows into LDS
-  const int k8 = K / 8;
-  if constexpr (!XG) {
-    for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
-      const int m = c / k8, kk = c % k8;
-      *reinterpret_cast<uint4*>(xs + m * xstride + kk * 8) =
-          *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8);
-    }
-  }
-  __syncthreads();
-  for (int m = w; m < 16; m += KS) {
-    float sc = 1.f;
-    if (p.fuse_rms && m < M) {
-      float s = 0.f;
-      for (int kk = lane; kk < k8; kk += 64) {
-        float f[8];
-        unpack8(XG ? *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8)
-                   : *reinterpret_cast<const uint4*>(xs + m * xstride + kk * 8), f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += f[j] * f[j];
-      }
-      s = wave_sum(s);
-      sc = rsqrtf(s / (float)K + p.eps);
-    }
-    if (lane == 0) rs[m] = sc;
-  }
-  __syncthreads();
-
   for (int it = 0; it < n_items; it += 2) {
     load_item(B, it + 1);
     if constexpr (XG) load_x(XB, it + 1);
@@ -288,6 +286,45 @@ __global__ __launch_bounds__(KS * 64) void skinny_fp8_kernel(SkinnyParams p, int
   const int nl = lane & 15, g = lane >> 4;
   const int k8 = K / 8;
 
+  // ---- per-row statistics (sum of squares for the fused RMSNorm, amax for the fp8 scale)
+  for (int m = w; m < 16; m += KS) {
+    float sc = 1.f, iv = 1.f;
+    if (m < M) {
+      float ss = 0.f, am = 0.f;
+      for (int kk = lane; kk < k8; kk += 64) {
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ss += f[j] * f[j];
+          am = fmaxf(am, fabsf(f[j]));
+        }
+      }
+      ss = wave_sum(ss);
+      am = wave_max(am);
+      const float sx = am > 0.f ? am * (1.f / 448.f) : 1.f;
+      iv = 1.f / sx;
+      sc = (p.fuse_rms ? rsqrtf(ss / (float)K + p.eps) : 1.f) * sx;
+    }
+    if (lane == 0) {
+      rs[m] = sc;
+      inv[m] = iv;
+    }
+  }
+  __syncthreads();
+  // ---- quantise X rows into LDS (e4m3, 8 values -> 8 bytes)
+  for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
+    const int m = c / k8, kk = c % k8;
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8), f);
+    const float iv = inv[m];
+    uint2 q;
+    q.x = cvt_pk_fp8(f[0] * iv, f[1] * iv) | (cvt_pk_fp8(f[2] * iv, f[3] * iv) << 16);
+    q.y = cvt_pk_fp8(f[4] * iv, f[5] * iv) | (cvt_pk_fp8(f[6] * iv, f[7] * iv) << 16);
+    *reinterpret_cast<uint2*>(xs + m * xstride + kk * 8) = q;
+  }
+  __syncthreads();
+
   const int G = K / 128;
   const int gb = (G * w) / KS, ge = (G * (w + 1)) / KS;
   const __amdgpu_buffer_rsrc_t rw =
@@ -341,46 +378,6 @@ __global__ __launch_bounds__(KS * 64) void skinny_fp8_kernel(SkinnyParams p, int
 
   uint4 A[NT][U][2], B[NT][U][2];
   load_item(A, 0);
-  // activation statistics + quantised staging overlap the first weight item's round trip
-  // ---- per-row statistics (sum of squares for the fused RMSNorm, amax for the fp8 scale)
-  for (int m = w; m < 16; m += KS) {
-    float sc = 1.f, iv = 1.f;
-    if (m < M) {
-      float ss = 0.f, am = 0.f;
-      for (int kk = lane; kk < k8; kk += 64) {
-        float f[8];
-        unpack8(*reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8), f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          ss += f[j] * f[j];
-          am = fmaxf(am, fabsf(f[j]));
-        }
-      }
-      ss = wave_sum(ss);
-      am = wave_max(am);
-      const float sx = am > 0.f ? am * (1.f / 448.f) : 1.f;
-      iv = 1.f / sx;
-      sc = (p.fuse_rms ? rsqrtf(ss / (float)K + p.eps) : 1.f) * sx;
-    }
-    if (lane == 0) {
-      rs[m] = sc;
-      inv[m] = iv;
-    }
-  }
-  __syncthreads();
-  // ---- quantise X rows into LDS (e4m3, 8 values -> 8 bytes)
-  for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
-    const int m = c / k8, kk = c % k8;
-    float f[8];
-    unpack8(*reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8), f);
-    const float iv = inv[m];
-    uint2 q;
-    q.x = cvt_pk_fp8(f[0] * iv, f[1] * iv) | (cvt_pk_fp8(f[2] * iv, f[3] * iv) << 16);
-    q.y = cvt_pk_fp8(f[4] * iv, f[5] * iv) | (cvt_pk_fp8(f[6] * iv, f[7] * iv) << 16);
-    *reinterpret_cast<uint2*>(xs + m * xstride + kk * 8) = q;
-  }
-  __syncthreads();
-
   for (int it = 0; it < n_items; it += 2) {
     load_item(B, it + 1);
     compute_item(A, it);

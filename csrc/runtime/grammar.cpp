@@ -643,8 +643,13 @@ std::string Grammar::canon(const State& s) const {
         k.append(f.buf, f.blen);
         break;
       case F_REC: case F_ARR: {
+        // The item count only matters near the bounds: below min_items (closing not yet
+        // allowed) and within reach of max_items (whether ',' may follow the current item).  One
+        // token spans at most 64 items (>= 2 bytes each, <= 128-byte tokens), so counts farther
+        // than that from max_items share one class.  Merging count = max-1 with count = max-2
+        // would hand a mask that allows ',' after the last permitted item to the other state.
         const Node& n = nodes_[f.node];
-        int cls = f.count < n.min_items ? f.count : (f.count >= n.max_items ? 1000 : 999);
+        const int cls = (f.count < n.min_items || n.max_items - f.count <= 64) ? f.count : -1;
         k.append(reinterpret_cast<const char*>(&cls), 4);
         break;
       }

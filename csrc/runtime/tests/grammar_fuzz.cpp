@@ -74,7 +74,16 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "walk %d: empty mask after %zu bytes: %s\n", wk, out.size(), out.c_str());
         return 11;
       }
-      // mask and can_accept_token must agree on a sample of tokens
+      // every token the (cached) mask allows must be accepted from this exact state, and a sample
+      // of the rejected ones must be rejected (a cache-key collision between two states shows up
+      // here as an allowed token the state cannot take)
+      for (int t : allowed) {
+        if (!m.can_accept_token(t)) {
+          std::fprintf(stderr, "walk %d: mask allows token %d the state rejects (after %zu bytes)\n", wk, t,
+                       out.size());
+          return 12;
+        }
+      }
       for (int k = 0; k < 64; ++k) {
         const int t = (int)(rng() % n);
         const bool in = (mask[t >> 5] >> (t & 31)) & 1u;
