@@ -40,10 +40,12 @@ void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, what, " launch fa
 int g_skinny_mode = 1;
 int g_grid_cap = 256;
 int g_ks = 8;
-void set_skinny_mode(int64_t mode, int64_t grid_cap, int64_t ks) {
+int g_w_first = 2;  // 0: never, 1: only with the fused RMSNorm prologue, 2: always (measured best)
+void set_skinny_mode(int64_t mode, int64_t grid_cap, int64_t ks, int64_t w_first) {
   g_skinny_mode = (int)mode;
   g_grid_cap = (int)grid_cap;
   g_ks = (int)ks;
+  g_w_first = (int)w_first;
 }
 int run_skinny(int epi, const SkinnyParams& p, hipStream_t st) {
   if (g_skinny_mode == 1) {
@@ -83,6 +85,7 @@ SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<T
   p.fuse_rms = fuse_rms ? 1 : 0;
   p.eps = (float)eps;
   p.w_scale = w_scale.has_value() ? w_scale->data_ptr<float>() : nullptr;
+  p.w_first = g_w_first == 2 || (g_w_first == 1 && fuse_rms);
   return p;
 }
 
@@ -433,6 +436,17 @@ void conv1d_gelu(Tensor x, Tensor w, c10::optional<Tensor> b, c10::optional<Tens
 
 }  // namespace
 
+void quant_fp8_rows(Tensor x, Tensor q, Tensor scale) {
+  c10::DeviceGuard g(x.device());
+  check_bf16(x, "x");
+  check_contig_rows(x, "x");
+  TORCH_CHECK(q.scalar_type() == at::kFloat8_e4m3fn && q.is_contiguous() && q.sizes() == x.sizes(), "q fp8 [rows, D]");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() >= x.size(0), "scale f32 [rows]");
+  check_rc(vwa_quant_fp8_rows(bfp(x), (int)x.stride(0), (int)x.size(0), (int)x.size(1),
+                              reinterpret_cast<uint8_t*>(q.data_ptr()), scale.data_ptr<float>(), cur_stream(x)),
+           "quant_fp8_rows");
+}
+
 // ---- one-shot all-reduce (opaque state handle as int64)
 int64_t ar_create(int64_t rank, int64_t world, int64_t max_elems) {
   void* st = vwa_ar_create((int)rank, (int)world, max_elems);
@@ -460,6 +474,7 @@ int64_t ar_error(int64_t st) { return vwa_ar_error(reinterpret_cast<void*>(st));
 void ar_destroy(int64_t st) { vwa_ar_destroy(reinterpret_cast<void*>(st)); }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("quant_fp8_rows", &quant_fp8_rows);
   m.def("ar_create", &ar_create);
   m.def("ar_handles", &ar_handles);
   m.def("ar_open_peer", &ar_open_peer);
@@ -487,6 +502,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pcm16_to_f32", &pcm16_to_f32);
   m.def("log_mel", &log_mel);
   m.def("conv1d_gelu", &conv1d_gelu);
-  m.def("set_skinny_mode", &set_skinny_mode, py::arg("mode"), py::arg("grid_cap") = 256, py::arg("ks") = 8);
+  m.def("set_skinny_mode", &set_skinny_mode, py::arg("mode"), py::arg("grid_cap") = 256, py::arg("ks") = 8,
+        py::arg("w_first") = 2);
   m.def("attention_split_tokens", []() { return vwa_attention_split_tokens(); });
 }

@@ -222,9 +222,47 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ 
   *reinterpret_cast<uint4*>(out + (size_t)row * D + c) = pack8(v);
 }
 
+// Per-row dynamic fp8 quantisation of activations for the large-M fp8 GEMM path (prefill):
+// amax over the row -> scale = amax/448 -> e4m3 bytes.  One workgroup per row.
+__global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const u16* __restrict__ x, int ldx, int D,
+                                                             uint8_t* __restrict__ q, float* __restrict__ scale) {
+  __shared__ float red[4];
+  const int row = blockIdx.x;
+  const u16* xr = x + (size_t)row * ldx;
+  float am = 0.f;
+  for (int c = threadIdx.x * 8; c < D; c += 256 * 8) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + c), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(f[j]));
+  }
+  am = wave_max(am);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+  __syncthreads();
+  am = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float sx = am > 0.f ? am * (1.f / 448.f) : 1.f;
+  const float iv = 1.f / sx;
+  if (threadIdx.x == 0) scale[row] = sx;
+  for (int c = threadIdx.x * 8; c < D; c += 256 * 8) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + c), f);
+    uint2 o;
+    o.x = cvt_pk_fp8(f[0] * iv, f[1] * iv) | (cvt_pk_fp8(f[2] * iv, f[3] * iv) << 16);
+    o.y = cvt_pk_fp8(f[4] * iv, f[5] * iv) | (cvt_pk_fp8(f[6] * iv, f[7] * iv) << 16);
+    *reinterpret_cast<uint2*>(q + (size_t)row * D + c) = o;
+  }
+}
+
 inline int nblk(int64_t n, int b) { return (int)((n + b - 1) / b); }
 
 }  // namespace
+
+extern "C" int vwa_quant_fp8_rows(const uint16_t* x, int ldx, int rows, int D, uint8_t* q, float* scale,
+                                  hipStream_t st) {
+  if (D % 8) return -1;
+  hipLaunchKernelGGL(quant_fp8_rows_kernel, dim3(rows), dim3(256), 0, st, x, ldx, D, q, scale);
+  return (int)hipGetLastError();
+}
 
 extern "C" int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
                            uint16_t* y, int rows, int D, int ldx, float eps, hipStream_t st) {

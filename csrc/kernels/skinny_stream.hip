@@ -37,14 +37,51 @@ VWA_DEVICE uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Epilogue operands that do not depend on the GEMM (residual tile, fp8 column scales, QKV row
+// positions / KV slots / rotary factors) are loaded for the workgroup's FIRST tile at kernel
+// start, so they are not one more dependent memory round trip after the reduction.  Thread o
+// owns output o of the tile (M*16*NT <= threads for every shape the launcher accepts).
+struct EpiPre {
+  float r = 0.f, cs0 = 1.f, cs1 = 1.f, rc = 1.f, rsn = 0.f;
+  int64_t slot = -1;
+};
+
+template <int EPI, int NT>
+VWA_DEVICE void epi_values(const SkinnyParams& p, int tile, int o, EpiPre& e) {
+  const int n0 = tile * 16 * NT;
+  if constexpr (EPI == EPI_SWIGLU || EPI == EPI_QKV) {
+    if (o >= p.M * 16) return;
+    const int m = o >> 4, q = o & 15;
+    if (p.w_scale) {
+      e.cs0 = p.w_scale[n0 + q];
+      e.cs1 = p.w_scale[n0 + (EPI == EPI_SWIGLU ? 16 + q : (q ^ 8))];
+    }
+    if constexpr (EPI == EPI_QKV) {
+      const int hd = p.head_dim, half = hd >> 1, t = (n0 % hd) >> 4;
+      e.slot = p.slots[m];
+      if (p.use_rope) {
+        const int di = (q < 8) ? (8 * t + q) : (8 * t + q - 8);
+        const int pos = p.positions[m];
+        e.rc = p.rope[((size_t)pos * half + di) * 2 + 0];
+        e.rsn = p.rope[((size_t)pos * half + di) * 2 + 1];
+      }
+    }
+  } else {
+    if (o >= p.M * 16 * NT) return;
+    const int m = o / (16 * NT), nn = o % (16 * NT);
+    if (p.w_scale) e.cs0 = p.w_scale[n0 + nn];
+    if constexpr (EPI == EPI_RESID) e.r = bf2f(p.R[(size_t)m * p.ldr + n0 + nn]);
+  }
+}
+
 // Cross-wave reduction of one column tile + fused epilogue.  rs[m]: per-row scale (fused RMSNorm
-// and, on the fp8 path, the activation quantisation scale); p.w_scale: per-column weight scale.
+// and, on the fp8 path, the activation quantisation scale); column scales (fp8) come with the
+// epilogue operands (`pre` when this is the workgroup's first tile).
 template <int EPI, int NT, int KS>
 VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs, int tile, f32x4 (&acc)[NT], int w,
-                              int lane) {
+                              int lane, const EpiPre& pre, bool first) {
   const int M = p.M;
   const int n0 = tile * 16 * NT;
-  const float* cs = p.w_scale;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -56,13 +93,20 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
     float s = 0.f;
 #pragma unroll
     for (int ww = 0; ww < KS; ++ww) s += red[((ww * NT + nt) * 4 + i) * 64 + ln];
-    return cs ? s * cs[n0 + nn] : s;
+    return s;
+  };
+  auto operands = [&](int o) {
+    if (first && o == (int)threadIdx.x) return pre;
+    EpiPre e;
+    epi_values<EPI, NT>(p, tile, o, e);
+    return e;
   };
   if constexpr (EPI == EPI_SWIGLU) {
     for (int o = threadIdx.x; o < M * 16; o += KS * 64) {
       const int m = o >> 4, q = o & 15;
+      const EpiPre e = operands(o);
       const float sc = rs[m];
-      float gv = red_at(m, q) * sc, uv = red_at(m, 16 + q) * sc;
+      float gv = red_at(m, q) * sc * e.cs0, uv = red_at(m, 16 + q) * sc * e.cs1;
       if (p.bias) {
         gv += bf2f(p.bias[n0 + q]);
         uv += bf2f(p.bias[n0 + 16 + q]);
@@ -76,25 +120,20 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
     const bool is_v = head >= p.n_q_heads + p.n_kv_heads;
     for (int o = threadIdx.x; o < M * 16; o += KS * 64) {
       const int m = o >> 4, q = o & 15;
+      const EpiPre e = operands(o);
       const float sc = rs[m];
-      float v = red_at(m, q) * sc, pv = red_at(m, q ^ 8) * sc;
+      float v = red_at(m, q) * sc * e.cs0, pv = red_at(m, q ^ 8) * sc * e.cs1;
       if (p.bias) {
         v += bf2f(p.bias[n0 + q]);
         pv += bf2f(p.bias[n0 + (q ^ 8)]);
       }
       const int d = (q < 8) ? (8 * t + q) : (half + 8 * t + q - 8);
-      if (p.use_rope && !is_v) {
-        const int pos = p.positions[m];
-        const int di = (q < 8) ? (8 * t + q) : (8 * t + q - 8);
-        const float c = p.rope[((size_t)pos * half + di) * 2 + 0];
-        const float sn = p.rope[((size_t)pos * half + di) * 2 + 1];
-        v = (q < 8) ? (v * c - pv * sn) : (v * c + pv * sn);
-      }
+      if (p.use_rope && !is_v) v = (q < 8) ? (v * e.rc - pv * e.rsn) : (v * e.rc + pv * e.rsn);
       const u16 out = f2bf(v);
       if (head < p.n_q_heads) {
         p.q_out[(size_t)m * p.ldq + head * hd + d] = out;
       } else {
-        const int64_t slot = p.slots[m];
+        const int64_t slot = e.slot;
         if (slot >= 0) {
           const int64_t blk = slot / p.block_size, off = slot % p.block_size;
           const int kvh = is_v ? head - p.n_q_heads - p.n_kv_heads : head - p.n_q_heads;
@@ -107,10 +146,11 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
     for (int o = threadIdx.x; o < M * 16 * NT; o += KS * 64) {
       const int m = o / (16 * NT), nn = o % (16 * NT);
       const int n = n0 + nn;
-      float v = red_at(m, nn) * rs[m];
+      const EpiPre e = operands(o);
+      float v = red_at(m, nn) * rs[m] * e.cs0;
       if (p.bias) v += bf2f(p.bias[n]);
       if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
-      if constexpr (EPI == EPI_RESID) v += bf2f(p.R[(size_t)m * p.ldr + n]);
+      if constexpr (EPI == EPI_RESID) v += e.r;
       if (p.y_f32) reinterpret_cast<float*>(p.Y)[(size_t)m * p.ldy + n] = v;
       else reinterpret_cast<u16*>(p.Y)[(size_t)m * p.ldy + n] = f2bf(v);
     }
@@ -132,34 +172,8 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nl = lane & 15, g = lane >> 4;
 
-  // ---- stage X rows into LDS
-  const int k8 = K / 8;
-  if constexpr (!XG) {
-    for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
-      const int m = c / k8, kk = c % k8;
-      *reinterpret_cast<uint4*>(xs + m * xstride + kk * 8) =
-          *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8);
-    }
-  }
-  __syncthreads();
-  for (int m = w; m < 16; m += KS) {
-    float sc = 1.f;
-    if (p.fuse_rms && m < M) {
-      float s = 0.f;
-      for (int kk = lane; kk < k8; kk += 64) {
-        float f[8];
-        unpack8(XG ? *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8)
-                   : *reinterpret_cast<const uint4*>(xs + m * xstride + kk * 8), f);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += f[j] * f[j];
-      }
-      s = wave_sum(s);
-      sc = rsqrtf(s / (float)K + p.eps);
-    }
-    if (lane == 0) rs[m] = sc;
-  }
-  __syncthreads();
-
+  EpiPre pre;
+  epi_values<EPI, NT>(p, blockIdx.x, threadIdx.x, pre);  // first tile's epilogue operands, early
   const int G = K / 128;
   const int gb = (G * w) / KS, ge = (G * (w + 1)) / KS;
   const __amdgpu_buffer_rsrc_t rw =
@@ -223,13 +237,49 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
 
   auto finish_tile = [&](int it) {
     const int tile = blockIdx.x + (it / nb) * gridDim.x;
-    tile_epilogue<EPI, NT, KS>(p, red, rs, tile, acc, w, lane);
+    tile_epilogue<EPI, NT, KS>(p, red, rs, tile, acc, w, lane, pre, it < nb);
   };
 
   uint4 A[NT][U][4], B[NT][U][4];
   uint4 XA[U][4], XB[U][4];  // XG only (dead otherwise)
-  load_item(A, 0);
-  if constexpr (XG) load_x(XA, 0);
+  // w_first: issue the first weight item before staging X (its round trip then overlaps the X
+  // staging + fused-RMSNorm statistics); otherwise stage X first (the X round trip is short).
+  if (p.w_first) {
+    load_item(A, 0);
+    if constexpr (XG) load_x(XA, 0);
+  }
+  // ---- stage X rows into LDS
+  const int k8 = K / 8;
+  if constexpr (!XG) {
+    for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
+      const int m = c / k8, kk = c % k8;
+      *reinterpret_cast<uint4*>(xs + m * xstride + kk * 8) =
+          *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8);
+    }
+  }
+  __syncthreads();
+  for (int m = w; m < 16; m += KS) {
+    float sc = 1.f;
+    if (p.fuse_rms && m < M) {
+      float s = 0.f;
+      for (int kk = lane; kk < k8; kk += 64) {
+        float f[8];
+        unpack8(XG ? *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8)
+                   : *reinterpret_cast<const uint4*>(xs + m * xstride + kk * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += f[j] * f[j];
+      }
+      s = wave_sum(s);
+      sc = rsqrtf(s / (float)K + p.eps);
+    }
+    if (lane == 0) rs[m] = sc;
+  }
+  __syncthreads();
+
+  if (!p.w_first) {
+    load_item(A, 0);
+    if constexpr (XG) load_x(XA, 0);
+  }
   for (int it = 0; it < n_items; it += 2) {
     load_item(B, it + 1);
     if constexpr (XG) load_x(XB, it + 1);
@@ -286,6 +336,8 @@ __global__ __launch_bounds__(KS * 64) void skinny_fp8_kernel(SkinnyParams p, int
   const int nl = lane & 15, g = lane >> 4;
   const int k8 = K / 8;
 
+  EpiPre pre;
+  epi_values<EPI, NT>(p, blockIdx.x, threadIdx.x, pre);  // first tile's epilogue operands, early
   // ---- per-row statistics (sum of squares for the fused RMSNorm, amax for the fp8 scale)
   for (int m = w; m < 16; m += KS) {
     float sc = 1.f, iv = 1.f;
@@ -381,12 +433,14 @@ __global__ __launch_bounds__(KS * 64) void skinny_fp8_kernel(SkinnyParams p, int
   for (int it = 0; it < n_items; it += 2) {
     load_item(B, it + 1);
     compute_item(A, it);
-    if (it % nb == nb - 1) tile_epilogue<EPI, NT, KS>(p, red, rs, blockIdx.x + (it / nb) * gridDim.x, acc, w, lane);
+    if (it % nb == nb - 1)
+      tile_epilogue<EPI, NT, KS>(p, red, rs, blockIdx.x + (it / nb) * gridDim.x, acc, w, lane, pre, it < nb);
     if (it + 1 >= n_items) break;
     load_item(A, it + 2);
     compute_item(B, it + 1);
     if ((it + 1) % nb == nb - 1)
-      tile_epilogue<EPI, NT, KS>(p, red, rs, blockIdx.x + ((it + 1) / nb) * gridDim.x, acc, w, lane);
+      tile_epilogue<EPI, NT, KS>(p, red, rs, blockIdx.x + ((it + 1) / nb) * gridDim.x, acc, w, lane, pre,
+                                 it + 1 < nb);
   }
 }
 

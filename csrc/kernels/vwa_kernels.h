@@ -22,6 +22,7 @@ struct SkinnyParams {
   int block_size;
   int64_t cache_stride_block, cache_stride_head, cache_stride_tok;
   const float* w_scale;  // non-null: W is OCP fp8 e4m3 [N, K] bytes with per-row scales (W8A8 path)
+  int w_first;           // stream kernel: issue the first weight loads before staging X
 };
 
 // Paged / strided KV addressing shared by the attention kernels:
@@ -90,6 +91,7 @@ int vwa_log_mel(const float* audio, int n_samples, int n_frames, const float* wi
 int vwa_conv1d_gelu_pos(const uint16_t* x, const uint16_t* w, const uint16_t* b, const uint16_t* pos, uint16_t* y,
                         int B, int Cin, int Tin, int Cout, int Tout, int stride, hipStream_t st);
 int vwa_attention_split_tokens();
+int vwa_quant_fp8_rows(const uint16_t* x, int ldx, int rows, int D, uint8_t* q, float* scale, hipStream_t st);
 // one-shot peer-to-peer all-reduce (allreduce.hip)
 void* vwa_ar_create(int rank, int world, int64_t max_elems);
 int vwa_ar_handles(void* st, void* out);

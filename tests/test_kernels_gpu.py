@@ -33,11 +33,12 @@ def close(a, b, atol, rtol=2e-2):
     assert err <= tol, f"max err {err} > tol {tol}"
 
 
-@pytest.fixture(params=[(0, 256, 8), (1, 256, 8), (1, 768, 4)], ids=["tile", "stream8", "stream4"])
+@pytest.fixture(params=[(0, 256, 8), (1, 256, 8, 0), (1, 768, 4), (1, 256, 8, 2)],
+                ids=["tile", "stream8_xfirst", "stream4", "stream8"])
 def skinny_mode(request):
     ops.ext().set_skinny_mode(*request.param)
     yield request.param
-    ops.ext().set_skinny_mode(1, 256, 8)
+    ops.ext().set_skinny_mode(1, 256, 8, 2)
 
 
 @pytest.mark.parametrize("M", [1, 5, 17, 40])

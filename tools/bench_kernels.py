@@ -41,7 +41,7 @@ def timeit(fn, iters=40, reps=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
-    ap.add_argument("--only", default="gemm,attn,flash", help="comma list of gemm,attn,flash,mall")
+    ap.add_argument("--only", default="gemm,attn,flash", help="comma list of floor,gemm,gemm8,wfirst,attn,flash,mall")
     args = ap.parse_args()
     only = set(args.only.split(","))
     dev = "cuda"
@@ -82,6 +82,66 @@ def main():
                      hipblaslt_tbps=round(gb / (t_blas * 1e-6) / 1e3, 3))
             print(json.dumps(r), flush=True)
             res.append(r)
+    # launch floor: the smallest kernels in the decode graph (graph-replayed like everything here)
+    if "floor" in only:
+        ids = torch.zeros(1, dtype=torch.int32, device=dev)
+        tab = torch.randn(1024, 4096, device=dev).to(torch.bfloat16)
+        o1 = torch.empty(1, 4096, device=dev, dtype=torch.bfloat16)
+        r = dict(kernel="launch_floor", embedding_1row_us=round(timeit(lambda: ops.embedding(ids, tab, out=o1)), 2),
+                 torch_fill_us=round(timeit(lambda: o1.fill_(1.0)), 2))
+        print(json.dumps(r), flush=True)
+        res.append(r)
+    # prologue order A/B: first weight item before / after the X staging (+ fused RMSNorm)
+    for M in ((1, 4) if "wfirst" in only else ()):
+        for name, N, K in shapes[:4]:
+            x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            ncopy = max(1, int(1.0e9 // (N * K * 2)) + 1)
+            ws = [(torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16) for _ in range(ncopy)]
+            y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            it = [0]
+            out = {}
+            for rms in (False, True):
+                for wf in (0, 2):
+                    def f():
+                        it[0] = (it[0] + 1) % ncopy
+                        ops.ext().skinny_gemm(x, ws[it[0]], None, y, 0, rms, 1e-5, None)
+                    ops.ext().set_skinny_mode(1, 256, 8, wf)
+                    out[f"rms{int(rms)}_wf{wf}"] = round(timeit(f), 2)
+            ops.ext().set_skinny_mode(1, 256, 8, 2)
+            del ws
+            r = dict(kernel="prologue_order", shape=name, M=M, **out)
+            print(json.dumps(r), flush=True)
+            res.append(r)
+    # fp8 (W8A8) streaming GEMM on the same shapes, vs torch._scaled_mm (hipBLASLt fp8) where available
+    for M in ((1, 4, 16) if "gemm8" in only else ()):
+        for name, N, K in shapes:
+            x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            ncopy = max(1, int(1.0e9 // (N * K)) + 1)
+            ws = [ops.FP8Weight.quantize(torch.randn(N, K, device=dev) * 0.02) for _ in range(ncopy)]
+            y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            it = [0]
+            fits = ops._fp8_stream_fits(M, K)
+
+            def ours8():
+                it[0] = (it[0] + 1) % ncopy
+                w8 = ws[it[0]]
+                ops.ext().skinny_gemm(x, w8.w8, None, y, 0, False, 1e-5, None, w8.scale)
+
+            def smm():
+                it[0] = (it[0] + 1) % ncopy
+                ops._fp8_matmul(x, ws[it[0]])
+
+            t8 = timeit(ours8) if fits else float("nan")
+            try:
+                ts = timeit(smm)
+            except Exception:  # noqa: BLE001
+                ts = float("nan")
+            del ws
+            gb = N * K / 1e9
+            r = dict(kernel="skinny_gemm_fp8", shape=name, M=M, N=N, K=K, us=round(t8, 2),
+                     tbps=round(gb / (t8 * 1e-6) / 1e3, 3), scaled_mm_us=round(ts, 2))
+            print(json.dumps(r), flush=True)
+            res.append(r)
     # Infinity-Cache (MALL) experiment: GEMM time when its weights were read by the previous
     # kernel (prefetched into the 256 MB memory-side cache) vs cold
     for name, N, K in (shapes[1:3] if "mall" in only else ()):
@@ -113,7 +173,8 @@ def main():
         del ws
     # decode attention, Llama-3-8B geometry, ctx 1200
     nq, nkv, hd, bs = 32, 8, 128, 16
-    for rows, ctx in (((1, 1200), (8, 1200), (32, 1200)) if "attn" in only else ()):
+    for rows, ctx in (((1, 64), (1, 256), (1, 512), (1, 1200), (1, 2000), (8, 1200), (32, 1200))
+                      if "attn" in only else ()):
         blocks = rows * ((ctx + bs - 1) // bs) + 8
         kc = torch.randn(blocks, nkv, bs, hd, device=dev).to(torch.bfloat16)
         vc = torch.randn_like(kc)
