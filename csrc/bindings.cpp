@@ -505,4 +505,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_skinny_mode", &set_skinny_mode, py::arg("mode"), py::arg("grid_cap") = 256, py::arg("ks") = 8,
         py::arg("w_first") = 2);
   m.def("attention_split_tokens", []() { return vwa_attention_split_tokens(); });
+  m.def("set_attention_impl", [](int64_t impl) { vwa_set_attention_impl((int)impl); });
 }

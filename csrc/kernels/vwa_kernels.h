@@ -23,6 +23,10 @@ struct SkinnyParams {
   int64_t cache_stride_block, cache_stride_head, cache_stride_tok;
   const float* w_scale;  // non-null: W is OCP fp8 e4m3 [N, K] bytes with per-row scales (W8A8 path)
   int w_first;           // stream kernel: issue the first weight loads before staging X
+  // fuse_rms == 2: LayerNorm folded into the GEMM (stream kernel, bf16 weights): W holds
+  // W*gamma, bias holds b + W.beta, ln_c[n] = sum_k (W*gamma)[n][k]; the kernel computes each
+  // row's mean/rstd from the staged X and applies y = rstd * (acc - mean * ln_c[n]) + bias
+  const float* ln_c;
 };
 
 // Paged / strided KV addressing shared by the attention kernels:
@@ -78,6 +82,7 @@ int vwa_swiglu(const uint16_t* gu, uint16_t* h, int rows, int F, hipStream_t st)
 int vwa_bias_act(const uint16_t* x, const uint16_t* bias, const uint16_t* residual, uint16_t* y, int rows, int N,
                  int act, hipStream_t st);
 int vwa_decode_attention(const DecodeAttnParams* p, hipStream_t st);
+void vwa_set_attention_impl(int impl);  // 1: multi-query MFMA kernel (default), 0: split VALU kernel
 int vwa_flash_attention(const FlashAttnParams* p, hipStream_t st);
 int vwa_embedding(const int* ids, const uint16_t* table, const uint16_t* pos_table, const int* positions,
                   uint16_t* out, int rows, int D, int vocab_start, int vocab_end, hipStream_t st);

@@ -195,6 +195,58 @@ def test_decode_attention_paged(hd, nq, nkv, ctx):
     close(out1, exp1, 2e-2)
 
 
+@pytest.fixture(params=["mq", "split"])
+def attn_impl(request):
+    ops.set_attention_impl(request.param)
+    yield request.param
+    ops.set_attention_impl("mq")
+
+
+@pytest.mark.parametrize("hd,nq,nkv", [(128, 32, 8), (128, 8, 1), (64, 6, 6), (64, 8, 4)])
+def test_decode_attention_row_groups(hd, nq, nkv, attn_impl):
+    """Ragged step as the engines build it: jump-forward runs of one sequence (consecutive
+    positions, shared K/V), single rows of other sessions, and a run longer than one row group
+    (16 / G rows); contexts straddle chunk boundaries and one row sees a single key."""
+    bs, blocks = 16, 160
+    kc = rnd(blocks, nkv, bs, hd)
+    vc = rnd(blocks, nkv, bs, hd)
+    table = torch.stack([torch.randperm(blocks, device=DEV)[:40] for _ in range(4)]).to(torch.int32)
+    seqs = [0] * 5 + [1] + [2] * 19 + [3]
+    ctx = list(range(300, 305)) + [1] + list(range(620, 639)) + [129]
+    rows = len(seqs)
+    seq_ids = torch.tensor(seqs, dtype=torch.int32, device=DEV)
+    ctx_lens = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    q = rnd(rows, nq * hd)
+    kv = ops.KVLayout.paged(kc, vc, table)
+    out = torch.empty_like(q)
+    cnt = torch.zeros(rows * nkv, dtype=torch.int32, device=DEV)
+    for _ in range(2):  # second launch: tickets must have been left zero
+        ops.decode_attention(q, kv, ctx_lens, seq_ids, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
+                             scale=hd ** -0.5, max_ctx=40 * bs, out=out, counters=cnt)
+    assert int(cnt.abs().sum()) == 0
+    exp = ref.decode_attention(q.cpu(), ops.KVLayout.paged(kc.cpu(), vc.cpu(), table.cpu()), ctx_lens.cpu(),
+                               seq_ids.cpu(), n_q_heads=nq, n_kv_heads=nkv, head_dim=hd, scale=hd ** -0.5,
+                               out=torch.empty(rows, nq * hd, dtype=BF))
+    close(out, exp, 2e-2)
+
+
+def test_decode_attention_cross_contiguous(attn_impl):
+    """Whisper cross-attention: contiguous [B, 1500, H, 64] encoder K/V, one block per session."""
+    B, T, H, hd = 3, 1500, 6, 64
+    k, v = rnd(B, T, H, hd), rnd(B, T, H, hd)
+    table = torch.arange(B, dtype=torch.int32, device=DEV)[:, None].contiguous()
+    seq_ids = torch.tensor([2, 0, 1, 1], dtype=torch.int32, device=DEV)
+    lens = torch.full((4,), T, dtype=torch.int32, device=DEV)
+    q = rnd(4, H * hd)
+    out = torch.empty_like(q)
+    ops.decode_attention(q, ops.KVLayout.contiguous(k, v, table), lens, seq_ids, n_q_heads=H, n_kv_heads=H,
+                         head_dim=hd, scale=hd ** -0.5, max_ctx=T, out=out)
+    exp = ref.decode_attention(q.cpu(), ops.KVLayout.contiguous(k.cpu(), v.cpu(), table.cpu()), lens.cpu(),
+                               seq_ids.cpu(), n_q_heads=H, n_kv_heads=H, head_dim=hd, scale=hd ** -0.5,
+                               out=torch.empty(4, H * hd, dtype=BF))
+    close(out, exp, 2e-2)
+
+
 def test_flash_attention_causal_paged_prefix():
     hd, nq, nkv, bs = 128, 8, 2, 16
     blocks = 40

@@ -40,6 +40,9 @@ def ext():
     try:
         from . import _vwa_kernels as m  # type: ignore
 
+        impl = os.environ.get("VWA_ATTN_IMPL")
+        if impl:
+            m.set_attention_impl(ATTENTION_IMPLS[impl])
         _EXT = m
         return m
     except BaseException as e:  # noqa: BLE001
@@ -368,7 +371,15 @@ class KVLayout:
 
 
 def decode_split_tokens() -> int:
-    return 256  # keys per decode-attention workgroup (4 waves x 64)
+    return 128  # chunk granularity of the decode-attention grid (attention.hip kMqChunk)
+
+
+ATTENTION_IMPLS = {"split": 0, "mq": 1}
+
+
+def set_attention_impl(name: str) -> None:
+    """Decode-attention kernel: "mq" (multi-query MFMA, default) or "split" (VALU split-K)."""
+    ext().set_attention_impl(ATTENTION_IMPLS[name])
 
 
 _COUNTERS: dict = {}

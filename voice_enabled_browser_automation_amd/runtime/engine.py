@@ -88,6 +88,12 @@ class StepBuffers:
         self.h_sel = self.h_meta[6 * R :]
         self.h_table = torch.zeros(max_seqs, max_blocks_per_seq, dtype=torch.int32, pin_memory=pin)
         self.table_dirty = True
+        # numpy views of the pinned staging buffers: the per-step row metadata is written with a
+        # handful of slice assignments instead of ~5 torch element writes per row
+        self.np_i32 = self.h_i32.numpy()
+        self.np_slots = self.h_slots.numpy()
+        self.np_sel = self.h_sel.numpy()
+        self.np_table = self.h_table.numpy()
 
     def upload(self, n_rows: int) -> None:
         nb = True
@@ -164,10 +170,9 @@ class LLMEngine:
             self._sync_table(seq)
 
     def _sync_table(self, seq: Sequence_) -> None:
-        row = self.bufs.h_table[seq.sid]
-        row.zero_()
-        if seq.blocks:
-            row[: len(seq.blocks)] = torch.tensor(seq.blocks, dtype=torch.int32)
+        row = self.bufs.np_table[seq.sid]
+        row[:] = 0
+        row[: len(seq.blocks)] = seq.blocks
         self.bufs.table_dirty = True
 
     def slot_of(self, seq: Sequence_, pos: int) -> int:
@@ -217,37 +222,39 @@ class LLMEngine:
         n = len(rows)
         M = bucket_for(n)
         b = self.bufs
-        hi = b.h_i32
         if logits_for is None or len(logits_for) == n:
             nl, L = n, M
         else:
             nl = len(logits_for)
             L = min(bucket_for(nl), M)
-            if L == M:  # no saving: compute every row and index on the host side
-                pass
-            else:
-                for j, r in enumerate(logits_for):
-                    b.h_sel[j] = r
-                for j in range(nl, L):
-                    b.h_sel[j] = logits_for[-1]
+            if L < M:  # (L == M: no saving -- compute every row and index on the host side)
+                b.np_sel[:nl] = logits_for
+                b.np_sel[nl:L] = logits_for[-1]
         pending: Dict[int, int] = {}
-        for i, (seq, tok) in enumerate(rows):
-            pos = pending.get(seq.sid, seq.n_computed)
-            self._ensure_blocks(seq, pos + 1)
+        bs = self.block_size
+        toks, poss, sids, slots = [], [], [], []
+        for seq, tok in rows:
+            sid = seq.sid
+            pos = pending.get(sid, seq.n_computed)
+            if pos // bs >= len(seq.blocks):
+                self._ensure_blocks(seq, pos + 1)
             if pos >= len(seq.tokens):
                 seq.tokens.append(tok)
-            hi[0, i] = tok
-            hi[1, i] = pos
-            hi[2, i] = seq.sid
-            hi[3, i] = pos + 1
-            b.h_slots[i] = self.slot_of(seq, pos)
-            pending[seq.sid] = pos + 1
-        for i in range(n, M):  # padded rows: no KV write, 1-token context on scratch block 0
-            hi[0, i] = 0
-            hi[1, i] = 0
-            hi[2, i] = 0
-            hi[3, i] = 1
-            b.h_slots[i] = -1
+            toks.append(tok)
+            poss.append(pos)
+            sids.append(sid)
+            slots.append(seq.blocks[pos // bs] * bs + pos % bs)
+            pending[sid] = pos + 1
+        hi = b.np_i32
+        hi[0, :n] = toks
+        hi[1, :n] = poss
+        hi[2, :n] = sids
+        hi[3, :n] = hi[1, :n] + 1
+        b.np_slots[:n] = slots
+        if M > n:  # padded rows: no KV write, 1-token context on scratch block 0
+            hi[0:3, n:M] = 0
+            hi[3, n:M] = 1
+            b.np_slots[n:M] = -1
         b.upload(M)
         if self.use_graphs:
             g, out = self.graphs.get((M, L)) or self._capture(M, L)
