@@ -92,16 +92,29 @@ SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<T
 // fp8 weights run only on the streaming kernel; a shape it cannot take is an error, never a
 // silent bf16 fallback (the Python layer routes those shapes to the dequantising path).
 int run_skinny_checked(int epi, const SkinnyParams& p, hipStream_t st) {
-  if (p.w_scale) return vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
+  if (p.w_scale || p.fuse_rms == 2) return vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
   return run_skinny(epi, p, st);
+}
+
+// Folded LayerNorm (fuse_rms = 2): streaming kernel only, bf16 weights, <= 16 rows.
+void set_ln_fold(SkinnyParams& p, const c10::optional<Tensor>& ln_c, int epi) {
+  if (!ln_c.has_value()) return;
+  TORCH_CHECK(p.w_scale == nullptr, "folded LayerNorm needs bf16 weights");
+  TORCH_CHECK(epi != 2, "folded LayerNorm is not supported with the SwiGLU epilogue");
+  TORCH_CHECK(p.M <= 16, "folded LayerNorm runs on the streaming kernel (<= 16 rows)");
+  TORCH_CHECK(ln_c->is_cuda() && ln_c->scalar_type() == at::kFloat && ln_c->is_contiguous() && ln_c->numel() == p.N,
+              "ln_c must be f32 [N]");
+  p.fuse_rms = 2;
+  p.ln_c = ln_c->data_ptr<float>();
 }
 
 // epi: 0 store, 1 residual add, 3 gelu
 void skinny_gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi, bool fuse_rms, double eps,
-                 c10::optional<Tensor> residual, c10::optional<Tensor> w_scale) {
+                 c10::optional<Tensor> residual, c10::optional<Tensor> w_scale, c10::optional<Tensor> ln_c) {
   c10::DeviceGuard g(x.device());
   SkinnyParams p = base_params(x, w, bias, fuse_rms, eps, w_scale);
   TORCH_CHECK(epi == 0 || epi == 1 || epi == 3, "bad epilogue");
+  set_ln_fold(p, ln_c, (int)epi);
   TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be a 2-D row-contiguous GPU tensor");
   TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) == w.size(0), "y shape mismatch");
   TORCH_CHECK(y.scalar_type() == at::kBFloat16 || y.scalar_type() == at::kFloat, "y must be bf16 or f32");
@@ -141,9 +154,10 @@ void check_cache(const Tensor& c, const char* name) {
 void skinny_gemm_qkv(Tensor x, Tensor w_qkv, c10::optional<Tensor> bias, bool fuse_rms, double eps, int64_t n_q_heads,
                      int64_t n_kv_heads, int64_t head_dim, bool use_rope, Tensor positions, Tensor slots,
                      c10::optional<Tensor> rope, Tensor q_out, Tensor k_cache, Tensor v_cache,
-                     c10::optional<Tensor> w_scale) {
+                     c10::optional<Tensor> w_scale, c10::optional<Tensor> ln_c) {
   c10::DeviceGuard g(x.device());
   SkinnyParams p = base_params(x, w_qkv, bias, fuse_rms, eps, w_scale);
+  set_ln_fold(p, ln_c, 4);
   TORCH_CHECK(w_qkv.size(0) == (n_q_heads + 2 * n_kv_heads) * head_dim, "w_qkv rows mismatch");
   TORCH_CHECK(head_dim % 16 == 0, "head_dim must be a multiple of 16");
   TORCH_CHECK(positions.scalar_type() == at::kInt && positions.numel() >= x.size(0), "positions int32 [M]");
@@ -483,13 +497,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ar_destroy", &ar_destroy);
   m.doc() = "MI355X (gfx950) HIP kernels for the voice-web-agent inference engine";
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
-        py::arg("fuse_rms"), py::arg("eps"), py::arg("residual"), py::arg("w_scale") = py::none());
+        py::arg("fuse_rms"), py::arg("eps"), py::arg("residual"), py::arg("w_scale") = py::none(),
+        py::arg("ln_c") = py::none());
   m.def("skinny_gemm_swiglu", &skinny_gemm_swiglu, py::arg("x"), py::arg("w_gu"), py::arg("bias"), py::arg("h"),
         py::arg("fuse_rms"), py::arg("eps"), py::arg("w_scale") = py::none());
   m.def("skinny_gemm_qkv", &skinny_gemm_qkv, py::arg("x"), py::arg("w_qkv"), py::arg("bias"), py::arg("fuse_rms"),
         py::arg("eps"), py::arg("n_q_heads"), py::arg("n_kv_heads"), py::arg("head_dim"), py::arg("use_rope"),
         py::arg("positions"), py::arg("slots"), py::arg("rope"), py::arg("q_out"), py::arg("k_cache"),
-        py::arg("v_cache"), py::arg("w_scale") = py::none());
+        py::arg("v_cache"), py::arg("w_scale") = py::none(), py::arg("ln_c") = py::none());
   m.def("rmsnorm", &rmsnorm);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);

@@ -346,7 +346,6 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
   // ---- row groups of the whole step (<= 64 rows; every wave derives the same answer): runs of
   //      consecutive rows of one sequence, cut every RG rows from the run's start
   const int sl = lane < p.rows ? p.seq_ids[lane] : -1;
-  const int cl = lane < p.rows ? p.ctx_lens[lane] : 0;  // same round trip as the sequence ids
   const int sp = __shfl(sl, lane > 0 ? lane - 1 : 0, 64);
   const unsigned long long run_starts = __ballot(lane < p.rows && (lane == 0 || sl != sp));
   const int run0 = 63 - __builtin_clzll(run_starts & ((2ull << lane) - 1ull));  // lane 0 always starts a run
@@ -369,8 +368,7 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
   const int nr = min(RG, run_end - r0);  // rows in this group
   const int seq = __shfl(sl, r0, 64);
   __syncthreads();  // the previous item's LDS readers are done
-  const int c_src = __shfl(cl, min(r0 + lane, 63), 64);
-  const int c_own = lane < nr ? c_src : 0;
+  const int c_own = lane < nr ? p.ctx_lens[r0 + lane] : 0;
   int ctxmax = c_own;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) ctxmax = max(ctxmax, __shfl_xor(ctxmax, o, 64));
@@ -402,20 +400,9 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
     }
   }
 
-  // block-table entries of this wave's key range, one per lane, loaded once: the K/V loads of
-  // every step then need no dependent table load (a table load queued behind the previous
-  // step's K/V loads would serialise the steps, vmcnt being in order)
-  const int bsz = p.kv.block_size;
-  const int blk0 = wb / bsz;
-  const bool lane_tab = nsteps > 0 && (we - 1) / bsz - blk0 < 64;
-  const int* trow = p.kv.block_table + (int64_t)seq * p.kv.table_stride;
-  const int tab = (lane_tab && blk0 + lane <= (we - 1) / bsz) ? trow[blk0 + lane] : 0;
-  auto kv_off = [&](int key) -> int64_t {
-    const int b = key / bsz;
-    const int blk = lane_tab ? __shfl(tab, b - blk0, 64) : trow[b];
-    return (int64_t)blk * p.kv.stride_block + (int64_t)kvh * p.kv.stride_head +
-           (int64_t)(key - b * bsz) * p.kv.stride_tok;
-  };
+  // (measured: staging the wave's block-table entries in lanes and fetching them with __shfl,
+  // instead of the per-key table loads below, was 1.5-3 us SLOWER on every shape)
+  auto kv_off = [&](int key) -> int64_t { return kv_offset(p.kv, seq, kvh, key); };
 
   // K: A-operand row n of tile t is key kb + 8(n>>2) + 4t + (n&3) (so the S^T accumulator of lane
   // (n, g) holds keys kb + 8g + 4t + i); V: 32 rows x NCH chunks, chunk idx = i*64 + lane

@@ -75,11 +75,12 @@ VWA_DEVICE void epi_values(const SkinnyParams& p, int tile, int o, EpiPre& e) {
 }
 
 // Cross-wave reduction of one column tile + fused epilogue.  rs[m]: per-row scale (fused RMSNorm
-// and, on the fp8 path, the activation quantisation scale); column scales (fp8) come with the
-// epilogue operands (`pre` when this is the workgroup's first tile).
+// / LayerNorm rstd and, on the fp8 path, the activation quantisation scale); mus[m] (folded
+// LayerNorm only, else null): row mean, removed as mean * ln_c[n]; column scales (fp8) come
+// with the epilogue operands (`pre` when this is the workgroup's first tile).
 template <int EPI, int NT, int KS>
-VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs, int tile, f32x4 (&acc)[NT], int w,
-                              int lane, const EpiPre& pre, bool first) {
+VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs, const float* mus, int tile,
+                              f32x4 (&acc)[NT], int w, int lane, const EpiPre& pre, bool first) {
   const int M = p.M;
   const int n0 = tile * 16 * NT;
 #pragma unroll
@@ -122,7 +123,13 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
       const int m = o >> 4, q = o & 15;
       const EpiPre e = operands(o);
       const float sc = rs[m];
-      float v = red_at(m, q) * sc * e.cs0, pv = red_at(m, q ^ 8) * sc * e.cs1;
+      float v = red_at(m, q), pv = red_at(m, q ^ 8);
+      if (mus) {
+        v -= mus[m] * p.ln_c[n0 + q];
+        pv -= mus[m] * p.ln_c[n0 + (q ^ 8)];
+      }
+      v *= sc * e.cs0;
+      pv *= sc * e.cs1;
       if (p.bias) {
         v += bf2f(p.bias[n0 + q]);
         pv += bf2f(p.bias[n0 + (q ^ 8)]);
@@ -147,7 +154,9 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
       const int m = o / (16 * NT), nn = o % (16 * NT);
       const int n = n0 + nn;
       const EpiPre e = operands(o);
-      float v = red_at(m, nn) * rs[m] * e.cs0;
+      float v = red_at(m, nn);
+      if (mus) v -= mus[m] * p.ln_c[n];
+      v *= rs[m] * e.cs0;
       if (p.bias) v += bf2f(p.bias[n]);
       if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
       if constexpr (EPI == EPI_RESID) v += e.r;
@@ -168,7 +177,9 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
   u16* xs = reinterpret_cast<u16*>(smem);
   const int xbytes = XG ? 0 : ((M * xstride * 2) + 15) & ~15;
   float* red = reinterpret_cast<float*>(smem + xbytes);  // [KS][NT][4][64]
-  float* rs = red + KS * NT * 4 * 64;                     // [16]
+  float* rs = red + KS * NT * 4 * 64;                     // [16] row scales (1/rms, LayerNorm rstd)
+  float* mu = rs + 16;                                    // [16] row means (folded LayerNorm)
+  const float* mus = (p.fuse_rms == 2) ? mu : nullptr;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nl = lane & 15, g = lane >> 4;
 
@@ -237,7 +248,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
 
   auto finish_tile = [&](int it) {
     const int tile = blockIdx.x + (it / nb) * gridDim.x;
-    tile_epilogue<EPI, NT, KS>(p, red, rs, tile, acc, w, lane, pre, it < nb);
+    tile_epilogue<EPI, NT, KS>(p, red, rs, mus, tile, acc, w, lane, pre, it < nb);
   };
 
   uint4 A[NT][U][4], B[NT][U][4];
@@ -259,20 +270,31 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
   }
   __syncthreads();
   for (int m = w; m < 16; m += KS) {
-    float sc = 1.f;
+    float sc = 1.f, mean = 0.f;
     if (p.fuse_rms && m < M) {
-      float s = 0.f;
+      float s = 0.f, s1 = 0.f;
       for (int kk = lane; kk < k8; kk += 64) {
         float f[8];
         unpack8(XG ? *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8)
                    : *reinterpret_cast<const uint4*>(xs + m * xstride + kk * 8), f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s += f[j] * f[j];
+        for (int j = 0; j < 8; ++j) {
+          s += f[j] * f[j];
+          s1 += f[j];
+        }
       }
       s = wave_sum(s);
-      sc = rsqrtf(s / (float)K + p.eps);
+      if (p.fuse_rms == 2) {  // LayerNorm: rstd from E[x^2] - mean^2
+        mean = wave_sum(s1) / (float)K;
+        sc = rsqrtf(fmaxf(s / (float)K - mean * mean, 0.f) + p.eps);
+      } else {
+        sc = rsqrtf(s / (float)K + p.eps);
+      }
     }
-    if (lane == 0) rs[m] = sc;
+    if (lane == 0) {
+      rs[m] = sc;
+      mu[m] = mean;
+    }
   }
   __syncthreads();
 
@@ -309,7 +331,7 @@ template <int EPI, int NT, int KS>
 int launch(const SkinnyParams& p, hipStream_t st, int grid_cap) {
   const int xstride = p.K + 8;
   const size_t xbytes = ((size_t)p.M * xstride * 2 + 15) & ~(size_t)15;
-  const size_t red = (size_t)(KS * NT * 4 * 64 + 16) * sizeof(float);
+  const size_t red = (size_t)(KS * NT * 4 * 64 + 32) * sizeof(float);  // + row scales + row means
   if (xbytes + red <= 160 * 1024) return launch_v<EPI, NT, KS, false>(p, st, grid_cap, xbytes + red, xstride);
   if ((size_t)p.M * p.ldx * 2 >= 0x7FFFFFF0ull) return -10;
   return launch_v<EPI, NT, KS, true>(p, st, grid_cap, red, xstride);
@@ -434,12 +456,12 @@ __global__ __launch_bounds__(KS * 64) void skinny_fp8_kernel(SkinnyParams p, int
     load_item(B, it + 1);
     compute_item(A, it);
     if (it % nb == nb - 1)
-      tile_epilogue<EPI, NT, KS>(p, red, rs, blockIdx.x + (it / nb) * gridDim.x, acc, w, lane, pre, it < nb);
+      tile_epilogue<EPI, NT, KS>(p, red, rs, nullptr, blockIdx.x + (it / nb) * gridDim.x, acc, w, lane, pre, it < nb);
     if (it + 1 >= n_items) break;
     load_item(A, it + 2);
     compute_item(B, it + 1);
     if ((it + 1) % nb == nb - 1)
-      tile_epilogue<EPI, NT, KS>(p, red, rs, blockIdx.x + ((it + 1) / nb) * gridDim.x, acc, w, lane, pre,
+      tile_epilogue<EPI, NT, KS>(p, red, rs, nullptr, blockIdx.x + ((it + 1) / nb) * gridDim.x, acc, w, lane, pre,
                                  it + 1 < nb);
   }
 }

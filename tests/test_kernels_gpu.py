@@ -136,6 +136,49 @@ def test_qkv_rope_write(M, skinny_mode):
     close(vc, vc2, 3e-2)
 
 
+@pytest.mark.parametrize("M", [1, 6, 16, 24])
+def test_folded_layernorm_linear_and_qkv(M):
+    """LayerNorm folded into the streaming GEMM (mean/rstd from the staged rows) vs LayerNorm ->
+    linear in f32; 24 rows take the normalise-then-GEMM path.  Inputs carry a large mean (the
+    residual stream's offset) to exercise the mean * rowsum correction."""
+    K, N = 384, 512
+    x = (torch.randn(M, K, device=DEV) * 2 + 3).to(BF)
+    gamma, beta = rnd(K, scale=0.5) + 1, rnd(K, scale=0.2)
+    w, b = rnd(N, K, scale=0.05), rnd(N, scale=0.1)
+    wf, bf, c = ops.fold_layernorm(w, b, gamma, beta)
+    xf = torch.nn.functional.layer_norm(x.float().cpu(), (K,), gamma.float().cpu(), beta.float().cpu(), 1e-5)
+    res = rnd(M, N)
+    for act, r in (("none", None), ("gelu", None), ("none", res)):
+        out = torch.empty(M, N, dtype=BF, device=DEV)
+        ops.linear(x, wf, bf, out=out, act=act, residual=r, eps=1e-5, ln_c=c)
+        exp = xf @ w.float().cpu().t() + b.float().cpu()
+        if act == "gelu":
+            exp = torch.nn.functional.gelu(exp)
+        if r is not None:
+            exp = exp + r.float().cpu()
+        close(out, exp, 3e-2)
+    # QKV epilogue with the folded norm (Whisper decoder self-attention: no RoPE)
+    H, hd = 4, 64
+    wq, bq = rnd(3 * H * hd, K, scale=0.05), rnd(3 * H * hd, scale=0.1)
+    wqp = ops.permute_qkv_rows(wq, 3 * H, hd)
+    bqp = ops.permute_qkv_rows(bq[:, None], 3 * H, hd)[:, 0].contiguous()
+    wfq, bfq, cq = ops.fold_layernorm(wqp, bqp, gamma, beta)
+    pos = torch.arange(M, dtype=torch.int32, device=DEV)
+    slots = torch.randperm(8 * 16, device=DEV)[:M].to(torch.int64)
+    kc, vc = _kv_setup(H, H, hd, blocks=8)
+    q = torch.zeros(M, H * hd, dtype=BF, device=DEV)
+    ops.qkv_rope_write(x, wfq, bfq, fuse_rms=False, eps=1e-5, n_q_heads=H, n_kv_heads=H, head_dim=hd, rope=None,
+                       positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc, ln_c=cq)
+    kc2, vc2 = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q2 = torch.zeros(M, H * hd, dtype=BF)
+    ref.qkv_rope_write(xf.to(BF), wqp.cpu(), bqp.cpu(), fuse_rms=False, eps=1e-5, n_q_heads=H, n_kv_heads=H,
+                       head_dim=hd, rope=None, positions=pos.cpu(), slots=slots.cpu(), q_out=q2, k_cache=kc2,
+                       v_cache=vc2)
+    close(q, q2, 3e-2)
+    close(kc, kc2, 3e-2)
+    close(vc, vc2, 3e-2)
+
+
 def test_norms():
     for D in (384, 4096):
         x, r = rnd(9, D), rnd(9, D)

@@ -223,6 +223,8 @@ def move_model(model, device) -> None:
             return obj
         if isinstance(obj, list):
             return [mv(x) for x in obj]
+        if isinstance(obj, tuple):
+            return tuple(mv(x) for x in obj)
         return obj
 
     for k, v in list(vars(model).items()):

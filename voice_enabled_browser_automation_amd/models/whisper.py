@@ -6,11 +6,11 @@ Encoder (one pass per 30 s window, batch of sessions = DP):
             -> out-proj + bias + residual (K-epilogue) -> layernorm -> fc1 + bias + GELU -> fc2 + residual]
     -> layernorm -> cross-attention K/V for every decoder layer (computed once per window).
 Decoder (per token, hipGraph-captured per batch bucket):
-    embedding + learned positions (K14) -> L x [layernorm -> fused QKV skinny GEMM + bias + paged
-    self-KV write (K12 QKV epilogue, no RoPE) -> decode attention (K10) -> out-proj residual epilogue
-    -> layernorm -> q skinny GEMM -> cross attention over the window's K/V (K7) -> out-proj residual
-    -> layernorm -> fc1 GELU epilogue -> fc2 residual epilogue] -> layernorm -> tied LM head (f32)
-    -> masked greedy sampling (K13).
+    embedding + learned positions (K14) -> L x [fused QKV skinny GEMM + bias + paged self-KV write
+    (K12 QKV epilogue, no RoPE) -> decode attention (K10) -> out-proj residual epilogue -> q skinny
+    GEMM -> cross attention over the window's K/V (K7) -> out-proj residual -> fc1 GELU epilogue ->
+    fc2 residual epilogue] -> tied LM head (f32) -> masked greedy sampling (K13).  Every decoder
+    LayerNorm is folded into the GEMM that consumes it (fold_decoder_norms): 8 launches per layer.
 """
 from __future__ import annotations
 
@@ -55,6 +55,11 @@ class DecLayer:
     ln2_w: torch.Tensor; ln2_b: torch.Tensor
     fc1: torch.Tensor; fc1_b: torch.Tensor
     fc2: torch.Tensor; fc2_b: torch.Tensor
+    # decode-path copies with the preceding LayerNorm folded in (ops.fold_layernorm):
+    # (weight * gamma, bias + weight @ beta, row sums of the folded weight)
+    f_qkv: Optional[tuple] = None
+    f_xq: Optional[tuple] = None
+    f_fc1: Optional[tuple] = None
 
 
 class WhisperModel:
@@ -111,6 +116,7 @@ class WhisperModel:
         self.vocab_padded = vp
         self.lm_head = torch.zeros(vp, d, device=self.device, dtype=dtype)
         self.lm_head[: cfg.vocab_size] = self.tok_emb
+        self.fold_decoder_norms()
         # front-end constants
         self.window = torch.hann_window(400, periodic=True, device=self.device)
         self.cos_table = torch.cos(torch.arange(400, dtype=torch.float64) * 2 * math.pi / 400).float().to(self.device)
@@ -165,6 +171,19 @@ class WhisperModel:
                 g(p + "fc1.bias"), g(p + "fc2.weight"), g(p + "fc2.bias")))
         self.dec_ln_w, self.dec_ln_b = g(dd + "layer_norm.weight"), g(dd + "layer_norm.bias")
 
+    def fold_decoder_norms(self) -> None:
+        """Fold every decoder LayerNorm into the projection that consumes it (self-attention QKV,
+        cross-attention query, fc1, LM head): a decode step then has no LayerNorm launches; the
+        streaming GEMM computes each row's mean / rstd from the activation rows it stages anyway
+        (8 instead of 11 kernels per layer).  The unfolded weights stay for the encoder-side
+        cross K/V projections and checkpoint round trips."""
+        fold = ops.fold_layernorm
+        for L in self.dec:
+            L.f_qkv = fold(L.qkv, L.qkv_b, L.ln1_w, L.ln1_b)
+            L.f_xq = fold(L.xq, L.xq_b, L.lnx_w, L.lnx_b)
+            L.f_fc1 = fold(L.fc1, L.fc1_b, L.ln2_w, L.ln2_b)
+        self.f_lm = fold(self.lm_head, None, self.dec_ln_w, self.dec_ln_b)
+
     # ------------------------------------------------------------------ encoder
     def log_mel(self, audio: torch.Tensor, n_frames: int = 3000) -> torch.Tensor:
         """audio: f32 samples (<= 30 s). Returns [n_frames, n_mels] bf16 (channels-last)."""
@@ -217,19 +236,20 @@ class WhisperModel:
         d = cfg.d_model
         x = bufs.hidden[:M]
         ops.embedding(bufs.tokens, self.tok_emb, pos_table=self.pos_emb, positions=bufs.positions, out=x, rows=M)
+        eps = cfg.ln_eps
         for li, L in enumerate(self.dec):
-            h = ops.layernorm(x, L.ln1_w, L.ln1_b, eps=cfg.ln_eps, out=bufs.h[:M])
-            q = ops.qkv_rope_write(h, L.qkv, L.qkv_b, fuse_rms=False, eps=0.0, n_q_heads=self.H, n_kv_heads=self.H,
+            w, b, c = L.f_qkv  # self_attn_layer_norm folded in
+            q = ops.qkv_rope_write(x, w, b, fuse_rms=False, eps=eps, n_q_heads=self.H, n_kv_heads=self.H,
                                    head_dim=self.hd, rope=None, positions=bufs.positions, slots=bufs.slots,
-                                   q_out=bufs.q, k_cache=bufs.k_cache[li], v_cache=bufs.v_cache[li])
+                                   q_out=bufs.q, k_cache=bufs.k_cache[li], v_cache=bufs.v_cache[li], ln_c=c)
             att = ops.decode_attention(q, ops.KVLayout.paged(bufs.k_cache[li], bufs.v_cache[li], bufs.block_table),
                                        bufs.ctx_lens, bufs.seq_ids, n_q_heads=self.H, n_kv_heads=self.H,
                                        head_dim=self.hd, scale=self.hd ** -0.5, max_ctx=bufs.max_ctx,
                                        out=bufs.att[:M], part_o=bufs.part_o, part_ml=bufs.part_ml,
                                        counters=bufs.attn_cnt)
             ops.linear(att, L.o, L.o_b, out=x, residual=x)
-            h = ops.layernorm(x, L.lnx_w, L.lnx_b, eps=cfg.ln_eps, out=bufs.h[:M])
-            xq = ops.linear(h, L.xq, L.xq_b, out=bufs.q[:M])
+            w, b, c = L.f_xq  # encoder_attn_layer_norm folded in
+            xq = ops.linear(x, w, b, out=bufs.q[:M], eps=eps, ln_c=c)
             ck, cv = bufs.cross[li]
             att = ops.decode_attention(xq, ops.KVLayout.contiguous(ck, cv, bufs.cross_table), bufs.cross_lens,
                                        bufs.seq_ids, n_q_heads=self.H, n_kv_heads=self.H, head_dim=self.hd,
@@ -237,8 +257,8 @@ class WhisperModel:
                                        part_o=bufs.part_o, part_ml=bufs.part_ml,
                                        counters=bufs.attn_cnt)
             ops.linear(att, L.xo, L.xo_b, out=x, residual=x)
-            h = ops.layernorm(x, L.ln2_w, L.ln2_b, eps=cfg.ln_eps, out=bufs.h[:M])
-            f = ops.linear(h, L.fc1, L.fc1_b, act="gelu", out=bufs.f[:M])
+            w, b, c = L.f_fc1  # final_layer_norm folded in
+            f = ops.linear(x, w, b, act="gelu", out=bufs.f[:M], eps=eps, ln_c=c)
             ops.linear(f, L.fc2, L.fc2_b, out=x, residual=x)
-        h = ops.layernorm(x, self.dec_ln_w, self.dec_ln_b, eps=cfg.ln_eps, out=bufs.h[:M])
-        return ops.linear(h, self.lm_head, out=bufs.logits[:M])
+        w, b, c = self.f_lm  # decoder layer_norm folded into the tied LM head
+        return ops.linear(x, w, b, out=bufs.logits[:M], eps=eps, ln_c=c)

@@ -190,6 +190,39 @@ def fold_norm(w: torch.Tensor, gamma: torch.Tensor) -> torch.Tensor:
     return (w.float() * gamma.float()[None, :]).to(w.dtype)
 
 
+def fold_layernorm(w: torch.Tensor, bias: Optional[torch.Tensor], gamma: torch.Tensor, beta: torch.Tensor):
+    """LayerNorm(gamma, beta) folded into the following linear (w, bias).
+
+    LN(x) @ w^T + b = rstd * (x @ (w*gamma)^T - mean * c) + (b + w @ beta),  c[n] = sum_k (w*gamma)[n, k]
+    Returns (w*gamma, b + w@beta, c) -- c is computed from the ROUNDED folded weights so the
+    kernel's mean term cancels exactly what its GEMM accumulates.
+    """
+    wf = w.float()
+    wg = (wf * gamma.float()[None, :]).to(w.dtype).contiguous()
+    b = wf @ beta.float()
+    if bias is not None:
+        b = b + bias.float()
+    return wg, b.to(w.dtype).contiguous(), wg.float().sum(1).contiguous()
+
+
+_LN_UNIT: dict = {}
+
+
+def _layernorm_plain(x: torch.Tensor, eps: float) -> torch.Tensor:
+    """(x - mean) * rstd (no affine): the input of a linear whose LayerNorm affine is folded in."""
+    key = (x.shape[1], str(x.device), x.dtype)
+    if key not in _LN_UNIT:
+        _LN_UNIT[key] = (torch.ones(x.shape[1], dtype=x.dtype, device=x.device),
+                         torch.zeros(x.shape[1], dtype=x.dtype, device=x.device))
+    one, zero = _LN_UNIT[key]
+    return layernorm(x, one, zero, eps=eps)
+
+
+def _ln_fold_fits(x: torch.Tensor, w) -> bool:
+    return (_gpu(x) and not isinstance(w, FP8Weight) and x.shape[0] <= SKINNY_MAX_M and x.shape[1] % 128 == 0
+            and w.shape[0] % 16 == 0)
+
+
 def rope_table(max_pos: int, head_dim: int, theta: float, device=None, scaling: Optional[dict] = None) -> torch.Tensor:
     half = head_dim // 2
     inv = 1.0 / (theta ** (torch.arange(0, half, dtype=torch.float64) * 2.0 / head_dim))
@@ -216,16 +249,24 @@ SKINNY_MAX_M = 16
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, out: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, act: str = "none", fuse_rms: bool = False, eps: float = 1e-5,
-           out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+           out_dtype: Optional[torch.dtype] = None, ln_c: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = act(rms(x) @ w^T + bias) [+ residual].
 
     GPU: rows <= 64 -> MFMA skinny GEMM with fused epilogue (decode); otherwise hipBLASLt
     (torch.matmul) for the plain GEMM + HIP epilogue kernels (prefill).
+    ln_c (from fold_layernorm): x goes through a LayerNorm whose affine is folded into (w, bias);
+    decode rows compute its mean/rstd inside the streaming GEMM, other shapes normalise first.
     """
     M = x.shape[0]
     dt = out_dtype or (x.dtype if out is None else out.dtype)
     if out is None:
         out = torch.empty((M, w.shape[0]), dtype=dt, device=x.device)
+    if ln_c is not None:
+        if _ln_fold_fits(x, w):
+            epi = {"none": 0, "gelu": 3}[act] if residual is None else 1
+            ext().skinny_gemm(x, w, bias, out, epi, False, eps, residual, None, ln_c)
+            return out
+        return linear(_layernorm_plain(x, eps), w, bias, out=out, residual=residual, act=act, out_dtype=out_dtype)
     if not _gpu(x):
         xr, wr, fr = _ref_w8(x, w, fuse_rms, eps)
         return ref.linear(xr, wr, bias, out=out, residual=residual, act=act, fuse_rms=fr, eps=eps)
@@ -285,9 +326,16 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
 def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Tensor], *, fuse_rms: bool, eps: float,
                    n_q_heads: int, n_kv_heads: int, head_dim: int, rope: Optional[torch.Tensor],
                    positions: torch.Tensor, slots: torch.Tensor, q_out: torch.Tensor, k_cache: torch.Tensor,
-                   v_cache: torch.Tensor) -> torch.Tensor:
-    """Fused QKV projection + rotary + paged KV write. Returns q_out[:M] (natural layout)."""
+                   v_cache: torch.Tensor, ln_c: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused QKV projection + rotary + paged KV write. Returns q_out[:M] (natural layout).
+    ln_c: folded LayerNorm on x (see linear)."""
     M = x.shape[0]
+    if ln_c is not None:
+        if _ln_fold_fits(x, w_qkv):
+            ext().skinny_gemm_qkv(x, w_qkv, bias, False, eps, n_q_heads, n_kv_heads, head_dim, rope is not None,
+                                  positions, slots, rope, q_out, k_cache, v_cache, None, ln_c)
+            return q_out[:M]
+        x = _layernorm_plain(x, eps)
     if not _gpu(x):
         x, w_qkv, fuse_rms = _ref_w8(x, w_qkv, fuse_rms, eps)
         ref.qkv_rope_write(x, w_qkv, bias, fuse_rms=fuse_rms, eps=eps, n_q_heads=n_q_heads, n_kv_heads=n_kv_heads,
