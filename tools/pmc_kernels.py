@@ -38,6 +38,13 @@ def main():
         ops.linear_swiglu(x, ws[i % 3], fuse_rms=True, out=h)
     torch.cuda.synchronize()
     del ws
+    # the same gate/up on the fp8 path (OCP e4m3 weights, per-row scales, fp8 MFMA)
+    ws = [ops.FP8Weight.quantize((torch.randn(28672, 4096, device=dev) * 0.02).to(torch.bfloat16))
+          for _ in range(5)]
+    for i in range(ITERS):
+        ops.linear_swiglu(x, ws[i % 5], fuse_rms=True, out=h)
+    torch.cuda.synchronize()
+    del ws
     # decode attention (multi-query MFMA kernel): 1 row, then a 64-row prompt chunk of one sequence
     nq, nkv, hd, bs, ctx = 32, 8, 128, 16, 1100
     per = 2048 // bs
