@@ -151,19 +151,17 @@ void check_cache(const Tensor& c, const char* name) {
   TORCH_CHECK(c.dim() == 4 && c.is_contiguous(), name, " must be contiguous [blocks, kv_heads, block_size, head_dim]");
 }
 
-void skinny_gemm_qkv(Tensor x, Tensor w_qkv, c10::optional<Tensor> bias, bool fuse_rms, double eps, int64_t n_q_heads,
-                     int64_t n_kv_heads, int64_t head_dim, bool use_rope, Tensor positions, Tensor slots,
-                     c10::optional<Tensor> rope, Tensor q_out, Tensor k_cache, Tensor v_cache,
-                     c10::optional<Tensor> w_scale, c10::optional<Tensor> ln_c) {
-  c10::DeviceGuard g(x.device());
-  SkinnyParams p = base_params(x, w_qkv, bias, fuse_rms, eps, w_scale);
-  set_ln_fold(p, ln_c, 4);
+// QKV epilogue operands (RoPE table, positions, paged-KV slots and cache strides) into p
+void set_qkv_epilogue(SkinnyParams& p, const Tensor& w_qkv, int64_t n_q_heads, int64_t n_kv_heads, int64_t head_dim,
+                      bool use_rope, const Tensor& positions, const Tensor& slots, const c10::optional<Tensor>& rope,
+                      const Tensor& q_out, const Tensor& k_cache, const Tensor& v_cache) {
   TORCH_CHECK(w_qkv.size(0) == (n_q_heads + 2 * n_kv_heads) * head_dim, "w_qkv rows mismatch");
   TORCH_CHECK(head_dim % 16 == 0, "head_dim must be a multiple of 16");
-  TORCH_CHECK(positions.scalar_type() == at::kInt && positions.numel() >= x.size(0), "positions int32 [M]");
-  TORCH_CHECK(slots.scalar_type() == at::kLong && slots.numel() >= x.size(0), "slots int64 [M]");
+  TORCH_CHECK(positions.is_cuda() && positions.scalar_type() == at::kInt && positions.numel() >= p.M,
+              "positions int32 [M]");
+  TORCH_CHECK(slots.is_cuda() && slots.scalar_type() == at::kLong && slots.numel() >= p.M, "slots int64 [M]");
   check_bf16(q_out, "q_out");
-  TORCH_CHECK(q_out.dim() == 2 && q_out.size(0) >= x.size(0) && q_out.size(1) == n_q_heads * head_dim, "q_out shape");
+  TORCH_CHECK(q_out.dim() == 2 && q_out.size(0) >= p.M && q_out.size(1) == n_q_heads * head_dim, "q_out shape");
   check_cache(k_cache, "k_cache");
   check_cache(v_cache, "v_cache");
   TORCH_CHECK(k_cache.size(1) == n_kv_heads && k_cache.size(3) == head_dim, "cache shape mismatch");
@@ -186,7 +184,102 @@ void skinny_gemm_qkv(Tensor x, Tensor w_qkv, c10::optional<Tensor> bias, bool fu
   p.cache_stride_block = k_cache.stride(0);
   p.cache_stride_head = k_cache.stride(1);
   p.cache_stride_tok = k_cache.stride(2);
+}
+
+void skinny_gemm_qkv(Tensor x, Tensor w_qkv, c10::optional<Tensor> bias, bool fuse_rms, double eps, int64_t n_q_heads,
+                     int64_t n_kv_heads, int64_t head_dim, bool use_rope, Tensor positions, Tensor slots,
+                     c10::optional<Tensor> rope, Tensor q_out, Tensor k_cache, Tensor v_cache,
+                     c10::optional<Tensor> w_scale, c10::optional<Tensor> ln_c) {
+  c10::DeviceGuard g(x.device());
+  SkinnyParams p = base_params(x, w_qkv, bias, fuse_rms, eps, w_scale);
+  set_ln_fold(p, ln_c, 4);
+  set_qkv_epilogue(p, w_qkv, n_q_heads, n_kv_heads, head_dim, use_rope, positions, slots, rope, q_out, k_cache,
+                   v_cache);
   check_rc(run_skinny_checked(4, p, cur_stream(x)), "skinny_gemm_qkv");
+}
+
+// ---- chained decode layer tail (skinny_stream.hip, vwa_chain_*): descriptor built once on the
+// host and copied to a device tensor (graph replays then only launch); M <= 4, bf16, one GPU.
+void set_resid(SkinnyParams& p, const Tensor& h) {
+  p.Y = h.data_ptr();
+  p.ldy = (int)h.stride(0);
+  p.R = bfp(h);
+  p.ldr = (int)h.stride(0);
+}
+
+// Returns (descriptor uint8 tensor, dynamic LDS bytes); descriptor is empty when the shapes do
+// not fit the chain (the caller keeps the per-kernel path).
+std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor w_o, Tensor w_gu, Tensor w_down,
+                                       double eps, c10::optional<Tensor> w_qkv, int64_t n_q_heads, int64_t n_kv_heads,
+                                       int64_t head_dim, c10::optional<Tensor> positions, c10::optional<Tensor> slots,
+                                       c10::optional<Tensor> rope, c10::optional<Tensor> q_out,
+                                       c10::optional<Tensor> k_cache, c10::optional<Tensor> v_cache, Tensor bar,
+                                       Tensor work, c10::optional<Tensor> ts, int64_t bar_mode) {
+  c10::DeviceGuard g(h.device());
+  const int64_t M = h.size(0);
+  TORCH_CHECK(att.size(0) == M && act.size(0) == M, "row counts differ");
+  TORCH_CHECK(act.size(1) * 2 == w_gu.size(0) && w_gu.size(0) % 32 == 0, "act must be [M, gate_up rows / 2]");
+  TORCH_CHECK(w_down.size(1) == act.size(1) && w_down.size(0) == h.size(1) && w_o.size(0) == h.size(1),
+              "down / o_proj shapes");
+  TORCH_CHECK(bar.is_cuda() && bar.scalar_type() == at::kInt && bar.numel() >= 384 && bar.is_contiguous() &&
+                  (reinterpret_cast<uintptr_t>(bar.data_ptr()) & 127) == 0,
+              "bar must be a 128-byte aligned int32[>=384] on the GPU");
+  ChainParams cp{};
+  cp.ph[0].p = base_params(att, w_o, c10::nullopt, false, eps);
+  cp.ph[0].epi = 1;
+  set_resid(cp.ph[0].p, h);
+  cp.ph[1].p = base_params(h, w_gu, c10::nullopt, true, eps);
+  cp.ph[1].epi = 2;
+  check_bf16(act, "act");
+  TORCH_CHECK(act.stride(1) == 1, "act rows must be contiguous");
+  cp.ph[1].p.Y = act.data_ptr();
+  cp.ph[1].p.ldy = (int)act.stride(0);
+  cp.ph[2].p = base_params(act, w_down, c10::nullopt, false, eps);
+  cp.ph[2].epi = 1;
+  set_resid(cp.ph[2].p, h);
+  cp.n = 3;
+  if (w_qkv.has_value()) {
+    TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
+                    v_cache.has_value(),
+                "the QKV phase needs positions, slots, q_out and the KV caches");
+    cp.ph[3].p = base_params(h, *w_qkv, c10::nullopt, true, eps);
+    cp.ph[3].epi = 4;
+    set_qkv_epilogue(cp.ph[3].p, *w_qkv, n_q_heads, n_kv_heads, head_dim, rope.has_value(), *positions, *slots, rope,
+                     *q_out, *k_cache, *v_cache);
+    cp.n = 4;
+  }
+  cp.bar = reinterpret_cast<unsigned*>(bar.data_ptr<int>());
+  cp.bar_mode = (int)bar_mode;
+  // work: [0, 8192) u32 split-tile tickets (zeroed, self-resetting) | f32 partial slots
+  TORCH_CHECK(work.is_cuda() && work.scalar_type() == at::kInt && work.is_contiguous() && work.numel() > 8192 + 4096,
+              "work must be a zeroed int32 GPU tensor of > 12288 elements");
+  cp.tickets = reinterpret_cast<unsigned*>(work.data_ptr<int>());
+  cp.max_tiles = 8192;
+  cp.part = reinterpret_cast<float*>(work.data_ptr<int>() + 8192);
+  cp.part_floats = (int)(work.numel() - 8192);
+  if (ts.has_value()) {
+    TORCH_CHECK(ts->is_cuda() && ts->scalar_type() == at::kLong && ts->numel() >= 1024 * 16, "ts must be int64[>=16384]");
+    cp.ts = reinterpret_cast<unsigned long long*>(ts->data_ptr<int64_t>());
+  }
+  int cus = 0;
+  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h.device().index()) == hipSuccess,
+              "CU count");
+  const int lds = vwa_chain_prepare(&cp, cus);
+  if (lds < 0) return {torch::empty({0}, torch::dtype(torch::kUInt8).device(h.device())), 0};
+  Tensor host = torch::empty({(int64_t)sizeof(ChainParams)}, torch::dtype(torch::kUInt8));
+  std::memcpy(host.data_ptr(), &cp, sizeof(ChainParams));
+  return {host.to(h.device()), (int64_t)lds};
+}
+
+void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like) {
+  c10::DeviceGuard g(like.device());
+  TORCH_CHECK(desc.is_cuda() && desc.numel() == (int64_t)sizeof(ChainParams), "bad chain descriptor");
+  int dev = like.device().index(), cus = 0;
+  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess, "CU count");
+  // one workgroup per CU: the barrier needs every workgroup resident
+  check_rc(vwa_chain_launch(reinterpret_cast<const ChainParams*>(desc.data_ptr()), (int)n_phases, (int)lds, cus,
+                            cur_stream(like)),
+           "chain");
 }
 
 void rmsnorm(Tensor x, c10::optional<Tensor> residual, c10::optional<Tensor> residual_out, c10::optional<Tensor> w,
@@ -505,6 +598,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("eps"), py::arg("n_q_heads"), py::arg("n_kv_heads"), py::arg("head_dim"), py::arg("use_rope"),
         py::arg("positions"), py::arg("slots"), py::arg("rope"), py::arg("q_out"), py::arg("k_cache"),
         py::arg("v_cache"), py::arg("w_scale") = py::none(), py::arg("ln_c") = py::none());
+  m.def("chain_make", &chain_make, py::arg("h"), py::arg("att"), py::arg("act"), py::arg("w_o"), py::arg("w_gu"),
+        py::arg("w_down"), py::arg("eps"), py::arg("w_qkv"), py::arg("n_q_heads"), py::arg("n_kv_heads"),
+        py::arg("head_dim"), py::arg("positions"), py::arg("slots"), py::arg("rope"), py::arg("q_out"),
+        py::arg("k_cache"), py::arg("v_cache"), py::arg("bar"), py::arg("work"), py::arg("ts") = py::none(), py::arg("bar_mode") = 1);
+  m.def("chain_run", &chain_run);
   m.def("rmsnorm", &rmsnorm);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);

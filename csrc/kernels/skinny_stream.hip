@@ -46,7 +46,25 @@ struct EpiPre {
   int64_t slot = -1;
 };
 
-template <int EPI, int NT>
+// In-launch hand-off accessors (chain kernel): agent-scope relaxed atomics compile to sc1 loads /
+// stores, which bypass the non-coherent per-XCD L2 state another workgroup could have left.
+template <bool SC1>
+VWA_DEVICE u16 ld_u16(const u16* p) {
+  if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool SC1>
+VWA_DEVICE void st_u16(u16* p, u16 v) {
+  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool SC1>
+VWA_DEVICE void st_f32(float* p, float v) {
+  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
+template <int EPI, int NT, bool SC1 = false>
 VWA_DEVICE void epi_values(const SkinnyParams& p, int tile, int o, EpiPre& e) {
   const int n0 = tile * 16 * NT;
   if constexpr (EPI == EPI_SWIGLU || EPI == EPI_QKV) {
@@ -70,7 +88,7 @@ VWA_DEVICE void epi_values(const SkinnyParams& p, int tile, int o, EpiPre& e) {
     if (o >= p.M * 16 * NT) return;
     const int m = o / (16 * NT), nn = o % (16 * NT);
     if (p.w_scale) e.cs0 = p.w_scale[n0 + nn];
-    if constexpr (EPI == EPI_RESID) e.r = bf2f(p.R[(size_t)m * p.ldr + n0 + nn]);
+    if constexpr (EPI == EPI_RESID) e.r = bf2f(ld_u16<SC1>(p.R + (size_t)m * p.ldr + n0 + nn));
   }
 }
 
@@ -78,9 +96,10 @@ VWA_DEVICE void epi_values(const SkinnyParams& p, int tile, int o, EpiPre& e) {
 // / LayerNorm rstd and, on the fp8 path, the activation quantisation scale); mus[m] (folded
 // LayerNorm only, else null): row mean, removed as mean * ln_c[n]; column scales (fp8) come
 // with the epilogue operands (`pre` when this is the workgroup's first tile).
-template <int EPI, int NT, int KS>
+template <int EPI, int NT, int KS, bool SC1 = false>
 VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs, const float* mus, int tile,
-                              f32x4 (&acc)[NT], int w, int lane, const EpiPre& pre, bool first) {
+                              f32x4 (&acc)[NT], int w, int lane, const EpiPre& pre, bool first,
+                              const float* partner = nullptr) {
   const int M = p.M;
   const int n0 = tile * 16 * NT;
 #pragma unroll
@@ -94,12 +113,14 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
     float s = 0.f;
 #pragma unroll
     for (int ww = 0; ww < KS; ++ww) s += red[((ww * NT + nt) * 4 + i) * 64 + ln];
+    // split tile (chain kernel): the other workgroup's partial sums, published with sc1 stores
+    if (partner) s += __hip_atomic_load(partner + m * 16 * NT + nn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return s;
   };
   auto operands = [&](int o) {
     if (first && o == (int)threadIdx.x) return pre;
     EpiPre e;
-    epi_values<EPI, NT>(p, tile, o, e);
+    epi_values<EPI, NT, SC1>(p, tile, o, e);
     return e;
   };
   if constexpr (EPI == EPI_SWIGLU) {
@@ -112,7 +133,7 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
         gv += bf2f(p.bias[n0 + q]);
         uv += bf2f(p.bias[n0 + 16 + q]);
       }
-      reinterpret_cast<u16*>(p.Y)[(size_t)m * p.ldy + tile * 16 + q] = f2bf(silu(gv) * uv);
+      st_u16<SC1>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + tile * 16 + q, f2bf(silu(gv) * uv));
     }
   } else if constexpr (EPI == EPI_QKV) {
     const int hd = p.head_dim, half = hd >> 1;
@@ -138,14 +159,14 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
       if (p.use_rope && !is_v) v = (q < 8) ? (v * e.rc - pv * e.rsn) : (v * e.rc + pv * e.rsn);
       const u16 out = f2bf(v);
       if (head < p.n_q_heads) {
-        p.q_out[(size_t)m * p.ldq + head * hd + d] = out;
+        st_u16<SC1>(p.q_out + (size_t)m * p.ldq + head * hd + d, out);
       } else {
         const int64_t slot = e.slot;
         if (slot >= 0) {
           const int64_t blk = slot / p.block_size, off = slot % p.block_size;
           const int kvh = is_v ? head - p.n_q_heads - p.n_kv_heads : head - p.n_q_heads;
           const int64_t idx = blk * p.cache_stride_block + kvh * p.cache_stride_head + off * p.cache_stride_tok + d;
-          (is_v ? p.v_cache : p.k_cache)[idx] = out;
+          st_u16<SC1>((is_v ? p.v_cache : p.k_cache) + idx, out);
         }
       }
     }
@@ -160,8 +181,8 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
       if (p.bias) v += bf2f(p.bias[n]);
       if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
       if constexpr (EPI == EPI_RESID) v += e.r;
-      if (p.y_f32) reinterpret_cast<float*>(p.Y)[(size_t)m * p.ldy + n] = v;
-      else reinterpret_cast<u16*>(p.Y)[(size_t)m * p.ldy + n] = f2bf(v);
+      if (p.y_f32) st_f32<SC1>(reinterpret_cast<float*>(p.Y) + (size_t)m * p.ldy + n, v);
+      else st_u16<SC1>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + n, f2bf(v));
     }
   }
   __syncthreads();
@@ -482,6 +503,343 @@ int launch_fp8(const SkinnyParams& p, hipStream_t st, int grid_cap) {
   return 0;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Chained phases (decode, M <= 4 rows): the GEMM tail of a Llama layer -- o_proj + residual ->
+// RMSNorm + gate/up + SwiGLU -> down + residual [-> RMSNorm + QKV + RoPE + KV write of the next
+// layer] -- as ONE persistent launch, the phases separated by grid barriers.  What this buys
+// over separate launches is the weight stream: before a workgroup waits at a barrier it has
+// already issued the first weight item of the next phase (weights never depend on the
+// activations), so the HBM pipe keeps streaming through the barrier, and the next phase has no
+// launch boundary.  Activations crossing a barrier are written and read with sc1 (agent-scope)
+// accesses; the barrier itself is an arrival counter + generation word with bounded spins (a
+// timed-out spin sets an error word instead of hanging the GPU).  All workgroups must be
+// co-resident: the grid is one workgroup per CU.
+// ------------------------------------------------------------------------------------------
+constexpr int kChainSpinLimit = 1 << 18;  // ~0.3 s: a lost workgroup ends the launch, not the GPU
+
+// Grid barrier on monotonic 64-bit tickets (no reset, no generation word, never wraps): a
+// workgroup's ticket t on its counter tells it which barrier instance it is in, so it can wait for
+// that instance's completion count directly.  bar (u64 words, each in its own 128-byte line):
+// flat mode uses [0]; two-level mode puts group g (block id mod 8, one per XCD under round-robin
+// dispatch) at [16 g] and the top counter at [128]; [160] is the timeout flag.
+// Measured (tools/chain_probe.py): a reset + generation barrier cost 5-7 us from the last
+// arrival to release (four dependent agent-scope round trips).
+constexpr int kBarTop = 128, kBarErr = 160;
+
+VWA_DEVICE unsigned long long chain_arrive(unsigned long long* bar, int nwg, int mode) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are performed
+  __syncthreads();
+  unsigned long long target = 0;
+  if (threadIdx.x == 0) {
+    if (mode == 0) {
+      const unsigned long long t = __hip_atomic_fetch_add(&bar[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      target = (t / (unsigned long long)nwg + 1ull) * (unsigned long long)nwg;
+    } else {
+      const int grp = blockIdx.x & 7;
+      const unsigned long long members = (unsigned long long)((nwg - grp + 7) >> 3);
+      const unsigned long long ngroups = (unsigned long long)(nwg < 8 ? nwg : 8);
+      const unsigned long long t =
+          __hip_atomic_fetch_add(&bar[16 * grp], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t % members == members - 1ull)
+        __hip_atomic_fetch_add(&bar[kBarTop], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      target = (t / members + 1ull) * ngroups;
+    }
+  }
+  return target;
+}
+
+VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, int mode) {
+  if (threadIdx.x == 0) {
+    unsigned long long* w = mode == 0 ? &bar[0] : &bar[kBarTop];
+    int spins = 0;
+    while ((long long)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kChainSpinLimit) {
+        __hip_atomic_store(&bar[kBarErr], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Work distribution (measured: with whole tiles per workgroup, gate/up's 896 tiles over 256
+// workgroups left half of them a fourth tile -- 65 us max vs 54 us median): a phase is a list of
+// ntiles x nb units (unit = one k-batch of every wave's K slice of a tile) and workgroup b takes
+// the contiguous range [units*b/grid, units*(b+1)/grid).  A tile whose units straddle two ranges
+// is finished by whichever of its two workgroups arrives second: both publish their reduced
+// partial tile (sc1 stores) into a per-tile slot and draw a ticket; the second adds the other
+// slot to its own sums and runs the epilogue.  The host guarantees <= 2 workgroups per tile.
+struct PhaseRange {
+  int u0, n_items, gb, ge;
+};
+
+template <int KS>
+VWA_DEVICE PhaseRange chain_range(const ChainPhase& ph) {
+  PhaseRange r;
+  const int w = threadIdx.x >> 6;
+  const int G = ph.p.K / 128;
+  r.gb = (G * w) / KS;
+  r.ge = (G * (w + 1)) / KS;
+  const long long units = (long long)(ph.p.N / (16 * ph.nt)) * ph.nb;
+  r.u0 = (int)(units * blockIdx.x / gridDim.x);
+  r.n_items = (int)(units * (blockIdx.x + 1) / gridDim.x) - r.u0;
+  return r;
+}
+
+// weight item `it` (unit u0 + it) of phase p into the registers wr (NT * U <= 4 groups of 4)
+template <int NT, int U>
+VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[16], int it, const PhaseRange& r) {
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.W), (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
+  const int lane = threadIdx.x & 63, nl = lane & 15, g = lane >> 4;
+  const int unit = r.u0 + it;
+  const int tile = unit / nb, b = unit % nb;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int kg = r.gb + b * U + u;
+    const bool ok = (it < r.n_items) && (kg < r.ge);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const unsigned row = (unsigned)(tile * 16 * NT + nt * 16 + nl);
+      const unsigned base = (row * (unsigned)p.K + (unsigned)(kg * 128 + 32 * g)) * 2u;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) wr[(nt * U + u) * 4 + s] = bload(rw, ok ? base + 16u * s : kOOB);
+    }
+  }
+}
+
+template <int EPI>
+struct PhaseShape {
+  static constexpr int NT = EPI == EPI_SWIGLU ? 2 : 1;
+  // (measured: QKV in half-tile units -- 384 tiles -> 3 units per workgroup, one split tile each --
+  // was 12.5 us vs 6.7 median / 11.5 max with whole tiles: it is bandwidth-bound either way)
+  static constexpr int U = 4 / NT;
+};
+
+template <int EPI, int KS>
+VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[16]) {
+  const PhaseRange r = chain_range<KS>(ph);
+  chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U>(ph.p, ph.nb, wr, 0, r);
+}
+
+// partial tile of a split tile: cross-wave sums of this workgroup's units -> slot (sc1)
+template <int NT, int KS>
+VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[((w * NT + nt) * 4 + i) * 64 + lane] = acc[nt][i];
+  __syncthreads();
+  for (int o = threadIdx.x; o < M * 16 * NT; o += KS * 64) {
+    const int m = o / (16 * NT), nn = o % (16 * NT);
+    const int nt = nn >> 4, q = nn & 15;
+    const int ln = q + 16 * (m >> 2), i = m & 3;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < KS; ++ww) v += red[((ww * NT + nt) * 4 + i) * 64 + ln];
+    st_f32<true>(slot + o, v);
+  }
+  __syncthreads();
+}
+
+// One phase.  X0 holds this phase's item 0 (issued before the barrier wait).
+template <int EPI, int KS>
+VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4 (&X1)[16], char* smem) {
+  constexpr int NT = PhaseShape<EPI>::NT, U = PhaseShape<EPI>::U;
+  const ChainPhase& ph = cp.ph[i];
+  const SkinnyParams& p = ph.p;
+  const int nb = ph.nb, M = p.M, K = p.K;
+  const int xstride = K + 8;
+  u16* xs = reinterpret_cast<u16*>(smem);
+  const int xbytes = ((M * xstride * 2) + 15) & ~15;
+  float* red = reinterpret_cast<float*>(smem + xbytes);
+  float* rs = red + KS * NT * 4 * 64;
+  int* s_flag = reinterpret_cast<int*>(rs + 16);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nl = lane & 15, g = lane >> 4;
+  const PhaseRange r = chain_range<KS>(ph);
+  const int first_tile = r.u0 / nb;
+
+  EpiPre pre;
+  if (r.n_items > 0) epi_values<EPI, NT, true>(p, first_tile, threadIdx.x, pre);
+  // ---- stage X (written by the previous phase: sc1 loads) + RMSNorm row scales
+  const int k8 = K / 8;
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.X), (short)0, (int)((size_t)M * p.ldx * 2), 0x00020000);
+  for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
+    const int m = c / k8, kk = c % k8;
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(((size_t)m * p.ldx + kk * 8) * 2), 0, 16);
+    *reinterpret_cast<uint4*>(xs + m * xstride + kk * 8) = make_uint4(v.x, v.y, v.z, v.w);
+  }
+  __syncthreads();
+  for (int m = w; m < 16; m += KS) {
+    float sc = 1.f;
+    if (p.fuse_rms && m < M) {
+      float s = 0.f;
+      for (int kk = lane; kk < k8; kk += 64) {
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(xs + m * xstride + kk * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += f[j] * f[j];
+      }
+      sc = rsqrtf(wave_sum(s) / (float)K + p.eps);
+    }
+    if (lane == 0) rs[m] = sc;
+  }
+  __syncthreads();
+
+  f32x4 acc[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](const uint4 (&wr)[16], int it) {
+    const int b = (r.u0 + it) % nb;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kg = r.gb + b * U + u;
+      if (kg >= r.ge) break;  // wave-uniform
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        uint4 a = make_uint4(0, 0, 0, 0);
+        if (nl < M) a = *reinterpret_cast<const uint4*>(xs + nl * xstride + kg * 128 + 32 * g + 8 * s);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16(as_bf16x8(a), as_bf16x8(wr[(nt * U + u) * 4 + s]), acc[nt]);
+      }
+    }
+  };
+  const int u1 = r.u0 + r.n_items;
+  auto finish = [&](int it) {
+    const int unit = r.u0 + it;
+    const int tile = unit / nb;
+    if (unit % nb != nb - 1 && it != r.n_items - 1) return;  // tile continues in this range
+    const bool whole = tile * nb >= r.u0 && (tile + 1) * nb <= u1;
+    if (whole) {
+      tile_epilogue<EPI, NT, KS, true>(p, red, rs, nullptr, tile, acc, w, lane, pre, tile == first_tile);
+      return;
+    }
+    // split tile: publish, ticket, the second arriver finishes it
+    const int mine = tile * nb >= r.u0 ? 0 : 1;  // slot 0: owner of the tile's first unit
+    const int per = M * 16 * NT;
+    float* slots = cp.part + (size_t)tile * 2 * per;
+    tile_publish<NT, KS>(M, red, acc, slots + mine * per);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned t = __hip_atomic_fetch_add(&cp.tickets[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == 1u;
+      if (last) __hip_atomic_store(&cp.tickets[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *s_flag = last;
+    }
+    __syncthreads();
+    if (*s_flag) {
+      tile_epilogue<EPI, NT, KS, true>(p, red, rs, nullptr, tile, acc, w, lane, pre, false,
+                                       slots + (1 - mine) * per);
+    } else {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  // items in pairs (X0, X1); an odd count is padded with one all-OOB item (zero weights, no
+  // traffic, no epilogue)
+  const int n_pad = (r.n_items + 1) & ~1;
+  for (int it = 0; it < n_pad; it += 2) {
+    chain_load<NT, U>(p, nb, X1, it + 1, r);
+    compute(X0, it);
+    finish(it);
+    if (it + 2 < n_pad) chain_load<NT, U>(p, nb, X0, it + 2, r);
+    compute(X1, it + 1);
+    if (it + 1 < r.n_items) finish(it + 1);
+  }
+}
+
+// The phase sequence is static (the Llama layer tail: o_proj+residual, gate/up+SwiGLU,
+// down+residual [, next layer's QKV]); a runtime epilogue switch measured 50+ VGPR spills.
+template <int KS, bool WITH_QKV>
+__global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __restrict__ cpp) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const ChainParams& cp = *cpp;  // device-resident descriptor
+  uint4 A[16], B[16];
+  // barrier = arrive (stores drained), issue the next phase's first weight item, then wait: the
+  // weight stream is in flight while the slowest workgroup finishes
+  const int nwg = (int)gridDim.x;
+  unsigned long long gen;
+  unsigned long long* bar = reinterpret_cast<unsigned long long*>(cp.bar);
+  int nts = 0;
+  auto stamp = [&]() {
+    if (cp.ts && threadIdx.x == 0) cp.ts[blockIdx.x * 16 + nts] = __builtin_amdgcn_s_memrealtime();
+    ++nts;
+  };
+  stamp();
+  chain_issue_first<EPI_RESID, KS>(cp.ph[0], A);
+  chain_phase<EPI_RESID, KS>(cp, 0, A, B, smem);
+  stamp();
+  gen = chain_arrive(bar, nwg, cp.bar_mode);
+  chain_issue_first<EPI_SWIGLU, KS>(cp.ph[1], A);
+  chain_wait(bar, gen, cp.bar_mode);
+  stamp();
+  chain_phase<EPI_SWIGLU, KS>(cp, 1, A, B, smem);
+  stamp();
+  gen = chain_arrive(bar, nwg, cp.bar_mode);
+  chain_issue_first<EPI_RESID, KS>(cp.ph[2], A);
+  chain_wait(bar, gen, cp.bar_mode);
+  stamp();
+  chain_phase<EPI_RESID, KS>(cp, 2, A, B, smem);
+  stamp();
+  if constexpr (WITH_QKV) {
+    gen = chain_arrive(bar, nwg, cp.bar_mode);
+    chain_issue_first<EPI_QKV, KS>(cp.ph[3], A);
+    chain_wait(bar, gen, cp.bar_mode);
+    stamp();
+    chain_phase<EPI_QKV, KS>(cp, 3, A, B, smem);
+    stamp();
+  }
+}
+
+}  // namespace
+
+// Host side: fill nt / nb of every phase and return the dynamic LDS bytes the chain needs, or
+// -10 when a phase does not fit (X rows must fit in LDS next to the reduction scratch, M <= 4,
+// K % 128 == 0, bf16 weights).  The filled descriptor is then copied to device memory once and
+// launched with vwa_chain_launch (graph-capturable: no allocation, no copy at launch).
+extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
+  constexpr int KS = 8;
+  if (cp->n < 3 || cp->n > kChainMaxPhases || grid < 1) return -10;
+  static const int kSeq[kChainMaxPhases] = {EPI_RESID, EPI_SWIGLU, EPI_RESID, EPI_QKV};
+  size_t lds = 0;
+  for (int i = 0; i < cp->n; ++i) {
+    ChainPhase& ph = cp->ph[i];
+    const SkinnyParams& p = ph.p;
+    if (ph.epi != kSeq[i]) return -10;
+    ph.nt = (ph.epi == EPI_SWIGLU) ? 2 : 1;
+    const int U = 4 / ph.nt;
+    if (p.M < 1 || p.M > 4 || p.K % 128 != 0 || p.N % (16 * ph.nt) != 0 || p.w_scale || p.fuse_rms == 2) return -10;
+    if ((size_t)p.N * p.K * 2 >= 0x7FFFFFF0ull || (size_t)p.M * p.ldx * 2 >= 0x7FFFFFF0ull) return -10;
+    const int G = p.K / 128;
+    const int per_wave = (G + KS - 1) / KS;
+    ph.nb = (per_wave + U - 1) / U;
+    const long long ntiles = p.N / (16 * ph.nt);
+    const long long units = ntiles * ph.nb;
+    // a tile may straddle at most two workgroup ranges (two partial slots per tile)
+    if (ph.nb > 1 && units / grid < ph.nb - 1) return -10;
+    if (ntiles > cp->max_tiles || (size_t)ntiles * 2 * p.M * 16 * ph.nt > (size_t)cp->part_floats) return -10;
+    const size_t x = ((size_t)p.M * (p.K + 8) * 2 + 15) & ~(size_t)15;
+    const size_t need = x + (size_t)(KS * ph.nt * 4 * 64 + 32) * sizeof(float);
+    if (need > lds) lds = need;
+  }
+  if (lds > 160 * 1024) return -10;
+  return (int)lds;
+}
+
+extern "C" int vwa_chain_launch(const ChainParams* d_cp, int n_phases, int lds, int grid, hipStream_t st) {
+  if (n_phases == 4) hipLaunchKernelGGL((chain_kernel<8, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+  else if (n_phases == 3) hipLaunchKernelGGL((chain_kernel<8, false>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+  else return -10;
+  return (int)hipGetLastError();
+}
+
+namespace {
 }  // namespace
 
 // Returns -10 when this shape does not fit the streaming kernel (caller falls back).

@@ -120,3 +120,37 @@ def test_llama_fp8_gpu_engine_matches_cpu_emulation():
     for i, (a, b) in enumerate(zip(got, ref)):
         err = (a - b).abs().max().item()
         assert err < 0.08 * (1 + b.abs().max().item()), (i, err)
+
+
+@pytest.mark.parametrize("cfg", [CFG, LlamaConfig(name="t8", vocab_size=4096, hidden=4096, n_layers=2, n_heads=32,
+                                                  n_kv_heads=8, head_dim=128, ffn=14336, max_pos=2048)],
+                         ids=["small", "llama8b-layers"])
+def test_chained_layer_tail_matches_per_kernel_path(cfg, monkeypatch):
+    """The chained decode launch (o_proj -> gate/up -> down -> next layer's QKV behind grid
+    barriers, skinny_stream.hip chain_kernel) against the per-kernel path on the same weights,
+    for 1, 2 and 4 rows (the small config leaves most workgroups without a tile; the 8B-shaped
+    one gives them several items per phase)."""
+    ops.ext()
+    torch.manual_seed(0)
+    toks = torch.randint(0, cfg.vocab_size, (40,)).tolist()
+    model = LlamaModel(cfg, device="cuda", seed=2)
+
+    def run(chain: bool):
+        monkeypatch.setenv("VWA_CHAIN", "1" if chain else "0")
+        e = LLMEngine(model, max_seqs=2, max_model_len=256, kv_blocks=20, block_size=16)
+        s = e.new_sequence(toks[:30], use_prefix_cache=False)
+        e.prefill(s)
+        out, i = [], 30
+        for n in (1, 2, 4, 1):
+            out.append(e.run_rows([(s, t) for t in toks[i:i + n]]).float().cpu().clone())
+            i += n
+        e.free_sequence(s, publish=False)
+        return out
+
+    ref = run(False)
+    got = run(True)
+    assert not model.chain_error()
+    assert model._chains and all(v is not None for v in model._chains.values())
+    for a, b in zip(got, ref):
+        err = (a - b).abs().max().item()
+        assert err < 0.02 * (1 + b.abs().max().item()), err

@@ -1,0 +1,80 @@
+"""Chained layer-tail launch vs separate launches on Llama-3-8B decode shapes (M rows), with
+per-phase s_memrealtime stamps (100 MHz) from every workgroup of the chained kernel.
+
+    python tools/chain_probe.py [--rows 1] [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import voice_enabled_browser_automation_amd.ops as ops  # noqa: E402
+from tools.bench_kernels import timeit  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1)
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--bar-mode", type=int, default=1)
+    a = ap.parse_args()
+    dev, bf = "cuda", torch.bfloat16
+    E = ops.ext()
+    torch.manual_seed(0)
+    M, d, F, nq, nkv, hd = a.rows, 4096, 14336, 32, 8, 128
+    ncopy = 3  # rotate weights over > 256 MB Infinity Cache
+    mk = lambda *s: (torch.randn(*s, device=dev) * 0.02).to(bf)  # noqa: E731
+    Ws = [dict(o=mk(d, nq * hd), gu=mk(2 * F, d), down=mk(d, F), qkv=mk((nq + 2 * nkv) * hd, d)) for _ in range(ncopy)]
+    h, att, act = mk(M, d), mk(M, nq * hd), mk(M, F)
+    q = torch.zeros(M, nq * hd, dtype=bf, device=dev)
+    kc = torch.zeros(64, nkv, 16, hd, dtype=bf, device=dev)
+    vc = torch.zeros_like(kc)
+    pos = torch.arange(M, dtype=torch.int32, device=dev)
+    slots = torch.arange(M, dtype=torch.int64, device=dev)
+    rope = ops.rope_table(4096, hd, 5e5, device=dev)
+    bar = torch.zeros(512, dtype=torch.int32, device=dev)
+    ts = torch.zeros(1024 * 16, dtype=torch.int64, device=dev)
+    work = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
+    descs = [E.chain_make(h, att, act, w["o"], w["gu"], w["down"], 1e-5, w["qkv"], nq, nkv, hd, pos, slots, rope, q,
+                          kc, vc, bar, work, ts, a.bar_mode) for w in Ws]
+    it = [0]
+
+    def chained():
+        it[0] = (it[0] + 1) % ncopy
+        dsc, lds = descs[it[0]]
+        E.chain_run(dsc, 4, lds, h)
+
+    def separate():
+        it[0] = (it[0] + 1) % ncopy
+        w = Ws[it[0]]
+        ops.linear(att, w["o"], out=h, residual=h)
+        ops.linear_swiglu(h, w["gu"], fuse_rms=True, eps=1e-5, out=act)
+        ops.linear(act, w["down"], out=h, residual=h)
+        ops.qkv_rope_write(h, w["qkv"], None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
+                           rope=rope, positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc)
+
+    t_sep = timeit(separate)
+    t_ch = timeit(chained)
+    assert int(bar.view(torch.int64)[160].item()) == 0, "barrier timeout"
+    # stamps of the last launch: [start, end0, wait0, end1, wait1, end2, wait2, end3]
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    st = ts.view(-1, 16)[:cus, :8].double().cpu()
+    st = (st - st[:, :1].min()) * 10e-3  # us
+    med = st.median(dim=0).values.tolist()
+    mx = st.max(dim=0).values.tolist()
+    mn = st.min(dim=0).values.tolist()
+    r = dict(kernel="chain_probe", rows=M, bar_mode=a.bar_mode, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
+             stamps_med_us=[round(x, 2) for x in med], stamps_min_us=[round(x, 2) for x in mn],
+             stamps_max_us=[round(x, 2) for x in mx],
+             legend="start,end_o,wait_o,end_gu,wait_gu,end_down,wait_down,end_qkv")
+    print(json.dumps(r), flush=True)
+    if a.json:
+        with open(a.json, "a") as f:
+            f.write(json.dumps(r) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -159,6 +159,39 @@ class LlamaModel:
                 ops.linear(x, w, out=h)
             self.tp.all_reduce(h)
 
+    # ---- chained layer tail (o_proj -> gate/up -> down -> next QKV in one launch; M <= 4 rows)
+    def _chain_ok(self, M: int) -> bool:
+        return (M <= 4 and self.tp.size == 1 and self.wdtype == "bf16" and self.device.type == "cuda"
+                and ops.env_flag("VWA_CHAIN", True) and ops.native_available())
+
+    def _chain_desc(self, bufs, kv, M: int, li: int):
+        """(descriptor, n_phases, lds) of layer li's chained tail for this engine's buffers,
+        built on first use (an eager warm-up call precedes every graph capture)."""
+        cache = self.__dict__.setdefault("_chains", {})
+        key = (id(bufs), id(kv), M, li)
+        if key in cache:
+            return cache[key]
+        if getattr(self, "_chain_bar", None) is None:
+            self._chain_bar = torch.zeros(512, dtype=torch.int32, device=self.device)
+            # split-tile tickets + partial slots (ops: skinny_stream.hip chain_phase)
+            self._chain_work = torch.zeros(1 << 20, dtype=torch.int32, device=self.device)
+        L = self.layers[li]
+        nxt = li + 1 < len(self.layers)
+        N = self.layers[li + 1] if nxt else None
+        desc, lds = ops.ext().chain_make(
+            bufs.hidden[:M], bufs.attn[:M], bufs.act[:M], L.o, L.gu, L.down, self.cfg.rms_eps,
+            N.qkv if nxt else None, self.nq, self.nkv, self.hd,
+            bufs.positions if nxt else None, bufs.slots if nxt else None, self.rope if nxt else None,
+            bufs.q[:M] if nxt else None, kv.k[li + 1] if nxt else None, kv.v[li + 1] if nxt else None,
+            self._chain_bar, self._chain_work)
+        cache[key] = (desc, 4 if nxt else 3, lds) if desc.numel() else None
+        return cache[key]
+
+    def chain_error(self) -> bool:
+        """True when a chained launch's grid barrier timed out (results of that step are invalid)."""
+        bar = getattr(self, "_chain_bar", None)
+        return bool(bar is not None and int(bar.view(torch.int64)[160].item()) != 0)
+
     def forward(self, bufs, M: int, kv, *, prefill_seq: Optional[int] = None, q_offset: int = 0,
                 logits_rows: Optional[slice] = None, n_sel: Optional[int] = None) -> torch.Tensor:
         """Run M token rows described by ``bufs`` (runtime.buffers.StepBuffers).
@@ -174,11 +207,15 @@ class LlamaModel:
         ops.embedding(bufs.tokens, self.embed, out=h, rows=M)
         qbuf = bufs.q[:M] if M <= bufs.q.shape[0] else torch.empty((M, self.nq * self.hd), dtype=self.dtype,
                                                                       device=self.device)
+        chain = prefill_seq is None and self._chain_ok(M)
         for li, L in enumerate(self.layers):
             kc, vc = kv.k[li], kv.v[li]
-            q = ops.qkv_rope_write(h, L.qkv, None, fuse_rms=True, eps=cfg.rms_eps, n_q_heads=self.nq,
-                                   n_kv_heads=self.nkv, head_dim=self.hd, rope=self.rope,
-                                   positions=bufs.positions, slots=bufs.slots, q_out=qbuf, k_cache=kc, v_cache=vc)
+            if chain and li > 0:
+                q = qbuf  # written by the previous layer's chained launch
+            else:
+                q = ops.qkv_rope_write(h, L.qkv, None, fuse_rms=True, eps=cfg.rms_eps, n_q_heads=self.nq,
+                                       n_kv_heads=self.nkv, head_dim=self.hd, rope=self.rope,
+                                       positions=bufs.positions, slots=bufs.slots, q_out=qbuf, k_cache=kc, v_cache=vc)
             if prefill_seq is None:
                 attn = bufs.attn[:M]
                 ops.decode_attention(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens, bufs.seq_ids,
@@ -192,6 +229,12 @@ class LlamaModel:
                 ops.flash_attention(q4, ops.KVLayout.paged(kc, vc, table), Sk=q_offset + M, n_kv_heads=self.nkv,
                                     causal=True, scale=self.scale, q_offset=q_offset, out=attn4)
                 attn = attn4.view(M, self.nq * self.hd)
+            if chain:
+                d = self._chain_desc(bufs, kv, M, li)
+                if d is not None:
+                    ops.ext().chain_run(d[0], d[1], d[2], h)
+                    continue
+                chain = False  # shapes the chain cannot take: per-kernel path from here on
             self._row_parallel(attn, L.o, h)
             act = bufs.act[:M] if M <= bufs.act.shape[0] else None
             act = ops.linear_swiglu(h, L.gu, fuse_rms=True, eps=cfg.rms_eps, out=act)
