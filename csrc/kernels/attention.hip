@@ -318,6 +318,14 @@ VWA_DEVICE uint2 lds_tr16(const unsigned char* ptr) {
   return __builtin_bit_cast(uint2, v);
 }
 
+// 16-byte global load through a native vector type: a struct (uint4) copy is emitted as a memcpy
+// that SROA cannot promote, and the V staging registers ended up in scratch (measured: 272 B of
+// scratch per lane and a vmcnt(0) after every scratch reload inside the key loop)
+VWA_DEVICE uint4 ld128(const u16* ptr) {
+  const u32x4 v = *reinterpret_cast<const u32x4*>(ptr);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 VWA_DEVICE void st_sc1_f4(__amdgpu_buffer_rsrc_t r, int64_t idx, const float* v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_float4(v[0], v[1], v[2], v[3])), r,
                                          (int)(idx * 4), 0, 16);
@@ -412,13 +420,13 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
       const int key = min(kb + 8 * (n >> 2) + 4 * t + (n & 3), kmax);
       const u16* kp = p.kv.k + kv_off(key) + 8 * g;
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) kr[t][ks] = *reinterpret_cast<const uint4*>(kp + 32 * ks);
+      for (int ks = 0; ks < NKS; ++ks) kr[t][ks] = ld128(kp + 32 * ks);
     }
 #pragma unroll
     for (int i = 0; i < NVL; ++i) {
       const int idx = i * 64 + lane;
       const int key = min(kb + idx / NCH, kmax);
-      vr[i] = *reinterpret_cast<const uint4*>(p.kv.v + kv_off(key) + 8 * (idx % NCH));
+      vr[i] = ld128(p.kv.v + kv_off(key) + 8 * (idx % NCH));
     }
   };
 
