@@ -614,7 +614,8 @@ template <int EPI>
 struct PhaseShape {
   static constexpr int NT = EPI == EPI_SWIGLU ? 2 : 1;
   // (measured: QKV in half-tile units -- 384 tiles -> 3 units per workgroup, one split tile each --
-  // was 12.5 us vs 6.7 median / 11.5 max with whole tiles: it is bandwidth-bound either way)
+  // 12.5-13.4 us vs 6.7 median / 11.5 max with whole tiles, also with the split tile processed
+  // first and published before the next item's loads under a counted vmcnt)
   static constexpr int U = 4 / NT;
 };
 

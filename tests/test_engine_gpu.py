@@ -154,3 +154,20 @@ def test_chained_layer_tail_matches_per_kernel_path(cfg, monkeypatch):
     for a, b in zip(got, ref):
         err = (a - b).abs().max().item()
         assert err < 0.02 * (1 + b.abs().max().item()), err
+
+
+def test_chain_timeout_falls_back_to_per_kernel_launches():
+    """A grid-barrier timeout (error word set by the chained kernel) switches the model to the
+    per-kernel path and drops the captured graphs (runtime/engine.py _check_chain)."""
+    ops.ext()
+    model = LlamaModel(CFG, device="cuda", seed=4)
+    e = LLMEngine(model, max_seqs=1, max_model_len=128, kv_blocks=10, block_size=16)
+    s = e.new_sequence(list(range(10)), use_prefix_cache=False)
+    e.prefill(s)
+    a = e.run_rows([(s, 11)]).float().cpu()
+    assert model._chains and not model.chain_error()
+    model._chain_bar.view(torch.int64)[160] = 1  # what a timed-out spin writes
+    e._check_chain()
+    assert e.stats.get("chain_fallbacks") == 1 and not e.graphs and not model._chain_ok(1)
+    b = e.run_rows([(s, 12)]).float().cpu()
+    assert torch.isfinite(a).all() and torch.isfinite(b).all()

@@ -162,7 +162,12 @@ class LlamaModel:
     # ---- chained layer tail (o_proj -> gate/up -> down -> next QKV in one launch; M <= 4 rows)
     def _chain_ok(self, M: int) -> bool:
         return (M <= 4 and self.tp.size == 1 and self.wdtype == "bf16" and self.device.type == "cuda"
-                and ops.env_flag("VWA_CHAIN", True) and ops.native_available())
+                and not getattr(self, "_chain_disabled", False) and ops.env_flag("VWA_CHAIN", True)
+                and ops.native_available())
+
+    def disable_chain(self) -> None:
+        self._chain_disabled = True
+        self._chains = {}
 
     def _chain_desc(self, bufs, kv, M: int, li: int):
         """(descriptor, n_phases, lds) of layer li's chained tail for this engine's buffers,

@@ -266,9 +266,24 @@ class LLMEngine:
             self.seqs[sid].n_computed = ln
         self.stats["steps"] += 1
         self.stats["rows"] += n
+        if self.stats["steps"] % 64 == 0:
+            self._check_chain()
         if L == M and nl != n:
             return out[torch.tensor(logits_for, device=out.device)]
         return out[:nl]
+
+    def _check_chain(self) -> None:
+        """Health check of the chained decode launch (models/llama.py): a grid-barrier spin that
+        timed out (workgroups not co-resident, e.g. another persistent kernel on the GPU) leaves an
+        error word; the model then falls back to per-kernel launches and the graphs are recaptured."""
+        m = self.model
+        if getattr(m, "chain_error", None) is not None and m.chain_error():
+            import warnings
+
+            warnings.warn("chained decode launch timed out at a grid barrier; using per-kernel launches")
+            m.disable_chain()
+            self.graphs.clear()
+            self.stats["chain_fallbacks"] = self.stats.get("chain_fallbacks", 0) + 1
 
     def prefill(self, seq: Sequence_, chunk: int = 2048, upto: Optional[int] = None) -> Optional[torch.Tensor]:
         """Compute K/V for seq.tokens[n_computed:upto] (default: all tokens); returns f32 logits
