@@ -271,6 +271,17 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   return {host.to(h.device()), (int64_t)lds};
 }
 
+// Device memory the L2 does not cache (hipDeviceMallocUncached): chain barrier words polled with
+// scalar loads.  Returned as an int32 tensor that frees the allocation with hipFree.
+Tensor alloc_uncached_i32(int64_t n, Tensor like) {
+  c10::DeviceGuard g(like.device());
+  void* ptr = nullptr;
+  TORCH_CHECK(hipExtMallocWithFlags(&ptr, (size_t)n * 4, hipDeviceMallocUncached) == hipSuccess, "uncached malloc");
+  TORCH_CHECK(hipMemset(ptr, 0, (size_t)n * 4) == hipSuccess, "memset");
+  return torch::from_blob(ptr, {n}, [](void* p) { (void)hipFree(p); },
+                          torch::dtype(torch::kInt).device(like.device()));
+}
+
 void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like) {
   c10::DeviceGuard g(like.device());
   TORCH_CHECK(desc.is_cuda() && desc.numel() == (int64_t)sizeof(ChainParams), "bad chain descriptor");
@@ -603,6 +614,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("head_dim"), py::arg("positions"), py::arg("slots"), py::arg("rope"), py::arg("q_out"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("bar"), py::arg("work"), py::arg("ts") = py::none(), py::arg("bar_mode") = 1);
   m.def("chain_run", &chain_run);
+  m.def("alloc_uncached_i32", &alloc_uncached_i32);
   m.def("rmsnorm", &rmsnorm);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);

@@ -550,6 +550,29 @@ VWA_DEVICE unsigned long long chain_arrive(unsigned long long* bar, int nwg, int
 }
 
 VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, int mode) {
+  if (mode == 2) {
+    // wave 0 polls with scalar loads (glc: past the scalar cache; bar lives in uncached memory so
+    // no L2 copy can be stale): SMEM completes on lgkmcnt, so the poll is not queued behind the
+    // next phase's weight loads this wave just issued (vmcnt retires in order)
+    if (threadIdx.x < 64) {
+      const unsigned long long tgt = __builtin_amdgcn_readfirstlane((unsigned)target) |
+                                     ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(target >> 32)) << 32);
+      const unsigned long long* top = &bar[kBarTop];
+      int spins = 0;
+      while (true) {
+        unsigned long long v;
+        asm volatile("s_load_dwordx2 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(top) : "memory");
+        if ((long long)(v - tgt) >= 0) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kChainSpinLimit) {
+          if (threadIdx.x == 0) __hip_atomic_store(&bar[kBarErr], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    return;
+  }
   if (threadIdx.x == 0) {
     unsigned long long* w = mode == 0 ? &bar[0] : &bar[kBarTop];
     int spins = 0;

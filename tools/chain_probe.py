@@ -35,7 +35,8 @@ def main():
     pos = torch.arange(M, dtype=torch.int32, device=dev)
     slots = torch.arange(M, dtype=torch.int64, device=dev)
     rope = ops.rope_table(4096, hd, 5e5, device=dev)
-    bar = torch.zeros(512, dtype=torch.int32, device=dev)
+    bar = E.alloc_uncached_i32(512, torch.empty(1, device=dev)) if a.bar_mode == 2 else \
+        torch.zeros(512, dtype=torch.int32, device=dev)
     ts = torch.zeros(1024 * 16, dtype=torch.int64, device=dev)
     work = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
     descs = [E.chain_make(h, att, act, w["o"], w["gu"], w["down"], 1e-5, w["qkv"], nq, nkv, hd, pos, slots, rope, q,
@@ -56,6 +57,9 @@ def main():
         ops.qkv_rope_write(h, w["qkv"], None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
                            rope=rope, positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc)
 
+    chained()  # one launch first: a broken barrier shows up as the error word, not a long run
+    torch.cuda.synchronize()
+    assert int(bar.view(torch.int64)[160].item()) == 0, "barrier timeout"
     t_sep = timeit(separate)
     t_ch = timeit(chained)
     assert int(bar.view(torch.int64)[160].item()) == 0, "barrier timeout"

@@ -177,7 +177,15 @@ class LlamaModel:
         if key in cache:
             return cache[key]
         if getattr(self, "_chain_bar", None) is None:
-            self._chain_bar = torch.zeros(512, dtype=torch.int32, device=self.device)
+            # barrier words in L2-uncached memory, polled with scalar loads (bar_mode 2: the poll
+            # does not queue behind the next phase's weight loads); plain memory + vector polls
+            # (bar_mode 1) if the uncached allocation is unavailable
+            try:
+                self._chain_bar = ops.ext().alloc_uncached_i32(512, torch.empty(1, device=self.device))
+                self._chain_bar_mode = 2
+            except RuntimeError:
+                self._chain_bar = torch.zeros(512, dtype=torch.int32, device=self.device)
+                self._chain_bar_mode = 1
             # split-tile tickets + partial slots (ops: skinny_stream.hip chain_phase)
             self._chain_work = torch.zeros(1 << 20, dtype=torch.int32, device=self.device)
         L = self.layers[li]
@@ -188,7 +196,7 @@ class LlamaModel:
             N.qkv if nxt else None, self.nq, self.nkv, self.hd,
             bufs.positions if nxt else None, bufs.slots if nxt else None, self.rope if nxt else None,
             bufs.q[:M] if nxt else None, kv.k[li + 1] if nxt else None, kv.v[li + 1] if nxt else None,
-            self._chain_bar, self._chain_work)
+            self._chain_bar, self._chain_work, None, self._chain_bar_mode)
         cache[key] = (desc, 4 if nxt else 3, lds) if desc.numel() else None
         return cache[key]
 
