@@ -354,6 +354,7 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
   // ---- row groups of the whole step (<= 64 rows; every wave derives the same answer): runs of
   //      consecutive rows of one sequence, cut every RG rows from the run's start
   const int sl = lane < p.rows ? p.seq_ids[lane] : -1;
+  const int cl = lane < p.rows ? p.ctx_lens[lane] : 0;  // same round trip as the sequence ids
   const int sp = __shfl(sl, lane > 0 ? lane - 1 : 0, 64);
   const unsigned long long run_starts = __ballot(lane < p.rows && (lane == 0 || sl != sp));
   const int run0 = 63 - __builtin_clzll(run_starts & ((2ull << lane) - 1ull));  // lane 0 always starts a run
@@ -376,7 +377,8 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
   const int nr = min(RG, run_end - r0);  // rows in this group
   const int seq = __shfl(sl, r0, 64);
   __syncthreads();  // the previous item's LDS readers are done
-  const int c_own = lane < nr ? p.ctx_lens[r0 + lane] : 0;
+  const int c_src = __shfl(cl, min(r0 + lane, 63), 64);
+  const int c_own = lane < nr ? c_src : 0;
   int ctxmax = c_own;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) ctxmax = max(ctxmax, __shfl_xor(ctxmax, o, 64));
