@@ -271,6 +271,21 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   return {host.to(h.device()), (int64_t)lds};
 }
 
+// One-row device-resident decode loop step (see elementwise.hip decode_advance_kernel)
+void decode_advance(Tensor tokens, Tensor positions, Tensor ctx_lens, Tensor slots, Tensor sampled, Tensor out,
+                    Tensor counter, int64_t base_block, int64_t block_size) {
+  c10::DeviceGuard g(tokens.device());
+  for (const Tensor* t : {&tokens, &positions, &ctx_lens, &sampled, &out, &counter})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->numel() >= 1, "int32 GPU tensors expected");
+  TORCH_CHECK(slots.is_cuda() && slots.scalar_type() == at::kLong && slots.numel() >= 1, "slots int64");
+  TORCH_CHECK(block_size > 0 && base_block >= 0, "bad block geometry");
+  check_rc(vwa_decode_advance(tokens.data_ptr<int>(), positions.data_ptr<int>(), ctx_lens.data_ptr<int>(),
+                              slots.data_ptr<int64_t>(), sampled.data_ptr<int>(), out.data_ptr<int>(),
+                              counter.data_ptr<int>(), (int)out.numel(), (int)base_block, (int)block_size,
+                              cur_stream(tokens)),
+           "decode_advance");
+}
+
 // Device memory the L2 does not cache (hipDeviceMallocUncached): chain barrier words polled with
 // scalar loads.  Returned as an int32 tensor that frees the allocation with hipFree.
 Tensor alloc_uncached_i32(int64_t n, Tensor like) {
@@ -615,6 +630,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("k_cache"), py::arg("v_cache"), py::arg("bar"), py::arg("work"), py::arg("ts") = py::none(), py::arg("bar_mode") = 1);
   m.def("chain_run", &chain_run);
   m.def("alloc_uncached_i32", &alloc_uncached_i32);
+  m.def("decode_advance", &decode_advance);
   m.def("rmsnorm", &rmsnorm);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);

@@ -313,3 +313,31 @@ extern "C" int vwa_embedding(const int* ids, const uint16_t* table, const uint16
                      pos_table, positions, out, rows, D, vocab_start, vocab_end);
   return (int)hipGetLastError();
 }
+
+// ---- device-resident greedy decode (Whisper): after a step's sampler, feed the sampled token
+// back as the next step's input and advance the row's position / context / KV slot, so a run of
+// decode steps replays back to back with no host round trip.  out[*counter] records the token.
+namespace {
+__global__ void decode_advance_kernel(int* tokens, int* positions, int* ctx_lens, int64_t* slots, const int* sampled,
+                                      int* out, int* counter, int max_out, int base_block, int block_size) {
+  if (threadIdx.x != 0) return;
+  const int tok = sampled[0];
+  const int c = counter[0];
+  if (c < max_out) out[c] = tok;
+  counter[0] = c + 1;
+  tokens[0] = tok;
+  const int pos = positions[0] + 1;
+  positions[0] = pos;
+  ctx_lens[0] = pos + 1;
+  slots[0] = (int64_t)(base_block + pos / block_size) * block_size + pos % block_size;
+}
+}  // namespace
+
+extern "C" int vwa_decode_advance(int* tokens, int* positions, int* ctx_lens, int64_t* slots, const int* sampled,
+                                  int* out, int* counter, int max_out, int base_block, int block_size,
+                                  hipStream_t st) {
+  hipLaunchKernelGGL(decode_advance_kernel, dim3(1), dim3(64), 0, st, tokens, positions, ctx_lens, slots, sampled, out,
+                     counter, max_out, base_block, block_size);
+  return (int)hipGetLastError();
+}
+

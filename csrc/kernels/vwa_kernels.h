@@ -119,6 +119,8 @@ int vwa_log_mel(const float* audio, int n_samples, int n_frames, const float* wi
 int vwa_conv1d_gelu_pos(const uint16_t* x, const uint16_t* w, const uint16_t* b, const uint16_t* pos, uint16_t* y,
                         int B, int Cin, int Tin, int Cout, int Tout, int stride, hipStream_t st);
 int vwa_attention_split_tokens();
+int vwa_decode_advance(int* tokens, int* positions, int* ctx_lens, int64_t* slots, const int* sampled,
+                       int* out, int* counter, int max_out, int base_block, int block_size, hipStream_t st);
 int vwa_quant_fp8_rows(const uint16_t* x, int ldx, int rows, int D, uint8_t* q, float* scale, hipStream_t st);
 // one-shot peer-to-peer all-reduce (allreduce.hip)
 void* vwa_ar_create(int rank, int world, int64_t max_elems);

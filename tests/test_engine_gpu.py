@@ -171,3 +171,23 @@ def test_chain_timeout_falls_back_to_per_kernel_launches():
     assert e.stats.get("chain_fallbacks") == 1 and not e.graphs and not model._chain_ok(1)
     b = e.run_rows([(s, 12)]).float().cpu()
     assert torch.isfinite(a).all() and torch.isfinite(b).all()
+
+
+def test_asr_device_decode_loop_matches_host_loop():
+    """The device-resident greedy loop (sampled token fed back on the GPU, decode_advance kernel,
+    step graphs replayed back to back) produces the same tokens as the host-driven loop, in the
+    fixed-work and the stop-at-EOT modes."""
+    ops.ext()
+    tok = load_tokenizer("whisper")
+    m = WhisperModel(get_config("whisper-test"), device="cuda", seed=3)
+    a = AsrEngine(m, tok, max_sessions=2)
+    pcm = (np.sin(np.arange(16000 * 2) * 2 * np.pi * 250 / 16000) * 6000).astype(np.int16)
+    audio = a.pcm_to_audio(pcm)
+    for kw in (dict(exact_tokens=12), dict(max_tokens=20)):
+        a.device_loop = False
+        host = a.transcribe(audio, **kw)
+        n_host = a.last_stats["tokens"]
+        a.device_loop = True
+        dev = a.transcribe(audio, **kw)
+        assert dev == host and a.last_stats["tokens"] == n_host, (kw, host, dev)
+    assert a.loop_graphs
