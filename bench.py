@@ -152,14 +152,16 @@ def main():
     llama = LlamaModel(lcfg, device=dev, tp=tp, seed=2, wdtype=args.dtype)
     engine = LLMEngine(llama, max_seqs=max(4, C), max_model_len=2048, use_graphs=use_graphs)
     brain = LLMIntentEngine(engine, load_tokenizer("llama3"), budget_chars=args.budget_chars, temperature=0.1,
-                            seed=1234 + tp.dp_rank)  # identical within a TP group (lockstep decode)
+                            seed=1234)  # every replica does the same work (weak scaling; TP lockstep)
     engine.capture_all()
     torch.cuda.synchronize()
     load_s = time.time() - t_load
 
     asr_tokens = int(math.ceil(args.audio_s * args.asr_tokens_per_s))
-    # identical audio within a TP group (its ranks decode in lockstep); distinct across DP replicas
-    utterances = [synth_speech(args.audio_s, seed=100 * tp.dp_rank + i) for i in range(8)]
+    # the same utterances on every rank: a DP replica's work per step is then exactly the 1-GPU
+    # work (weak scaling measures interference, not a different mix of transcripts / intent
+    # lengths), and the ranks of a TP group decode in lockstep
+    utterances = [synth_speech(args.audio_s, seed=i) for i in range(8)]
 
     def one(i: int):
         pcm = utterances[i % len(utterances)]
