@@ -191,3 +191,26 @@ def test_asr_device_decode_loop_matches_host_loop():
         dev = a.transcribe(audio, **kw)
         assert dev == host and a.last_stats["tokens"] == n_host, (kw, host, dev)
     assert a.loop_graphs
+
+
+def test_prefix_cached_prefill_decode_attention_slices(monkeypatch):
+    """A prompt suffix behind a cached prefix runs its attention through the decode kernel in
+    <= 64-row slices; logits match the flash-attention path."""
+    ops.ext()
+    torch.manual_seed(0)
+    toks = torch.randint(0, CFG.vocab_size, (300,)).tolist()
+    model = LlamaModel(CFG, device="cuda", seed=6)
+
+    def run(flag: str):
+        monkeypatch.setenv("VWA_PREFILL_DECODE_ATTN", flag)
+        e = LLMEngine(model, max_seqs=2, max_model_len=512, kv_blocks=60, block_size=16)
+        head = e.new_sequence(toks[:208])
+        e.prefill(head)
+        e.free_sequence(head)  # publishes the 208-token prefix
+        s = e.new_sequence(toks)  # 13 cached blocks, 92-token suffix with q_offset 208
+        assert s.n_computed == 208
+        return e.prefill(s).float().cpu()
+
+    a, b = run("1"), run("0")
+    err = (a - b).abs().max().item()
+    assert err < 0.02 * (1 + b.abs().max().item()), err

@@ -221,6 +221,18 @@ class LlamaModel:
         qbuf = bufs.q[:M] if M <= bufs.q.shape[0] else torch.empty((M, self.nq * self.hd), dtype=self.dtype,
                                                                       device=self.device)
         chain = prefill_seq is None and self._chain_ok(M)
+        # prompt suffix behind a cached prefix (few queries, long keys): the decode attention
+        # kernel in <= 64-row slices (per-row causal context, K/V split over many workgroups)
+        # instead of flash attention's one workgroup per 64 queries x head (measured 82 us/layer
+        # for 84 queries over 1.1k keys: 64 workgroups each walking every key tile)
+        pf_slices = None
+        if (prefill_seq is not None and q_offset >= M and M <= 256 and self.device.type == "cuda"
+                and ops.env_flag("VWA_PREFILL_DECODE_ATTN", True)):
+            i32 = dict(dtype=torch.int32, device=self.device)
+            pf_ctx = torch.arange(q_offset + 1, q_offset + M + 1, **i32)
+            pf_sid = torch.full((M,), prefill_seq, **i32)
+            pf_slices = [(i, min(M, i + 64)) for i in range(0, M, 64)]
+            pf_out = torch.empty((M, self.nq * self.hd), dtype=self.dtype, device=self.device)
         for li, L in enumerate(self.layers):
             kc, vc = kv.k[li], kv.v[li]
             if chain and li > 0:
@@ -235,6 +247,14 @@ class LlamaModel:
                                      n_q_heads=self.nq, n_kv_heads=self.nkv, head_dim=self.hd, scale=self.scale,
                                      max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o, part_ml=bufs.part_ml,
                                      counters=bufs.attn_cnt)
+            elif pf_slices is not None:
+                attn = pf_out
+                lay = ops.KVLayout.paged(kc, vc, bufs.block_table)
+                for i, j in pf_slices:
+                    ops.decode_attention(q[i:j], lay, pf_ctx[i:j], pf_sid[i:j], n_q_heads=self.nq,
+                                         n_kv_heads=self.nkv, head_dim=self.hd, scale=self.scale,
+                                         max_ctx=bufs.max_ctx, out=attn[i:j], part_o=bufs.part_o,
+                                         part_ml=bufs.part_ml, counters=bufs.attn_cnt)
             else:
                 table = bufs.block_table[prefill_seq : prefill_seq + 1]
                 q4 = q.view(1, M, self.nq, self.hd)

@@ -315,7 +315,8 @@ class LLMEngine:
                 hidden=torch.empty(n, m.cfg.hidden, dtype=m.dtype, device=dev),
                 q=torch.empty(n, m.nq * m.hd, dtype=m.dtype, device=dev),
                 act=torch.empty(n, m.F, dtype=m.dtype, device=dev),
-                logits_local=self.bufs.logits_local, logits=self.bufs.logits, max_ctx=self.max_model_len,
+                logits_local=self.bufs.logits_local, logits=self.bufs.logits, max_ctx=self.bufs.max_ctx,
+                part_o=self.bufs.part_o, part_ml=self.bufs.part_ml, attn_cnt=self.bufs.attn_cnt,
             )
             logits = m.forward(scratch, n, self.kv, prefill_seq=seq.sid, q_offset=start,
                                logits_rows=slice(n - 1, n))
