@@ -167,7 +167,9 @@ def test_chain_timeout_falls_back_to_per_kernel_launches():
     a = e.run_rows([(s, 11)]).float().cpu()
     assert model._chains and not model.chain_error()
     model._chain_bar.view(torch.int64)[160] = 1  # what a timed-out spin writes
-    e._check_chain()
+    e._check_chain()  # non-blocking: queues the copy of the error word ...
+    torch.cuda.synchronize()
+    e._check_chain()  # ... and acts on it at the next check
     assert e.stats.get("chain_fallbacks") == 1 and not e.graphs and not model._chain_ok(1)
     b = e.run_rows([(s, 12)]).float().cpu()
     assert torch.isfinite(a).all() and torch.isfinite(b).all()

@@ -1,0 +1,44 @@
+"""cProfile of the intent engine's host side during decode (which Python / native calls sit
+between two GPU steps).  python tools/host_profile.py [--llm llama3-8b] > gpurun_out/host_prof.txt"""
+import argparse
+import cProfile
+import os
+import pstats
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from voice_enabled_browser_automation_amd import ops  # noqa: E402
+from voice_enabled_browser_automation_amd.brain.intent_engine import LLMIntentEngine  # noqa: E402
+from voice_enabled_browser_automation_amd.brain.prompt import COMMANDS  # noqa: E402
+from voice_enabled_browser_automation_amd.models.config import get_config  # noqa: E402
+from voice_enabled_browser_automation_amd.models.llama import LlamaModel  # noqa: E402
+from voice_enabled_browser_automation_amd.runtime.engine import LLMEngine  # noqa: E402
+from voice_enabled_browser_automation_amd.tokenizer import load_tokenizer  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--llm", default="llama3-8b")
+    ap.add_argument("--n", type=int, default=6)
+    a = ap.parse_args()
+    ops.ext()
+    m = LlamaModel(get_config(a.llm), device="cuda", seed=2)
+    eng = LLMEngine(m, max_seqs=4, max_model_len=2048)
+    brain = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=512, temperature=0.1, seed=1234)
+    eng.capture_all()
+    for i in range(2):
+        brain.parse({"text": COMMANDS[i], "context": {"url": "https://www.bestbuy.com"}})
+    torch.cuda.synchronize()
+    pr = cProfile.Profile()
+    pr.enable()
+    for i in range(a.n):
+        brain.parse({"text": COMMANDS[i % len(COMMANDS)], "context": {"url": "https://www.bestbuy.com"}})
+    pr.disable()
+    st = pstats.Stats(pr)
+    st.sort_stats("tottime").print_stats(30)
+
+
+if __name__ == "__main__":
+    main()

@@ -71,6 +71,9 @@ class IntentRequest:
                     total_ms=(t_end - self.t_start) * 1e3)
 
 
+_TOK_PENDING = -0x7A7A7A7A  # never a token id nor the sampler's -1 failure code
+
+
 class LLMIntentEngine:
     """Grammar-constrained intent decoding with continuous batching.
 
@@ -108,6 +111,11 @@ class LLMIntentEngine:
         self.d_step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.d_tok = torch.zeros(R, dtype=torch.int32, device=dev)
         self.h_tok = torch.zeros(R, dtype=torch.int32, pin_memory=pin)
+        self.h_tok_np = self.h_tok.numpy()
+        # wait for the sampled tokens by polling the pinned readback buffer (sentinel -> token)
+        # instead of a stream synchronize: the GPU idles from the sampler's end until the host
+        # has posted the next step, so the wake-up latency is on the critical path
+        self.spin_wait = pin and ops.env_flag("VWA_SPIN_WAIT", True)
         self.part_val = torch.zeros(R * 64, dtype=torch.float32, device=dev)
         self.part_idx = torch.zeros(R * 64, dtype=torch.int32, device=dev)
         self.last_stats: Dict[str, Any] = {}
@@ -244,9 +252,19 @@ class LLMIntentEngine:
                    seed=self.d_seed, step=self.d_step, out_tokens=self.d_tok, part_val=self.part_val[: n * 64],
                    part_idx=self.part_idx[: n * 64])
         if self.dev.type == "cuda":
+            if self.spin_wait:
+                self.h_tok_np[:n] = _TOK_PENDING
             self.h_tok[:n].copy_(self.d_tok[:n], non_blocking=True)
             t3 = time.perf_counter()
-            torch.cuda.current_stream().synchronize()
+            if self.spin_wait:
+                hv = self.h_tok_np[:n]
+                deadline = t3 + 0.05
+                while (hv == _TOK_PENDING).any():
+                    if time.perf_counter() > deadline:  # long step (or none in flight): block instead
+                        torch.cuda.current_stream().synchronize()
+                        break
+            else:
+                torch.cuda.current_stream().synchronize()
             toks = self.h_tok[:n].tolist()
         else:
             t3 = time.perf_counter()

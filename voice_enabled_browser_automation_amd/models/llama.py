@@ -200,6 +200,11 @@ class LlamaModel:
         cache[key] = (desc, 4 if nxt else 3, lds) if desc.numel() else None
         return cache[key]
 
+    def chain_error_word(self):
+        """The device word a timed-out chain barrier sets (None before the first chained launch)."""
+        bar = getattr(self, "_chain_bar", None)
+        return None if bar is None else bar.view(torch.int64)[160:161]
+
     def chain_error(self) -> bool:
         """True when a chained launch's grid barrier timed out (results of that step are invalid)."""
         bar = getattr(self, "_chain_bar", None)

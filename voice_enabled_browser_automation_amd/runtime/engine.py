@@ -272,12 +272,26 @@ class LLMEngine:
             return out[torch.tensor(logits_for, device=out.device)]
         return out[:nl]
 
-    def _check_chain(self) -> None:
+    def _check_chain(self, blocking: bool = False) -> None:
         """Health check of the chained decode launch (models/llama.py): a grid-barrier spin that
         timed out (workgroups not co-resident, e.g. another persistent kernel on the GPU) leaves an
-        error word; the model then falls back to per-kernel launches and the graphs are recaptured."""
+        error word; the model then falls back to per-kernel launches and the graphs are recaptured.
+        Non-blocking by default: reads the word copied to pinned memory at the previous check (the
+        step has been synchronised since) and queues the next copy."""
         m = self.model
-        if getattr(m, "chain_error", None) is not None and m.chain_error():
+        if getattr(m, "chain_error", None) is None:
+            return
+        if blocking or self.device.type != "cuda":
+            err = m.chain_error()
+        else:
+            word = m.chain_error_word()
+            if word is None:
+                return
+            if getattr(self, "_chain_err_h", None) is None:
+                self._chain_err_h = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+            err = bool(self._chain_err_h.item() != 0)
+            self._chain_err_h.copy_(word, non_blocking=True)
+        if err:
             import warnings
 
             warnings.warn("chained decode launch timed out at a grid barrier; using per-kernel launches")
