@@ -615,15 +615,23 @@ int g_attn_impl = 1;  // 1: multi-query MFMA kernel (default), 0: split VALU ker
 // ------------------------------------------------------------------------------------------
 constexpr int kBQ = 64;   // queries per workgroup (4 waves x 16)
 constexpr int kBK = 64;   // keys per tile
-constexpr int kVTP = kBK + 4;  // padded V^T row (elements)
 
+// v2 (rocprof: v1 spent 39-60% of LDS cycles in bank conflicts and exposed every key tile's global
+// load latency -- 82 us/layer for 84 queries x 1.1k keys):
+//  * K / V of the NEXT 64-key tile are loaded into registers while the current tile computes;
+//  * V is stored row-major in the dual-use image (b) of the guide (256-byte rows, chunk XOR) and
+//    read as the O^T A operand with ds_read_b64_tr_b16 (no 2-byte transposing stores);
+//  * the S^T tiles read K rows in an interleaved key order (A row n of tile t in a 32-key block =
+//    key 8(n>>2) + 4t + (n&3)) so each lane's probabilities are 8 consecutive keys: the two
+//    transposed V reads of a 32-lane half are then 8 rows apart (conflict-free).
 template <int D, bool CAUSAL>
 __global__ __launch_bounds__(256) void flash_attn_kernel(FlashAttnParams p) {
-  constexpr int NCH = D / 8;       // 16-byte chunks per K row
-  constexpr int NDS = D / 32;      // MFMA k-steps over head dim
-  constexpr int NDT = D / 16;      // 16-row d tiles of O^T
+  constexpr int NCH = D / 8;               // 16-byte chunks per K / V row
+  constexpr int NDS = D / 32;              // MFMA k-steps over head dim
+  constexpr int NDT = D / 16;              // 16-row d tiles of O^T
+  constexpr int LPT = kBK * NCH / 256;     // 16-byte chunks per thread per tile (K and V each)
   __shared__ __attribute__((aligned(16))) u16 ks[kBK * D];
-  __shared__ __attribute__((aligned(16))) u16 vt[D * kVTP];
+  __shared__ __attribute__((aligned(16))) unsigned char vimg[kBK * 256];
 
   const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int kvh = h / (p.n_q_heads / p.n_kv_heads);
@@ -660,48 +668,65 @@ __global__ __launch_bounds__(256) void flash_attn_kernel(FlashAttnParams p) {
 
   int k_end = Sk;
   if (CAUSAL) k_end = min(Sk, qoff + qb * kBQ + kBQ);
-  for (int k0 = 0; k0 < k_end; k0 += kBK) {
-    // ---- stage K (swizzled rows) and V^T into LDS
-    for (int c = threadIdx.x; c < kBK * NCH; c += 256) {
+
+  uint4 kr[LPT], vr[LPT];
+  auto load_tile = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = threadIdx.x + i * 256;
       const int r = c / NCH, ch = c % NCH;
       const int t = k0 + r;
-      uint4 kv4 = make_uint4(0, 0, 0, 0), vv4 = make_uint4(0, 0, 0, 0);
       if (t < Sk) {
         const int64_t off = kv_offset(p.kv, b, kvh, t) + ch * 8;
-        kv4 = *reinterpret_cast<const uint4*>(p.kv.k + off);
-        vv4 = *reinterpret_cast<const uint4*>(p.kv.v + off);
+        kr[i] = ld128(p.kv.k + off);
+        vr[i] = ld128(p.kv.v + off);
+      } else {
+        kr[i] = make_uint4(0, 0, 0, 0);
+        vr[i] = make_uint4(0, 0, 0, 0);
       }
-      *reinterpret_cast<uint4*>(&ks[r * D + ((ch ^ (r % NCH)) * 8)]) = kv4;
-      const u16* ve = reinterpret_cast<const u16*>(&vv4);
+    }
+  };
+  if (k_end > 0) load_tile(0);
+  for (int k0 = 0; k0 < k_end; k0 += kBK) {
+    // ---- registers -> LDS (K swizzled rows, V image (b)); then the next tile's loads go out
 #pragma unroll
-      for (int j = 0; j < 8; ++j) vt[(ch * 8 + j) * kVTP + r] = ve[j];
+    for (int i = 0; i < LPT; ++i) {
+      const int c = threadIdx.x + i * 256;
+      const int r = c / NCH, ch = c % NCH;
+      *reinterpret_cast<uint4*>(&ks[r * D + ((ch ^ (r % NCH)) * 8)]) = kr[i];
+      *reinterpret_cast<uint4*>(vimg + vimg_off(r, ch)) = vr[i];
     }
     __syncthreads();
+    if (k0 + kBK < k_end) load_tile(k0 + kBK);
 
-    // ---- S^T = K . Q^T  (4 key blocks of 16)
-    f32x4 s[4];
+    // ---- S^T = K . Q^T: 2 blocks of 32 keys x 2 interleaved 16-row tiles
+    f32x4 s[2][2];
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int r = kb * 16 + ql;
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int ds = 0; ds < NDS; ++ds) {
-        const int ch = ds * 4 + g;
-        const uint4 a = *reinterpret_cast<const uint4*>(&ks[r * D + ((ch ^ (r % NCH)) * 8)]);
-        s[kb] = mfma16(as_bf16x8(a), qf[ds], s[kb]);
+      for (int t = 0; t < 2; ++t) {
+        s[kk][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int r = 32 * kk + 8 * (ql >> 2) + 4 * t + (ql & 3);
+#pragma unroll
+        for (int ds = 0; ds < NDS; ++ds) {
+          const int ch = ds * 4 + g;
+          const uint4 a = *reinterpret_cast<const uint4*>(&ks[r * D + ((ch ^ (r % NCH)) * 8)]);
+          s[kk][t] = mfma16(as_bf16x8(a), qf[ds], s[kk][t]);
+        }
       }
-    }
-    // ---- mask + online softmax (column = this lane's query)
+    // ---- mask + online softmax (column = this lane's query); lane holds keys 32kk + 8g + 4t + i
     float tmax = -INFINITY;
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int kidx = k0 + kb * 16 + 4 * g + i;
-        const bool ok = (kidx < Sk) && (!CAUSAL || kidx <= qpos);
-        if (!ok) s[kb][i] = -INFINITY;
-        tmax = fmaxf(tmax, s[kb][i]);
-      }
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int kidx = k0 + 32 * kk + 8 * g + 4 * t + i;
+          const bool ok = (kidx < Sk) && (!CAUSAL || kidx <= qpos);
+          if (!ok) s[kk][t][i] = -INFINITY;
+          tmax = fmaxf(tmax, s[kk][t][i]);
+        }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
     const float m_new = fmaxf(m_run, tmax);
@@ -709,35 +734,37 @@ __global__ __launch_bounds__(256) void flash_attn_kernel(FlashAttnParams p) {
     const bool any = (m_new != -INFINITY);
     float psum = 0.f;
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float e = (any && s[kb][i] != -INFINITY) ? exp2f(s[kb][i] - m_new) : 0.f;
-        s[kb][i] = e;
-        psum += e;
-      }
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e = (any && s[kk][t][i] != -INFINITY) ? exp2f(s[kk][t][i] - m_new) : 0.f;
+          s[kk][t][i] = e;
+          psum += e;
+        }
     l_run = l_run * alpha + psum;
     m_run = m_new;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) oacc[dt] *= alpha;
 
-    // ---- O^T += V^T . P^T  (2 k-steps of 32 keys)
+    // ---- O^T += V^T . P^T per 32-key block: P^T[keys 8g..8g+7][query column]
+    const int q4 = ql >> 2, p4 = ql & 3;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       float pf[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        pf[i] = s[2 * kk][i];
-        pf[4 + i] = s[2 * kk + 1][i];
+        pf[i] = s[kk][0][i];
+        pf[4 + i] = s[kk][1][i];
       }
       const bf16x8 pb = as_bf16x8(pack8(pf));
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
-        const int d = dt * 16 + ql;
-        const uint2 lo = *reinterpret_cast<const uint2*>(&vt[d * kVTP + 32 * kk + 4 * g]);
-        const uint2 hi = *reinterpret_cast<const uint2*>(&vt[d * kVTP + 32 * kk + 16 + 4 * g]);
-        const uint4 a = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        oacc[dt] = mfma16(as_bf16x8(a), pb, oacc[dt]);
+        const int ch = 2 * dt + (p4 >> 1), sub = 8 * (p4 & 1);
+        const uint2 lo = lds_tr16(vimg + vimg_off(32 * kk + 8 * g + q4, ch) + sub);
+        const uint2 hi = lds_tr16(vimg + vimg_off(32 * kk + 8 * g + 4 + q4, ch) + sub);
+        oacc[dt] = mfma16(as_bf16x8(make_uint4(lo.x, lo.y, hi.x, hi.y)), pb, oacc[dt]);
       }
     }
     __syncthreads();
