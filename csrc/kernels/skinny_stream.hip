@@ -524,7 +524,8 @@ constexpr int kChainSpinLimit = 1 << 18;  // ~0.3 s: a lost workgroup ends the l
 // flat mode uses [0]; two-level mode puts group g (block id mod 8, one per XCD under round-robin
 // dispatch) at [16 g] and the top counter at [128]; [160] is the timeout flag.
 // Measured (tools/chain_probe.py): a reset + generation barrier cost 5-7 us from the last
-// arrival to release (four dependent agent-scope round trips).
+// arrival to release (four dependent agent-scope round trips).  A flat counter polled with scalar loads
+// on uncached memory (256 same-address atomics) measured 121 us per chained layer vs 99.6 two-level.
 constexpr int kBarTop = 128, kBarErr = 160;
 
 VWA_DEVICE unsigned long long chain_arrive(unsigned long long* bar, int nwg, int mode) {
