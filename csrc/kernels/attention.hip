@@ -334,18 +334,47 @@ VWA_DEVICE float4 ld_sc1_f4(__amdgpu_buffer_rsrc_t r, int64_t idx) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, 16));
 }
 
-template <int D, int G>
-__global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams p) {
+template <bool SC1>
+VWA_DEVICE void store_out(u16* dst, uint4 v) {
+  if constexpr (SC1) {
+    // agent-scope write-through: read by other workgroups later in the same (chained) launch
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v.x | ((unsigned long long)v.y << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst) + 1, (unsigned long long)v.z | ((unsigned long long)v.w << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *reinterpret_cast<uint4*>(dst) = v;
+  }
+}
+
+// LDS of one multi-query attention workgroup with NW waves: V images, per-wave O^T, (m, l), ticket
+template <int D, int NW>
+struct MqLds {
+  static constexpr int OWP = D + 4;
+  static constexpr int vimg = 0;
+  static constexpr int ow = NW * kMqStep * 256;
+  static constexpr int mlw = ow + NW * kMqCols * OWP * 4;
+  static constexpr int last = mlw + NW * kMqCols * 2 * 4;
+  static constexpr int bytes = last + 16;
+};
+
+// Body of the multi-query decode attention for workgroup `bid` of `grid` workgroups with NW
+// waves (the standalone kernel: NW = 4; the chained layer launch: NW = 8).  SC1OUT: outputs are
+// written with sc1 stores (read by another workgroup later in the same launch).
+template <int D, int G, int NW, bool SC1OUT>
+VWA_DEVICE void mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid, int bid) {
+  constexpr int kWv = NW;
+  constexpr int kChunk = NW * kMqStep;     // chunk granularity (keys)
   constexpr int RG = kMqCols / G;          // rows per group
   constexpr int NKS = D / 32;              // S^T k-steps over the head dim
   constexpr int NDT = D / 16;              // O^T dim tiles
   constexpr int NCH = D / 8;               // 16-byte chunks per key row
   constexpr int NVL = kMqStep * NCH / 64;  // V row chunks per lane per step
   constexpr int OWP = D + 4;               // padded o row (floats): conflict-free float4 stores
-  __shared__ __attribute__((aligned(16))) unsigned char vimg[kWaves][kMqStep * 256];
-  __shared__ __attribute__((aligned(16))) float ow[kWaves][kMqCols][OWP];
-  __shared__ float mlw[kWaves][kMqCols][2];
-  __shared__ int s_last;
+  using L = MqLds<D, NW>;
+  float* ow = reinterpret_cast<float*>(lds + L::ow);    // [NW][kMqCols][OWP]
+  float* mlw = reinterpret_cast<float*>(lds + L::mlw);  // [NW][kMqCols][2]
+  int& s_last = *reinterpret_cast<int*>(lds + L::last);
 
   const int nkv = p.n_kv_heads, nq = p.n_q_heads;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -363,10 +392,10 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
   const int my_rank = __builtin_popcountll(leaders & ((1ull << lane) - 1ull));
   // chunks per (group, kv head): spread the work over the grid (one item per workgroup when it
   // fits), never more than the partial buffers hold
-  const int n_eff = max(1, min(p.n_splits, (int)gridDim.x / max(1, n_groups * nkv)));
+  const int n_eff = max(1, min(p.n_splits, grid / max(1, n_groups * nkv)));
   const int n_items = n_groups * nkv * n_eff;
 
-  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+  for (int item = bid; item < n_items; item += grid) {
   // item -> (kv head, group, chunk); kv head fastest so a head's workgroups share one XCD (b % 8)
   const int kvh = item % nkv;
   const int gi = (item / nkv) % n_groups, chunk = item / (nkv * n_groups);
@@ -385,13 +414,13 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
   const int rho = n / G;                     // group row of this lane's query column
   const int ctx_n = __shfl(c_own, rho, 64);  // its context (0 for padded columns)
 
-  // ---- this item's chunk of the group's keys (4 waves x CL/4 keys)
-  const int CL = ((ctxmax + n_eff - 1) / n_eff + kMqChunk - 1) / kMqChunk * kMqChunk;
+  // ---- this item's chunk of the group's keys (NW waves x CL/NW keys)
+  const int CL = ((ctxmax + n_eff - 1) / n_eff + kChunk - 1) / kChunk * kChunk;
   const int kbeg = chunk * CL;
   if (kbeg >= ctxmax) continue;
   const int nact = (ctxmax + CL - 1) / CL;
-  const int wb = kbeg + w * (CL / kWaves);
-  const int we = min(ctxmax, wb + CL / kWaves);
+  const int wb = kbeg + w * (CL / kWv);
+  const int we = min(ctxmax, wb + CL / kWv);
   const int nsteps = we > wb ? (we - wb + kMqStep - 1) / kMqStep : 0;
   const int kmax = ctxmax - 1;  // keys past the context are clamped (finite data, masked scores)
 
@@ -436,7 +465,7 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
   f32x4 o[NDT];
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  unsigned char* vi = vimg[w];
+  unsigned char* vi = lds + L::vimg + w * kMqStep * 256;
 
   auto compute_step = [&](int kb, const uint4 (&kr)[2][NKS], const uint4 (&vr)[NVL]) {
 #pragma unroll
@@ -501,12 +530,12 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
   float l_tot = l_run + __shfl_xor(l_run, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
   if (g == 0) {
-    mlw[w][n][0] = m_run;
-    mlw[w][n][1] = l_tot;
+    mlw[(w * kMqCols + n) * 2 + 0] = m_run;
+    mlw[(w * kMqCols + n) * 2 + 1] = l_tot;
   }
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
-    *reinterpret_cast<float4*>(&ow[w][n][16 * dt + 4 * g]) = make_float4(o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
+    *reinterpret_cast<float4*>(&ow[(w * kMqCols + n) * OWP + 16 * dt + 4 * g]) = make_float4(o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
   __syncthreads();
 
   // ---- merge the waves: thread -> (query column cn, 8-dim chunk dc)
@@ -519,17 +548,17 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
   if (act) {
     float M = -INFINITY;
 #pragma unroll
-    for (int ww = 0; ww < kWaves; ++ww) M = fmaxf(M, mlw[ww][cn][0]);
+    for (int ww = 0; ww < kWv; ++ww) M = fmaxf(M, mlw[(ww * kMqCols + cn) * 2]);
     float L = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < kWaves; ++ww) {
-      const float mw = mlw[ww][cn][0];
+    for (int ww = 0; ww < kWv; ++ww) {
+      const float mw = mlw[(ww * kMqCols + cn) * 2];
       const float f = (mw == -INFINITY) ? 0.f : exp2f(mw - M);
-      L += mlw[ww][cn][1] * f;
-      const float4 a = *reinterpret_cast<const float4*>(&ow[ww][cn][8 * dc]);
-      const float4 b = *reinterpret_cast<const float4*>(&ow[ww][cn][8 * dc + 4]);
+      L += mlw[(ww * kMqCols + cn) * 2 + 1] * f;
+      const float4 a = *reinterpret_cast<const float4*>(&ow[(ww * kMqCols + cn) * OWP + 8 * dc]);
+      const float4 b = *reinterpret_cast<const float4*>(&ow[(ww * kMqCols + cn) * OWP + 8 * dc + 4]);
       acc[0] += f * a.x; acc[1] += f * a.y; acc[2] += f * a.z; acc[3] += f * a.w;
       acc[4] += f * b.x; acc[5] += f * b.y; acc[6] += f * b.z; acc[7] += f * b.w;
     }
@@ -537,7 +566,7 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
       const float inv = L > 0.f ? 1.f / L : 0.f;
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] *= inv;
-      *reinterpret_cast<uint4*>(p.out + (int64_t)crow * p.ldo + ch * D + 8 * dc) = pack8(acc);
+      store_out<SC1OUT>(p.out + (int64_t)crow * p.ldo + ch * D + 8 * dc, pack8(acc));
     } else {
       const int64_t base = ((int64_t)crow * p.n_splits + chunk) * nq + ch;
       st_sc1_f4(r_o, base * D + 8 * dc, acc);
@@ -586,9 +615,15 @@ __global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams
     const float inv = L > 0.f ? 1.f / L : 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] *= inv;
-    *reinterpret_cast<uint4*>(p.out + (int64_t)crow * p.ldo + ch * D + 8 * dc) = pack8(acc);
+    store_out<SC1OUT>(p.out + (int64_t)crow * p.ldo + ch * D + 8 * dc, pack8(acc));
   }
   }  // items
+}
+
+template <int D, int G>
+__global__ __launch_bounds__(kWaves * 64) void decode_mq_kernel(DecodeAttnParams p) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[MqLds<D, kWaves>::bytes];
+  mq_body<D, G, kWaves, false>(p, lds, (int)gridDim.x, (int)blockIdx.x);
 }
 
 constexpr int kMqMaxGrid = 512;  // two 67 KB-LDS workgroups per CU: the whole grid is resident
