@@ -207,6 +207,12 @@ void set_resid(SkinnyParams& p, const Tensor& h) {
   p.ldr = (int)h.stride(0);
 }
 
+DecodeAttnParams decode_params(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& table,
+                               int64_t block_size, int64_t sb, int64_t sh, int64_t stok, const Tensor& ctx_lens,
+                               const Tensor& seq_ids, int64_t n_q_heads, int64_t n_kv_heads, int64_t head_dim,
+                               double scale, int64_t n_splits, const Tensor& part_o, const Tensor& part_ml,
+                               const Tensor& counters, const Tensor& out);
+
 // Returns (descriptor uint8 tensor, dynamic LDS bytes); descriptor is empty when the shapes do
 // not fit the chain (the caller keeps the per-kernel path).
 std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor w_o, Tensor w_gu, Tensor w_down,
@@ -214,7 +220,12 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                                        int64_t head_dim, c10::optional<Tensor> positions, c10::optional<Tensor> slots,
                                        c10::optional<Tensor> rope, c10::optional<Tensor> q_out,
                                        c10::optional<Tensor> k_cache, c10::optional<Tensor> v_cache, Tensor bar,
-                                       Tensor work, c10::optional<Tensor> ts, int64_t bar_mode) {
+                                       Tensor work, c10::optional<Tensor> ts, int64_t bar_mode,
+                                       c10::optional<Tensor> a_q, c10::optional<Tensor> a_k, c10::optional<Tensor> a_v,
+                                       c10::optional<Tensor> a_table, int64_t a_block_size, int64_t a_sb, int64_t a_sh,
+                                       int64_t a_st, c10::optional<Tensor> a_ctx, c10::optional<Tensor> a_seq,
+                                       double a_scale, int64_t a_n_splits, c10::optional<Tensor> a_part_o,
+                                       c10::optional<Tensor> a_part_ml, c10::optional<Tensor> a_counters) {
   c10::DeviceGuard g(h.device());
   const int64_t M = h.size(0);
   TORCH_CHECK(att.size(0) == M && act.size(0) == M, "row counts differ");
@@ -261,6 +272,17 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
     TORCH_CHECK(ts->is_cuda() && ts->scalar_type() == at::kLong && ts->numel() >= 1024 * 16, "ts must be int64[>=16384]");
     cp.ts = reinterpret_cast<unsigned long long*>(ts->data_ptr<int64_t>());
   }
+  if (a_q.has_value()) {  // decode attention as the launch's first phase (its output is `att`)
+    TORCH_CHECK(a_k && a_v && a_table && a_ctx && a_seq && a_part_o && a_part_ml && a_counters,
+                "attention phase: every a_* tensor is required");
+    TORCH_CHECK(head_dim == 128 && (n_q_heads / n_kv_heads == 4 || n_q_heads / n_kv_heads == 8) &&
+                    n_q_heads % n_kv_heads == 0 && a_q->size(0) == M && M <= 64,
+                "attention phase: head_dim 128, GQA group 4 or 8, one query row per chained row");
+    cp.attn = decode_params(*a_q, *a_k, *a_v, *a_table, a_block_size, a_sb, a_sh, a_st, *a_ctx, *a_seq, n_q_heads,
+                            n_kv_heads, head_dim, a_scale, a_n_splits, *a_part_o, *a_part_ml, *a_counters, att);
+    TORCH_CHECK(a_n_splits > 1, "attention phase: the in-launch chunk merge needs n_splits > 1");
+    cp.attn_g = (int)(n_q_heads / n_kv_heads);
+  }
   int cus = 0;
   TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h.device().index()) == hipSuccess,
               "CU count");
@@ -297,13 +319,13 @@ Tensor alloc_uncached_i32(int64_t n, Tensor like) {
                           torch::dtype(torch::kInt).device(like.device()));
 }
 
-void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like) {
+void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like, int64_t attn_g) {
   c10::DeviceGuard g(like.device());
   TORCH_CHECK(desc.is_cuda() && desc.numel() == (int64_t)sizeof(ChainParams), "bad chain descriptor");
   int dev = like.device().index(), cus = 0;
   TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess, "CU count");
   // one workgroup per CU: the barrier needs every workgroup resident
-  check_rc(vwa_chain_launch(reinterpret_cast<const ChainParams*>(desc.data_ptr()), (int)n_phases, (int)lds, cus,
+  check_rc(vwa_chain_launch(reinterpret_cast<const ChainParams*>(desc.data_ptr()), (int)n_phases, (int)attn_g, (int)lds, cus,
                             cur_stream(like)),
            "chain");
 }
@@ -403,11 +425,10 @@ KVView make_view(const Tensor& k, const Tensor& v, const Tensor& table, int64_t 
   return kv;
 }
 
-void decode_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_size, int64_t sb, int64_t sh,
-                      int64_t stok, Tensor ctx_lens, Tensor seq_ids, int64_t n_q_heads, int64_t n_kv_heads,
-                      int64_t head_dim, double scale, int64_t n_splits, Tensor part_o, Tensor part_ml,
-                      Tensor counters, Tensor out) {
-  c10::DeviceGuard g(q.device());
+DecodeAttnParams decode_params(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& table, int64_t block_size, int64_t sb, int64_t sh,
+                      int64_t stok, const Tensor& ctx_lens, const Tensor& seq_ids, int64_t n_q_heads, int64_t n_kv_heads,
+                      int64_t head_dim, double scale, int64_t n_splits, const Tensor& part_o, const Tensor& part_ml,
+                      const Tensor& counters, const Tensor& out) {
   check_bf16(q, "q");
   TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1 && q.size(1) == n_q_heads * head_dim, "q shape");
   TORCH_CHECK(q.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0,
@@ -445,6 +466,16 @@ void decode_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_
   p.counters = counters.data_ptr<int>();
   p.out = bfp_mut(out);
   p.ldo = (int)out.stride(0);
+  return p;
+}
+
+void decode_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_size, int64_t sb, int64_t sh,
+                      int64_t stok, Tensor ctx_lens, Tensor seq_ids, int64_t n_q_heads, int64_t n_kv_heads,
+                      int64_t head_dim, double scale, int64_t n_splits, Tensor part_o, Tensor part_ml,
+                      Tensor counters, Tensor out) {
+  c10::DeviceGuard g(q.device());
+  DecodeAttnParams p = decode_params(q, k, v, table, block_size, sb, sh, stok, ctx_lens, seq_ids, n_q_heads,
+                                     n_kv_heads, head_dim, scale, n_splits, part_o, part_ml, counters, out);
   check_rc(vwa_decode_attention(&p, cur_stream(q)), "decode_attention");
 }
 
@@ -627,8 +658,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("chain_make", &chain_make, py::arg("h"), py::arg("att"), py::arg("act"), py::arg("w_o"), py::arg("w_gu"),
         py::arg("w_down"), py::arg("eps"), py::arg("w_qkv"), py::arg("n_q_heads"), py::arg("n_kv_heads"),
         py::arg("head_dim"), py::arg("positions"), py::arg("slots"), py::arg("rope"), py::arg("q_out"),
-        py::arg("k_cache"), py::arg("v_cache"), py::arg("bar"), py::arg("work"), py::arg("ts") = py::none(), py::arg("bar_mode") = 1);
-  m.def("chain_run", &chain_run);
+        py::arg("k_cache"), py::arg("v_cache"), py::arg("bar"), py::arg("work"), py::arg("ts") = py::none(), py::arg("bar_mode") = 1,
+        py::arg("a_q") = py::none(), py::arg("a_k") = py::none(), py::arg("a_v") = py::none(),
+        py::arg("a_table") = py::none(), py::arg("a_block_size") = 0, py::arg("a_sb") = 0, py::arg("a_sh") = 0,
+        py::arg("a_st") = 0, py::arg("a_ctx") = py::none(), py::arg("a_seq") = py::none(), py::arg("a_scale") = 0.0,
+        py::arg("a_n_splits") = 0, py::arg("a_part_o") = py::none(), py::arg("a_part_ml") = py::none(),
+        py::arg("a_counters") = py::none());
+  m.def("chain_run", &chain_run, py::arg("desc"), py::arg("n_phases"), py::arg("lds"), py::arg("like"),
+        py::arg("attn_g") = 0);
   m.def("alloc_uncached_i32", &alloc_uncached_i32);
   m.def("decode_advance", &decode_advance);
   m.def("rmsnorm", &rmsnorm);

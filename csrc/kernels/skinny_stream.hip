@@ -23,6 +23,7 @@
 // two-register-set pipeline; only the reduction scratch lives in LDS.
 #include "common.h"
 #include "vwa_kernels.h"
+#include "mq_attention.h"
 
 using namespace vwa;
 
@@ -781,7 +782,14 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
 
 // The phase sequence is static (the Llama layer tail: o_proj+residual, gate/up+SwiGLU,
 // down+residual [, next layer's QKV]); a runtime epilogue switch measured 50+ VGPR spills.
-template <int KS, bool WITH_QKV>
+// AG > 0: the layer's decode attention (GQA group AG, head_dim 128) runs first, as phase 0 of
+// the same launch (mq_attention.h with 8 waves, one register set, outputs written through to
+// memory); workgroups without an attention item issue their o_proj weights at once.  Measured
+// (tools/chain_probe.py --attn, 1 row, ctx 1100): 111.6 us vs 111-112 us for the standalone
+// attention kernel + the GEMM chain -- the attention phase itself is slower in the 8-wave form
+// (13-14 us vs 10.5 us) and o_proj still needs X staging + reduction after the barrier, so the
+// model keeps the separate attention launch (VWA_CHAIN_ATTN=1 selects this form).
+template <int KS, bool WITH_QKV, int AG>
 __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __restrict__ cpp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ChainParams& cp = *cpp;  // device-resident descriptor
@@ -797,7 +805,22 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     ++nts;
   };
   stamp();
-  chain_issue_first<EPI_RESID, KS>(cp.ph[0], A);
+  if constexpr (AG > 0) {
+    // (measured: issuing the o_proj weights BEFORE the attention doubled the attention phase,
+    // 21.5 vs 10.5 us: its dependent metadata / K / V round trips queued behind 33 MB of weight
+    // loads -- vmcnt retires in order -- so they go out at the barrier instead)
+    // workgroups without an attention item issue their o_proj weights at once; the others after
+    // their item, at the barrier
+    const bool idle = mq_body<128, AG, KS, true, false>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
+                                                        (int)blockIdx.x,
+                                                        [&]() { chain_issue_first<EPI_RESID, KS>(cp.ph[0], A); });
+    stamp();
+    gen = chain_arrive(bar, nwg, cp.bar_mode);
+    if (!idle) chain_issue_first<EPI_RESID, KS>(cp.ph[0], A);
+    chain_wait(bar, gen, cp.bar_mode);
+  } else {
+    chain_issue_first<EPI_RESID, KS>(cp.ph[0], A);
+  }
   chain_phase<EPI_RESID, KS>(cp, 0, A, B, smem);
   stamp();
   gen = chain_arrive(bar, nwg, cp.bar_mode);
@@ -857,10 +880,18 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
   return (int)lds;
 }
 
-extern "C" int vwa_chain_launch(const ChainParams* d_cp, int n_phases, int lds, int grid, hipStream_t st) {
-  if (n_phases == 4) hipLaunchKernelGGL((chain_kernel<8, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
-  else if (n_phases == 3) hipLaunchKernelGGL((chain_kernel<8, false>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
-  else return -10;
+extern "C" int vwa_chain_launch(const ChainParams* d_cp, int n_phases, int attn_g, int lds, int grid, hipStream_t st) {
+  if (attn_g) lds = lds > (int)MqLds<128, 8>::bytes ? lds : (int)MqLds<128, 8>::bytes;
+#define VWA_CHAIN_LAUNCH(Q, G) hipLaunchKernelGGL((chain_kernel<8, Q, G>), dim3(grid), dim3(8 * 64), lds, st, d_cp)
+  if (n_phases != 3 && n_phases != 4) return -10;
+  const bool q = n_phases == 4;
+  switch (attn_g) {
+    case 0: if (q) VWA_CHAIN_LAUNCH(true, 0); else VWA_CHAIN_LAUNCH(false, 0); break;
+    case 4: if (q) VWA_CHAIN_LAUNCH(true, 4); else VWA_CHAIN_LAUNCH(false, 4); break;
+    case 8: if (q) VWA_CHAIN_LAUNCH(true, 8); else VWA_CHAIN_LAUNCH(false, 8); break;
+    default: return -10;
+  }
+#undef VWA_CHAIN_LAUNCH
   return (int)hipGetLastError();
 }
 

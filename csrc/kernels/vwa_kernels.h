@@ -29,27 +29,6 @@ struct SkinnyParams {
   const float* ln_c;
 };
 
-// Chained decode GEMM phases in one persistent launch (skinny_stream.hip, vwa_chain): each phase
-// is a streaming-GEMM SkinnyParams + epilogue id (1 residual, 2 SwiGLU, 4 QKV, 0 store); the
-// launcher fills nt / nb.  bar: >= 1536 zero-initialised bytes of monotonic ticket counters and
-// the timeout flag (skinny_stream.hip chain_arrive), valid across launches.
-constexpr int kChainMaxPhases = 4;
-struct ChainPhase {
-  SkinnyParams p;
-  int epi, nt, nb;
-};
-struct ChainParams {
-  ChainPhase ph[kChainMaxPhases];
-  int n;
-  unsigned* bar;
-  int bar_mode;            // 0: flat ticket counter, 1: two-level (8 groups + top)
-  float* part;             // split-tile partial slots [max_tiles][2][M][16*nt] f32
-  int part_floats;
-  unsigned* tickets;       // [max_tiles] zero-initialised, self-resetting
-  int max_tiles;
-  unsigned long long* ts;  // optional [grid][16] s_memrealtime stamps per workgroup (profiling)
-};
-
 // Paged / strided KV addressing shared by the attention kernels:
 //   addr(seq b, kv head h, token t) = base + table[b*table_stride + t/block_size]*stride_block
 //                                     + h*stride_head + (t%block_size)*stride_tok
@@ -74,6 +53,31 @@ struct DecodeAttnParams {
   uint16_t* out; int ldo;           // [rows, n_q_heads*D]
 };
 
+// Chained decode GEMM phases in one persistent launch (skinny_stream.hip, vwa_chain): each phase
+// is a streaming-GEMM SkinnyParams + epilogue id (1 residual, 2 SwiGLU, 4 QKV, 0 store); the
+// launcher fills nt / nb.  bar: >= 1536 zero-initialised bytes of monotonic ticket counters and
+// the timeout flag (skinny_stream.hip chain_arrive), valid across launches.
+constexpr int kChainMaxPhases = 4;
+struct ChainPhase {
+  SkinnyParams p;
+  int epi, nt, nb;
+};
+struct ChainParams {
+  ChainPhase ph[kChainMaxPhases];
+  int n;
+  unsigned* bar;
+  int bar_mode;            // 0: flat ticket counter, 1: two-level (8 groups + top), 2: two-level + scalar polls
+  float* part;             // split-tile partial slots [max_tiles][2][M][16*nt] f32
+  int part_floats;
+  unsigned* tickets;       // [max_tiles] zero-initialised, self-resetting
+  int max_tiles;
+  unsigned long long* ts;  // optional [grid][16] s_memrealtime stamps per workgroup (profiling)
+  // optional decode-attention phase in front of the GEMM phases (head_dim 128, attn_g = GQA
+  // group size; 0: none): the o_proj weights stream while the attention runs
+  DecodeAttnParams attn;
+  int attn_g;
+};
+
 struct FlashAttnParams {
   const uint16_t* q; int64_t q_stride_b, q_stride_s, q_stride_h;   // q[b][s][h][d]
   KVView kv;                        // keys of sequence b: table row b
@@ -92,7 +96,7 @@ extern "C" {
 int vwa_skinny_gemm(int epi, const SkinnyParams* p, hipStream_t st);
 int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st);
 int vwa_chain_prepare(ChainParams* cp, int grid);
-int vwa_chain_launch(const ChainParams* d_cp, int n_phases, int lds, int grid, hipStream_t st);
+int vwa_chain_launch(const ChainParams* d_cp, int n_phases, int attn_g, int lds, int grid, hipStream_t st);
 int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
                 uint16_t* y, int rows, int D, int ldx, float eps, hipStream_t st);
 int vwa_layernorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,

@@ -150,6 +150,14 @@ def test_chained_layer_tail_matches_per_kernel_path(cfg, monkeypatch):
     ref = run(False)
     got = run(True)
     assert not model.chain_error()
+    if cfg.head_dim == 128:  # decode attention as the chained launch's first phase
+        monkeypatch.setenv("VWA_CHAIN_ATTN", "1")
+        model._chains = {}
+        got_a = run(True)
+        monkeypatch.delenv("VWA_CHAIN_ATTN")
+        for a, b in zip(got_a, ref):
+            err = (a - b).abs().max().item()
+            assert err < 0.02 * (1 + b.abs().max().item()), err
     assert model._chains and all(v is not None for v in model._chains.values())
     for a, b in zip(got, ref):
         err = (a - b).abs().max().item()

@@ -19,7 +19,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=1)
     ap.add_argument("--json", default=None)
-    ap.add_argument("--bar-mode", type=int, default=1)
+    ap.add_argument("--bar-mode", type=int, default=2)
+    ap.add_argument("--attn", action="store_true", help="decode attention (ctx 1100) as the first phase")
     a = ap.parse_args()
     dev, bf = "cuda", torch.bfloat16
     E = ops.ext()
@@ -35,22 +36,42 @@ def main():
     pos = torch.arange(M, dtype=torch.int32, device=dev)
     slots = torch.arange(M, dtype=torch.int64, device=dev)
     rope = ops.rope_table(4096, hd, 5e5, device=dev)
-    bar = E.alloc_uncached_i32(512, torch.empty(1, device=dev)) if a.bar_mode == 2 else \
+    bar = E.alloc_uncached_i32(512, torch.empty(1, device=dev)) if a.bar_mode >= 2 else \
         torch.zeros(512, dtype=torch.int32, device=dev)
     ts = torch.zeros(1024 * 16, dtype=torch.int64, device=dev)
     work = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
+    akw, ag = {}, 0
+    if a.attn:  # the layer's attention over a 1100-token paged context as phase 0
+        ctx, bs = 1100, 16
+        nblk = (ctx + M + bs - 1) // bs + 1
+        akc = (torch.randn(nblk + 4, nkv, bs, hd, device=dev) * 0.5).to(bf)
+        akv = torch.randn_like(akc)
+        table = (torch.randperm(nblk + 3, device=dev)[:nblk].to(torch.int32) + 1).view(1, nblk)
+        lay = ops.KVLayout.paged(akc, akv, table)
+        ns = ops.decode_n_splits(2048)
+        akw = dict(a_q=mk(M, nq * hd), a_k=akc, a_v=akv, a_table=table, a_block_size=bs, a_sb=lay.sb, a_sh=lay.sh,
+                   a_st=lay.st, a_ctx=torch.arange(ctx, ctx + M, dtype=torch.int32, device=dev) + 1,
+                   a_seq=torch.zeros(M, dtype=torch.int32, device=dev), a_scale=hd ** -0.5, a_n_splits=ns,
+                   a_part_o=torch.zeros(M * ns * nq * hd, device=dev), a_part_ml=torch.zeros(M * ns * nq * 2, device=dev),
+                   a_counters=torch.zeros(M * nkv, dtype=torch.int32, device=dev))
+        ag = nq // nkv
     descs = [E.chain_make(h, att, act, w["o"], w["gu"], w["down"], 1e-5, w["qkv"], nq, nkv, hd, pos, slots, rope, q,
-                          kc, vc, bar, work, ts, a.bar_mode) for w in Ws]
+                          kc, vc, bar, work, ts, a.bar_mode, **akw) for w in Ws]
     it = [0]
 
     def chained():
         it[0] = (it[0] + 1) % ncopy
         dsc, lds = descs[it[0]]
-        E.chain_run(dsc, 4, lds, h)
+        E.chain_run(dsc, 4, lds, h, ag)
 
     def separate():
         it[0] = (it[0] + 1) % ncopy
         w = Ws[it[0]]
+        if a.attn:
+            ops.decode_attention(akw["a_q"], ops.KVLayout.paged(akw["a_k"], akw["a_v"], akw["a_table"]), akw["a_ctx"],
+                                 akw["a_seq"], n_q_heads=nq, n_kv_heads=nkv, head_dim=hd, scale=hd ** -0.5,
+                                 max_ctx=2048, out=att, part_o=akw["a_part_o"], part_ml=akw["a_part_ml"],
+                                 counters=akw["a_counters"])
         ops.linear(att, w["o"], out=h, residual=h)
         ops.linear_swiglu(h, w["gu"], fuse_rms=True, eps=1e-5, out=act)
         ops.linear(act, w["down"], out=h, residual=h)
@@ -65,7 +86,8 @@ def main():
     assert int(bar.view(torch.int64)[160].item()) == 0, "barrier timeout"
     # stamps of the last launch: [start, end0, wait0, end1, wait1, end2, wait2, end3]
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    st = ts.view(-1, 16)[:cus, :8].double().cpu()
+    ns_ = 9 if a.attn else 8
+    st = ts.view(-1, 16)[:cus, :ns_].double().cpu()
     st = (st - st[:, :1].min()) * 10e-3  # us
     med = st.median(dim=0).values.tolist()
     mx = st.max(dim=0).values.tolist()
@@ -73,7 +95,7 @@ def main():
     r = dict(kernel="chain_probe", rows=M, bar_mode=a.bar_mode, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
              stamps_med_us=[round(x, 2) for x in med], stamps_min_us=[round(x, 2) for x in mn],
              stamps_max_us=[round(x, 2) for x in mx],
-             legend="start,end_o,wait_o,end_gu,wait_gu,end_down,wait_down,end_qkv")
+             legend=("start,end_attn," if a.attn else "start,") + "end_o,wait_o,end_gu,wait_gu,end_down,wait_down,end_qkv")
     print(json.dumps(r), flush=True)
     if a.json:
         with open(a.json, "a") as f:

@@ -191,13 +191,24 @@ class LlamaModel:
         L = self.layers[li]
         nxt = li + 1 < len(self.layers)
         N = self.layers[li + 1] if nxt else None
+        # optionally the layer's decode attention as the launch's first phase (VWA_CHAIN_ATTN=1;
+        # measured equal to the separate attention launch, skinny_stream.hip chain_kernel)
+        attn = (self.hd == 128 and self.nq // self.nkv in (4, 8) and ops.env_flag("VWA_CHAIN_ATTN", False)
+                and ops.decode_n_splits(bufs.max_ctx) > 1)
+        a = {}
+        if attn:
+            lay = ops.KVLayout.paged(kv.k[li], kv.v[li], bufs.block_table)
+            a = dict(a_q=bufs.q[:M], a_k=lay.k, a_v=lay.v, a_table=lay.table, a_block_size=lay.block_size,
+                     a_sb=lay.sb, a_sh=lay.sh, a_st=lay.st, a_ctx=bufs.ctx_lens, a_seq=bufs.seq_ids,
+                     a_scale=self.scale, a_n_splits=ops.decode_n_splits(bufs.max_ctx), a_part_o=bufs.part_o,
+                     a_part_ml=bufs.part_ml, a_counters=bufs.attn_cnt)
         desc, lds = ops.ext().chain_make(
             bufs.hidden[:M], bufs.attn[:M], bufs.act[:M], L.o, L.gu, L.down, self.cfg.rms_eps,
             N.qkv if nxt else None, self.nq, self.nkv, self.hd,
             bufs.positions if nxt else None, bufs.slots if nxt else None, self.rope if nxt else None,
             bufs.q[:M] if nxt else None, kv.k[li + 1] if nxt else None, kv.v[li + 1] if nxt else None,
-            self._chain_bar, self._chain_work, None, self._chain_bar_mode)
-        cache[key] = (desc, 4 if nxt else 3, lds) if desc.numel() else None
+            self._chain_bar, self._chain_work, None, self._chain_bar_mode, **a)
+        cache[key] = (desc, 4 if nxt else 3, lds, self.nq // self.nkv if attn else 0) if desc.numel() else None
         return cache[key]
 
     def chain_error_word(self):
@@ -246,6 +257,17 @@ class LlamaModel:
                 q = ops.qkv_rope_write(h, L.qkv, None, fuse_rms=True, eps=cfg.rms_eps, n_q_heads=self.nq,
                                        n_kv_heads=self.nkv, head_dim=self.hd, rope=self.rope,
                                        positions=bufs.positions, slots=bufs.slots, q_out=qbuf, k_cache=kc, v_cache=vc)
+            d = self._chain_desc(bufs, kv, M, li) if chain else None
+            if d is not None:
+                # chained layer: [decode attention ->] o_proj -> gate/up -> down [-> next QKV]
+                if not d[3]:
+                    ops.decode_attention(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens,
+                                         bufs.seq_ids, n_q_heads=self.nq, n_kv_heads=self.nkv, head_dim=self.hd,
+                                         scale=self.scale, max_ctx=bufs.max_ctx, out=bufs.attn[:M],
+                                         part_o=bufs.part_o, part_ml=bufs.part_ml, counters=bufs.attn_cnt)
+                ops.ext().chain_run(d[0], d[1], d[2], h, d[3])
+                continue
+            chain = False  # shapes the chain cannot take: per-kernel path from here on
             if prefill_seq is None:
                 attn = bufs.attn[:M]
                 ops.decode_attention(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens, bufs.seq_ids,
@@ -267,12 +289,6 @@ class LlamaModel:
                 ops.flash_attention(q4, ops.KVLayout.paged(kc, vc, table), Sk=q_offset + M, n_kv_heads=self.nkv,
                                     causal=True, scale=self.scale, q_offset=q_offset, out=attn4)
                 attn = attn4.view(M, self.nq * self.hd)
-            if chain:
-                d = self._chain_desc(bufs, kv, M, li)
-                if d is not None:
-                    ops.ext().chain_run(d[0], d[1], d[2], h)
-                    continue
-                chain = False  # shapes the chain cannot take: per-kernel path from here on
             self._row_parallel(attn, L.o, h)
             act = bufs.act[:M] if M <= bufs.act.shape[0] else None
             act = ops.linear_swiglu(h, L.gu, fuse_rms=True, eps=cfg.rms_eps, out=act)
