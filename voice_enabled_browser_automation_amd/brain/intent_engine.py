@@ -102,6 +102,7 @@ class LLMIntentEngine:
         dev = engine.device
         self.dev = dev
         pin = dev.type == "cuda"
+        self._cuda_index = (dev.index if dev.index is not None else torch.cuda.current_device()) if pin else None
         R, W = self.max_active, self.grammar.words
         self.h_mask = torch.zeros(R, W, dtype=torch.int32, pin_memory=pin)
         self.h_mask_np = self.h_mask.numpy()
@@ -361,7 +362,9 @@ class LLMIntentEngine:
 
     def _loop(self) -> None:
         if self.dev.type == "cuda":
-            torch.cuda.set_device(self.dev)
+            # the scheduler thread inherits no current device: use the model's ("cuda" with no
+            # index means the device that was current when the engine was built)
+            torch.cuda.set_device(self._cuda_index)
         while True:
             with self._lock:
                 while not self._stop and not self.waiting and not self.active:
