@@ -249,6 +249,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   cp.ph[2].epi = 1;
   set_resid(cp.ph[2].p, h);
   cp.n = 3;
+  cp.seq = 0;
   if (w_qkv.has_value()) {
     TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
                     v_cache.has_value(),
@@ -319,13 +320,13 @@ Tensor alloc_uncached_i32(int64_t n, Tensor like) {
                           torch::dtype(torch::kInt).device(like.device()));
 }
 
-void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like, int64_t attn_g) {
+void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like, int64_t attn_g, int64_t seq) {
   c10::DeviceGuard g(like.device());
   TORCH_CHECK(desc.is_cuda() && desc.numel() == (int64_t)sizeof(ChainParams), "bad chain descriptor");
   int dev = like.device().index(), cus = 0;
   TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess, "CU count");
   // one workgroup per CU: the barrier needs every workgroup resident
-  check_rc(vwa_chain_launch(reinterpret_cast<const ChainParams*>(desc.data_ptr()), (int)n_phases, (int)attn_g, (int)lds, cus,
+  check_rc(vwa_chain_launch(reinterpret_cast<const ChainParams*>(desc.data_ptr()), (int)seq, (int)n_phases, (int)attn_g, (int)lds, cus,
                             cur_stream(like)),
            "chain");
 }
@@ -665,7 +666,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_n_splits") = 0, py::arg("a_part_o") = py::none(), py::arg("a_part_ml") = py::none(),
         py::arg("a_counters") = py::none());
   m.def("chain_run", &chain_run, py::arg("desc"), py::arg("n_phases"), py::arg("lds"), py::arg("like"),
-        py::arg("attn_g") = 0);
+        py::arg("attn_g") = 0, py::arg("seq") = 0);
   m.def("alloc_uncached_i32", &alloc_uncached_i32);
   m.def("decode_advance", &decode_advance);
   m.def("rmsnorm", &rmsnorm);

@@ -682,8 +682,10 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
   u16* xs = reinterpret_cast<u16*>(smem);
   const int xbytes = ((M * xstride * 2) + 15) & ~15;
   float* red = reinterpret_cast<float*>(smem + xbytes);
-  float* rs = red + KS * NT * 4 * 64;
-  int* s_flag = reinterpret_cast<int*>(rs + 16);
+  float* rs = red + KS * NT * 4 * 64;  // [16] row scales (1/rms or LayerNorm rstd)
+  float* mu = rs + 16;                  // [16] row means (folded LayerNorm)
+  int* s_flag = reinterpret_cast<int*>(rs + 32);
+  const float* mus = p.fuse_rms == 2 ? mu : nullptr;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nl = lane & 15, g = lane >> 4;
   const PhaseRange r = chain_range<KS>(ph);
@@ -702,18 +704,30 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
   }
   __syncthreads();
   for (int m = w; m < 16; m += KS) {
-    float sc = 1.f;
+    float sc = 1.f, mean = 0.f;
     if (p.fuse_rms && m < M) {
-      float s = 0.f;
+      float s = 0.f, s1 = 0.f;
       for (int kk = lane; kk < k8; kk += 64) {
         float f[8];
         unpack8(*reinterpret_cast<const uint4*>(xs + m * xstride + kk * 8), f);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s += f[j] * f[j];
+        for (int j = 0; j < 8; ++j) {
+          s += f[j] * f[j];
+          s1 += f[j];
+        }
       }
-      sc = rsqrtf(wave_sum(s) / (float)K + p.eps);
+      s = wave_sum(s);
+      if (p.fuse_rms == 2) {  // folded LayerNorm (Whisper): rstd from E[x^2] - mean^2
+        mean = wave_sum(s1) / (float)K;
+        sc = rsqrtf(fmaxf(s / (float)K - mean * mean, 0.f) + p.eps);
+      } else {
+        sc = rsqrtf(s / (float)K + p.eps);
+      }
     }
-    if (lane == 0) rs[m] = sc;
+    if (lane == 0) {
+      rs[m] = sc;
+      mu[m] = mean;
+    }
   }
   __syncthreads();
 
@@ -742,7 +756,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
     if (unit % nb != nb - 1 && it != r.n_items - 1) return;  // tile continues in this range
     const bool whole = tile * nb >= r.u0 && (tile + 1) * nb <= u1;
     if (whole) {
-      tile_epilogue<EPI, NT, KS, true>(p, red, rs, nullptr, tile, acc, w, lane, pre, tile == first_tile);
+      tile_epilogue<EPI, NT, KS, true>(p, red, rs, mus, tile, acc, w, lane, pre, tile == first_tile);
       return;
     }
     // split tile: publish, ticket, the second arriver finishes it
@@ -760,7 +774,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
     }
     __syncthreads();
     if (*s_flag) {
-      tile_epilogue<EPI, NT, KS, true>(p, red, rs, nullptr, tile, acc, w, lane, pre, false,
+      tile_epilogue<EPI, NT, KS, true>(p, red, rs, mus, tile, acc, w, lane, pre, false,
                                        slots + (1 - mine) * per);
     } else {
 #pragma unroll
@@ -780,16 +794,27 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
   }
 }
 
-// The phase sequence is static (the Llama layer tail: o_proj+residual, gate/up+SwiGLU,
-// down+residual [, next layer's QKV]); a runtime epilogue switch measured 50+ VGPR spills.
-// AG > 0: the layer's decode attention (GQA group AG, head_dim 128) runs first, as phase 0 of
-// the same launch (mq_attention.h with 8 waves, one register set, outputs written through to
-// memory); workgroups without an attention item issue their o_proj weights at once.  Measured
-// (tools/chain_probe.py --attn, 1 row, ctx 1100): 111.6 us vs 111-112 us for the standalone
-// attention kernel + the GEMM chain -- the attention phase itself is slower in the 8-wave form
-// (13-14 us vs 10.5 us) and o_proj still needs X staging + reduction after the barrier, so the
-// model keeps the separate attention launch (VWA_CHAIN_ATTN=1 selects this form).
-template <int KS, bool WITH_QKV, int AG>
+// The phase sequence is static (a runtime epilogue switch measured 50+ VGPR spills):
+//   SEQ 0  Llama tail       o_proj+res -> RMSNorm gate/up+SwiGLU -> down+res [-> RMSNorm QKV+RoPE+KV]
+//   SEQ 1  Whisper tail     out-proj+res -> LN fc1+GELU -> fc2+res [-> LN self-attn QKV+KV]
+//   SEQ 2  Whisper middle   self-attn out-proj+res -> LN cross-attn query (store)
+// (Whisper LayerNorms folded into the weights, mean/rstd from the staged rows; biases in the
+// epilogues.)  AG > 0 (Llama only): the layer's decode attention (GQA group AG, head_dim 128)
+// runs first, as phase 0 of the same launch (mq_attention.h with 8 waves, one register set,
+// outputs written through to memory); workgroups without an attention item issue their o_proj
+// weights at once.  Measured (tools/chain_probe.py --attn, 1 row, ctx 1100): 111.6 us vs
+// 111-112 us for the standalone attention kernel + the GEMM chain -- the attention phase itself
+// is slower in the 8-wave form (13-14 us vs 10.5 us) and o_proj still needs X staging +
+// reduction after the barrier, so the model keeps the separate attention launch
+// (VWA_CHAIN_ATTN=1 selects this form).
+template <int SEQ, int I>
+struct SeqEpi {
+  static constexpr int value = SEQ == 0 ? (I == 0 ? EPI_RESID : I == 1 ? EPI_SWIGLU : I == 2 ? EPI_RESID : EPI_QKV)
+                               : SEQ == 1 ? (I == 0 ? EPI_RESID : I == 1 ? EPI_GELU : I == 2 ? EPI_RESID : EPI_QKV)
+                                          : (I == 0 ? EPI_RESID : EPI_STORE);
+};
+
+template <int KS, int SEQ, int NPH, int AG>
 __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __restrict__ cpp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ChainParams& cp = *cpp;  // device-resident descriptor
@@ -805,42 +830,41 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     ++nts;
   };
   stamp();
+  constexpr int E0 = SeqEpi<SEQ, 0>::value, E1 = SeqEpi<SEQ, 1>::value, E2 = SeqEpi<SEQ, 2>::value,
+                E3 = SeqEpi<SEQ, 3>::value;
   if constexpr (AG > 0) {
-    // (measured: issuing the o_proj weights BEFORE the attention doubled the attention phase,
-    // 21.5 vs 10.5 us: its dependent metadata / K / V round trips queued behind 33 MB of weight
-    // loads -- vmcnt retires in order -- so they go out at the barrier instead)
-    // workgroups without an attention item issue their o_proj weights at once; the others after
-    // their item, at the barrier
     const bool idle = mq_body<128, AG, KS, true, false>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
                                                         (int)blockIdx.x,
-                                                        [&]() { chain_issue_first<EPI_RESID, KS>(cp.ph[0], A); });
+                                                        [&]() { chain_issue_first<E0, KS>(cp.ph[0], A); });
     stamp();
     gen = chain_arrive(bar, nwg, cp.bar_mode);
-    if (!idle) chain_issue_first<EPI_RESID, KS>(cp.ph[0], A);
+    if (!idle) chain_issue_first<E0, KS>(cp.ph[0], A);
     chain_wait(bar, gen, cp.bar_mode);
   } else {
-    chain_issue_first<EPI_RESID, KS>(cp.ph[0], A);
+    chain_issue_first<E0, KS>(cp.ph[0], A);
   }
-  chain_phase<EPI_RESID, KS>(cp, 0, A, B, smem);
+  chain_phase<E0, KS>(cp, 0, A, B, smem);
   stamp();
   gen = chain_arrive(bar, nwg, cp.bar_mode);
-  chain_issue_first<EPI_SWIGLU, KS>(cp.ph[1], A);
+  chain_issue_first<E1, KS>(cp.ph[1], A);
   chain_wait(bar, gen, cp.bar_mode);
   stamp();
-  chain_phase<EPI_SWIGLU, KS>(cp, 1, A, B, smem);
+  chain_phase<E1, KS>(cp, 1, A, B, smem);
   stamp();
-  gen = chain_arrive(bar, nwg, cp.bar_mode);
-  chain_issue_first<EPI_RESID, KS>(cp.ph[2], A);
-  chain_wait(bar, gen, cp.bar_mode);
-  stamp();
-  chain_phase<EPI_RESID, KS>(cp, 2, A, B, smem);
-  stamp();
-  if constexpr (WITH_QKV) {
+  if constexpr (NPH >= 3) {
     gen = chain_arrive(bar, nwg, cp.bar_mode);
-    chain_issue_first<EPI_QKV, KS>(cp.ph[3], A);
+    chain_issue_first<E2, KS>(cp.ph[2], A);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<EPI_QKV, KS>(cp, 3, A, B, smem);
+    chain_phase<E2, KS>(cp, 2, A, B, smem);
+    stamp();
+  }
+  if constexpr (NPH >= 4) {
+    gen = chain_arrive(bar, nwg, cp.bar_mode);
+    chain_issue_first<E3, KS>(cp.ph[3], A);
+    chain_wait(bar, gen, cp.bar_mode);
+    stamp();
+    chain_phase<E3, KS>(cp, 3, A, B, smem);
     stamp();
   }
 }
@@ -853,16 +877,19 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
 // launched with vwa_chain_launch (graph-capturable: no allocation, no copy at launch).
 extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
   constexpr int KS = 8;
-  if (cp->n < 3 || cp->n > kChainMaxPhases || grid < 1) return -10;
-  static const int kSeq[kChainMaxPhases] = {EPI_RESID, EPI_SWIGLU, EPI_RESID, EPI_QKV};
+  if (cp->n < 2 || cp->n > kChainMaxPhases || grid < 1) return -10;
+  static const int kSeq[3][kChainMaxPhases] = {{EPI_RESID, EPI_SWIGLU, EPI_RESID, EPI_QKV},
+                                               {EPI_RESID, EPI_GELU, EPI_RESID, EPI_QKV},
+                                               {EPI_RESID, EPI_STORE, -1, -1}};
+  if (cp->seq < 0 || cp->seq > 2 || (cp->seq == 2 ? cp->n != 2 : cp->n < 3)) return -10;
   size_t lds = 0;
   for (int i = 0; i < cp->n; ++i) {
     ChainPhase& ph = cp->ph[i];
     const SkinnyParams& p = ph.p;
-    if (ph.epi != kSeq[i]) return -10;
+    if (ph.epi != kSeq[cp->seq][i]) return -10;
     ph.nt = (ph.epi == EPI_SWIGLU) ? 2 : 1;
     const int U = 4 / ph.nt;
-    if (p.M < 1 || p.M > 4 || p.K % 128 != 0 || p.N % (16 * ph.nt) != 0 || p.w_scale || p.fuse_rms == 2) return -10;
+    if (p.M < 1 || p.M > 4 || p.K % 128 != 0 || p.N % (16 * ph.nt) != 0 || p.w_scale) return -10;
     if ((size_t)p.N * p.K * 2 >= 0x7FFFFFF0ull || (size_t)p.M * p.ldx * 2 >= 0x7FFFFFF0ull) return -10;
     const int G = p.K / 128;
     const int per_wave = (G + KS - 1) / KS;
@@ -873,23 +900,34 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     if (ph.nb > 1 && units / grid < ph.nb - 1) return -10;
     if (ntiles > cp->max_tiles || (size_t)ntiles * 2 * p.M * 16 * ph.nt > (size_t)cp->part_floats) return -10;
     const size_t x = ((size_t)p.M * (p.K + 8) * 2 + 15) & ~(size_t)15;
-    const size_t need = x + (size_t)(KS * ph.nt * 4 * 64 + 32) * sizeof(float);
+    const size_t need = x + (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float);  // + scales, means, flag
     if (need > lds) lds = need;
   }
   if (lds > 160 * 1024) return -10;
   return (int)lds;
 }
 
-extern "C" int vwa_chain_launch(const ChainParams* d_cp, int n_phases, int attn_g, int lds, int grid, hipStream_t st) {
+extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid,
+                                hipStream_t st) {
   if (attn_g) lds = lds > (int)MqLds<128, 8>::bytes ? lds : (int)MqLds<128, 8>::bytes;
-#define VWA_CHAIN_LAUNCH(Q, G) hipLaunchKernelGGL((chain_kernel<8, Q, G>), dim3(grid), dim3(8 * 64), lds, st, d_cp)
-  if (n_phases != 3 && n_phases != 4) return -10;
-  const bool q = n_phases == 4;
-  switch (attn_g) {
-    case 0: if (q) VWA_CHAIN_LAUNCH(true, 0); else VWA_CHAIN_LAUNCH(false, 0); break;
-    case 4: if (q) VWA_CHAIN_LAUNCH(true, 4); else VWA_CHAIN_LAUNCH(false, 4); break;
-    case 8: if (q) VWA_CHAIN_LAUNCH(true, 8); else VWA_CHAIN_LAUNCH(false, 8); break;
-    default: return -10;
+#define VWA_CHAIN_LAUNCH(S, N, G) hipLaunchKernelGGL((chain_kernel<8, S, N, G>), dim3(grid), dim3(8 * 64), lds, st, d_cp)
+  if (seq == 0) {
+    if (n_phases != 3 && n_phases != 4) return -10;
+    const bool q = n_phases == 4;
+    switch (attn_g) {
+      case 0: if (q) VWA_CHAIN_LAUNCH(0, 4, 0); else VWA_CHAIN_LAUNCH(0, 3, 0); break;
+      case 4: if (q) VWA_CHAIN_LAUNCH(0, 4, 4); else VWA_CHAIN_LAUNCH(0, 3, 4); break;
+      case 8: if (q) VWA_CHAIN_LAUNCH(0, 4, 8); else VWA_CHAIN_LAUNCH(0, 3, 8); break;
+      default: return -10;
+    }
+  } else if (seq == 1 && attn_g == 0) {
+    if (n_phases == 4) VWA_CHAIN_LAUNCH(1, 4, 0);
+    else if (n_phases == 3) VWA_CHAIN_LAUNCH(1, 3, 0);
+    else return -10;
+  } else if (seq == 2 && attn_g == 0 && n_phases == 2) {
+    VWA_CHAIN_LAUNCH(2, 2, 0);
+  } else {
+    return -10;
   }
 #undef VWA_CHAIN_LAUNCH
   return (int)hipGetLastError();

@@ -65,6 +65,7 @@ struct ChainPhase {
 struct ChainParams {
   ChainPhase ph[kChainMaxPhases];
   int n;
+  int seq;                 // 0 Llama tail, 1 Whisper tail, 2 Whisper middle (skinny_stream.hip chain_kernel)
   unsigned* bar;
   int bar_mode;            // 0: flat ticket counter, 1: two-level (8 groups + top), 2: two-level + scalar polls
   float* part;             // split-tile partial slots [max_tiles][2][M][16*nt] f32
@@ -96,7 +97,7 @@ extern "C" {
 int vwa_skinny_gemm(int epi, const SkinnyParams* p, hipStream_t st);
 int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st);
 int vwa_chain_prepare(ChainParams* cp, int grid);
-int vwa_chain_launch(const ChainParams* d_cp, int n_phases, int attn_g, int lds, int grid, hipStream_t st);
+int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid, hipStream_t st);
 int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
                 uint16_t* y, int rows, int D, int ldx, float eps, hipStream_t st);
 int vwa_layernorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
