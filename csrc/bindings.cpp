@@ -294,6 +294,68 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   return {host.to(h.device()), (int64_t)lds};
 }
 
+// Whisper decoder chains (skinny_stream.hip chain_kernel SEQ 1 / 2): phase i computes
+// Y[i] (=|+=) X[i] . W[i]^T + bias[i] with the epilogue epi[i] (0 store, 1 residual into Y, 3 GELU,
+// 4 QKV + self-KV write, no RoPE); ln_c[i] set = LayerNorm folded into W[i] (fuse_rms 2).
+std::tuple<Tensor, int64_t> chain_make_seq(int64_t seq, std::vector<Tensor> X, std::vector<Tensor> W,
+                                           std::vector<c10::optional<Tensor>> bias,
+                                           std::vector<c10::optional<Tensor>> ln_c, std::vector<Tensor> Y,
+                                           std::vector<int64_t> epi, double eps, int64_t n_heads, int64_t head_dim,
+                                           c10::optional<Tensor> positions, c10::optional<Tensor> slots,
+                                           c10::optional<Tensor> k_cache, c10::optional<Tensor> v_cache, Tensor bar,
+                                           Tensor work, int64_t bar_mode) {
+  const size_t n = X.size();
+  TORCH_CHECK(n >= 2 && n <= (size_t)kChainMaxPhases && W.size() == n && bias.size() == n && ln_c.size() == n &&
+                  Y.size() == n && epi.size() == n,
+              "chain_make_seq: one X/W/bias/ln_c/Y/epi per phase");
+  TORCH_CHECK(seq == 1 || seq == 2, "chain_make_seq: seq 1 (Whisper tail) or 2 (Whisper middle)");
+  c10::DeviceGuard g(X[0].device());
+  TORCH_CHECK(bar.is_cuda() && bar.scalar_type() == at::kInt && bar.numel() >= 384 && bar.is_contiguous() &&
+                  (reinterpret_cast<uintptr_t>(bar.data_ptr()) & 127) == 0,
+              "bar must be a 128-byte aligned int32[>=384] on the GPU");
+  TORCH_CHECK(work.is_cuda() && work.scalar_type() == at::kInt && work.is_contiguous() && work.numel() > 8192 + 4096,
+              "work must be a zeroed int32 GPU tensor of > 12288 elements");
+  ChainParams cp{};
+  const int64_t M = X[0].size(0);
+  for (size_t i = 0; i < n; ++i) {
+    TORCH_CHECK(X[i].size(0) == M && Y[i].size(0) == M, "row counts differ");
+    SkinnyParams& p = cp.ph[i].p;
+    p = base_params(X[i], W[i], bias[i], false, eps);
+    cp.ph[i].epi = (int)epi[i];
+    set_ln_fold(p, ln_c[i], (int)epi[i]);
+    if (epi[i] == 4) {
+      TORCH_CHECK(positions && slots && k_cache && v_cache, "the QKV phase needs positions, slots and the KV caches");
+      set_qkv_epilogue(p, W[i], n_heads, n_heads, head_dim, false, *positions, *slots, c10::nullopt, Y[i], *k_cache,
+                       *v_cache);
+      continue;
+    }
+    check_bf16(Y[i], "Y");
+    TORCH_CHECK(Y[i].dim() == 2 && Y[i].stride(1) == 1 && Y[i].size(1) == W[i].size(0), "Y must be [M, N] rows");
+    if (epi[i] == 1) {
+      set_resid(p, Y[i]);
+    } else {
+      p.Y = Y[i].data_ptr();
+      p.ldy = (int)Y[i].stride(0);
+    }
+  }
+  cp.n = (int)n;
+  cp.seq = (int)seq;
+  cp.bar = reinterpret_cast<unsigned*>(bar.data_ptr<int>());
+  cp.bar_mode = (int)bar_mode;
+  cp.tickets = reinterpret_cast<unsigned*>(work.data_ptr<int>());
+  cp.max_tiles = 8192;
+  cp.part = reinterpret_cast<float*>(work.data_ptr<int>() + 8192);
+  cp.part_floats = (int)(work.numel() - 8192);
+  int cus = 0;
+  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, X[0].device().index()) == hipSuccess,
+              "CU count");
+  const int lds = vwa_chain_prepare(&cp, cus);
+  if (lds < 0) return {torch::empty({0}, torch::dtype(torch::kUInt8).device(X[0].device())), 0};
+  Tensor host = torch::empty({(int64_t)sizeof(ChainParams)}, torch::dtype(torch::kUInt8));
+  std::memcpy(host.data_ptr(), &cp, sizeof(ChainParams));
+  return {host.to(X[0].device()), (int64_t)lds};
+}
+
 // One-row device-resident decode loop step (see elementwise.hip decode_advance_kernel)
 void decode_advance(Tensor tokens, Tensor positions, Tensor ctx_lens, Tensor slots, Tensor sampled, Tensor out,
                     Tensor counter, int64_t base_block, int64_t block_size) {
@@ -665,6 +727,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_st") = 0, py::arg("a_ctx") = py::none(), py::arg("a_seq") = py::none(), py::arg("a_scale") = 0.0,
         py::arg("a_n_splits") = 0, py::arg("a_part_o") = py::none(), py::arg("a_part_ml") = py::none(),
         py::arg("a_counters") = py::none());
+  m.def("chain_make_seq", &chain_make_seq, py::arg("seq"), py::arg("X"), py::arg("W"), py::arg("bias"),
+        py::arg("ln_c"), py::arg("Y"), py::arg("epi"), py::arg("eps"), py::arg("n_heads"), py::arg("head_dim"),
+        py::arg("positions"), py::arg("slots"), py::arg("k_cache"), py::arg("v_cache"), py::arg("bar"),
+        py::arg("work"), py::arg("bar_mode") = 1);
   m.def("chain_run", &chain_run, py::arg("desc"), py::arg("n_phases"), py::arg("lds"), py::arg("like"),
         py::arg("attn_g") = 0, py::arg("seq") = 0);
   m.def("alloc_uncached_i32", &alloc_uncached_i32);

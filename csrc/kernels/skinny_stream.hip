@@ -896,8 +896,10 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     ph.nb = (per_wave + U - 1) / U;
     const long long ntiles = p.N / (16 * ph.nt);
     const long long units = ntiles * ph.nb;
-    // a tile may straddle at most two workgroup ranges (two partial slots per tile)
-    if (ph.nb > 1 && units / grid < ph.nb - 1) return -10;
+    // a tile may straddle at most two workgroup ranges (two partial slots per tile): every
+    // non-empty range (floor or ceil of units / grid units, >= 1) must hold >= nb - 1 units
+    const long long min_range = units / grid > 0 ? units / grid : 1;
+    if (ph.nb > 1 && min_range < ph.nb - 1) return -10;
     if (ntiles > cp->max_tiles || (size_t)ntiles * 2 * p.M * 16 * ph.nt > (size_t)cp->part_floats) return -10;
     const size_t x = ((size_t)p.M * (p.K + 8) * 2 + 15) & ~(size_t)15;
     const size_t need = x + (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float);  // + scales, means, flag

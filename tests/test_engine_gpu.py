@@ -224,3 +224,42 @@ def test_prefix_cached_prefill_decode_attention_slices(monkeypatch):
     a, b = run("1"), run("0")
     err = (a - b).abs().max().item()
     assert err < 0.02 * (1 + b.abs().max().item()), err
+
+
+@pytest.mark.parametrize("name", ["whisper-test", "whisper-tiny", "whisper-large-v3"])
+def test_whisper_chained_decoder_matches_per_kernel_path(name, monkeypatch):
+    """The chained Whisper decoder launches (out-proj -> LN cross query; out-proj -> LN fc1 GELU
+    -> fc2 -> next layer's LN QKV + self-KV write, skinny_stream.hip chain_kernel SEQ 2 / 1)
+    against the per-kernel path on the same weights and caches, for 1, 2 and 4 rows over a few
+    positions (large-v3: its layer shapes, 3 decoder layers)."""
+    from voice_enabled_browser_automation_amd.asr.engine import WhisperRunner
+
+    ops.ext()
+    cfg = get_config(name)
+    if name == "whisper-large-v3":
+        import dataclasses
+
+        cfg = dataclasses.replace(cfg, n_enc_layers=1, n_dec_layers=3)
+    m = WhisperModel(cfg, device="cuda", seed=7)
+    torch.manual_seed(1)
+    enc = torch.randn(1, cfg.n_audio_ctx, cfg.d_model, device="cuda").to(torch.bfloat16)
+
+    def run(chain: bool):
+        monkeypatch.setenv("VWA_CHAIN_ASR", "1" if chain else "0")
+        r = WhisperRunner(m, max_sessions=2, use_graphs=False)
+        r.set_cross(0, enc)
+        r.set_cross(1, enc)
+        out, pos = [], 0
+        for n in (1, 2, 4, 1, 4):
+            rows = [(i % 2, (7 * pos + 3 * i) % 1000, pos + i // 2) for i in range(n)]
+            out.append(r.step(rows).float().cpu().clone())
+            pos += 2
+        return out
+
+    ref = run(False)
+    got = run(True)
+    assert not m.chain_error()
+    assert m._chains and all(a is not None and b is not None for a, b in m._chains.values())
+    for a, b in zip(got, ref):
+        err = (a - b).abs().max().item()
+        assert err < 0.03 * (1 + b.abs().max().item()), err

@@ -1,0 +1,56 @@
+"""Whisper transcription time split (encoder / decoder) with and without the chained decoder
+launches (models/whisper.py, skinny_stream.hip chain_kernel SEQ 1/2), fixed 40-token work on the
+bench's synthetic 10 s utterance.  One JSON line per mode.
+python tools/asr_timing.py [--asr whisper-large-v3] [--reps 10]"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import synth_speech  # noqa: E402
+from voice_enabled_browser_automation_amd import ops  # noqa: E402
+from voice_enabled_browser_automation_amd.asr.engine import AsrEngine  # noqa: E402
+from voice_enabled_browser_automation_amd.models.config import get_config  # noqa: E402
+from voice_enabled_browser_automation_amd.models.whisper import WhisperModel  # noqa: E402
+from voice_enabled_browser_automation_amd.tokenizer import load_tokenizer  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--asr", default="whisper-tiny")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--tokens", type=int, default=40)
+    a = ap.parse_args()
+    ops.ext()
+    m = WhisperModel(get_config(a.asr), device="cuda", seed=0)
+    audio = None
+    texts = {}
+    for chain in ("0", "1"):
+        os.environ["VWA_CHAIN_ASR"] = chain
+        m._chains = {}
+        eng = AsrEngine(m, load_tokenizer("whisper"), max_sessions=2)
+        audio = eng.pcm_to_audio(synth_speech(10.0, seed=100))
+        for _ in range(2):
+            eng.transcribe(audio, exact_tokens=a.tokens)
+        enc, dec, tot = [], [], []
+        for _ in range(a.reps):
+            torch.cuda.synchronize()
+            texts[chain] = eng.transcribe(audio, exact_tokens=a.tokens)
+            s = eng.last_stats
+            enc.append(s["encode_ms"])
+            dec.append(s["decode_ms"])
+            tot.append(s["total_ms"])
+        print(json.dumps(dict(tool="asr_timing", asr=a.asr, chain=chain == "1", tokens=a.tokens,
+                              encode_ms=round(statistics.median(enc), 2), decode_ms=round(statistics.median(dec), 2),
+                              total_ms=round(statistics.median(tot), 2),
+                              decode_us_per_token=round(1e3 * statistics.median(dec) / a.tokens, 1),
+                              chained=bool(m._chains))), flush=True)
+    print(json.dumps(dict(tool="asr_timing", same_text=texts["0"] == texts["1"])), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -264,6 +264,7 @@ class AsrEngine:
         if B > len(self.free_slots):
             raise RuntimeError(f"{B} utterances exceed the {len(self.free_slots)} free ASR session slots")
         slots = [self.free_slots.pop() for _ in range(B)]
+        retry = False
         try:
             mel = torch.stack([m.log_mel(a) for a in audios])
             enc = m.encode(mel)
@@ -296,13 +297,32 @@ class AsrEngine:
                     break
                 logits = self.runner.step([(slots[j], outs[j][-1], pos) for j in live])
                 pos += 1
+            if self._chain_failed():  # results of a timed-out chained launch are invalid: redo
+                retry = True
             texts = [self.tok.decode(o) for o in outs]
             t_end = time.perf_counter()
             self.last_stats = dict(encode_ms=(t_enc - t0) * 1e3, decode_ms=(t_end - t_enc) * 1e3,
                                    total_ms=(t_end - t0) * 1e3, tokens=sum(len(o) for o in outs), batch=B)
-            return texts
+            if not retry:
+                return texts
         finally:
             self.free_slots.extend(slots)
+        return self.transcribe_many(audios, max_tokens=max_tokens, min_tokens=min_tokens, exact_tokens=exact_tokens)
+
+    def _chain_failed(self) -> bool:
+        """Health check of the chained decoder launches (models/whisper.py): a grid barrier that
+        timed out (workgroups not co-resident) leaves an error word; the model then falls back to
+        per-kernel launches and every captured graph is dropped."""
+        m = self.model
+        if getattr(m, "chain_error", None) is None or getattr(m, "_chain_disabled", False) or not m.chain_error():
+            return False
+        import warnings
+
+        warnings.warn("chained Whisper decode launch timed out at a grid barrier; using per-kernel launches")
+        m.disable_chain()
+        self.runner.graphs.clear()
+        self.loop_graphs.clear()
+        return True
 
     def _sample_rows(self, logits: torch.Tensor, allow_eot: bool) -> List[int]:
         n = logits.shape[0]

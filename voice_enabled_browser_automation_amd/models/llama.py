@@ -177,17 +177,7 @@ class LlamaModel:
         if key in cache:
             return cache[key]
         if getattr(self, "_chain_bar", None) is None:
-            # barrier words in L2-uncached memory, polled with scalar loads (bar_mode 2: the poll
-            # does not queue behind the next phase's weight loads); plain memory + vector polls
-            # (bar_mode 1) if the uncached allocation is unavailable
-            try:
-                self._chain_bar = ops.ext().alloc_uncached_i32(512, torch.empty(1, device=self.device))
-                self._chain_bar_mode = 2
-            except RuntimeError:
-                self._chain_bar = torch.zeros(512, dtype=torch.int32, device=self.device)
-                self._chain_bar_mode = 1
-            # split-tile tickets + partial slots (ops: skinny_stream.hip chain_phase)
-            self._chain_work = torch.zeros(1 << 20, dtype=torch.int32, device=self.device)
+            self._chain_bar, self._chain_bar_mode, self._chain_work = ops.chain_buffers(self.device)
         L = self.layers[li]
         nxt = li + 1 < len(self.layers)
         N = self.layers[li + 1] if nxt else None
@@ -213,8 +203,7 @@ class LlamaModel:
 
     def chain_error_word(self):
         """The device word a timed-out chain barrier sets (None before the first chained launch)."""
-        bar = getattr(self, "_chain_bar", None)
-        return None if bar is None else bar.view(torch.int64)[160:161]
+        return ops.chain_error_word(getattr(self, "_chain_bar", None))
 
     def chain_error(self) -> bool:
         """True when a chained launch's grid barrier timed out (results of that step are invalid)."""

@@ -229,33 +229,106 @@ class WhisperModel:
         return out
 
     # ------------------------------------------------------------------ decoder step
+    # ---- chained decode launches (skinny_stream.hip chain_kernel SEQ 2 / SEQ 1; M <= 4 rows).
+    # Opt-in (VWA_CHAIN_ASR=1): measured (tools/asr_timing.py, 1 row, 40 tokens) 2.32 vs 2.26 ms
+    # per token for whisper-large-v3 and 260 vs 244 us for whisper-tiny -- the decoder's
+    # phases are 0.3-13 MB each, so every phase is latency-bound and a grid barrier (~4-5 us,
+    # arrival spread + two-level atomics in uncached memory) costs what a kernel boundary does.
+    def _chain_ok(self, M: int) -> bool:
+        return (M <= 4 and self.device.type == "cuda" and self.dtype == torch.bfloat16
+                and not getattr(self, "_chain_disabled", False) and ops.env_flag("VWA_CHAIN_ASR", False)
+                and ops.native_available() and all(hasattr(L, "f_qkv") for L in self.dec))
+
+    def disable_chain(self) -> None:
+        self._chain_disabled = True
+        self._chains = {}
+
+    def chain_error_word(self):
+        return ops.chain_error_word(getattr(self, "_chain_bar", None))
+
+    def chain_error(self) -> bool:
+        w = self.chain_error_word()
+        return bool(w is not None and int(w.item()) != 0)
+
+    def _chain_descs(self, bufs, M: int, li: int):
+        """Layer li's two chained launches for these buffers, built on first use:
+        middle = self-attn out-proj + residual -> LN cross-attn query (store to bufs.q);
+        tail = cross-attn out-proj + residual -> LN fc1 + GELU -> fc2 + residual [-> next layer's
+        LN self-attn QKV + self-KV write].  Each entry (descriptor, n_phases, lds) or None."""
+        cache = self.__dict__.setdefault("_chains", {})
+        key = (id(bufs), M, li)
+        if key in cache:
+            return cache[key]
+        if getattr(self, "_chain_bar", None) is None:
+            self._chain_bar, self._chain_bar_mode, self._chain_work = ops.chain_buffers(self.device)
+        L, eps = self.dec[li], self.cfg.ln_eps
+        x, att, q, f = bufs.hidden[:M], bufs.att[:M], bufs.q[:M], bufs.f[:M]
+        common = dict(eps=eps, n_heads=self.H, head_dim=self.hd, bar=self._chain_bar, work=self._chain_work,
+                      bar_mode=self._chain_bar_mode)
+        (wq, bq, cq), (w1, b1, c1) = L.f_xq, L.f_fc1
+        mid = ops.ext().chain_make_seq(2, [att, x], [L.o, wq], [L.o_b, bq], [None, cq], [x, q], [1, 0],
+                                       positions=None, slots=None, k_cache=None, v_cache=None, **common)
+        X, W, B, C, Y, E = [att, x, f], [L.xo, w1, L.fc2], [L.xo_b, b1, L.fc2_b], [None, c1, None], [x, f, x], [1, 3, 1]
+        nxt = li + 1 < len(self.dec)
+        if nxt:
+            wn, bn, cn = self.dec[li + 1].f_qkv
+            X, W, B, C, Y, E = X + [x], W + [wn], B + [bn], C + [cn], Y + [q], E + [4]
+        tail = ops.ext().chain_make_seq(1, X, W, B, C, Y, E, positions=bufs.positions if nxt else None,
+                                        slots=bufs.slots if nxt else None,
+                                        k_cache=bufs.k_cache[li + 1] if nxt else None,
+                                        v_cache=bufs.v_cache[li + 1] if nxt else None, **common)
+        cache[key] = ((mid[0], 2, mid[1]) if mid[0].numel() else None,
+                      (tail[0], len(E), tail[1]) if tail[0].numel() else None)
+        return cache[key]
+
     def decode_step(self, bufs, M: int) -> torch.Tensor:
         """M token rows (bufs: tokens/positions/slots/seq_ids/ctx_lens + self cache + cross K/V).
-        Returns f32 logits [M, vocab]."""
+        Returns f32 logits [M, vocab].  Eight launches per layer; with VWA_CHAIN_ASR=1 and M <= 4
+        four (self-attention, chained out-proj -> cross query, cross-attention, chained out-proj
+        -> MLP -> next QKV)."""
         cfg = self.cfg
         d = cfg.d_model
         x = bufs.hidden[:M]
         ops.embedding(bufs.tokens, self.tok_emb, pos_table=self.pos_emb, positions=bufs.positions, out=x, rows=M)
         eps = cfg.ln_eps
+        chain = self._chain_ok(M)
+        qkv_done = False
         for li, L in enumerate(self.dec):
-            w, b, c = L.f_qkv  # self_attn_layer_norm folded in
-            q = ops.qkv_rope_write(x, w, b, fuse_rms=False, eps=eps, n_q_heads=self.H, n_kv_heads=self.H,
-                                   head_dim=self.hd, rope=None, positions=bufs.positions, slots=bufs.slots,
-                                   q_out=bufs.q, k_cache=bufs.k_cache[li], v_cache=bufs.v_cache[li], ln_c=c)
+            mid = tail = None
+            if chain:
+                mid, tail = self._chain_descs(bufs, M, li)
+                if mid is None or tail is None:
+                    chain = False  # shapes the chain cannot take: per-kernel path
+            if qkv_done:
+                q = bufs.q[:M]  # written by the previous layer's chained launch
+            else:
+                w, b, c = L.f_qkv  # self_attn_layer_norm folded in
+                q = ops.qkv_rope_write(x, w, b, fuse_rms=False, eps=eps, n_q_heads=self.H, n_kv_heads=self.H,
+                                       head_dim=self.hd, rope=None, positions=bufs.positions, slots=bufs.slots,
+                                       q_out=bufs.q, k_cache=bufs.k_cache[li], v_cache=bufs.v_cache[li], ln_c=c)
             att = ops.decode_attention(q, ops.KVLayout.paged(bufs.k_cache[li], bufs.v_cache[li], bufs.block_table),
                                        bufs.ctx_lens, bufs.seq_ids, n_q_heads=self.H, n_kv_heads=self.H,
                                        head_dim=self.hd, scale=self.hd ** -0.5, max_ctx=bufs.max_ctx,
                                        out=bufs.att[:M], part_o=bufs.part_o, part_ml=bufs.part_ml,
                                        counters=bufs.attn_cnt)
-            ops.linear(att, L.o, L.o_b, out=x, residual=x)
-            w, b, c = L.f_xq  # encoder_attn_layer_norm folded in
-            xq = ops.linear(x, w, b, out=bufs.q[:M], eps=eps, ln_c=c)
+            if chain:
+                ops.ext().chain_run(mid[0], mid[1], mid[2], x, 0, 2)
+                xq = bufs.q[:M]
+            else:
+                ops.linear(att, L.o, L.o_b, out=x, residual=x)
+                w, b, c = L.f_xq  # encoder_attn_layer_norm folded in
+                xq = ops.linear(x, w, b, out=bufs.q[:M], eps=eps, ln_c=c)
             ck, cv = bufs.cross[li]
             att = ops.decode_attention(xq, ops.KVLayout.contiguous(ck, cv, bufs.cross_table), bufs.cross_lens,
                                        bufs.seq_ids, n_q_heads=self.H, n_kv_heads=self.H, head_dim=self.hd,
                                        scale=self.hd ** -0.5, max_ctx=ck.shape[1], out=bufs.att[:M],
                                        part_o=bufs.part_o, part_ml=bufs.part_ml,
                                        counters=bufs.attn_cnt)
+            if chain:
+                ops.ext().chain_run(tail[0], tail[1], tail[2], x, 0, 1)
+                qkv_done = tail[1] == 4
+                continue
+            qkv_done = False
             ops.linear(att, L.xo, L.xo_b, out=x, residual=x)
             w, b, c = L.f_fc1  # final_layer_norm folded in
             f = ops.linear(x, w, b, act="gelu", out=bufs.f[:M], eps=eps, ln_c=c)

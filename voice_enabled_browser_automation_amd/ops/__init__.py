@@ -443,6 +443,24 @@ def split_counters(device, n: int) -> torch.Tensor:
     return t
 
 
+def chain_buffers(device):
+    """(barrier words, bar_mode, work) for one model's chained decode launches
+    (skinny_stream.hip chain_kernel): barrier words in L2-uncached memory polled with scalar
+    loads (bar_mode 2: the poll does not queue behind the next phase's weight loads), plain
+    memory + vector polls (bar_mode 1) if the uncached allocation is unavailable; work = split-tile
+    tickets + partial slots.  One set per model: launches sharing a set must be stream-ordered."""
+    try:
+        bar, mode = ext().alloc_uncached_i32(512, torch.empty(1, device=device)), 2
+    except RuntimeError:
+        bar, mode = torch.zeros(512, dtype=torch.int32, device=device), 1
+    return bar, mode, torch.zeros(1 << 20, dtype=torch.int32, device=device)
+
+
+def chain_error_word(bar: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    """The device word a timed-out chain barrier sets (skinny_stream.hip chain_wait)."""
+    return None if bar is None else bar.view(torch.int64)[160:161]
+
+
 def decode_n_splits(max_ctx: int) -> int:
     return max(1, -(-int(max_ctx) // decode_split_tokens()))
 

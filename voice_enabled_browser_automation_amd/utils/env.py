@@ -69,6 +69,8 @@ class Settings(BaseModel):
     VWA_DTYPE: str = "bf16"
     VWA_MAX_SESSIONS: int = 8
     VWA_HIPGRAPH: bool = True
+    VWA_CHAIN: bool = True  # chained Llama decode layer tail (skinny_stream.hip chain_kernel SEQ 0)
+    VWA_CHAIN_ASR: bool = False  # chained Whisper decoder launches (SEQ 1 / 2; measured no gain)
     VWA_KV_GB: float = 0.0
     VWA_DEBOUNCE_MS: float = 1000.0
     VWA_BUDGET_CHARS: int = 512
