@@ -198,6 +198,12 @@ void skinny_gemm_qkv(Tensor x, Tensor w_qkv, c10::optional<Tensor> bias, bool fu
   check_rc(run_skinny_checked(4, p, cur_stream(x)), "skinny_gemm_qkv");
 }
 
+// VWA_CHAIN_PRE2=0|1: weight items issued ahead of each chain barrier (ChainParams::pre2)
+int chain_pre2() {
+  const char* e = std::getenv("VWA_CHAIN_PRE2");
+  return e ? (std::atoi(e) != 0) : 1;
+}
+
 // ---- chained decode layer tail (skinny_stream.hip, vwa_chain_*): descriptor built once on the
 // host and copied to a device tensor (graph replays then only launch); M <= 4, bf16, one GPU.
 void set_resid(SkinnyParams& p, const Tensor& h) {
@@ -250,6 +256,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   set_resid(cp.ph[2].p, h);
   cp.n = 3;
   cp.seq = 0;
+  cp.pre2 = chain_pre2();
   if (w_qkv.has_value()) {
     TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
                     v_cache.has_value(),
@@ -340,6 +347,7 @@ std::tuple<Tensor, int64_t> chain_make_seq(int64_t seq, std::vector<Tensor> X, s
   }
   cp.n = (int)n;
   cp.seq = (int)seq;
+  cp.pre2 = chain_pre2();
   cp.bar = reinterpret_cast<unsigned*>(bar.data_ptr<int>());
   cp.bar_mode = (int)bar_mode;
   cp.tickets = reinterpret_cast<unsigned*>(work.data_ptr<int>());

@@ -644,10 +644,13 @@ struct PhaseShape {
   static constexpr int U = 4 / NT;
 };
 
+// the phase's first weight item (and with pre2 its second) before the barrier wait: a
+// workgroup that arrives early keeps HBM busy while the grid catches up
 template <int EPI, int KS>
-VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[16]) {
+VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[16], uint4 (&wr2)[16], int pre2) {
   const PhaseRange r = chain_range<KS>(ph);
   chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U>(ph.p, ph.nb, wr, 0, r);
+  if (pre2) chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U>(ph.p, ph.nb, wr2, 1, r);
 }
 
 // partial tile of a split tile: cross-wave sums of this workgroup's units -> slot (sc1)
@@ -673,7 +676,7 @@ VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
 
 // One phase.  X0 holds this phase's item 0 (issued before the barrier wait).
 template <int EPI, int KS>
-VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4 (&X1)[16], char* smem) {
+VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4 (&X1)[16], char* smem, int pre2) {
   constexpr int NT = PhaseShape<EPI>::NT, U = PhaseShape<EPI>::U;
   const ChainPhase& ph = cp.ph[i];
   const SkinnyParams& p = ph.p;
@@ -785,7 +788,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
   // traffic, no epilogue)
   const int n_pad = (r.n_items + 1) & ~1;
   for (int it = 0; it < n_pad; it += 2) {
-    chain_load<NT, U>(p, nb, X1, it + 1, r);
+    if (it > 0 || !pre2) chain_load<NT, U>(p, nb, X1, it + 1, r);
     compute(X0, it);
     finish(it);
     if (it + 2 < n_pad) chain_load<NT, U>(p, nb, X0, it + 2, r);
@@ -835,36 +838,36 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   if constexpr (AG > 0) {
     const bool idle = mq_body<128, AG, KS, true, false>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
                                                         (int)blockIdx.x,
-                                                        [&]() { chain_issue_first<E0, KS>(cp.ph[0], A); });
+                                                        [&]() { chain_issue_first<E0, KS>(cp.ph[0], A, B, 0); });
     stamp();
     gen = chain_arrive(bar, nwg, cp.bar_mode);
-    if (!idle) chain_issue_first<E0, KS>(cp.ph[0], A);
+    if (!idle) chain_issue_first<E0, KS>(cp.ph[0], A, B, 0);
     chain_wait(bar, gen, cp.bar_mode);
   } else {
-    chain_issue_first<E0, KS>(cp.ph[0], A);
+    chain_issue_first<E0, KS>(cp.ph[0], A, B, cp.pre2);
   }
-  chain_phase<E0, KS>(cp, 0, A, B, smem);
+  chain_phase<E0, KS>(cp, 0, A, B, smem, AG > 0 ? 0 : cp.pre2);
   stamp();
   gen = chain_arrive(bar, nwg, cp.bar_mode);
-  chain_issue_first<E1, KS>(cp.ph[1], A);
+  chain_issue_first<E1, KS>(cp.ph[1], A, B, cp.pre2);
   chain_wait(bar, gen, cp.bar_mode);
   stamp();
-  chain_phase<E1, KS>(cp, 1, A, B, smem);
+  chain_phase<E1, KS>(cp, 1, A, B, smem, cp.pre2);
   stamp();
   if constexpr (NPH >= 3) {
     gen = chain_arrive(bar, nwg, cp.bar_mode);
-    chain_issue_first<E2, KS>(cp.ph[2], A);
+    chain_issue_first<E2, KS>(cp.ph[2], A, B, cp.pre2);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E2, KS>(cp, 2, A, B, smem);
+    chain_phase<E2, KS>(cp, 2, A, B, smem, cp.pre2);
     stamp();
   }
   if constexpr (NPH >= 4) {
     gen = chain_arrive(bar, nwg, cp.bar_mode);
-    chain_issue_first<E3, KS>(cp.ph[3], A);
+    chain_issue_first<E3, KS>(cp.ph[3], A, B, cp.pre2);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E3, KS>(cp, 3, A, B, smem);
+    chain_phase<E3, KS>(cp, 3, A, B, smem, cp.pre2);
     stamp();
   }
 }

@@ -66,6 +66,7 @@ struct ChainParams {
   ChainPhase ph[kChainMaxPhases];
   int n;
   int seq;                 // 0 Llama tail, 1 Whisper tail, 2 Whisper middle (skinny_stream.hip chain_kernel)
+  int pre2;                // issue a phase's first two weight items before the barrier wait (else one)
   unsigned* bar;
   int bar_mode;            // 0: flat ticket counter, 1: two-level (8 groups + top), 2: two-level + scalar polls
   float* part;             // split-tile partial slots [max_tiles][2][M][16*nt] f32
