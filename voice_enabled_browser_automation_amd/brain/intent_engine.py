@@ -262,10 +262,18 @@ class LLMIntentEngine:
                 deadline = t3 + 0.05
                 while (hv == _TOK_PENDING).any():
                     if time.perf_counter() > deadline:  # long step (or none in flight): block instead
-                        torch.cuda.current_stream().synchronize()
                         break
-            else:
-                torch.cuda.current_stream().synchronize()
+            # always end on the stream: the spin only sees the copy START landing -- its bytes are
+            # not written atomically per int32 (seen with two processes on one GPU: the low byte
+            # of a token over the sentinel's upper bytes, 0x85858561), so the values are read
+            # only after the copy completed.  Polled with stream queries (a blocking synchronize
+            # measured +38 us per iteration: its wake-up, not the copy)
+            st = torch.cuda.current_stream()
+            if self.spin_wait:
+                while not st.query():
+                    if time.perf_counter() > deadline:
+                        break
+            st.synchronize()
             toks = self.h_tok[:n].tolist()
         else:
             t3 = time.perf_counter()
