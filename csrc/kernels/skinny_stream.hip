@@ -835,18 +835,24 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   stamp();
   constexpr int E0 = SeqEpi<SEQ, 0>::value, E1 = SeqEpi<SEQ, 1>::value, E2 = SeqEpi<SEQ, 2>::value,
                 E3 = SeqEpi<SEQ, 3>::value;
+  int pre0 = cp.pre2;  // phase 0's pre-issued items: two, or one for a workgroup that ran attention
   if constexpr (AG > 0) {
+    // idle workgroups (no attention item) issue their o_proj weights at once; the others after
+    // their item, at the barrier (one item: their attention registers were live until then)
     const bool idle = mq_body<128, AG, KS, true, false>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
                                                         (int)blockIdx.x,
-                                                        [&]() { chain_issue_first<E0, KS>(cp.ph[0], A, B, 0); });
+                                                        [&]() { chain_issue_first<E0, KS>(cp.ph[0], A, B, pre0); });
     stamp();
     gen = chain_arrive(bar, nwg, cp.bar_mode);
-    if (!idle) chain_issue_first<E0, KS>(cp.ph[0], A, B, 0);
+    if (!idle) {
+      pre0 = 0;
+      chain_issue_first<E0, KS>(cp.ph[0], A, B, 0);
+    }
     chain_wait(bar, gen, cp.bar_mode);
   } else {
-    chain_issue_first<E0, KS>(cp.ph[0], A, B, cp.pre2);
+    chain_issue_first<E0, KS>(cp.ph[0], A, B, pre0);
   }
-  chain_phase<E0, KS>(cp, 0, A, B, smem, AG > 0 ? 0 : cp.pre2);
+  chain_phase<E0, KS>(cp, 0, A, B, smem, pre0);
   stamp();
   gen = chain_arrive(bar, nwg, cp.bar_mode);
   chain_issue_first<E1, KS>(cp.ph[1], A, B, cp.pre2);
