@@ -47,8 +47,17 @@ void set_skinny_mode(int64_t mode, int64_t grid_cap, int64_t ks, int64_t w_first
   g_ks = (int)ks;
   g_w_first = (int)w_first;
 }
+// Small weights (<= g_small_bytes, e.g. every Whisper-tiny projection): the one-tile kernel.
+// Measured (tools/bench_kernels.py --only small, M = 1, weights cache-resident as in the ASR
+// decode loop): 2.2 vs 4.3 us for 384-1536 wide projections, 3.3 vs 5.0 us for 1280 x 1280.
+size_t g_small_bytes = 4u << 20;
+void set_small_gemm_bytes(int64_t n) { g_small_bytes = (size_t)(n > 0 ? n : 0); }
+bool small_gemm(const SkinnyParams& p) {
+  return !p.w_scale && g_small_bytes && (size_t)p.N * p.K * 2 <= g_small_bytes && p.M <= 16;
+}
+
 int run_skinny(int epi, const SkinnyParams& p, hipStream_t st) {
-  if (g_skinny_mode == 1) {
+  if (g_skinny_mode == 1 && !small_gemm(p)) {
     const int r = vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
     if (r != -10) return r;
   }
@@ -92,7 +101,7 @@ SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<T
 // fp8 weights run only on the streaming kernel; a shape it cannot take is an error, never a
 // silent bf16 fallback (the Python layer routes those shapes to the dequantising path).
 int run_skinny_checked(int epi, const SkinnyParams& p, hipStream_t st) {
-  if (p.w_scale || p.fuse_rms == 2) return vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
+  if (p.w_scale || (p.fuse_rms == 2 && !small_gemm(p))) return vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
   return run_skinny(epi, p, st);
 }
 
@@ -735,6 +744,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_st") = 0, py::arg("a_ctx") = py::none(), py::arg("a_seq") = py::none(), py::arg("a_scale") = 0.0,
         py::arg("a_n_splits") = 0, py::arg("a_part_o") = py::none(), py::arg("a_part_ml") = py::none(),
         py::arg("a_counters") = py::none());
+  m.def("set_small_gemm_bytes", &set_small_gemm_bytes);
   m.def("chain_make_seq", &chain_make_seq, py::arg("seq"), py::arg("X"), py::arg("W"), py::arg("bias"),
         py::arg("ln_c"), py::arg("Y"), py::arg("epi"), py::arg("eps"), py::arg("n_heads"), py::arg("head_dim"),
         py::arg("positions"), py::arg("slots"), py::arg("k_cache"), py::arg("v_cache"), py::arg("bar"),

@@ -72,6 +72,15 @@ VWA_DEVICE float sumsq8(const uint4& v) {
   return s;
 }
 
+VWA_DEVICE float sum8(const uint4& v) {
+  float f[8];
+  unpack8(v, f);
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += f[j];
+  return s;
+}
+
 template <int EPI, int NT, int MT, int KS>
 __global__ __launch_bounds__(KS * 64) void skinny_gemm_kernel(SkinnyParams p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -88,9 +97,12 @@ __global__ __launch_bounds__(KS * 64) void skinny_gemm_kernel(SkinnyParams p) {
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float ssq[MT];
+  // row statistics of the streamed X: sum of squares (fused RMSNorm, fuse_rms 1) and, for a
+  // LayerNorm folded into W (fuse_rms 2, y = rstd * (acc - mean * ln_c[n]) + bias), the sum
+  const bool ln = p.fuse_rms == 2;
+  float ssq[MT], ssum[MT];
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) ssq[mt] = 0.f;
+  for (int mt = 0; mt < MT; ++mt) ssq[mt] = ssum[mt] = 0.f;
 
   // Main loop: batches of U k-groups whose loads are ALL issued before the first MFMA that
   // consumes them (static indices, no data-dependent load predicates -> hipcc emits counted
@@ -117,7 +129,10 @@ __global__ __launch_bounds__(KS * 64) void skinny_gemm_kernel(SkinnyParams p) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-          for (int s = 0; s < 4; ++s) ssq[mt] += sumsq8(f[u].x[mt][s]);
+          for (int s = 0; s < 4; ++s) {
+            ssq[mt] += sumsq8(f[u].x[mt][s]);
+            if (ln) ssum[mt] += sum8(f[u].x[mt][s]);
+          }
       }
     }
   }
@@ -137,13 +152,17 @@ __global__ __launch_bounds__(KS * 64) void skinny_gemm_kernel(SkinnyParams p) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) ssq[mt] += sumsq8(f.x[mt][s]);
+        for (int s = 0; s < 4; ++s) {
+          ssq[mt] += sumsq8(f.x[mt][s]);
+          if (ln) ssum[mt] += sum8(f.x[mt][s]);
+        }
     }
   }
 
   // ---- cross-wave reduction through LDS: red[w][mt][nt][i][lane]
   float* red = smem;
   float* red_ssq = smem + KS * MT * NT * 4 * 64;  // [w][mt*16 + m]
+  float* red_sum = red_ssq + KS * MT * 16;          // [w][mt*16 + m] (folded LayerNorm)
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -157,6 +176,12 @@ __global__ __launch_bounds__(KS * 64) void skinny_gemm_kernel(SkinnyParams p) {
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
       if (lane < 16) red_ssq[w * MT * 16 + mt * 16 + lane] = v;
+      if (ln) {
+        float t = ssum[mt];
+        t += __shfl_xor(t, 16, 64);
+        t += __shfl_xor(t, 32, 64);
+        if (lane < 16) red_sum[w * MT * 16 + mt * 16 + lane] = t;
+      }
     }
   }
   __syncthreads();
@@ -169,12 +194,27 @@ __global__ __launch_bounds__(KS * 64) void skinny_gemm_kernel(SkinnyParams p) {
     for (int ww = 0; ww < KS; ++ww) s += red[(((ww * MT + mt) * NT + nt) * 4 + i) * 64 + ln];
     return s;
   };
+  auto row_mean = [&](int m) -> float {
+    float s = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < KS; ++ww) s += red_sum[ww * MT * 16 + m];
+    return s / (float)p.K;
+  };
   auto row_scale = [&](int m) -> float {
     if (!p.fuse_rms) return 1.f;
     float s = 0.f;
 #pragma unroll
     for (int ww = 0; ww < KS; ++ww) s += red_ssq[ww * MT * 16 + m];
+    if (ln) {
+      const float mu = row_mean(m);
+      return rsqrtf(fmaxf(s / (float)p.K - mu * mu, 0.f) + p.eps);
+    }
     return rsqrtf(s / (float)p.K + p.eps);
+  };
+  // accumulator of (row m, column n) with the folded LayerNorm's mean term removed
+  auto lin = [&](int m, int nn, int n) -> float {
+    const float v = red_at(m, nn);
+    return ln ? v - row_mean(m) * p.ln_c[n] : v;
   };
 
   const int Mrows = p.M < MT * 16 ? p.M : MT * 16;
@@ -198,8 +238,8 @@ __global__ __launch_bounds__(KS * 64) void skinny_gemm_kernel(SkinnyParams p) {
     for (int o = threadIdx.x; o < Mrows * 16; o += KS * 64) {
       const int m = o >> 4, nl = o & 15;
       const float sc = row_scale(m);
-      float v = red_at(m, nl) * sc;
-      float pv = red_at(m, nl ^ 8) * sc;
+      float v = lin(m, nl, n0 + nl) * sc;
+      float pv = lin(m, nl ^ 8, n0 + (nl ^ 8)) * sc;
       if (p.bias) {
         v += bf2f(p.bias[n0 + nl]);
         pv += bf2f(p.bias[n0 + (nl ^ 8)]);
@@ -230,7 +270,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_gemm_kernel(SkinnyParams p) {
     for (int o = threadIdx.x; o < Mrows * 16 * NT; o += KS * 64) {
       const int m = o / (16 * NT), nn = o % (16 * NT);
       const int n = n0 + nn;
-      float v = red_at(m, nn) * row_scale(m);
+      float v = lin(m, nn, n) * row_scale(m);
       if (p.bias) v += bf2f(p.bias[n]);
       if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
       if constexpr (EPI == EPI_RESID) v += bf2f(p.R[(size_t)m * p.ldr + n]);
@@ -243,7 +283,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_gemm_kernel(SkinnyParams p) {
 template <int EPI, int NT, int MT, int KS>
 void launch_t(const SkinnyParams& p, hipStream_t st) {
   const int ntiles = p.N / (16 * NT);
-  const size_t lds = (size_t)(KS * MT * NT * 4 * 64 + KS * MT * 16) * sizeof(float);
+  const size_t lds = (size_t)(KS * MT * NT * 4 * 64 + 2 * KS * MT * 16) * sizeof(float);
   hipLaunchKernelGGL((skinny_gemm_kernel<EPI, NT, MT, KS>), dim3(ntiles), dim3(KS * 64), lds, st, p);
 }
 
@@ -264,6 +304,7 @@ void launch_mt(const SkinnyParams& p, hipStream_t st) {
 
 extern "C" int vwa_skinny_gemm(int epi, const SkinnyParams* p, hipStream_t st) {
   if (p->M < 1 || p->M > 64 || p->K % 128 != 0) return -1;
+  if (p->fuse_rms == 2 && (epi == EPI_SWIGLU || p->ln_c == nullptr)) return -3;
   switch (epi) {
     case EPI_STORE: if (p->N % 16) return -2; launch_mt<EPI_STORE, 1>(*p, st); break;
     case EPI_RESID: if (p->N % 16) return -2; launch_mt<EPI_RESID, 1>(*p, st); break;

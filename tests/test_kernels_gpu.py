@@ -37,8 +37,10 @@ def close(a, b, atol, rtol=2e-2):
                 ids=["tile", "stream8_xfirst", "stream4", "stream8"])
 def skinny_mode(request):
     ops.ext().set_skinny_mode(*request.param)
+    ops.ext().set_small_gemm_bytes(0)  # every shape on the selected kernel (no small-weight routing)
     yield request.param
     ops.ext().set_skinny_mode(1, 256, 8, 2)
+    ops.ext().set_small_gemm_bytes(4 << 20)
 
 
 @pytest.mark.parametrize("M", [1, 5, 17, 40])
@@ -136,11 +138,21 @@ def test_qkv_rope_write(M, skinny_mode):
     close(vc, vc2, 3e-2)
 
 
+@pytest.mark.parametrize("small_bytes", [0, 4 << 20], ids=["stream", "one_tile"])
 @pytest.mark.parametrize("M", [1, 6, 16, 24])
-def test_folded_layernorm_linear_and_qkv(M):
-    """LayerNorm folded into the streaming GEMM (mean/rstd from the staged rows) vs LayerNorm ->
-    linear in f32; 24 rows take the normalise-then-GEMM path.  Inputs carry a large mean (the
-    residual stream's offset) to exercise the mean * rowsum correction."""
+def test_folded_layernorm_linear_and_qkv(M, small_bytes):
+    """LayerNorm folded into the GEMM (mean/rstd from the streamed / staged rows) vs LayerNorm ->
+    linear in f32, on the persistent streaming kernel and on the one-tile kernel small weights
+    are routed to (skinny_gemm.hip); 24 rows take the normalise-then-GEMM path.  Inputs carry a
+    large mean (the residual stream's offset) to exercise the mean * rowsum correction."""
+    ops.ext().set_small_gemm_bytes(small_bytes)
+    try:
+        _folded_layernorm_case(M)
+    finally:
+        ops.ext().set_small_gemm_bytes(4 << 20)
+
+
+def _folded_layernorm_case(M):
     K, N = 384, 512
     x = (torch.randn(M, K, device=DEV) * 2 + 3).to(BF)
     gamma, beta = rnd(K, scale=0.5) + 1, rnd(K, scale=0.2)

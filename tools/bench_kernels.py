@@ -82,6 +82,25 @@ def main():
                      hipblaslt_tbps=round(gb / (t_blas * 1e-6) / 1e3, 3))
             print(json.dumps(r), flush=True)
             res.append(r)
+    # small decoder GEMMs (Whisper): latency-bound, weights cache-resident across decode tokens;
+    # one-tile kernel (m0) vs the persistent streaming kernel at several grid caps / wave splits
+    small = [("tiny_qkv", 1152, 384), ("tiny_o", 384, 384), ("tiny_fc1", 1536, 384), ("tiny_fc2", 384, 1536),
+             ("lv3_qkv", 3840, 1280), ("lv3_o", 1280, 1280), ("lv3_fc1", 5120, 1280), ("lv3_fc2", 1280, 5120)]
+    for name, N, K in (small if "small" in only else ()):
+        x = torch.randn(1, K, device=dev).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+        y = torch.empty(1, N, device=dev, dtype=torch.bfloat16)
+        variants = {}
+        ops.ext().set_small_gemm_bytes(0)  # measure each kernel as selected, not the size routing
+        for mode, cap, ks in ((0, 256, 8), (1, 256, 8), (1, 128, 8), (1, 64, 8), (1, 32, 8), (1, 64, 4), (1, 32, 4)):
+            ops.ext().set_skinny_mode(mode, cap, ks)
+            variants[f"m{mode}_g{cap}_k{ks}"] = round(timeit(lambda: ops.ext().skinny_gemm(x, w, None, y, 0, False,
+                                                                                             1e-5, None)), 2)
+        ops.ext().set_skinny_mode(1, 256, 8)
+        ops.ext().set_small_gemm_bytes(4 << 20)
+        r = dict(kernel="skinny_small", shape=name, M=1, N=N, K=K, variants=variants)
+        print(json.dumps(r), flush=True)
+        res.append(r)
     # launch floor: the smallest kernels in the decode graph (graph-replayed like everything here)
     if "floor" in only:
         ids = torch.zeros(1, dtype=torch.int32, device=dev)
