@@ -52,8 +52,10 @@ void set_skinny_mode(int64_t mode, int64_t grid_cap, int64_t ks, int64_t w_first
 // decode loop): 2.2 vs 4.3 us for 384-1536 wide projections, 3.3 vs 5.0 us for 1280 x 1280.
 size_t g_small_bytes = 4u << 20;
 void set_small_gemm_bytes(int64_t n) { g_small_bytes = (size_t)(n > 0 ? n : 0); }
+// Also every K < 1024: the streaming kernel splits K over its 8 waves in 128-wide groups, so
+// with fewer than 8 groups most of its waves idle (Whisper-tiny's 40 MB LM head, K = 384).
 bool small_gemm(const SkinnyParams& p) {
-  return !p.w_scale && g_small_bytes && (size_t)p.N * p.K * 2 <= g_small_bytes && p.M <= 16;
+  return !p.w_scale && g_small_bytes && p.M <= 16 && ((size_t)p.N * p.K * 2 <= g_small_bytes || p.K < 1024);
 }
 
 int run_skinny(int epi, const SkinnyParams& p, hipStream_t st) {

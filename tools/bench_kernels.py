@@ -85,7 +85,7 @@ def main():
     # small decoder GEMMs (Whisper): latency-bound, weights cache-resident across decode tokens;
     # one-tile kernel (m0) vs the persistent streaming kernel at several grid caps / wave splits
     small = [("tiny_qkv", 1152, 384), ("tiny_o", 384, 384), ("tiny_fc1", 1536, 384), ("tiny_fc2", 384, 1536),
-             ("lv3_qkv", 3840, 1280), ("lv3_o", 1280, 1280), ("lv3_fc1", 5120, 1280), ("lv3_fc2", 1280, 5120)]
+             ("tiny_lm", 51872, 384), ("lv3_qkv", 3840, 1280), ("lv3_o", 1280, 1280), ("lv3_fc1", 5120, 1280), ("lv3_fc2", 1280, 5120)]
     for name, N, K in (small if "small" in only else ()):
         x = torch.randn(1, K, device=dev).to(torch.bfloat16)
         w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
