@@ -154,7 +154,9 @@ def test_chained_layer_tail_matches_per_kernel_path(cfg, monkeypatch):
         monkeypatch.setenv("VWA_CHAIN_ATTN", "1")
         model._chains = {}
         got_a = run(True)
-        monkeypatch.delenv("VWA_CHAIN_ATTN")
+        monkeypatch.setenv("VWA_CHAIN_ATTN", "0")  # and the separate attention launch
+        model._chains = {}
+        got = run(True)
         for a, b in zip(got_a, ref):
             err = (a - b).abs().max().item()
             assert err < 0.02 * (1 + b.abs().max().item()), err

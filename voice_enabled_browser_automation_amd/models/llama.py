@@ -181,9 +181,10 @@ class LlamaModel:
         L = self.layers[li]
         nxt = li + 1 < len(self.layers)
         N = self.layers[li + 1] if nxt else None
-        # optionally the layer's decode attention as the launch's first phase (VWA_CHAIN_ATTN=1;
-        # measured equal to the separate attention launch, skinny_stream.hip chain_kernel)
-        attn = (self.hd == 128 and self.nq // self.nkv in (4, 8) and ops.env_flag("VWA_CHAIN_ATTN", False)
+        # the layer's decode attention as the launch's first phase (VWA_CHAIN_ATTN, default on;
+        # same-box bench A/B/A: GPU time per decode step 3868 vs 3897 / 3907 us, p50 276 vs 284 /
+        # 285 ms, profiles/r1_bench_results.jsonl; skinny_stream.hip chain_kernel)
+        attn = (self.hd == 128 and self.nq // self.nkv in (4, 8) and ops.env_flag("VWA_CHAIN_ATTN", True)
                 and ops.decode_n_splits(bufs.max_ctx) > 1)
         a = {}
         if attn:
