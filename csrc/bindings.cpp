@@ -107,12 +107,13 @@ int run_skinny_checked(int epi, const SkinnyParams& p, hipStream_t st) {
   return run_skinny(epi, p, st);
 }
 
-// Folded LayerNorm (fuse_rms = 2): streaming kernel only, bf16 weights, <= 16 rows.
+// Folded LayerNorm (fuse_rms = 2): bf16 weights, <= 16 rows; runs on the streaming kernel, or on
+// the one-tile kernel for the small GEMMs it takes (run_skinny_checked: small_gemm).
 void set_ln_fold(SkinnyParams& p, const c10::optional<Tensor>& ln_c, int epi) {
   if (!ln_c.has_value()) return;
   TORCH_CHECK(p.w_scale == nullptr, "folded LayerNorm needs bf16 weights");
   TORCH_CHECK(epi != 2, "folded LayerNorm is not supported with the SwiGLU epilogue");
-  TORCH_CHECK(p.M <= 16, "folded LayerNorm runs on the streaming kernel (<= 16 rows)");
+  TORCH_CHECK(p.M <= 16, "folded LayerNorm takes <= 16 rows");
   TORCH_CHECK(ln_c->is_cuda() && ln_c->scalar_type() == at::kFloat && ln_c->is_contiguous() && ln_c->numel() == p.N,
               "ln_c must be f32 [N]");
   p.fuse_rms = 2;
@@ -610,7 +611,7 @@ void embedding(Tensor ids, Tensor table, c10::optional<Tensor> pos_table, c10::o
 }
 
 void sample(Tensor logits, c10::optional<Tensor> mask, c10::optional<Tensor> temperature, Tensor seed, Tensor step,
-            Tensor out_tokens, Tensor part_val, Tensor part_idx) {
+            Tensor out_tokens, Tensor part_val, Tensor part_idx, c10::optional<Tensor> fail_word) {
   c10::DeviceGuard g(logits.device());
   TORCH_CHECK(logits.scalar_type() == at::kFloat && logits.dim() == 2 && logits.stride(1) == 1, "logits f32 2-D");
   const int rows = (int)logits.size(0), V = (int)logits.size(1);
@@ -627,12 +628,15 @@ void sample(Tensor logits, c10::optional<Tensor> mask, c10::optional<Tensor> tem
   TORCH_CHECK(out_tokens.scalar_type() == at::kInt && out_tokens.numel() >= rows, "out_tokens");
   const int n_chunks = (int)(part_val.numel() / rows);
   TORCH_CHECK(n_chunks >= 1 && part_idx.numel() >= (int64_t)rows * n_chunks, "partials");
+  if (fail_word.has_value())
+    TORCH_CHECK(fail_word->scalar_type() == at::kLong && fail_word->numel() >= 1 && fail_word->is_cuda(),
+                "fail_word: one device int64");
   check_rc(vwa_sample(logits.data_ptr<float>(), (int)logits.stride(0), rows, V,
                       mask.has_value() ? reinterpret_cast<const uint32_t*>(mask->data_ptr<int>()) : nullptr,
                       mask_words, temperature.has_value() ? temperature->data_ptr<float>() : nullptr,
                       reinterpret_cast<const uint64_t*>(seed.data_ptr<int64_t>()), step.data_ptr<int>(),
                       out_tokens.data_ptr<int>(), part_val.data_ptr<float>(), part_idx.data_ptr<int>(), n_chunks,
-                      cur_stream(logits)),
+                      fail_word.has_value() ? fail_word->data_ptr<int64_t>() : nullptr, cur_stream(logits)),
            "sample");
 }
 

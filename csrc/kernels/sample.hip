@@ -82,7 +82,8 @@ __global__ __launch_bounds__(256) void sample_partial_kernel(const float* __rest
 
 __global__ __launch_bounds__(256) void sample_final_kernel(const float* __restrict__ part_val,
                                                            const int* __restrict__ part_idx, int n_chunks,
-                                                           int* out_tokens, int* step, int rows) {
+                                                           int* out_tokens, int* step, int rows,
+                                                           const int64_t* __restrict__ fail_word) {
   __shared__ float sv[256];
   __shared__ int si[256];
   const int row = blockIdx.x;
@@ -103,8 +104,11 @@ __global__ __launch_bounds__(256) void sample_final_kernel(const float* __restri
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    // no admissible token (empty mask) -> -1, the host treats it as a grammar error
-    out_tokens[row] = (sv[0] == -INFINITY) ? -1 : si[0];
+    // no admissible token (empty mask) -> -1, the host treats it as a grammar error; a set
+    // fail word (the forward's chained launch timed out at a grid barrier, so these logits are
+    // invalid) -> -2 in every row: the host re-runs the step on the per-kernel path
+    const bool failed = fail_word != nullptr && fail_word[0] != 0;
+    out_tokens[row] = failed ? -2 : (sv[0] == -INFINITY) ? -1 : si[0];
     if (row == rows - 1) step[0] += 1;
   }
 }
@@ -113,11 +117,11 @@ __global__ __launch_bounds__(256) void sample_final_kernel(const float* __restri
 
 extern "C" int vwa_sample(const float* logits, int ld, int rows, int V, const uint32_t* mask, int mask_words,
                           const float* temperature, const uint64_t* seed, const int* step, int* out_tokens,
-                          float* part_val, int* part_idx, int n_chunks, hipStream_t st) {
+                          float* part_val, int* part_idx, int n_chunks, const int64_t* fail_word, hipStream_t st) {
   if (n_chunks < 1 || n_chunks > 1024) return -1;
   hipLaunchKernelGGL(sample_partial_kernel, dim3(rows, n_chunks), dim3(256), 0, st, logits, ld, V, mask, mask_words,
                      temperature, seed, step, part_val, part_idx, n_chunks);
   hipLaunchKernelGGL(sample_final_kernel, dim3(rows), dim3(256), 0, st, part_val, part_idx, n_chunks, out_tokens,
-                     const_cast<int*>(step), rows);
+                     const_cast<int*>(step), rows, fail_word);
   return (int)hipGetLastError();
 }

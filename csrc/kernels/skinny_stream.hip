@@ -805,11 +805,10 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
 // epilogues.)  AG > 0 (Llama only): the layer's decode attention (GQA group AG, head_dim 128)
 // runs first, as phase 0 of the same launch (mq_attention.h with 8 waves, one register set,
 // outputs written through to memory); workgroups without an attention item issue their o_proj
-// weights at once.  Measured (tools/chain_probe.py --attn, 1 row, ctx 1100): 111.6 us vs
-// 111-112 us for the standalone attention kernel + the GEMM chain -- the attention phase itself
-// is slower in the 8-wave form (13-14 us vs 10.5 us) and o_proj still needs X staging +
-// reduction after the barrier, so the model keeps the separate attention launch
-// (VWA_CHAIN_ATTN=1 selects this form).
+// weights at once.  The attention phase itself is slower in the 8-wave form (13-14 us vs 10.5 us
+// standalone, tools/chain_probe.py --attn), but the whole decode step gains one launch boundary
+// per layer: a same-box bench A/B/A measured 3868 vs 3897 / 3907 us of GPU time per decode step,
+// so this form is the model's default (VWA_CHAIN_ATTN=0 selects the separate attention launch).
 template <int SEQ, int I>
 struct SeqEpi {
   static constexpr int value = SEQ == 0 ? (I == 0 ? EPI_RESID : I == 1 ? EPI_SWIGLU : I == 2 ? EPI_RESID : EPI_QKV)

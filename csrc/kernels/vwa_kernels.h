@@ -117,7 +117,7 @@ int vwa_embedding(const int* ids, const uint16_t* table, const uint16_t* pos_tab
                   uint16_t* out, int rows, int D, int vocab_start, int vocab_end, hipStream_t st);
 int vwa_sample(const float* logits, int ld, int rows, int V, const uint32_t* mask, int mask_words,
                const float* temperature, const uint64_t* seed, const int* step, int* out_tokens,
-               float* part_val, int* part_idx, int n_chunks, hipStream_t st);
+               float* part_val, int* part_idx, int n_chunks, const int64_t* fail_word, hipStream_t st);
 int vwa_pcm16_to_f32(const int16_t* pcm, float* out, int n_in, int n_out, float ratio, hipStream_t st);
 int vwa_log_mel(const float* audio, int n_samples, int n_frames, const float* window, const float* dft_cos,
                 const float* dft_sin, const float* mel_fb, int n_mels, float* mel_out, float* max_buf,

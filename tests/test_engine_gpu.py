@@ -135,9 +135,12 @@ def test_chained_layer_tail_matches_per_kernel_path(cfg, monkeypatch):
     toks = torch.randint(0, cfg.vocab_size, (40,)).tolist()
     model = LlamaModel(cfg, device="cuda", seed=2)
 
+    engines = []  # kept alive: the chain descriptor cache is weakly keyed on each engine's buffers
+
     def run(chain: bool):
         monkeypatch.setenv("VWA_CHAIN", "1" if chain else "0")
         e = LLMEngine(model, max_seqs=2, max_model_len=256, kv_blocks=20, block_size=16)
+        engines.append(e)
         s = e.new_sequence(toks[:30], use_prefix_cache=False)
         e.prefill(s)
         out, i = [], 30
@@ -152,15 +155,15 @@ def test_chained_layer_tail_matches_per_kernel_path(cfg, monkeypatch):
     assert not model.chain_error()
     if cfg.head_dim == 128:  # decode attention as the chained launch's first phase
         monkeypatch.setenv("VWA_CHAIN_ATTN", "1")
-        model._chains = {}
+        model.reset_chains()
         got_a = run(True)
         monkeypatch.setenv("VWA_CHAIN_ATTN", "0")  # and the separate attention launch
-        model._chains = {}
+        model.reset_chains()
         got = run(True)
         for a, b in zip(got_a, ref):
             err = (a - b).abs().max().item()
             assert err < 0.02 * (1 + b.abs().max().item()), err
-    assert model._chains and all(v is not None for v in model._chains.values())
+    assert model.chain_descs() and all(v is not None for v in model.chain_descs())
     for a, b in zip(got, ref):
         err = (a - b).abs().max().item()
         assert err < 0.02 * (1 + b.abs().max().item()), err
@@ -175,7 +178,7 @@ def test_chain_timeout_falls_back_to_per_kernel_launches():
     s = e.new_sequence(list(range(10)), use_prefix_cache=False)
     e.prefill(s)
     a = e.run_rows([(s, 11)]).float().cpu()
-    assert model._chains and not model.chain_error()
+    assert model.chain_descs() and not model.chain_error()
     model._chain_bar.view(torch.int64)[160] = 1  # what a timed-out spin writes
     e._check_chain()  # non-blocking: queues the copy of the error word ...
     torch.cuda.synchronize()
@@ -183,6 +186,43 @@ def test_chain_timeout_falls_back_to_per_kernel_launches():
     assert e.stats.get("chain_fallbacks") == 1 and not e.graphs and not model._chain_ok(1)
     b = e.run_rows([(s, 12)]).float().cpu()
     assert torch.isfinite(a).all() and torch.isfinite(b).all()
+
+
+def test_failed_chained_step_is_rerun_on_per_kernel_path(monkeypatch):
+    """A chained step whose barrier timed out is never served: the sampler's fail word turns its
+    tokens into -2 and recover_step() re-runs the same rows on the per-kernel path (same logits
+    as an engine that never chained, sequence state rolled back and re-advanced)."""
+    ops.ext()
+    model = LlamaModel(CFG, device="cuda", seed=4)
+    toks = list(range(10, 24))
+
+    def engine():
+        e = LLMEngine(model, max_seqs=1, max_model_len=128, kv_blocks=10, block_size=16)
+        s = e.new_sequence(toks[:10], use_prefix_cache=False)
+        e.prefill(s)
+        return e, s
+
+    monkeypatch.setenv("VWA_CHAIN", "0")
+    e0, s0 = engine()
+    ref = [e0.run_rows([(s0, t)]).float().cpu() for t in toks[10:13]]
+    monkeypatch.setenv("VWA_CHAIN", "1")
+    e, s = engine()
+    a = e.run_rows([(s, toks[10])]).float().cpu()  # chained + verified (check=True)
+    logits = e.run_rows([(s, toks[11])], check=False)
+    word = e.step_fail_word()
+    assert word is not None and model.chain_descs()
+    word.fill_(1)  # what a timed-out barrier spin writes, after the forward in stream order
+    out = torch.zeros(4, dtype=torch.int32, device="cuda")
+    ops.sample(logits, mask=None, temperature=None, seed=torch.zeros(1, dtype=torch.int64, device="cuda"),
+               step=torch.zeros(1, dtype=torch.int32, device="cuda"), out_tokens=out, fail_word=word)
+    assert out[:1].tolist() == [-2]
+    b = e.recover_step().float().cpu()
+    assert e.stats["chain_fallbacks"] == 1 and not model._chain_ok(1) and not model.chain_error()
+    assert s.n_computed == 12
+    c = e.run_rows([(s, toks[12])]).float().cpu()
+    for got, want in zip((a, b, c), ref):
+        err = (got - want).abs().max().item()
+        assert err < 0.02 * (1 + want.abs().max().item()), err
 
 
 def test_asr_device_decode_loop_matches_host_loop():
@@ -246,9 +286,12 @@ def test_whisper_chained_decoder_matches_per_kernel_path(name, monkeypatch):
     torch.manual_seed(1)
     enc = torch.randn(1, cfg.n_audio_ctx, cfg.d_model, device="cuda").to(torch.bfloat16)
 
+    runners = []  # kept alive: the chain descriptor cache is weakly keyed on each runner's buffers
+
     def run(chain: bool):
         monkeypatch.setenv("VWA_CHAIN_ASR", "1" if chain else "0")
         r = WhisperRunner(m, max_sessions=2, use_graphs=False)
+        runners.append(r)
         r.set_cross(0, enc)
         r.set_cross(1, enc)
         out, pos = [], 0
@@ -261,7 +304,7 @@ def test_whisper_chained_decoder_matches_per_kernel_path(name, monkeypatch):
     ref = run(False)
     got = run(True)
     assert not m.chain_error()
-    assert m._chains and all(a is not None and b is not None for a, b in m._chains.values())
+    assert m.chain_descs() and all(a is not None and b is not None for a, b in m.chain_descs())
     for a, b in zip(got, ref):
         err = (a - b).abs().max().item()
         assert err < 0.03 * (1 + b.abs().max().item()), err

@@ -173,3 +173,33 @@ def test_tensor_parallel_gloo_matches_single():
         assert p.exitcode == 0
     assert got.shape == ref.shape
     assert torch.allclose(got, ref, atol=3e-2, rtol=3e-2), (got - ref).abs().max()
+
+
+def test_long_forced_feed_is_consumed_in_pieces():
+    """A jump-forward feed longer than the engine's row cap is run in pieces: every piece reaches
+    the KV cache (greedy answers equal the ones of an engine whose row cap takes the feed whole)."""
+    m = LlamaModel(LLAMA_PRESETS["llama-tiny"], device="cpu", seed=1)
+    outs, stats, rows = [], [], []
+    for max_rows in (64, 4):
+        eng = LLMEngine(m, max_seqs=2, max_model_len=2048, kv_blocks=400, max_rows=max_rows)
+        ie = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=160, temperature=0.0)
+        outs.append(ie.parse({"text": "search wireless earbuds", "context": {}}))
+        stats.append(dict(ie.batch_stats))
+        rows.append(eng.stats["rows"])
+    assert safe_parse(ParseResponse, outs[1]).success
+    assert stats[1]["iterations"] > stats[0]["iterations"]  # the capped engine split some feeds
+    assert rows[0] == rows[1]  # ... and still ran every fed token through the model
+    assert outs[0] == outs[1]
+
+
+def test_sampler_fail_word_marks_every_row():
+    from voice_enabled_browser_automation_amd import ops
+
+    logits = torch.randn(3, 64)
+    out = torch.zeros(3, dtype=torch.int32)
+    kw = dict(mask=None, temperature=None, seed=torch.tensor([0]), step=torch.zeros(1, dtype=torch.int32),
+              out_tokens=out)
+    ops.sample(logits, fail_word=torch.zeros(1, dtype=torch.int64), **kw)
+    assert out.tolist() == logits.argmax(-1).tolist()
+    ops.sample(logits, fail_word=torch.ones(1, dtype=torch.int64), **kw)
+    assert out.tolist() == [-2, -2, -2]

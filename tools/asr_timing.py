@@ -31,7 +31,7 @@ def main():
     texts = {}
     for chain in ("0", "1"):
         os.environ["VWA_CHAIN_ASR"] = chain
-        m._chains = {}
+        m.reset_chains()
         eng = AsrEngine(m, load_tokenizer("whisper"), max_sessions=2)
         audio = eng.pcm_to_audio(synth_speech(10.0, seed=100))
         for _ in range(2):
@@ -48,7 +48,7 @@ def main():
                               encode_ms=round(statistics.median(enc), 2), decode_ms=round(statistics.median(dec), 2),
                               total_ms=round(statistics.median(tot), 2),
                               decode_us_per_token=round(1e3 * statistics.median(dec) / a.tokens, 1),
-                              chained=bool(m._chains))), flush=True)
+                              chained=bool(m.chain_descs()))), flush=True)
     print(json.dumps(dict(tool="asr_timing", same_text=texts["0"] == texts["1"])), flush=True)
 
 

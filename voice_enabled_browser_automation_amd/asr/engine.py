@@ -21,6 +21,17 @@ from ..models.whisper import WhisperModel
 BUCKETS = (1, 2, 4, 8, 16, 32, 64)
 
 
+
+class RunnerBuffers(SimpleNamespace):
+    """The decoder step's fixed-address buffers.  Hashable by identity and weak-referenceable:
+    the model's chained-launch descriptors (raw pointers into these buffers) are cached per
+    buffers object in a WeakKeyDictionary (models/whisper.py _chain_descs)."""
+
+    __hash__ = object.__hash__
+
+    def __eq__(self, other):
+        return self is other
+
 class WhisperRunner:
     def __init__(self, model: WhisperModel, *, max_sessions: int = 4, block_size: int = 16,
                  use_graphs: Optional[bool] = None):
@@ -35,7 +46,7 @@ class WhisperRunner:
         H, hd, d = model.H, model.hd, cfg.d_model
         R = max(BUCKETS)
         i32 = dict(dtype=torch.int32, device=dev)
-        b = SimpleNamespace()
+        b = RunnerBuffers()
         b.tokens = torch.zeros(R, **i32)
         b.positions = torch.zeros(R, **i32)
         b.seq_ids = torch.zeros(R, **i32)

@@ -236,7 +236,12 @@ class LLMIntentEngine:
             return finished
         tm = self.timing
         t0 = time.perf_counter()
-        logits = self.engine.run_rows(rows, logits_for=last) if last else None
+        if last:
+            logits = self.engine.run_rows(rows, logits_for=last, check=False)
+        else:
+            # only part of one long feed fits this iteration: its rows still have to reach the KV
+            # cache (nothing is sampled, so the step is verified synchronously)
+            self.engine.run_rows(rows, logits_for=[len(rows) - 1], check=True)
         t1 = time.perf_counter()
         tm["build_launch_ms"] += (t1 - t0) * 1e3
         self.batch_stats["iterations"] += 1
@@ -249,9 +254,28 @@ class LLMIntentEngine:
             r.matcher.fill_mask(self.h_mask_np[i])
         t2 = time.perf_counter()
         self.d_mask[:n].copy_(self.h_mask[:n], non_blocking=True)
+        toks = self._sample(logits, n, self.engine.step_fail_word())
+        if any(t == -2 for t in toks):
+            # the forward's chained launch timed out at a grid barrier (tokens -2 from the
+            # sampler's fail word): re-run the step on the per-kernel path and sample again
+            logits = self.engine.recover_step()
+            toks = self._sample(logits, n, None)
+        t4 = time.perf_counter()
+        tm["mask_ms"] += (t2 - t1) * 1e3
+        tm["sample_launch_ms"] += (self._t3 - t2) * 1e3
+        tm["gpu_wait_ms"] += (t4 - self._t3) * 1e3
+        self.batch_stats["sampled"] += n
+        self._accept(batch, toks, finished)
+        if finished:
+            self.active = [r for r in self.active if not r.done]
+        tm["post_ms"] += (time.perf_counter() - t4) * 1e3
+        return finished
+
+    def _sample(self, logits: torch.Tensor, n: int, fail_word: Optional[torch.Tensor]) -> List[int]:
+        """Masked sampling of the n logits rows (masks already in d_mask) and the token readback."""
         ops.sample(logits, mask=self.d_mask, temperature=self.d_temp if self.temperature > 0 else None,
                    seed=self.d_seed, step=self.d_step, out_tokens=self.d_tok, part_val=self.part_val[: n * 64],
-                   part_idx=self.part_idx[: n * 64])
+                   part_idx=self.part_idx[: n * 64], fail_word=fail_word)
         if self.dev.type == "cuda":
             if self.spin_wait:
                 self.h_tok_np[:n] = _TOK_PENDING
@@ -278,11 +302,10 @@ class LLMIntentEngine:
         else:
             t3 = time.perf_counter()
             toks = self.d_tok[:n].tolist()
-        t4 = time.perf_counter()
-        tm["mask_ms"] += (t2 - t1) * 1e3
-        tm["sample_launch_ms"] += (t3 - t2) * 1e3
-        tm["gpu_wait_ms"] += (t4 - t3) * 1e3
-        self.batch_stats["sampled"] += n
+        self._t3 = t3
+        return toks
+
+    def _accept(self, batch: List[IntentRequest], toks: List[int], finished: List[IntentRequest]) -> None:
         for r, tok in zip(batch, toks):
             r.steps += 1
             m = r.matcher
@@ -301,10 +324,6 @@ class LLMIntentEngine:
                     self._jump_forward(r)
             if r.done:
                 finished.append(r)
-        if finished:
-            self.active = [r for r in self.active if not r.done]
-        tm["post_ms"] += (time.perf_counter() - t4) * 1e3
-        return finished
 
     def engine_stats(self) -> Dict[str, Any]:
         """Scheduler + KV-cache state for /metrics (batch size, KV utilisation, grammar cache)."""

@@ -18,6 +18,7 @@ deterministic generator and sliced, so a TP model is numerically the same model 
 """
 from __future__ import annotations
 
+import weakref
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -167,13 +168,28 @@ class LlamaModel:
 
     def disable_chain(self) -> None:
         self._chain_disabled = True
-        self._chains = {}
+        self.reset_chains()
+
+    def reset_chains(self) -> None:
+        """Drop every cached chain descriptor (they embed raw device pointers of the buffers)."""
+        self._chains = weakref.WeakKeyDictionary()
+
+    def chain_descs(self):
+        """Every cached descriptor entry over all live engines' buffers (tests / diagnostics)."""
+        return [v for d in getattr(self, "_chains", {}).values() for v in d.values()]
 
     def _chain_desc(self, bufs, kv, M: int, li: int):
         """(descriptor, n_phases, lds) of layer li's chained tail for this engine's buffers,
-        built on first use (an eager warm-up call precedes every graph capture)."""
-        cache = self.__dict__.setdefault("_chains", {})
-        key = (id(bufs), id(kv), M, li)
+        built on first use (an eager warm-up call precedes every graph capture).
+
+        The descriptors hold raw device pointers into ``bufs`` and ``kv``, so the cache lives in
+        a WeakKeyDictionary keyed on the StepBuffers object itself (an entry dies with its
+        engine's buffers; a new engine can never see a stale one through a reused ``id()``) and
+        the inner key carries the KV pointers and the context bound it was built for."""
+        if not isinstance(getattr(self, "_chains", None), weakref.WeakKeyDictionary):
+            self.reset_chains()
+        cache = self._chains.setdefault(bufs, {})
+        key = (M, li, kv.k[li].data_ptr(), kv.v[li].data_ptr(), bufs.max_ctx)
         if key in cache:
             return cache[key]
         if getattr(self, "_chain_bar", None) is None:

@@ -15,6 +15,7 @@ Decoder (per token, hipGraph-captured per batch bucket):
 from __future__ import annotations
 
 import math
+import weakref
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -241,7 +242,14 @@ class WhisperModel:
 
     def disable_chain(self) -> None:
         self._chain_disabled = True
-        self._chains = {}
+        self.reset_chains()
+
+    def reset_chains(self) -> None:
+        """Drop every cached chain descriptor (they embed raw device pointers of the buffers)."""
+        self._chains = weakref.WeakKeyDictionary()
+
+    def chain_descs(self):
+        return [v for d in getattr(self, "_chains", {}).values() for v in d.values()]
 
     def chain_error_word(self):
         return ops.chain_error_word(getattr(self, "_chain_bar", None))
@@ -255,8 +263,11 @@ class WhisperModel:
         middle = self-attn out-proj + residual -> LN cross-attn query (store to bufs.q);
         tail = cross-attn out-proj + residual -> LN fc1 + GELU -> fc2 + residual [-> next layer's
         LN self-attn QKV + self-KV write].  Each entry (descriptor, n_phases, lds) or None."""
-        cache = self.__dict__.setdefault("_chains", {})
-        key = (id(bufs), M, li)
+        # keyed on the buffers object itself (weakly): the descriptors embed its raw pointers
+        if not isinstance(getattr(self, "_chains", None), weakref.WeakKeyDictionary):
+            self.reset_chains()
+        cache = self._chains.setdefault(bufs, {})
+        key = (M, li)
         if key in cache:
             return cache[key]
         if getattr(self, "_chain_bar", None) is None:

@@ -505,14 +505,20 @@ def flash_attention(q: torch.Tensor, kv: KVLayout, *, Sk: int, n_kv_heads: int, 
 def sample(logits: torch.Tensor, *, mask: Optional[torch.Tensor], temperature: Optional[torch.Tensor],
            seed: torch.Tensor, step: torch.Tensor, out_tokens: torch.Tensor,
            part_val: Optional[torch.Tensor] = None, part_idx: Optional[torch.Tensor] = None,
-           n_chunks: int = 64) -> torch.Tensor:
+           n_chunks: int = 64, fail_word: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Masked Gumbel-max sampling (greedy without temperature).  ``fail_word``: a device int64
+    that, when nonzero at sampling time, turns every output token into -2 (the chained
+    forward's grid-barrier timeout word: the logits of that step are invalid)."""
     rows = logits.shape[0]
     if not _gpu(logits):
-        return ref.sample(logits, mask=mask, temperature=temperature, seed=seed, step=step, out_tokens=out_tokens)
+        out = ref.sample(logits, mask=mask, temperature=temperature, seed=seed, step=step, out_tokens=out_tokens)
+        if fail_word is not None and int(fail_word.reshape(-1)[0]) != 0:
+            out[:rows] = -2
+        return out
     if part_val is None:
         part_val = torch.empty((rows * n_chunks,), dtype=torch.float32, device=logits.device)
         part_idx = torch.empty((rows * n_chunks,), dtype=torch.int32, device=logits.device)
-    ext().sample(logits, mask, temperature, seed, step, out_tokens, part_val, part_idx)
+    ext().sample(logits, mask, temperature, seed, step, out_tokens, part_val, part_idx, fail_word)
     return out_tokens
 
 

@@ -133,6 +133,7 @@ class LLMEngine:
         self.graphs: Dict[Tuple[int, int], Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
         self.graph_pool = None
         self.stats = dict(steps=0, rows=0, prefill_tokens=0, cached_tokens=0, graph_replays=0)
+        self._last_step = None  # (rows, logits_for, n_computed before) of a chained step, for recover_step
 
     # ------------------------------------------------------------------ sequences
     def new_sequence(self, tokens: Sequence[int], use_prefix_cache: bool = True) -> Sequence_:
@@ -211,13 +212,21 @@ class LLMEngine:
                     self._capture(M, L)
         torch.cuda.synchronize()
 
-    def run_rows(self, rows: List[Tuple[Sequence_, int]], logits_for: Optional[List[int]] = None) -> torch.Tensor:
+    def run_rows(self, rows: List[Tuple[Sequence_, int]], logits_for: Optional[List[int]] = None,
+                 check: bool = True) -> torch.Tensor:
         """Append one token per row (row = (seq, token)); return f32 logits of the rows listed in
         ``logits_for`` ([len(logits_for), V], default: every row).
 
         Rows of the same sequence must be consecutive and in order.  Selecting rows (typically
         the last row of each sequence) keeps the LM head -- the largest GEMM of a step -- at one
         row per sequence when jump-forward appends forced tokens.
+
+        A step that ran the chained launch (models/llama.py) is only valid if none of its grid
+        barriers timed out (workgroups not co-resident: another process's persistent kernel on
+        the GPU).  ``check=True`` synchronises and verifies that here, re-running the step on the
+        per-kernel path if needed.  ``check=False`` leaves it to the caller, who passes
+        ``step_fail_word()`` to the sampler (tokens come back as -2 on a failed step) and calls
+        ``recover_step()`` -- so the hot decode loop pays no extra synchronisation.
         """
         n = len(rows)
         M = bucket_for(n)
@@ -256,6 +265,9 @@ class LLMEngine:
             hi[3, n:M] = 1
             b.np_slots[n:M] = -1
         b.upload(M)
+        chained = self._uses_chain(M)
+        self._last_step = (list(rows), logits_for, {sid: self.seqs[sid].n_computed for sid in pending}) \
+            if chained else None
         if self.use_graphs:
             g, out = self.graphs.get((M, L)) or self._capture(M, L)
             g.replay()
@@ -268,9 +280,47 @@ class LLMEngine:
         self.stats["rows"] += n
         if self.stats["steps"] % 64 == 0:
             self._check_chain()
+        if check and chained and self.device.type == "cuda":
+            torch.cuda.current_stream().synchronize()
+            if self.model.chain_error():
+                return self.recover_step()
         if L == M and nl != n:
             return out[torch.tensor(logits_for, device=out.device)]
         return out[:nl]
+
+    def _uses_chain(self, M: int) -> bool:
+        ok = getattr(self.model, "_chain_ok", None)
+        return bool(ok is not None and ok(M))
+
+    def step_fail_word(self) -> Optional[torch.Tensor]:
+        """The device word that is nonzero if the last step's chained launch timed out (None when
+        the last step did not run the chain): pass it to ops.sample as ``fail_word``."""
+        if self._last_step is None:
+            return None
+        return self.model.chain_error_word()
+
+    def recover_step(self) -> torch.Tensor:
+        """After a chained step failed (its grid barrier timed out, so its logits -- and the K/V it
+        wrote -- are invalid): switch the model to per-kernel launches, drop the captured graphs,
+        clear the error word and re-run the same rows (their K/V slots are rewritten).  Returns
+        the re-run step's logits.  Call only after the host has synchronised with the step."""
+        import warnings
+
+        rows, logits_for, pre = self._last_step
+        self._last_step = None
+        warnings.warn("chained decode launch timed out at a grid barrier; re-running the step with "
+                      "per-kernel launches")
+        word = self.model.chain_error_word()
+        self.model.disable_chain()
+        if word is not None:
+            word.zero_()
+        self.graphs.clear()
+        self.stats["chain_fallbacks"] = self.stats.get("chain_fallbacks", 0) + 1
+        self.stats["steps"] -= 1
+        self.stats["rows"] -= len(rows)
+        for sid, n_done in pre.items():
+            self.seqs[sid].n_computed = n_done
+        return self.run_rows(rows, logits_for)
 
     def _check_chain(self, blocking: bool = False) -> None:
         """Health check of the chained decode launch (models/llama.py): a grid-barrier spin that
