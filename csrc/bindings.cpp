@@ -67,7 +67,8 @@ int run_skinny(int epi, const SkinnyParams& p, hipStream_t st) {
 }
 
 SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool fuse_rms, double eps,
-                         const c10::optional<Tensor>& w_scale = c10::nullopt) {
+                         const c10::optional<Tensor>& w_scale = c10::nullopt, bool w_tiled = false) {
+  TORCH_CHECK(!(w_tiled && w_scale.has_value()), "pre-tiled weights are bf16 only");
   check_bf16(x, "x");
   if (w_scale.has_value()) {
     TORCH_CHECK(w.scalar_type() == at::kFloat8_e4m3fn && w.is_cuda(), "fp8 weights must be float8_e4m3fn on the GPU");
@@ -97,12 +98,16 @@ SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<T
   p.eps = (float)eps;
   p.w_scale = w_scale.has_value() ? w_scale->data_ptr<float>() : nullptr;
   p.w_first = g_w_first == 2 || (g_w_first == 1 && fuse_rms);
+  p.w_tiled = w_tiled ? 1 : 0;
+  if (w_tiled) TORCH_CHECK(w.size(0) % 16 == 0 && w.size(1) % 128 == 0, "pre-tiled weights need N % 16 == 0, K % 128 == 0");
   return p;
 }
 
 // fp8 weights run only on the streaming kernel; a shape it cannot take is an error, never a
 // silent bf16 fallback (the Python layer routes those shapes to the dequantising path).
 int run_skinny_checked(int epi, const SkinnyParams& p, hipStream_t st) {
+  // pre-tiled weights exist only for the streaming kernel (a shape it rejects is an error)
+  if (p.w_tiled) return vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
   if (p.w_scale || (p.fuse_rms == 2 && !small_gemm(p))) return vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
   return run_skinny(epi, p, st);
 }
@@ -122,9 +127,10 @@ void set_ln_fold(SkinnyParams& p, const c10::optional<Tensor>& ln_c, int epi) {
 
 // epi: 0 store, 1 residual add, 3 gelu
 void skinny_gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi, bool fuse_rms, double eps,
-                 c10::optional<Tensor> residual, c10::optional<Tensor> w_scale, c10::optional<Tensor> ln_c) {
+                 c10::optional<Tensor> residual, c10::optional<Tensor> w_scale, c10::optional<Tensor> ln_c,
+                 bool w_tiled) {
   c10::DeviceGuard g(x.device());
-  SkinnyParams p = base_params(x, w, bias, fuse_rms, eps, w_scale);
+  SkinnyParams p = base_params(x, w, bias, fuse_rms, eps, w_scale, w_tiled);
   TORCH_CHECK(epi == 0 || epi == 1 || epi == 3, "bad epilogue");
   set_ln_fold(p, ln_c, (int)epi);
   TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1, "y must be a 2-D row-contiguous GPU tensor");
@@ -146,9 +152,9 @@ void skinny_gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64
 }
 
 void skinny_gemm_swiglu(Tensor x, Tensor w_gu, c10::optional<Tensor> bias, Tensor h, bool fuse_rms, double eps,
-                        c10::optional<Tensor> w_scale) {
+                        c10::optional<Tensor> w_scale, bool w_tiled) {
   c10::DeviceGuard g(x.device());
-  SkinnyParams p = base_params(x, w_gu, bias, fuse_rms, eps, w_scale);
+  SkinnyParams p = base_params(x, w_gu, bias, fuse_rms, eps, w_scale, w_tiled);
   check_bf16(h, "h");
   TORCH_CHECK(h.dim() == 2 && h.stride(1) == 1 && h.size(0) == x.size(0) && h.size(1) * 2 == w_gu.size(0),
               "h must be [M, N/2]");
@@ -201,9 +207,9 @@ void set_qkv_epilogue(SkinnyParams& p, const Tensor& w_qkv, int64_t n_q_heads, i
 void skinny_gemm_qkv(Tensor x, Tensor w_qkv, c10::optional<Tensor> bias, bool fuse_rms, double eps, int64_t n_q_heads,
                      int64_t n_kv_heads, int64_t head_dim, bool use_rope, Tensor positions, Tensor slots,
                      c10::optional<Tensor> rope, Tensor q_out, Tensor k_cache, Tensor v_cache,
-                     c10::optional<Tensor> w_scale, c10::optional<Tensor> ln_c) {
+                     c10::optional<Tensor> w_scale, c10::optional<Tensor> ln_c, bool w_tiled) {
   c10::DeviceGuard g(x.device());
-  SkinnyParams p = base_params(x, w_qkv, bias, fuse_rms, eps, w_scale);
+  SkinnyParams p = base_params(x, w_qkv, bias, fuse_rms, eps, w_scale, w_tiled);
   set_ln_fold(p, ln_c, 4);
   set_qkv_epilogue(p, w_qkv, n_q_heads, n_kv_heads, head_dim, use_rope, positions, slots, rope, q_out, k_cache,
                    v_cache);
@@ -243,7 +249,8 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                                        c10::optional<Tensor> a_table, int64_t a_block_size, int64_t a_sb, int64_t a_sh,
                                        int64_t a_st, c10::optional<Tensor> a_ctx, c10::optional<Tensor> a_seq,
                                        double a_scale, int64_t a_n_splits, c10::optional<Tensor> a_part_o,
-                                       c10::optional<Tensor> a_part_ml, c10::optional<Tensor> a_counters) {
+                                       c10::optional<Tensor> a_part_ml, c10::optional<Tensor> a_counters,
+                                       bool w_tiled) {
   c10::DeviceGuard g(h.device());
   const int64_t M = h.size(0);
   TORCH_CHECK(att.size(0) == M && act.size(0) == M, "row counts differ");
@@ -254,16 +261,16 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                   (reinterpret_cast<uintptr_t>(bar.data_ptr()) & 127) == 0,
               "bar must be a 128-byte aligned int32[>=384] on the GPU");
   ChainParams cp{};
-  cp.ph[0].p = base_params(att, w_o, c10::nullopt, false, eps);
+  cp.ph[0].p = base_params(att, w_o, c10::nullopt, false, eps, c10::nullopt, w_tiled);
   cp.ph[0].epi = 1;
   set_resid(cp.ph[0].p, h);
-  cp.ph[1].p = base_params(h, w_gu, c10::nullopt, true, eps);
+  cp.ph[1].p = base_params(h, w_gu, c10::nullopt, true, eps, c10::nullopt, w_tiled);
   cp.ph[1].epi = 2;
   check_bf16(act, "act");
   TORCH_CHECK(act.stride(1) == 1, "act rows must be contiguous");
   cp.ph[1].p.Y = act.data_ptr();
   cp.ph[1].p.ldy = (int)act.stride(0);
-  cp.ph[2].p = base_params(act, w_down, c10::nullopt, false, eps);
+  cp.ph[2].p = base_params(act, w_down, c10::nullopt, false, eps, c10::nullopt, w_tiled);
   cp.ph[2].epi = 1;
   set_resid(cp.ph[2].p, h);
   cp.n = 3;
@@ -273,7 +280,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
     TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
                     v_cache.has_value(),
                 "the QKV phase needs positions, slots, q_out and the KV caches");
-    cp.ph[3].p = base_params(h, *w_qkv, c10::nullopt, true, eps);
+    cp.ph[3].p = base_params(h, *w_qkv, c10::nullopt, true, eps, c10::nullopt, w_tiled);
     cp.ph[3].epi = 4;
     set_qkv_epilogue(cp.ph[3].p, *w_qkv, n_q_heads, n_kv_heads, head_dim, rope.has_value(), *positions, *slots, rope,
                      *q_out, *k_cache, *v_cache);
@@ -734,13 +741,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for the voice-web-agent inference engine";
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
         py::arg("fuse_rms"), py::arg("eps"), py::arg("residual"), py::arg("w_scale") = py::none(),
-        py::arg("ln_c") = py::none());
+        py::arg("ln_c") = py::none(), py::arg("w_tiled") = false);
   m.def("skinny_gemm_swiglu", &skinny_gemm_swiglu, py::arg("x"), py::arg("w_gu"), py::arg("bias"), py::arg("h"),
-        py::arg("fuse_rms"), py::arg("eps"), py::arg("w_scale") = py::none());
+        py::arg("fuse_rms"), py::arg("eps"), py::arg("w_scale") = py::none(), py::arg("w_tiled") = false);
   m.def("skinny_gemm_qkv", &skinny_gemm_qkv, py::arg("x"), py::arg("w_qkv"), py::arg("bias"), py::arg("fuse_rms"),
         py::arg("eps"), py::arg("n_q_heads"), py::arg("n_kv_heads"), py::arg("head_dim"), py::arg("use_rope"),
         py::arg("positions"), py::arg("slots"), py::arg("rope"), py::arg("q_out"), py::arg("k_cache"),
-        py::arg("v_cache"), py::arg("w_scale") = py::none(), py::arg("ln_c") = py::none());
+        py::arg("v_cache"), py::arg("w_scale") = py::none(), py::arg("ln_c") = py::none(),
+        py::arg("w_tiled") = false);
   m.def("chain_make", &chain_make, py::arg("h"), py::arg("att"), py::arg("act"), py::arg("w_o"), py::arg("w_gu"),
         py::arg("w_down"), py::arg("eps"), py::arg("w_qkv"), py::arg("n_q_heads"), py::arg("n_kv_heads"),
         py::arg("head_dim"), py::arg("positions"), py::arg("slots"), py::arg("rope"), py::arg("q_out"),
@@ -749,7 +757,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_table") = py::none(), py::arg("a_block_size") = 0, py::arg("a_sb") = 0, py::arg("a_sh") = 0,
         py::arg("a_st") = 0, py::arg("a_ctx") = py::none(), py::arg("a_seq") = py::none(), py::arg("a_scale") = 0.0,
         py::arg("a_n_splits") = 0, py::arg("a_part_o") = py::none(), py::arg("a_part_ml") = py::none(),
-        py::arg("a_counters") = py::none());
+        py::arg("a_counters") = py::none(), py::arg("w_tiled") = false);
   m.def("set_small_gemm_bytes", &set_small_gemm_bytes);
   m.def("chain_make_seq", &chain_make_seq, py::arg("seq"), py::arg("X"), py::arg("W"), py::arg("bias"),
         py::arg("ln_c"), py::arg("Y"), py::arg("epi"), py::arg("eps"), py::arg("n_heads"), py::arg("head_dim"),
@@ -775,4 +783,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("w_first") = 2);
   m.def("attention_split_tokens", []() { return vwa_attention_split_tokens(); });
   m.def("set_attention_impl", [](int64_t impl) { vwa_set_attention_impl((int)impl); });
+  m.def("set_chain_weight_policy", [](int64_t aux) { vwa_set_chain_weight_policy((int)aux); });
 }

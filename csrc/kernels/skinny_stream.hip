@@ -37,6 +37,13 @@ VWA_DEVICE uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
   u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// weight-stream load with cache policy AUX (gfx950 buffer aux bits: 1 sc0, 2 nt, 16 sc1): decode
+// weights are read once per step by one CU, so nt (2) keeps them from displacing L2 lines
+template <int AUX>
+VWA_DEVICE uint4 bload_w(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, AUX);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 // Epilogue operands that do not depend on the GEMM (residual tile, fp8 column scales, QKV row
 // positions / KV slots / rotary factors) are loaded for the workgroup's FIRST tile at kernel
@@ -239,10 +246,17 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
       const bool ok = (it < n_items) && (kg < ge);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        const unsigned row = (unsigned)(tile * 16 * NT + nt * 16 + nl);
-        const unsigned base = (row * (unsigned)K + (unsigned)(kg * 128 + 32 * g)) * 2u;
+        if (p.w_tiled) {  // pre-tiled: 1 KB contiguous per load instruction
+          const unsigned T = (unsigned)(tile * NT + nt);
+          const unsigned base = ((T * (unsigned)G + (unsigned)kg) * 4u) * 1024u + (unsigned)lane * 16u;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) wr[nt][u][s] = bload(rw, ok ? base + 16u * s : kOOB);
+          for (int s = 0; s < 4; ++s) wr[nt][u][s] = bload(rw, ok ? base + 1024u * s : kOOB);
+        } else {
+          const unsigned row = (unsigned)(tile * 16 * NT + nt * 16 + nl);
+          const unsigned base = (row * (unsigned)K + (unsigned)(kg * 128 + 32 * g)) * 2u;
+#pragma unroll
+          for (int s = 0; s < 4; ++s) wr[nt][u][s] = bload(rw, ok ? base + 16u * s : kOOB);
+        }
       }
     }
   };
@@ -529,9 +543,46 @@ constexpr int kChainSpinLimit = 1 << 18;  // ~0.3 s: a lost workgroup ends the l
 // on uncached memory (256 same-address atomics) measured 121 us per chained layer vs 99.6 two-level.
 constexpr int kBarTop = 128, kBarErr = 160;
 
-VWA_DEVICE unsigned long long chain_arrive(unsigned long long* bar, int nwg, int mode) {
+// Sum of the 8 group counters (mode 4/5), read with scalar loads past the scalar cache: one
+// round trip for all eight (they complete on lgkmcnt, not behind the wave's weight loads).
+VWA_DEVICE unsigned long long bar_sum8(const unsigned long long* bar) {
+  unsigned long long v0, v1, v2, v3, v4, v5, v6, v7;
+  asm volatile(
+      "s_load_dwordx2 %0, %8, 0x0 glc\n\t"
+      "s_load_dwordx2 %1, %8, 0x80 glc\n\t"
+      "s_load_dwordx2 %2, %8, 0x100 glc\n\t"
+      "s_load_dwordx2 %3, %8, 0x180 glc\n\t"
+      "s_load_dwordx2 %4, %8, 0x200 glc\n\t"
+      "s_load_dwordx2 %5, %8, 0x280 glc\n\t"
+      "s_load_dwordx2 %6, %8, 0x300 glc\n\t"
+      "s_load_dwordx2 %7, %8, 0x380 glc\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&s"(v0), "=&s"(v1), "=&s"(v2), "=&s"(v3), "=&s"(v4), "=&s"(v5), "=&s"(v6), "=&s"(v7)
+      : "s"(bar)
+      : "memory");
+  return v0 + v1 + v2 + v3 + v4 + v5 + v6 + v7;
+}
+
+// Mode 4 (5 = diagnostic without the wait): arrival is a NO-RETURN add on the workgroup's group
+// counter (the wave never waits for a round trip to arrive), and the waiting wave polls the sum
+// of the eight group counters.  Targets: base + i * nwg, with base read once at kernel start
+// (every completed launch added a multiple of nwg; this workgroup has not arrived yet, so fewer
+// than nwg arrivals of this launch can be counted in it).
+VWA_DEVICE unsigned long long chain_base(const unsigned long long* bar, int nwg, int mode) {
+  if (mode < 4 || threadIdx.x >= 64) return 0;
+  const unsigned long long s = bar_sum8(bar);
+  return (s / (unsigned long long)nwg) * (unsigned long long)nwg;
+}
+
+VWA_DEVICE unsigned long long chain_arrive(unsigned long long* bar, int nwg, int mode, unsigned long long& next) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are performed
   __syncthreads();
+  if (mode >= 4) {
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(&bar[16 * (blockIdx.x & 7)], 1ull, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    next += (unsigned long long)nwg;
+    return next;
+  }
   unsigned long long target = 0;
   if (threadIdx.x == 0) {
     if (mode == 0) {
@@ -552,6 +603,26 @@ VWA_DEVICE unsigned long long chain_arrive(unsigned long long* bar, int nwg, int
 }
 
 VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, int mode) {
+  if (mode == 3 || mode == 5) {  // DIAGNOSTIC ONLY (tools/chain_probe.py --no-wait): arrive, never
+    __syncthreads();             // wait -> wrong results; what the phases cost without dependencies
+    return;
+  }
+  if (mode == 4) {
+    if (threadIdx.x < 64) {
+      const unsigned long long tgt = __builtin_amdgcn_readfirstlane((unsigned)target) |
+                                     ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(target >> 32)) << 32);
+      int spins = 0;
+      while ((long long)(bar_sum8(bar) - tgt) < 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kChainSpinLimit) {
+          if (threadIdx.x == 0) __hip_atomic_store(&bar[kBarErr], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    return;
+  }
   if (mode == 2) {
     // wave 0 polls with scalar loads (glc: past the scalar cache; bar lives in uncached memory so
     // no L2 copy can be stale): SMEM completes on lgkmcnt, so the poll is not queued behind the
@@ -614,7 +685,7 @@ VWA_DEVICE PhaseRange chain_range(const ChainPhase& ph) {
 }
 
 // weight item `it` (unit u0 + it) of phase p into the registers wr (NT * U <= 4 groups of 4)
-template <int NT, int U>
+template <int NT, int U, int WA>
 VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[16], int it, const PhaseRange& r) {
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.W), (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
@@ -627,10 +698,20 @@ VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[16], int i
     const bool ok = (it < r.n_items) && (kg < r.ge);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const unsigned row = (unsigned)(tile * 16 * NT + nt * 16 + nl);
-      const unsigned base = (row * (unsigned)p.K + (unsigned)(kg * 128 + 32 * g)) * 2u;
+      if (p.w_tiled) {
+        // pre-tiled weights (ops.tile_weight): each load instruction reads 1 KB contiguous.
+        // Measured (tools/chain_probe.py, Llama-3-8B layer tail): 89.6 vs 101.4 us at 1 row,
+        // 96.3 vs 106.8 us at 4 rows against the row-major [N, K] access
+        const unsigned T = (unsigned)(tile * NT + nt);
+        const unsigned base = ((T * (unsigned)(p.K / 128) + (unsigned)kg) * 4u) * 1024u + (unsigned)lane * 16u;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) wr[(nt * U + u) * 4 + s] = bload(rw, ok ? base + 16u * s : kOOB);
+        for (int s = 0; s < 4; ++s) wr[(nt * U + u) * 4 + s] = bload_w<WA>(rw, ok ? base + 1024u * s : kOOB);
+      } else {
+        const unsigned row = (unsigned)(tile * 16 * NT + nt * 16 + nl);
+        const unsigned base = (row * (unsigned)p.K + (unsigned)(kg * 128 + 32 * g)) * 2u;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) wr[(nt * U + u) * 4 + s] = bload_w<WA>(rw, ok ? base + 16u * s : kOOB);
+      }
     }
   }
 }
@@ -646,11 +727,11 @@ struct PhaseShape {
 
 // the phase's first weight item (and with pre2 its second) before the barrier wait: a
 // workgroup that arrives early keeps HBM busy while the grid catches up
-template <int EPI, int KS>
+template <int EPI, int KS, int WA>
 VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[16], uint4 (&wr2)[16], int pre2) {
   const PhaseRange r = chain_range<KS>(ph);
-  chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U>(ph.p, ph.nb, wr, 0, r);
-  if (pre2) chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U>(ph.p, ph.nb, wr2, 1, r);
+  chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U, WA>(ph.p, ph.nb, wr, 0, r);
+  if (pre2) chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U, WA>(ph.p, ph.nb, wr2, 1, r);
 }
 
 // partial tile of a split tile: cross-wave sums of this workgroup's units -> slot (sc1)
@@ -675,7 +756,7 @@ VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
 }
 
 // One phase.  X0 holds this phase's item 0 (issued before the barrier wait).
-template <int EPI, int KS>
+template <int EPI, int KS, int WA>
 VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4 (&X1)[16], char* smem, int pre2) {
   constexpr int NT = PhaseShape<EPI>::NT, U = PhaseShape<EPI>::U;
   const ChainPhase& ph = cp.ph[i];
@@ -788,10 +869,10 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
   // traffic, no epilogue)
   const int n_pad = (r.n_items + 1) & ~1;
   for (int it = 0; it < n_pad; it += 2) {
-    if (it > 0 || !pre2) chain_load<NT, U>(p, nb, X1, it + 1, r);
+    if (it > 0 || !pre2) chain_load<NT, U, WA>(p, nb, X1, it + 1, r);
     compute(X0, it);
     finish(it);
-    if (it + 2 < n_pad) chain_load<NT, U>(p, nb, X0, it + 2, r);
+    if (it + 2 < n_pad) chain_load<NT, U, WA>(p, nb, X0, it + 2, r);
     compute(X1, it + 1);
     if (it + 1 < r.n_items) finish(it + 1);
   }
@@ -816,7 +897,7 @@ struct SeqEpi {
                                           : (I == 0 ? EPI_RESID : EPI_STORE);
 };
 
-template <int KS, int SEQ, int NPH, int AG>
+template <int KS, int SEQ, int NPH, int AG, int WA>
 __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __restrict__ cpp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ChainParams& cp = *cpp;  // device-resident descriptor
@@ -826,6 +907,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   const int nwg = (int)gridDim.x;
   unsigned long long gen;
   unsigned long long* bar = reinterpret_cast<unsigned long long*>(cp.bar);
+  unsigned long long bar_next = chain_base(bar, nwg, cp.bar_mode);  // mode >= 4: running target
   int nts = 0;
   auto stamp = [&]() {
     if (cp.ts && threadIdx.x == 0) cp.ts[blockIdx.x * 16 + nts] = __builtin_amdgcn_s_memrealtime();
@@ -840,39 +922,39 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     // their item, at the barrier (one item: their attention registers were live until then)
     const bool idle = mq_body<128, AG, KS, true, false>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
                                                         (int)blockIdx.x,
-                                                        [&]() { chain_issue_first<E0, KS>(cp.ph[0], A, B, pre0); });
+                                                        [&]() { chain_issue_first<E0, KS, WA>(cp.ph[0], A, B, pre0); });
     stamp();
-    gen = chain_arrive(bar, nwg, cp.bar_mode);
+    gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
     if (!idle) {
       pre0 = 0;
-      chain_issue_first<E0, KS>(cp.ph[0], A, B, 0);
+      chain_issue_first<E0, KS, WA>(cp.ph[0], A, B, 0);
     }
     chain_wait(bar, gen, cp.bar_mode);
   } else {
-    chain_issue_first<E0, KS>(cp.ph[0], A, B, pre0);
+    chain_issue_first<E0, KS, WA>(cp.ph[0], A, B, pre0);
   }
-  chain_phase<E0, KS>(cp, 0, A, B, smem, pre0);
+  chain_phase<E0, KS, WA>(cp, 0, A, B, smem, pre0);
   stamp();
-  gen = chain_arrive(bar, nwg, cp.bar_mode);
-  chain_issue_first<E1, KS>(cp.ph[1], A, B, cp.pre2);
+  gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
+  chain_issue_first<E1, KS, WA>(cp.ph[1], A, B, cp.pre2);
   chain_wait(bar, gen, cp.bar_mode);
   stamp();
-  chain_phase<E1, KS>(cp, 1, A, B, smem, cp.pre2);
+  chain_phase<E1, KS, WA>(cp, 1, A, B, smem, cp.pre2);
   stamp();
   if constexpr (NPH >= 3) {
-    gen = chain_arrive(bar, nwg, cp.bar_mode);
-    chain_issue_first<E2, KS>(cp.ph[2], A, B, cp.pre2);
+    gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
+    chain_issue_first<E2, KS, WA>(cp.ph[2], A, B, cp.pre2);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E2, KS>(cp, 2, A, B, smem, cp.pre2);
+    chain_phase<E2, KS, WA>(cp, 2, A, B, smem, cp.pre2);
     stamp();
   }
   if constexpr (NPH >= 4) {
-    gen = chain_arrive(bar, nwg, cp.bar_mode);
-    chain_issue_first<E3, KS>(cp.ph[3], A, B, cp.pre2);
+    gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
+    chain_issue_first<E3, KS, WA>(cp.ph[3], A, B, cp.pre2);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E3, KS>(cp, 3, A, B, smem, cp.pre2);
+    chain_phase<E3, KS, WA>(cp, 3, A, B, smem, cp.pre2);
     stamp();
   }
 }
@@ -917,10 +999,19 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
   return (int)lds;
 }
 
+// weight-stream cache policy of the chained launch: 0 default; 2 nt measured 142.6 vs 100.7 us
+// per Llama-3-8B layer tail (tools/chain_probe.py --wpol 2), so 0
+static int g_chain_wa = 0;
+extern "C" void vwa_set_chain_weight_policy(int aux) { g_chain_wa = aux == 0 ? 0 : 2; }
+
 extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid,
                                 hipStream_t st) {
   if (attn_g) lds = lds > (int)MqLds<128, 8>::bytes ? lds : (int)MqLds<128, 8>::bytes;
-#define VWA_CHAIN_LAUNCH(S, N, G) hipLaunchKernelGGL((chain_kernel<8, S, N, G>), dim3(grid), dim3(8 * 64), lds, st, d_cp)
+#define VWA_CHAIN_LAUNCH(S, N, G)                                                                              \
+  do {                                                                                                         \
+    if (g_chain_wa) hipLaunchKernelGGL((chain_kernel<8, S, N, G, 2>), dim3(grid), dim3(8 * 64), lds, st, d_cp); \
+    else hipLaunchKernelGGL((chain_kernel<8, S, N, G, 0>), dim3(grid), dim3(8 * 64), lds, st, d_cp);           \
+  } while (0)
   if (seq == 0) {
     if (n_phases != 3 && n_phases != 4) return -10;
     const bool q = n_phases == 4;

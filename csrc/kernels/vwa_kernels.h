@@ -27,6 +27,11 @@ struct SkinnyParams {
   // W*gamma, bias holds b + W.beta, ln_c[n] = sum_k (W*gamma)[n][k]; the kernel computes each
   // row's mean/rstd from the staged X and applies y = rstd * (acc - mean * ln_c[n]) + bias
   const float* ln_c;
+  // w_tiled: W (bf16) is stored pre-tiled for the MFMA B operand: for each 16-row tile T and
+  // 128-wide k-group kg, a contiguous 4 KB block [s = 0..3][lane = 0..63][8 bf16] holding
+  // W[16 T + (lane & 15)][128 kg + 32 (lane >> 4) + 8 s + e] -- every weight load instruction of
+  // the streaming / chained kernels then reads 1 KB contiguous (ops.tile_weight)
+  int w_tiled;
 };
 
 // Paged / strided KV addressing shared by the attention kernels:
@@ -99,6 +104,7 @@ int vwa_skinny_gemm(int epi, const SkinnyParams* p, hipStream_t st);
 int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st);
 int vwa_chain_prepare(ChainParams* cp, int grid);
 int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid, hipStream_t st);
+void vwa_set_chain_weight_policy(int aux);  // 0: default cache policy, 2: nt (non-temporal) weight loads
 int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
                 uint16_t* y, int rows, int D, int ldx, float eps, hipStream_t st);
 int vwa_layernorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,

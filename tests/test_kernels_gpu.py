@@ -456,3 +456,45 @@ def test_fp8_qkv_rope_write(M):
     close(q, q2, 3e-2)
     close(kc, kc2, 3e-2)
     close(vc, vc2, 3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 4, 9, 16])
+def test_tiled_weights_match_row_major(M):
+    """Pre-tiled bf16 weights (ops.tile_weight / TiledWeight, SkinnyParams::w_tiled) on the
+    streaming kernel give the row-major results for every decode epilogue: store (f32 out, the LM
+    head), residual, the down shape (K = 14336, XG variant past 5 rows), SwiGLU and QKV + RoPE +
+    paged-KV write."""
+    K, N = 4096, 1024
+    x = rnd(M, K)
+    w = rnd(N, K, scale=0.02)
+    tw = ops.TiledWeight(w)
+    assert torch.equal(ops.untile_weight(tw.t), w)
+    a = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    b = torch.empty_like(a)
+    ops.linear(x, w, out=a, fuse_rms=True)
+    ops.linear(x, tw, out=b, fuse_rms=True)
+    close(b, a, 1e-3, 1e-3)
+    xd, wd, res = rnd(M, 14336), rnd(512, 14336, scale=0.01), rnd(M, 512)
+    a, b = res.clone(), res.clone()
+    ops.linear(xd, wd, out=a, residual=a)
+    ops.linear(xd, ops.TiledWeight(wd), out=b, residual=b)
+    close(b, a, 1e-2, 1e-2)
+    gu = ops.interleave_gate_up(rnd(512, K, scale=0.02), rnd(512, K, scale=0.02))
+    a = ops.linear_swiglu(x, gu, fuse_rms=True)
+    b = ops.linear_swiglu(x, ops.TiledWeight(gu), fuse_rms=True)
+    close(b, a, 1e-2, 1e-2)
+    nq, nkv, hd = 8, 2, 128
+    wq = ops.permute_qkv_rows(rnd((nq + 2 * nkv) * hd, K, scale=0.02), nq + 2 * nkv, hd)
+    rope = ops.rope_table(512, hd, 5e5, device=DEV)
+    pos = torch.arange(7, 7 + M, dtype=torch.int32, device=DEV)
+    slots = torch.arange(M, dtype=torch.int64, device=DEV) + 3
+    outs = []
+    for ww in (wq, ops.TiledWeight(wq)):
+        kc = torch.zeros(4, nkv, 16, hd, dtype=BF, device=DEV)
+        vc = torch.zeros_like(kc)
+        q = torch.zeros(M, nq * hd, dtype=BF, device=DEV)
+        ops.qkv_rope_write(x, ww, None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
+                           rope=rope, positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc)
+        outs.append((q, kc, vc))
+    for a, b in zip(*outs):
+        close(b, a, 1e-2, 1e-2)

@@ -21,9 +21,17 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--bar-mode", type=int, default=2)
     ap.add_argument("--attn", action="store_true", help="decode attention (ctx 1100) as the first phase")
+    ap.add_argument("--wpol", type=int, default=0, help="weight-load cache policy: 0 default, 2 nt")
+    ap.add_argument("--no-wait", action="store_true",
+                    help="DIAGNOSTIC: barriers arrive but never wait (wrong results): phase cost without dependencies")
+    ap.add_argument("--row-major", dest="tiled", action="store_false",
+                    help="row-major [N, K] weights instead of the pre-tiled layout (ops.tile_weight)")
     a = ap.parse_args()
+    if a.no_wait:
+        a.bar_mode = 5 if a.bar_mode >= 4 else 3
     dev, bf = "cuda", torch.bfloat16
     E = ops.ext()
+    E.set_chain_weight_policy(a.wpol)
     torch.manual_seed(0)
     M, d, F, nq, nkv, hd = a.rows, 4096, 14336, 32, 8, 128
     ncopy = 3  # rotate weights over > 256 MB Infinity Cache
@@ -55,8 +63,12 @@ def main():
                    a_part_o=torch.zeros(M * ns * nq * hd, device=dev), a_part_ml=torch.zeros(M * ns * nq * 2, device=dev),
                    a_counters=torch.zeros(M * nkv, dtype=torch.int32, device=dev))
         ag = nq // nkv
-    descs = [E.chain_make(h, att, act, w["o"], w["gu"], w["down"], 1e-5, w["qkv"], nq, nkv, hd, pos, slots, rope, q,
-                          kc, vc, bar, work, ts, a.bar_mode, **akw) for w in Ws]
+    if a.tiled:  # the descriptors hold raw pointers: keep the tiled copies alive in Ws
+        for w in Ws:
+            w.update({k + "_t": ops.tile_weight(w[k]) for k in ("o", "gu", "down", "qkv")})
+    wt = (lambda w, k: w[k + "_t"]) if a.tiled else (lambda w, k: w[k])  # noqa: E731
+    descs = [E.chain_make(h, att, act, wt(w, "o"), wt(w, "gu"), wt(w, "down"), 1e-5, wt(w, "qkv"), nq, nkv, hd, pos, slots, rope, q,
+                          kc, vc, bar, work, ts, a.bar_mode, **akw, w_tiled=a.tiled) for w in Ws]
     it = [0]
 
     def chained():
@@ -81,7 +93,7 @@ def main():
     chained()  # one launch first: a broken barrier shows up as the error word, not a long run
     torch.cuda.synchronize()
     assert int(bar.view(torch.int64)[160].item()) == 0, "barrier timeout"
-    t_sep = timeit(separate)
+    t_sep = 0.0 if a.no_wait else timeit(separate)
     t_ch = timeit(chained)
     assert int(bar.view(torch.int64)[160].item()) == 0, "barrier timeout"
     # stamps of the last launch: [start, end0, wait0, end1, wait1, end2, wait2, end3]
@@ -92,7 +104,7 @@ def main():
     med = st.median(dim=0).values.tolist()
     mx = st.max(dim=0).values.tolist()
     mn = st.min(dim=0).values.tolist()
-    r = dict(kernel="chain_probe", rows=M, bar_mode=a.bar_mode, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
+    r = dict(kernel="chain_probe", rows=M, bar_mode=a.bar_mode, wpol=a.wpol, tiled=a.tiled, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
              stamps_med_us=[round(x, 2) for x in med], stamps_min_us=[round(x, 2) for x in mn],
              stamps_max_us=[round(x, 2) for x in mx],
              legend=("start,end_attn," if a.attn else "start,") + "end_o,wait_o,end_gu,wait_gu,end_down,wait_down,end_qkv")

@@ -74,6 +74,17 @@ class LlamaModel:
             self._quantize_fp8()
         elif wdtype != "bf16":
             raise ValueError(f"unsupported weight dtype {wdtype!r} (bf16 | fp8)")
+        elif self.device.type == "cuda" and dtype == torch.bfloat16 and ops.env_flag("VWA_TILED_WEIGHTS", True):
+            self._tile_weights()
+
+    def _tile_weights(self) -> None:
+        """Second, pre-tiled copy of every projection + the LM head (ops.TiledWeight): the decode
+        streaming / chained kernels read it with 1 KB contiguous load instructions (Llama-3-8B
+        layer tail 89.6 vs 101.4 us, tools/chain_probe.py); prefill GEMMs keep the row-major copy."""
+        T = ops.TiledWeight
+        for L in self.layers:
+            L.qkv, L.o, L.gu, L.down = T(L.qkv), T(L.o), T(L.gu), T(L.down)
+        self.lm_head = T(self.lm_head)
 
     def _quantize_fp8(self) -> None:
         q = ops.FP8Weight.quantize
@@ -144,7 +155,8 @@ class LlamaModel:
         self.lm_head = ops.fold_norm(lm[self.v_start : self.v_end], get("model.norm.weight")).contiguous()
 
     def weight_bytes(self) -> int:
-        """Bytes streamed per decode step (projections + LM head; one embedding row is noise)."""
+        """Bytes streamed per decode step (projections + LM head, one layout of each; one
+        embedding row is noise)."""
         ts = [self.lm_head] + [t for L in self.layers for t in (L.qkv, L.o, L.gu, L.down)]
         return sum(t.numel() * t.element_size() for t in ts)
 
@@ -209,12 +221,14 @@ class LlamaModel:
                      a_sb=lay.sb, a_sh=lay.sh, a_st=lay.st, a_ctx=bufs.ctx_lens, a_seq=bufs.seq_ids,
                      a_scale=self.scale, a_n_splits=ops.decode_n_splits(bufs.max_ctx), a_part_o=bufs.part_o,
                      a_part_ml=bufs.part_ml, a_counters=bufs.attn_cnt)
+        tiled = isinstance(L.o, ops.TiledWeight)
+        wsel = (lambda w: w.t) if tiled else (lambda w: w)  # noqa: E731
         desc, lds = ops.ext().chain_make(
-            bufs.hidden[:M], bufs.attn[:M], bufs.act[:M], L.o, L.gu, L.down, self.cfg.rms_eps,
-            N.qkv if nxt else None, self.nq, self.nkv, self.hd,
+            bufs.hidden[:M], bufs.attn[:M], bufs.act[:M], wsel(L.o), wsel(L.gu), wsel(L.down), self.cfg.rms_eps,
+            wsel(N.qkv) if nxt else None, self.nq, self.nkv, self.hd,
             bufs.positions if nxt else None, bufs.slots if nxt else None, self.rope if nxt else None,
             bufs.q[:M] if nxt else None, kv.k[li + 1] if nxt else None, kv.v[li + 1] if nxt else None,
-            self._chain_bar, self._chain_work, None, self._chain_bar_mode, **a)
+            self._chain_bar, self._chain_work, None, self._chain_bar_mode, **a, w_tiled=tiled)
         cache[key] = (desc, 4 if nxt else 3, lds, self.nq // self.nkv if attn else 0) if desc.numel() else None
         return cache[key]
 
@@ -318,7 +332,7 @@ def move_model(model, device) -> None:
     device = torch.device(device)
 
     def mv(obj):
-        if isinstance(obj, (torch.Tensor, ops.FP8Weight)):
+        if isinstance(obj, (torch.Tensor, ops.FP8Weight, ops.TiledWeight)):
             return obj.to(device)
         if dataclasses.is_dataclass(obj) and not isinstance(obj, type):
             for f in dataclasses.fields(obj):

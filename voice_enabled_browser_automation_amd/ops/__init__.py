@@ -155,6 +155,70 @@ def _fp8_matmul(x: torch.Tensor, w: "FP8Weight") -> torch.Tensor:
     return torch.matmul(x, w.dequant(x.dtype).t())
 
 
+# ----------------------------------------------------------------------------- tiled bf16 weights
+def tile_weight(w: torch.Tensor) -> torch.Tensor:
+    """Pre-tiled copy of a bf16 weight [N, K] for the decode kernels (vwa_kernels.h
+    SkinnyParams::w_tiled): per 16-row tile T and 128-wide k-group kg, one contiguous 4 KB block
+    [s][lane][8] with lane = 16 * g + n holding W[16 T + n][128 kg + 32 g + 8 s + e], i.e. the
+    MFMA B-operand fragments in the order the wave loads them -- each load instruction then
+    reads 1 KB contiguous instead of 16 B pieces of 32 cache lines.  Same shape [N, K], so the
+    host-side shape checks are unchanged; only the element order differs."""
+    N, K = w.shape
+    assert N % 16 == 0 and K % 128 == 0, "tile_weight needs N % 16 == 0 and K % 128 == 0"
+    t = w.reshape(N // 16, 16, K // 128, 4, 4, 8)          # [T, n, kg, g, s, e]
+    return t.permute(0, 2, 4, 3, 1, 5).contiguous().view(N, K)  # [T, kg, s, g, n, e]
+
+
+def untile_weight(t: torch.Tensor) -> torch.Tensor:
+    """Inverse of tile_weight (tests)."""
+    N, K = t.shape
+    return t.reshape(N // 16, K // 128, 4, 4, 16, 8).permute(0, 4, 1, 3, 2, 5).contiguous().view(N, K)
+
+
+class TiledWeight:
+    """A bf16 projection weight kept in two layouts: ``w`` row-major [N, K] (hipBLASLt prefill,
+    the one-tile kernel, the CPU reference) and ``t`` = tile_weight(w) for the decode streaming /
+    chained kernels, which read it with fully contiguous 1 KB load instructions.  The second
+    copy is the price of that (15 GB for Llama-3-8B, sized for 288 GB of HBM per GPU)."""
+
+    __slots__ = ("w", "t")
+
+    def __init__(self, w: torch.Tensor, t: Optional[torch.Tensor] = None):
+        self.w = w
+        self.t = tile_weight(w) if t is None else t
+
+    @property
+    def shape(self):
+        return self.w.shape
+
+    @property
+    def device(self):
+        return self.w.device
+
+    @property
+    def dtype(self):
+        return self.w.dtype
+
+    def numel(self) -> int:
+        return self.w.numel()
+
+    def element_size(self) -> int:
+        return self.w.element_size()
+
+    def to(self, device) -> "TiledWeight":
+        return TiledWeight(self.w.to(device), self.t.to(device))
+
+
+def _stream_ok(x: torch.Tensor, w) -> bool:
+    """Decode rows the streaming kernel takes with a pre-tiled weight."""
+    return x.shape[0] <= SKINNY_MAX_M and x.shape[1] % 128 == 0 and w.shape[0] % 16 == 0
+
+
+def plain(w):
+    """The row-major tensor of a weight (TiledWeight -> .w; anything else unchanged)."""
+    return w.w if isinstance(w, TiledWeight) else w
+
+
 # ----------------------------------------------------------------------------- layout helpers
 def qkv_row_perm(head_dim: int) -> torch.Tensor:
     half = head_dim // 2
@@ -261,6 +325,15 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     dt = out_dtype or (x.dtype if out is None else out.dtype)
     if out is None:
         out = torch.empty((M, w.shape[0]), dtype=dt, device=x.device)
+    if isinstance(w, TiledWeight):
+        if _gpu(x) and _stream_ok(x, w) and (ln_c is None or _ln_fold_fits(x, w.w)):
+            epi = {"none": 0, "gelu": 3}[act]
+            if residual is not None:
+                assert act == "none"
+                epi = 1
+            ext().skinny_gemm(x, w.t, bias, out, epi, fuse_rms and ln_c is None, eps, residual, None, ln_c, True)
+            return out
+        w = w.w
     if ln_c is not None:
         if _ln_fold_fits(x, w):
             epi = {"none": 0, "gelu": 3}[act] if residual is None else 1
@@ -306,6 +379,11 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
     F = w_gu.shape[0] // 2
     if out is None:
         out = torch.empty((M, F), dtype=x.dtype, device=x.device)
+    if isinstance(w_gu, TiledWeight):
+        if _gpu(x) and _stream_ok(x, w_gu):
+            ext().skinny_gemm_swiglu(x, w_gu.t, None, out, fuse_rms, eps, None, True)
+            return out
+        w_gu = w_gu.w
     if not _gpu(x):
         xr, wr, fr = _ref_w8(x, w_gu, fuse_rms, eps)
         return ref.linear_swiglu(xr, wr, fuse_rms=fr, eps=eps, out=out)
@@ -330,6 +408,12 @@ def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Te
     """Fused QKV projection + rotary + paged KV write. Returns q_out[:M] (natural layout).
     ln_c: folded LayerNorm on x (see linear)."""
     M = x.shape[0]
+    if isinstance(w_qkv, TiledWeight):
+        if _gpu(x) and _stream_ok(x, w_qkv) and (ln_c is None or _ln_fold_fits(x, w_qkv.w)):
+            ext().skinny_gemm_qkv(x, w_qkv.t, bias, fuse_rms and ln_c is None, eps, n_q_heads, n_kv_heads, head_dim,
+                                  rope is not None, positions, slots, rope, q_out, k_cache, v_cache, None, ln_c, True)
+            return q_out[:M]
+        w_qkv = w_qkv.w
     if ln_c is not None:
         if _ln_fold_fits(x, w_qkv):
             ext().skinny_gemm_qkv(x, w_qkv, bias, False, eps, n_q_heads, n_kv_heads, head_dim, rope is not None,
