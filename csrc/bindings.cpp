@@ -221,6 +221,11 @@ int chain_pre2() {
   const char* e = std::getenv("VWA_CHAIN_PRE2");
   return e ? (std::atoi(e) != 0) : 1;
 }
+// VWA_CHAIN_NEXT0=0|1: phase 1's first item issued with a one-item phase 0 (ChainParams::next0)
+int chain_next0() {
+  const char* e = std::getenv("VWA_CHAIN_NEXT0");
+  return e ? (std::atoi(e) != 0) : 1;
+}
 
 // ---- chained decode layer tail (skinny_stream.hip, vwa_chain_*): descriptor built once on the
 // host and copied to a device tensor (graph replays then only launch); M <= 4, bf16, one GPU.
@@ -276,6 +281,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   cp.n = 3;
   cp.seq = 0;
   cp.pre2 = chain_pre2();
+  cp.next0 = chain_next0();
   if (w_qkv.has_value()) {
     TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
                     v_cache.has_value(),
@@ -367,6 +373,7 @@ std::tuple<Tensor, int64_t> chain_make_seq(int64_t seq, std::vector<Tensor> X, s
   cp.n = (int)n;
   cp.seq = (int)seq;
   cp.pre2 = chain_pre2();
+  cp.next0 = chain_next0();
   cp.bar = reinterpret_cast<unsigned*>(bar.data_ptr<int>());
   cp.bar_mode = (int)bar_mode;
   cp.tickets = reinterpret_cast<unsigned*>(work.data_ptr<int>());

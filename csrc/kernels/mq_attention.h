@@ -119,10 +119,16 @@ struct NoIdle {
 };
 
 // Returns true when this workgroup had no item (after calling on_idle(), before any barrier).
-template <int D, int G, int NW, bool SC1OUT, bool DB = true, class OnIdle = NoIdle>
+// FINE (the chained launch's attention phase): chunks are multiples of ONE 32-key step, the
+// steps of a chunk go to the waves round-robin, and the last arriver merges the chunks with two
+// threads per (query column, 8-dim slice), every partial load issued before any is used.  A lone
+// decode row then spreads its context over up to n_splits chunks (1100 keys: 12 workgroups of 96
+// keys per kv head instead of 5 of 256) -- the phase is latency-bound, each workgroup's K/V bytes
+// are its critical path.
+template <int D, int G, int NW, bool SC1OUT, bool DB = true, bool FINE = false, class OnIdle = NoIdle>
 VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid, int bid, OnIdle on_idle = {}) {
   constexpr int kWv = NW;
-  constexpr int kChunk = NW * kMqStep;     // chunk granularity (keys)
+  constexpr int kChunk = FINE ? kMqStep : NW * kMqStep;  // chunk granularity (keys)
   constexpr int RG = kMqCols / G;          // rows per group
   constexpr int NKS = D / 32;              // S^T k-steps over the head dim
   constexpr int NDT = D / 16;              // O^T dim tiles
@@ -150,7 +156,8 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   const int my_rank = __builtin_popcountll(leaders & ((1ull << lane) - 1ull));
   // chunks per (group, kv head): spread the work over the grid (one item per workgroup when it
   // fits), never more than the partial buffers hold
-  const int n_eff = max(1, min(p.n_splits, grid / max(1, n_groups * nkv)));
+  static_assert(!FINE || NW == 8, "the FINE merge pairs two threads per (column, slice): 512 threads");
+  const int n_eff = max(1, min(FINE ? min(p.n_splits, 16) : p.n_splits, grid / max(1, n_groups * nkv)));
   const int n_items = n_groups * nkv * n_eff;
   if (bid >= n_items) {
     on_idle();
@@ -181,8 +188,10 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   const int kbeg = chunk * CL;
   if (kbeg >= ctxmax) continue;
   const int nact = (ctxmax + CL - 1) / CL;
-  const int wb = kbeg + w * (CL / kWv);
-  const int we = min(ctxmax, wb + CL / kWv);
+  // non-FINE: wave w takes the contiguous CL / NW keys from wb; FINE: the chunk's 32-key steps
+  // round-robin over the waves (step s of the chunk -> wave s % NW)
+  const int wb = FINE ? kbeg : kbeg + w * (CL / kWv);
+  const int we = FINE ? min(ctxmax, kbeg + CL) : min(ctxmax, wb + CL / kWv);
   const int nsteps = we > wb ? (we - wb + kMqStep - 1) / kMqStep : 0;
   const int kmax = ctxmax - 1;  // keys past the context are clamped (finite data, masked scores)
 
@@ -289,7 +298,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
       }
     }
   } else {  // single register set (the chained launch holds the next GEMM's weights meanwhile)
-    for (int s = 0; s < nsteps; ++s) {
+    for (int s = FINE ? w : 0; s < nsteps; s += FINE ? kWv : 1) {
       uint4 kA[2][NKS], vA[NVL];
       load_step(wb + s * kMqStep, kA, vA);
       compute_step(wb + s * kMqStep, kA, vA);
@@ -360,6 +369,61 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   if (!s_last) continue;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // only orders the sc1 loads after the ticket
 
+  if constexpr (FINE) {
+    // ---- last arriver, FINE: two threads per (column, 8-dim slice) pair, each merging every
+    //      other chunk with all of its (<= n_splits / 2) partial loads in flight at once (clamped
+    //      indices, zero weight past nact), then the two halves combine through LDS
+    constexpr int MAXC = 8;  // chunks per thread: nact <= 2 * MAXC (host: n_splits <= 16)
+    const int pr = threadIdx.x & 255, hf = threadIdx.x >> 8;
+    const int pcn = pr >> 4, pdc = pr & 15;
+    const int prow = r0 + pcn / G, pch = kvh * G + pcn % G;
+    const bool pact = pcn / G < nr && pdc < NCH;
+    float pm = -INFINITY, pl = 0.f, pacc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pacc[j] = 0.f;
+    if (pact) {
+      const int64_t hb = (int64_t)prow * p.n_splits * nq + pch;
+      float2 ml[MAXC];
+      float4 x0[MAXC], x1[MAXC];
+#pragma unroll
+      for (int i = 0; i < MAXC; ++i) {
+        const int c = min(hf + 2 * i, nact - 1);
+        const int64_t b = hb + (int64_t)c * nq;
+        ml[i] = ld_sc1_f2(r_ml, b * 2);
+        x0[i] = ld_sc1_f4(r_o, b * D + 8 * pdc);
+        x1[i] = ld_sc1_f4(r_o, b * D + 8 * pdc + 4);
+      }
+#pragma unroll
+      for (int i = 0; i < MAXC; ++i)
+        if (hf + 2 * i < nact) pm = fmaxf(pm, ml[i].x);
+#pragma unroll
+      for (int i = 0; i < MAXC; ++i) {
+        const float f = (hf + 2 * i < nact && ml[i].x != -INFINITY) ? exp2f(ml[i].x - pm) : 0.f;
+        pl += ml[i].y * f;
+        pacc[0] += x0[i].x * f; pacc[1] += x0[i].y * f; pacc[2] += x0[i].z * f; pacc[3] += x0[i].w * f;
+        pacc[4] += x1[i].x * f; pacc[5] += x1[i].y * f; pacc[6] += x1[i].z * f; pacc[7] += x1[i].w * f;
+      }
+    }
+    float* xm = ow;  // reuse the per-wave O^T area: [256 pairs][10] floats of the second half
+    if (hf == 1) {
+      xm[pr * 10 + 0] = pm;
+      xm[pr * 10 + 1] = pl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xm[pr * 10 + 2 + j] = pacc[j];
+    }
+    __syncthreads();
+    if (hf == 0 && pact) {
+      const float om = xm[pr * 10 + 0];
+      const float M = fmaxf(pm, om);
+      const float fa = pm == -INFINITY ? 0.f : exp2f(pm - M), fb = om == -INFINITY ? 0.f : exp2f(om - M);
+      const float L = pl * fa + xm[pr * 10 + 1] * fb;
+      const float inv = L > 0.f ? 1.f / L : 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pacc[j] = (pacc[j] * fa + xm[pr * 10 + 2 + j] * fb) * inv;
+      store_out<SC1OUT>(p.out + (int64_t)prow * p.ldo + pch * D + 8 * pdc, pack8(pacc));
+    }
+    continue;
+  }
   // ---- last arriver: online merge of the nact chunks (sc1 loads only; measured: issuing the loads
   //      in unrolled batches of 8 chunks before combining was 2 us SLOWER in-bench, 13.6 vs 11.4 us)
   if (act) {

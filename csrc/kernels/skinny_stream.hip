@@ -734,6 +734,13 @@ VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[16], uint4 (
   if (pre2) chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U, WA>(ph.p, ph.nb, wr2, 1, r);
 }
 
+// one weight item `it` of a phase into wr (the next phase's item 0 / item 1, see chain_kernel)
+template <int EPI, int KS, int WA>
+VWA_DEVICE void chain_issue_item(const ChainPhase& ph, uint4 (&wr)[16], int it) {
+  const PhaseRange r = chain_range<KS>(ph);
+  chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U, WA>(ph.p, ph.nb, wr, it, r);
+}
+
 // partial tile of a split tile: cross-wave sums of this workgroup's units -> slot (sc1)
 template <int NT, int KS>
 VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
@@ -873,8 +880,9 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
     compute(X0, it);
     finish(it);
     if (it + 2 < n_pad) chain_load<NT, U, WA>(p, nb, X0, it + 2, r);
+    if (it + 1 >= r.n_items) break;  // padding item: no wait on it (X1 may hold the next phase's item 0)
     compute(X1, it + 1);
-    if (it + 1 < r.n_items) finish(it + 1);
+    finish(it + 1);
   }
 }
 
@@ -917,29 +925,43 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   constexpr int E0 = SeqEpi<SEQ, 0>::value, E1 = SeqEpi<SEQ, 1>::value, E2 = SeqEpi<SEQ, 2>::value,
                 E3 = SeqEpi<SEQ, 3>::value;
   int pre0 = cp.pre2;  // phase 0's pre-issued items: two, or one for a workgroup that ran attention
+  // Phase 0 with at most one item for this workgroup (o_proj at M <= 4 rows: one tile, one
+  // k-batch) never uses register set B, so B carries phase 1's first item from the start: it
+  // streams during the attention phase / the launch ramp, when HBM would otherwise idle.
+  const bool nx = cp.next0 && chain_range<KS>(cp.ph[0]).n_items <= 1;
+  // (phase 0 always runs on (B, A) and phase 1 on (A, B): one inlined copy of each phase body --
+  // swapping the sets per path measured 120 B of VGPR spills)
+  auto issue0 = [&](int pre) {
+    if (nx) {
+      chain_issue_item<E0, KS, WA>(cp.ph[0], B, 0);
+      chain_issue_item<E1, KS, WA>(cp.ph[1], A, 0);
+    } else {
+      chain_issue_first<E0, KS, WA>(cp.ph[0], B, A, pre);
+    }
+  };
   if constexpr (AG > 0) {
     // idle workgroups (no attention item) issue their o_proj weights at once; the others after
     // their item, at the barrier (one item: their attention registers were live until then)
-    const bool idle = mq_body<128, AG, KS, true, false>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
-                                                        (int)blockIdx.x,
-                                                        [&]() { chain_issue_first<E0, KS, WA>(cp.ph[0], A, B, pre0); });
+    const bool idle = mq_body<128, AG, KS, true, false, true>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
+                                                        (int)blockIdx.x, [&]() { issue0(pre0); });
     stamp();
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
     if (!idle) {
       pre0 = 0;
-      chain_issue_first<E0, KS, WA>(cp.ph[0], A, B, 0);
+      issue0(0);
     }
     chain_wait(bar, gen, cp.bar_mode);
   } else {
-    chain_issue_first<E0, KS, WA>(cp.ph[0], A, B, pre0);
+    issue0(pre0);
   }
-  chain_phase<E0, KS, WA>(cp, 0, A, B, smem, pre0);
+  chain_phase<E0, KS, WA>(cp, 0, B, A, smem, nx ? 1 : pre0);
   stamp();
   gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
-  chain_issue_first<E1, KS, WA>(cp.ph[1], A, B, cp.pre2);
+  if (nx) chain_issue_item<E1, KS, WA>(cp.ph[1], B, 1);  // phase 1's item 0 is already in A
+  else chain_issue_first<E1, KS, WA>(cp.ph[1], A, B, cp.pre2);
   chain_wait(bar, gen, cp.bar_mode);
   stamp();
-  chain_phase<E1, KS, WA>(cp, 1, A, B, smem, cp.pre2);
+  chain_phase<E1, KS, WA>(cp, 1, A, B, smem, nx ? 1 : cp.pre2);
   stamp();
   if constexpr (NPH >= 3) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);

@@ -188,7 +188,7 @@ class LlamaModel:
 
     def chain_descs(self):
         """Every cached descriptor entry over all live engines' buffers (tests / diagnostics)."""
-        return [v for d in getattr(self, "_chains", {}).values() for v in d.values()]
+        return [v for d in getattr(self, "_chains", {}).values() for k, v in d.items() if k[0] != "multi"]
 
     def _chain_desc(self, bufs, kv, M: int, li: int):
         """(descriptor, n_phases, lds) of layer li's chained tail for this engine's buffers,
