@@ -942,13 +942,19 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   if constexpr (AG > 0) {
     // idle workgroups (no attention item) issue their o_proj weights at once; the others after
     // their item, at the barrier (one item: their attention registers were live until then)
+    // cp.idle_pre: idle workgroups issue their first items during the attention (2, default) or
+    // only at the barrier (0)
     const bool idle = mq_body<128, AG, KS, true, false, true>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
-                                                        (int)blockIdx.x, [&]() { issue0(pre0); });
+                                                        (int)blockIdx.x, [&]() {
+                                                          if (cp.idle_pre) issue0(pre0);
+                                                        });
     stamp();
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
     if (!idle) {
       pre0 = 0;
       issue0(0);
+    } else if (!cp.idle_pre) {
+      issue0(pre0);
     }
     chain_wait(bar, gen, cp.bar_mode);
   } else {
