@@ -338,15 +338,19 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
     load_item(A, 0);
     if constexpr (XG) load_x(XA, 0);
   }
+  // the next item into a register set is issued right after that set's compute, BEFORE the tile
+  // epilogue, so two items stay in flight through every epilogue
+  load_item(B, 1);
+  if constexpr (XG) load_x(XB, 1);
   for (int it = 0; it < n_items; it += 2) {
-    load_item(B, it + 1);
-    if constexpr (XG) load_x(XB, it + 1);
     compute_item(A, XA, it);
-    if (it % nb == nb - 1) finish_tile(it);
-    if (it + 1 >= n_items) break;
     load_item(A, it + 2);
     if constexpr (XG) load_x(XA, it + 2);
+    if (it % nb == nb - 1) finish_tile(it);
+    if (it + 1 >= n_items) break;
     compute_item(B, XB, it + 1);
+    load_item(B, it + 3);
+    if constexpr (XG) load_x(XB, it + 3);
     if ((it + 1) % nb == nb - 1) finish_tile(it + 1);
   }
 }
@@ -874,15 +878,29 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
   };
   // items in pairs (X0, X1); an odd count is padded with one all-OOB item (zero weights, no
   // traffic, no epilogue)
+  // The next item into a set is issued right after that set's compute, before the epilogue, so
+  // two items stay in flight through every tile epilogue -- except after a split tile, whose
+  // publish drains vmcnt (it would wait for the new loads too).
   const int n_pad = (r.n_items + 1) & ~1;
+  auto split_end = [&](int it) -> bool {
+    if (it >= r.n_items) return false;
+    const int unit = r.u0 + it, tile = unit / nb;
+    if (unit % nb != nb - 1 && it != r.n_items - 1) return false;
+    return !(tile * nb >= r.u0 && (tile + 1) * nb <= u1);
+  };
+  if (!pre2) chain_load<NT, U, WA>(p, nb, X1, 1, r);
   for (int it = 0; it < n_pad; it += 2) {
-    if (it > 0 || !pre2) chain_load<NT, U, WA>(p, nb, X1, it + 1, r);
     compute(X0, it);
+    const bool e0 = !split_end(it);
+    if (e0 && it + 2 < n_pad) chain_load<NT, U, WA>(p, nb, X0, it + 2, r);
     finish(it);
-    if (it + 2 < n_pad) chain_load<NT, U, WA>(p, nb, X0, it + 2, r);
+    if (!e0 && it + 2 < n_pad) chain_load<NT, U, WA>(p, nb, X0, it + 2, r);
     if (it + 1 >= r.n_items) break;  // padding item: no wait on it (X1 may hold the next phase's item 0)
     compute(X1, it + 1);
+    const bool e1 = !split_end(it + 1);
+    if (e1 && it + 3 < n_pad) chain_load<NT, U, WA>(p, nb, X1, it + 3, r);
     finish(it + 1);
+    if (!e1 && it + 3 < n_pad) chain_load<NT, U, WA>(p, nb, X1, it + 3, r);
   }
 }
 
