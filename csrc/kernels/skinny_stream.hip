@@ -766,9 +766,15 @@ VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
   __syncthreads();
 }
 
-// One phase.  X0 holds this phase's item 0 (issued before the barrier wait).
+// One phase.  X0 holds this phase's item 0 (issued before the barrier wait), X1 item 1 when pre2.
+// cp.xdma: the LAST wave stages X alone, by LDS-DMA (no registers, all pieces in flight at once),
+// and issues no weights at the barrier -- its vmcnt queue is empty, so the X round trip is not
+// queued behind weight loads; the other waves issue their item 1 at once (pre2 == 0: one item at
+// the barrier), which streams while the X rows arrive.  hs = items the staging wave has already
+// issued into (X0, X1).
 template <int EPI, int KS, int WA>
-VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4 (&X1)[16], char* smem, int pre2) {
+VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4 (&X1)[16], char* smem, int pre2,
+                            int hs = 0) {
   constexpr int NT = PhaseShape<EPI>::NT, U = PhaseShape<EPI>::U;
   const ChainPhase& ph = cp.ph[i];
   const SkinnyParams& p = ph.p;
@@ -785,6 +791,8 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
   const int nl = lane & 15, g = lane >> 4;
   const PhaseRange r = chain_range<KS>(ph);
   const int first_tile = r.u0 / nb;
+  const bool xdma = cp.xdma != 0, stager = xdma && w == KS - 1;
+  if (xdma && !stager && !pre2) chain_load<NT, U, WA>(p, nb, X1, 1, r);  // streams during the staging
 
   EpiPre pre;
   if (r.n_items > 0) epi_values<EPI, NT, true>(p, first_tile, threadIdx.x, pre);
@@ -792,10 +800,34 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
   const int k8 = K / 8;
   const __amdgpu_buffer_rsrc_t rx =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.X), (short)0, (int)((size_t)M * p.ldx * 2), 0x00020000);
-  for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
-    const int m = c / k8, kk = c % k8;
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(((size_t)m * p.ldx + kk * 8) * 2), 0, 16);
-    *reinterpret_cast<uint4*>(xs + m * xstride + kk * 8) = make_uint4(v.x, v.y, v.z, v.w);
+  if (stager) {
+    // 1 KB pieces (512 bf16 of one row) straight into the padded LDS rows, sc1 (coherent) reads
+    const int pieces = K / 512;
+    for (int m = 0; m < M; ++m)
+      for (int j = 0; j < pieces; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rx, (__attribute__((address_space(3))) void*)(xs + m * xstride + j * 512), 16,
+            (unsigned)(((size_t)m * p.ldx + j * 512) * 2 + lane * 16), 0, 0, 16);
+    asm volatile("" ::: "memory");  // keep the weight loads below younger than the pieces
+    int nw = 0;
+    if (hs < 1) {
+      chain_load<NT, U, WA>(p, nb, X0, 0, r);
+      ++nw;
+    }
+    if (hs < 2) {
+      chain_load<NT, U, WA>(p, nb, X1, 1, r);
+      ++nw;
+    }
+    // the pieces are older than the nw weight items (16 loads each): wait for them only
+    if (nw == 2) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if (nw == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (!xdma) {
+    for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
+      const int m = c / k8, kk = c % k8;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(((size_t)m * p.ldx + kk * 8) * 2), 0, 16);
+      *reinterpret_cast<uint4*>(xs + m * xstride + kk * 8) = make_uint4(v.x, v.y, v.z, v.w);
+    }
   }
   __syncthreads();
   for (int m = w; m < 16; m += KS) {
@@ -888,7 +920,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
     if (unit % nb != nb - 1 && it != r.n_items - 1) return false;
     return !(tile * nb >= r.u0 && (tile + 1) * nb <= u1);
   };
-  if (!pre2) chain_load<NT, U, WA>(p, nb, X1, 1, r);
+  if (!pre2 && !xdma) chain_load<NT, U, WA>(p, nb, X1, 1, r);
   for (int it = 0; it < n_pad; it += 2) {
     compute(X0, it);
     const bool e0 = !split_end(it);
@@ -978,29 +1010,35 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   } else {
     issue0(pre0);
   }
-  chain_phase<E0, KS, WA>(cp, 0, B, A, smem, nx ? 1 : pre0);
+  // cp.xdma: the staging wave issues nothing at the barriers (chain_phase), the others one item
+  // (their second follows right at the release)
+  const bool stg = cp.xdma && (threadIdx.x >> 6) == KS - 1;
+  const int preb = cp.xdma ? 0 : cp.pre2;
+  chain_phase<E0, KS, WA>(cp, 0, B, A, smem, nx ? 1 : pre0, 2);
   stamp();
   gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
-  if (nx) chain_issue_item<E1, KS, WA>(cp.ph[1], B, 1);  // phase 1's item 0 is already in A
-  else chain_issue_first<E1, KS, WA>(cp.ph[1], A, B, cp.pre2);
+  if (!stg) {
+    if (nx) chain_issue_item<E1, KS, WA>(cp.ph[1], B, 1);  // phase 1's item 0 is already in A
+    else chain_issue_first<E1, KS, WA>(cp.ph[1], A, B, preb);
+  }
   chain_wait(bar, gen, cp.bar_mode);
   stamp();
-  chain_phase<E1, KS, WA>(cp, 1, A, B, smem, nx ? 1 : cp.pre2);
+  chain_phase<E1, KS, WA>(cp, 1, A, B, smem, nx ? 1 : preb, nx ? 1 : 0);
   stamp();
   if constexpr (NPH >= 3) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
-    chain_issue_first<E2, KS, WA>(cp.ph[2], A, B, cp.pre2);
+    if (!stg) chain_issue_first<E2, KS, WA>(cp.ph[2], A, B, preb);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E2, KS, WA>(cp, 2, A, B, smem, cp.pre2);
+    chain_phase<E2, KS, WA>(cp, 2, A, B, smem, preb, 0);
     stamp();
   }
   if constexpr (NPH >= 4) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
-    chain_issue_first<E3, KS, WA>(cp.ph[3], A, B, cp.pre2);
+    if (!stg) chain_issue_first<E3, KS, WA>(cp.ph[3], A, B, preb);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E3, KS, WA>(cp, 3, A, B, smem, cp.pre2);
+    chain_phase<E3, KS, WA>(cp, 3, A, B, smem, preb, 0);
     stamp();
   }
 }
@@ -1042,6 +1080,9 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     if (need > lds) lds = need;
   }
   if (lds > 160 * 1024) return -10;
+  // LDS-DMA staging moves whole 1 KB pieces of a row (512 bf16): only for K % 512 == 0 phases
+  for (int i = 0; i < cp->n; ++i)
+    if (cp->ph[i].p.K % 512 != 0) cp->xdma = 0;
   return (int)lds;
 }
 

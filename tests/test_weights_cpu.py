@@ -165,3 +165,27 @@ def test_whisper_safetensors_load(tmp_path):
     mel = ref.log_mel(torch.zeros(16000))
     enc = m.encode(mel[None])
     assert enc.shape == (1, cfg.n_audio_ctx, d) and torch.isfinite(enc.float()).all()
+
+
+def test_tiled_weight_layout_and_cpu_routing():
+    """ops.tile_weight: the 4 KB block of (16-row tile T, 128-wide k-group kg) holds, at [s][lane][e],
+    W[16 T + lane % 16][128 kg + 32 (lane // 16) + 8 s + e] (the MFMA B fragments in wave-load
+    order, vwa_kernels.h SkinnyParams::w_tiled); untile_weight inverts it; CPU ops on a TiledWeight
+    use its row-major copy."""
+    from voice_enabled_browser_automation_amd import ops
+    from voice_enabled_browser_automation_amd.ops import reference as ref
+
+    torch.manual_seed(0)
+    w = torch.randn(48, 384).to(torch.bfloat16)
+    t = ops.tile_weight(w)
+    assert t.shape == w.shape and torch.equal(ops.untile_weight(t), w)
+    blk = t.reshape(-1).view(48 // 16, 384 // 128, 4, 64, 8)
+    for T, kg, s, lane, e in [(0, 0, 0, 0, 0), (2, 1, 3, 63, 7), (1, 2, 2, 17, 4)]:
+        assert blk[T, kg, s, lane, e] == w[16 * T + lane % 16, 128 * kg + 32 * (lane // 16) + 8 * s + e]
+    tw = ops.TiledWeight(w)
+    x = torch.randn(3, 384).to(torch.bfloat16)
+    out = ops.linear(x, tw, fuse_rms=True)
+    exp = torch.empty(3, 48, dtype=torch.bfloat16)
+    ref.linear(x, w, None, out=exp, fuse_rms=True)
+    assert torch.equal(out, exp)
+    assert tw.numel() == w.numel() and tw.shape == w.shape

@@ -86,6 +86,8 @@ class StepBuffers:
         self.h_i32 = self.h_meta[: 4 * R].view(4, R)
         self.h_slots = self.h_meta[4 * R : 6 * R].view(torch.int64)
         self.h_sel = self.h_meta[6 * R :]
+        self.h_i32[3].fill_(1)  # the same inert rows as the device copy (captured graphs upload it)
+        self.h_slots.fill_(-1)
         self.h_table = torch.zeros(max_seqs, max_blocks_per_seq, dtype=torch.int32, pin_memory=pin)
         self.table_dirty = True
         # numpy views of the pinned staging buffers: the per-step row metadata is written with a
@@ -95,11 +97,13 @@ class StepBuffers:
         self.np_sel = self.h_sel.numpy()
         self.np_table = self.h_table.numpy()
 
-    def upload(self, n_rows: int) -> None:
-        nb = True
-        self.meta.copy_(self.h_meta, non_blocking=nb)
+    def upload(self, n_rows: int, meta: bool = True) -> None:
+        """H2D copy of the step metadata (skipped when the replayed graph contains it) and of the
+        block table when it changed."""
+        if meta:
+            self.meta.copy_(self.h_meta, non_blocking=True)
         if self.table_dirty:
-            self.block_table.copy_(self.h_table, non_blocking=nb)
+            self.block_table.copy_(self.h_table, non_blocking=True)
             self.table_dirty = False
 
 
@@ -180,7 +184,11 @@ class LLMEngine:
         return seq.blocks[pos // self.block_size] * self.block_size + pos % self.block_size
 
     # ------------------------------------------------------------------ forward
-    def _forward_rows(self, M: int, L: int) -> torch.Tensor:
+    def _forward_rows(self, M: int, L: int, upload_meta: bool = False) -> torch.Tensor:
+        if upload_meta:
+            # inside a captured graph: the pinned -> device metadata copy is the graph's first node,
+            # so a replay is one host call instead of a copy + a replay
+            self.bufs.meta.copy_(self.bufs.h_meta, non_blocking=True)
         return self.model.forward(self.bufs, M, self.kv, n_sel=None if L == M else L)
 
     def _capture(self, M: int, L: int):
@@ -188,13 +196,13 @@ class LLMEngine:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(2):
-                self._forward_rows(M, L)
+                self._forward_rows(M, L, upload_meta=True)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
         if self.graph_pool is None:
             self.graph_pool = torch.cuda.graph_pool_handle()
         with torch.cuda.graph(g, pool=self.graph_pool):
-            out = self._forward_rows(M, L)
+            out = self._forward_rows(M, L, upload_meta=True)
         self.graphs[(M, L)] = (g, out)
         return self.graphs[(M, L)]
 
@@ -264,7 +272,7 @@ class LLMEngine:
             hi[0:3, n:M] = 0
             hi[3, n:M] = 1
             b.np_slots[n:M] = -1
-        b.upload(M)
+        b.upload(M, meta=not self.use_graphs)  # the step graphs copy the metadata themselves
         chained = self._uses_chain(M)
         self._last_step = (list(rows), logits_for, {sid: self.seqs[sid].n_computed for sid in pending}) \
             if chained else None
