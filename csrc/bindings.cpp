@@ -231,6 +231,11 @@ int chain_xdma() {
   const char* e = std::getenv("VWA_CHAIN_XDMA");
   return e ? (std::atoi(e) != 0) : 1;
 }
+// VWA_CHAIN_OSUB=0|1: o_proj units only on the workgroups without an attention item (ChainParams::osub)
+int chain_osub() {
+  const char* e = std::getenv("VWA_CHAIN_OSUB");
+  return e ? (std::atoi(e) != 0) : 1;
+}
 // VWA_CHAIN_NEXT0=0|1: phase 1's first item issued with a one-item phase 0 (ChainParams::next0)
 int chain_next0() {
   const char* e = std::getenv("VWA_CHAIN_NEXT0");
@@ -294,6 +299,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   cp.next0 = chain_next0();
   cp.idle_pre = chain_idle_pre();
   cp.xdma = chain_xdma();
+  cp.osub = chain_osub();
   if (w_qkv.has_value()) {
     TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
                     v_cache.has_value(),
@@ -388,6 +394,7 @@ std::tuple<Tensor, int64_t> chain_make_seq(int64_t seq, std::vector<Tensor> X, s
   cp.next0 = chain_next0();
   cp.idle_pre = chain_idle_pre();
   cp.xdma = chain_xdma();
+  cp.osub = chain_osub();
   cp.bar = reinterpret_cast<unsigned*>(bar.data_ptr<int>());
   cp.bar_mode = (int)bar_mode;
   cp.tickets = reinterpret_cast<unsigned*>(work.data_ptr<int>());

@@ -125,8 +125,11 @@ struct NoIdle {
 // decode row then spreads its context over up to n_splits chunks (1100 keys: 12 workgroups of 96
 // keys per kv head instead of 5 of 256) -- the phase is latency-bound, each workgroup's K/V bytes
 // are its critical path.
+// n_items_out (optional): the step's attention item count (the same in every workgroup), set
+// before on_idle runs.
 template <int D, int G, int NW, bool SC1OUT, bool DB = true, bool FINE = false, class OnIdle = NoIdle>
-VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid, int bid, OnIdle on_idle = {}) {
+VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid, int bid, OnIdle on_idle = {},
+                        int* n_items_out = nullptr) {
   constexpr int kWv = NW;
   constexpr int kChunk = FINE ? kMqStep : NW * kMqStep;  // chunk granularity (keys)
   constexpr int RG = kMqCols / G;          // rows per group
@@ -159,6 +162,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   static_assert(!FINE || NW == 8, "the FINE merge pairs two threads per (column, slice): 512 threads");
   const int n_eff = max(1, min(FINE ? min(p.n_splits, 16) : p.n_splits, grid / max(1, n_groups * nkv)));
   const int n_items = n_groups * nkv * n_eff;
+  if (n_items_out) *n_items_out = n_items;
   if (bid >= n_items) {
     on_idle();
     return true;

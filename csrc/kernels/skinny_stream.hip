@@ -675,16 +675,24 @@ struct PhaseRange {
   int u0, n_items, gb, ge;
 };
 
+// wb0 / wn: the phase's units go to the wn workgroups [wb0, wb0 + wn) (others get none); wn = 0:
+// every workgroup
 template <int KS>
-VWA_DEVICE PhaseRange chain_range(const ChainPhase& ph) {
+VWA_DEVICE PhaseRange chain_range(const ChainPhase& ph, int wb0 = 0, int wn = 0) {
   PhaseRange r;
   const int w = threadIdx.x >> 6;
   const int G = ph.p.K / 128;
   r.gb = (G * w) / KS;
   r.ge = (G * (w + 1)) / KS;
   const long long units = (long long)(ph.p.N / (16 * ph.nt)) * ph.nb;
-  r.u0 = (int)(units * blockIdx.x / gridDim.x);
-  r.n_items = (int)(units * (blockIdx.x + 1) / gridDim.x) - r.u0;
+  const long long n = wn > 0 ? wn : (long long)gridDim.x, b = (long long)blockIdx.x - wb0;
+  if (b < 0 || b >= n) {
+    r.u0 = 0;
+    r.n_items = 0;
+    return r;
+  }
+  r.u0 = (int)(units * b / n);
+  r.n_items = (int)(units * (b + 1) / n) - r.u0;
   return r;
 }
 
@@ -732,16 +740,17 @@ struct PhaseShape {
 // the phase's first weight item (and with pre2 its second) before the barrier wait: a
 // workgroup that arrives early keeps HBM busy while the grid catches up
 template <int EPI, int KS, int WA>
-VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[16], uint4 (&wr2)[16], int pre2) {
-  const PhaseRange r = chain_range<KS>(ph);
+VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[16], uint4 (&wr2)[16], int pre2, int wb0 = 0,
+                                  int wn = 0) {
+  const PhaseRange r = chain_range<KS>(ph, wb0, wn);
   chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U, WA>(ph.p, ph.nb, wr, 0, r);
   if (pre2) chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U, WA>(ph.p, ph.nb, wr2, 1, r);
 }
 
 // one weight item `it` of a phase into wr (the next phase's item 0 / item 1, see chain_kernel)
 template <int EPI, int KS, int WA>
-VWA_DEVICE void chain_issue_item(const ChainPhase& ph, uint4 (&wr)[16], int it) {
-  const PhaseRange r = chain_range<KS>(ph);
+VWA_DEVICE void chain_issue_item(const ChainPhase& ph, uint4 (&wr)[16], int it, int wb0 = 0, int wn = 0) {
+  const PhaseRange r = chain_range<KS>(ph, wb0, wn);
   chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U, WA>(ph.p, ph.nb, wr, it, r);
 }
 
@@ -774,7 +783,7 @@ VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
 // issued into (X0, X1).
 template <int EPI, int KS, int WA>
 VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4 (&X1)[16], char* smem, int pre2,
-                            int hs = 0) {
+                            int hs = 0, int wb0 = 0, int wn = 0) {
   constexpr int NT = PhaseShape<EPI>::NT, U = PhaseShape<EPI>::U;
   const ChainPhase& ph = cp.ph[i];
   const SkinnyParams& p = ph.p;
@@ -789,7 +798,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
   const float* mus = p.fuse_rms == 2 ? mu : nullptr;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nl = lane & 15, g = lane >> 4;
-  const PhaseRange r = chain_range<KS>(ph);
+  const PhaseRange r = chain_range<KS>(ph, wb0, wn);
   const int first_tile = r.u0 / nb;
   const bool xdma = cp.xdma != 0, stager = xdma && w == KS - 1;
   if (xdma && !stager && !pre2) chain_load<NT, U, WA>(p, nb, X1, 1, r);  // streams during the staging
@@ -975,18 +984,28 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   constexpr int E0 = SeqEpi<SEQ, 0>::value, E1 = SeqEpi<SEQ, 1>::value, E2 = SeqEpi<SEQ, 2>::value,
                 E3 = SeqEpi<SEQ, 3>::value;
   int pre0 = cp.pre2;  // phase 0's pre-issued items: two, or one for a workgroup that ran attention
+  // Phase-0 window (cp.osub, attention launches): the o_proj units go only to the workgroups that
+  // get no attention item -- they stream their o_proj weights during the attention, while an
+  // attention workgroup loads its share only after it (measured on the critical path).
+  int ob0 = 0, on = 0;
   // Phase 0 with at most one item for this workgroup (o_proj at M <= 4 rows: one tile, one
   // k-batch) never uses register set B, so B carries phase 1's first item from the start: it
   // streams during the attention phase / the launch ramp, when HBM would otherwise idle.
-  const bool nx = cp.next0 && chain_range<KS>(cp.ph[0]).n_items <= 1;
+  bool nx = false;
+  auto setup0 = [&](int n_attn) {
+    const bool sub = cp.osub && n_attn > 0 && n_attn <= nwg / 2;
+    ob0 = sub ? n_attn : 0;
+    on = sub ? nwg - n_attn : 0;
+    nx = cp.next0 && chain_range<KS>(cp.ph[0], ob0, on).n_items <= 1;
+  };
   // (phase 0 always runs on (B, A) and phase 1 on (A, B): one inlined copy of each phase body --
   // swapping the sets per path measured 120 B of VGPR spills)
   auto issue0 = [&](int pre) {
     if (nx) {
-      chain_issue_item<E0, KS, WA>(cp.ph[0], B, 0);
+      chain_issue_item<E0, KS, WA>(cp.ph[0], B, 0, ob0, on);
       chain_issue_item<E1, KS, WA>(cp.ph[1], A, 0);
     } else {
-      chain_issue_first<E0, KS, WA>(cp.ph[0], B, A, pre);
+      chain_issue_first<E0, KS, WA>(cp.ph[0], B, A, pre, ob0, on);
     }
   };
   if constexpr (AG > 0) {
@@ -994,10 +1013,13 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     // their item, at the barrier (one item: their attention registers were live until then)
     // cp.idle_pre: idle workgroups issue their first items during the attention (2, default) or
     // only at the barrier (0)
+    int n_attn = 0;
     const bool idle = mq_body<128, AG, KS, true, false, true>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
                                                         (int)blockIdx.x, [&]() {
+                                                          setup0(n_attn);
                                                           if (cp.idle_pre) issue0(pre0);
-                                                        });
+                                                        }, &n_attn);
+    if (!idle) setup0(n_attn);
     stamp();
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
     if (!idle) {
@@ -1008,13 +1030,14 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     }
     chain_wait(bar, gen, cp.bar_mode);
   } else {
+    setup0(0);
     issue0(pre0);
   }
   // cp.xdma: the staging wave issues nothing at the barriers (chain_phase), the others one item
   // (their second follows right at the release)
   const bool stg = cp.xdma && (threadIdx.x >> 6) == KS - 1;
   const int preb = cp.xdma ? 0 : cp.pre2;
-  chain_phase<E0, KS, WA>(cp, 0, B, A, smem, nx ? 1 : pre0, 2);
+  chain_phase<E0, KS, WA>(cp, 0, B, A, smem, nx ? 1 : pre0, 2, ob0, on);
   stamp();
   gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
   if (!stg) {

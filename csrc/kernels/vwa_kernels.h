@@ -75,6 +75,7 @@ struct ChainParams {
   int next0;               // phase 1's item 0 rides in the register set a 1-item phase 0 leaves free
   int idle_pre;            // weight items idle workgroups issue during the attention phase (0..2)
   int xdma;                // X staged by one wave with LDS-DMA while the others stream (chain_phase)
+  int osub;                // attention launches: phase 0 only on the workgroups without an attention item
   unsigned* bar;
   int bar_mode;            // 0: flat ticket counter, 1: two-level (8 groups + top), 2: two-level + scalar polls
   float* part;             // split-tile partial slots [max_tiles][2][M][16*nt] f32
