@@ -270,7 +270,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                                        int64_t a_st, c10::optional<Tensor> a_ctx, c10::optional<Tensor> a_seq,
                                        double a_scale, int64_t a_n_splits, c10::optional<Tensor> a_part_o,
                                        c10::optional<Tensor> a_part_ml, c10::optional<Tensor> a_counters,
-                                       bool w_tiled) {
+                                       bool w_tiled, c10::optional<Tensor> a_row_table) {
   c10::DeviceGuard g(h.device());
   const int64_t M = h.size(0);
   TORCH_CHECK(att.size(0) == M && act.size(0) == M, "row counts differ");
@@ -333,6 +333,14 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                             n_kv_heads, head_dim, a_scale, a_n_splits, *a_part_o, *a_part_ml, *a_counters, att);
     TORCH_CHECK(a_n_splits > 1, "attention phase: the in-launch chunk merge needs n_splits > 1");
     cp.attn_g = (int)(n_q_heads / n_kv_heads);
+    if (a_row_table.has_value()) {
+      const Tensor& rtab = *a_row_table;
+      TORCH_CHECK(rtab.is_cuda() && rtab.scalar_type() == at::kInt && rtab.dim() == 2 && rtab.is_contiguous() &&
+                      rtab.size(0) >= M && rtab.size(1) <= 128 && rtab.size(1) % 2 == 0,
+                  "a_row_table must be int32 [>= rows, <= 128 (even)] contiguous");
+      cp.attn.row_table = rtab.data_ptr<int>();
+      cp.attn.rt_stride = (int)rtab.size(1);
+    }
   }
   int cus = 0;
   TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h.device().index()) == hipSuccess,
@@ -785,7 +793,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_table") = py::none(), py::arg("a_block_size") = 0, py::arg("a_sb") = 0, py::arg("a_sh") = 0,
         py::arg("a_st") = 0, py::arg("a_ctx") = py::none(), py::arg("a_seq") = py::none(), py::arg("a_scale") = 0.0,
         py::arg("a_n_splits") = 0, py::arg("a_part_o") = py::none(), py::arg("a_part_ml") = py::none(),
-        py::arg("a_counters") = py::none(), py::arg("w_tiled") = false);
+        py::arg("a_counters") = py::none(), py::arg("w_tiled") = false, py::arg("a_row_table") = py::none());
   m.def("set_small_gemm_bytes", &set_small_gemm_bytes);
   m.def("chain_make_seq", &chain_make_seq, py::arg("seq"), py::arg("X"), py::arg("W"), py::arg("bias"),
         py::arg("ln_c"), py::arg("Y"), py::arg("epi"), py::arg("eps"), py::arg("n_heads"), py::arg("head_dim"),

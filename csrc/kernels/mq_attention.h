@@ -117,6 +117,9 @@ struct MqLds {
 struct NoIdle {
   VWA_DEVICE void operator()() const {}
 };
+struct NoStamp {
+  VWA_DEVICE void operator()(int) const {}
+};
 
 // Returns true when this workgroup had no item (after calling on_idle(), before any barrier).
 // FINE (the chained launch's attention phase): chunks are multiples of ONE 32-key step, the
@@ -127,9 +130,11 @@ struct NoIdle {
 // are its critical path.
 // n_items_out (optional): the step's attention item count (the same in every workgroup), set
 // before on_idle runs.
-template <int D, int G, int NW, bool SC1OUT, bool DB = true, bool FINE = false, class OnIdle = NoIdle>
+// stamp(k) (diagnostic, tools/chain_probe.py --attn): in-body timestamps 9..14 of the first item
+template <int D, int G, int NW, bool SC1OUT, bool DB = true, bool FINE = false, class OnIdle = NoIdle,
+          class Stamp = NoStamp>
 VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid, int bid, OnIdle on_idle = {},
-                        int* n_items_out = nullptr) {
+                        int* n_items_out = nullptr, Stamp stamp = {}) {
   constexpr int kWv = NW;
   constexpr int kChunk = FINE ? kMqStep : NW * kMqStep;  // chunk granularity (keys)
   constexpr int RG = kMqCols / G;          // rows per group
@@ -149,6 +154,14 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
 
   // ---- row groups of the whole step (<= 64 rows; every wave derives the same answer): runs of
   //      consecutive rows of one sequence, cut every RG rows from the run's start
+  // per-row block tables (FINE, <= 4 rows): fetched with the sequence ids, two entries per lane
+  const bool rowtab = FINE && p.row_table != nullptr && p.rows <= 4;
+  int2 rt[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    rt[r] = (rowtab && r < p.rows && 2 * lane < p.rt_stride)
+                ? *reinterpret_cast<const int2*>(p.row_table + r * p.rt_stride + 2 * lane)
+                : make_int2(0, 0);
   const int sl = lane < p.rows ? p.seq_ids[lane] : -1;
   const int cl = lane < p.rows ? p.ctx_lens[lane] : 0;  // same round trip as the sequence ids
   const int sp = __shfl(sl, lane > 0 ? lane - 1 : 0, 64);
@@ -179,6 +192,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   const int nr = min(RG, run_end - r0);  // rows in this group
   const int seq = __shfl(sl, r0, 64);
   __syncthreads();  // the previous item's LDS readers are done
+  if (item == bid) stamp(9);  // step rows / contexts known
   const int c_src = __shfl(cl, min(r0 + lane, 63), 64);
   const int c_own = lane < nr ? c_src : 0;
   int ctxmax = c_own;
@@ -214,9 +228,20 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
     }
   }
 
+  if (item == bid) stamp(10);  // q fragments in registers
   // (measured: staging the wave's block-table entries in lanes and fetching them with __shfl,
   // instead of the per-key table loads below, was 1.5-3 us SLOWER on every shape)
-  auto kv_off = [&](int key) -> int64_t { return kv_offset(p.kv, seq, kvh, key); };
+  const int2 rtr = r0 == 0 ? rt[0] : r0 == 1 ? rt[1] : r0 == 2 ? rt[2] : rt[3];  // the group's row table
+  auto kv_off = [&](int key) -> int64_t {
+    if (rowtab) {
+      const int b = key / p.kv.block_size;
+      const int ex = __shfl(rtr.x, b >> 1, 64), ey = __shfl(rtr.y, b >> 1, 64);
+      const int blk = (b & 1) ? ey : ex;
+      return (int64_t)blk * p.kv.stride_block + (int64_t)kvh * p.kv.stride_head +
+             (int64_t)(key % p.kv.block_size) * p.kv.stride_tok;
+    }
+    return kv_offset(p.kv, seq, kvh, key);
+  };
 
   // K: A-operand row n of tile t is key kb + 8(n>>2) + 4t + (n&3) (so the S^T accumulator of lane
   // (n, g) holds keys kb + 8g + 4t + i); V: 32 rows x NCH chunks, chunk idx = i*64 + lane
@@ -309,6 +334,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
     }
   }
 
+  if (item == bid) stamp(11);  // K/V of the wave's steps consumed
   // ---- per-wave (m, l, O) -> LDS; O^T accumulator of lane (n, g): dims 16dt + 4g + i
   float l_tot = l_run + __shfl_xor(l_run, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
@@ -361,6 +387,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
 
   // ---- ticket (same protocol as the split kernel): drained sc1 stores, then one counter add
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (item == bid) stamp(12);  // partials stored
   __syncthreads();
   if (threadIdx.x == 0) {
     int* cnt = p.counters + r0 * nkv + kvh;
@@ -371,6 +398,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   }
   __syncthreads();
   if (!s_last) continue;
+  if (item == bid) stamp(13);  // last arriver known
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // only orders the sc1 loads after the ticket
 
   if constexpr (FINE) {
@@ -426,6 +454,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
       for (int j = 0; j < 8; ++j) pacc[j] = (pacc[j] * fa + xm[pr * 10 + 2 + j] * fb) * inv;
       store_out<SC1OUT>(p.out + (int64_t)prow * p.ldo + pch * D + 8 * pdc, pack8(pacc));
     }
+    if (item == bid) stamp(14);  // merged output stored (issued)
     continue;
   }
   // ---- last arriver: online merge of the nact chunks (sc1 loads only; measured: issuing the loads

@@ -1018,7 +1018,10 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                         (int)blockIdx.x, [&]() {
                                                           setup0(n_attn);
                                                           if (cp.idle_pre) issue0(pre0);
-                                                        }, &n_attn);
+                                                        }, &n_attn, [&](int k) {
+                                                          if (cp.ts && threadIdx.x == 0)
+                                                            cp.ts[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memrealtime();
+                                                        });
     if (!idle) setup0(n_attn);
     stamp();
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);

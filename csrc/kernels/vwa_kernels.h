@@ -56,6 +56,9 @@ struct DecodeAttnParams {
   float* part_o; float* part_ml;    // [rows][n_splits][n_q_heads][D], [rows][n_splits][n_q_heads][2]
   int* counters;                    // [rows * n_kv_heads] chunk tickets, zero between launches
   uint16_t* out; int ldo;           // [rows, n_q_heads*D]
+  // optional (chained attention, <= 4 rows): the block table of each ROW's sequence, [rows][rt_stride
+  // <= 128] -- read in the same round trip as seq_ids / ctx_lens (no dependent table load)
+  const int* row_table; int rt_stride;
 };
 
 // Chained decode GEMM phases in one persistent launch (skinny_stream.hip, vwa_chain): each phase

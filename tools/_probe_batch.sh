@@ -1,7 +1,6 @@
-set -e
-timeout -k 10 500 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/t_osub.log 2>&1
-for x in 1 0; do for r in 1 4; do
-  VWA_CHAIN_OSUB=$x timeout -k 10 120 python tools/chain_probe.py --rows $r --attn --json gpurun_out/probe11_o$x.jsonl
-done; done
-timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_osub.log 2>&1
-VWA_CHAIN_OSUB=0 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_osub0.log 2>&1
+timeout -k 10 200 python tools/_dbg_rt.py > gpurun_out/dbg_rt.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/t_rt.log 2>&1
+for rt in "--row-table" "" "--row-table" ""; do
+  timeout -k 10 120 python tools/chain_probe.py --rows 1 --attn $rt --json gpurun_out/probe14.jsonl
+done
+exit 0

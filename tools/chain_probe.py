@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--wpol", type=int, default=0, help="weight-load cache policy: 0 default, 2 nt")
     ap.add_argument("--no-wait", action="store_true",
                     help="DIAGNOSTIC: barriers arrive but never wait (wrong results): phase cost without dependencies")
+    ap.add_argument("--row-table", action="store_true", help="attention: per-row block tables (a_row_table)")
     ap.add_argument("--row-major", dest="tiled", action="store_false",
                     help="row-major [N, K] weights instead of the pre-tiled layout (ops.tile_weight)")
     a = ap.parse_args()
@@ -63,6 +64,10 @@ def main():
                    a_part_o=torch.zeros(M * ns * nq * hd, device=dev), a_part_ml=torch.zeros(M * ns * nq * 2, device=dev),
                    a_counters=torch.zeros(M * nkv, dtype=torch.int32, device=dev))
         ag = nq // nkv
+        if a.row_table:  # per-row copies of the sequence's block table (one table round trip less)
+            rt = torch.zeros(M, 128, dtype=torch.int32, device=dev)
+            rt[:, :nblk] = table[0]
+            akw["a_row_table"] = rt
     if a.tiled:  # the descriptors hold raw pointers: keep the tiled copies alive in Ws
         for w in Ws:
             w.update({k + "_t": ops.tile_weight(w[k]) for k in ("o", "gu", "down", "qkv")})
@@ -104,10 +109,23 @@ def main():
     med = st.median(dim=0).values.tolist()
     mx = st.max(dim=0).values.tolist()
     mn = st.min(dim=0).values.tolist()
-    r = dict(kernel="chain_probe", rows=M, bar_mode=a.bar_mode, wpol=a.wpol, tiled=a.tiled, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
+    if a.attn:  # in-attention stamps 9..14 of the attention workgroups (slots stay 0 elsewhere)
+        full = ts.view(-1, 16)[:cus].double().cpu()
+        t0 = full[:, 0].min()
+        att = full[full[:, 11] > 0]
+        names = ["ctx_known", "q_ready", "kv_done", "partials_stored", "last_known", "merged"]
+        extra = {}
+        for j, nm in enumerate(names):
+            col = att[:, 9 + j]
+            col = col[col > 0]
+            if col.numel():
+                extra[nm] = [round(float((col.median() - t0) * 10e-3), 2), round(float((col.max() - t0) * 10e-3), 2)]
+    r = dict(kernel="chain_probe", rows=M, bar_mode=a.bar_mode, wpol=a.wpol, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
              stamps_med_us=[round(x, 2) for x in med], stamps_min_us=[round(x, 2) for x in mn],
              stamps_max_us=[round(x, 2) for x in mx],
              legend=("start,end_attn," if a.attn else "start,") + "end_o,wait_o,end_gu,wait_gu,end_down,wait_down,end_qkv")
+    if a.attn:
+        r["attn_stamps_med_max_us"] = extra
     print(json.dumps(r), flush=True)
     if a.json:
         with open(a.json, "a") as f:

@@ -221,6 +221,8 @@ class LlamaModel:
                      a_sb=lay.sb, a_sh=lay.sh, a_st=lay.st, a_ctx=bufs.ctx_lens, a_seq=bufs.seq_ids,
                      a_scale=self.scale, a_n_splits=ops.decode_n_splits(bufs.max_ctx), a_part_o=bufs.part_o,
                      a_part_ml=bufs.part_ml, a_counters=bufs.attn_cnt)
+            if getattr(bufs, "rt_cols", 0) and ops.env_flag("VWA_ROW_TABLE", True):
+                a["a_row_table"] = bufs.row_table
         tiled = isinstance(L.o, ops.TiledWeight)
         wsel = (lambda w: w.t) if tiled else (lambda w: w)  # noqa: E731
         desc, lds = ops.ext().chain_make(

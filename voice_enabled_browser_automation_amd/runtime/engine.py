@@ -86,6 +86,12 @@ class StepBuffers:
         self.h_i32 = self.h_meta[: 4 * R].view(4, R)
         self.h_slots = self.h_meta[4 * R : 6 * R].view(torch.int64)
         self.h_sel = self.h_meta[6 * R :]
+        # per-ROW copy of each row's sequence block table (chained attention: read in the same round
+        # trip as seq_ids / ctx_lens instead of a dependent table load); <= 128 blocks per sequence
+        self.rt_cols = max_blocks_per_seq if max_blocks_per_seq <= 128 and max_blocks_per_seq % 2 == 0 else 0
+        self.row_table = torch.zeros(max_rows, max(2, self.rt_cols), **i32)
+        self.h_row_table = torch.zeros(max_rows, max(2, self.rt_cols), dtype=torch.int32, pin_memory=pin)
+        self.np_row_table = self.h_row_table.numpy()
         self.h_i32[3].fill_(1)  # the same inert rows as the device copy (captured graphs upload it)
         self.h_slots.fill_(-1)
         self.h_table = torch.zeros(max_seqs, max_blocks_per_seq, dtype=torch.int32, pin_memory=pin)
@@ -189,6 +195,8 @@ class LLMEngine:
             # inside a captured graph: the pinned -> device metadata copy is the graph's first node,
             # so a replay is one host call instead of a copy + a replay
             self.bufs.meta.copy_(self.bufs.h_meta, non_blocking=True)
+            if self.bufs.rt_cols and M <= 4:
+                self.bufs.row_table[:M].copy_(self.bufs.h_row_table[:M], non_blocking=True)
         return self.model.forward(self.bufs, M, self.kv, n_sel=None if L == M else L)
 
     def _capture(self, M: int, L: int):
@@ -250,6 +258,7 @@ class LLMEngine:
         pending: Dict[int, int] = {}
         bs = self.block_size
         toks, poss, sids, slots = [], [], [], []
+        rtab = b.np_row_table if b.rt_cols and M <= 4 else None
         for seq, tok in rows:
             sid = seq.sid
             pos = pending.get(sid, seq.n_computed)
@@ -262,6 +271,9 @@ class LLMEngine:
             sids.append(sid)
             slots.append(seq.blocks[pos // bs] * bs + pos % bs)
             pending[sid] = pos + 1
+        if rtab is not None:  # after the loop: a later row of a sequence may have added its last block
+            for i, (seq, _) in enumerate(rows):
+                rtab[i, : len(seq.blocks)] = seq.blocks
         hi = b.np_i32
         hi[0, :n] = toks
         hi[1, :n] = poss
@@ -273,6 +285,8 @@ class LLMEngine:
             hi[3, n:M] = 1
             b.np_slots[n:M] = -1
         b.upload(M, meta=not self.use_graphs)  # the step graphs copy the metadata themselves
+        if rtab is not None and not self.use_graphs:
+            b.row_table[:M].copy_(b.h_row_table[:M], non_blocking=True)
         chained = self._uses_chain(M)
         self._last_step = (list(rows), logits_for, {sid: self.seqs[sid].n_computed for sid in pending}) \
             if chained else None
