@@ -329,7 +329,9 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   } else {  // single register set (the chained launch holds the next GEMM's weights meanwhile)
     for (int s = FINE ? w : 0; s < nsteps; s += FINE ? kWv : 1) {
       uint4 kA[2][NKS], vA[NVL];
+      if (item == bid && s == w) stamp(13);  // (diagnostic: about to issue the first K/V step)
       load_step(wb + s * kMqStep, kA, vA);
+      if (item == bid && s == w) stamp(15);  // (diagnostic stamp 15: the wave's first K/V step landed)
       compute_step(wb + s * kMqStep, kA, vA);
     }
   }
@@ -398,7 +400,6 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   }
   __syncthreads();
   if (!s_last) continue;
-  if (item == bid) stamp(13);  // last arriver known
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // only orders the sc1 loads after the ticket
 
   if constexpr (FINE) {

@@ -968,6 +968,24 @@ template <int KS, int SEQ, int NPH, int AG, int WA>
 __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __restrict__ cpp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ChainParams& cp = *cpp;  // device-resident descriptor
+  // Warm the scalar cache with the whole descriptor (20 x 64-byte lines) in ONE round trip: the
+  // fields are otherwise fetched behind branches and earlier fields' values, a chain of dependent
+  // scalar misses (the attention prologue measured ~6 of them before its first vector load)
+  static_assert(sizeof(ChainParams) <= 20 * 64, "descriptor warm-up covers 20 lines");
+  {
+    // (non-volatile, no memory clobber: a volatile block counts as a memory write and turns every
+    // later descriptor read into a vector load; the never-true test keeps it alive)
+    unsigned junk;
+    asm("s_load_dword %0, %1, 0x0\n\t""s_load_dword %0, %1, 0x40\n\t""s_load_dword %0, %1, 0x80\n\t""s_load_dword %0, %1, 0xc0\n\t"
+        "s_load_dword %0, %1, 0x100\n\t""s_load_dword %0, %1, 0x140\n\t""s_load_dword %0, %1, 0x180\n\t""s_load_dword %0, %1, 0x1c0\n\t"
+        "s_load_dword %0, %1, 0x200\n\t""s_load_dword %0, %1, 0x240\n\t""s_load_dword %0, %1, 0x280\n\t""s_load_dword %0, %1, 0x2c0\n\t"
+        "s_load_dword %0, %1, 0x300\n\t""s_load_dword %0, %1, 0x340\n\t""s_load_dword %0, %1, 0x380\n\t""s_load_dword %0, %1, 0x3c0\n\t"
+        "s_load_dword %0, %1, 0x400\n\t""s_load_dword %0, %1, 0x440\n\t""s_load_dword %0, %1, 0x480\n\t""s_load_dword %0, %1, 0x4c0\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(junk)
+        : "s"(cpp));
+    if (junk == 0x9e3779b9u) __builtin_amdgcn_s_sleep(1);
+  }
   uint4 A[16], B[16];
   // barrier = arrive (stores drained), issue the next phase's first weight item, then wait: the
   // weight stream is in flight while the slowest workgroup finishes
@@ -1019,6 +1037,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                           setup0(n_attn);
                                                           if (cp.idle_pre) issue0(pre0);
                                                         }, &n_attn, [&](int k) {
+                                                          if ((k == 15 || k == 10) && cp.ts) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                                                           if (cp.ts && threadIdx.x == 0)
                                                             cp.ts[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memrealtime();
                                                         });

@@ -25,6 +25,10 @@ def main():
     ap.add_argument("--no-wait", action="store_true",
                     help="DIAGNOSTIC: barriers arrive but never wait (wrong results): phase cost without dependencies")
     ap.add_argument("--row-table", action="store_true", help="attention: per-row block tables (a_row_table)")
+    ap.add_argument("--ctx", type=int, default=1100, help="attention context length (tokens)")
+    ap.add_argument("--warm-kv", action="store_true",
+                    help="diagnostic: a standalone decode attention over the same K/V right before each chained "
+                         "launch (its stamps then show the attention with warm caches / TLB)")
     ap.add_argument("--row-major", dest="tiled", action="store_false",
                     help="row-major [N, K] weights instead of the pre-tiled layout (ops.tile_weight)")
     a = ap.parse_args()
@@ -51,7 +55,7 @@ def main():
     work = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
     akw, ag = {}, 0
     if a.attn:  # the layer's attention over a 1100-token paged context as phase 0
-        ctx, bs = 1100, 16
+        ctx, bs = a.ctx, 16
         nblk = (ctx + M + bs - 1) // bs + 1
         akc = (torch.randn(nblk + 4, nkv, bs, hd, device=dev) * 0.5).to(bf)
         akv = torch.randn_like(akc)
@@ -68,6 +72,11 @@ def main():
             rt = torch.zeros(M, 128, dtype=torch.int32, device=dev)
             rt[:, :nblk] = table[0]
             akw["a_row_table"] = rt
+    if a.attn:  # the QKV phase writes the step's new keys into the attention's own paged cache
+        kc, vc = akw["a_k"], akw["a_v"]  # (as the engine's next layer: same blocks, same table)
+        tb = akw["a_table"][0].long()
+        p_new = torch.arange(a.ctx, a.ctx + M, device=dev)
+        slots = tb[p_new // 16] * 16 + p_new % 16
     if a.tiled:  # the descriptors hold raw pointers: keep the tiled copies alive in Ws
         for w in Ws:
             w.update({k + "_t": ops.tile_weight(w[k]) for k in ("o", "gu", "down", "qkv")})
@@ -79,6 +88,11 @@ def main():
     def chained():
         it[0] = (it[0] + 1) % ncopy
         dsc, lds = descs[it[0]]
+        if a.warm_kv and a.attn:
+            ops.decode_attention(akw["a_q"], ops.KVLayout.paged(akw["a_k"], akw["a_v"], akw["a_table"]), akw["a_ctx"],
+                                 akw["a_seq"], n_q_heads=nq, n_kv_heads=nkv, head_dim=hd, scale=hd ** -0.5,
+                                 max_ctx=2048, out=akw["a_q"].new_empty(akw["a_q"].shape), part_o=akw["a_part_o"],
+                                 part_ml=akw["a_part_ml"], counters=akw["a_counters"])
         E.chain_run(dsc, 4, lds, h, ag)
 
     def separate():
@@ -113,14 +127,14 @@ def main():
         full = ts.view(-1, 16)[:cus].double().cpu()
         t0 = full[:, 0].min()
         att = full[full[:, 11] > 0]
-        names = ["ctx_known", "q_ready", "kv_done", "partials_stored", "last_known", "merged"]
+        names = ["ctx_known", "q_ready", "kv_done", "partials_stored", "kv_issue", "merged", "kv_landed"]
         extra = {}
         for j, nm in enumerate(names):
             col = att[:, 9 + j]
             col = col[col > 0]
             if col.numel():
                 extra[nm] = [round(float((col.median() - t0) * 10e-3), 2), round(float((col.max() - t0) * 10e-3), 2)]
-    r = dict(kernel="chain_probe", rows=M, bar_mode=a.bar_mode, wpol=a.wpol, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
+    r = dict(kernel="chain_probe", rows=M, ctx=a.ctx if a.attn else None, warm_kv=a.warm_kv, kvpf=os.environ.get("VWA_CHAIN_KVPF", "1"), bar_mode=a.bar_mode, wpol=a.wpol, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
              stamps_med_us=[round(x, 2) for x in med], stamps_min_us=[round(x, 2) for x in mn],
              stamps_max_us=[round(x, 2) for x in mx],
              legend=("start,end_attn," if a.attn else "start,") + "end_o,wait_o,end_gu,wait_gu,end_down,wait_down,end_qkv")
