@@ -126,9 +126,12 @@ void set_ln_fold(SkinnyParams& p, const c10::optional<Tensor>& ln_c, int epi) {
 }
 
 // epi: 0 store, 1 residual add, 3 gelu
+// col_mask (epi 0): int32 token bitmask rows [>= rows_used, words]; column n of y is the mask's bit
+// col_mask_off * 32 + n (vocab shard offset under TP) -- tiles without an admissible bit in any of
+// the first mask_rows rows are not computed (their y columns are left as they were)
 void skinny_gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi, bool fuse_rms, double eps,
                  c10::optional<Tensor> residual, c10::optional<Tensor> w_scale, c10::optional<Tensor> ln_c,
-                 bool w_tiled) {
+                 bool w_tiled, c10::optional<Tensor> col_mask, int64_t col_mask_off, int64_t mask_rows) {
   c10::DeviceGuard g(x.device());
   SkinnyParams p = base_params(x, w, bias, fuse_rms, eps, w_scale, w_tiled);
   TORCH_CHECK(epi == 0 || epi == 1 || epi == 3, "bad epilogue");
@@ -147,6 +150,18 @@ void skinny_gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64
                 "residual shape mismatch");
     p.R = bfp(*residual);
     p.ldr = (int)residual->stride(0);
+  }
+  if (col_mask.has_value()) {
+    const Tensor& cm = *col_mask;
+    TORCH_CHECK(epi == 0, "col_mask needs the store epilogue");
+    TORCH_CHECK(cm.is_cuda() && cm.scalar_type() == at::kInt && cm.dim() == 2 && cm.stride(1) == 1,
+                "col_mask must be an int32 [rows, words] GPU tensor with contiguous rows");
+    TORCH_CHECK(mask_rows >= 1 && mask_rows <= cm.size(0) && col_mask_off >= 0 &&
+                    (col_mask_off + (w.size(0) + 31) / 32) <= cm.size(1),
+                "col_mask does not cover the output columns");
+    p.col_mask = reinterpret_cast<const uint32_t*>(cm.data_ptr<int>()) + col_mask_off;
+    p.col_mask_ld = (int)cm.stride(0);
+    p.col_mask_rows = (int)mask_rows;
   }
   check_rc(run_skinny_checked((int)epi, p, cur_stream(x)), "skinny_gemm");
 }
@@ -777,7 +792,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for the voice-web-agent inference engine";
   m.def("skinny_gemm", &skinny_gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
         py::arg("fuse_rms"), py::arg("eps"), py::arg("residual"), py::arg("w_scale") = py::none(),
-        py::arg("ln_c") = py::none(), py::arg("w_tiled") = false);
+        py::arg("ln_c") = py::none(), py::arg("w_tiled") = false, py::arg("col_mask") = py::none(),
+        py::arg("col_mask_off") = 0, py::arg("mask_rows") = 1);
   m.def("skinny_gemm_swiglu", &skinny_gemm_swiglu, py::arg("x"), py::arg("w_gu"), py::arg("bias"), py::arg("h"),
         py::arg("fuse_rms"), py::arg("eps"), py::arg("w_scale") = py::none(), py::arg("w_tiled") = false);
   m.def("skinny_gemm_qkv", &skinny_gemm_qkv, py::arg("x"), py::arg("w_qkv"), py::arg("bias"), py::arg("fuse_rms"),

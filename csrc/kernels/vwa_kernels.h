@@ -32,6 +32,11 @@ struct SkinnyParams {
   // W[16 T + (lane & 15)][128 kg + 32 (lane >> 4) + 8 s + e] -- every weight load instruction of
   // the streaming / chained kernels then reads 1 KB contiguous (ops.tile_weight)
   int w_tiled;
+  // col_mask (LM head under a grammar mask, EPI store, <= 64 tiles per workgroup): u32 token
+  // bitmask rows [col_mask_rows][col_mask_ld]; only the 16-column tiles holding an admissible token
+  // of some row are computed, the other outputs are left unwritten (the sampler never reads a
+  // masked logit).  Ignored (every tile computed) where the kernel cannot take it.
+  const uint32_t* col_mask; int col_mask_ld; int col_mask_rows;
 };
 
 // Paged / strided KV addressing shared by the attention kernels:

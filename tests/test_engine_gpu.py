@@ -87,6 +87,29 @@ def test_intent_engine_continuous_batching_gpu():
     assert any(L < M for (M, L) in eng.graphs)
 
 
+def test_masked_lm_head_gives_the_dense_heads_answers():
+    """The grammar-masked LM head (LLMEngine.head_logits(col_mask=...)) skips the vocab tiles no
+    row may sample; the admissible logits are the dense head's, so the sampled answers are the
+    same token for token (one session and a continuous batch)."""
+    from voice_enabled_browser_automation_amd.brain.intent_engine import LLMIntentEngine
+    from voice_enabled_browser_automation_amd.models.config import LLAMA_PRESETS
+
+    ops.ext()
+    m = LlamaModel(LLAMA_PRESETS["llama-tiny"], device="cuda", seed=4)
+    assert isinstance(m.lm_head, ops.TiledWeight)  # the streaming kernel (the masked path) runs the head
+    texts = ["search wireless earbuds", "scroll down", "sort by price", "go back"]
+    outs = {}
+    for masked in (True, False):
+        eng = LLMEngine(m, max_seqs=4, max_model_len=2048)
+        ie = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=200, temperature=0.1, seed=7)
+        ie.masked_head = masked
+        outs[masked] = [ie.generate(ie_msgs) for ie_msgs in
+                        ([{"role": "user", "content": t}] for t in texts[:1])]
+        outs[masked] += ie.generate_many([[{"role": "user", "content": t}] for t in texts])
+        m.reset_chains()
+    assert outs[True] == outs[False]
+
+
 def test_gpt2_gpu_engine_matches_cpu_reference():
     """GPT-2 (LayerNorm, learned positions, biased QKV without RoPE, GELU MLP, MHA head_dim 64)
     through the native kernels vs the CPU reference with the same bf16 weights."""

@@ -498,3 +498,33 @@ def test_tiled_weights_match_row_major(M):
         outs.append((q, kc, vc))
     for a, b in zip(*outs):
         close(b, a, 1e-2, 1e-2)
+
+
+@pytest.mark.parametrize("M", [1, 3])
+@pytest.mark.parametrize("tiled", [False, True])
+def test_masked_lm_head_computes_only_admissible_tiles(M, tiled):
+    """Grammar-masked LM head (SkinnyParams::col_mask, ops.linear(col_mask=...)): every 16-column
+    tile with an admissible bit in one of the mask rows equals the dense f32 result, every other
+    column of ``out`` is left untouched; a word offset (vocab shard under TP) shifts the bits."""
+    K, N, W = 4096, 8192, 300
+    x = rnd(M, K)
+    w = rnd(N, K, scale=0.02)
+    wt = ops.TiledWeight(w) if tiled else w
+    dense = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    ops.linear(x, w, out=dense, fuse_rms=True)
+    g = torch.Generator().manual_seed(3)
+    for off in (0, 7):
+        bits = torch.rand(M, W * 32, generator=g) < 0.004  # sparse, scattered
+        bits[0, (off * 32 + 5000):(off * 32 + 5040)] = True  # and one dense run
+        words = torch.zeros(M, W, dtype=torch.int64)
+        for b in range(32):
+            words |= bits[:, b::32].long() << b
+        mask = words.to(torch.int32).to(DEV)  # (bit 31 wraps to the sign: same bits)
+        out = torch.full((M, N), float("nan"), dtype=torch.float32, device=DEV)
+        ops.linear(x, wt, out=out, fuse_rms=True, col_mask=mask, col_mask_off=off, mask_rows=M)
+        cols = bits[:, off * 32 : off * 32 + N].any(0)
+        live = cols.view(-1, 16).any(1).repeat_interleave(16)
+        assert 0 < int(live.sum()) < N
+        o = out.cpu()
+        assert torch.isnan(o[:, ~live]).all(), "a tile without admissible tokens was computed"
+        close(o[:, live], dense.cpu()[:, live], 1e-3, 1e-3)

@@ -117,6 +117,9 @@ class LLMIntentEngine:
         # instead of a stream synchronize: the GPU idles from the sampler's end until the host
         # has posted the next step, so the wake-up latency is on the critical path
         self.spin_wait = pin and ops.env_flag("VWA_SPIN_WAIT", True)
+        # LM head under the grammar mask (LLMEngine.head_logits): the vocab tiles no row may sample
+        # are skipped -- 42 % of the tiles live per step on average on the intent grammar
+        self.masked_head = ops.env_flag("VWA_MASKED_HEAD", True)
         self.part_val = torch.zeros(R * 64, dtype=torch.float32, device=dev)
         self.part_idx = torch.zeros(R * 64, dtype=torch.int32, device=dev)
         self.last_stats: Dict[str, Any] = {}
@@ -237,11 +240,11 @@ class LLMIntentEngine:
         tm = self.timing
         t0 = time.perf_counter()
         if last:
-            logits = self.engine.run_rows(rows, logits_for=last, check=False)
+            self.engine.run_rows(rows, logits_for=last, check=False, defer_head=True)
         else:
             # only part of one long feed fits this iteration: its rows still have to reach the KV
-            # cache (nothing is sampled, so the step is verified synchronously)
-            self.engine.run_rows(rows, logits_for=[len(rows) - 1], check=True)
+            # cache (nothing is sampled -- no LM head -- so the step is verified synchronously)
+            self.engine.run_rows(rows, logits_for=[len(rows) - 1], check=True, defer_head=True)
         t1 = time.perf_counter()
         tm["build_launch_ms"] += (t1 - t0) * 1e3
         self.batch_stats["iterations"] += 1
@@ -254,6 +257,8 @@ class LLMIntentEngine:
             r.matcher.fill_mask(self.h_mask_np[i])
         t2 = time.perf_counter()
         self.d_mask[:n].copy_(self.h_mask[:n], non_blocking=True)
+        # the LM head under the same masks: only vocab tiles some row may sample are computed
+        logits = self.engine.head_logits(col_mask=self.d_mask if self.masked_head else None, mask_rows=n)
         toks = self._sample(logits, n, self.engine.step_fail_word())
         if any(t == -2 for t in toks):
             # the forward's chained launch timed out at a grid barrier (tokens -2 from the

@@ -133,7 +133,7 @@ class GPT2Model:
 
     # ------------------------------------------------------------------ forward
     def forward(self, bufs, M: int, kv, *, prefill_seq: Optional[int] = None, q_offset: int = 0,
-                logits_rows: Optional[slice] = None, n_sel: Optional[int] = None) -> torch.Tensor:
+                logits_rows: Optional[slice] = None, n_sel: Optional[int] = None, head: bool = True) -> torch.Tensor:
         """Same contract as LlamaModel.forward (runtime.engine.StepBuffers rows)."""
         cfg = self.cfg
         eps = cfg.ln_eps
@@ -169,7 +169,12 @@ class GPT2Model:
             hs = torch.index_select(h, 0, bufs.sel[:n_sel], out=bufs.hidden_sel[:n_sel])
         else:
             hs = h[logits_rows if logits_rows is not None else slice(0, M)]
-        hs = ops.layernorm(hs, self.lnf_w, self.lnf_b, eps=eps)
+        return self.lm_logits(bufs, hs) if head else hs
+
+    def lm_logits(self, bufs, hs: torch.Tensor, col_mask: Optional[torch.Tensor] = None,
+                  mask_rows: int = 1) -> torch.Tensor:
+        """Final LayerNorm + tied LM head -> f32 logits (same contract as LlamaModel.lm_logits)."""
+        hs = ops.layernorm(hs, self.lnf_w, self.lnf_b, eps=self.cfg.ln_eps)
         n = hs.shape[0]
         out = bufs.logits_local[:n] if n <= bufs.logits_local.shape[0] else None
-        return ops.linear(hs, self.lm_head, out=out, out_dtype=torch.float32)
+        return ops.linear(hs, self.lm_head, out=out, out_dtype=torch.float32, col_mask=col_mask, mask_rows=mask_rows)

@@ -244,14 +244,16 @@ class LlamaModel:
         return bool(bar is not None and int(bar.view(torch.int64)[160].item()) != 0)
 
     def forward(self, bufs, M: int, kv, *, prefill_seq: Optional[int] = None, q_offset: int = 0,
-                logits_rows: Optional[slice] = None, n_sel: Optional[int] = None) -> torch.Tensor:
+                logits_rows: Optional[slice] = None, n_sel: Optional[int] = None, head: bool = True) -> torch.Tensor:
         """Run M token rows described by ``bufs`` (runtime.buffers.StepBuffers).
 
         Decode/ragged mode (M <= 64): each row is one token of some sequence (seq_ids /
         ctx_lens / positions / slots per row).  Prefill mode (prefill_seq given): the M rows are
         consecutive tokens of table row ``prefill_seq`` starting at position q_offset.
         Returns f32 logits [rows, vocab] (all ranks, gathered under TP) for every row, for
-        ``logits_rows``, or (``n_sel``) for the rows listed in ``bufs.sel[:n_sel]``.
+        ``logits_rows``, or (``n_sel``) for the rows listed in ``bufs.sel[:n_sel]``.  head=False:
+        the final hidden rows instead (``lm_logits`` turns them into logits -- the engine runs the
+        LM head outside the step graph, under the sampler's grammar mask).
         """
         cfg = self.cfg
         h = bufs.hidden[:M]
@@ -319,12 +321,25 @@ class LlamaModel:
             hs = torch.index_select(h, 0, bufs.sel[:n_sel], out=bufs.hidden_sel[:n_sel])
         else:
             hs = h[logits_rows if logits_rows is not None else slice(0, M)]
+        return self.lm_logits(bufs, hs) if head else hs
+
+    def lm_logits(self, bufs, hs: torch.Tensor, col_mask: Optional[torch.Tensor] = None,
+                  mask_rows: int = 1) -> torch.Tensor:
+        """Final RMSNorm (folded into the weights) + LM head of the hidden rows ``hs`` -> f32 logits
+        [rows, vocab], gathered under TP.  col_mask (the sampler's int32 token bitmask rows): only
+        the vocab tiles with an admissible token in one of the first ``mask_rows`` rows are
+        computed (ops.linear); the other logits are stale and must only be read through the mask."""
         n = hs.shape[0]
         local = bufs.logits_local[:n] if n <= bufs.logits_local.shape[0] else None
-        local = ops.linear(hs, self.lm_head, out=local, fuse_rms=True, eps=cfg.rms_eps, out_dtype=torch.float32)
+        mk = {}
+        if col_mask is not None and self.v_start % 32 == 0 and col_mask.shape[1] * 32 >= self.v_end:
+            mk = dict(col_mask=col_mask, col_mask_off=self.v_start // 32, mask_rows=mask_rows)
+        local = ops.linear(hs, self.lm_head, out=local, fuse_rms=True, eps=self.cfg.rms_eps, out_dtype=torch.float32,
+                           **mk)
         if self.tp.size == 1:
             return local
-        return self.tp.all_gather_vocab(local, cfg.vocab_size, out=bufs.logits[:n] if n <= bufs.logits.shape[0] else None)
+        return self.tp.all_gather_vocab(local, self.cfg.vocab_size,
+                                        out=bufs.logits[:n] if n <= bufs.logits.shape[0] else None)
 
 
 def move_model(model, device) -> None:

@@ -313,15 +313,23 @@ SKINNY_MAX_M = 16
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, out: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, act: str = "none", fuse_rms: bool = False, eps: float = 1e-5,
-           out_dtype: Optional[torch.dtype] = None, ln_c: Optional[torch.Tensor] = None) -> torch.Tensor:
+           out_dtype: Optional[torch.dtype] = None, ln_c: Optional[torch.Tensor] = None,
+           col_mask: Optional[torch.Tensor] = None, col_mask_off: int = 0, mask_rows: int = 1) -> torch.Tensor:
     """y = act(rms(x) @ w^T + bias) [+ residual].
 
     GPU: rows <= 64 -> MFMA skinny GEMM with fused epilogue (decode); otherwise hipBLASLt
     (torch.matmul) for the plain GEMM + HIP epilogue kernels (prefill).
     ln_c (from fold_layernorm): x goes through a LayerNorm whose affine is folded into (w, bias);
     decode rows compute its mean/rstd inside the streaming GEMM, other shapes normalise first.
+    col_mask (int32 token bitmask rows, the sampler's grammar mask; plain store epilogue): the
+    streaming kernel computes only the 16-column tiles with an admissible bit (word col_mask_off
+    onward) in one of the first mask_rows rows and leaves the other columns of ``out`` untouched
+    -- they must only be read through the same mask.  Other paths compute every column.
     """
     M = x.shape[0]
+    mk = {}
+    if col_mask is not None and residual is None and act == "none" and bias is None and ln_c is None:
+        mk = dict(col_mask=col_mask, col_mask_off=col_mask_off, mask_rows=mask_rows)
     dt = out_dtype or (x.dtype if out is None else out.dtype)
     if out is None:
         out = torch.empty((M, w.shape[0]), dtype=dt, device=x.device)
@@ -331,7 +339,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
             if residual is not None:
                 assert act == "none"
                 epi = 1
-            ext().skinny_gemm(x, w.t, bias, out, epi, fuse_rms and ln_c is None, eps, residual, None, ln_c, True)
+            ext().skinny_gemm(x, w.t, bias, out, epi, fuse_rms and ln_c is None, eps, residual, None, ln_c, True,
+                              **mk)
             return out
         w = w.w
     if ln_c is not None:
@@ -354,7 +363,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         if fp8:
             E.skinny_gemm(x, w.w8, bias, out, epi, fuse_rms, eps, residual, w.scale)
         else:
-            E.skinny_gemm(x, w, bias, out, epi, fuse_rms, eps, residual)
+            E.skinny_gemm(x, w, bias, out, epi, fuse_rms, eps, residual, **mk)
         return out
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
     y = _fp8_matmul(xin, w) if fp8 else torch.matmul(xin, w.t())

@@ -144,6 +144,7 @@ class LLMEngine:
         self.graph_pool = None
         self.stats = dict(steps=0, rows=0, prefill_tokens=0, cached_tokens=0, graph_replays=0)
         self._last_step = None  # (rows, logits_for, n_computed before) of a chained step, for recover_step
+        self._head_rows: Optional[torch.Tensor] = None  # the last step's hidden rows for head_logits()
 
     # ------------------------------------------------------------------ sequences
     def new_sequence(self, tokens: Sequence[int], use_prefix_cache: bool = True) -> Sequence_:
@@ -197,7 +198,7 @@ class LLMEngine:
             self.bufs.meta.copy_(self.bufs.h_meta, non_blocking=True)
             if self.bufs.rt_cols and M <= 4:
                 self.bufs.row_table[:M].copy_(self.bufs.h_row_table[:M], non_blocking=True)
-        return self.model.forward(self.bufs, M, self.kv, n_sel=None if L == M else L)
+        return self.model.forward(self.bufs, M, self.kv, n_sel=None if L == M else L, head=False)
 
     def _capture(self, M: int, L: int):
         s = torch.cuda.Stream()
@@ -229,9 +230,14 @@ class LLMEngine:
         torch.cuda.synchronize()
 
     def run_rows(self, rows: List[Tuple[Sequence_, int]], logits_for: Optional[List[int]] = None,
-                 check: bool = True) -> torch.Tensor:
+                 check: bool = True, defer_head: bool = False) -> Optional[torch.Tensor]:
         """Append one token per row (row = (seq, token)); return f32 logits of the rows listed in
         ``logits_for`` ([len(logits_for), V], default: every row).
+
+        The step graph ends at the final hidden rows; the LM head is its own launch.
+        ``defer_head=True`` returns None and leaves it to ``head_logits(col_mask=...)``, so the
+        caller can compute the grammar mask on the CPU while the layers run and have the LM head
+        skip the vocab tiles no row may sample.
 
         Rows of the same sequence must be consecutive and in order.  Selecting rows (typically
         the last row of each sequence) keeps the LM head -- the largest GEMM of a step -- at one
@@ -291,11 +297,11 @@ class LLMEngine:
         self._last_step = (list(rows), logits_for, {sid: self.seqs[sid].n_computed for sid in pending}) \
             if chained else None
         if self.use_graphs:
-            g, out = self.graphs.get((M, L)) or self._capture(M, L)
+            g, hs = self.graphs.get((M, L)) or self._capture(M, L)
             g.replay()
             self.stats["graph_replays"] += 1
         else:
-            out = self._forward_rows(M, L)
+            hs = self._forward_rows(M, L)
         for sid, ln in pending.items():
             self.seqs[sid].n_computed = ln
         self.stats["steps"] += 1
@@ -305,10 +311,21 @@ class LLMEngine:
         if check and chained and self.device.type == "cuda":
             torch.cuda.current_stream().synchronize()
             if self.model.chain_error():
+                self._head_rows = None
                 return self.recover_step()
-        if L == M and nl != n:
-            return out[torch.tensor(logits_for, device=out.device)]
-        return out[:nl]
+        self._head_rows = hs[torch.tensor(logits_for, device=hs.device)] if L == M and nl != n else hs[:nl]
+        if defer_head:
+            return None
+        return self.head_logits()
+
+    def head_logits(self, col_mask: Optional[torch.Tensor] = None, mask_rows: int = 1) -> torch.Tensor:
+        """LM head of the last ``run_rows`` step's selected rows -> f32 logits [rows, V].
+        col_mask: the sampler's int32 token bitmask rows (row i <-> logits row i); vocab tiles with
+        no admissible token in the first ``mask_rows`` rows are skipped and their logits are stale
+        (read them only through the same mask)."""
+        hs = self._head_rows
+        assert hs is not None, "head_logits() needs a run_rows() step first"
+        return self.model.lm_logits(self.bufs, hs, col_mask=col_mask, mask_rows=mask_rows)
 
     def _uses_chain(self, M: int) -> bool:
         ok = getattr(self.model, "_chain_ok", None)

@@ -71,6 +71,7 @@ class Settings(BaseModel):
     VWA_HIPGRAPH: bool = True
     VWA_CHAIN: bool = True  # chained Llama decode layer tail (skinny_stream.hip chain_kernel SEQ 0)
     VWA_CHAIN_ASR: bool = False  # chained Whisper decoder launches (SEQ 1 / 2; measured no gain)
+    VWA_MASKED_HEAD: bool = True  # LM head skips the vocab tiles the grammar mask excludes (intent decode)
     VWA_KV_GB: float = 0.0
     VWA_DEBOUNCE_MS: float = 1000.0
     VWA_BUDGET_CHARS: int = 512
