@@ -181,7 +181,9 @@ void skinny_gemm_swiglu(Tensor x, Tensor w_gu, c10::optional<Tensor> bias, Tenso
 
 void check_cache(const Tensor& c, const char* name) {
   check_bf16(c, name);
-  TORCH_CHECK(c.dim() == 4 && c.is_contiguous(), name, " must be contiguous [blocks, kv_heads, block_size, head_dim]");
+  // any block / head / token strides (the kernels address by stride), contiguous head_dim rows
+  TORCH_CHECK(c.dim() == 4 && c.stride(3) == 1 && c.stride(0) > 0 && c.stride(1) > 0 && c.stride(2) > 0, name,
+              " must be [blocks, kv_heads, block_size, head_dim] with contiguous head_dim rows");
 }
 
 // QKV epilogue operands (RoPE table, positions, paged-KV slots and cache strides) into p

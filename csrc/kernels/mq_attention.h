@@ -152,18 +152,39 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
 
+  // FINE: the Q fragments of the likely first item -- KV head bid % nkv, the group of rows
+  // [0, min(rows, RG)) (one decode row, or one sequence's jump-forward rows) -- are issued with
+  // the step metadata instead of one round trip after it; checked once the groups are known
+  uint4 qspec[NKS];
+  const int nr_spec = min(p.rows, RG);
+  if constexpr (FINE) {
+    const u16* qr = p.q + (int64_t)min(n / G, nr_spec - 1) * p.ldq + ((bid % nkv) * G + n % G) * D + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) qspec[ks] = *reinterpret_cast<const uint4*>(qr + 32 * ks);
+  }
+
   // ---- row groups of the whole step (<= 64 rows; every wave derives the same answer): runs of
   //      consecutive rows of one sequence, cut every RG rows from the run's start
   // per-row block tables (FINE, <= 4 rows): fetched with the sequence ids, two entries per lane
+  // All of it in ONE round trip: branch-free buffer loads (past the end -> 0).  (The conditional
+  // plain loads this replaces compiled to a wait after each load: five dependent round trips.)
   const bool rowtab = FINE && p.row_table != nullptr && p.rows <= 4;
+  const __amdgpu_buffer_rsrc_t r_rt = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int*>(p.row_table), (short)0, rowtab ? p.rows * p.rt_stride * 4 : 0, 0x00020000);
   int2 rt[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
-    rt[r] = (rowtab && r < p.rows && 2 * lane < p.rt_stride)
-                ? *reinterpret_cast<const int2*>(p.row_table + r * p.rt_stride + 2 * lane)
-                : make_int2(0, 0);
-  const int sl = lane < p.rows ? p.seq_ids[lane] : -1;
-  const int cl = lane < p.rows ? p.ctx_lens[lane] : 0;  // same round trip as the sequence ids
+    rt[r] = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
+                                         r_rt, 2 * lane < p.rt_stride ? (r * p.rt_stride + 2 * lane) * 4 : 0x7FFFFFF0,
+                                         0, 0));
+  const __amdgpu_buffer_rsrc_t r_sid =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.seq_ids), (short)0, p.rows * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r_ctx =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.ctx_lens), (short)0, p.rows * 4, 0x00020000);
+  const int sl_ld = (int)__builtin_amdgcn_raw_buffer_load_b32(r_sid, lane * 4, 0, 0);
+  const int cl_ld = (int)__builtin_amdgcn_raw_buffer_load_b32(r_ctx, lane * 4, 0, 0);
+  const int sl = lane < p.rows ? sl_ld : -1;
+  const int cl = lane < p.rows ? cl_ld : 0;
   const int sp = __shfl(sl, lane > 0 ? lane - 1 : 0, 64);
   const unsigned long long run_starts = __ballot(lane < p.rows && (lane == 0 || sl != sp));
   const int run0 = 63 - __builtin_clzll(run_starts & ((2ull << lane) - 1ull));  // lane 0 always starts a run
@@ -218,10 +239,11 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   {
     const float qs = p.scale * 1.4426950408889634f;
     const u16* qr = p.q + (int64_t)(r0 + min(rho, nr - 1)) * p.ldq + (kvh * G + n % G) * D + 8 * g;
+    const bool spec = FINE && item == bid && r0 == 0 && nr == nr_spec;  // (kvh == bid % nkv here)
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       float f[8];
-      unpack8(*reinterpret_cast<const uint4*>(qr + 32 * ks), f);
+      unpack8(spec ? qspec[ks] : *reinterpret_cast<const uint4*>(qr + 32 * ks), f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = rho < nr ? f[j] * qs : 0.f;
       qf[ks] = as_bf16x8(pack8(f));

@@ -1060,7 +1060,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     const bool idle = mq_body<128, AG, KS, true, false, true>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
                                                         (int)blockIdx.x, [&]() {
                                                           setup0(n_attn);
-                                                          if (cp.idle_pre) issue0(pre0);
+                                                          if (cp.idle_pre > 0) issue0(pre0);
                                                         }, &n_attn, [&](int k) {
                                                           if ((k == 15 || k == 10) && cp.ts) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                                                           if (cp.ts && threadIdx.x == 0)
@@ -1072,10 +1072,11 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     if (!idle) {
       pre0 = 0;
       issue0(0);
-    } else if (!cp.idle_pre) {
+    } else if (cp.idle_pre == 0) {
       issue0(pre0);
     }
     chain_wait(bar, gen, cp.bar_mode);
+    if (idle && cp.idle_pre < 0) issue0(pre0);  // DIAGNOSTIC: no weight stream during the attention
   } else {
     setup0(0);
     issue0(pre0);

@@ -26,6 +26,9 @@ def main():
                     help="DIAGNOSTIC: barriers arrive but never wait (wrong results): phase cost without dependencies")
     ap.add_argument("--row-table", action="store_true", help="attention: per-row block tables (a_row_table)")
     ap.add_argument("--ctx", type=int, default=1100, help="attention context length (tokens)")
+    ap.add_argument("--kv-tok-major", action="store_true",
+                    help="K/V blocks stored [block][token][head][dim] (a head's 16 tokens at 2 KB stride) "
+                         "instead of [block][head][token][dim] (4 KB contiguous per head)")
     ap.add_argument("--warm-kv", action="store_true",
                     help="diagnostic: a standalone decode attention over the same K/V right before each chained "
                          "launch (its stamps then show the attention with warm caches / TLB)")
@@ -57,8 +60,12 @@ def main():
     if a.attn:  # the layer's attention over a 1100-token paged context as phase 0
         ctx, bs = a.ctx, 16
         nblk = (ctx + M + bs - 1) // bs + 1
-        akc = (torch.randn(nblk + 4, nkv, bs, hd, device=dev) * 0.5).to(bf)
-        akv = torch.randn_like(akc)
+        if a.kv_tok_major:
+            akc = (torch.randn(nblk + 4, bs, nkv, hd, device=dev) * 0.5).to(bf).permute(0, 2, 1, 3)
+            akv = torch.randn(nblk + 4, bs, nkv, hd, device=dev).to(bf).permute(0, 2, 1, 3)
+        else:
+            akc = (torch.randn(nblk + 4, nkv, bs, hd, device=dev) * 0.5).to(bf)
+            akv = torch.randn_like(akc)
         table = (torch.randperm(nblk + 3, device=dev)[:nblk].to(torch.int32) + 1).view(1, nblk)
         lay = ops.KVLayout.paged(akc, akv, table)
         ns = ops.decode_n_splits(2048)
@@ -134,7 +141,7 @@ def main():
             col = col[col > 0]
             if col.numel():
                 extra[nm] = [round(float((col.median() - t0) * 10e-3), 2), round(float((col.max() - t0) * 10e-3), 2)]
-    r = dict(kernel="chain_probe", rows=M, ctx=a.ctx if a.attn else None, warm_kv=a.warm_kv, kvpf=os.environ.get("VWA_CHAIN_KVPF", "1"), bar_mode=a.bar_mode, wpol=a.wpol, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
+    r = dict(kernel="chain_probe", rows=M, ctx=a.ctx if a.attn else None, warm_kv=a.warm_kv, kv_tok_major=a.kv_tok_major, bar_mode=a.bar_mode, wpol=a.wpol, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
              stamps_med_us=[round(x, 2) for x in med], stamps_min_us=[round(x, 2) for x in mn],
              stamps_max_us=[round(x, 2) for x in mx],
              legend=("start,end_attn," if a.attn else "start,") + "end_o,wait_o,end_gu,wait_gu,end_down,wait_down,end_qkv")

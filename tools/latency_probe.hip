@@ -1,0 +1,150 @@
+// Load-latency probe (diagnostic, not part of the framework): what a cold vector load costs on
+// MI355X after the decode step's weight stream has gone through the caches -- the chained
+// attention's K/V round trip measured ~6 us cold vs ~3.5 us right after another read of the same
+// K/V (tools/chain_probe.py --attn / --warm-kv).  One lane times single dependent loads
+// (s_memrealtime, 100 MHz) at offsets chosen to separate a new 2 MB region, a new 4 KB page, a
+// new line of a touched page, and a re-read.
+//
+//   hipcc --offload-arch=gfx950 -O2 tools/latency_probe.hip -o tools/latency_probe && tools/latency_probe
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <algorithm>
+#include <vector>
+
+#define CK(x)                                                                 \
+  do {                                                                        \
+    hipError_t e_ = (x);                                                      \
+    if (e_ != hipSuccess) {                                                   \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      std::exit(1);                                                           \
+    }                                                                         \
+  } while (0)
+
+__global__ void probe(const char* base, const long long* offs, int n, unsigned long long* ticks, int* sink) {
+  if (threadIdx.x != 0) return;
+  int acc = 0;
+  for (int i = 0; i < n; ++i) {
+    const char* p = base + offs[i];
+    unsigned long long t0, t1;
+    int v;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+    asm volatile("global_load_dword %0, %1, off\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+    acc += v;
+    ticks[i] = t1 - t0;
+  }
+  sink[0] = acc;
+}
+
+// the chained attention's K/V step shape: every wave of `grid` workgroups x `waves` issues 16 load
+// instructions (8 "K": 16 keys x 64 B at a 256 B key stride, 8 "V": 4 keys x 256 B), all before
+// the first wait, at its own 32-key range of a paged region; lane 0 stamps issue and landing
+__global__ void kv_gather(const char* base, long long region, unsigned long long* ticks, int* sink) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, n = lane & 15, g = lane >> 4;
+  const long long wid = (long long)blockIdx.x * (blockDim.x >> 6) + w;
+  const char* kb = base + (wid * 32 * 256) % region;  // 32 keys x 256 B per wave
+  unsigned long long t0, t1;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  uint4 r[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int key = 8 * (n >> 2) + 4 * (i & 1) + (n & 3);
+    r[i] = *reinterpret_cast<const uint4*>(kb + key * 256 + 16 * g + 64 * (i >> 1));
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int idx = i * 64 + lane;
+    r[8 + i] = *reinterpret_cast<const uint4*>(kb + (idx / 16) * 256 + 16 * (idx % 16));
+  }
+  unsigned acc = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc ^= r[i].x ^ r[i].w;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  if (lane == 0) ticks[wid] = t1 - t0;
+  if (acc == 0x12345678u) sink[2] = (int)acc;
+}
+
+// every lane of every workgroup streams its share of `bytes` (the weight stream's cache pressure)
+__global__ void stream(const uint4* p, size_t n16, int* sink) {
+  unsigned acc = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
+    const uint4 v = p[i];
+    acc ^= v.x ^ v.w;
+  }
+  if (acc == 0x12345678u) sink[1] = (int)acc;
+}
+
+int main() {
+  const size_t big = (size_t)1 << 30, probe_bytes = (size_t)64 << 20;
+  char *A, *B;
+  CK(hipMalloc(&A, big));
+  CK(hipMalloc(&B, probe_bytes));
+  CK(hipMemset(A, 1, big));
+  CK(hipMemset(B, 2, probe_bytes));
+  // offsets: a new 2 MB region, then within it +256 B (same 4 KB page, new line), +4 KB, +64 KB,
+  // +1 MB (same 2 MB region), then the first offset again (re-read)
+  std::vector<long long> offs;
+  const char* what[] = {"new_2MB", "same_page_new_line", "next_4KB_page", "plus_64KB", "plus_1MB", "reread_first"};
+  const int per = 6;
+  for (int r = 0; r < 8; ++r) {
+    const long long b = (long long)(r * 4 + 3) << 21;  // 8 separate 2 MB regions
+    offs.insert(offs.end(), {b, b + 256, b + 4096, b + 65536, b + (1 << 20), b});
+  }
+  const int n = (int)offs.size();
+  long long* d_offs;
+  unsigned long long* d_t;
+  int* d_sink;
+  CK(hipMalloc(&d_offs, n * sizeof(long long)));
+  CK(hipMalloc(&d_t, n * sizeof(unsigned long long)));
+  CK(hipMalloc(&d_sink, 8));
+  CK(hipMemcpy(d_offs, offs.data(), n * sizeof(long long), hipMemcpyHostToDevice));
+  std::vector<unsigned long long> t(n);
+  auto run = [&](const char* label, bool flush) {
+    if (flush) hipLaunchKernelGGL(stream, dim3(1024), dim3(512), 0, 0, (const uint4*)A, big / 16, d_sink);
+    hipLaunchKernelGGL(probe, dim3(1), dim3(64), 0, 0, B, d_offs, n, d_t, d_sink);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(t.data(), d_t, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    std::printf("{\"case\": \"%s\"", label);
+    for (int k = 0; k < per; ++k) {
+      std::vector<double> v;
+      for (int r = 0; r < n / per; ++r) v.push_back(t[r * per + k] * 0.01);  // 10 ns ticks -> us
+      double s = 0;
+      for (double x : v) s += x;
+      std::printf(", \"%s_us\": [%.2f, %.2f, %.2f]", what[k], v[0], s / v.size(), v.back());
+    }
+    std::printf("}\n");
+  };
+  // K/V-step gathers: 1 wave alone, then 128 workgroups x 3 waves (the chained attention's shape)
+  {
+    unsigned long long* d_g;
+    CK(hipMalloc(&d_g, 4096 * sizeof(unsigned long long)));
+    std::vector<unsigned long long> tg(4096);
+    const long long region = (long long)32 << 20;
+    auto gather = [&](const char* label, int grid, int waves, bool flush) {
+      if (flush) hipLaunchKernelGGL(stream, dim3(1024), dim3(512), 0, 0, (const uint4*)A, big / 16, d_sink);
+      hipLaunchKernelGGL(kv_gather, dim3(grid), dim3(64 * waves), 0, 0, B, region, d_g, d_sink);
+      CK(hipDeviceSynchronize());
+      const int nw = grid * waves;
+      CK(hipMemcpy(tg.data(), d_g, nw * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      std::vector<double> v(nw);
+      for (int i = 0; i < nw; ++i) v[i] = tg[i] * 0.01;
+      std::sort(v.begin(), v.end());
+      std::printf("{\"case\": \"%s\", \"waves\": %d, \"kv_step_us_min_med_max\": [%.2f, %.2f, %.2f]}\n", label, nw,
+                  v[0], v[nw / 2], v[nw - 1]);
+    };
+    gather("kv_step_1wave_cold", 1, 1, true);
+    gather("kv_step_1wave_warm", 1, 1, false);
+    gather("kv_step_128x3_cold", 128, 3, true);
+    gather("kv_step_128x3_warm", 128, 3, false);
+    gather("kv_step_256x8_cold", 256, 8, true);
+    CK(hipFree(d_g));
+  }
+  run("first_touch_after_1GB_stream", true);
+  run("immediate_repeat", false);
+  run("repeat_after_1GB_stream", true);
+  run("immediate_repeat_2", false);
+  CK(hipFree(A));
+  CK(hipFree(B));
+  return 0;
+}
