@@ -350,7 +350,9 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                             n_kv_heads, head_dim, a_scale, a_n_splits, *a_part_o, *a_part_ml, *a_counters, att);
     TORCH_CHECK(a_n_splits > 1, "attention phase: the in-launch chunk merge needs n_splits > 1");
     cp.attn_g = (int)(n_q_heads / n_kv_heads);
-    if (a_row_table.has_value()) {
+    TORCH_CHECK(a_row_table.has_value(), "attention phase: a_row_table (per-row block tables) is required");
+    TORCH_CHECK(a_block_size == 16, "attention phase: 16-token KV blocks (mq_attention.h FINE addressing)");
+    {
       const Tensor& rtab = *a_row_table;
       TORCH_CHECK(rtab.is_cuda() && rtab.scalar_type() == at::kInt && rtab.dim() == 2 && rtab.is_contiguous() &&
                       rtab.size(0) >= M && rtab.size(1) <= 128 && rtab.size(1) % 2 == 0,

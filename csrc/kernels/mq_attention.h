@@ -7,8 +7,9 @@
 namespace {
 using namespace vwa;
 
+typedef __attribute__((address_space(1))) const int gint;  // global-space loads: vmcnt only (ld128)
 VWA_DEVICE int64_t kv_offset(const KVView& kv, int seq, int kvh, int t) {
-  const int blk = kv.block_table[(int64_t)seq * kv.table_stride + t / kv.block_size];
+  const int blk = *(gint*)(kv.block_table + (int64_t)seq * kv.table_stride + t / kv.block_size);
   return (int64_t)blk * kv.stride_block + (int64_t)kvh * kv.stride_head + (int64_t)(t % kv.block_size) * kv.stride_tok;
 }
 
@@ -73,8 +74,13 @@ VWA_DEVICE uint2 lds_tr16(const unsigned char* ptr) {
 // 16-byte global load through a native vector type: a struct (uint4) copy is emitted as a memcpy
 // that SROA cannot promote, and the V staging registers ended up in scratch (measured: 272 B of
 // scratch per lane and a vmcnt(0) after every scratch reload inside the key loop)
+// Through the GLOBAL address space: a flat (generic) load also counts on lgkmcnt, so every wait
+// for an LDS op or a lane shuffle after it (the block-id shuffles of the next key's address) also
+// waited for all K/V loads in flight -- the chained attention's 16 K/V loads per wave measured as
+// ~5 serialized round trips (6.6 us; the same gather alone: 1.2 us, tools/latency_probe.hip)
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 VWA_DEVICE uint4 ld128(const u16* ptr) {
-  const u32x4 v = *reinterpret_cast<const u32x4*>(ptr);
+  const u32x4 v = *(gu32x4*)(ptr);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
@@ -152,39 +158,40 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int n = lane & 15, g = lane >> 4;
 
-  // FINE: the Q fragments of the likely first item -- KV head bid % nkv, the group of rows
-  // [0, min(rows, RG)) (one decode row, or one sequence's jump-forward rows) -- are issued with
-  // the step metadata instead of one round trip after it; checked once the groups are known
-  uint4 qspec[NKS];
-  const int nr_spec = min(p.rows, RG);
-  if constexpr (FINE) {
-    const u16* qr = p.q + (int64_t)min(n / G, nr_spec - 1) * p.ldq + ((bid % nkv) * G + n % G) * D + 8 * g;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) qspec[ks] = *reinterpret_cast<const uint4*>(qr + 32 * ks);
-  }
-
   // ---- row groups of the whole step (<= 64 rows; every wave derives the same answer): runs of
   //      consecutive rows of one sequence, cut every RG rows from the run's start
   // per-row block tables (FINE, <= 4 rows): fetched with the sequence ids, two entries per lane
   // All of it in ONE round trip: branch-free buffer loads (past the end -> 0).  (The conditional
   // plain loads this replaces compiled to a wait after each load: five dependent round trips.)
-  const bool rowtab = FINE && p.row_table != nullptr && p.rows <= 4;
+  // FINE (the chained launch, <= 4 rows) always has them (chain_make requires a_row_table):
+  // K/V addresses come from lane shuffles only, no table loads whose waits the K/V loads share
+  constexpr bool rowtab = FINE;
   const __amdgpu_buffer_rsrc_t r_rt = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<int*>(p.row_table), (short)0, rowtab ? p.rows * p.rt_stride * 4 : 0, 0x00020000);
+  // Loaded by wave 0 only and shared through LDS (the per-item partials area, free until the
+  // first item's outputs): every wave of every workgroup asking for the same few lines at the
+  // launch's start is 8x the requests on the same L2 lines.
+  int* s_meta = reinterpret_cast<int*>(lds + L::ow);  // [4][128] row tables | [64] seq ids | [64] contexts
+  if (w == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      *reinterpret_cast<int2*>(s_meta + r * 128 + 2 * lane) = __builtin_bit_cast(
+          int2, __builtin_amdgcn_raw_buffer_load_b64(
+                    r_rt, 2 * lane < p.rt_stride ? (r * p.rt_stride + 2 * lane) * 4 : 0x7FFFFFF0, 0, 0));
+    const __amdgpu_buffer_rsrc_t r_sid =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.seq_ids), (short)0, p.rows * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_ctx =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.ctx_lens), (short)0, p.rows * 4, 0x00020000);
+    s_meta[512 + lane] = (int)__builtin_amdgcn_raw_buffer_load_b32(r_sid, lane * 4, 0, 0);
+    s_meta[576 + lane] = (int)__builtin_amdgcn_raw_buffer_load_b32(r_ctx, lane * 4, 0, 0);
+  }
+  __syncthreads();
+  stamp(12);  // (diagnostic: step metadata in LDS)
   int2 rt[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
-    rt[r] = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
-                                         r_rt, 2 * lane < p.rt_stride ? (r * p.rt_stride + 2 * lane) * 4 : 0x7FFFFFF0,
-                                         0, 0));
-  const __amdgpu_buffer_rsrc_t r_sid =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.seq_ids), (short)0, p.rows * 4, 0x00020000);
-  const __amdgpu_buffer_rsrc_t r_ctx =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.ctx_lens), (short)0, p.rows * 4, 0x00020000);
-  const int sl_ld = (int)__builtin_amdgcn_raw_buffer_load_b32(r_sid, lane * 4, 0, 0);
-  const int cl_ld = (int)__builtin_amdgcn_raw_buffer_load_b32(r_ctx, lane * 4, 0, 0);
-  const int sl = lane < p.rows ? sl_ld : -1;
-  const int cl = lane < p.rows ? cl_ld : 0;
+  for (int r = 0; r < 4; ++r) rt[r] = *reinterpret_cast<const int2*>(s_meta + r * 128 + 2 * lane);
+  const int sl = lane < p.rows ? s_meta[512 + lane] : -1;
+  const int cl = lane < p.rows ? s_meta[576 + lane] : 0;
   const int sp = __shfl(sl, lane > 0 ? lane - 1 : 0, 64);
   const unsigned long long run_starts = __ballot(lane < p.rows && (lane == 0 || sl != sp));
   const int run0 = 63 - __builtin_clzll(run_starts & ((2ull << lane) - 1ull));  // lane 0 always starts a run
@@ -212,6 +219,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   const int run_end = later ? __builtin_ctzll(later) : p.rows;
   const int nr = min(RG, run_end - r0);  // rows in this group
   const int seq = __shfl(sl, r0, 64);
+  if (item == bid) stamp(11);  // (diagnostic: before the item's barrier)
   __syncthreads();  // the previous item's LDS readers are done
   if (item == bid) stamp(9);  // step rows / contexts known
   const int c_src = __shfl(cl, min(r0 + lane, 63), 64);
@@ -236,51 +244,60 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
 
   // ---- Q^T fragments (B operand): Q[column n][dims 32ks + 8g ..], pre-scaled by scale*log2(e)
   bf16x8 qf[NKS];
-  {
+  auto make_qf = [&]() {
     const float qs = p.scale * 1.4426950408889634f;
     const u16* qr = p.q + (int64_t)(r0 + min(rho, nr - 1)) * p.ldq + (kvh * G + n % G) * D + 8 * g;
-    const bool spec = FINE && item == bid && r0 == 0 && nr == nr_spec;  // (kvh == bid % nkv here)
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       float f[8];
-      unpack8(spec ? qspec[ks] : *reinterpret_cast<const uint4*>(qr + 32 * ks), f);
+      unpack8(ld128(qr + 32 * ks), f);
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = rho < nr ? f[j] * qs : 0.f;
       qf[ks] = as_bf16x8(pack8(f));
     }
+  };
+  if constexpr (DB) {
+    make_qf();
+    if (item == bid) stamp(10);  // q fragments in registers
   }
-
-  if (item == bid) stamp(10);  // q fragments in registers
   // (measured: staging the wave's block-table entries in lanes and fetching them with __shfl,
   // instead of the per-key table loads below, was 1.5-3 us SLOWER on every shape)
   const int2 rtr = r0 == 0 ? rt[0] : r0 == 1 ? rt[1] : r0 == 2 ? rt[2] : rt[3];  // the group's row table
-  auto kv_off = [&](int key) -> int64_t {
-    if (rowtab) {
-      const int b = key / p.kv.block_size;
-      const int ex = __shfl(rtr.x, b >> 1, 64), ey = __shfl(rtr.y, b >> 1, 64);
-      const int blk = (b & 1) ? ey : ex;
-      return (int64_t)blk * p.kv.stride_block + (int64_t)kvh * p.kv.stride_head +
-             (int64_t)(key % p.kv.block_size) * p.kv.stride_tok;
-    }
-    return kv_offset(p.kv, seq, kvh, key);
-  };
 
   // K: A-operand row n of tile t is key kb + 8(n>>2) + 4t + (n&3) (so the S^T accumulator of lane
   // (n, g) holds keys kb + 8g + 4t + i); V: 32 rows x NCH chunks, chunk idx = i*64 + lane
+  // every address first (block ids: row-table shuffles or one round of table loads), then all 16
+  // loads back to back -- no wait between them
+  // (the two block-id sources in separate uniform branches, each finishing its offsets: a shared
+  // helper left a vmcnt(0) at every join, which also waited for the Q loads in flight)
   auto load_step = [&](int kb, uint4 (&kr)[2][NKS], uint4 (&vr)[NVL]) {
+    int64_t ko[2], vo[NVL];
+    auto offsets = [&](auto off) {
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int key = min(kb + 8 * (n >> 2) + 4 * t + (n & 3), kmax);
-      const u16* kp = p.kv.k + kv_off(key) + 8 * g;
+      for (int t = 0; t < 2; ++t) ko[t] = off(min(kb + 8 * (n >> 2) + 4 * t + (n & 3), kmax));
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) kr[t][ks] = ld128(kp + 32 * ks);
+      for (int i = 0; i < NVL; ++i) vo[i] = off(min(kb + (i * 64 + lane) / NCH, kmax));
+    };
+    if constexpr (rowtab) {
+      // 16-key blocks (chain_make checks) and a step start kb that is a multiple of 32: the step
+      // spans exactly blocks kb/16 (even: entry .x) and kb/16 + 1 (.y) of one row-table lane, two
+      // wave-uniform block ids read straight into scalars -- per key only a select and a multiply
+      // (the per-key shuffles and 64-bit products before measured ~1 us of issue per step)
+      const int tl = kb >> 5;
+      const int64_t bA = (int64_t)__builtin_amdgcn_readlane(rtr.x, tl) * p.kv.stride_block,
+                    bB = (int64_t)__builtin_amdgcn_readlane(rtr.y, tl) * p.kv.stride_block;
+      const int64_t hoff = (int64_t)kvh * p.kv.stride_head;
+      const int st = (int)p.kv.stride_tok;
+      offsets([&](int key) -> int64_t { return ((key & 16) ? bB : bA) + hoff + (key & 15) * st; });
+    } else {
+      offsets([&](int key) -> int64_t { return kv_offset(p.kv, seq, kvh, key); });
     }
 #pragma unroll
-    for (int i = 0; i < NVL; ++i) {
-      const int idx = i * 64 + lane;
-      const int key = min(kb + idx / NCH, kmax);
-      vr[i] = ld128(p.kv.v + kv_off(key) + 8 * (idx % NCH));
-    }
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) kr[t][ks] = ld128(p.kv.k + ko[t] + 8 * g + 32 * ks);
+#pragma unroll
+    for (int i = 0; i < NVL; ++i) vr[i] = ld128(p.kv.v + vo[i] + 8 * ((i * 64 + lane) % NCH));
   };
 
   float m_run = -INFINITY, l_run = 0.f;  // per query column (log2 units); l is this lane's share
@@ -349,16 +366,22 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
       }
     }
   } else {  // single register set (the chained launch holds the next GEMM's weights meanwhile)
+    // the first step's K/V loads go out before the Q fragments are built (Q's round trip and
+    // scaling overlap the K/V round trip)
+    bool have_q = false;
     for (int s = FINE ? w : 0; s < nsteps; s += FINE ? kWv : 1) {
       uint4 kA[2][NKS], vA[NVL];
       if (item == bid && s == w) stamp(13);  // (diagnostic: about to issue the first K/V step)
       load_step(wb + s * kMqStep, kA, vA);
+      if (!have_q) {
+        make_qf();
+        have_q = true;
+      }
       if (item == bid && s == w) stamp(15);  // (diagnostic stamp 15: the wave's first K/V step landed)
       compute_step(wb + s * kMqStep, kA, vA);
     }
   }
 
-  if (item == bid) stamp(11);  // K/V of the wave's steps consumed
   // ---- per-wave (m, l, O) -> LDS; O^T accumulator of lane (n, g): dims 16dt + 4g + i
   float l_tot = l_run + __shfl_xor(l_run, 16, 64);
   l_tot += __shfl_xor(l_tot, 32, 64);
@@ -411,7 +434,6 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
 
   // ---- ticket (same protocol as the split kernel): drained sc1 stores, then one counter add
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (item == bid) stamp(12);  // partials stored
   __syncthreads();
   if (threadIdx.x == 0) {
     int* cnt = p.counters + r0 * nkv + kvh;

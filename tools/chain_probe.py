@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--wpol", type=int, default=0, help="weight-load cache policy: 0 default, 2 nt")
     ap.add_argument("--no-wait", action="store_true",
                     help="DIAGNOSTIC: barriers arrive but never wait (wrong results): phase cost without dependencies")
-    ap.add_argument("--row-table", action="store_true", help="attention: per-row block tables (a_row_table)")
+    ap.add_argument("--row-table", action="store_true", help="(always on: the chained attention requires them)")
     ap.add_argument("--ctx", type=int, default=1100, help="attention context length (tokens)")
     ap.add_argument("--kv-tok-major", action="store_true",
                     help="K/V blocks stored [block][token][head][dim] (a head's 16 tokens at 2 KB stride) "
@@ -75,7 +75,7 @@ def main():
                    a_part_o=torch.zeros(M * ns * nq * hd, device=dev), a_part_ml=torch.zeros(M * ns * nq * 2, device=dev),
                    a_counters=torch.zeros(M * nkv, dtype=torch.int32, device=dev))
         ag = nq // nkv
-        if a.row_table:  # per-row copies of the sequence's block table (one table round trip less)
+        if True:  # per-row copies of the sequence's block table (required by the chained attention)
             rt = torch.zeros(M, 128, dtype=torch.int32, device=dev)
             rt[:, :nblk] = table[0]
             akw["a_row_table"] = rt
@@ -133,8 +133,8 @@ def main():
     if a.attn:  # in-attention stamps 9..14 of the attention workgroups (slots stay 0 elsewhere)
         full = ts.view(-1, 16)[:cus].double().cpu()
         t0 = full[:, 0].min()
-        att = full[full[:, 11] > 0]
-        names = ["ctx_known", "q_ready", "kv_done", "partials_stored", "kv_issue", "merged", "kv_landed"]
+        att = full[full[:, 9] > 0]
+        names = ["ctx_known", "q_ready", "pre_sync", "meta_landed", "kv_issue", "merged", "kv_landed"]
         extra = {}
         for j, nm in enumerate(names):
             col = att[:, 9 + j]

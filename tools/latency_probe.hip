@@ -65,6 +65,32 @@ __global__ void kv_gather(const char* base, long long region, unsigned long long
   if (acc == 0x12345678u) sink[2] = (int)acc;
 }
 
+// the chained attention's prologue: every workgroup reads the SAME step metadata (wave 0: 4 x 8 B +
+// 2 x 4 B per lane over ~2.5 KB) and every wave the same 8 KB of Q (4 x 16 B per lane); lane 0 of
+// wave 0 stamps the landing of both
+__global__ void meta_broadcast(const char* meta, const char* q, int per_wave_q, unsigned long long* ticks, int* sink) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long t0, t1;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  unsigned acc = 0;
+  if (per_wave_q || w == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = *reinterpret_cast<const uint4*>(q + ((w * 4 + k) * 64 + lane) % 512 * 16);
+      acc ^= v.x;
+    }
+  }
+  if (w == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc ^= *reinterpret_cast<const unsigned*>(meta + r * 512 + lane * 8);
+    acc ^= *reinterpret_cast<const unsigned*>(meta + 2048 + lane * 4);
+    acc ^= *reinterpret_cast<const unsigned*>(meta + 2304 + lane * 4);
+  }
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+  if (threadIdx.x == 0) ticks[blockIdx.x] = t1 - t0;
+  if (acc == 0x12345678u) sink[3] = (int)acc;
+}
+
 // every lane of every workgroup streams its share of `bytes` (the weight stream's cache pressure)
 __global__ void stream(const uint4* p, size_t n16, int* sink) {
   unsigned acc = 0;
@@ -138,6 +164,21 @@ int main() {
     gather("kv_step_128x3_cold", 128, 3, true);
     gather("kv_step_128x3_warm", 128, 3, false);
     gather("kv_step_256x8_cold", 256, 8, true);
+    auto meta = [&](const char* label, int grid, int q_all, bool flush) {
+      if (flush) hipLaunchKernelGGL(stream, dim3(1024), dim3(512), 0, 0, (const uint4*)A, big / 16, d_sink);
+      hipLaunchKernelGGL(meta_broadcast, dim3(grid), dim3(512), 0, 0, B + (40 << 20), B + (41 << 20), q_all, d_g, d_sink);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(tg.data(), d_g, grid * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+      std::vector<double> v(grid);
+      for (int i = 0; i < grid; ++i) v[i] = tg[i] * 0.01;
+      std::sort(v.begin(), v.end());
+      std::printf("{\"case\": \"%s\", \"workgroups\": %d, \"meta_us_min_med_max\": [%.2f, %.2f, %.2f]}\n", label,
+                  grid, v[0], v[grid / 2], v[grid - 1]);
+    };
+    meta("meta_1wg_cold", 1, 1, true);
+    meta("meta_256wg_q_all_waves_cold", 256, 1, true);
+    meta("meta_256wg_q_wave0_cold", 256, 0, true);
+    meta("meta_256wg_q_all_waves_warm", 256, 1, false);
     CK(hipFree(d_g));
   }
   run("first_touch_after_1GB_stream", true);

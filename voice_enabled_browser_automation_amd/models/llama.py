@@ -212,17 +212,19 @@ class LlamaModel:
         # the layer's decode attention as the launch's first phase (VWA_CHAIN_ATTN, default on;
         # same-box bench A/B/A: GPU time per decode step 3868 vs 3897 / 3907 us, p50 276 vs 284 /
         # 285 ms, profiles/r1_bench_results.jsonl; skinny_stream.hip chain_kernel)
+        # (the chained attention addresses K/V through per-row copies of the block table, which
+        # the step buffers keep for contexts of <= 128 blocks, in 16-token blocks: otherwise the
+        # separate launch)
         attn = (self.hd == 128 and self.nq // self.nkv in (4, 8) and ops.env_flag("VWA_CHAIN_ATTN", True)
-                and ops.decode_n_splits(bufs.max_ctx) > 1)
+                and ops.decode_n_splits(bufs.max_ctx) > 1 and getattr(bufs, "rt_cols", 0) > 0
+                and kv.k[li].shape[2] == 16)
         a = {}
         if attn:
             lay = ops.KVLayout.paged(kv.k[li], kv.v[li], bufs.block_table)
             a = dict(a_q=bufs.q[:M], a_k=lay.k, a_v=lay.v, a_table=lay.table, a_block_size=lay.block_size,
                      a_sb=lay.sb, a_sh=lay.sh, a_st=lay.st, a_ctx=bufs.ctx_lens, a_seq=bufs.seq_ids,
                      a_scale=self.scale, a_n_splits=ops.decode_n_splits(bufs.max_ctx), a_part_o=bufs.part_o,
-                     a_part_ml=bufs.part_ml, a_counters=bufs.attn_cnt)
-            if getattr(bufs, "rt_cols", 0) and ops.env_flag("VWA_ROW_TABLE", True):
-                a["a_row_table"] = bufs.row_table
+                     a_part_ml=bufs.part_ml, a_counters=bufs.attn_cnt, a_row_table=bufs.row_table)
         tiled = isinstance(L.o, ops.TiledWeight)
         wsel = (lambda w: w.t) if tiled else (lambda w: w)  # noqa: E731
         desc, lds = ops.ext().chain_make(
