@@ -25,6 +25,18 @@ namespace vwa {
 
 constexpr int kWave = 64;
 
+// Global-address-space view of a pointer.  Pointers read from a descriptor are generic, and a
+// generic (FLAT) access also counts on lgkmcnt: every later wait for an LDS op or a lane shuffle
+// then waits for it as well.  Accesses through gp() are global_* instructions (vmcnt only).
+template <class T>
+VWA_DEVICE __attribute__((address_space(1))) T* gp(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
+}
+template <class T>
+VWA_DEVICE T gld(const T* p) {
+  return *gp(p);
+}
+
 VWA_DEVICE float bf2f(u16 v) { return __uint_as_float(((uint32_t)v) << 16); }
 
 VWA_DEVICE u16 f2bf(float f) {

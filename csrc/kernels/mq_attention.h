@@ -96,12 +96,12 @@ template <bool SC1>
 VWA_DEVICE void store_out(u16* dst, uint4 v) {
   if constexpr (SC1) {
     // agent-scope write-through: read by other workgroups later in the same (chained) launch
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)v.x | ((unsigned long long)v.y << 32),
+    __hip_atomic_store(gp(reinterpret_cast<unsigned long long*>(dst)), (unsigned long long)v.x | ((unsigned long long)v.y << 32),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst) + 1, (unsigned long long)v.z | ((unsigned long long)v.w << 32),
+    __hip_atomic_store(gp(reinterpret_cast<unsigned long long*>(dst) + 1), (unsigned long long)v.z | ((unsigned long long)v.w << 32),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
-    *reinterpret_cast<uint4*>(dst) = v;
+    *gp(reinterpret_cast<u32x4*>(dst)) = u32x4{v.x, v.y, v.z, v.w};
   }
 }
 
@@ -437,9 +437,9 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   __syncthreads();
   if (threadIdx.x == 0) {
     int* cnt = p.counters + r0 * nkv + kvh;
-    const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int ticket = __hip_atomic_fetch_add(gp(cnt), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = (ticket == nact - 1);
-    if (last) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (last) __hip_atomic_store(gp(cnt), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = last;
   }
   __syncthreads();

@@ -58,18 +58,18 @@ struct EpiPre {
 // stores, which bypass the non-coherent per-XCD L2 state another workgroup could have left.
 template <bool SC1>
 VWA_DEVICE u16 ld_u16(const u16* p) {
-  if constexpr (SC1) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else return *p;
+  if constexpr (SC1) return __hip_atomic_load(gp(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return gld(p);
 }
 template <bool SC1>
 VWA_DEVICE void st_u16(u16* p, u16 v) {
-  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
+  if constexpr (SC1) __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *gp(p) = v;
 }
 template <bool SC1>
 VWA_DEVICE void st_f32(float* p, float v) {
-  if constexpr (SC1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
+  if constexpr (SC1) __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *gp(p) = v;
 }
 
 template <int EPI, int NT, bool SC1 = false>
@@ -79,23 +79,23 @@ VWA_DEVICE void epi_values(const SkinnyParams& p, int tile, int o, EpiPre& e) {
     if (o >= p.M * 16) return;
     const int m = o >> 4, q = o & 15;
     if (p.w_scale) {
-      e.cs0 = p.w_scale[n0 + q];
-      e.cs1 = p.w_scale[n0 + (EPI == EPI_SWIGLU ? 16 + q : (q ^ 8))];
+      e.cs0 = gld(p.w_scale + n0 + q);
+      e.cs1 = gld(p.w_scale + n0 + (EPI == EPI_SWIGLU ? 16 + q : (q ^ 8)));
     }
     if constexpr (EPI == EPI_QKV) {
       const int hd = p.head_dim, half = hd >> 1, t = (n0 % hd) >> 4;
-      e.slot = p.slots[m];
+      e.slot = gld(p.slots + m);
       if (p.use_rope) {
         const int di = (q < 8) ? (8 * t + q) : (8 * t + q - 8);
-        const int pos = p.positions[m];
-        e.rc = p.rope[((size_t)pos * half + di) * 2 + 0];
-        e.rsn = p.rope[((size_t)pos * half + di) * 2 + 1];
+        const int pos = gld(p.positions + m);
+        e.rc = gld(p.rope + ((size_t)pos * half + di) * 2 + 0);
+        e.rsn = gld(p.rope + ((size_t)pos * half + di) * 2 + 1);
       }
     }
   } else {
     if (o >= p.M * 16 * NT) return;
     const int m = o / (16 * NT), nn = o % (16 * NT);
-    if (p.w_scale) e.cs0 = p.w_scale[n0 + nn];
+    if (p.w_scale) e.cs0 = gld(p.w_scale + n0 + nn);
     if constexpr (EPI == EPI_RESID) e.r = bf2f(ld_u16<SC1>(p.R + (size_t)m * p.ldr + n0 + nn));
   }
 }
@@ -122,7 +122,7 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
 #pragma unroll
     for (int ww = 0; ww < KS; ++ww) s += red[((ww * NT + nt) * 4 + i) * 64 + ln];
     // split tile (chain kernel): the other workgroup's partial sums, published with sc1 stores
-    if (partner) s += __hip_atomic_load(partner + m * 16 * NT + nn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (partner) s += __hip_atomic_load(gp(partner + m * 16 * NT + nn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return s;
   };
   auto operands = [&](int o) {
@@ -138,8 +138,8 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
       const float sc = rs[m];
       float gv = red_at(m, q) * sc * e.cs0, uv = red_at(m, 16 + q) * sc * e.cs1;
       if (p.bias) {
-        gv += bf2f(p.bias[n0 + q]);
-        uv += bf2f(p.bias[n0 + 16 + q]);
+        gv += bf2f(gld(p.bias + n0 + q));
+        uv += bf2f(gld(p.bias + n0 + 16 + q));
       }
       st_u16<SC1>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + tile * 16 + q, f2bf(silu(gv) * uv));
     }
@@ -154,14 +154,14 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
       const float sc = rs[m];
       float v = red_at(m, q), pv = red_at(m, q ^ 8);
       if (mus) {
-        v -= mus[m] * p.ln_c[n0 + q];
-        pv -= mus[m] * p.ln_c[n0 + (q ^ 8)];
+        v -= mus[m] * gld(p.ln_c + n0 + q);
+        pv -= mus[m] * gld(p.ln_c + n0 + (q ^ 8));
       }
       v *= sc * e.cs0;
       pv *= sc * e.cs1;
       if (p.bias) {
-        v += bf2f(p.bias[n0 + q]);
-        pv += bf2f(p.bias[n0 + (q ^ 8)]);
+        v += bf2f(gld(p.bias + n0 + q));
+        pv += bf2f(gld(p.bias + n0 + (q ^ 8)));
       }
       const int d = (q < 8) ? (8 * t + q) : (half + 8 * t + q - 8);
       if (p.use_rope && !is_v) v = (q < 8) ? (v * e.rc - pv * e.rsn) : (v * e.rc + pv * e.rsn);
@@ -184,9 +184,9 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
       const int n = n0 + nn;
       const EpiPre e = operands(o);
       float v = red_at(m, nn);
-      if (mus) v -= mus[m] * p.ln_c[n];
+      if (mus) v -= mus[m] * gld(p.ln_c + n);
       v *= rs[m] * e.cs0;
-      if (p.bias) v += bf2f(p.bias[n]);
+      if (p.bias) v += bf2f(gld(p.bias + n));
       if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
       if constexpr (EPI == EPI_RESID) v += e.r;
       if (p.y_f32) st_f32<SC1>(reinterpret_cast<float*>(p.Y) + (size_t)m * p.ldy + n, v);
@@ -607,7 +607,7 @@ VWA_DEVICE unsigned long long chain_arrive(unsigned long long* bar, int nwg, int
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are performed
   __syncthreads();
   if (mode >= 4) {
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(&bar[16 * (blockIdx.x & 7)], 1ull, __ATOMIC_RELAXED,
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(gp(&bar[16 * (blockIdx.x & 7)]), 1ull, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
     next += (unsigned long long)nwg;
     return next;
@@ -615,16 +615,16 @@ VWA_DEVICE unsigned long long chain_arrive(unsigned long long* bar, int nwg, int
   unsigned long long target = 0;
   if (threadIdx.x == 0) {
     if (mode == 0) {
-      const unsigned long long t = __hip_atomic_fetch_add(&bar[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long t = __hip_atomic_fetch_add(gp(&bar[0]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       target = (t / (unsigned long long)nwg + 1ull) * (unsigned long long)nwg;
     } else {
       const int grp = blockIdx.x & 7;
       const unsigned long long members = (unsigned long long)((nwg - grp + 7) >> 3);
       const unsigned long long ngroups = (unsigned long long)(nwg < 8 ? nwg : 8);
       const unsigned long long t =
-          __hip_atomic_fetch_add(&bar[16 * grp], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(gp(&bar[16 * grp]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (t % members == members - 1ull)
-        __hip_atomic_fetch_add(&bar[kBarTop], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(gp(&bar[kBarTop]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       target = (t / members + 1ull) * ngroups;
     }
   }
@@ -644,7 +644,7 @@ VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, i
       while ((long long)(bar_sum8(bar) - tgt) < 0) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > kChainSpinLimit) {
-          if (threadIdx.x == 0) __hip_atomic_store(&bar[kBarErr], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (threadIdx.x == 0) __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }
@@ -667,7 +667,7 @@ VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, i
         if ((long long)(v - tgt) >= 0) break;
         __builtin_amdgcn_s_sleep(1);
         if (++spins > kChainSpinLimit) {
-          if (threadIdx.x == 0) __hip_atomic_store(&bar[kBarErr], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (threadIdx.x == 0) __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }
@@ -678,10 +678,10 @@ VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, i
   if (threadIdx.x == 0) {
     unsigned long long* w = mode == 0 ? &bar[0] : &bar[kBarTop];
     int spins = 0;
-    while ((long long)(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+    while ((long long)(__hip_atomic_load(gp(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > kChainSpinLimit) {
-        __hip_atomic_store(&bar[kBarErr], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -928,9 +928,9 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      const unsigned t = __hip_atomic_fetch_add(&cp.tickets[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned t = __hip_atomic_fetch_add(gp(&cp.tickets[tile]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = t == 1u;
-      if (last) __hip_atomic_store(&cp.tickets[tile], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (last) __hip_atomic_store(gp(&cp.tickets[tile]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *s_flag = last;
     }
     __syncthreads();
@@ -1020,7 +1020,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   unsigned long long bar_next = chain_base(bar, nwg, cp.bar_mode);  // mode >= 4: running target
   int nts = 0;
   auto stamp = [&]() {
-    if (cp.ts && threadIdx.x == 0) cp.ts[blockIdx.x * 16 + nts] = __builtin_amdgcn_s_memrealtime();
+    if (cp.ts && threadIdx.x == 0) *gp(cp.ts + blockIdx.x * 16 + nts) = __builtin_amdgcn_s_memrealtime();
     ++nts;
   };
   stamp();
@@ -1064,7 +1064,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                         }, &n_attn, [&](int k) {
                                                           if ((k == 15 || k == 10) && cp.ts) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                                                           if (cp.ts && threadIdx.x == 0)
-                                                            cp.ts[blockIdx.x * 16 + k] = __builtin_amdgcn_s_memrealtime();
+                                                            *gp(cp.ts + blockIdx.x * 16 + k) = __builtin_amdgcn_s_memrealtime();
                                                         });
     if (!idle) setup0(n_attn);
     stamp();
