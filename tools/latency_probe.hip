@@ -12,6 +12,8 @@
 #include <algorithm>
 #include <vector>
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 #define CK(x)                                                                 \
   do {                                                                        \
     hipError_t e_ = (x);                                                      \
@@ -89,6 +91,89 @@ __global__ void meta_broadcast(const char* meta, const char* q, int per_wave_q, 
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
   if (threadIdx.x == 0) ticks[blockIdx.x] = t1 - t0;
   if (acc == 0x12345678u) sink[3] = (int)acc;
+}
+
+// The decode GEMMs' weight stream, isolated: every wave of 256 x 8 streams its contiguous share of
+// `bytes` as "items" of 16 x 1 KB-contiguous load instructions (the tiled-weight pattern) with SETS
+// register sets in flight (the chained kernel: 2), consuming each set with a cheap reduction.
+template <int SETS, int NL = 16>
+__global__ __launch_bounds__(1024) void item_stream(const char* base, size_t bytes, int* sink) {
+  const int lane = threadIdx.x & 63, wpg = blockDim.x >> 6;
+  const size_t wid = (size_t)blockIdx.x * wpg + (threadIdx.x >> 6), nwaves = (size_t)gridDim.x * wpg;
+  const size_t items = bytes / (NL * 1024), per = items / nwaves;
+  const char* p = base + wid * per * (NL * 1024) + lane * 16;
+  u32x4 r[SETS][NL];
+  unsigned acc = 0;
+  auto load = [&](int s, size_t it) {
+#pragma unroll
+    for (int i = 0; i < NL; ++i) r[s][i] = *(__attribute__((address_space(1))) const u32x4*)(p + it * (NL * 1024) + i * 1024);
+  };
+#pragma unroll
+  for (int s = 0; s < SETS; ++s) load(s, s);
+  for (size_t it = 0; it < per; it += SETS) {
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) {
+#pragma unroll
+      for (int i = 0; i < NL; ++i) acc ^= r[s][i].x ^ r[s][i].w;
+      if (it + s + SETS < per) load(s, it + s + SETS);
+    }
+  }
+  if (acc == 0x12345678u) sink[4] = (int)acc;
+}
+
+// the chained kernel's form exactly: 8 waves x SETS register sets of 16 buffer loads (32-bit
+// offsets: no 64-bit address registers), loads of set s re-issued right after its use
+template <int SETS>
+__global__ __launch_bounds__(512) void item_stream_buf(const char* base, size_t bytes, int* sink) {
+  const int lane = threadIdx.x & 63;
+  const unsigned wid = blockIdx.x * 8 + (threadIdx.x >> 6), nwaves = gridDim.x * 8;
+  const unsigned items = (unsigned)(bytes / 16384), per = items / nwaves;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+  u32x4 v[SETS][16];
+  unsigned acc = 0;
+  const unsigned b0 = wid * per * 16384u + lane * 16u;
+  auto load = [&](int s, unsigned it) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[s][i] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(b0 + it * 16384u + i * 1024u), 0, 0);
+  };
+#pragma unroll
+  for (int s = 0; s < SETS; ++s) load(s, s);
+  for (unsigned it = 0; it < per; it += SETS) {
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc ^= v[s][i].x ^ v[s][i].w;
+      if (it + s + SETS < per) load(s, it + s + SETS);
+    }
+  }
+  if (acc == 0x12345678u) sink[4] = (int)acc;
+}
+
+// the same items, interleaved: item j of wave w sits at (j * nwaves + w) * 16 KB, so the waves in
+// flight together read one contiguous region
+template <int SETS>
+__global__ __launch_bounds__(512) void item_stream_il(const char* base, size_t bytes, int* sink) {
+  const int lane = threadIdx.x & 63;
+  const size_t wid = (size_t)blockIdx.x * 8 + (threadIdx.x >> 6), nwaves = (size_t)gridDim.x * 8;
+  const size_t items = bytes / 16384, per = items / nwaves;
+  u32x4 r[SETS][16];
+  unsigned acc = 0;
+  auto load = [&](int s, size_t it) {
+    const char* p = base + (it * nwaves + wid) * 16384 + lane * 16;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[s][i] = *(__attribute__((address_space(1))) const u32x4*)(p + i * 1024);
+  };
+#pragma unroll
+  for (int s = 0; s < SETS; ++s) load(s, s);
+  for (size_t it = 0; it < per; it += SETS) {
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc ^= r[s][i].x ^ r[s][i].w;
+      if (it + s + SETS < per) load(s, it + s + SETS);
+    }
+  }
+  if (acc == 0x12345678u) sink[4] = (int)acc;
 }
 
 // every lane of every workgroup streams its share of `bytes` (the weight stream's cache pressure)
@@ -180,6 +265,59 @@ int main() {
     meta("meta_256wg_q_wave0_cold", 256, 0, true);
     meta("meta_256wg_q_all_waves_warm", 256, 1, false);
     CK(hipFree(d_g));
+  }
+  {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto bw = [&](const char* label, auto kern, int grid, size_t bytes, int threads = 512) {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, 0, (const char*)A, bytes, d_sink);  // warm-up
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, 0, (const char*)A, bytes, d_sink);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      std::printf("{\"case\": \"%s\", \"MB\": %zu, \"us_per_launch\": %.2f, \"TBps\": %.3f}\n", label, bytes >> 20,
+                  ms * 200.0, bytes / (ms / 5 * 1e-3) / 1e12);
+    };
+    bw("items_2sets_436MB", item_stream<2>, 256, (size_t)436 << 20);
+    bw("buf_2sets_8waves_436MB", item_stream_buf<2>, 256, (size_t)436 << 20);
+    bw("buf_1set_8waves_436MB", item_stream_buf<1>, 256, (size_t)436 << 20);
+    bw("buf_3sets_8waves_436MB", item_stream_buf<3>, 256, (size_t)436 << 20);
+    bw("buf_2sets_8waves_512wg_436MB", item_stream_buf<2>, 512, (size_t)436 << 20);
+    bw("items_1set_436MB", item_stream<1>, 256, (size_t)436 << 20);
+    bw("items_1set_16waves_436MB", item_stream<1>, 256, (size_t)436 << 20, 1024);
+    bw("items_2sets_8loads_16waves_436MB", item_stream<2, 8>, 256, (size_t)436 << 20, 1024);
+    bw("items_1set_32loads_436MB", item_stream<1, 32>, 256, (size_t)436 << 20);
+    bw("items_1set_8loads_436MB", item_stream<1, 8>, 256, (size_t)436 << 20);
+    bw("items_1set_4waves_436MB", item_stream<1>, 256, (size_t)436 << 20, 256);
+    bw("items_2sets_8loads_436MB", item_stream<2, 8>, 256, (size_t)436 << 20);
+    bw("items_4sets_8loads_436MB", item_stream<4, 8>, 256, (size_t)436 << 20);
+    bw("items_4sets_4loads_436MB", item_stream<4, 4>, 256, (size_t)436 << 20);
+    bw("items_8sets_4loads_436MB", item_stream<8, 4>, 256, (size_t)436 << 20);
+    bw("items_1set_512wg_436MB", item_stream<1>, 512, (size_t)436 << 20);
+    bw("items_2sets_8loads_512wg_436MB", item_stream<2, 8>, 512, (size_t)436 << 20);
+    bw("items_2sets_1GB", item_stream<2>, 256, (size_t)1 << 30);
+    bw("items_2sets_117MB", item_stream<2>, 256, (size_t)117 << 20);
+    bw("items_2sets_50MB", item_stream<2>, 256, (size_t)50 << 20);
+    bw("items_2sets_512wg_436MB", item_stream<2>, 512, (size_t)436 << 20);
+    // linear sweep: consecutive lanes / waves / workgroups on consecutive 16-byte pieces
+    auto sweep = [&](const char* label, int grid, size_t bytes) {
+      hipLaunchKernelGGL(stream, dim3(grid), dim3(512), 0, 0, (const uint4*)A, bytes / 16, d_sink);
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(stream, dim3(grid), dim3(512), 0, 0, (const uint4*)A, bytes / 16, d_sink);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      std::printf("{\"case\": \"%s\", \"MB\": %zu, \"us_per_launch\": %.2f, \"TBps\": %.3f}\n", label, bytes >> 20,
+                  ms * 200.0, bytes / (ms / 5 * 1e-3) / 1e12);
+    };
+    sweep("linear_sweep_256wg_436MB", 256, (size_t)436 << 20);
+    sweep("linear_sweep_1024wg_436MB", 1024, (size_t)436 << 20);
+    sweep("linear_sweep_2048wg_1GB", 2048, (size_t)1 << 30);
+    bw("items_interleaved_2sets_436MB", item_stream_il<2>, 256, (size_t)436 << 20);
   }
   run("first_touch_after_1GB_stream", true);
   run("immediate_repeat", false);
