@@ -337,7 +337,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   cp.part = reinterpret_cast<float*>(work.data_ptr<int>() + 8192);
   cp.part_floats = (int)(work.numel() - 8192);
   if (ts.has_value()) {
-    TORCH_CHECK(ts->is_cuda() && ts->scalar_type() == at::kLong && ts->numel() >= 1024 * 16, "ts must be int64[>=16384]");
+    TORCH_CHECK(ts->is_cuda() && ts->scalar_type() == at::kLong && ts->numel() >= 1024 * 32, "ts must be int64[>=32768]");
     cp.ts = reinterpret_cast<unsigned long long*>(ts->data_ptr<int64_t>());
   }
   if (a_q.has_value()) {  // decode attention as the launch's first phase (its output is `att`)

@@ -192,6 +192,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   for (int r = 0; r < 4; ++r) rt[r] = *reinterpret_cast<const int2*>(s_meta + r * 128 + 2 * lane);
   const int sl = lane < p.rows ? s_meta[512 + lane] : -1;
   const int cl = lane < p.rows ? s_meta[576 + lane] : 0;
+  stamp(16);
   const int sp = __shfl(sl, lane > 0 ? lane - 1 : 0, 64);
   const unsigned long long run_starts = __ballot(lane < p.rows && (lane == 0 || sl != sp));
   const int run0 = 63 - __builtin_clzll(run_starts & ((2ull << lane) - 1ull));  // lane 0 always starts a run
@@ -204,12 +205,14 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   const int n_eff = max(1, min(FINE ? min(p.n_splits, 16) : p.n_splits, grid / max(1, n_groups * nkv)));
   const int n_items = n_groups * nkv * n_eff;
   if (n_items_out) *n_items_out = n_items;
+  stamp(17);
   if (bid >= n_items) {
     on_idle();
     return true;
   }
 
   for (int item = bid; item < n_items; item += grid) {
+  if (item == bid) stamp(18);
   // item -> (kv head, group, chunk); kv head fastest so a head's workgroups share one XCD (b % 8)
   const int kvh = item % nkv;
   const int gi = (item / nkv) % n_groups, chunk = item / (nkv * n_groups);
@@ -227,6 +230,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   int ctxmax = c_own;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) ctxmax = max(ctxmax, __shfl_xor(ctxmax, o, 64));
+  if (item == bid) stamp(19);
   const int rho = n / G;                     // group row of this lane's query column
   const int ctx_n = __shfl(c_own, rho, 64);  // its context (0 for padded columns)
 
@@ -241,6 +245,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   const int we = FINE ? min(ctxmax, kbeg + CL) : min(ctxmax, wb + CL / kWv);
   const int nsteps = we > wb ? (we - wb + kMqStep - 1) / kMqStep : 0;
   const int kmax = ctxmax - 1;  // keys past the context are clamped (finite data, masked scores)
+  if (item == bid) stamp(20);
 
   // ---- Q^T fragments (B operand): Q[column n][dims 32ks + 8g ..], pre-scaled by scale*log2(e)
   bf16x8 qf[NKS];
@@ -305,6 +310,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   unsigned char* vi = lds + L::vimg + w * kMqStep * 256;
+  if (item == bid) stamp(21);
 
   auto compute_step = [&](int kb, const uint4 (&kr)[2][NKS], const uint4 (&vr)[NVL]) {
 #pragma unroll

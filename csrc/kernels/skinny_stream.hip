@@ -1020,7 +1020,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   unsigned long long bar_next = chain_base(bar, nwg, cp.bar_mode);  // mode >= 4: running target
   int nts = 0;
   auto stamp = [&]() {
-    if (cp.ts && threadIdx.x == 0) *gp(cp.ts + blockIdx.x * 16 + nts) = __builtin_amdgcn_s_memrealtime();
+    if (cp.ts && threadIdx.x == 0) *gp(cp.ts + blockIdx.x * 32 + nts) = __builtin_amdgcn_s_memrealtime();
     ++nts;
   };
   stamp();
@@ -1064,7 +1064,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                         }, &n_attn, [&](int k) {
                                                           if ((k == 15 || k == 10) && cp.ts) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                                                           if (cp.ts && threadIdx.x == 0)
-                                                            *gp(cp.ts + blockIdx.x * 16 + k) = __builtin_amdgcn_s_memrealtime();
+                                                            *gp(cp.ts + blockIdx.x * 32 + k) = __builtin_amdgcn_s_memrealtime();
                                                         });
     if (!idle) setup0(n_attn);
     stamp();
@@ -1159,15 +1159,18 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
 
 // weight-stream cache policy of the chained launch: 0 default; 2 nt measured 142.6 vs 100.7 us
 // per Llama-3-8B layer tail (tools/chain_probe.py --wpol 2), so 0
+#ifndef VWA_CHAIN_ALT_AUX
+#define VWA_CHAIN_ALT_AUX 2
+#endif
 static int g_chain_wa = 0;
-extern "C" void vwa_set_chain_weight_policy(int aux) { g_chain_wa = aux == 0 ? 0 : 2; }
+extern "C" void vwa_set_chain_weight_policy(int aux) { g_chain_wa = aux == 0 ? 0 : VWA_CHAIN_ALT_AUX; }
 
 extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid,
                                 hipStream_t st) {
   if (attn_g) lds = lds > (int)MqLds<128, 8>::bytes ? lds : (int)MqLds<128, 8>::bytes;
 #define VWA_CHAIN_LAUNCH(S, N, G)                                                                              \
   do {                                                                                                         \
-    if (g_chain_wa) hipLaunchKernelGGL((chain_kernel<8, S, N, G, 2>), dim3(grid), dim3(8 * 64), lds, st, d_cp); \
+    if (g_chain_wa) hipLaunchKernelGGL((chain_kernel<8, S, N, G, VWA_CHAIN_ALT_AUX>), dim3(grid), dim3(8 * 64), lds, st, d_cp); \
     else hipLaunchKernelGGL((chain_kernel<8, S, N, G, 0>), dim3(grid), dim3(8 * 64), lds, st, d_cp);           \
   } while (0)
   if (seq == 0) {

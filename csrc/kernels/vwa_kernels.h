@@ -90,7 +90,7 @@ struct ChainParams {
   int part_floats;
   unsigned* tickets;       // [max_tiles] zero-initialised, self-resetting
   int max_tiles;
-  unsigned long long* ts;  // optional [grid][16] s_memrealtime stamps per workgroup (profiling)
+  unsigned long long* ts;  // optional [grid][32] s_memrealtime stamps per workgroup (profiling)
   // optional decode-attention phase in front of the GEMM phases (head_dim 128, attn_g = GQA
   // group size; 0: none): the o_proj weights stream while the attention runs
   DecodeAttnParams attn;
