@@ -26,6 +26,7 @@ def main():
                     help="DIAGNOSTIC: barriers arrive but never wait (wrong results): phase cost without dependencies")
     ap.add_argument("--row-table", action="store_true", help="(always on: the chained attention requires them)")
     ap.add_argument("--ctx", type=int, default=1100, help="attention context length (tokens)")
+    ap.add_argument("--n-splits", type=int, default=0, help="attention chunks per kv head cap (0: decode_n_splits(2048))")
     ap.add_argument("--kv-tok-major", action="store_true",
                     help="K/V blocks stored [block][token][head][dim] (a head's 16 tokens at 2 KB stride) "
                          "instead of [block][head][token][dim] (4 KB contiguous per head)")
@@ -68,11 +69,12 @@ def main():
             akv = torch.randn_like(akc)
         table = (torch.randperm(nblk + 3, device=dev)[:nblk].to(torch.int32) + 1).view(1, nblk)
         lay = ops.KVLayout.paged(akc, akv, table)
-        ns = ops.decode_n_splits(2048)
+        ns0 = ops.decode_n_splits(2048)
+        ns = a.n_splits or ns0
         akw = dict(a_q=mk(M, nq * hd), a_k=akc, a_v=akv, a_table=table, a_block_size=bs, a_sb=lay.sb, a_sh=lay.sh,
                    a_st=lay.st, a_ctx=torch.arange(ctx, ctx + M, dtype=torch.int32, device=dev) + 1,
                    a_seq=torch.zeros(M, dtype=torch.int32, device=dev), a_scale=hd ** -0.5, a_n_splits=ns,
-                   a_part_o=torch.zeros(M * ns * nq * hd, device=dev), a_part_ml=torch.zeros(M * ns * nq * 2, device=dev),
+                   a_part_o=torch.zeros(M * ns0 * nq * hd, device=dev), a_part_ml=torch.zeros(M * ns0 * nq * 2, device=dev),
                    a_counters=torch.zeros(M * nkv, dtype=torch.int32, device=dev))
         ag = nq // nkv
         if True:  # per-row copies of the sequence's block table (required by the chained attention)
@@ -141,7 +143,7 @@ def main():
             col = col[col > 0]
             if col.numel():
                 extra[nm] = [round(float((col.median() - t0) * 10e-3), 2), round(float((col.max() - t0) * 10e-3), 2)]
-    r = dict(kernel="chain_probe", rows=M, ctx=a.ctx if a.attn else None, warm_kv=a.warm_kv, kv_tok_major=a.kv_tok_major, bar_mode=a.bar_mode, wpol=a.wpol, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
+    r = dict(kernel="chain_probe", rows=M, ctx=a.ctx if a.attn else None, warm_kv=a.warm_kv, n_splits=a.n_splits, kv_tok_major=a.kv_tok_major, bar_mode=a.bar_mode, wpol=a.wpol, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
              stamps_med_us=[round(x, 2) for x in med], stamps_min_us=[round(x, 2) for x in mn],
              stamps_max_us=[round(x, 2) for x in mx],
              legend=("start,end_attn," if a.attn else "start,") + "end_o,wait_o,end_gu,wait_gu,end_down,wait_down,end_qkv")

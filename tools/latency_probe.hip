@@ -128,7 +128,7 @@ __global__ __launch_bounds__(512) void item_stream_buf(const char* base, size_t 
   const int lane = threadIdx.x & 63;
   const unsigned wid = blockIdx.x * 8 + (threadIdx.x >> 6), nwaves = gridDim.x * 8;
   const unsigned items = (unsigned)(bytes / 16384), per = items / nwaves;
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, (int)bytes, 0x00020000);
   u32x4 v[SETS][16];
   unsigned acc = 0;
   const unsigned b0 = wid * per * 16384u + lane * 16u;
@@ -147,6 +147,40 @@ __global__ __launch_bounds__(512) void item_stream_buf(const char* base, size_t 
     }
   }
   if (acc == 0x12345678u) sink[4] = (int)acc;
+}
+
+// two named register sets exactly like the chained kernel's loop (compute A, reload A, compute B,
+// reload B), with a real MFMA consumer so the loads cannot be reordered past their use
+__global__ __launch_bounds__(512) void item_stream_ab(const char* base, size_t bytes, int* sink) {
+  const int lane = threadIdx.x & 63;
+  const unsigned wid = blockIdx.x * 8 + (threadIdx.x >> 6), nwaves = gridDim.x * 8;
+  const unsigned items = (unsigned)(bytes / 16384), per = items / nwaves;
+  // num_records = the stream's bytes: the past-the-end sentinel below is beyond it (reads 0)
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, (int)bytes, 0x00020000);
+  const unsigned b0 = wid * per * 16384u + lane * 16u;
+  u32x4 A[16], B[16];
+  typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  const bf16x8_t xv = __builtin_bit_cast(bf16x8_t, u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
+  auto load = [&](u32x4 (&v)[16], unsigned it) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(it < per ? b0 + it * 16384u + i * 1024u : 0xFFFFFFF0u), 0, 0);
+  };
+  auto compute = [&](const u32x4 (&v)[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xv, __builtin_bit_cast(bf16x8_t, v[i]), acc, 0, 0, 0);
+  };
+  load(A, 0);
+  load(B, 1);
+#pragma unroll 1
+  for (unsigned it = 0; it < per; it += 2) {
+    compute(A);
+    load(A, it + 2);
+    compute(B);
+    load(B, it + 3);
+  }
+  if (acc[0] == 1234.5f) sink[4] = (int)acc[1];
 }
 
 // the same items, interleaved: item j of wave w sits at (j * nwaves + w) * 16 KB, so the waves in
@@ -282,6 +316,8 @@ int main() {
                   ms * 200.0, bytes / (ms / 5 * 1e-3) / 1e12);
     };
     bw("items_2sets_436MB", item_stream<2>, 256, (size_t)436 << 20);
+    bw("ab_2sets_8waves_436MB", item_stream_ab, 256, (size_t)436 << 20);
+    bw("ab_2sets_8waves_436MB_again", item_stream_ab, 256, (size_t)436 << 20);
     bw("buf_2sets_8waves_436MB", item_stream_buf<2>, 256, (size_t)436 << 20);
     bw("buf_1set_8waves_436MB", item_stream_buf<1>, 256, (size_t)436 << 20);
     bw("buf_3sets_8waves_436MB", item_stream_buf<3>, 256, (size_t)436 << 20);
