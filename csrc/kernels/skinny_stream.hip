@@ -44,6 +44,15 @@ VWA_DEVICE uint4 bload_w(__amdgpu_buffer_rsrc_t r, unsigned off) {
   u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, AUX);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// the same with the constant part of the offset in soffset (a scalar): one VGPR offset per 4
+// loads instead of one per load.  Past-the-end items use voff = kOOB2 (>= 2 GB, above every
+// weight's num_records even with soffset added)
+constexpr unsigned kOOB2 = 0x80000000u;
+template <int AUX>
+VWA_DEVICE uint4 bload_w_so(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, AUX);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
 
 // Epilogue operands that do not depend on the GEMM (residual tile, fp8 column scales, QKV row
 // positions / KV slots / rotary factors) are loaded for the workgroup's FIRST tile at kernel
@@ -722,8 +731,9 @@ VWA_DEVICE PhaseRange chain_range(const ChainPhase& ph, int wb0 = 0, int wn = 0)
 }
 
 // weight item `it` (unit u0 + it) of phase p into the registers wr (NT * U <= 4 groups of 4)
-template <int NT, int U, int WA>
-VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[16], int it, const PhaseRange& r) {
+template <int NT, int U, int WA, int R>
+VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[R], int it, const PhaseRange& r) {
+  static_assert(NT * U * 4 == R, "an item fills its register set");
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.W), (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
   const int lane = threadIdx.x & 63, nl = lane & 15, g = lane >> 4;
@@ -741,42 +751,51 @@ VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[16], int i
         // 96.3 vs 106.8 us at 4 rows against the row-major [N, K] access
         const unsigned T = (unsigned)(tile * NT + nt);
         const unsigned base = ((T * (unsigned)(p.K / 128) + (unsigned)kg) * 4u) * 1024u + (unsigned)lane * 16u;
+        const unsigned vb = ok ? base : kOOB2;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) wr[(nt * U + u) * 4 + s] = bload_w<WA>(rw, ok ? base + 1024u * s : kOOB);
+        for (int s = 0; s < 4; ++s) wr[(nt * U + u) * 4 + s] = bload_w_so<WA>(rw, vb, 1024 * s);
       } else {
         const unsigned row = (unsigned)(tile * 16 * NT + nt * 16 + nl);
         const unsigned base = (row * (unsigned)p.K + (unsigned)(kg * 128 + 32 * g)) * 2u;
+        const unsigned vb = ok ? base : kOOB2;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) wr[(nt * U + u) * 4 + s] = bload_w<WA>(rw, ok ? base + 16u * s : kOOB);
+        for (int s = 0; s < 4; ++s) wr[(nt * U + u) * 4 + s] = bload_w_so<WA>(rw, vb, 16 * s);
       }
     }
   }
 }
 
-template <int EPI>
+// loads per weight item (register set): 16 with 8 waves per workgroup, 8 with 16 waves (a wave's
+// VGPR budget halves with twice the waves)
+template <int KS>
+struct ChainShape {
+  static constexpr int R = KS == 16 ? 8 : 16;
+};
+
+template <int EPI, int KS = 8>
 struct PhaseShape {
   static constexpr int NT = EPI == EPI_SWIGLU ? 2 : 1;
   // (measured: QKV in half-tile units -- 384 tiles -> 3 units per workgroup, one split tile each --
   // 12.5-13.4 us vs 6.7 median / 11.5 max with whole tiles, also with the split tile processed
   // first and published before the next item's loads under a counted vmcnt)
-  static constexpr int U = 4 / NT;
+  static constexpr int U = ChainShape<KS>::R / 4 / NT;
 };
 
 // the phase's first weight item (and with pre2 its second) before the barrier wait: a
 // workgroup that arrives early keeps HBM busy while the grid catches up
-template <int EPI, int KS, int WA>
-VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[16], uint4 (&wr2)[16], int pre2, int wb0 = 0,
+template <int EPI, int KS, int WA, int R>
+VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[R], uint4 (&wr2)[R], int pre2, int wb0 = 0,
                                   int wn = 0) {
   const PhaseRange r = chain_range<KS>(ph, wb0, wn);
-  chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U, WA>(ph.p, ph.nb, wr, 0, r);
-  if (pre2) chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U, WA>(ph.p, ph.nb, wr2, 1, r);
+  chain_load<PhaseShape<EPI, KS>::NT, PhaseShape<EPI, KS>::U, WA>(ph.p, ph.nb, wr, 0, r);
+  if (pre2) chain_load<PhaseShape<EPI, KS>::NT, PhaseShape<EPI, KS>::U, WA>(ph.p, ph.nb, wr2, 1, r);
 }
 
 // one weight item `it` of a phase into wr (the next phase's item 0 / item 1, see chain_kernel)
-template <int EPI, int KS, int WA>
-VWA_DEVICE void chain_issue_item(const ChainPhase& ph, uint4 (&wr)[16], int it, int wb0 = 0, int wn = 0) {
+template <int EPI, int KS, int WA, int R>
+VWA_DEVICE void chain_issue_item(const ChainPhase& ph, uint4 (&wr)[R], int it, int wb0 = 0, int wn = 0) {
   const PhaseRange r = chain_range<KS>(ph, wb0, wn);
-  chain_load<PhaseShape<EPI>::NT, PhaseShape<EPI>::U, WA>(ph.p, ph.nb, wr, it, r);
+  chain_load<PhaseShape<EPI, KS>::NT, PhaseShape<EPI, KS>::U, WA>(ph.p, ph.nb, wr, it, r);
 }
 
 // partial tile of a split tile: cross-wave sums of this workgroup's units -> slot (sc1)
@@ -806,10 +825,10 @@ VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
 // queued behind weight loads; the other waves issue their item 1 at once (pre2 == 0: one item at
 // the barrier), which streams while the X rows arrive.  hs = items the staging wave has already
 // issued into (X0, X1).
-template <int EPI, int KS, int WA>
-VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4 (&X1)[16], char* smem, int pre2,
+template <int EPI, int KS, int WA, int R>
+VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 (&X1)[R], char* smem, int pre2,
                             int hs = 0, int wb0 = 0, int wn = 0) {
-  constexpr int NT = PhaseShape<EPI>::NT, U = PhaseShape<EPI>::U;
+  constexpr int NT = PhaseShape<EPI, KS>::NT, U = PhaseShape<EPI, KS>::U;
   const ChainPhase& ph = cp.ph[i];
   const SkinnyParams& p = ph.p;
   const int nb = ph.nb, M = p.M, K = p.K;
@@ -853,9 +872,16 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
       ++nw;
     }
     // the pieces are older than the nw weight items (16 loads each): wait for them only
-    if (nw == 2) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
-    else if (nw == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (R == 16) {
+      if (nw == 2) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      else if (nw == 1) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      static_assert(R == 8, "item sizes: 16 or 8 loads");
+      if (nw == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if (nw == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   } else if (!xdma) {
     for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
       const int m = c / k8, kk = c % k8;
@@ -895,7 +921,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[16], uint4
   f32x4 acc[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](const uint4 (&wr)[16], int it) {
+  auto compute = [&](const uint4 (&wr)[R], int it) {
     const int b = (r.u0 + it) % nb;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1011,7 +1037,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
         : "s"(cpp));
     if (junk == 0x9e3779b9u) __builtin_amdgcn_s_sleep(1);
   }
-  uint4 A[16], B[16];
+  uint4 A[ChainShape<KS>::R], B[ChainShape<KS>::R];
   // barrier = arrive (stores drained), issue the next phase's first weight item, then wait: the
   // weight stream is in flight while the slowest workgroup finishes
   const int nwg = (int)gridDim.x;
@@ -1121,7 +1147,10 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
 // K % 128 == 0, bf16 weights).  The filled descriptor is then copied to device memory once and
 // launched with vwa_chain_launch (graph-capturable: no allocation, no copy at launch).
 extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
+  // (8 waves: a 16-wave form -- 1024-thread workgroups, 8-load items -- has a 128-VGPR budget;
+  // compiled it spilled 200 B/lane and measured 160 vs 97 us per layer tail)
   constexpr int KS = 8;
+  constexpr int R = ChainShape<KS>::R;
   if (cp->n < 2 || cp->n > kChainMaxPhases || grid < 1) return -10;
   static const int kSeq[3][kChainMaxPhases] = {{EPI_RESID, EPI_SWIGLU, EPI_RESID, EPI_QKV},
                                                {EPI_RESID, EPI_GELU, EPI_RESID, EPI_QKV},
@@ -1133,7 +1162,7 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     const SkinnyParams& p = ph.p;
     if (ph.epi != kSeq[cp->seq][i]) return -10;
     ph.nt = (ph.epi == EPI_SWIGLU) ? 2 : 1;
-    const int U = 4 / ph.nt;
+    const int U = R / 4 / ph.nt;
     if (p.M < 1 || p.M > 4 || p.K % 128 != 0 || p.N % (16 * ph.nt) != 0 || p.w_scale) return -10;
     if ((size_t)p.N * p.K * 2 >= 0x7FFFFFF0ull || (size_t)p.M * p.ldx * 2 >= 0x7FFFFFF0ull) return -10;
     const int G = p.K / 128;
