@@ -154,8 +154,9 @@ void skinny_gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64
   if (col_mask.has_value()) {
     const Tensor& cm = *col_mask;
     TORCH_CHECK(epi == 0, "col_mask needs the store epilogue");
-    TORCH_CHECK(cm.is_cuda() && cm.scalar_type() == at::kInt && cm.dim() == 2 && cm.stride(1) == 1,
-                "col_mask must be an int32 [rows, words] GPU tensor with contiguous rows");
+    TORCH_CHECK((cm.is_cuda() || cm.is_pinned()) && cm.scalar_type() == at::kInt && cm.dim() == 2 &&
+                    cm.stride(1) == 1,
+                "col_mask must be an int32 [rows, words] GPU or pinned host tensor with contiguous rows");
     TORCH_CHECK(mask_rows >= 1 && mask_rows <= cm.size(0) && col_mask_off >= 0 &&
                     (col_mask_off + (w.size(0) + 31) / 32) <= cm.size(1),
                 "col_mask does not cover the output columns");

@@ -30,6 +30,8 @@ VWA_DEVICE void argmax_merge(float& bv, int& bi, float v, int i) {
   }
 }
 
+constexpr int kMaskWordsMax = 4096;  // mask words per chunk staged in LDS (16 KB)
+
 __global__ __launch_bounds__(256) void sample_partial_kernel(const float* __restrict__ logits, int ld, int V,
                                                              const uint32_t* __restrict__ mask, int mask_words,
                                                              const float* __restrict__ temperature,
@@ -38,9 +40,16 @@ __global__ __launch_bounds__(256) void sample_partial_kernel(const float* __rest
                                                              int* part_idx, int n_chunks) {
   __shared__ float sv[256];
   __shared__ int si[256];
+  __shared__ uint32_t smask[kMaskWordsMax];
   const int row = blockIdx.x, chunk = blockIdx.y;
   const int per = (V + n_chunks - 1) / n_chunks;
   const int v0 = chunk * per, v1 = min(V, v0 + per);
+  // the chunk's mask words, all loaded at once into LDS: the mask may live in pinned HOST memory
+  // (zero-copy: no H2D copy per step), where a per-token load would be a PCIe round trip each
+  const int w0 = v0 >> 5, nw = v1 > v0 ? ((v1 - 1) >> 5) - w0 + 1 : 0;
+  if (mask)
+    for (int i = threadIdx.x; i < nw; i += 256) smask[i] = mask[(int64_t)row * mask_words + w0 + i];
+  __syncthreads();
   const float T = temperature ? temperature[row] : 0.f;
   const float invT = T > 0.f ? 1.f / T : 1.f;
   const uint64_t base = splitmix64(seed[0] ^ splitmix64((uint64_t)step[0] * 0x100000001B3ull + row));
@@ -48,7 +57,7 @@ __global__ __launch_bounds__(256) void sample_partial_kernel(const float* __rest
   int bi = 0x7fffffff;
   for (int v = v0 + threadIdx.x; v < v1; v += 256) {
     if (mask) {
-      const uint32_t wd = mask[(int64_t)row * mask_words + (v >> 5)];
+      const uint32_t wd = smask[(v >> 5) - w0];
       if (!((wd >> (v & 31)) & 1u)) continue;
     }
     float key = logits[(int64_t)row * ld + v];
@@ -108,7 +117,9 @@ __global__ __launch_bounds__(256) void sample_final_kernel(const float* __restri
     // fail word (the forward's chained launch timed out at a grid barrier, so these logits are
     // invalid) -> -2 in every row: the host re-runs the step on the per-kernel path
     const bool failed = fail_word != nullptr && fail_word[0] != 0;
-    out_tokens[row] = failed ? -2 : (sv[0] == -INFINITY) ? -1 : si[0];
+    // system scope: out_tokens may be pinned host memory the host polls (no D2H copy per step)
+    __hip_atomic_store(out_tokens + row, failed ? -2 : (sv[0] == -INFINITY) ? -1 : si[0], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
     if (row == rows - 1) step[0] += 1;
   }
 }
@@ -119,6 +130,7 @@ extern "C" int vwa_sample(const float* logits, int ld, int rows, int V, const ui
                           const float* temperature, const uint64_t* seed, const int* step, int* out_tokens,
                           float* part_val, int* part_idx, int n_chunks, const int64_t* fail_word, hipStream_t st) {
   if (n_chunks < 1 || n_chunks > 1024) return -1;
+  if (mask && ((V + n_chunks - 1) / n_chunks + 31) / 32 + 1 > kMaskWordsMax) return -10;
   hipLaunchKernelGGL(sample_partial_kernel, dim3(rows, n_chunks), dim3(256), 0, st, logits, ld, V, mask, mask_words,
                      temperature, seed, step, part_val, part_idx, n_chunks);
   hipLaunchKernelGGL(sample_final_kernel, dim3(rows), dim3(256), 0, st, part_val, part_idx, n_chunks, out_tokens,

@@ -120,6 +120,10 @@ class LLMIntentEngine:
         # LM head under the grammar mask (LLMEngine.head_logits): the vocab tiles no row may sample
         # are skipped -- 42 % of the tiles live per step on average on the intent grammar
         self.masked_head = ops.env_flag("VWA_MASKED_HEAD", True)
+        # zero-copy host buffers (GPU): the LM head and the sampler read the grammar masks straight
+        # from the pinned host rows and the sampler stores the tokens into pinned host memory -- no
+        # H2D mask copy and no D2H token copy per step (each a DMA start on the critical path)
+        self.zero_copy = pin and ops.env_flag("VWA_ZERO_COPY", True)
         self.part_val = torch.zeros(R * 64, dtype=torch.float32, device=dev)
         self.part_idx = torch.zeros(R * 64, dtype=torch.int32, device=dev)
         self.last_stats: Dict[str, Any] = {}
@@ -256,9 +260,11 @@ class LLMIntentEngine:
         for i, r in enumerate(batch):  # CPU grammar masks overlap the in-flight forward
             r.matcher.fill_mask(self.h_mask_np[i])
         t2 = time.perf_counter()
-        self.d_mask[:n].copy_(self.h_mask[:n], non_blocking=True)
+        if not self.zero_copy:
+            self.d_mask[:n].copy_(self.h_mask[:n], non_blocking=True)
+        mask = self.h_mask if self.zero_copy else self.d_mask
         # the LM head under the same masks: only vocab tiles some row may sample are computed
-        logits = self.engine.head_logits(col_mask=self.d_mask if self.masked_head else None, mask_rows=n)
+        logits = self.engine.head_logits(col_mask=mask if self.masked_head else None, mask_rows=n)
         toks = self._sample(logits, n, self.engine.step_fail_word())
         if any(t == -2 for t in toks):
             # the forward's chained launch timed out at a grid barrier (tokens -2 from the
@@ -278,12 +284,32 @@ class LLMIntentEngine:
 
     def _sample(self, logits: torch.Tensor, n: int, fail_word: Optional[torch.Tensor]) -> List[int]:
         """Masked sampling of the n logits rows (masks already in d_mask) and the token readback."""
-        ops.sample(logits, mask=self.d_mask, temperature=self.d_temp if self.temperature > 0 else None,
-                   seed=self.d_seed, step=self.d_step, out_tokens=self.d_tok, part_val=self.part_val[: n * 64],
+        zc = self.zero_copy
+        if zc and self.spin_wait:
+            self.h_tok_np[:n] = _TOK_PENDING  # before the launch: the sampler stores into it directly
+        ops.sample(logits, mask=self.h_mask if zc else self.d_mask,
+                   temperature=self.d_temp if self.temperature > 0 else None, seed=self.d_seed, step=self.d_step,
+                   out_tokens=self.h_tok if zc else self.d_tok, part_val=self.part_val[: n * 64],
                    part_idx=self.part_idx[: n * 64], fail_word=fail_word)
-        if self.dev.type == "cuda":
+        if self.dev.type == "cuda" and zc and self.spin_wait:
+            t3 = time.perf_counter()
+            hv = self.h_tok_np[:n]
+            deadline = t3 + 0.05
+            while (hv == _TOK_PENDING).any():
+                if time.perf_counter() > deadline:  # long step: block on the stream instead
+                    torch.cuda.current_stream().synchronize()
+                    break
+            # (the sampler's system-scope int32 stores land whole; the masks it and the LM head
+            # read are done by then -- the host may overwrite them for the next step)
+            toks = hv.tolist()
+        elif self.dev.type == "cuda":
             if self.spin_wait:
                 self.h_tok_np[:n] = _TOK_PENDING
+            if zc:
+                t3 = time.perf_counter()
+                torch.cuda.current_stream().synchronize()
+                self._t3 = t3
+                return self.h_tok[:n].tolist()
             self.h_tok[:n].copy_(self.d_tok[:n], non_blocking=True)
             t3 = time.perf_counter()
             if self.spin_wait:
