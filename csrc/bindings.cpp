@@ -318,6 +318,11 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   cp.idle_pre = chain_idle_pre();
   cp.xdma = chain_xdma();
   cp.osub = chain_osub();
+  if (const char* e = std::getenv("VWA_CHAIN_DIAG_SKIP")) cp.diag_skip = std::atoi(e);  // (diagnostic)
+  {  // VWA_CHAIN_LDS_ITEM=0|1: phase 1's item 2 preloaded into LDS during the attention (ChainParams::lds_item)
+    const char* e = std::getenv("VWA_CHAIN_LDS_ITEM");
+    cp.lds_item_req = e ? std::atoi(e) : 1;  // (2: diagnostic, full LDS without the item)
+  }
   if (w_qkv.has_value()) {
     TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
                     v_cache.has_value(),

@@ -168,10 +168,11 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   constexpr bool rowtab = FINE;
   const __amdgpu_buffer_rsrc_t r_rt = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<int*>(p.row_table), (short)0, rowtab ? p.rows * p.rt_stride * 4 : 0, 0x00020000);
-  // Loaded by wave 0 only and shared through LDS (the per-item partials area, free until the
-  // first item's outputs): every wave of every workgroup asking for the same few lines at the
-  // launch's start is 8x the requests on the same L2 lines.
-  int* s_meta = reinterpret_cast<int*>(lds + L::ow);  // [4][128] row tables | [64] seq ids | [64] contexts
+  // Loaded by wave 0 only and shared through LDS (the start of the V-image area, free until the
+  // first item's __syncthreads): every wave of every workgroup asking for the same few lines at
+  // the launch's start is 8x the requests on the same L2 lines.  (In the first 2.5 KB: the chained
+  // launch's idle workgroups LDS-DMA weights above 32 KB while other waves may still read it.)
+  int* s_meta = reinterpret_cast<int*>(lds + L::vimg);  // [4][128] row tables | [64] seq ids | [64] contexts
   if (w == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)

@@ -765,6 +765,37 @@ VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[R], int it
   }
 }
 
+// LDS item (cp.lds_item): weight item `it` of this workgroup's range of a phase, LDS-DMA'd into
+// dst + wave * 16 KB in the register-set order (load k of the item -> dst + k KB, lane l's 16 bytes
+// at + 16 l).  Issued during the attention window, when HBM idles behind the latency-bound
+// attention and o_proj; the bandwidth-bound gate/up phase then streams one item less per
+// workgroup (measured: 5.5 us per item, tools/chain_probe.py --diag-skip).  Pre-tiled weights.
+template <int NT, int U, int WA>
+VWA_DEVICE void chain_preload(const SkinnyParams& p, int nb, const PhaseRange& r, int it, char* dst) {
+  static_assert(NT * U == 4, "an item = 16 loads of 1 KB per wave");
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.W), (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
+  const unsigned lane = threadIdx.x & 63;
+  char* wd = dst + (threadIdx.x >> 6) * 16384;
+  const int unit = r.u0 + it;
+  const int tile = unit / nb, b = unit % nb;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int kg = r.gb + b * U + u;
+    const bool ok = it < r.n_items && kg < r.ge;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const unsigned T = (unsigned)(tile * NT + nt);
+      const unsigned base = ((T * (unsigned)(p.K / 128) + (unsigned)kg) * 4u) * 1024u + lane * 16u;
+      const unsigned vb = ok ? base : kOOB2;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rw, (__attribute__((address_space(3))) void*)(wd + ((nt * U + u) * 4 + s) * 1024), 16, vb, 1024 * s, 0, WA);
+    }
+  }
+}
+
 // loads per weight item (register set): 16 with 8 waves per workgroup, 8 with 16 waves (a wave's
 // VGPR budget halves with twice the waves)
 template <int KS>
@@ -845,6 +876,13 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
   const PhaseRange r = chain_range<KS>(ph, wb0, wn);
   const int first_tile = r.u0 / nb;
   const bool xdma = cp.xdma != 0, stager = xdma && w == KS - 1;
+  // diagnostic in-phase stamps (tools/chain_probe.py, wave 0): phase 0 -> slots 22..28, phase 1
+  // -> 29..31 (entry, X staged, row scales, item 0 computed, ...)
+  auto pst = [&](int k) {
+    const int slot = i == 0 ? 22 + k : i == 1 && k < 3 ? 29 + k : -1;
+    if (cp.ts && threadIdx.x == 0 && slot >= 0) *gp(cp.ts + blockIdx.x * 32 + slot) = __builtin_amdgcn_s_memrealtime();
+  };
+  pst(0);
   if (xdma && !stager && !pre2) chain_load<NT, U, WA>(p, nb, X1, 1, r);  // streams during the staging
 
   EpiPre pre;
@@ -890,6 +928,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     }
   }
   __syncthreads();
+  pst(1);
   for (int m = w; m < 16; m += KS) {
     float sc = 1.f, mean = 0.f;
     if (p.fuse_rms && m < M) {
@@ -917,6 +956,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     }
   }
   __syncthreads();
+  pst(2);
 
   f32x4 acc[NT];
 #pragma unroll
@@ -981,18 +1021,39 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     return !(tile * nb >= r.u0 && (tile + 1) * nb <= u1);
   };
   if (!pre2 && !xdma) chain_load<NT, U, WA>(p, nb, X1, 1, r);
+  // DIAGNOSTIC (cp.diag_skip, tools/chain_probe.py): phase 1's items 2 .. 2 + diag_skip - 1 are not
+  // loaded (zero weights, wrong results): what the phase costs with fewer bytes to stream
+  auto ldi = [&](uint4 (&wr)[R], int idx) {
+    if (i == 1 && idx == 2 && cp.lds_item) {  // preloaded during the attention window (chain_preload)
+      static_assert(R == 16, "LDS item: 16 loads of 1 KB per wave");
+      const char* src = smem + cp.lds_item + w * 16384 + lane * 16;
+#pragma unroll
+      for (int k = 0; k < R; ++k) wr[k] = *reinterpret_cast<const uint4*>(src + k * 1024);
+      return;
+    }
+    if (i == 1 && idx >= 2 && idx < 2 + cp.diag_skip) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) wr[k] = make_uint4(0u, 0u, 0u, 0u);
+      return;
+    }
+    chain_load<NT, U, WA>(p, nb, wr, idx, r);
+  };
   for (int it = 0; it < n_pad; it += 2) {
     compute(X0, it);
+    if (it == 0) pst(3);
     const bool e0 = !split_end(it);
-    if (e0 && it + 2 < n_pad) chain_load<NT, U, WA>(p, nb, X0, it + 2, r);
+    if (e0 && it + 2 < n_pad) ldi(X0, it + 2);
     finish(it);
-    if (!e0 && it + 2 < n_pad) chain_load<NT, U, WA>(p, nb, X0, it + 2, r);
+    if (it == 0) pst(4);
+    if (!e0 && it + 2 < n_pad) ldi(X0, it + 2);
     if (it + 1 >= r.n_items) break;  // padding item: no wait on it (X1 may hold the next phase's item 0)
     compute(X1, it + 1);
+    if (it == 0) pst(5);
     const bool e1 = !split_end(it + 1);
-    if (e1 && it + 3 < n_pad) chain_load<NT, U, WA>(p, nb, X1, it + 3, r);
+    if (e1 && it + 3 < n_pad) ldi(X1, it + 3);
     finish(it + 1);
-    if (!e1 && it + 3 < n_pad) chain_load<NT, U, WA>(p, nb, X1, it + 3, r);
+    if (it == 0) pst(6);
+    if (!e1 && it + 3 < n_pad) ldi(X1, it + 3);
   }
 }
 
@@ -1077,6 +1138,10 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
       chain_issue_first<E0, KS, WA>(cp.ph[0], B, A, pre, ob0, on);
     }
   };
+  auto preload1 = [&]() {
+    chain_preload<PhaseShape<E1, KS>::NT, PhaseShape<E1, KS>::U, WA>(cp.ph[1].p, cp.ph[1].nb, chain_range<KS>(cp.ph[1]),
+                                                                     2, smem + cp.lds_item);
+  };
   if constexpr (AG > 0) {
     // idle workgroups (no attention item) issue their o_proj weights at once; the others after
     // their item, at the barrier (one item: their attention registers were live until then)
@@ -1101,6 +1166,12 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     } else if (cp.idle_pre == 0) {
       issue0(pre0);
     }
+    // LDS item: every workgroup right after its arrival (whose __syncthreads ends the
+    // attention's use of LDS).  Measured (tools/chain_probe.py, 1 row): 101.7-102.0 vs
+    // 104.2-104.9 us per layer; issued earlier (idle workgroups at once) its bytes delayed the
+    // attention's K/V (+1.7 us), issued inside the o_proj phase they delayed its end (+4.5 us)
+    if (cp.lds_item) preload1();
+
     chain_wait(bar, gen, cp.bar_mode);
     if (idle && cp.idle_pre < 0) issue0(pre0);  // DIAGNOSTIC: no weight stream during the attention
   } else {
@@ -1180,6 +1251,24 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     if (need > lds) lds = need;
   }
   if (lds > 160 * 1024) return -10;
+  // LDS item (Llama tail with the attention phase, one row, pre-tiled weights): phases 0 and 1
+  // use LDS below 32 KB, the item takes [32 KB, 160 KB) -- phase 2 may overlap it (the item is
+  // consumed at the start of phase 1); the attention's own LDS is free again before the preload
+  cp->lds_item = 0;
+  if (cp->lds_item_req == 1 && cp->seq == 0 && cp->attn_g > 0 && cp->n >= 2 && cp->ph[0].p.M == 1 &&
+      cp->ph[1].p.w_tiled) {
+    bool fits = true;
+    for (int i = 0; i < 2; ++i) {
+      const ChainPhase& ph = cp->ph[i];
+      const size_t x = ((size_t)ph.p.M * (ph.p.K + 8) * 2 + 15) & ~(size_t)15;
+      if (x + (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float) > 32 * 1024) fits = false;
+    }
+    if (fits) {
+      cp->lds_item = 32 * 1024;
+      lds = 160 * 1024;
+    }
+  }
+  if (cp->lds_item_req == 2) lds = 160 * 1024;  // DIAGNOSTIC: the full LDS without the item
   // LDS-DMA staging moves whole 1 KB pieces of a row (512 bf16): only for K % 512 == 0 phases
   for (int i = 0; i < cp->n; ++i)
     if (cp->ph[i].p.K % 512 != 0) cp->xdma = 0;

@@ -95,6 +95,11 @@ struct ChainParams {
   // group size; 0: none): the o_proj weights stream while the attention runs
   DecodeAttnParams attn;
   int attn_g;
+  int diag_skip;  // DIAGNOSTIC only (VWA_CHAIN_DIAG_SKIP): phase-1 items not loaded (wrong results)
+  // LDS item (attention launches, M = 1): byte offset of the LDS region that receives phase 1's
+  // weight item 2 of every workgroup by LDS-DMA during the attention window (0: off)
+  int lds_item;
+  int lds_item_req;  // host request for the LDS item (vwa_chain_prepare decides lds_item)
 };
 
 struct FlashAttnParams {

@@ -180,6 +180,9 @@ def test_chained_layer_tail_matches_per_kernel_path(cfg, monkeypatch):
         monkeypatch.setenv("VWA_CHAIN_ATTN", "1")
         model.reset_chains()
         got_a = run(True)
+        # 1-row steps there preload gate/up's item 2 into LDS during the attention window
+        # (ChainParams::lds_item: the whole 160 KB of LDS)
+        assert any(v[2] == 160 * 1024 for v in model.chain_descs())
         monkeypatch.setenv("VWA_CHAIN_ATTN", "0")  # and the separate attention launch
         model.reset_chains()
         got = run(True)

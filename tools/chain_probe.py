@@ -149,6 +149,25 @@ def main():
              legend=("start,end_attn," if a.attn else "start,") + "end_o,wait_o,end_gu,wait_gu,end_down,wait_down,end_qkv")
     if a.attn:
         r["attn_stamps_med_max_us"] = extra
+        # phase stamps split by role: workgroups that ran an attention item vs the others
+        isatt = full[:, 9] > 0
+        for nm, sel in (("attn_wg", isatt), ("other_wg", ~isatt)):
+            if int(sel.sum()):
+                s = st[sel]
+                r[nm] = dict(n=int(sel.sum()), med=[round(x, 2) for x in s.median(dim=0).values.tolist()],
+                             max=[round(x, 2) for x in s.max(dim=0).values.tolist()],
+                             argmax=[int(i) for i in torch.nonzero(sel).flatten()[s.argmax(dim=0)].tolist()])
+                # in-phase stamps (chain_phase pst): o_proj entry, X staged, scales, item0, fin0,
+                # item1, fin1 | gate/up entry, X staged, scales
+                ph = {}
+                for j, pn in enumerate(["o_entry", "o_xstaged", "o_scales", "o_item0", "o_fin0", "o_item1",
+                                        "o_fin1", "gu_entry", "gu_xstaged", "gu_scales"]):
+                    col = full[sel, 22 + j]
+                    col = col[col > 0]
+                    if col.numel():
+                        ph[pn] = [round(float((col.median() - t0) * 10e-3), 2), round(float((col.max() - t0) * 10e-3), 2),
+                                  int(col.numel())]
+                r[nm + "_phase"] = ph
     print(json.dumps(r), flush=True)
     if a.json:
         with open(a.json, "a") as f:
