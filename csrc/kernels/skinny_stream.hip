@@ -1024,7 +1024,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
   // DIAGNOSTIC (cp.diag_skip, tools/chain_probe.py): phase 1's items 2 .. 2 + diag_skip - 1 are not
   // loaded (zero weights, wrong results): what the phase costs with fewer bytes to stream
   auto ldi = [&](uint4 (&wr)[R], int idx) {
-    if (i == 1 && idx == 2 && cp.lds_item) {  // preloaded during the attention window (chain_preload)
+    if (i == 1 && idx == 2 && cp.lds_item && w < cp.lds_item_waves) {  // preloaded (chain_preload)
       static_assert(R == 16, "LDS item: 16 loads of 1 KB per wave");
       const char* src = smem + cp.lds_item + w * 16384 + lane * 16;
 #pragma unroll
@@ -1170,7 +1170,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     // attention's use of LDS).  Measured (tools/chain_probe.py, 1 row): 101.7-102.0 vs
     // 104.2-104.9 us per layer; issued earlier (idle workgroups at once) its bytes delayed the
     // attention's K/V (+1.7 us), issued inside the o_proj phase they delayed its end (+4.5 us)
-    if (cp.lds_item) preload1();
+    if (cp.lds_item && (int)(threadIdx.x >> 6) < cp.lds_item_waves) preload1();
 
     chain_wait(bar, gen, cp.bar_mode);
     if (idle && cp.idle_pre < 0) issue0(pre0);  // DIAGNOSTIC: no weight stream during the attention
@@ -1251,20 +1251,25 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     if (need > lds) lds = need;
   }
   if (lds > 160 * 1024) return -10;
-  // LDS item (Llama tail with the attention phase, one row, pre-tiled weights): phases 0 and 1
-  // use LDS below 32 KB, the item takes [32 KB, 160 KB) -- phase 2 may overlap it (the item is
-  // consumed at the start of phase 1); the attention's own LDS is free again before the preload
+  // LDS item (Llama tail with the attention phase, pre-tiled weights): the region above phases
+  // 0 and 1's LDS (1 KB aligned) up to 160 KB holds item 2 of as many waves as fit (8 at one
+  // row, 7 at 2-3, 6 at 4 rows) -- phase 2 may overlap it (the item is consumed at the start of
+  // phase 1); the attention's own LDS is free again before the preload
   cp->lds_item = 0;
-  if (cp->lds_item_req == 1 && cp->seq == 0 && cp->attn_g > 0 && cp->n >= 2 && cp->ph[0].p.M == 1 &&
-      cp->ph[1].p.w_tiled) {
-    bool fits = true;
+  cp->lds_item_waves = 0;
+  if (cp->lds_item_req == 1 && cp->seq == 0 && cp->attn_g > 0 && cp->n >= 2 && cp->ph[1].p.w_tiled) {
+    size_t start = 0;
     for (int i = 0; i < 2; ++i) {
       const ChainPhase& ph = cp->ph[i];
       const size_t x = ((size_t)ph.p.M * (ph.p.K + 8) * 2 + 15) & ~(size_t)15;
-      if (x + (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float) > 32 * 1024) fits = false;
+      const size_t need = x + (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float);
+      if (need > start) start = need;
     }
-    if (fits) {
-      cp->lds_item = 32 * 1024;
+    start = (start + 1023) & ~(size_t)1023;
+    const int nw = start < 160 * 1024 ? (int)((160 * 1024 - start) / 16384) : 0;
+    if (nw >= 4) {
+      cp->lds_item = (int)start;
+      cp->lds_item_waves = nw < KS ? nw : KS;
       lds = 160 * 1024;
     }
   }

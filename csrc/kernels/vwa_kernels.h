@@ -99,6 +99,7 @@ struct ChainParams {
   // LDS item (attention launches, M = 1): byte offset of the LDS region that receives phase 1's
   // weight item 2 of every workgroup by LDS-DMA during the attention window (0: off)
   int lds_item;
+  int lds_item_waves;  // waves whose item 2 is in LDS (the region holds 16 KB per wave)
   int lds_item_req;  // host request for the LDS item (vwa_chain_prepare decides lds_item)
 };
 
