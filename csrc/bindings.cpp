@@ -323,6 +323,14 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
     const char* e = std::getenv("VWA_CHAIN_LDS_ITEM");
     cp.lds_item_req = e ? std::atoi(e) : 1;  // (2: diagnostic, full LDS without the item)
   }
+  {  // VWA_CHAIN_LDS_ITEM2=0|1: phase 2's (down) item 2 preloaded into LDS at the gate/up -> down barrier
+    const char* e = std::getenv("VWA_CHAIN_LDS_ITEM2");
+    cp.lds_item2_req = e ? std::atoi(e) : 1;
+  }
+  {  // VWA_CHAIN_XPRE2=0|1: with X staged by one wave, the others issue two items at each barrier
+    const char* e = std::getenv("VWA_CHAIN_XPRE2");
+    cp.xpre2 = e ? (std::atoi(e) != 0) : 0;
+  }
   if (w_qkv.has_value()) {
     TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
                     v_cache.has_value(),

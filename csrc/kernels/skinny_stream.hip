@@ -1024,9 +1024,10 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
   // DIAGNOSTIC (cp.diag_skip, tools/chain_probe.py): phase 1's items 2 .. 2 + diag_skip - 1 are not
   // loaded (zero weights, wrong results): what the phase costs with fewer bytes to stream
   auto ldi = [&](uint4 (&wr)[R], int idx) {
-    if (i == 1 && idx == 2 && cp.lds_item && w < cp.lds_item_waves) {  // preloaded (chain_preload)
+    if (idx == 2 && ((i == 1 && cp.lds_item && w < cp.lds_item_waves) ||
+                     (i == 2 && cp.lds_item2 && w < cp.lds_item2_waves))) {  // preloaded (chain_preload)
       static_assert(R == 16, "LDS item: 16 loads of 1 KB per wave");
-      const char* src = smem + cp.lds_item + w * 16384 + lane * 16;
+      const char* src = smem + (i == 1 ? cp.lds_item : cp.lds_item2) + w * 16384 + lane * 16;
 #pragma unroll
       for (int k = 0; k < R; ++k) wr[k] = *reinterpret_cast<const uint4*>(src + k * 1024);
       return;
@@ -1181,7 +1182,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   // cp.xdma: the staging wave issues nothing at the barriers (chain_phase), the others one item
   // (their second follows right at the release)
   const bool stg = cp.xdma && (threadIdx.x >> 6) == KS - 1;
-  const int preb = cp.xdma ? 0 : cp.pre2;
+  const int preb = cp.xdma ? cp.xpre2 : cp.pre2;
   chain_phase<E0, KS, WA>(cp, 0, B, A, smem, nx ? 1 : pre0, 2, ob0, on);
   stamp();
   gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
@@ -1196,6 +1197,12 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   if constexpr (NPH >= 3) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
     if (!stg) chain_issue_first<E2, KS, WA>(cp.ph[2], A, B, preb);
+    // phase 2's LDS item (down projection): its item 2 streams through the barrier window too
+    // (phase 1's LDS use ended at the arrival's __syncthreads; the region lies above phase 2's
+    // X rows and scratch, which the staging wave fills after the release)
+    if (cp.lds_item2 && (int)(threadIdx.x >> 6) < cp.lds_item2_waves)
+      chain_preload<PhaseShape<E2, KS>::NT, PhaseShape<E2, KS>::U, WA>(cp.ph[2].p, cp.ph[2].nb,
+                                                                     chain_range<KS>(cp.ph[2]), 2, smem + cp.lds_item2);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
     chain_phase<E2, KS, WA>(cp, 2, A, B, smem, preb, 0);
@@ -1273,10 +1280,27 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
       lds = 160 * 1024;
     }
   }
-  if (cp->lds_item_req == 2) lds = 160 * 1024;  // DIAGNOSTIC: the full LDS without the item
   // LDS-DMA staging moves whole 1 KB pieces of a row (512 bf16): only for K % 512 == 0 phases
   for (int i = 0; i < cp->n; ++i)
     if (cp->ph[i].p.K % 512 != 0) cp->xdma = 0;
+  // phase 2's LDS item (Llama tail): the region above phase 2's own X rows + scratch holds item 2
+  // of as many waves as fit (7 at one row; the staging wave never takes one: its vmcnt queue
+  // must hold nothing but the X pieces at the release)
+  cp->lds_item2 = 0;
+  cp->lds_item2_waves = 0;
+  if (cp->lds_item2_req == 1 && cp->seq == 0 && cp->n >= 3 && cp->ph[2].p.w_tiled) {
+    const ChainPhase& ph = cp->ph[2];
+    const size_t x = ((size_t)ph.p.M * (ph.p.K + 8) * 2 + 15) & ~(size_t)15;
+    const size_t start = (x + (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float) + 1023) & ~(size_t)1023;
+    const int nw = start < 160 * 1024 ? (int)((160 * 1024 - start) / 16384) : 0;
+    const int cap = cp->xdma ? KS - 1 : KS;
+    if (nw >= 2) {
+      cp->lds_item2 = (int)start;
+      cp->lds_item2_waves = nw < cap ? nw : cap;
+      lds = 160 * 1024;
+    }
+  }
+  if (cp->lds_item_req == 2) lds = 160 * 1024;  // DIAGNOSTIC: the full LDS without the item
   return (int)lds;
 }
 

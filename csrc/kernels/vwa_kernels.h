@@ -98,9 +98,16 @@ struct ChainParams {
   int diag_skip;  // DIAGNOSTIC only (VWA_CHAIN_DIAG_SKIP): phase-1 items not loaded (wrong results)
   // LDS item (attention launches, M = 1): byte offset of the LDS region that receives phase 1's
   // weight item 2 of every workgroup by LDS-DMA during the attention window (0: off)
-  int lds_item;
+  int lds_item;   // (phase 1)
   int lds_item_waves;  // waves whose item 2 is in LDS (the region holds 16 KB per wave)
   int lds_item_req;  // host request for the LDS item (vwa_chain_prepare decides lds_item)
+  // LDS item of phase 2 (the down projection, Llama tail): item 2 of every workgroup's range,
+  // LDS-DMA'd at the gate/up -> down barrier into the region above phase 2's X rows and
+  // reduction scratch; the staging wave (xdma) takes none (0: off)
+  int lds_item2;
+  int lds_item2_waves;
+  int lds_item2_req;  // host request (VWA_CHAIN_LDS_ITEM2)
+  int xpre2;          // with xdma: the non-staging waves issue a phase's first TWO items at the barrier
 };
 
 struct FlashAttnParams {

@@ -168,6 +168,7 @@ def main():
                         ph[pn] = [round(float((col.median() - t0) * 10e-3), 2), round(float((col.max() - t0) * 10e-3), 2),
                                   int(col.numel())]
                 r[nm + "_phase"] = ph
+    r["env"] = {k: v for k, v in os.environ.items() if k.startswith("VWA_CHAIN")}
     print(json.dumps(r), flush=True)
     if a.json:
         with open(a.json, "a") as f:
