@@ -9,8 +9,10 @@
 * flags are read at call time (the reference reads them at import time, before dotenv runs:
   SURVEY.md §3.5).
 
-Playwright is an optional runtime dependency (not installable in this image): without it,
-``open_session`` raises and the server answers 500 -- tests inject a page factory instead.
+Playwright is an optional runtime dependency (not installable in this image): without it the
+sessions run on the built-in CDP driver (``executor/cdp.py``: local Chrome with remote debugging,
+``CDP_URL``, or Browserbase's CDP ``connectUrl``); ``VWA_BROWSER_DRIVER=playwright|cdp`` forces
+one.  Tests inject a page factory or a fake CDP endpoint.
 """
 from __future__ import annotations
 
@@ -39,11 +41,42 @@ def artifacts_dir() -> str:
     return os.environ.get("ARTIFACTS_DIR", ".artifacts")
 
 
-async def _playwright_factory(sid: str) -> Session:
+async def _cdp_factory(sid: str) -> Session:
+    """Playwright-free session (executor/cdp.py): a CDP endpoint from ``CDP_URL``, a Browserbase
+    session's ``connectUrl``, or a local Chrome launched with remote debugging."""
+    from . import cdp
+
+    d = os.path.join(artifacts_dir(), sid)
+    os.makedirs(d, exist_ok=True)
+    bb_key, bb_proj = os.environ.get("BROWSERBASE_API_KEY"), os.environ.get("BROWSERBASE_PROJECT_ID")
+    if os.environ.get("CDP_URL"):
+        conn = await cdp.connect(os.environ["CDP_URL"])
+    elif bb_key and bb_proj:
+        from .browserbase import create_browserbase_session
+
+        conn = await cdp.connect((await create_browserbase_session(bb_key, bb_proj))["connectUrl"])
+    else:
+        conn = await cdp.launch_chrome(headless=os.environ.get("EXECUTOR_HEADLESS", "false") == "true")
+    page = await conn.new_page()
+    return Session(id=sid, page=page, dir=d, browser=conn)
+
+
+def _driver() -> str:
+    """``VWA_BROWSER_DRIVER``: playwright | cdp | auto (default: Playwright when importable)."""
+    want = os.environ.get("VWA_BROWSER_DRIVER", "auto")
+    if want != "auto":
+        return want
     try:
-        from playwright.async_api import async_playwright  # type: ignore
-    except ImportError as e:  # pragma: no cover - depends on the deployment
-        raise RuntimeError("playwright is not installed; install it to drive a real browser") from e
+        import playwright.async_api  # type: ignore  # noqa: F401
+        return "playwright"
+    except ImportError:
+        return "cdp"
+
+
+async def _playwright_factory(sid: str) -> Session:
+    if _driver() == "cdp":
+        return await _cdp_factory(sid)
+    from playwright.async_api import async_playwright  # type: ignore
     d = os.path.join(artifacts_dir(), sid)
     os.makedirs(d, exist_ok=True)
     pw = await async_playwright().start()
