@@ -137,10 +137,14 @@ struct NoStamp {
 // n_items_out (optional): the step's attention item count (the same in every workgroup), set
 // before on_idle runs.
 // stamp(k) (diagnostic, tools/chain_probe.py --attn): in-body timestamps 9..14 of the first item
+// done (optional, the chained launch's attention -> o_proj hand-off): after a (row group, kv
+// head)'s final output is stored and drained, one no-return add of 1 to *done -- the consumers
+// wait for *n_final_out of them instead of a grid barrier.
 template <int D, int G, int NW, bool SC1OUT, bool DB = true, bool FINE = false, class OnIdle = NoIdle,
           class Stamp = NoStamp>
 VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid, int bid, OnIdle on_idle = {},
-                        int* n_items_out = nullptr, Stamp stamp = {}) {
+                        int* n_items_out = nullptr, Stamp stamp = {}, unsigned long long* done = nullptr,
+                        int* n_final_out = nullptr) {
   constexpr int kWv = NW;
   constexpr int kChunk = FINE ? kMqStep : NW * kMqStep;  // chunk granularity (keys)
   constexpr int RG = kMqCols / G;          // rows per group
@@ -206,12 +210,20 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   const int n_eff = max(1, min(FINE ? min(p.n_splits, 16) : p.n_splits, grid / max(1, n_groups * nkv)));
   const int n_items = n_groups * nkv * n_eff;
   if (n_items_out) *n_items_out = n_items;
+  if (n_final_out) *n_final_out = n_groups * nkv;
   stamp(17);
   if (bid >= n_items) {
     on_idle();
     return true;
   }
 
+  // a (group, kv head)'s final output is complete once every thread's stores drained
+  auto publish = [&]() {
+    if (done == nullptr) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(gp(done), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
   for (int item = bid; item < n_items; item += grid) {
   if (item == bid) stamp(18);
   // item -> (kv head, group, chunk); kv head fastest so a head's workgroups share one XCD (b % 8)
@@ -437,7 +449,10 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
       if (dc == 0) st_sc1_f2(r_ml, base * 2, M, L);
     }
   }
-  if (nact == 1) continue;
+  if (nact == 1) {
+    publish();
+    continue;
+  }
 
   // ---- ticket (same protocol as the split kernel): drained sc1 stores, then one counter add
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -507,6 +522,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
       store_out<SC1OUT>(p.out + (int64_t)prow * p.ldo + pch * D + 8 * pdc, pack8(pacc));
     }
     if (item == bid) stamp(14);  // merged output stored (issued)
+    publish();
     continue;
   }
   // ---- last arriver: online merge of the nact chunks (sc1 loads only; measured: issuing the loads
@@ -536,6 +552,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
     for (int j = 0; j < 8; ++j) acc[j] *= inv;
     store_out<SC1OUT>(p.out + (int64_t)crow * p.ldo + ch * D + 8 * dc, pack8(acc));
   }
+  publish();
   }  // items
   return false;
 }

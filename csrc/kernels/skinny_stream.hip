@@ -579,7 +579,7 @@ constexpr int kChainSpinLimit = 1 << 18;  // ~0.3 s: a lost workgroup ends the l
 // Measured (tools/chain_probe.py): a reset + generation barrier cost 5-7 us from the last
 // arrival to release (four dependent agent-scope round trips).  A flat counter polled with scalar loads
 // on uncached memory (256 same-address atomics) measured 121 us per chained layer vs 99.6 two-level.
-constexpr int kBarTop = 128, kBarErr = 160;
+constexpr int kBarTop = 128, kBarErr = 160, kBarAttnDone = 176;
 
 // Sum of the 8 group counters (mode 4/5), read with scalar loads past the scalar cache: one
 // round trip for all eight (they complete on lgkmcnt, not behind the wave's weight loads).
@@ -1144,6 +1144,49 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                                      2, smem + cp.lds_item);
   };
   if constexpr (AG > 0) {
+   if (cp.attn_flag) {
+    // Hand-off by completion count (cp.attn_flag): the attention workgroups publish each final
+    // output (mq_body `done`) and go straight on -- no grid barrier after the attention; a
+    // workgroup with o_proj units waits until all (row group, kv head) outputs are in.
+    int n_attn = 0, n_final = 0;
+    unsigned long long* done = &bar[kBarAttnDone];
+    const bool idle = mq_body<128, AG, KS, true, false, true>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
+                                                        (int)blockIdx.x, [&]() {
+                                                          setup0(n_attn);
+                                                          if (cp.idle_pre > 0) issue0(pre0);
+                                                        }, &n_attn, [&](int k) {
+                                                          if ((k == 15 || k == 10) && cp.ts) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                                                          if (cp.ts && threadIdx.x == 0)
+                                                            *gp(cp.ts + blockIdx.x * 32 + k) = __builtin_amdgcn_s_memrealtime();
+                                                        }, done, &n_final);
+    if (!idle) setup0(n_attn);
+    stamp();
+    __syncthreads();  // the attention's LDS readers are done (idle workgroups: the metadata's)
+    if (!idle) {
+      pre0 = 0;
+      issue0(0);
+    } else if (cp.idle_pre == 0) {
+      issue0(pre0);
+    }
+    if (cp.lds_item && (int)(threadIdx.x >> 6) < cp.lds_item_waves) preload1();
+    if (chain_range<KS>(cp.ph[0], ob0, on).n_items > 0) {
+      if (threadIdx.x < 64) {
+        const unsigned long long tgt = (unsigned long long)n_final;
+        int spins = 0;
+        while (true) {
+          unsigned long long v;
+          asm volatile("s_load_dwordx2 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(done) : "memory");
+          if (v >= tgt) break;
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kChainSpinLimit) {
+            if (threadIdx.x == 0) __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+      __syncthreads();
+    }
+   } else {
     // idle workgroups (no attention item) issue their o_proj weights at once; the others after
     // their item, at the barrier (one item: their attention registers were live until then)
     // cp.idle_pre: idle workgroups issue their first items during the attention (2, default) or
@@ -1175,6 +1218,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
 
     chain_wait(bar, gen, cp.bar_mode);
     if (idle && cp.idle_pre < 0) issue0(pre0);  // DIAGNOSTIC: no weight stream during the attention
+   }
   } else {
     setup0(0);
     issue0(pre0);
@@ -1183,7 +1227,10 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   // (their second follows right at the release)
   const bool stg = cp.xdma && (threadIdx.x >> 6) == KS - 1;
   const int preb = cp.xdma ? cp.xpre2 : cp.pre2;
-  chain_phase<E0, KS, WA>(cp, 0, B, A, smem, nx ? 1 : pre0, 2, ob0, on);
+  // (hand-off by count: a workgroup without o_proj units skips the phase -- its X rows may not be
+  // complete yet, and nothing of it is used)
+  if (!(AG > 0 && cp.attn_flag) || chain_range<KS>(cp.ph[0], ob0, on).n_items > 0)
+    chain_phase<E0, KS, WA>(cp, 0, B, A, smem, nx ? 1 : pre0, 2, ob0, on);
   stamp();
   gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
   if (!stg) {
@@ -1191,6 +1238,10 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     else chain_issue_first<E1, KS, WA>(cp.ph[1], A, B, preb);
   }
   chain_wait(bar, gen, cp.bar_mode);
+  // every attention output was counted and every waiter released before this barrier: reset the
+  // count for the next launch (ordered before it by the kernel boundary)
+  if (AG > 0 && cp.attn_flag && blockIdx.x == 0 && threadIdx.x == 0)
+    __hip_atomic_store(gp(&bar[kBarAttnDone]), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp();
   chain_phase<E1, KS, WA>(cp, 1, A, B, smem, nx ? 1 : preb, nx ? 1 : 0);
   stamp();

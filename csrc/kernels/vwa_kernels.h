@@ -108,6 +108,10 @@ struct ChainParams {
   int lds_item2_waves;
   int lds_item2_req;  // host request (VWA_CHAIN_LDS_ITEM2)
   int xpre2;          // with xdma: the non-staging waves issue a phase's first TWO items at the barrier
+  // attention -> o_proj hand-off without a grid barrier: every (row group, kv head) final output
+  // adds 1 to a counter (bar u64 word 176, reset after the next barrier); only the workgroups
+  // with o_proj units wait for the count (VWA_CHAIN_AFLAG)
+  int attn_flag;
 };
 
 struct FlashAttnParams {

@@ -334,3 +334,37 @@ def test_whisper_chained_decoder_matches_per_kernel_path(name, monkeypatch):
     for a, b in zip(got, ref):
         err = (a - b).abs().max().item()
         assert err < 0.03 * (1 + b.abs().max().item()), err
+
+
+def test_chain_is_rearmed_after_backoff(monkeypatch):
+    """After a fallback the engine re-arms the chained launch (fresh barrier counters) once the
+    backoff has passed; the re-armed chained steps match an engine that never chained."""
+    ops.ext()
+    model = LlamaModel(CFG, device="cuda", seed=4)
+    toks = list(range(30, 46))
+
+    def engine():
+        e = LLMEngine(model, max_seqs=1, max_model_len=128, kv_blocks=10, block_size=16)
+        s = e.new_sequence(toks[:10], use_prefix_cache=False)
+        e.prefill(s)
+        return e, s
+
+    monkeypatch.setenv("VWA_CHAIN", "0")
+    e0, s0 = engine()
+    ref = [e0.run_rows([(s0, t)]).float().cpu() for t in toks[10:14]]
+    monkeypatch.setenv("VWA_CHAIN", "1")
+    e, s = engine()
+    got = [e.run_rows([(s, toks[10])]).float().cpu()]
+    model._chain_bar.view(torch.int64)[160] = 1  # a timed-out spin (left partial arrivals too)
+    model._chain_bar.view(torch.int64)[16] += 3
+    e._check_chain(blocking=True)
+    assert e.stats["chain_fallbacks"] == 1 and not model._chain_ok(1)
+    assert e._chain_retry_at == e.stats["steps"] + 256
+    got.append(e.run_rows([(s, toks[11])]).float().cpu())  # per-kernel path
+    e._chain_retry_at = e.stats["steps"]  # backoff elapsed
+    got += [e.run_rows([(s, t)]).float().cpu() for t in toks[12:14]]
+    assert e.stats["chain_rearms"] == 1 and model._chain_ok(1) and model.chain_descs()
+    assert not model.chain_error()
+    for a, b in zip(got, ref):
+        err = (a - b).abs().max().item()
+        assert err < 0.02 * (1 + b.abs().max().item()), err

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Chain tests with the count-based attention hand-off, then an A/B of it (chain_probe per-layer time)
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out
+VWA_CHAIN_AFLAG=1 timeout -k 10 300 python -u -m pytest tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread -k "chain" > gpurun_out/t_aflag.log 2>&1 || { tail -30 gpurun_out/t_aflag.log; exit 1; }
+tail -2 gpurun_out/t_aflag.log
+for rows in 1 4; do
+  for rep in 1 2; do
+    for f in 0 1; do
+      VWA_CHAIN_AFLAG=$f timeout -k 10 120 python tools/chain_probe.py --rows $rows --attn \
+        --json gpurun_out/ab_aflag.jsonl > gpurun_out/ab_last.log 2>&1 || exit $?
+      python -c "import json,sys; d=json.loads(open(\"gpurun_out/ab_last.log\").read().strip().splitlines()[-1]); print(\"rows=$rows aflag=$f\", d[\"chained_us\"], d[\"stamps_med_us\"], d[\"stamps_max_us\"][1])"
+    done
+  done
+done

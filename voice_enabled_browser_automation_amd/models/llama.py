@@ -182,6 +182,16 @@ class LlamaModel:
         self._chain_disabled = True
         self.reset_chains()
 
+    def enable_chain(self) -> None:
+        """Re-arm the chained launch after a fallback (runtime/engine.py retries with backoff): a
+        timed-out launch leaves partial arrivals in the barrier tickets, split-tile tickets and
+        the error word, so they restart from zero (call with no chained launch in flight)."""
+        for t in (getattr(self, "_chain_bar", None), getattr(self, "_chain_work", None)):
+            if t is not None:
+                t.zero_()
+        self._chain_disabled = False
+        self.reset_chains()
+
     def reset_chains(self) -> None:
         """Drop every cached chain descriptor (they embed raw device pointers of the buffers)."""
         self._chains = weakref.WeakKeyDictionary()

@@ -253,6 +253,8 @@ class LLMEngine:
         n = len(rows)
         M = bucket_for(n)
         b = self.bufs
+        if getattr(self, "_chain_retry_at", None) is not None:
+            self._maybe_rearm_chain()
         if logits_for is None or len(logits_for) == n:
             nl, L = n, M
         else:
@@ -355,6 +357,7 @@ class LLMEngine:
             word.zero_()
         self.graphs.clear()
         self.stats["chain_fallbacks"] = self.stats.get("chain_fallbacks", 0) + 1
+        self._schedule_chain_retry()
         self.stats["steps"] -= 1
         self.stats["rows"] -= len(rows)
         for sid, n_done in pre.items():
@@ -387,6 +390,29 @@ class LLMEngine:
             m.disable_chain()
             self.graphs.clear()
             self.stats["chain_fallbacks"] = self.stats.get("chain_fallbacks", 0) + 1
+            self._schedule_chain_retry()
+
+    def _schedule_chain_retry(self) -> None:
+        """A chain timeout usually means another kernel held CUs for a while (e.g. the ASR engine
+        on another stream of the same GPU): the chained launch is re-armed after 256 steps, then
+        after 512, 1024, ... (capped at 65536) if it keeps failing (``VWA_CHAIN_RETRY=0``: never)."""
+        if not ops.env_flag("VWA_CHAIN_RETRY", True) or not hasattr(self.model, "enable_chain"):
+            return
+        self._chain_backoff = min(2 * getattr(self, "_chain_backoff", 128), 1 << 16)
+        self._chain_retry_at = self.stats["steps"] + self._chain_backoff
+
+    def _maybe_rearm_chain(self) -> None:
+        at = getattr(self, "_chain_retry_at", None)
+        if at is None or self.stats["steps"] < at:
+            return
+        self._chain_retry_at = None
+        if self.device.type == "cuda":
+            torch.cuda.current_stream().synchronize()  # no launch in flight uses the counters
+        if getattr(self.bufs, "attn_cnt", None) is not None:
+            self.bufs.attn_cnt.zero_()
+        self.model.enable_chain()
+        self.graphs.clear()
+        self.stats["chain_rearms"] = self.stats.get("chain_rearms", 0) + 1
 
     def prefill(self, seq: Sequence_, chunk: int = 2048, upto: Optional[int] = None) -> Optional[torch.Tensor]:
         """Compute K/V for seq.tokens[n_computed:upto] (default: all tokens); returns f32 logits
