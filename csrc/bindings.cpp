@@ -329,7 +329,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   }
   {  // VWA_CHAIN_AFLAG=0|1: attention -> o_proj hand-off by completion count instead of a grid barrier
     const char* e = std::getenv("VWA_CHAIN_AFLAG");
-    cp.attn_flag = e ? (std::atoi(e) != 0) : 0;
+    cp.attn_flag = e ? (std::atoi(e) != 0) : 1;
   }
   {  // VWA_CHAIN_XPRE2=0|1: with X staged by one wave, the others issue two items at each barrier
     const char* e = std::getenv("VWA_CHAIN_XPRE2");
