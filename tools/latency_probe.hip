@@ -183,6 +183,58 @@ __global__ __launch_bounds__(512) void item_stream_ab(const char* base, size_t b
   if (acc[0] == 1234.5f) sink[4] = (int)acc[1];
 }
 
+
+// the two-set loop with the weight loads as inline asm and EXPLICIT waits: the compiler does not
+// track these loads, so it cannot merge the sets' waits (item_stream_ab: one vmcnt(0) per
+// iteration, both sets drained together); here set S is awaited with vmcnt(16 * (SETS - 1)) --
+// the younger sets' loads stay in flight -- and re-issued right after its use
+typedef int vwa_v4i __attribute__((ext_vector_type(4)));
+#define VWA_TIE16(v) "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), \
+  "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+template <int SETS>
+__global__ __launch_bounds__(512) void item_stream_asm(const char* base, size_t bytes, int* sink) {
+  const int lane = threadIdx.x & 63;
+  const unsigned wid = blockIdx.x * 8 + (threadIdx.x >> 6), nwaves = gridDim.x * 8;
+  const unsigned items = (unsigned)(bytes / 16384), per = items / nwaves;
+  // buffer descriptor words: base lo, base hi | stride 0, num_records, the flags of make_buffer_rsrc
+  const unsigned long long ba = (unsigned long long)base;
+  const vwa_v4i rs = {(int)(unsigned)ba, (int)((unsigned)(ba >> 32) & 0xFFFFu), (int)bytes, 0x00020000};
+  const unsigned b0 = wid * per * 16384u + lane * 16u;
+  u32x4 V[SETS][16];
+  typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+  typedef float f32x4_t __attribute__((ext_vector_type(4)));
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  const bf16x8_t xv = __builtin_bit_cast(bf16x8_t, u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
+  auto load = [&](u32x4 (&v)[16], unsigned it) {
+    const unsigned o = it < per ? b0 + it * 16384u : 0x80000000u;  // past num_records: zeros
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(v[i]) : "v"(o), "s"(rs), "s"(i * 1024));
+  };
+  auto wait_set = [&](u32x4 (&v)[16]) {
+    if constexpr (SETS == 2) asm volatile("s_waitcnt vmcnt(16)" : VWA_TIE16(v));
+    else if constexpr (SETS == 3) asm volatile("s_waitcnt vmcnt(32)" : VWA_TIE16(v));
+    else asm volatile("s_waitcnt vmcnt(0)" : VWA_TIE16(v));
+  };
+  auto compute = [&](const u32x4 (&v)[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xv, __builtin_bit_cast(bf16x8_t, v[i]), acc, 0, 0, 0);
+  };
+#pragma unroll
+  for (int s = 0; s < SETS; ++s) load(V[s], s);
+#pragma unroll 1
+  for (unsigned it = 0; it < per; it += SETS) {
+#pragma unroll
+    for (int s = 0; s < SETS; ++s) {
+      wait_set(V[s]);
+      compute(V[s]);
+      load(V[s], it + s + SETS);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (acc[0] == 1234.5f) sink[4] = (int)acc[1];
+}
+
 // the same items, interleaved: item j of wave w sits at (j * nwaves + w) * 16 KB, so the waves in
 // flight together read one contiguous region
 template <int SETS>
@@ -318,6 +370,11 @@ int main() {
     bw("items_2sets_436MB", item_stream<2>, 256, (size_t)436 << 20);
     bw("ab_2sets_8waves_436MB", item_stream_ab, 256, (size_t)436 << 20);
     bw("ab_2sets_8waves_436MB_again", item_stream_ab, 256, (size_t)436 << 20);
+    bw("asm_1set_8waves_436MB", item_stream_asm<1>, 256, (size_t)436 << 20);
+    bw("asm_2sets_8waves_436MB", item_stream_asm<2>, 256, (size_t)436 << 20);
+    bw("asm_3sets_8waves_436MB", item_stream_asm<3>, 256, (size_t)436 << 20);
+    bw("asm_2sets_8waves_436MB_again", item_stream_asm<2>, 256, (size_t)436 << 20);
+    bw("ab_2sets_8waves_436MB_3rd", item_stream_ab, 256, (size_t)436 << 20);
     bw("buf_2sets_8waves_436MB", item_stream_buf<2>, 256, (size_t)436 << 20);
     bw("buf_1set_8waves_436MB", item_stream_buf<1>, 256, (size_t)436 << 20);
     bw("buf_3sets_8waves_436MB", item_stream_buf<3>, 256, (size_t)436 << 20);
