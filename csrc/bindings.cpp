@@ -386,7 +386,9 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   if (lds < 0) return {torch::empty({0}, torch::dtype(torch::kUInt8).device(h.device())), 0};
   Tensor host = torch::empty({(int64_t)sizeof(ChainParams)}, torch::dtype(torch::kUInt8));
   std::memcpy(host.data_ptr(), &cp, sizeof(ChainParams));
-  return {host.to(h.device()), (int64_t)lds};
+  // (bit 24 of the returned LDS size: the down phase streams X with the weights -- chain_run
+  // launches that instantiation)
+  return {host.to(h.device()), (int64_t)lds | (cp.n >= 3 && cp.ph[2].xg ? (int64_t)1 << 24 : 0)};
 }
 
 // Whisper decoder chains (skinny_stream.hip chain_kernel SEQ 1 / 2): phase i computes
@@ -488,8 +490,8 @@ void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like, int64_t 
   int dev = like.device().index(), cus = 0;
   TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess, "CU count");
   // one workgroup per CU: the barrier needs every workgroup resident
-  check_rc(vwa_chain_launch(reinterpret_cast<const ChainParams*>(desc.data_ptr()), (int)seq, (int)n_phases, (int)attn_g, (int)lds, cus,
-                            cur_stream(like)),
+  check_rc(vwa_chain_launch(reinterpret_cast<const ChainParams*>(desc.data_ptr()), (int)seq, (int)n_phases, (int)attn_g,
+                            (int)(lds & 0xFFFFFF), cus, cur_stream(like), (int)((lds >> 24) & 1)),
            "chain");
 }
 

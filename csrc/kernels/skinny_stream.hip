@@ -731,11 +731,19 @@ VWA_DEVICE PhaseRange chain_range(const ChainPhase& ph, int wb0 = 0, int wn = 0)
 }
 
 // weight item `it` (unit u0 + it) of phase p into the registers wr (NT * U <= 4 groups of 4)
-template <int NT, int U, int WA, int R>
-VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[R], int it, const PhaseRange& r) {
-  static_assert(NT * U * 4 == R, "an item fills its register set");
+// XG (ChainPhase::xg, the down projection with more rows than its X fits LDS): the item is half
+// the weight k-groups (U = 2: registers 0..7) plus the matching X fragments of rows nl < M
+// (registers 8..15, sc1 loads -- X was written earlier in this launch; L2-resident), so the phase
+// needs no X staging and no more registers
+// wx = false (XG): the weights only -- an item issued before the barrier wait must not read X,
+// which other workgroups are still writing; its X fragments follow after the wait (chain_load_x)
+template <int NT, int U, int WA, int R, bool XG = false>
+VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[R], int it, const PhaseRange& r, bool wx = true) {
+  static_assert(XG ? (NT == 1 && U == 2 && R == 16) : NT * U * 4 == R, "an item fills its register set");
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.W), (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rxg =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.X), (short)0, XG ? (int)((size_t)p.M * p.ldx * 2) : 0, 0x00020000);
   const int lane = threadIdx.x & 63, nl = lane & 15, g = lane >> 4;
   const int unit = r.u0 + it;
   const int tile = unit / nb, b = unit % nb;
@@ -761,6 +769,37 @@ VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[R], int it
 #pragma unroll
         for (int s = 0; s < 4; ++s) wr[(nt * U + u) * 4 + s] = bload_w_so<WA>(rw, vb, 16 * s);
       }
+    }
+    if constexpr (XG) {
+      if (!wx) continue;
+      const unsigned xb =
+          ok && nl < p.M ? ((unsigned)nl * (unsigned)p.ldx + (unsigned)(kg * 128 + 32 * g)) * 2u : kOOB2;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rxg, (int)xb, 16 * s, 16);
+        wr[8 + u * 4 + s] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+    }
+  }
+}
+
+// the X fragments (registers 8..15) of an XG item whose weights went out before the barrier wait
+template <int U, int R>
+VWA_DEVICE void chain_load_x(const SkinnyParams& p, int nb, uint4 (&wr)[R], int it, const PhaseRange& r) {
+  static_assert(U == 2 && R == 16, "XG items: 8 weight + 8 X registers");
+  const __amdgpu_buffer_rsrc_t rxg =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.X), (short)0, (int)((size_t)p.M * p.ldx * 2), 0x00020000);
+  const int lane = threadIdx.x & 63, nl = lane & 15, g = lane >> 4;
+  const int b = (r.u0 + it) % nb;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int kg = r.gb + b * U + u;
+    const bool ok = (it < r.n_items) && (kg < r.ge) && nl < p.M;
+    const unsigned xb = ok ? ((unsigned)nl * (unsigned)p.ldx + (unsigned)(kg * 128 + 32 * g)) * 2u : kOOB2;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rxg, (int)xb, 16 * s, 16);
+      wr[8 + u * 4 + s] = make_uint4(v.x, v.y, v.z, v.w);
     }
   }
 }
@@ -803,30 +842,33 @@ struct ChainShape {
   static constexpr int R = KS == 16 ? 8 : 16;
 };
 
-template <int EPI, int KS = 8>
+template <int EPI, int KS = 8, bool XG = false>
 struct PhaseShape {
   static constexpr int NT = EPI == EPI_SWIGLU ? 2 : 1;
   // (measured: QKV in half-tile units -- 384 tiles -> 3 units per workgroup, one split tile each --
   // 12.5-13.4 us vs 6.7 median / 11.5 max with whole tiles, also with the split tile processed
   // first and published before the next item's loads under a counted vmcnt)
-  static constexpr int U = ChainShape<KS>::R / 4 / NT;
+  static constexpr int U = XG ? 2 : ChainShape<KS>::R / 4 / NT;
 };
 
 // the phase's first weight item (and with pre2 its second) before the barrier wait: a
 // workgroup that arrives early keeps HBM busy while the grid catches up
-template <int EPI, int KS, int WA, int R>
+template <int EPI, int KS, int WA, bool XG = false, int R>
 VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[R], uint4 (&wr2)[R], int pre2, int wb0 = 0,
                                   int wn = 0) {
+  using S = PhaseShape<EPI, KS, XG>;
   const PhaseRange r = chain_range<KS>(ph, wb0, wn);
-  chain_load<PhaseShape<EPI, KS>::NT, PhaseShape<EPI, KS>::U, WA>(ph.p, ph.nb, wr, 0, r);
-  if (pre2) chain_load<PhaseShape<EPI, KS>::NT, PhaseShape<EPI, KS>::U, WA>(ph.p, ph.nb, wr2, 1, r);
+  // (issued before the barrier wait: XG items without their X fragments, chain_phase adds them)
+  chain_load<S::NT, S::U, WA, R, XG>(ph.p, ph.nb, wr, 0, r, !XG);
+  if (pre2) chain_load<S::NT, S::U, WA, R, XG>(ph.p, ph.nb, wr2, 1, r, !XG);
 }
 
 // one weight item `it` of a phase into wr (the next phase's item 0 / item 1, see chain_kernel)
-template <int EPI, int KS, int WA, int R>
+template <int EPI, int KS, int WA, bool XG = false, int R>
 VWA_DEVICE void chain_issue_item(const ChainPhase& ph, uint4 (&wr)[R], int it, int wb0 = 0, int wn = 0) {
+  using S = PhaseShape<EPI, KS, XG>;
   const PhaseRange r = chain_range<KS>(ph, wb0, wn);
-  chain_load<PhaseShape<EPI, KS>::NT, PhaseShape<EPI, KS>::U, WA>(ph.p, ph.nb, wr, it, r);
+  chain_load<S::NT, S::U, WA, R, XG>(ph.p, ph.nb, wr, it, r);
 }
 
 // partial tile of a split tile: cross-wave sums of this workgroup's units -> slot (sc1)
@@ -856,16 +898,16 @@ VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
 // queued behind weight loads; the other waves issue their item 1 at once (pre2 == 0: one item at
 // the barrier), which streams while the X rows arrive.  hs = items the staging wave has already
 // issued into (X0, X1).
-template <int EPI, int KS, int WA, int R>
+template <int EPI, int KS, int WA, bool XG = false, int R>
 VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 (&X1)[R], char* smem, int pre2,
                             int hs = 0, int wb0 = 0, int wn = 0) {
-  constexpr int NT = PhaseShape<EPI, KS>::NT, U = PhaseShape<EPI, KS>::U;
+  constexpr int NT = PhaseShape<EPI, KS, XG>::NT, U = PhaseShape<EPI, KS, XG>::U;
   const ChainPhase& ph = cp.ph[i];
   const SkinnyParams& p = ph.p;
   const int nb = ph.nb, M = p.M, K = p.K;
   const int xstride = K + 8;
   u16* xs = reinterpret_cast<u16*>(smem);
-  const int xbytes = ((M * xstride * 2) + 15) & ~15;
+  const int xbytes = XG ? 0 : ((M * xstride * 2) + 15) & ~15;  // (XG: X fragments stream in the items)
   float* red = reinterpret_cast<float*>(smem + xbytes);
   float* rs = red + KS * NT * 4 * 64;  // [16] row scales (1/rms or LayerNorm rstd)
   float* mu = rs + 16;                  // [16] row means (folded LayerNorm)
@@ -875,7 +917,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
   const int nl = lane & 15, g = lane >> 4;
   const PhaseRange r = chain_range<KS>(ph, wb0, wn);
   const int first_tile = r.u0 / nb;
-  const bool xdma = cp.xdma != 0, stager = xdma && w == KS - 1;
+  const bool xdma = cp.xdma != 0, stager = xdma && w == KS - 1 && !XG;
   // diagnostic in-phase stamps (tools/chain_probe.py, wave 0): phase 0 -> slots 22..28, phase 1
   // -> 29..31 (entry, X staged, row scales, item 0 computed, ...)
   auto pst = [&](int k) {
@@ -883,7 +925,11 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     if (cp.ts && threadIdx.x == 0 && slot >= 0) *gp(cp.ts + blockIdx.x * 32 + slot) = __builtin_amdgcn_s_memrealtime();
   };
   pst(0);
-  if (xdma && !stager && !pre2) chain_load<NT, U, WA>(p, nb, X1, 1, r);  // streams during the staging
+  if constexpr (XG) {  // X fragments of the items issued before the barrier wait (weights only)
+    chain_load_x<U>(p, nb, X0, 0, r);
+    if (pre2) chain_load_x<U>(p, nb, X1, 1, r);
+  }
+  if (xdma && !stager && !pre2) chain_load<NT, U, WA, R, XG>(p, nb, X1, 1, r);  // streams during the staging
 
   EpiPre pre;
   if (r.n_items > 0) epi_values<EPI, NT, true>(p, first_tile, threadIdx.x, pre);
@@ -902,11 +948,11 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     asm volatile("" ::: "memory");  // keep the weight loads below younger than the pieces
     int nw = 0;
     if (hs < 1) {
-      chain_load<NT, U, WA>(p, nb, X0, 0, r);
+      chain_load<NT, U, WA, R, XG>(p, nb, X0, 0, r);
       ++nw;
     }
     if (hs < 2) {
-      chain_load<NT, U, WA>(p, nb, X1, 1, r);
+      chain_load<NT, U, WA, R, XG>(p, nb, X1, 1, r);
       ++nw;
     }
     // the pieces are older than the nw weight items (16 loads each): wait for them only
@@ -920,7 +966,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
       else if (nw == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-  } else if (!xdma) {
+  } else if (!xdma && !XG) {
     for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
       const int m = c / k8, kk = c % k8;
       const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(((size_t)m * p.ldx + kk * 8) * 2), 0, 16);
@@ -931,7 +977,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
   pst(1);
   for (int m = w; m < 16; m += KS) {
     float sc = 1.f, mean = 0.f;
-    if (p.fuse_rms && m < M) {
+    if (p.fuse_rms && m < M && !XG) {  // (the host never folds a norm into an XG phase)
       float s = 0.f, s1 = 0.f;
       for (int kk = lane; kk < k8; kk += 64) {
         float f[8];
@@ -970,7 +1016,8 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         uint4 a = make_uint4(0, 0, 0, 0);
-        if (nl < M) a = *reinterpret_cast<const uint4*>(xs + nl * xstride + kg * 128 + 32 * g + 8 * s);
+        if constexpr (XG) a = wr[8 + u * 4 + s];
+        else if (nl < M) a = *reinterpret_cast<const uint4*>(xs + nl * xstride + kg * 128 + 32 * g + 8 * s);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16(as_bf16x8(a), as_bf16x8(wr[(nt * U + u) * 4 + s]), acc[nt]);
       }
@@ -1020,7 +1067,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     if (unit % nb != nb - 1 && it != r.n_items - 1) return false;
     return !(tile * nb >= r.u0 && (tile + 1) * nb <= u1);
   };
-  if (!pre2 && !xdma) chain_load<NT, U, WA>(p, nb, X1, 1, r);
+  if (!pre2 && !xdma) chain_load<NT, U, WA, R, XG>(p, nb, X1, 1, r);
   // DIAGNOSTIC (cp.diag_skip, tools/chain_probe.py): phase 1's items 2 .. 2 + diag_skip - 1 are not
   // loaded (zero weights, wrong results): what the phase costs with fewer bytes to stream
   auto ldi = [&](uint4 (&wr)[R], int idx) {
@@ -1037,7 +1084,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
       for (int k = 0; k < R; ++k) wr[k] = make_uint4(0u, 0u, 0u, 0u);
       return;
     }
-    chain_load<NT, U, WA>(p, nb, wr, idx, r);
+    chain_load<NT, U, WA, R, XG>(p, nb, wr, idx, r);
   };
   for (int it = 0; it < n_pad; it += 2) {
     compute(X0, it);
@@ -1077,7 +1124,9 @@ struct SeqEpi {
                                           : (I == 0 ? EPI_RESID : EPI_STORE);
 };
 
-template <int KS, int SEQ, int NPH, int AG, int WA>
+// XG2: phase 2 (the down projection) streams its X fragments with the weights (ChainParams
+// ph[2].xg: more rows than its X fits LDS, 5..16 rows, no attention phase)
+template <int KS, int SEQ, int NPH, int AG, int WA, bool XG2 = false>
 __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __restrict__ cpp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ChainParams& cp = *cpp;  // device-resident descriptor
@@ -1247,7 +1296,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   stamp();
   if constexpr (NPH >= 3) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
-    if (!stg) chain_issue_first<E2, KS, WA>(cp.ph[2], A, B, preb);
+    if (!stg || XG2) chain_issue_first<E2, KS, WA, XG2>(cp.ph[2], A, B, preb);  // (XG2: no staging wave)
     // phase 2's LDS item (down projection): its item 2 streams through the barrier window too
     // (phase 1's LDS use ended at the arrival's __syncthreads; the region lies above phase 2's
     // X rows and scratch, which the staging wave fills after the release)
@@ -1256,7 +1305,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                                      chain_range<KS>(cp.ph[2]), 2, smem + cp.lds_item2);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E2, KS, WA>(cp, 2, A, B, smem, preb, 0);
+    chain_phase<E2, KS, WA, XG2>(cp, 2, A, B, smem, preb, 0);
     stamp();
   }
   if constexpr (NPH >= 4) {
@@ -1291,8 +1340,19 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     const SkinnyParams& p = ph.p;
     if (ph.epi != kSeq[cp->seq][i]) return -10;
     ph.nt = (ph.epi == EPI_SWIGLU) ? 2 : 1;
-    const int U = R / 4 / ph.nt;
-    if (p.M < 1 || p.M > 4 || p.K % 128 != 0 || p.N % (16 * ph.nt) != 0 || p.w_scale) return -10;
+    // 5..16 rows: only without the attention phase (its row tables hold <= 4 rows), Llama tail; a
+    // phase whose X rows do not fit LDS next to the scratch streams X with the weights (xg: the
+    // down projection, residual epilogue, pre-tiled weights)
+    const int max_rows = (cp->seq == 0 && cp->attn_g == 0) ? 16 : 4;
+    if (p.M < 1 || p.M > max_rows || p.K % 128 != 0 || p.N % (16 * ph.nt) != 0 || p.w_scale) return -10;
+    const size_t scratch = (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float);
+    const size_t xrows = ((size_t)p.M * (p.K + 8) * 2 + 15) & ~(size_t)15;
+    ph.xg = 0;
+    if (xrows + scratch > 160 * 1024) {
+      if (!(cp->seq == 0 && i == 2 && ph.epi == EPI_RESID && p.w_tiled && p.fuse_rms == 0)) return -10;
+      ph.xg = 1;
+    }
+    const int U = ph.xg ? 2 : R / 4 / ph.nt;
     if ((size_t)p.N * p.K * 2 >= 0x7FFFFFF0ull || (size_t)p.M * p.ldx * 2 >= 0x7FFFFFF0ull) return -10;
     const int G = p.K / 128;
     const int per_wave = (G + KS - 1) / KS;
@@ -1304,8 +1364,7 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     const long long min_range = units / grid > 0 ? units / grid : 1;
     if (ph.nb > 1 && min_range < ph.nb - 1) return -10;
     if (ntiles > cp->max_tiles || (size_t)ntiles * 2 * p.M * 16 * ph.nt > (size_t)cp->part_floats) return -10;
-    const size_t x = ((size_t)p.M * (p.K + 8) * 2 + 15) & ~(size_t)15;
-    const size_t need = x + (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float);  // + scales, means, flag
+    const size_t need = (ph.xg ? 0 : xrows) + scratch;  // X rows + scales, means, flag
     if (need > lds) lds = need;
   }
   if (lds > 160 * 1024) return -10;
@@ -1339,7 +1398,7 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
   // must hold nothing but the X pieces at the release)
   cp->lds_item2 = 0;
   cp->lds_item2_waves = 0;
-  if (cp->lds_item2_req == 1 && cp->seq == 0 && cp->n >= 3 && cp->ph[2].p.w_tiled) {
+  if (cp->lds_item2_req == 1 && cp->seq == 0 && cp->n >= 3 && cp->ph[2].p.w_tiled && !cp->ph[2].xg) {
     const ChainPhase& ph = cp->ph[2];
     const size_t x = ((size_t)ph.p.M * (ph.p.K + 8) * 2 + 15) & ~(size_t)15;
     const size_t start = (x + (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float) + 1023) & ~(size_t)1023;
@@ -1364,8 +1423,19 @@ static int g_chain_wa = 0;
 extern "C" void vwa_set_chain_weight_policy(int aux) { g_chain_wa = aux == 0 ? 0 : VWA_CHAIN_ALT_AUX; }
 
 extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid,
-                                hipStream_t st) {
+                                hipStream_t st, int xg2) {
   if (attn_g) lds = lds > (int)MqLds<128, 8>::bytes ? lds : (int)MqLds<128, 8>::bytes;
+  if (xg2) {  // Llama tail of 5..16 rows: down projection with X from L2, no attention phase
+    if (seq != 0 || attn_g != 0 || (n_phases != 3 && n_phases != 4)) return -10;
+    if (n_phases == 4) {
+      if (g_chain_wa) hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, VWA_CHAIN_ALT_AUX, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+      else hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+    } else {
+      if (g_chain_wa) hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, VWA_CHAIN_ALT_AUX, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+      else hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+    }
+    return (int)hipGetLastError();
+  }
 #define VWA_CHAIN_LAUNCH(S, N, G)                                                                              \
   do {                                                                                                         \
     if (g_chain_wa) hipLaunchKernelGGL((chain_kernel<8, S, N, G, VWA_CHAIN_ALT_AUX>), dim3(grid), dim3(8 * 64), lds, st, d_cp); \

@@ -74,6 +74,7 @@ constexpr int kChainMaxPhases = 4;
 struct ChainPhase {
   SkinnyParams p;
   int epi, nt, nb;
+  int xg;  // X fragments streamed with the weights (X rows do not fit LDS; set by vwa_chain_prepare)
 };
 struct ChainParams {
   ChainPhase ph[kChainMaxPhases];
@@ -132,7 +133,8 @@ extern "C" {
 int vwa_skinny_gemm(int epi, const SkinnyParams* p, hipStream_t st);
 int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st);
 int vwa_chain_prepare(ChainParams* cp, int grid);
-int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid, hipStream_t st);
+int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid, hipStream_t st,
+                     int xg2 = 0);
 void vwa_set_chain_weight_policy(int aux);  // 0: default cache policy, 2: nt (non-temporal) weight loads
 int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
                 uint16_t* y, int rows, int D, int ldx, float eps, hipStream_t st);

@@ -368,3 +368,39 @@ def test_chain_is_rearmed_after_backoff(monkeypatch):
     for a, b in zip(got, ref):
         err = (a - b).abs().max().item()
         assert err < 0.02 * (1 + b.abs().max().item()), err
+
+
+def test_chained_layer_tail_5_to_16_rows(monkeypatch):
+    """Steps of 5..16 rows on the chained launch (VWA_CHAIN_MAX_ROWS): no attention phase, the
+    down projection streaming its X fragments with the weights (its 14336-wide rows do not fit LDS
+    above 5 rows: ChainPhase::xg) -- against the per-kernel path on 8B-shaped layers."""
+    ops.ext()
+    cfg = LlamaConfig(name="t8x", vocab_size=4096, hidden=4096, n_layers=2, n_heads=32, n_kv_heads=8, head_dim=128,
+                      ffn=14336, max_pos=2048)
+    torch.manual_seed(1)
+    toks = torch.randint(0, cfg.vocab_size, (80,)).tolist()
+    model = LlamaModel(cfg, device="cuda", seed=5)
+    engines = []
+
+    def run(chain: bool):
+        monkeypatch.setenv("VWA_CHAIN", "1" if chain else "0")
+        e = LLMEngine(model, max_seqs=2, max_model_len=256, kv_blocks=20, block_size=16)
+        engines.append(e)
+        s = e.new_sequence(toks[:30], use_prefix_cache=False)
+        e.prefill(s)
+        out, i = [], 30
+        for n in (5, 8, 16, 3, 1):
+            out.append(e.run_rows([(s, t) for t in toks[i:i + n]]).float().cpu().clone())
+            i += n
+        e.free_sequence(s, publish=False)
+        return out
+
+    monkeypatch.setenv("VWA_CHAIN_MAX_ROWS", "16")
+    ref = run(False)
+    got = run(True)
+    assert not model.chain_error()
+    descs = [v for v in model.chain_descs() if v is not None]
+    assert any((v[2] >> 24) & 1 for v in descs), "no descriptor streams X with the weights"
+    for a, b in zip(got, ref):
+        err = (a - b).abs().max().item()
+        assert err < 0.02 * (1 + b.abs().max().item()), err

@@ -174,7 +174,9 @@ class LlamaModel:
 
     # ---- chained layer tail (o_proj -> gate/up -> down -> next QKV in one launch; M <= 4 rows)
     def _chain_ok(self, M: int) -> bool:
-        return (M <= 4 and self.tp.size == 1 and self.wdtype == "bf16" and self.device.type == "cuda"
+        # 5..16 rows (jump-forward feeds, concurrent sessions): the chain without its attention
+        # phase, the down projection streaming X with the weights (skinny_stream.hip XG2)
+        return (M <= ops.env_int("VWA_CHAIN_MAX_ROWS", 4) and self.tp.size == 1 and self.wdtype == "bf16" and self.device.type == "cuda"
                 and not getattr(self, "_chain_disabled", False) and ops.env_flag("VWA_CHAIN", True)
                 and ops.native_available())
 
@@ -225,7 +227,7 @@ class LlamaModel:
         # (the chained attention addresses K/V through per-row copies of the block table, which
         # the step buffers keep for contexts of <= 128 blocks, in 16-token blocks: otherwise the
         # separate launch)
-        attn = (self.hd == 128 and self.nq // self.nkv in (4, 8) and ops.env_flag("VWA_CHAIN_ATTN", True)
+        attn = (M <= 4 and self.hd == 128 and self.nq // self.nkv in (4, 8) and ops.env_flag("VWA_CHAIN_ATTN", True)
                 and ops.decode_n_splits(bufs.max_ctx) > 1 and getattr(bufs, "rt_cols", 0) > 0
                 and kv.k[li].shape[2] == 16)
         a = {}

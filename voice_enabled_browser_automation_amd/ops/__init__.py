@@ -38,7 +38,18 @@ def ext():
     if _EXT_ERR is not None:
         raise RuntimeError(f"native gfx950 kernel library unavailable: {_EXT_ERR}") from _EXT_ERR
     try:
-        from . import _vwa_kernels as m  # type: ignore
+        alt = os.environ.get("VWA_KERNEL_SO")  # (A/B experiments: another build of the same library)
+        if alt:
+            import importlib.machinery
+            import importlib.util
+
+            name = __name__ + "._vwa_kernels"
+            spec = importlib.util.spec_from_file_location(
+                name, alt, loader=importlib.machinery.ExtensionFileLoader(name, alt))
+            m = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(m)
+        else:
+            from . import _vwa_kernels as m  # type: ignore
 
         impl = os.environ.get("VWA_ATTN_IMPL")
         if impl:
@@ -660,3 +671,11 @@ def env_flag(name: str, default: bool = False) -> bool:
     if v is None:
         return default
     return v.strip().lower() in ("1", "true", "yes", "on")
+
+
+def env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    try:
+        return int(v) if v not in (None, "") else default
+    except ValueError:
+        return default
