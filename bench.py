@@ -110,11 +110,37 @@ def run_concurrent(args, C, asr, brain, utterances, asr_tokens, world):
             "samples_per_iteration": round(bs["sampled"] / max(1, bs["iterations"]), 2)}
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` started without torchrun: run N ranks (one process per GPU) under
+    torch.distributed.run as a CHILD process and return its exit code.  Runs before this process
+    touches the GPU (torch.cuda.device_count() does not initialise it)."""
+    import subprocess
+
+    have = torch.cuda.device_count()
+    if have < n:
+        raise SystemExit(f"bench.py --gpus {n}: only {have} GPU(s) visible -- refusing to time fewer GPUs "
+                         f"than requested (one rank per GPU over RCCL)")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--asr", default=os.environ.get("VWA_ASR_MODEL", "whisper-tiny"))
     ap.add_argument("--llm", default=os.environ.get("VWA_LLM_MODEL", "llama3-8b"))
     ap.add_argument("--tp", type=int, default=int(os.environ.get("VWA_TP", "1")))
@@ -130,6 +156,12 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={env_world}: one rank per GPU expected")
 
     tp = init_distributed(tp_size=args.tp if int(os.environ.get("WORLD_SIZE", "1")) > 1 else None)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -211,6 +243,17 @@ def main():
         torch.distributed.all_gather(allt, local_t)
     else:
         allt = [local_t]
+    # evidence that the collective backend really saw every rank on its own GPU
+    rccl_world, n_devices, backend = 1, 1, None
+    if world > 1:
+        backend = str(torch.distributed.get_backend())
+        rccl_world = torch.distributed.get_world_size()
+        pr = torch.cuda.get_device_properties(dev)
+        ident = torch.tensor([float(pr.pci_domain_id), float(pr.pci_bus_id), float(pr.pci_device_id)],
+                             dtype=torch.float64, device=dev)
+        ids = [torch.zeros_like(ident) for _ in range(world)]
+        torch.distributed.all_gather(ids, ident)
+        n_devices = len({tuple(a.tolist()) for a in ids})
     K = args.steps
     elapsed_max = max(float(t[0]) for t in allt)
     all_lat = [float(x) for t in allt for x in t[1 : 1 + K]]
@@ -249,6 +292,10 @@ def main():
             "decode_iteration_host_us": host_us,
             "throughput_utt_per_s": round(len(all_lat) / (elapsed_max / 1e3), 3),
             "load_s": round(load_s, 1),
+            "rccl_world": rccl_world,
+            "distinct_devices": n_devices,
+            "dist_backend": backend,
+            "tp": tp.size,
         }
         if conc is not None:
             res["concurrent"] = conc

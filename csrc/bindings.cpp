@@ -234,30 +234,19 @@ void skinny_gemm_qkv(Tensor x, Tensor w_qkv, c10::optional<Tensor> bias, bool fu
   check_rc(run_skinny_checked(4, p, cur_stream(x)), "skinny_gemm_qkv");
 }
 
-// VWA_CHAIN_PRE2=0|1: weight items issued ahead of each chain barrier (ChainParams::pre2)
-int chain_pre2() {
-  const char* e = std::getenv("VWA_CHAIN_PRE2");
-  return e ? (std::atoi(e) != 0) : 1;
-}
-// VWA_CHAIN_IDLE_PRE=0|1|2: items idle workgroups issue during the chained attention phase
-int chain_idle_pre() {
-  const char* e = std::getenv("VWA_CHAIN_IDLE_PRE");
-  return e ? std::atoi(e) : 2;
-}
-// VWA_CHAIN_XDMA=0|1: X rows staged by one wave via LDS-DMA (ChainParams::xdma)
-int chain_xdma() {
-  const char* e = std::getenv("VWA_CHAIN_XDMA");
-  return e ? (std::atoi(e) != 0) : 1;
-}
-// VWA_CHAIN_OSUB=0|1: o_proj units only on the workgroups without an attention item (ChainParams::osub)
-int chain_osub() {
-  const char* e = std::getenv("VWA_CHAIN_OSUB");
-  return e ? (std::atoi(e) != 0) : 1;
-}
-// VWA_CHAIN_NEXT0=0|1: phase 1's first item issued with a one-item phase 0 (ChainParams::next0)
-int chain_next0() {
-  const char* e = std::getenv("VWA_CHAIN_NEXT0");
-  return e ? (std::atoi(e) != 0) : 1;
+// Chained-launch schedule (ChainParams): the measured-best settings of the round-2 A/B runs
+// (profiles/r2_*): two weight items issued ahead of each barrier, phase 1's item 0 in the free
+// register set of a one-item phase 0, X staged by one wave with LDS-DMA, o_proj units only on
+// workgroups without an attention item, LDS items for phases 1 and 2, attention -> o_proj
+// hand-off by completion count.
+void chain_schedule(ChainParams& cp) {
+  cp.pre2 = 1;
+  cp.next0 = 1;
+  cp.xdma = 1;
+  cp.osub = 1;
+  cp.lds_item_req = 1;
+  cp.lds_item2_req = 1;
+  cp.attn_flag = 1;
 }
 
 // ---- chained decode layer tail (skinny_stream.hip, vwa_chain_*): descriptor built once on the
@@ -313,28 +302,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   set_resid(cp.ph[2].p, h);
   cp.n = 3;
   cp.seq = 0;
-  cp.pre2 = chain_pre2();
-  cp.next0 = chain_next0();
-  cp.idle_pre = chain_idle_pre();
-  cp.xdma = chain_xdma();
-  cp.osub = chain_osub();
-  if (const char* e = std::getenv("VWA_CHAIN_DIAG_SKIP")) cp.diag_skip = std::atoi(e);  // (diagnostic)
-  {  // VWA_CHAIN_LDS_ITEM=0|1: phase 1's item 2 preloaded into LDS during the attention (ChainParams::lds_item)
-    const char* e = std::getenv("VWA_CHAIN_LDS_ITEM");
-    cp.lds_item_req = e ? std::atoi(e) : 1;  // (2: diagnostic, full LDS without the item)
-  }
-  {  // VWA_CHAIN_LDS_ITEM2=0|1: phase 2's (down) item 2 preloaded into LDS at the gate/up -> down barrier
-    const char* e = std::getenv("VWA_CHAIN_LDS_ITEM2");
-    cp.lds_item2_req = e ? std::atoi(e) : 1;
-  }
-  {  // VWA_CHAIN_AFLAG=0|1: attention -> o_proj hand-off by completion count instead of a grid barrier
-    const char* e = std::getenv("VWA_CHAIN_AFLAG");
-    cp.attn_flag = e ? (std::atoi(e) != 0) : 1;
-  }
-  {  // VWA_CHAIN_XPRE2=0|1: with X staged by one wave, the others issue two items at each barrier
-    const char* e = std::getenv("VWA_CHAIN_XPRE2");
-    cp.xpre2 = e ? (std::atoi(e) != 0) : 0;
-  }
+  chain_schedule(cp);
   if (w_qkv.has_value()) {
     TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
                     v_cache.has_value(),
@@ -437,11 +405,10 @@ std::tuple<Tensor, int64_t> chain_make_seq(int64_t seq, std::vector<Tensor> X, s
   }
   cp.n = (int)n;
   cp.seq = (int)seq;
-  cp.pre2 = chain_pre2();
-  cp.next0 = chain_next0();
-  cp.idle_pre = chain_idle_pre();
-  cp.xdma = chain_xdma();
-  cp.osub = chain_osub();
+  cp.pre2 = 1;  // (the Llama schedule without its attention-phase and LDS-item parts)
+  cp.next0 = 1;
+  cp.xdma = 1;
+  cp.osub = 1;
   cp.bar = reinterpret_cast<unsigned*>(bar.data_ptr<int>());
   cp.bar_mode = (int)bar_mode;
   cp.tickets = reinterpret_cast<unsigned*>(work.data_ptr<int>());
@@ -859,5 +826,4 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("w_first") = 2);
   m.def("attention_split_tokens", []() { return vwa_attention_split_tokens(); });
   m.def("set_attention_impl", [](int64_t impl) { vwa_set_attention_impl((int)impl); });
-  m.def("set_chain_weight_policy", [](int64_t aux) { vwa_set_chain_weight_policy((int)aux); });
 }

@@ -1068,8 +1068,6 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     return !(tile * nb >= r.u0 && (tile + 1) * nb <= u1);
   };
   if (!pre2 && !xdma) chain_load<NT, U, WA, R, XG>(p, nb, X1, 1, r);
-  // DIAGNOSTIC (cp.diag_skip, tools/chain_probe.py): phase 1's items 2 .. 2 + diag_skip - 1 are not
-  // loaded (zero weights, wrong results): what the phase costs with fewer bytes to stream
   auto ldi = [&](uint4 (&wr)[R], int idx) {
     if (idx == 2 && ((i == 1 && cp.lds_item && w < cp.lds_item_waves) ||
                      (i == 2 && cp.lds_item2 && w < cp.lds_item2_waves))) {  // preloaded (chain_preload)
@@ -1077,11 +1075,6 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
       const char* src = smem + (i == 1 ? cp.lds_item : cp.lds_item2) + w * 16384 + lane * 16;
 #pragma unroll
       for (int k = 0; k < R; ++k) wr[k] = *reinterpret_cast<const uint4*>(src + k * 1024);
-      return;
-    }
-    if (i == 1 && idx >= 2 && idx < 2 + cp.diag_skip) {
-#pragma unroll
-      for (int k = 0; k < R; ++k) wr[k] = make_uint4(0u, 0u, 0u, 0u);
       return;
     }
     chain_load<NT, U, WA, R, XG>(p, nb, wr, idx, r);
@@ -1202,7 +1195,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     const bool idle = mq_body<128, AG, KS, true, false, true>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
                                                         (int)blockIdx.x, [&]() {
                                                           setup0(n_attn);
-                                                          if (cp.idle_pre > 0) issue0(pre0);
+                                                          issue0(pre0);
                                                         }, &n_attn, [&](int k) {
                                                           if ((k == 15 || k == 10) && cp.ts) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                                                           if (cp.ts && threadIdx.x == 0)
@@ -1214,8 +1207,6 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     if (!idle) {
       pre0 = 0;
       issue0(0);
-    } else if (cp.idle_pre == 0) {
-      issue0(pre0);
     }
     if (cp.lds_item && (int)(threadIdx.x >> 6) < cp.lds_item_waves) preload1();
     if (chain_range<KS>(cp.ph[0], ob0, on).n_items > 0) {
@@ -1238,13 +1229,11 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
    } else {
     // idle workgroups (no attention item) issue their o_proj weights at once; the others after
     // their item, at the barrier (one item: their attention registers were live until then)
-    // cp.idle_pre: idle workgroups issue their first items during the attention (2, default) or
-    // only at the barrier (0)
     int n_attn = 0;
     const bool idle = mq_body<128, AG, KS, true, false, true>(cp.attn, reinterpret_cast<unsigned char*>(smem), nwg,
                                                         (int)blockIdx.x, [&]() {
                                                           setup0(n_attn);
-                                                          if (cp.idle_pre > 0) issue0(pre0);
+                                                          issue0(pre0);
                                                         }, &n_attn, [&](int k) {
                                                           if ((k == 15 || k == 10) && cp.ts) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                                                           if (cp.ts && threadIdx.x == 0)
@@ -1256,8 +1245,6 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     if (!idle) {
       pre0 = 0;
       issue0(0);
-    } else if (cp.idle_pre == 0) {
-      issue0(pre0);
     }
     // LDS item: every workgroup right after its arrival (whose __syncthreads ends the
     // attention's use of LDS).  Measured (tools/chain_probe.py, 1 row): 101.7-102.0 vs
@@ -1266,7 +1253,6 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     if (cp.lds_item && (int)(threadIdx.x >> 6) < cp.lds_item_waves) preload1();
 
     chain_wait(bar, gen, cp.bar_mode);
-    if (idle && cp.idle_pre < 0) issue0(pre0);  // DIAGNOSTIC: no weight stream during the attention
    }
   } else {
     setup0(0);
@@ -1275,7 +1261,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   // cp.xdma: the staging wave issues nothing at the barriers (chain_phase), the others one item
   // (their second follows right at the release)
   const bool stg = cp.xdma && (threadIdx.x >> 6) == KS - 1;
-  const int preb = cp.xdma ? cp.xpre2 : cp.pre2;
+  const int preb = cp.xdma ? 0 : cp.pre2;
   // (hand-off by count: a workgroup without o_proj units skips the phase -- its X rows may not be
   // complete yet, and nothing of it is used)
   if (!(AG > 0 && cp.attn_flag) || chain_range<KS>(cp.ph[0], ob0, on).n_items > 0)
@@ -1410,37 +1396,20 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
       lds = 160 * 1024;
     }
   }
-  if (cp->lds_item_req == 2) lds = 160 * 1024;  // DIAGNOSTIC: the full LDS without the item
   return (int)lds;
 }
-
-// weight-stream cache policy of the chained launch: 0 default; 2 nt measured 142.6 vs 100.7 us
-// per Llama-3-8B layer tail (tools/chain_probe.py --wpol 2), so 0
-#ifndef VWA_CHAIN_ALT_AUX
-#define VWA_CHAIN_ALT_AUX 2
-#endif
-static int g_chain_wa = 0;
-extern "C" void vwa_set_chain_weight_policy(int aux) { g_chain_wa = aux == 0 ? 0 : VWA_CHAIN_ALT_AUX; }
 
 extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid,
                                 hipStream_t st, int xg2) {
   if (attn_g) lds = lds > (int)MqLds<128, 8>::bytes ? lds : (int)MqLds<128, 8>::bytes;
   if (xg2) {  // Llama tail of 5..16 rows: down projection with X from L2, no attention phase
     if (seq != 0 || attn_g != 0 || (n_phases != 3 && n_phases != 4)) return -10;
-    if (n_phases == 4) {
-      if (g_chain_wa) hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, VWA_CHAIN_ALT_AUX, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
-      else hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
-    } else {
-      if (g_chain_wa) hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, VWA_CHAIN_ALT_AUX, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
-      else hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
-    }
+    if (n_phases == 4) hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+    else hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
     return (int)hipGetLastError();
   }
-#define VWA_CHAIN_LAUNCH(S, N, G)                                                                              \
-  do {                                                                                                         \
-    if (g_chain_wa) hipLaunchKernelGGL((chain_kernel<8, S, N, G, VWA_CHAIN_ALT_AUX>), dim3(grid), dim3(8 * 64), lds, st, d_cp); \
-    else hipLaunchKernelGGL((chain_kernel<8, S, N, G, 0>), dim3(grid), dim3(8 * 64), lds, st, d_cp);           \
-  } while (0)
+#define VWA_CHAIN_LAUNCH(S, N, G) \
+  hipLaunchKernelGGL((chain_kernel<8, S, N, G, 0>), dim3(grid), dim3(8 * 64), lds, st, d_cp)
   if (seq == 0) {
     if (n_phases != 3 && n_phases != 4) return -10;
     const bool q = n_phases == 4;

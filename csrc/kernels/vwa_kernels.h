@@ -82,7 +82,6 @@ struct ChainParams {
   int seq;                 // 0 Llama tail, 1 Whisper tail, 2 Whisper middle (skinny_stream.hip chain_kernel)
   int pre2;                // issue a phase's first two weight items before the barrier wait (else one)
   int next0;               // phase 1's item 0 rides in the register set a 1-item phase 0 leaves free
-  int idle_pre;            // weight items idle workgroups issue during the attention phase (0..2)
   int xdma;                // X staged by one wave with LDS-DMA while the others stream (chain_phase)
   int osub;                // attention launches: phase 0 only on the workgroups without an attention item
   unsigned* bar;
@@ -96,7 +95,6 @@ struct ChainParams {
   // group size; 0: none): the o_proj weights stream while the attention runs
   DecodeAttnParams attn;
   int attn_g;
-  int diag_skip;  // DIAGNOSTIC only (VWA_CHAIN_DIAG_SKIP): phase-1 items not loaded (wrong results)
   // LDS item (attention launches, M = 1): byte offset of the LDS region that receives phase 1's
   // weight item 2 of every workgroup by LDS-DMA during the attention window (0: off)
   int lds_item;   // (phase 1)
@@ -107,11 +105,10 @@ struct ChainParams {
   // reduction scratch; the staging wave (xdma) takes none (0: off)
   int lds_item2;
   int lds_item2_waves;
-  int lds_item2_req;  // host request (VWA_CHAIN_LDS_ITEM2)
-  int xpre2;          // with xdma: the non-staging waves issue a phase's first TWO items at the barrier
+  int lds_item2_req;  // host request
   // attention -> o_proj hand-off without a grid barrier: every (row group, kv head) final output
   // adds 1 to a counter (bar u64 word 176, reset after the next barrier); only the workgroups
-  // with o_proj units wait for the count (VWA_CHAIN_AFLAG)
+  // with o_proj units wait for the count
   int attn_flag;
 };
 
@@ -135,7 +132,6 @@ int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipS
 int vwa_chain_prepare(ChainParams* cp, int grid);
 int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid, hipStream_t st,
                      int xg2 = 0);
-void vwa_set_chain_weight_policy(int aux);  // 0: default cache policy, 2: nt (non-temporal) weight loads
 int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
                 uint16_t* y, int rows, int D, int ldx, float eps, hipStream_t st);
 int vwa_layernorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,

@@ -1,0 +1,107 @@
+"""Streaming ASR serving path on CPU (reference ops, whisper-test weights): forced-prefix decoding
+(the local-agreement commit) and cross-session batching of recognition passes through the live
+voice WebSocket service with 8 concurrent sessions (SURVEY.md §7.3 hard part #2)."""
+import asyncio
+import json
+import statistics
+import time
+
+import numpy as np
+import pytest
+from aiohttp.test_utils import TestClient, TestServer
+
+from voice_enabled_browser_automation_amd.asr.engine import AsrEngine
+from voice_enabled_browser_automation_amd.asr.streaming import AsrBatcher, EngineRecognizer, StreamingAsrSession
+from voice_enabled_browser_automation_amd.models.config import get_config
+from voice_enabled_browser_automation_amd.models.whisper import WhisperModel
+from voice_enabled_browser_automation_amd.tokenizer import load_tokenizer
+from voice_enabled_browser_automation_amd.voice.server import build_app
+
+
+def _speech(seconds, f0, rate=16000, seed=0):
+    rng = np.random.default_rng(seed)
+    t = np.arange(int(seconds * rate)) / rate
+    sig = np.sin(2 * np.pi * f0 * t) + 0.5 * np.sin(2 * np.pi * 2.3 * f0 * t) + 0.05 * rng.standard_normal(len(t))
+    return (sig / np.abs(sig).max() * 9000).astype(np.int16)
+
+
+@pytest.fixture(scope="module")
+def engine():
+    w = WhisperModel(get_config("whisper-test"), device="cpu", seed=3)
+    return AsrEngine(w, load_tokenizer("whisper"), max_sessions=8)
+
+
+def test_forced_prefix_continues_the_same_greedy_decode(engine):
+    audio = engine.pcm_to_audio(_speech(2.0, 240))
+    full = engine.decode_many([audio], max_tokens=12, min_tokens=12)[0]
+    assert len(full) == 12
+    for k in (1, 5, 11):
+        tail = engine.decode_many([audio], [full[:k]], max_tokens=12 - k, min_tokens=12 - k)[0]
+        assert tail == full[k:], (k, tail, full)
+    # ragged batch: different prefixes per session in one prompt step
+    tails = engine.decode_many([audio, audio, audio], [[], full[:3], full[:7]], max_tokens=4, min_tokens=4)
+    assert tails == [full[:4], full[3:7], full[7:11]]
+
+
+def test_engine_recognizer_returns_prefix_plus_continuation(engine):
+    rec = EngineRecognizer(engine, max_tokens=6)
+    pcm = _speech(1.5, 300)
+    h0 = rec.recognize(pcm)
+    h1 = rec.recognize(pcm, h0.tokens[:2])
+    assert h1.tokens[:2] == h0.tokens[:2] and isinstance(h1.text, str)
+
+
+def test_eight_concurrent_websocket_sessions_batch_their_passes(engine):
+    batcher = AsrBatcher(engine, max_tokens=8)
+
+    def factory():
+        return StreamingAsrSession(batcher, partial_every_s=0.5, endpoint_silence_s=0.3, energy_threshold=300)
+
+    factory.batcher = batcher
+    n_sess, pkt = 8, 960  # 60 ms packets (apps/web/src/App.tsx:279-288)
+    lat = {}
+
+    async def client(c, i):
+        ws = await c.ws_connect("/stream")
+        assert json.loads((await ws.receive()).data)["payload"] == "deepgram_connected"
+        await ws.receive()  # {state: open}
+        pcm = np.concatenate([_speech(1.5, 200 + 37 * i, seed=i), np.zeros(int(0.5 * 16000), np.int16)])
+        t0 = time.perf_counter()
+        finals = []
+
+        async def reader():
+            while True:
+                msg = await ws.receive()
+                if msg.type != 1:  # TEXT
+                    return
+                f = json.loads(msg.data)
+                if f["type"] == "transcript_final":
+                    finals.append(time.perf_counter())
+                    return
+
+        rd = asyncio.ensure_future(reader())
+        for j in range(0, len(pcm), pkt):
+            await ws.send_bytes(pcm[j : j + pkt].tobytes())
+            await asyncio.sleep(0)
+        await asyncio.wait_for(rd, 120)
+        lat[i] = (finals[0] - t0) * 1e3
+        await ws.close()
+
+    async def go():
+        async with TestClient(TestServer(build_app(factory, debounce_ms=10))) as c:
+            await asyncio.gather(*(client(c, i) for i in range(n_sess)))
+            m = await (await c.get("/metrics")).json()
+            return m
+
+    try:
+        m = asyncio.run(go())
+    finally:
+        batcher.close()
+    assert len(lat) == n_sess
+    vals = sorted(lat.values())
+    p50, p95 = statistics.median(vals), vals[min(len(vals) - 1, int(0.95 * len(vals)))]
+    print(json.dumps({"sessions": n_sess, "speech_to_final_ms_p50": round(p50, 1), "speech_to_final_ms_p95": round(p95, 1),
+                      "asr_rows_per_batch": round(batcher.rows_per_batch(), 2), "batches": batcher.stats["batches"]}))
+    assert batcher.rows_per_batch() > 1.0, batcher.stats
+    assert m["asr_batcher"]["max_batch"] > 1
+    assert m["counters"]["finals"] == n_sess

@@ -76,7 +76,9 @@ def test_full_flow_with_fake_brain_and_executor():
                              executor_url=str(es.make_url("")).rstrip("/"), debounce_ms=20)
             async with TestClient(TestServer(vapp)) as c:
                 ws = await c.ws_connect("/stream")
-                assert json.loads((await ws.receive()).data) == {"type": "info", "payload": "asr_connected"}
+                # connection-state frames of the reference's Deepgram socket (server.ts:233-244)
+                assert json.loads((await ws.receive()).data) == {"type": "info", "payload": "deepgram_connected"}
+                assert json.loads((await ws.receive()).data) == {"type": "info", "payload": {"state": "open"}}
                 await ws.send_str(json.dumps({"type": "context_update", "payload": {"url": "https://bestbuy.com"}}))
                 await ws.send_bytes(b"\x01\x00" * 960)
                 p = json.loads((await ws.receive()).data)
@@ -133,3 +135,139 @@ def test_streaming_session_vad_partials_finals():
     assert final[0]["type"] == "Results" and final[0]["speech_final"] is True
     assert final[0]["start"] >= 0.25  # leading silence trimmed (endpoint-sized chunks), stream clock kept
     assert s.flush() == []  # nothing pending
+
+
+def test_recognizer_start_failure_sends_error_frame():
+    def broken():
+        raise RuntimeError("no GPU")
+
+    async def go():
+        async with TestClient(TestServer(build_app(broken, debounce_ms=10))) as c:
+            ws = await c.ws_connect("/stream")
+            assert json.loads((await ws.receive()).data) == {"type": "error", "payload": "deepgram_connect_failed"}
+            await ws.send_bytes(b"\x00\x00" * 960)  # the connection stays usable (audio dropped)
+            await ws.send_str(json.dumps({"type": "context_update", "payload": {"a": 1}}))
+            await ws.close()
+
+    asyncio.run(go())
+
+
+def test_recognizer_error_is_a_state_frame_and_session_continues():
+    class Flaky(FakeAsr):
+        def push(self, data):
+            self.n += 1
+            if self.n == 1:
+                raise RuntimeError("engine fault")
+            return super().push(data)
+
+    async def go():
+        async with TestClient(TestServer(build_app(lambda: Flaky(), debounce_ms=10))) as c:
+            ws = await c.ws_connect("/stream")
+            await _recv_types(ws, ["info"])
+            await ws.receive()  # {state: open}
+            await ws.send_bytes(b"\x01\x00" * 960)
+            err = json.loads((await ws.receive()).data)
+            assert err == {"type": "info", "payload": {"state": "error", "info": "engine fault"}}
+            await ws.send_bytes(b"\x01\x00" * 960)
+            p = json.loads((await ws.receive()).data)
+            assert p["type"] == "transcript_partial"
+            await ws.close()
+
+    asyncio.run(go())
+
+
+def test_context_stays_bounded_over_300_utterances(monkeypatch):
+    """the reference's context grows without bound (server.ts:162-170); here the
+    merged context is capped (oldest keys evicted) so a long session keeps a bounded prompt."""
+    from voice_enabled_browser_automation_amd.utils.context import DEFAULT_MAX_BYTES
+
+    sizes, n_calls = [], [0]
+
+    async def brain(req):
+        body = await req.json()
+        sizes.append(len(json.dumps(body["context"], separators=(",", ":"))))
+        n_calls[0] += 1
+        k = n_calls[0]
+        return web.json_response({"version": "1.0", "intents": [{"type": "scroll", "args": {}, "priority": 0,
+                                                                  "requires_confirmation": True, "retries": 1}],
+                                  "context_updates": {f"note_{k}": "x" * 40, "url": f"https://e.com/{k}"},
+                                  "confidence": 0.9})
+
+    async def go():
+        bapp = web.Application()
+        bapp.router.add_post("/parse", brain)
+        async with TestServer(bapp) as bs:
+            vapp = build_app(lambda: FakeAsr(), brain_url=str(bs.make_url("/parse")), executor_url="http://127.0.0.1:9",
+                             debounce_ms=0)
+            async with TestClient(TestServer(vapp)) as c:
+                ws = await c.ws_connect("/stream")
+                for _ in range(300):
+                    await ws.send_str(json.dumps({"type": "flush"}))
+                    await _recv_types(ws, ["confirmation_required"])
+                await ws.close()
+
+    asyncio.run(go())
+    assert n_calls[0] == 300
+    assert max(sizes) <= DEFAULT_MAX_BYTES
+    assert sizes[-1] > DEFAULT_MAX_BYTES // 2  # still carries recent context
+
+
+def test_context_cap_evicts_oldest_and_refreshes_updated_keys():
+    from voice_enabled_browser_automation_amd.utils.context import cap_context, merge_context
+
+    ctx = {}
+    for i in range(50):
+        ctx = merge_context(ctx, {f"k{i}": "v" * 20, "url": f"u{i}"}, max_bytes=300)
+    assert len(json.dumps(ctx, separators=(",", ":"))) <= 300
+    assert ctx["url"] == "u49" and "k49" in ctx and "k0" not in ctx
+    assert list(ctx)[-1] == "url"  # refreshed every time: youngest
+    assert cap_context({"huge": "x" * 1000}, max_bytes=100) == {}
+
+
+def test_brain_caps_request_context():
+    from voice_enabled_browser_automation_amd.brain.intent_engine import FakeIntentEngine
+    from voice_enabled_browser_automation_amd.brain.server import build_app as brain_app
+
+    reply = {"version": "1.0", "intents": [{"type": "back"}], "confidence": 0.9}
+    eng = FakeIntentEngine(reply=reply)
+
+    async def go():
+        async with TestClient(TestServer(brain_app(eng))) as c:
+            big = {f"k{i}": "y" * 100 for i in range(200)}
+            r = await c.post("/parse", json={"text": "go back", "context": big})
+            assert r.status == 200
+        user = json.loads(eng.calls[0][-1]["content"])
+        assert len(json.dumps(user["context"], separators=(",", ":"))) <= 2048
+        assert "k199" in user["context"] and "k0" not in user["context"]
+
+    asyncio.run(go())
+
+
+def test_local_agreement_commits_stable_prefix():
+    """Interim passes force the tokens two consecutive hypotheses agreed on as the decoder prefix."""
+    from voice_enabled_browser_automation_amd.asr.streaming import Hypothesis
+
+    seen = []
+
+    class Rec:
+        def recognize(self, pcm, prefix=()):
+            seen.append(list(prefix))
+            n = len(pcm) // 8000  # one more "word" per half second of audio
+            toks = list(prefix) + [t for t in range(1, n + 1)][len(prefix):]
+            return Hypothesis(toks, " ".join(map(str, toks)))
+
+    import numpy as np
+
+    s = StreamingAsrSession(Rec(), partial_every_s=0.5, endpoint_silence_s=0.3, energy_threshold=500)
+    sr = 16000
+    speech = (np.sin(2 * np.pi * 220 * np.arange(3 * sr) / sr) * 8000).astype(np.int16)
+    evs = []
+    for chunk in np.split(speech, 30):
+        evs += s.push(chunk.tobytes())
+    fin = s.flush()
+    assert seen[0] == [] and len(seen) >= 5
+    assert any(len(p) > 0 for p in seen[2:]), seen  # later passes decode only past the committed prefix
+    for a, b in zip(seen, seen[1:]):  # the committed prefix only grows
+        assert b[: len(a)] == a
+    assert fin[0]["is_final"] and fin[0]["channel"]["alternatives"][0]["transcript"].startswith("1 2")
+    assert s.committed == [] and s.stats["committed_tokens"] > 0

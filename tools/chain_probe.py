@@ -21,7 +21,6 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--bar-mode", type=int, default=2)
     ap.add_argument("--attn", action="store_true", help="decode attention (ctx 1100) as the first phase")
-    ap.add_argument("--wpol", type=int, default=0, help="weight-load cache policy: 0 default, 2 nt")
     ap.add_argument("--no-wait", action="store_true",
                     help="DIAGNOSTIC: barriers arrive but never wait (wrong results): phase cost without dependencies")
     ap.add_argument("--row-table", action="store_true", help="(always on: the chained attention requires them)")
@@ -40,7 +39,6 @@ def main():
         a.bar_mode = 5 if a.bar_mode >= 4 else 3
     dev, bf = "cuda", torch.bfloat16
     E = ops.ext()
-    E.set_chain_weight_policy(a.wpol)
     torch.manual_seed(0)
     M, d, F, nq, nkv, hd = a.rows, 4096, 14336, 32, 8, 128
     ncopy = 3  # rotate weights over > 256 MB Infinity Cache
@@ -143,7 +141,7 @@ def main():
             col = col[col > 0]
             if col.numel():
                 extra[nm] = [round(float((col.median() - t0) * 10e-3), 2), round(float((col.max() - t0) * 10e-3), 2)]
-    r = dict(kernel="chain_probe", rows=M, ctx=a.ctx if a.attn else None, warm_kv=a.warm_kv, n_splits=a.n_splits, kv_tok_major=a.kv_tok_major, bar_mode=a.bar_mode, wpol=a.wpol, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
+    r = dict(kernel="chain_probe", rows=M, ctx=a.ctx if a.attn else None, warm_kv=a.warm_kv, n_splits=a.n_splits, kv_tok_major=a.kv_tok_major, bar_mode=a.bar_mode, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
              stamps_med_us=[round(x, 2) for x in med], stamps_min_us=[round(x, 2) for x in mn],
              stamps_max_us=[round(x, 2) for x in mx],
              legend=("start,end_attn," if a.attn else "start,") + "end_o,wait_o,end_gu,wait_gu,end_down,wait_down,end_qkv")

@@ -178,7 +178,7 @@ class AsrEngine:
         ops.sample(logits, mask=self.mask_text_eot if allow_eot else self.mask_text, temperature=None,
                    seed=self.d_seed, step=self.d_step, out_tokens=self.d_tok, part_val=self.part_val,
                    part_idx=self.part_idx)
-        return int(self.d_tok.item())
+        return int(self.d_tok[0].item())
 
     # ---- device-resident greedy decode (one session): step graph = forward -> masked argmax ->
     # decode_advance (sampled token becomes the next input, position / context / KV slot move on),
@@ -222,12 +222,17 @@ class AsrEngine:
             self.loop_graphs[key] = g
         return g
 
-    def _decode_device(self, slot: int, first_logits: torch.Tensor, n_max: int, exact: bool) -> List[int]:
+    def _decode_device(self, slot: int, first_logits: torch.Tensor, n_max: int, exact: bool,
+                       P: Optional[int] = None) -> List[int]:
+        """P: the session's prompt length (SOT sequence + any forced prefix) -- the first sampled
+        token sits at position P."""
         cfg = self.model.cfg
         r = self.runner
         b = r.b
-        P = len(self.prompt)
+        P = len(self.prompt) if P is None else P
         n_max = min(n_max, self.loop_out.numel(), r.bps * r.bs - P)
+        if n_max <= 0:
+            return []
         g = self._loop_graph(slot, not exact)
         # row 0 = this session at the last prompt position; the first advance moves it to P
         b.seq_ids[:1].fill_(slot)
@@ -269,11 +274,25 @@ class AsrEngine:
         """Batch of utterances (concurrent voice sessions on this GPU): one batched encoder pass
         ([B, 3000, mels] through conv/flash-attention/GEMMs), then every decode step is one
         ragged row-per-session graph replay with one masked-argmax launch for all sessions."""
+        toks = self.decode_many(audios, max_tokens=max_tokens, min_tokens=min_tokens, exact_tokens=exact_tokens)
+        return [self.tok.decode(o) for o in toks]
+
+    def decode_many(self, audios: List[torch.Tensor], prefixes: Optional[Sequence[Sequence[int]]] = None, *,
+                    max_tokens: int = 96, min_tokens: int = 0, exact_tokens: Optional[int] = None) -> List[List[int]]:
+        """Token ids decoded for each utterance.  ``prefixes[i]``: text tokens forced after the
+        SOT sequence (a streaming session's committed transcript -- asr/streaming.py local
+        agreement): they are prefilled in the same ragged prompt step as the SOT tokens and only
+        the continuation is decoded; the result EXCLUDES the prefix."""
         t0 = time.perf_counter()
         m = self.model
         B = len(audios)
         if B > len(self.free_slots):
             raise RuntimeError(f"{B} utterances exceed the {len(self.free_slots)} free ASR session slots")
+        prefixes = [list(p) for p in prefixes] if prefixes is not None else [[] for _ in range(B)]
+        assert len(prefixes) == B
+        r = self.runner
+        cap = r.bps * r.bs  # decoder positions per session
+        prompts = [self.prompt + p[: max(0, cap - len(self.prompt) - 1)] for p in prefixes]
         slots = [self.free_slots.pop() for _ in range(B)]
         retry = False
         try:
@@ -281,19 +300,15 @@ class AsrEngine:
             enc = m.encode(mel)
             self.set_cross_batch(slots, enc)
             t_enc = time.perf_counter()
-            P = len(self.prompt)
-            per = max(1, max(BUCKETS) // P)  # sessions per prompt step
-            # (clone: every step's logits live in the replayed graph's static output buffer)
-            logits = torch.cat([self.runner.step([(slot, t, p) for slot in slots[i : i + per]
-                                                  for p, t in enumerate(self.prompt)])[P - 1 :: P].clone()
-                                for i in range(0, B, per)])
+            logits = self._prompt_logits(slots, prompts)
             outs: List[List[int]] = [[] for _ in range(B)]
             live = list(range(B))
             n_max = exact_tokens if exact_tokens is not None else max_tokens
+            pos = [len(p) for p in prompts]  # next position per session
+            limit = [min(n_max, cap - len(p)) for p in prompts]
             if B == 1 and self.device_loop and (exact_tokens is not None or min_tokens == 0) and n_max > 0:
-                outs[0] = self._decode_device(slots[0], logits, n_max, exact_tokens is not None)
+                outs[0] = self._decode_device(slots[0], logits, limit[0], exact_tokens is not None, P=pos[0])
                 live = []
-            pos = P
             for i in range(n_max if live else 0):
                 allow_eot = exact_tokens is None and i >= min_tokens
                 toks = self._sample_rows(logits, allow_eot)
@@ -302,23 +317,52 @@ class AsrEngine:
                     if tok == m.cfg.eot or tok < 0:
                         continue
                     outs[j].append(tok)
-                    nxt.append(j)
+                    if len(outs[j]) < limit[j]:
+                        nxt.append(j)
                 live = nxt
                 if not live or i + 1 >= n_max:
                     break
-                logits = self.runner.step([(slots[j], outs[j][-1], pos) for j in live])
-                pos += 1
+                logits = self.runner.step([(slots[j], outs[j][-1], pos[j] + len(outs[j]) - 1) for j in live])
             if self._chain_failed():  # results of a timed-out chained launch are invalid: redo
                 retry = True
-            texts = [self.tok.decode(o) for o in outs]
             t_end = time.perf_counter()
             self.last_stats = dict(encode_ms=(t_enc - t0) * 1e3, decode_ms=(t_end - t_enc) * 1e3,
-                                   total_ms=(t_end - t0) * 1e3, tokens=sum(len(o) for o in outs), batch=B)
+                                   total_ms=(t_end - t0) * 1e3, tokens=sum(len(o) for o in outs), batch=B,
+                                   prefix_tokens=sum(len(p) - len(self.prompt) for p in prompts))
             if not retry:
-                return texts
+                return outs
         finally:
             self.free_slots.extend(slots)
-        return self.transcribe_many(audios, max_tokens=max_tokens, min_tokens=min_tokens, exact_tokens=exact_tokens)
+        return self.decode_many(audios, prefixes, max_tokens=max_tokens, min_tokens=min_tokens,
+                                exact_tokens=exact_tokens)
+
+    def _prompt_logits(self, slots: List[int], prompts: List[List[int]]) -> torch.Tensor:
+        """Prefill every session's prompt (ragged rows, <= 64 per step; a session's rows stay in
+        order) and return the logits of each session's LAST prompt row, in session order."""
+        R = max(BUCKETS)
+        rows: List[Tuple[int, int, int]] = []
+        want: List[int] = []   # row index (within the pending step) of a session's last prompt token
+        got: List[torch.Tensor] = []
+
+        def run():
+            nonlocal rows, want
+            if rows:
+                out = self.runner.step(rows)
+                if want:
+                    # (clone: the logits live in the replayed graph's static output buffer)
+                    got.append(out[torch.tensor(want, device=out.device)].clone())
+            rows, want = [], []
+
+        for slot, prompt in zip(slots, prompts):
+            if len(rows) + len(prompt) > R and len(prompt) <= R:
+                run()
+            for p, t in enumerate(prompt):
+                if len(rows) == R:
+                    run()
+                rows.append((slot, t, p))
+            want.append(len(rows) - 1)
+        run()
+        return torch.cat(got)
 
     def _chain_failed(self) -> bool:
         """Health check of the chained decoder launches (models/whisper.py): a grid barrier that

@@ -5,19 +5,32 @@ The voice server feeds raw PCM16 LE 16 kHz mono frames (the UI sends ~60 ms pack
 apps/web/src/App.tsx:279-288).  A session keeps the current utterance buffer and:
 
 * energy VAD on 20 ms frames tracks speech start and trailing silence;
-* every ``partial_every_s`` of new speech it re-transcribes the buffer and emits an interim
-  result (``is_final: false``), like Deepgram's interim_results;
+* every ``partial_every_s`` of new speech it runs a recognition pass and emits an interim result
+  (``is_final: false``), like Deepgram's interim_results;
+* **local agreement**: the token prefix on which the last two interim hypotheses agree is
+  *committed* -- later passes force it as the decoder prefix (prefilled in one ragged step with
+  the SOT tokens) and decode only the continuation, so a long utterance does not re-decode its
+  whole transcript at every partial, and the committed words never flicker;
 * on an endpoint (``endpoint_silence_s`` of silence after speech), on ``flush()`` (client
   end-of-utterance) or when the 30 s Whisper window is full, it emits a final result
   (``is_final: true, speech_final: true``) and starts a new utterance.
+
+Recognition passes go through a *recognizer* (``recognize(pcm, prefix) -> Hypothesis``).
+``AsrBatcher`` is the serving recognizer: one scheduler thread per GPU engine that gathers the
+pending passes of ALL live sessions and runs them as one batch (``AsrEngine.decode_many``: one
+batched encoder pass, then one ragged decode step per token for every session) -- the
+session-DP unit of a GPU.
 
 Events use the Deepgram ``Results`` shape that the unchanged UI and voice logic read
 (``payload.is_final``, ``payload.channel.alternatives[0].transcript``; apps/voice/src/server.ts:112,123).
 """
 from __future__ import annotations
 
+import threading
 import time
-from typing import Callable, Dict, List, Optional
+from concurrent.futures import Future
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Sequence
 
 import numpy as np
 
@@ -36,11 +49,42 @@ def results_event(text: str, *, is_final: bool, start: float, duration: float, m
     }
 
 
+@dataclass
+class Hypothesis:
+    """One recognition pass: the full transcript's token ids (forced prefix included) and text."""
+
+    tokens: List[int] = field(default_factory=list)
+    text: str = ""
+
+
+class TextRecognizer:
+    """Adapter for a plain ``transcribe(pcm) -> str`` callable (tests, CPU stand-ins): no token
+    ids, so no committed prefix (local agreement is a no-op)."""
+
+    def __init__(self, fn: Callable[[np.ndarray], str]):
+        self.fn = fn
+
+    def recognize(self, pcm: np.ndarray, prefix: Sequence[int] = ()) -> Hypothesis:
+        return Hypothesis([], self.fn(pcm).strip())
+
+
+def _as_recognizer(r: Any):
+    return r if hasattr(r, "recognize") else TextRecognizer(r)
+
+
+def common_prefix(a: Sequence[int], b: Sequence[int]) -> int:
+    n = min(len(a), len(b))
+    i = 0
+    while i < n and a[i] == b[i]:
+        i += 1
+    return i
+
+
 class StreamingAsrSession:
-    def __init__(self, transcribe: Callable[[np.ndarray], str], *, rate: int = 16000, model_name: str = "whisper",
+    def __init__(self, recognizer: Any, *, rate: int = 16000, model_name: str = "whisper",
                  partial_every_s: float = 1.0, endpoint_silence_s: float = 0.6, energy_threshold: float = 300.0,
-                 max_window_s: float = 30.0, min_speech_s: float = 0.2):
-        self.transcribe = transcribe
+                 max_window_s: float = 30.0, min_speech_s: float = 0.2, local_agreement: bool = True):
+        self.rec = _as_recognizer(recognizer)
         self.rate = rate
         self.model_name = model_name
         self.partial_every = int(partial_every_s * rate)
@@ -48,6 +92,7 @@ class StreamingAsrSession:
         self.thresh = energy_threshold
         self.max_window = int(max_window_s * rate)
         self.min_speech = int(min_speech_s * rate)
+        self.local_agreement = local_agreement
         self.frame = rate // 50  # 20 ms
         self.buf = np.zeros(0, dtype=np.int16)
         self._carry = b""
@@ -56,27 +101,52 @@ class StreamingAsrSession:
         self.trailing_silence = 0
         self.since_partial = 0
         self.last_partial = ""
-        self.stats: Dict[str, float] = {"partials": 0, "finals": 0, "asr_ms": 0.0}
+        self.committed: List[int] = []   # agreed token prefix of the current utterance
+        self.prev_tokens: List[int] = []  # previous interim hypothesis
+        self.stats: Dict[str, float] = {"partials": 0, "finals": 0, "asr_ms": 0.0, "passes": 0,
+                                        "committed_tokens": 0}
 
     # ------------------------------------------------------------------ internals
-    def _run(self) -> str:
+    def _run(self) -> Hypothesis:
         t0 = time.perf_counter()
-        text = self.transcribe(self.buf)
+        hyp = self.rec.recognize(self.buf, self.committed if self.local_agreement else ())
         self.stats["asr_ms"] += (time.perf_counter() - t0) * 1e3
-        return text.strip()
+        self.stats["passes"] += 1
+        return hyp
 
-    def _final(self) -> List[Dict]:
-        out: List[Dict] = []
-        if self.speech >= self.min_speech and len(self.buf):
-            text = self._run()
-            out.append(results_event(text, is_final=True, start=self.t_offset, duration=len(self.buf) / self.rate,
-                                     model=self.model_name))
-            self.stats["finals"] += 1
+    def _reset_utterance(self) -> None:
         self.t_offset += len(self.buf) / self.rate
         self.buf = np.zeros(0, dtype=np.int16)
         self.speech = self.trailing_silence = self.since_partial = 0
         self.last_partial = ""
+        self.committed = []
+        self.prev_tokens = []
+
+    def _final(self) -> List[Dict]:
+        out: List[Dict] = []
+        if self.speech >= self.min_speech and len(self.buf):
+            hyp = self._run()
+            out.append(results_event(hyp.text, is_final=True, start=self.t_offset, duration=len(self.buf) / self.rate,
+                                     model=self.model_name))
+            self.stats["finals"] += 1
+        self._reset_utterance()
         return out
+
+    def _partial(self) -> List[Dict]:
+        hyp = self._run()
+        if self.local_agreement and hyp.tokens:
+            # LocalAgreement-2: what two consecutive hypotheses agree on is stable
+            n = common_prefix(self.prev_tokens, hyp.tokens)
+            if n > len(self.committed):
+                self.stats["committed_tokens"] += n - len(self.committed)
+                self.committed = list(hyp.tokens[:n])
+            self.prev_tokens = list(hyp.tokens)
+        if hyp.text == self.last_partial:
+            return []
+        self.last_partial = hyp.text
+        self.stats["partials"] += 1
+        return [results_event(hyp.text, is_final=False, start=self.t_offset, duration=len(self.buf) / self.rate,
+                              model=self.model_name)]
 
     # ------------------------------------------------------------------ API
     def push(self, data: bytes) -> List[Dict]:
@@ -111,20 +181,105 @@ class StreamingAsrSession:
                 self.trailing_silence = 0
         if self.speech >= self.min_speech and self.since_partial >= self.partial_every:
             self.since_partial = 0
-            text = self._run()
-            if text != self.last_partial:
-                self.last_partial = text
-                events.append(results_event(text, is_final=False, start=self.t_offset,
-                                            duration=len(self.buf) / self.rate, model=self.model_name))
-                self.stats["partials"] += 1
+            events += self._partial()
         return events
 
     def flush(self) -> List[Dict]:
         return self._final()
 
+    def close(self) -> None:
+        pass
+
+
+# ---------------------------------------------------------------------------------- recognizers
+class EngineRecognizer:
+    """Serial recognizer on an AsrEngine (one pass at a time, caller's thread)."""
+
+    def __init__(self, asr_engine, *, max_tokens: int = 96):
+        self.eng = asr_engine
+        self.max_tokens = max_tokens
+
+    def recognize(self, pcm: np.ndarray, prefix: Sequence[int] = ()) -> Hypothesis:
+        toks = self.eng.decode_many([self.eng.pcm_to_audio(pcm)], [list(prefix)], max_tokens=self.max_tokens)[0]
+        full = list(prefix) + toks
+        return Hypothesis(full, self.eng.tok.decode(full).strip())
+
+
+class AsrBatcher:
+    """Cross-session batching of recognition passes on one ASR engine (one GPU).
+
+    ``recognize`` is called from the voice server's worker threads (one blocking call per session
+    pass); the scheduler thread takes EVERY pass queued since its last batch -- up to the
+    engine's free session slots -- and runs them as one ``decode_many`` batch.  While a batch is
+    on the GPU the next one accumulates, so under load each GPU pass serves many sessions."""
+
+    def __init__(self, asr_engine, *, max_tokens: int = 96, max_batch: Optional[int] = None):
+        self.eng = asr_engine
+        self.max_tokens = max_tokens
+        self.max_batch = max_batch or len(asr_engine.free_slots)
+        self._q: List[tuple] = []
+        self._cv = threading.Condition()
+        self._stop = False
+        self.stats = {"batches": 0, "passes": 0, "max_batch": 0, "gpu_ms": 0.0}
+        dev = getattr(asr_engine.model, "device", None)
+        self._cuda_index = None
+        if dev is not None and getattr(dev, "type", "cpu") == "cuda":
+            import torch
+
+            self._cuda_index = dev.index if dev.index is not None else torch.cuda.current_device()
+        self._thread = threading.Thread(target=self._loop, name="asr-batcher", daemon=True)
+        self._thread.start()
+
+    def recognize(self, pcm: np.ndarray, prefix: Sequence[int] = ()) -> Hypothesis:
+        fut: Future = Future()
+        with self._cv:
+            if self._stop:
+                raise RuntimeError("ASR batcher stopped")
+            self._q.append((np.array(pcm, dtype=np.int16, copy=True), list(prefix), fut))
+            self._cv.notify()
+        return fut.result()
+
+    def rows_per_batch(self) -> float:
+        return self.stats["passes"] / max(1, self.stats["batches"])
+
+    def _loop(self) -> None:
+        if self._cuda_index is not None:
+            import torch
+
+            torch.cuda.set_device(self._cuda_index)
+        while True:
+            with self._cv:
+                while not self._q and not self._stop:
+                    self._cv.wait()
+                if self._stop and not self._q:
+                    return
+                batch, self._q = self._q[: self.max_batch], self._q[self.max_batch :]
+            t0 = time.perf_counter()
+            try:
+                audios = [self.eng.pcm_to_audio(p) for p, _, _ in batch]
+                toks = self.eng.decode_many(audios, [pre for _, pre, _ in batch], max_tokens=self.max_tokens)
+                for (_, pre, fut), t in zip(batch, toks):
+                    full = pre + t
+                    fut.set_result(Hypothesis(full, self.eng.tok.decode(full).strip()))
+            except BaseException as e:  # noqa: BLE001  (fail this batch's passes, keep serving)
+                for _, _, fut in batch:
+                    if not fut.done():
+                        fut.set_exception(e)
+            n = len(batch)
+            self.stats["batches"] += 1
+            self.stats["passes"] += n
+            self.stats["max_batch"] = max(self.stats["max_batch"], n)
+            self.stats["gpu_ms"] += (time.perf_counter() - t0) * 1e3
+
+    def close(self) -> None:
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+        self._thread.join(timeout=30)
+
 
 def make_asr_transcriber(asr_engine, *, tokens_per_s: Optional[float] = None) -> Callable[[np.ndarray], str]:
-    """Adapter: AsrEngine -> transcribe(pcm int16) callable."""
+    """Adapter: AsrEngine -> transcribe(pcm int16) callable (fixed-work mode with tokens_per_s)."""
 
     def fn(pcm: np.ndarray) -> str:
         audio = asr_engine.pcm_to_audio(pcm)

@@ -266,6 +266,7 @@ class LLMIntentEngine:
         # the LM head under the same masks: only vocab tiles some row may sample are computed
         logits = self.engine.head_logits(col_mask=mask if self.masked_head else None, mask_rows=n)
         toks = self._sample(logits, n, self.engine.step_fail_word())
+        self.engine.host_synced()  # the sampled tokens are back: the step's staging copy has run
         if any(t == -2 for t in toks):
             # the forward's chained launch timed out at a grid barrier (tokens -2 from the
             # sampler's fail word): re-run the step on the per-kernel path and sample again

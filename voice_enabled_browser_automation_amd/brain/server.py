@@ -25,6 +25,7 @@ from typing import Any, Optional
 from aiohttp import web
 
 from ..contracts import ParseRequest, ParseResponse, safe_parse
+from ..utils.context import cap_context
 from ..utils.metrics import Metrics
 from .prompt import messages_for
 
@@ -76,6 +77,10 @@ def build_app(engine: Any = None) -> web.Application:
             m.inc("invalid_request")
             return web.json_response({"error": "invalid_request", "detail": pr.format_error()}, status=400)
         request = pr.data
+        # bounded context: whatever a client accumulated, the prompt stays
+        # inside the model's window (oldest keys evicted first)
+        if isinstance(request.get("context"), dict):
+            request = {**request, "context": cap_context(request["context"])}
         eng = app["engine"]
         try:
             out = await call(eng, messages_for(request))

@@ -32,6 +32,7 @@ import re
 import shutil
 import subprocess
 import tempfile
+import threading
 from typing import Any, Dict, List, Optional
 
 import aiohttp
@@ -480,6 +481,14 @@ async def connect(endpoint: str, proc: Optional[subprocess.Popen] = None,
     return CdpConnection(ws, http, proc, profile_dir)
 
 
+def _drain(stream) -> None:
+    try:
+        for _ in stream:
+            pass
+    except (OSError, ValueError):
+        pass
+
+
 async def launch_chrome(headless: bool = True, executable: Optional[str] = None,
                         timeout: float = 30.0) -> CdpConnection:
     exe = executable or find_chrome()
@@ -487,18 +496,27 @@ async def launch_chrome(headless: bool = True, executable: Optional[str] = None,
         raise RuntimeError("no Chrome / Chromium found (set CHROME_PATH) and playwright is not installed")
     prof = tempfile.mkdtemp(prefix="vwa-chrome-")
     args = [exe, "--remote-debugging-port=0", f"--user-data-dir={prof}", "--no-first-run",
-            "--no-default-browser-check", "--window-size=1366,768", "about:blank"]
+            "--no-default-browser-check", "--window-size=1366,768", "--disable-dev-shm-usage"]
+    if hasattr(os, "geteuid") and os.geteuid() == 0:
+        args.append("--no-sandbox")  # Chrome refuses to run as root with its sandbox (Playwright's default too)
+    args.append("about:blank")
     if headless:
         args.insert(1, "--headless=new")
     proc = subprocess.Popen(args, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
     loop = asyncio.get_running_loop()
 
     def _read_url() -> Optional[str]:
+        url = None
         for line in proc.stderr:  # "DevTools listening on ws://127.0.0.1:PORT/devtools/browser/<id>"
             m = re.search(r"DevTools listening on (ws://\S+)", line)
             if m:
-                return m.group(1)
-        return None
+                url = m.group(1)
+                break
+        if url is not None:
+            # keep draining: Chrome logs to stderr for its whole life, and a full 64 KB pipe would
+            # block its next log write (the browser hangs mid-session)
+            threading.Thread(target=_drain, args=(proc.stderr,), name="chrome-stderr", daemon=True).start()
+        return url
 
     try:
         url = await asyncio.wait_for(loop.run_in_executor(None, _read_url), timeout)

@@ -144,6 +144,10 @@ class LLMEngine:
         self.graph_pool = None
         self.stats = dict(steps=0, rows=0, prefill_tokens=0, cached_tokens=0, graph_replays=0)
         self._last_step = None  # (rows, logits_for, n_computed before) of a chained step, for recover_step
+        # True from a step's launch until the host knows the stream has passed it: the pinned
+        # staging rows (h_meta, h_row_table) are read by that step's H2D copy -- inside the
+        # replayed graph -- so the next step may only rewrite them once it has executed
+        self._staging_inflight = False
         self._head_rows: Optional[torch.Tensor] = None  # the last step's hidden rows for head_logits()
 
     # ------------------------------------------------------------------ sequences
@@ -253,6 +257,12 @@ class LLMEngine:
         n = len(rows)
         M = bucket_for(n)
         b = self.bufs
+        if self._staging_inflight:
+            # back-to-back steps with no host sync in between (several admissions in one scheduler
+            # iteration, partial feeds, non-chained check=False steps): the previous step's copy of
+            # the staging rows may still be queued behind its forward
+            torch.cuda.current_stream().synchronize()
+            self._staging_inflight = False
         if getattr(self, "_chain_retry_at", None) is not None:
             self._maybe_rearm_chain()
         if logits_for is None or len(logits_for) == n:
@@ -304,6 +314,7 @@ class LLMEngine:
             self.stats["graph_replays"] += 1
         else:
             hs = self._forward_rows(M, L)
+        self._staging_inflight = self.device.type == "cuda"
         for sid, ln in pending.items():
             self.seqs[sid].n_computed = ln
         self.stats["steps"] += 1
@@ -312,6 +323,7 @@ class LLMEngine:
             self._check_chain()
         if check and chained and self.device.type == "cuda":
             torch.cuda.current_stream().synchronize()
+            self._staging_inflight = False
             if self.model.chain_error():
                 self._head_rows = None
                 return self.recover_step()
@@ -319,6 +331,11 @@ class LLMEngine:
         if defer_head:
             return None
         return self.head_logits()
+
+    def host_synced(self) -> None:
+        """The caller has observed the stream past the last step (e.g. read its sampled tokens):
+        the next run_rows may rewrite the pinned staging rows without a synchronize."""
+        self._staging_inflight = False
 
     def head_logits(self, col_mask: Optional[torch.Tensor] = None, mask_rows: int = 1) -> torch.Tensor:
         """LM head of the last ``run_rows`` step's selected rows -> f32 logits [rows, V].
@@ -355,6 +372,8 @@ class LLMEngine:
         self.model.disable_chain()
         if word is not None:
             word.zero_()
+        if getattr(self, "_chain_err_h", None) is not None:
+            self._chain_err_h.zero_()  # the pinned copy may hold this failure: _check_chain must not re-see it
         self.graphs.clear()
         self.stats["chain_fallbacks"] = self.stats.get("chain_fallbacks", 0) + 1
         self._schedule_chain_retry()
@@ -371,8 +390,8 @@ class LLMEngine:
         Non-blocking by default: reads the word copied to pinned memory at the previous check (the
         step has been synchronised since) and queues the next copy."""
         m = self.model
-        if getattr(m, "chain_error", None) is None:
-            return
+        if getattr(m, "chain_error", None) is None or getattr(m, "_chain_disabled", False):
+            return  # (already on the per-kernel path: a recovery handled this failure)
         if blocking or self.device.type != "cuda":
             err = m.chain_error()
         else:

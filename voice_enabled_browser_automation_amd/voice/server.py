@@ -29,6 +29,7 @@ from typing import Any, Callable, Dict, Optional
 import aiohttp
 from aiohttp import WSMsgType, web
 
+from ..utils.context import merge_context
 from ..utils.metrics import Metrics
 
 VERSION = "0.1.0"
@@ -50,7 +51,12 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
     None = passthrough mode (no recognizer, as the reference without DEEPGRAM_API_KEY)."""
     app = web.Application()
     app["metrics"] = Metrics("voice")
-    app["asr_pool"] = ThreadPoolExecutor(max_workers=1, thread_name_prefix="asr")  # one GPU stream of work
+    # one worker per live session pass: a session's recognition pass blocks its worker inside the
+    # recognizer (asr/streaming.py AsrBatcher), whose single scheduler thread batches the passes
+    # of all sessions onto the GPU -- so the pool only needs to be as wide as the session count
+    app["asr_pool"] = ThreadPoolExecutor(max_workers=int(os.environ.get("VWA_MAX_SESSIONS", "32")) + 4,
+                                         thread_name_prefix="asr")
+    app["asr_factory"] = asr_factory
     brain_url = brain_url or os.environ.get("BRAIN_URL", "http://127.0.0.1:8090/parse")
     executor_url = executor_url or os.environ.get("EXECUTOR_URL", "http://127.0.0.1:7081")
     if debounce_ms is None:
@@ -70,7 +76,11 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
         return web.json_response({"status": "ok", "service": "voice", "version": VERSION})
 
     async def metrics(_req):
-        return web.json_response(app["metrics"].snapshot())
+        snap = app["metrics"].snapshot()
+        batcher = getattr(asr_factory, "batcher", None)
+        if batcher is not None:  # cross-session ASR batching: passes per GPU batch
+            snap["asr_batcher"] = dict(batcher.stats, rows_per_batch=round(batcher.rows_per_batch(), 3))
+        return web.json_response(snap)
 
     async def stream(req: web.Request) -> web.WebSocketResponse:
         ws = web.WebSocketResponse()
@@ -91,11 +101,35 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
             except (ConnectionResetError, RuntimeError):
                 st["closed"] = True
 
-        asr = asr_factory() if asr_factory is not None else None
-        if asr is not None:
-            await send({"type": "info", "payload": "asr_connected"})
+        # connection-state frames as the reference sends them for its Deepgram socket
+        # (apps/voice/src/server.ts:233-250): "deepgram_connected" once the recognizer exists, then
+        # the recognizer's own state events {state: open|close|error, info}; a recognizer that
+        # cannot be created -> error "deepgram_connect_failed" and the connection stays up
+        # without transcription (as the reference, whose audio then goes nowhere)
+        asr = None
+        if asr_factory is not None:
+            try:
+                asr = asr_factory()
+            except Exception as e:  # noqa: BLE001
+                print(f"[voice] recognizer start failed: {e}", flush=True)
+                m.inc("asr_connect_failed")
+                await send({"type": "error", "payload": "deepgram_connect_failed"})
+            else:
+                await send({"type": "info", "payload": "deepgram_connected"})
+                await send({"type": "info", "payload": {"state": "open"}})
         else:
             await send({"type": "warn", "payload": "no_api_key; running in passthrough"})
+
+        async def asr_call(fn, *a):
+            """One recognizer call on the worker pool; an engine failure is reported as the
+            reference reports a Deepgram socket error ({state: "error", info}) and the session
+            continues (the next audio retries)."""
+            try:
+                return await loop.run_in_executor(app["asr_pool"], fn, *a)
+            except Exception as e:  # noqa: BLE001
+                m.inc("asr_errors")
+                await send({"type": "info", "payload": {"state": "error", "info": str(e) or e.__class__.__name__}})
+                return []
 
         async def run_executor(safe):
             try:
@@ -131,7 +165,7 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                 if isinstance(resp, dict) and resp.get("tts_summary"):
                     await send({"type": "tts", "payload": resp["tts_summary"]})
                 if isinstance(resp, dict) and isinstance(resp.get("context_updates"), dict):
-                    st["context"] = {**st["context"], **resp["context_updates"]}
+                    st["context"] = merge_context(st["context"], resp["context_updates"])
                 intents = resp.get("intents") if isinstance(resp, dict) else None
                 if isinstance(intents, list):
                     safe = [i for i in intents if not (isinstance(i, dict) and i.get("requires_confirmation"))]
@@ -180,7 +214,7 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                         st["t_utt"] = time.perf_counter()
                     if asr is not None:
                         t_push = time.perf_counter()
-                        events = await loop.run_in_executor(app["asr_pool"], asr.push, msg.data)
+                        events = await asr_call(asr.push, msg.data)
                         dt = time.perf_counter() - t_push
                         m.observe("asr_push_ms", dt * 1e3)
                         if events:  # a recognition pass ran: real-time factor of this packet's work
@@ -197,9 +231,9 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                         await ws.close()
                         break
                     if ctl.get("type") == "context_update" and isinstance(ctl.get("payload"), dict):
-                        st["context"] = {**st["context"], **ctl["payload"]}
+                        st["context"] = merge_context(st["context"], ctl["payload"])
                     elif ctl.get("type") == "flush" and asr is not None:
-                        events = await loop.run_in_executor(app["asr_pool"], asr.flush)
+                        events = await asr_call(asr.flush)
                         await handle_events(events)
                 elif msg.type in (WSMsgType.ERROR, WSMsgType.CLOSE):
                     break
@@ -207,6 +241,8 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
             st["closed"] = True
             if st["debounce"] is not None:
                 st["debounce"].cancel()
+            if asr is not None and hasattr(asr, "close"):
+                asr.close()
         return ws
 
     app.router.add_get("/health", health)
@@ -222,7 +258,7 @@ def asr_factory_from_env() -> Optional[Callable[[], Any]]:
     import torch
 
     from ..asr.engine import AsrEngine
-    from ..asr.streaming import StreamingAsrSession, make_asr_transcriber
+    from ..asr.streaming import AsrBatcher, StreamingAsrSession
     from ..models.config import get_config
     from ..models.whisper import WhisperModel
     from ..tokenizer import load_tokenizer
@@ -235,10 +271,15 @@ def asr_factory_from_env() -> Optional[Callable[[], Any]]:
 
     model = WhisperModel(get_config(name), device=dev, weights=LazySafetensors(wpath) if wpath else None)
     eng = AsrEngine(model, load_tokenizer("whisper"),
-                    max_sessions=int(os.environ.get("VWA_MAX_SESSIONS", "4")))
-    fn = make_asr_transcriber(eng)
+                    max_sessions=int(os.environ.get("VWA_MAX_SESSIONS", "8")))
+    batcher = AsrBatcher(eng)
     every = float(os.environ.get("VWA_PARTIAL_EVERY_S", "1.0"))
-    return lambda: StreamingAsrSession(fn, model_name=name, partial_every_s=every)
+
+    def factory():
+        return StreamingAsrSession(batcher, model_name=name, partial_every_s=every)
+
+    factory.batcher = batcher
+    return factory
 
 
 def main():
