@@ -180,6 +180,83 @@ void skinny_gemm_swiglu(Tensor x, Tensor w_gu, c10::optional<Tensor> bias, Tenso
   check_rc(run_skinny_checked(2, p, cur_stream(x)), "skinny_gemm_swiglu");
 }
 
+int device_cus(const Tensor& t) {
+  static int cached[64] = {0};
+  const int d = t.device().index();
+  if (d >= 0 && d < 64 && cached[d]) return cached[d];
+  int cus = 0;
+  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess, "CU count");
+  if (d >= 0 && d < 64) cached[d] = cus;
+  return cus;
+}
+
+// LDS-tiled MFMA GEMM (gemm.hip), M > 16 rows.  epi: 0 store (+bias, bf16 / f32 out), 1 residual
+// add (+bias), 2 SwiGLU over interleaved gate/up tiles (y [M, N/2]), 3 GELU (+bias).  rstd: f32
+// [M] per-row RMSNorm scale applied to the product (gammas folded into w).  ws: f32 split-K
+// workspace (the launcher splits K only when the output tiles alone cannot fill the CUs).
+void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi, c10::optional<Tensor> rstd,
+          c10::optional<Tensor> residual, bool w_tiled, c10::optional<Tensor> ws) {
+  c10::DeviceGuard g(x.device());
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  check_contig_rows(x, "x");
+  TORCH_CHECK(w.is_contiguous() && w.dim() == 2 && w.size(1) == x.size(1), "w must be contiguous [N, K] with x's K");
+  TORCH_CHECK(epi >= 0 && epi <= 3, "gemm: bad epilogue");
+  GemmParams p{};
+  p.X = bfp(x);
+  p.ldx = (int)x.stride(0);
+  p.W = bfp(w);
+  p.w_tiled = w_tiled ? 1 : 0;
+  p.M = (int)x.size(0);
+  p.N = (int)w.size(0);
+  p.K = (int)w.size(1);
+  TORCH_CHECK(p.N % 16 == 0 && p.K % 128 == 0, "gemm: N % 16 == 0 and K % 128 == 0 required");
+  if (epi == 2) TORCH_CHECK(p.N % 32 == 0, "gemm SwiGLU: gate/up rows must be a multiple of 32");
+  TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1 && y.size(0) == p.M &&
+                  y.size(1) == (epi == 2 ? p.N / 2 : p.N),
+              "y shape");
+  TORCH_CHECK(y.scalar_type() == at::kBFloat16 || (y.scalar_type() == at::kFloat && epi != 2), "y bf16 (or f32)");
+  p.Y = y.data_ptr();
+  p.ldy = (int)y.stride(0);
+  p.y_f32 = y.scalar_type() == at::kFloat;
+  if (bias.has_value()) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->numel() == p.N && bias->is_contiguous(), "bias [N]");
+    p.bias = bfp(*bias);
+  }
+  if (epi == 1) {
+    TORCH_CHECK(residual.has_value(), "residual epilogue needs residual");
+    check_bf16(*residual, "residual");
+    TORCH_CHECK(residual->dim() == 2 && residual->size(0) == p.M && residual->size(1) == p.N &&
+                    residual->stride(1) == 1,
+                "residual shape");
+    TORCH_CHECK(!p.y_f32, "residual epilogue writes bf16");
+    p.R = bfp(*residual);
+    p.ldr = (int)residual->stride(0);
+  }
+  if (rstd.has_value()) {
+    TORCH_CHECK(rstd->is_cuda() && rstd->scalar_type() == at::kFloat && rstd->numel() >= p.M, "rstd f32 [M]");
+    p.rstd = rstd->data_ptr<float>();
+  }
+  p.splits = 1;
+  if (ws.has_value()) {
+    TORCH_CHECK(ws->is_cuda() && ws->scalar_type() == at::kFloat && ws->is_contiguous(), "ws f32");
+    p.ws = ws->data_ptr<float>();
+    p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws->numel());
+  }
+  check_rc(vwa_gemm((int)epi, &p, cur_stream(x)), "gemm");
+}
+
+void row_rstd(Tensor x, Tensor rstd, double eps) {
+  c10::DeviceGuard g(x.device());
+  check_bf16(x, "x");
+  check_contig_rows(x, "x");
+  TORCH_CHECK(rstd.is_cuda() && rstd.scalar_type() == at::kFloat && rstd.numel() >= x.size(0), "rstd f32 [M]");
+  check_rc(vwa_row_rstd(bfp(x), (int)x.stride(0), (int)x.size(0), (int)x.size(1), (float)eps, rstd.data_ptr<float>(),
+                        cur_stream(x)),
+           "row_rstd");
+}
+
 void check_cache(const Tensor& c, const char* name) {
   check_bf16(c, name);
   // any block / head / token strides (the kernels address by stride), contiguous head_dim rows
@@ -659,34 +736,94 @@ void embedding(Tensor ids, Tensor table, c10::optional<Tensor> pos_table, c10::o
            "embedding");
 }
 
-void sample(Tensor logits, c10::optional<Tensor> mask, c10::optional<Tensor> temperature, Tensor seed, Tensor step,
-            Tensor out_tokens, Tensor part_val, Tensor part_idx, c10::optional<Tensor> fail_word) {
-  c10::DeviceGuard g(logits.device());
-  TORCH_CHECK(logits.scalar_type() == at::kFloat && logits.dim() == 2 && logits.stride(1) == 1, "logits f32 2-D");
-  const int rows = (int)logits.size(0), V = (int)logits.size(1);
-  int mask_words = 0;
+struct SampleArgs {
+  int rows = 0, V = 0, mask_words = 0;
+  const uint32_t* mask = nullptr;
+  const float* temperature = nullptr;
+  const int64_t* fail = nullptr;
+};
+
+SampleArgs check_sample(const Tensor& logits, const c10::optional<Tensor>& mask,
+                        const c10::optional<Tensor>& temperature, const Tensor& seed, const Tensor& step,
+                        const Tensor& out_tokens, const c10::optional<Tensor>& fail_word, int64_t v_offset) {
+  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kFloat && logits.dim() == 2 && logits.stride(1) == 1,
+              "logits f32 2-D on the GPU");
+  SampleArgs a;
+  a.rows = (int)logits.size(0);
+  a.V = (int)logits.size(1);
+  TORCH_CHECK(v_offset >= 0 && v_offset % 32 == 0, "v_offset must be a non-negative multiple of 32");
   if (mask.has_value()) {
-    TORCH_CHECK(mask->scalar_type() == at::kInt && mask->dim() == 2 && mask->is_contiguous() && mask->size(0) >= rows,
+    // (pinned host rows allowed: zero-copy grammar masks)
+    TORCH_CHECK((mask->is_cuda() || mask->is_pinned()) && mask->scalar_type() == at::kInt && mask->dim() == 2 &&
+                    mask->is_contiguous() && mask->size(0) >= a.rows,
                 "mask int32 [rows, words]");
-    mask_words = (int)mask->size(1);
-    TORCH_CHECK(mask_words * 32 >= V, "mask too short");
+    a.mask_words = (int)mask->size(1);
+    TORCH_CHECK((int64_t)a.mask_words * 32 >= v_offset + a.V, "mask too short");
+    a.mask = reinterpret_cast<const uint32_t*>(mask->data_ptr<int>());
   }
-  if (temperature.has_value())
-    TORCH_CHECK(temperature->scalar_type() == at::kFloat && temperature->numel() >= rows, "temperature");
-  TORCH_CHECK(seed.scalar_type() == at::kLong && step.scalar_type() == at::kInt, "seed int64, step int32");
-  TORCH_CHECK(out_tokens.scalar_type() == at::kInt && out_tokens.numel() >= rows, "out_tokens");
-  const int n_chunks = (int)(part_val.numel() / rows);
-  TORCH_CHECK(n_chunks >= 1 && part_idx.numel() >= (int64_t)rows * n_chunks, "partials");
-  if (fail_word.has_value())
+  if (temperature.has_value()) {
+    TORCH_CHECK(temperature->scalar_type() == at::kFloat && temperature->numel() >= a.rows, "temperature");
+    a.temperature = temperature->data_ptr<float>();
+  }
+  TORCH_CHECK(seed.is_cuda() && step.is_cuda() && seed.scalar_type() == at::kLong && step.scalar_type() == at::kInt,
+              "seed int64, step int32 (device)");
+  TORCH_CHECK((out_tokens.is_cuda() || out_tokens.is_pinned()) && out_tokens.scalar_type() == at::kInt &&
+                  out_tokens.numel() >= a.rows,
+              "out_tokens");
+  if (fail_word.has_value()) {
     TORCH_CHECK(fail_word->scalar_type() == at::kLong && fail_word->numel() >= 1 && fail_word->is_cuda(),
                 "fail_word: one device int64");
-  check_rc(vwa_sample(logits.data_ptr<float>(), (int)logits.stride(0), rows, V,
-                      mask.has_value() ? reinterpret_cast<const uint32_t*>(mask->data_ptr<int>()) : nullptr,
-                      mask_words, temperature.has_value() ? temperature->data_ptr<float>() : nullptr,
-                      reinterpret_cast<const uint64_t*>(seed.data_ptr<int64_t>()), step.data_ptr<int>(),
-                      out_tokens.data_ptr<int>(), part_val.data_ptr<float>(), part_idx.data_ptr<int>(), n_chunks,
-                      fail_word.has_value() ? fail_word->data_ptr<int64_t>() : nullptr, cur_stream(logits)),
-           "sample");
+    a.fail = fail_word->data_ptr<int64_t>();
+  }
+  return a;
+}
+
+void sample(Tensor logits, c10::optional<Tensor> mask, c10::optional<Tensor> temperature, Tensor seed, Tensor step,
+            Tensor out_tokens, Tensor part_val, Tensor part_idx, c10::optional<Tensor> fail_word, int64_t v_offset) {
+  c10::DeviceGuard g(logits.device());
+  const SampleArgs a = check_sample(logits, mask, temperature, seed, step, out_tokens, fail_word, v_offset);
+  const int n_chunks = (int)(part_val.numel() / a.rows);
+  TORCH_CHECK(n_chunks >= 1 && part_idx.numel() >= (int64_t)a.rows * n_chunks, "partials");
+  hipStream_t st = cur_stream(logits);
+  check_rc(vwa_sample_partial(logits.data_ptr<float>(), (int)logits.stride(0), a.rows, a.V, (int)v_offset, a.mask,
+                              a.mask_words, a.temperature, reinterpret_cast<const uint64_t*>(seed.data_ptr<int64_t>()),
+                              step.data_ptr<int>(), part_val.data_ptr<float>(), part_idx.data_ptr<int>(), n_chunks, st),
+           "sample (partial)");
+  check_rc(vwa_sample_final(part_val.data_ptr<float>(), part_idx.data_ptr<int>(), n_chunks, 1, 0,
+                            out_tokens.data_ptr<int>(), step.data_ptr<int>(), a.rows, a.fail, st),
+           "sample (final)");
+}
+
+// Vocab-parallel sampling (SURVEY.md §2.8 C4 as [B, 2] per rank): partial maxima over this rank's
+// logits shard (global ids from v_offset) into xin = [val f32 | idx i32] x [rows][n_chunks], the
+// one-shot IPC all-gather of xin over the TP group, then every rank merges all ranks' partials in
+// rank order -- bit-identical tokens on every rank, and the same token a TP=1 sampler draws
+// (the Gumbel noise and the tie-break use global token ids).  Three launches, no host sync.
+void sample_tp(Tensor logits, c10::optional<Tensor> mask, c10::optional<Tensor> temperature, Tensor seed, Tensor step,
+               Tensor out_tokens, Tensor xin, Tensor xout, int64_t n_chunks, c10::optional<Tensor> fail_word,
+               int64_t v_offset, int64_t ar_state, int64_t world) {
+  c10::DeviceGuard g(logits.device());
+  const SampleArgs a = check_sample(logits, mask, temperature, seed, step, out_tokens, fail_word, v_offset);
+  const int64_t words = 2 * (int64_t)a.rows * n_chunks;
+  TORCH_CHECK(n_chunks >= 1 && n_chunks <= 1024, "n_chunks");
+  TORCH_CHECK(world >= 1 && world <= 8 && ar_state != 0, "TP group state");
+  TORCH_CHECK(words <= vwa_ar_gather_max_words(), "sampler partials exceed the all-gather region");
+  TORCH_CHECK(xin.is_cuda() && xin.scalar_type() == at::kInt && xin.is_contiguous() && xin.numel() >= words,
+              "xin int32 [>= 2 * rows * n_chunks]");
+  TORCH_CHECK(xout.is_cuda() && xout.scalar_type() == at::kInt && xout.is_contiguous() && xout.numel() >= world * words,
+              "xout int32 [>= world * 2 * rows * n_chunks]");
+  hipStream_t st = cur_stream(logits);
+  int* in = xin.data_ptr<int>();
+  check_rc(vwa_sample_partial(logits.data_ptr<float>(), (int)logits.stride(0), a.rows, a.V, (int)v_offset, a.mask,
+                              a.mask_words, a.temperature, reinterpret_cast<const uint64_t*>(seed.data_ptr<int64_t>()),
+                              step.data_ptr<int>(), reinterpret_cast<float*>(in), in + a.rows * n_chunks,
+                              (int)n_chunks, st),
+           "sample_tp (partial)");
+  int* out = xout.data_ptr<int>();
+  check_rc(vwa_ar_gather(reinterpret_cast<void*>(ar_state), in, out, words, st), "sample_tp (all-gather)");
+  check_rc(vwa_sample_final(reinterpret_cast<const float*>(out), out + a.rows * n_chunks, (int)n_chunks, (int)world,
+                            words, out_tokens.data_ptr<int>(), step.data_ptr<int>(), a.rows, a.fail, st),
+           "sample_tp (merge)");
 }
 
 void pcm16_to_f32(Tensor pcm, Tensor out, double ratio) {
@@ -769,6 +906,16 @@ void ar_allreduce(int64_t st, Tensor in, Tensor out) {
   check_rc(vwa_ar_allreduce(reinterpret_cast<void*>(st), bfp(in), bfp_mut(out), in.numel(), cur_stream(in)),
            "one-shot all-reduce");
 }
+void ar_gather(int64_t st, Tensor in, Tensor out) {
+  c10::DeviceGuard g(in.device());
+  TORCH_CHECK(in.is_cuda() && in.scalar_type() == at::kInt && in.is_contiguous() && out.is_cuda() &&
+                  out.scalar_type() == at::kInt && out.is_contiguous() && out.numel() % in.numel() == 0 &&
+                  in.numel() <= vwa_ar_gather_max_words(),
+              "ar_gather: int32 in [n], out [world * n] on the GPU");
+  check_rc(vwa_ar_gather(reinterpret_cast<void*>(st), in.data_ptr<int>(), out.data_ptr<int>(), in.numel(),
+                         cur_stream(in)),
+           "one-shot all-gather");
+}
 int64_t ar_error(int64_t st) { return vwa_ar_error(reinterpret_cast<void*>(st)); }
 void ar_destroy(int64_t st) { vwa_ar_destroy(reinterpret_cast<void*>(st)); }
 
@@ -778,6 +925,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ar_handles", &ar_handles);
   m.def("ar_open_peer", &ar_open_peer);
   m.def("ar_allreduce", &ar_allreduce);
+  m.def("ar_gather", &ar_gather);
   m.def("ar_error", &ar_error);
   m.def("ar_destroy", &ar_destroy);
   m.doc() = "MI355X (gfx950) HIP kernels for the voice-web-agent inference engine";
@@ -810,6 +958,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("attn_g") = 0, py::arg("seq") = 0);
   m.def("alloc_uncached_i32", &alloc_uncached_i32);
   m.def("decode_advance", &decode_advance);
+  m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
+        py::arg("rstd") = py::none(), py::arg("residual") = py::none(), py::arg("w_tiled") = false,
+        py::arg("ws") = py::none());
+  m.def("row_rstd", &row_rstd);
   m.def("rmsnorm", &rmsnorm);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);
@@ -818,7 +970,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_attention", &decode_attention);
   m.def("flash_attention", &flash_attention);
   m.def("embedding", &embedding);
-  m.def("sample", &sample);
+  m.def("sample", &sample, py::arg("logits"), py::arg("mask"), py::arg("temperature"), py::arg("seed"), py::arg("step"),
+        py::arg("out_tokens"), py::arg("part_val"), py::arg("part_idx"), py::arg("fail_word") = py::none(),
+        py::arg("v_offset") = 0);
+  m.def("sample_tp", &sample_tp);
   m.def("pcm16_to_f32", &pcm16_to_f32);
   m.def("log_mel", &log_mel);
   m.def("conv1d_gelu", &conv1d_gelu);

@@ -17,6 +17,11 @@
 //   4. acquire (system-scope fence) and sum the chunk of all ranks' staging buffers in rank
 //      order (bit-identical result on every rank) into the output.
 // Buffers come from hipMalloc and are shared with hipIpcGetMemHandle / hipIpcOpenMemHandle.
+//
+// The same buffers also carry a one-shot ALL-GATHER of small int32 payloads (vwa_ar_gather: the
+// vocab-parallel sampler's per-rank partial (value, index) maxima, SURVEY.md §2.8 C4 as [B, 2]
+// instead of [B, V/T] logits): a separate double-buffered region behind the all-reduce staging
+// and its own flag / epoch slot (index kMaxBlocks), same protocol, one workgroup.
 #include "common.h"
 
 using namespace vwa;
@@ -26,11 +31,37 @@ namespace {
 constexpr int kMaxRanks = 8;
 constexpr int kThreads = 512;
 constexpr int kMaxBlocks = 64;
+constexpr int kGatherSlot = kMaxBlocks;   // flag / epoch slot of the all-gather
+constexpr int kSlots = kMaxBlocks + 1;
+constexpr int64_t kGatherWords = 64 * 1024;  // int32 words per rank per call (256 KB)
 
 struct ArPeers {
-  uint16_t* staging[kMaxRanks];  // each rank's staging base (2 x max_elems bf16)
-  int* flags[kMaxRanks];         // each rank's flag array [kMaxBlocks][kMaxRanks]
+  uint16_t* staging[kMaxRanks];  // each rank's staging base (2 x max_elems bf16, then 2 x kGatherWords int32)
+  int* flags[kMaxRanks];         // each rank's flag array [kSlots][kMaxRanks]
 };
+
+// signal every peer (flag slot [slot][rank] in the peer's memory) and wait for every peer's
+// signal in our own array; bounded: a peer that never arrives raises the error word
+__device__ void ar_signal_wait(const ArPeers& peers, int slot, int rank, int world, int e, int* error) {
+  if (threadIdx.x < world) {
+    __threadfence_system();
+    __hip_atomic_store(peers.flags[threadIdx.x] + slot * kMaxRanks + rank, e, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x < world) {
+    int* f = peers.flags[rank] + slot * kMaxRanks + threadIdx.x;
+    int64_t spins = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1ll << 24)) {  // ~seconds: a peer never arrived
+        atomicExch(error, 1);
+        break;
+      }
+    }
+    __threadfence_system();
+  }
+  __syncthreads();
+}
 
 __global__ __launch_bounds__(kThreads) void oneshot_ar_kernel(const uint16_t* __restrict__ in, uint16_t* out,
                                                               int64_t n, int64_t max_elems,
@@ -48,26 +79,8 @@ __global__ __launch_bounds__(kThreads) void oneshot_ar_kernel(const uint16_t* __
   for (int64_t i = lo + (int64_t)threadIdx.x * 8; i < hi; i += (int64_t)kThreads * 8)
     *reinterpret_cast<uint4*>(mine + i) = *reinterpret_cast<const uint4*>(in + i);
   __syncthreads();
-  // 2. release + signal every peer (flag slot [b][rank] lives in the peer's memory)
-  if (threadIdx.x < world) {
-    __threadfence_system();
-    __hip_atomic_store(peers.flags[threadIdx.x] + b * kMaxRanks + rank, e, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  // 3. wait for every peer's signal in our own flag array (bounded)
-  if (threadIdx.x < world) {
-    int* f = peers.flags[rank] + b * kMaxRanks + threadIdx.x;
-    int64_t spins = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1ll << 24)) {  // ~seconds: a peer never arrived
-        atomicExch(error, 1);
-        break;
-      }
-    }
-    __threadfence_system();
-  }
-  __syncthreads();
+  // 2. release + signal every peer, 3. wait for every peer's signal (bounded)
+  ar_signal_wait(peers, b, rank, world, e, error);
   // 4. reduce in rank order
   for (int64_t i = lo + (int64_t)threadIdx.x * 8; i < hi; i += (int64_t)kThreads * 8) {
     float acc[8];
@@ -85,12 +98,34 @@ __global__ __launch_bounds__(kThreads) void oneshot_ar_kernel(const uint16_t* __
   if (threadIdx.x == 0) epochs[b] = e;
 }
 
+// out[p * n + i] = rank p's in[i] on every rank (n <= kGatherWords int32 words); one workgroup
+__global__ __launch_bounds__(kThreads) void oneshot_gather_kernel(const int* __restrict__ in, int* __restrict__ out,
+                                                                  int n, int64_t gather_off, int rank, int world,
+                                                                  ArPeers peers, int* epochs, int* error) {
+  __shared__ int s_epoch;
+  if (threadIdx.x == 0) s_epoch = epochs[kGatherSlot] + 1;
+  __syncthreads();
+  const int e = s_epoch;
+  auto region = [&](int p) {
+    return reinterpret_cast<int*>(reinterpret_cast<char*>(peers.staging[p]) + gather_off) + (int64_t)(e & 1) * kGatherWords;
+  };
+  int* mine = region(rank);
+  for (int i = threadIdx.x; i < n; i += kThreads) mine[i] = in[i];
+  __syncthreads();
+  ar_signal_wait(peers, kGatherSlot, rank, world, e, error);
+  for (int p = 0; p < world; ++p) {
+    const int* src = region(p);
+    for (int i = threadIdx.x; i < n; i += kThreads) out[(int64_t)p * n + i] = src[i];
+  }
+  if (threadIdx.x == 0) epochs[kGatherSlot] = e;
+}
+
 struct ArState {
   int rank = 0, world = 1;
   int64_t max_elems = 0;
   uint16_t* staging = nullptr;  // local
-  int* flags = nullptr;         // local [kMaxBlocks][kMaxRanks]
-  int* epochs = nullptr;        // local, private [kMaxBlocks]
+  int* flags = nullptr;         // local [kSlots][kMaxRanks]
+  int* epochs = nullptr;        // local, private [kSlots]
   int* error = nullptr;
   ArPeers peers{};
   bool opened[kMaxRanks] = {};
@@ -107,14 +142,14 @@ void* vwa_ar_create(int rank, int world, int64_t max_elems) {
   s->rank = rank;
   s->world = world;
   s->max_elems = max_elems;
-  if (hipMalloc(&s->staging, 2 * max_elems * sizeof(uint16_t)) != hipSuccess ||
-      hipMalloc(&s->flags, kMaxBlocks * kMaxRanks * sizeof(int)) != hipSuccess ||
-      hipMalloc(&s->epochs, kMaxBlocks * sizeof(int)) != hipSuccess || hipMalloc(&s->error, sizeof(int)) != hipSuccess) {
+  if (hipMalloc(&s->staging, 2 * max_elems * sizeof(uint16_t) + 2 * kGatherWords * sizeof(int)) != hipSuccess ||
+      hipMalloc(&s->flags, kSlots * kMaxRanks * sizeof(int)) != hipSuccess ||
+      hipMalloc(&s->epochs, kSlots * sizeof(int)) != hipSuccess || hipMalloc(&s->error, sizeof(int)) != hipSuccess) {
     delete s;
     return nullptr;
   }
-  (void)hipMemset(s->flags, 0, kMaxBlocks * kMaxRanks * sizeof(int));
-  (void)hipMemset(s->epochs, 0, kMaxBlocks * sizeof(int));
+  (void)hipMemset(s->flags, 0, kSlots * kMaxRanks * sizeof(int));
+  (void)hipMemset(s->epochs, 0, kSlots * sizeof(int));
   (void)hipMemset(s->error, 0, sizeof(int));
   (void)hipDeviceSynchronize();
   s->peers.staging[rank] = s->staging;
@@ -158,6 +193,20 @@ int vwa_ar_allreduce(void* st, const uint16_t* in, uint16_t* out, int64_t n, hip
                      s->rank, s->world, s->peers, s->epochs, s->error);
   return (int)hipGetLastError();
 }
+
+// All-gather of n int32 words per rank: out[world][n].  n <= kGatherWords.
+int vwa_ar_gather(void* st, const int* in, int* out, int64_t n, hipStream_t stream) {
+  auto* s = static_cast<ArState*>(st);
+  if (n < 0 || n > kGatherWords) return -1;
+  for (int p = 0; p < s->world; ++p)
+    if (!s->peers.staging[p] || !s->peers.flags[p]) return -2;
+  hipLaunchKernelGGL(oneshot_gather_kernel, dim3(1), dim3(kThreads), 0, stream, in, out, (int)n,
+                     (int64_t)(2 * s->max_elems * sizeof(uint16_t)), s->rank, s->world, s->peers, s->epochs,
+                     s->error);
+  return (int)hipGetLastError();
+}
+
+int64_t vwa_ar_gather_max_words() { return kGatherWords; }
 
 // Non-zero if a call timed out waiting for a peer (sticky).
 int vwa_ar_error(void* st) {

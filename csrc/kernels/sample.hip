@@ -33,7 +33,8 @@ VWA_DEVICE void argmax_merge(float& bv, int& bi, float v, int i) {
 constexpr int kMaskWordsMax = 4096;  // mask words per chunk staged in LDS (16 KB)
 
 __global__ __launch_bounds__(256) void sample_partial_kernel(const float* __restrict__ logits, int ld, int V,
-                                                             const uint32_t* __restrict__ mask, int mask_words,
+                                                             int v_off, const uint32_t* __restrict__ mask,
+                                                             int mask_words,
                                                              const float* __restrict__ temperature,
                                                              const uint64_t* __restrict__ seed,
                                                              const int* __restrict__ step, float* part_val,
@@ -46,9 +47,10 @@ __global__ __launch_bounds__(256) void sample_partial_kernel(const float* __rest
   const int v0 = chunk * per, v1 = min(V, v0 + per);
   // the chunk's mask words, all loaded at once into LDS: the mask may live in pinned HOST memory
   // (zero-copy: no H2D copy per step), where a per-token load would be a PCIe round trip each
+  // (v_off: global id of local column 0 under vocab parallelism, a multiple of 32)
   const int w0 = v0 >> 5, nw = v1 > v0 ? ((v1 - 1) >> 5) - w0 + 1 : 0;
   if (mask)
-    for (int i = threadIdx.x; i < nw; i += 256) smask[i] = mask[(int64_t)row * mask_words + w0 + i];
+    for (int i = threadIdx.x; i < nw; i += 256) smask[i] = mask[(int64_t)row * mask_words + (v_off >> 5) + w0 + i];
   __syncthreads();
   const float T = temperature ? temperature[row] : 0.f;
   const float invT = T > 0.f ? 1.f / T : 1.f;
@@ -61,12 +63,13 @@ __global__ __launch_bounds__(256) void sample_partial_kernel(const float* __rest
       if (!((wd >> (v & 31)) & 1u)) continue;
     }
     float key = logits[(int64_t)row * ld + v];
+    const int gv = v_off + v;  // global token id: the noise and the index are vocab-shard invariant
     if (T > 0.f) {
-      const uint64_t h = splitmix64(base ^ (uint64_t)v);
+      const uint64_t h = splitmix64(base ^ (uint64_t)gv);
       const float u = ((float)(h >> 41) + 0.5f) * (1.0f / 8388608.0f);  // in (0,1), exact in f32
       key = key * invT - __logf(-__logf(u));
     }
-    argmax_merge(bv, bi, key, v);
+    argmax_merge(bv, bi, key, gv);
   }
   sv[threadIdx.x] = bv;
   si[threadIdx.x] = bi;
@@ -91,6 +94,7 @@ __global__ __launch_bounds__(256) void sample_partial_kernel(const float* __rest
 
 __global__ __launch_bounds__(256) void sample_final_kernel(const float* __restrict__ part_val,
                                                            const int* __restrict__ part_idx, int n_chunks,
+                                                           int n_src, int64_t src_stride,
                                                            int* out_tokens, int* step, int rows,
                                                            const int64_t* __restrict__ fail_word) {
   __shared__ float sv[256];
@@ -98,7 +102,9 @@ __global__ __launch_bounds__(256) void sample_final_kernel(const float* __restri
   const int row = blockIdx.x;
   float bv = -INFINITY;
   int bi = 0x7fffffff;
-  for (int c = threadIdx.x; c < n_chunks; c += 256) argmax_merge(bv, bi, part_val[row * n_chunks + c], part_idx[row * n_chunks + c]);
+  for (int p = 0; p < n_src; ++p)
+    for (int c = threadIdx.x; c < n_chunks; c += 256)
+      argmax_merge(bv, bi, part_val[p * src_stride + row * n_chunks + c], part_idx[p * src_stride + row * n_chunks + c]);
   sv[threadIdx.x] = bv;
   si[threadIdx.x] = bi;
   __syncthreads();
@@ -126,14 +132,31 @@ __global__ __launch_bounds__(256) void sample_final_kernel(const float* __restri
 
 }  // namespace
 
+extern "C" int vwa_sample_partial(const float* logits, int ld, int rows, int V, int v_off, const uint32_t* mask,
+                                  int mask_words, const float* temperature, const uint64_t* seed, const int* step,
+                                  float* part_val, int* part_idx, int n_chunks, hipStream_t st) {
+  if (n_chunks < 1 || n_chunks > 1024 || rows < 1 || (v_off & 31)) return -1;
+  if (mask && ((V + n_chunks - 1) / n_chunks + 31) / 32 + 1 > kMaskWordsMax) return -10;
+  if (mask && (int64_t)mask_words * 32 < (int64_t)v_off + V) return -11;
+  hipLaunchKernelGGL(sample_partial_kernel, dim3(rows, n_chunks), dim3(256), 0, st, logits, ld, V, v_off, mask,
+                     mask_words, temperature, seed, step, part_val, part_idx, n_chunks);
+  return (int)hipGetLastError();
+}
+
+extern "C" int vwa_sample_final(const float* part_val, const int* part_idx, int n_chunks, int n_src,
+                                int64_t src_stride, int* out_tokens, int* step, int rows, const int64_t* fail_word,
+                                hipStream_t st) {
+  if (n_chunks < 1 || n_src < 1 || rows < 1) return -1;
+  hipLaunchKernelGGL(sample_final_kernel, dim3(rows), dim3(256), 0, st, part_val, part_idx, n_chunks, n_src,
+                     src_stride, out_tokens, step, rows, fail_word);
+  return (int)hipGetLastError();
+}
+
 extern "C" int vwa_sample(const float* logits, int ld, int rows, int V, const uint32_t* mask, int mask_words,
                           const float* temperature, const uint64_t* seed, const int* step, int* out_tokens,
                           float* part_val, int* part_idx, int n_chunks, const int64_t* fail_word, hipStream_t st) {
-  if (n_chunks < 1 || n_chunks > 1024) return -1;
-  if (mask && ((V + n_chunks - 1) / n_chunks + 31) / 32 + 1 > kMaskWordsMax) return -10;
-  hipLaunchKernelGGL(sample_partial_kernel, dim3(rows, n_chunks), dim3(256), 0, st, logits, ld, V, mask, mask_words,
-                     temperature, seed, step, part_val, part_idx, n_chunks);
-  hipLaunchKernelGGL(sample_final_kernel, dim3(rows), dim3(256), 0, st, part_val, part_idx, n_chunks, out_tokens,
-                     const_cast<int*>(step), rows, fail_word);
-  return (int)hipGetLastError();
+  const int r = vwa_sample_partial(logits, ld, rows, V, 0, mask, mask_words, temperature, seed, step, part_val,
+                                   part_idx, n_chunks, st);
+  if (r) return r;
+  return vwa_sample_final(part_val, part_idx, n_chunks, 1, 0, out_tokens, const_cast<int*>(step), rows, fail_word, st);
 }

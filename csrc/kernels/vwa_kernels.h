@@ -112,6 +112,18 @@ struct ChainParams {
   int attn_flag;
 };
 
+// LDS-tiled MFMA GEMM (gemm.hip) for M > 16 rows: Y = epi(rstd[m] * X . W^T (+bias) ...)
+struct GemmParams {
+  const uint16_t* X; int ldx;       // [M, K] bf16 row-major
+  const uint16_t* W; int w_tiled;   // [N, K] bf16: pre-tiled (ops.tile_weight) or row-major
+  int M, N, K;
+  void* Y; int ldy; int y_f32;      // [M, N] (SwiGLU: [M, N/2]) bf16 or f32
+  const uint16_t* bias;             // [N] or null
+  const uint16_t* R; int ldr;       // residual (epilogue 1), may alias Y
+  const float* rstd;                // [M] per-row scale (RMSNorm with gamma folded into W) or null
+  float* ws; int splits; int kg_per_split;  // split-K f32 slabs [splits][M][N] (launcher fills kg_per_split)
+};
+
 struct FlashAttnParams {
   const uint16_t* q; int64_t q_stride_b, q_stride_s, q_stride_h;   // q[b][s][h][d]
   KVView kv;                        // keys of sequence b: table row b
@@ -132,6 +144,9 @@ int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipS
 int vwa_chain_prepare(ChainParams* cp, int grid);
 int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid, hipStream_t st,
                      int xg2 = 0);
+int vwa_gemm(int epi, const GemmParams* p, hipStream_t st);
+int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats);
+int vwa_row_rstd(const uint16_t* x, int ldx, int M, int K, float eps, float* rstd, hipStream_t st);
 int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
                 uint16_t* y, int rows, int D, int ldx, float eps, hipStream_t st);
 int vwa_layernorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
@@ -151,6 +166,14 @@ int vwa_embedding(const int* ids, const uint16_t* table, const uint16_t* pos_tab
 int vwa_sample(const float* logits, int ld, int rows, int V, const uint32_t* mask, int mask_words,
                const float* temperature, const uint64_t* seed, const int* step, int* out_tokens,
                float* part_val, int* part_idx, int n_chunks, const int64_t* fail_word, hipStream_t st);
+// vocab-parallel sampling stages: partial maxima over the local vocab shard (global token ids =
+// v_off + local column; mask rows indexed by global id), then the merge of n_src ranks' partials
+// (rank p's at part_val / part_idx + p * src_stride)
+int vwa_sample_partial(const float* logits, int ld, int rows, int V, int v_off, const uint32_t* mask, int mask_words,
+                       const float* temperature, const uint64_t* seed, const int* step, float* part_val,
+                       int* part_idx, int n_chunks, hipStream_t st);
+int vwa_sample_final(const float* part_val, const int* part_idx, int n_chunks, int n_src, int64_t src_stride,
+                     int* out_tokens, int* step, int rows, const int64_t* fail_word, hipStream_t st);
 int vwa_pcm16_to_f32(const int16_t* pcm, float* out, int n_in, int n_out, float ratio, hipStream_t st);
 int vwa_log_mel(const float* audio, int n_samples, int n_frames, const float* window, const float* dft_cos,
                 const float* dft_sin, const float* mel_fb, int n_mels, float* mel_out, float* max_buf,
@@ -167,6 +190,8 @@ int vwa_ar_handles(void* st, void* out);
 int vwa_ar_handle_bytes();
 int vwa_ar_open_peer(void* st, int p, const void* in);
 int vwa_ar_allreduce(void* st, const uint16_t* in, uint16_t* out, int64_t n, hipStream_t stream);
+int vwa_ar_gather(void* st, const int* in, int* out, int64_t n, hipStream_t stream);
+int64_t vwa_ar_gather_max_words();
 int vwa_ar_error(void* st);
 void vwa_ar_destroy(void* st);
 #ifdef __cplusplus

@@ -61,7 +61,8 @@ def test_voice_to_intent_to_execution_on_gpu(tmp_path):
                                debounce_ms=20)
             async with TestClient(TestServer(vapp)) as c:
                 ws = await c.ws_connect("/stream")
-                assert json.loads((await ws.receive()).data) == {"type": "info", "payload": "asr_connected"}
+                assert json.loads((await ws.receive()).data) == {"type": "info", "payload": "deepgram_connected"}
+                assert json.loads((await ws.receive()).data) == {"type": "info", "payload": {"state": "open"}}
                 await ws.send_str(json.dumps({"type": "context_update", "payload": {"url": "https://www.bestbuy.com"}}))
                 pcm = _speech(2.0).tobytes()
                 for i in range(0, len(pcm), 1920):  # 60 ms packets, as the UI sends them

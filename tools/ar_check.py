@@ -59,6 +59,28 @@ def main():
     us = (time.perf_counter() - t0) / 200 * 1e6
     if rank == 0:
         print(f"graph_err={gerr} oneshot_graph_us={us:.1f} error_flag={ar.error()}", flush=True)
+    # one-shot all-gather (vocab-parallel sampler exchange), eager and replayed
+    for n in (1, 100, 4096):
+        mine = torch.arange(n, dtype=torch.int32, device="cuda") + 1000 * rank
+        got = ar.gather(mine)
+        torch.cuda.synchronize()
+        want_g = torch.stack([torch.arange(n, dtype=torch.int32) + 1000 * p for p in range(world)])
+        ok &= bool(torch.equal(got.cpu(), want_g))
+    src = torch.full((64,), rank + 7, dtype=torch.int32, device="cuda")
+    gout = torch.zeros((world, 64), dtype=torch.int32, device="cuda")
+    g2 = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        ar.gather(src, gout)
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g2):
+        ar.gather(src, gout)
+    for k in range(10):
+        src.fill_(rank + 7 + k)
+        g2.replay()
+        torch.cuda.synchronize()
+        ok &= bool(all(int(gout[p, 0]) == p + 7 + k for p in range(world)))
+    if rank == 0:
+        print(f"gather_ok={ok}", flush=True)
     ok &= not ar.error()
     dist.barrier()
     ar.close()

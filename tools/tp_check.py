@@ -3,10 +3,14 @@
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29556 \
         tools/tp_check.py
 Every rank builds the TP shard of the same random model (deterministic per-layer generator),
-runs prefill + ragged decode through the hipGraph engine with the one-shot all-reduce for the
-row-parallel outputs and the vocab-parallel LM head, and compares the logits with a TP=1 model
-run on the same device.  VWA_DIST_BACKEND selects the control/collective backend (gloo here,
-since RCCL needs one GPU per rank).
+runs prefill + ragged decode through the engine -- eagerly AND with every decode step replayed
+from a hipGraph -- with the one-shot IPC all-reduce for the vocab-parallel embedding and the
+row-parallel outputs, and compares the (diagnostically gathered) logits with a TP=1 model run
+on the same device.  Then the vocab-parallel sampler (partial maxima -> one-shot IPC all-gather
+-> merge, ops.sample tp=...) is checked token for token against the TP=1 full-vocab sampler,
+under grammar-like random masks and temperature.  VWA_DIST_BACKEND selects the control /
+large-message backend (gloo when two ranks share one GPU, RCCL needs one GPU per rank); the
+decode step itself contains no torch.distributed call, so it is graph-captured either way.
 """
 import os
 import sys
@@ -15,6 +19,7 @@ import torch
 import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from voice_enabled_browser_automation_amd import ops  # noqa: E402
 from voice_enabled_browser_automation_amd.models.config import LlamaConfig  # noqa: E402
 from voice_enabled_browser_automation_amd.models.llama import LlamaModel  # noqa: E402
 from voice_enabled_browser_automation_amd.parallel.tp import TPContext, init_distributed  # noqa: E402
@@ -26,12 +31,38 @@ CFG = LlamaConfig(name="tp", vocab_size=4096, hidden=512, n_layers=3, n_heads=8,
 
 def run(model, toks, graphs):
     e = LLMEngine(model, max_seqs=2, max_model_len=512, kv_blocks=80, use_graphs=graphs)
+    if graphs:
+        e.capture_all()
     s = e.new_sequence(toks[:100], use_prefix_cache=False)
     out = [e.prefill(s).float().cpu().clone()]
     for t in toks[100:104]:
         out.append(e.run_rows([(s, t)]).float().cpu().clone())
     out.append(e.run_rows([(s, t) for t in toks[104:110]], logits_for=[5]).float().cpu().clone())
-    return out
+    return out, e
+
+
+def sample_check(tp, dev, ref_model, tp_model):
+    """Tokens of the vocab-parallel sampler == tokens of the full-vocab sampler on the same logits."""
+    torch.manual_seed(1)
+    rows, V = 5, CFG.vocab_size
+    full = torch.randn(rows, V, device=dev) * 2
+    words = (V + 31) // 32
+    mask = torch.randint(-2**31, 2**31 - 1, (rows, words), dtype=torch.int64).to(torch.int32).to(dev)
+    temp = torch.full((rows,), 0.3, device=dev)
+    seed = torch.tensor([99], dtype=torch.int64, device=dev)
+    ok = True
+    for step0 in range(4):
+        want = torch.zeros(rows, dtype=torch.int32, device=dev)
+        ops.sample(full, mask=mask, temperature=temp if step0 % 2 else None, seed=seed,
+                   step=torch.tensor([step0], dtype=torch.int32, device=dev), out_tokens=want)
+        got = torch.zeros(rows, dtype=torch.int32, device=dev)
+        shard = full[:, tp_model.v_start : tp_model.v_end].contiguous()
+        ops.sample(shard, mask=mask, temperature=temp if step0 % 2 else None, seed=seed,
+                   step=torch.tensor([step0], dtype=torch.int32, device=dev), out_tokens=got,
+                   v_offset=tp_model.v_start, tp=tp)
+        torch.cuda.synchronize()
+        ok &= torch.equal(got.cpu(), want.cpu())
+    return ok
 
 
 def main():
@@ -40,20 +71,30 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     torch.manual_seed(0)
     toks = torch.randint(0, CFG.vocab_size, (110,)).tolist()
-    ref = run(LlamaModel(CFG, device=dev, seed=7, tp=TPContext.single()), toks, graphs=False)
+    ref_model = LlamaModel(CFG, device=dev, seed=7, tp=TPContext.single())
+    ref, _ = run(ref_model, toks, graphs=False)
     ok = True
-    # gloo collectives (the vocab all-gather) cannot be captured into a hipGraph; with RCCL they can
-    for graphs in ((False,) if dist.get_backend() == "gloo" else (False, True)):
-        got = run(LlamaModel(CFG, device=dev, seed=7, tp=tp), toks, graphs=graphs)
+    for graphs in (False, True):
+        m = LlamaModel(CFG, device=dev, seed=7, tp=tp)
+        got, e = run(m, toks, graphs=graphs)
         errs = [(a - b).abs().max().item() for a, b in zip(got, ref)]
         ok &= max(errs) < 0.05 * (1 + max(r.abs().max().item() for r in ref))
+        if graphs:
+            ok &= e.stats["graph_replays"] >= 5
         if tp.rank == 0:
-            print(f"graphs={graphs} custom_ar={tp.custom_ar is not None} max_errs={[round(x, 4) for x in errs]}",
-                  flush=True)
+            print(f"graphs={graphs} custom_ar={tp.custom_ar is not None} embed_rows={m.embed.shape[0]} "
+                  f"replays={e.stats['graph_replays']} max_errs={[round(x, 4) for x in errs]}", flush=True)
+    s_ok = sample_check(tp, dev, ref_model, m)
+    ok &= s_ok
+    if tp.custom_ar is not None:
+        ok &= not tp.custom_ar.error()
+    if tp.rank == 0:
+        print(f"vocab_parallel_sampling_equal={s_ok}", flush=True)
     res = torch.tensor([int(ok)])
     dist.all_reduce(res, op=dist.ReduceOp.MIN)
     if tp.rank == 0:
         print("TP_CHECK", "PASS" if res.item() else "FAIL", flush=True)
+    dist.barrier()
     if tp.custom_ar is not None:
         tp.custom_ar.close()
     dist.destroy_process_group()

@@ -264,7 +264,7 @@ class LLMIntentEngine:
             self.d_mask[:n].copy_(self.h_mask[:n], non_blocking=True)
         mask = self.h_mask if self.zero_copy else self.d_mask
         # the LM head under the same masks: only vocab tiles some row may sample are computed
-        logits = self.engine.head_logits(col_mask=mask if self.masked_head else None, mask_rows=n)
+        logits = self.engine.head_logits(col_mask=mask if self.masked_head else None, mask_rows=n, gather=False)
         toks = self._sample(logits, n, self.engine.step_fail_word())
         self.engine.host_synced()  # the sampled tokens are back: the step's staging copy has run
         if any(t == -2 for t in toks):
@@ -288,10 +288,10 @@ class LLMIntentEngine:
         zc = self.zero_copy
         if zc and self.spin_wait:
             self.h_tok_np[:n] = _TOK_PENDING  # before the launch: the sampler stores into it directly
-        ops.sample(logits, mask=self.h_mask if zc else self.d_mask,
-                   temperature=self.d_temp if self.temperature > 0 else None, seed=self.d_seed, step=self.d_step,
-                   out_tokens=self.h_tok if zc else self.d_tok, part_val=self.part_val[: n * 64],
-                   part_idx=self.part_idx[: n * 64], fail_word=fail_word)
+        self.engine.sample(logits, mask=self.h_mask if zc else self.d_mask,
+                           temperature=self.d_temp if self.temperature > 0 else None, seed=self.d_seed,
+                           step=self.d_step, out_tokens=self.h_tok if zc else self.d_tok,
+                           part_val=self.part_val[: n * 64], part_idx=self.part_idx[: n * 64], fail_word=fail_word)
         if self.dev.type == "cuda" and zc and self.spin_wait:
             t3 = time.perf_counter()
             hv = self.h_tok_np[:n]

@@ -188,15 +188,26 @@ class TPIntentEngine:
         self.last_stats = self.inner.last_stats
         return out
 
+    def parse(self, request, repair: bool = False):
+        return self(messages_for(request, repair=repair))
+
+    def stop(self):
+        """Rank 0: release the TP workers from worker_loop."""
+        self._bcast(None)
+
     def worker_loop(self):
+        """TP ranks != 0: follow rank 0's requests until stop(); returns the answers decoded here
+        (identical to rank 0's: lockstep decode, vocab-parallel sampling)."""
+        outs = []
         while True:
             messages = self._bcast(None)
             if messages is None:
-                return
+                return outs
             try:
-                self.inner(messages)
+                outs.append(self.inner(messages))
             except Exception as e:  # noqa: BLE001  (rank 0 reports the error to the client)
                 print(f"[brain worker {self.tp.rank}] {e}", flush=True)
+                outs.append(None)
 
 
 def main():

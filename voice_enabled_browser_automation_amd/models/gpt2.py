@@ -172,7 +172,7 @@ class GPT2Model:
         return self.lm_logits(bufs, hs) if head else hs
 
     def lm_logits(self, bufs, hs: torch.Tensor, col_mask: Optional[torch.Tensor] = None,
-                  mask_rows: int = 1) -> torch.Tensor:
+                  mask_rows: int = 1, gather: bool = True) -> torch.Tensor:
         """Final LayerNorm + tied LM head -> f32 logits (same contract as LlamaModel.lm_logits)."""
         hs = ops.layernorm(hs, self.lnf_w, self.lnf_b, eps=self.cfg.ln_eps)
         n = hs.shape[0]

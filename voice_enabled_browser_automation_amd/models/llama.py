@@ -61,7 +61,9 @@ class LlamaModel:
         self.F = cfg.ffn // T
         self.hd = cfg.head_dim
         V = cfg.vocab_size
-        self.v_per = (V + T - 1) // T
+        # vocab shards start on 32-token boundaries: the grammar mask words (32 tokens each) and
+        # the masked LM head's tile skipping then line up with every shard
+        self.v_per = ((V + T - 1) // T + 31) // 32 * 32
         self.v_start = self.tp.rank * self.v_per
         self.v_end = min(V, self.v_start + self.v_per)
         self.rope = ops.rope_table(cfg.max_pos, cfg.head_dim, cfg.rope_theta, device=self.device)
@@ -78,13 +80,15 @@ class LlamaModel:
             self._tile_weights()
 
     def _tile_weights(self) -> None:
-        """Second, pre-tiled copy of every projection + the LM head (ops.TiledWeight): the decode
-        streaming / chained kernels read it with 1 KB contiguous load instructions (Llama-3-8B
-        layer tail 89.6 vs 101.4 us, tools/chain_probe.py); prefill GEMMs keep the row-major copy."""
+        """Every projection + the LM head re-laid out ONCE into the pre-tiled MFMA-fragment order
+        (ops.TiledWeight; the row-major copy is freed): the decode streaming / chained kernels read
+        it with 1 KB contiguous load instructions (Llama-3-8B layer tail 89.6 vs 101.4 us,
+        tools/chain_probe.py) and the prefill / many-row GEMM (gemm.hip) stages it to LDS as is."""
         T = ops.TiledWeight
         for L in self.layers:
             L.qkv, L.o, L.gu, L.down = T(L.qkv), T(L.o), T(L.gu), T(L.down)
         self.lm_head = T(self.lm_head)
+        torch.cuda.empty_cache()
 
     def _quantize_fp8(self) -> None:
         q = ops.FP8Weight.quantize
@@ -115,7 +119,8 @@ class LlamaModel:
         gen = torch.Generator(device=dev)
         std = cfg.init_std
         gen.manual_seed(seed * 1000003 + 1)
-        self.embed = _randn(gen, (cfg.vocab_size, cfg.hidden), std, dev, dt)
+        embed = _randn(gen, (cfg.vocab_size, cfg.hidden), std, dev, dt)
+        self.embed = self._vocab_shard(embed)
         ones = torch.ones(cfg.hidden, device=dev, dtype=dt)
         self.layers: List[LlamaLayerWeights] = []
         for li in range(cfg.n_layers):
@@ -131,18 +136,27 @@ class LlamaModel:
             del q, k, v, o, g, u, dn
         gen.manual_seed(seed * 1000003 + 3)
         if cfg.tie_embeddings:
-            lm = self.embed
+            lm = embed
         else:
             lm = _randn(gen, (cfg.vocab_size, cfg.hidden), std, dev, dt)
         self.lm_head = ops.fold_norm(lm[self.v_start : self.v_end], ones).contiguous()
+        del embed, lm
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
+
+    def _vocab_shard(self, embed: torch.Tensor) -> torch.Tensor:
+        """This rank's rows [v_start, v_end) of the token embedding (SURVEY.md §2.7 K14 / §2.8 C3:
+        rows outside the shard embed to zero, the all-reduce after the gather completes them)."""
+        if self.tp.size == 1:
+            return embed
+        return embed[self.v_start : self.v_end].contiguous()
 
     def _load(self, w: dict):
         """HF-layout state dict (safetensors names); sharded + fused on load."""
         cfg, dev, dt = self.cfg, self.device, self.dtype
         get = lambda n: w[n].to(device=dev, dtype=dt)  # noqa: E731
-        self.embed = get("model.embed_tokens.weight")
+        embed = get("model.embed_tokens.weight")
+        self.embed = self._vocab_shard(embed)
         self.layers = []
         for li in range(cfg.n_layers):
             p = f"model.layers.{li}."
@@ -151,7 +165,7 @@ class LlamaModel:
                 get(p + "self_attn.v_proj.weight"), get(p + "self_attn.o_proj.weight"),
                 get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight"), get(p + "mlp.down_proj.weight"),
                 get(p + "input_layernorm.weight"), get(p + "post_attention_layernorm.weight")))
-        lm = get("lm_head.weight") if "lm_head.weight" in w else self.embed
+        lm = get("lm_head.weight") if "lm_head.weight" in w else embed
         self.lm_head = ops.fold_norm(lm[self.v_start : self.v_end], get("model.norm.weight")).contiguous()
 
     def weight_bytes(self) -> int:
@@ -271,7 +285,9 @@ class LlamaModel:
         """
         cfg = self.cfg
         h = bufs.hidden[:M]
-        ops.embedding(bufs.tokens, self.embed, out=h, rows=M)
+        ops.embedding(bufs.tokens, self.embed, out=h, rows=M, vocab_start=self.v_start)
+        if self.tp.size > 1:
+            self.tp.all_reduce(h)  # vocab-parallel embedding: every row is non-zero on one rank only
         qbuf = bufs.q[:M] if M <= bufs.q.shape[0] else torch.empty((M, self.nq * self.hd), dtype=self.dtype,
                                                                       device=self.device)
         chain = prefill_seq is None and self._chain_ok(M)
@@ -338,11 +354,13 @@ class LlamaModel:
         return self.lm_logits(bufs, hs) if head else hs
 
     def lm_logits(self, bufs, hs: torch.Tensor, col_mask: Optional[torch.Tensor] = None,
-                  mask_rows: int = 1) -> torch.Tensor:
+                  mask_rows: int = 1, gather: bool = True) -> torch.Tensor:
         """Final RMSNorm (folded into the weights) + LM head of the hidden rows ``hs`` -> f32 logits
-        [rows, vocab], gathered under TP.  col_mask (the sampler's int32 token bitmask rows): only
-        the vocab tiles with an admissible token in one of the first ``mask_rows`` rows are
-        computed (ops.linear); the other logits are stale and must only be read through the mask."""
+        [rows, vocab] (``gather=False`` under TP: this rank's shard [rows, v_end - v_start], tokens
+        v_start.. -- what the vocab-parallel sampler takes; the decode loop never gathers logits).
+        col_mask (the sampler's int32 token bitmask rows): only the vocab tiles with an admissible
+        token in one of the first ``mask_rows`` rows are computed (ops.linear); the other logits
+        are stale and must only be read through the mask."""
         n = hs.shape[0]
         local = bufs.logits_local[:n] if n <= bufs.logits_local.shape[0] else None
         mk = {}
@@ -350,10 +368,9 @@ class LlamaModel:
             mk = dict(col_mask=col_mask, col_mask_off=self.v_start // 32, mask_rows=mask_rows)
         local = ops.linear(hs, self.lm_head, out=local, fuse_rms=True, eps=self.cfg.rms_eps, out_dtype=torch.float32,
                            **mk)
-        if self.tp.size == 1:
+        if self.tp.size == 1 or not gather:
             return local
-        return self.tp.all_gather_vocab(local, self.cfg.vocab_size,
-                                        out=bufs.logits[:n] if n <= bufs.logits.shape[0] else None)
+        return self.tp.all_gather_vocab(local, self.cfg.vocab_size)
 
 
 def move_model(model, device) -> None:

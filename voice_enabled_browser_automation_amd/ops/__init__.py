@@ -187,37 +187,45 @@ def untile_weight(t: torch.Tensor) -> torch.Tensor:
 
 
 class TiledWeight:
-    """A bf16 projection weight kept in two layouts: ``w`` row-major [N, K] (hipBLASLt prefill,
-    the one-tile kernel, the CPU reference) and ``t`` = tile_weight(w) for the decode streaming /
-    chained kernels, which read it with fully contiguous 1 KB load instructions.  The second
-    copy is the price of that (15 GB for Llama-3-8B, sized for 288 GB of HBM per GPU)."""
+    """A bf16 projection weight stored ONLY in the pre-tiled layout ``t`` = tile_weight(w) (same
+    [N, K] shape, MFMA B-fragment element order).  Every GPU consumer reads it directly: the decode
+    streaming / chained kernels (1 KB contiguous load instructions) and the LDS-tiled GEMM for
+    prefill and > 16-row steps (gemm.hip copies the 4 KB fragment blocks to LDS verbatim) -- so
+    the model keeps one copy of each weight.  ``dense()`` rebuilds the row-major matrix for the
+    CPU reference and diagnostics."""
 
-    __slots__ = ("w", "t")
+    __slots__ = ("t",)
 
-    def __init__(self, w: torch.Tensor, t: Optional[torch.Tensor] = None):
-        self.w = w
+    def __init__(self, w: Optional[torch.Tensor] = None, t: Optional[torch.Tensor] = None):
         self.t = tile_weight(w) if t is None else t
+
+    def dense(self) -> torch.Tensor:
+        return untile_weight(self.t)
+
+    @property
+    def w(self) -> torch.Tensor:  # row-major view for legacy callers (materialised on demand)
+        return self.dense()
 
     @property
     def shape(self):
-        return self.w.shape
+        return self.t.shape
 
     @property
     def device(self):
-        return self.w.device
+        return self.t.device
 
     @property
     def dtype(self):
-        return self.w.dtype
+        return self.t.dtype
 
     def numel(self) -> int:
-        return self.w.numel()
+        return self.t.numel()
 
     def element_size(self) -> int:
-        return self.w.element_size()
+        return self.t.element_size()
 
     def to(self, device) -> "TiledWeight":
-        return TiledWeight(self.w.to(device), self.t.to(device))
+        return TiledWeight(t=self.t.to(device))
 
 
 def _stream_ok(x: torch.Tensor, w) -> bool:
@@ -226,8 +234,8 @@ def _stream_ok(x: torch.Tensor, w) -> bool:
 
 
 def plain(w):
-    """The row-major tensor of a weight (TiledWeight -> .w; anything else unchanged)."""
-    return w.w if isinstance(w, TiledWeight) else w
+    """The row-major tensor of a weight (TiledWeight -> dense(); anything else unchanged)."""
+    return w.dense() if isinstance(w, TiledWeight) else w
 
 
 # ----------------------------------------------------------------------------- layout helpers
@@ -315,6 +323,51 @@ def rope_table(max_pos: int, head_dim: int, theta: float, device=None, scaling: 
     return tab.to(device) if device is not None else tab
 
 
+# ----------------------------------------------------------------------------- scratch
+_SCRATCH: dict = {}
+
+
+def scratch(device, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
+    """A per-device reusable buffer of at least ``numel`` elements (stream-ordered users only;
+    created on the first -- eager -- call, so graph captures after a warm-up reuse it)."""
+    key = (str(device), name, dtype)
+    t = _SCRATCH.get(key)
+    if t is None or t.numel() < numel:
+        t = torch.empty(max(numel, 1), dtype=dtype, device=device)
+        _SCRATCH[key] = t
+    return t[:numel]
+
+
+GEMM_WS_FLOATS = 8 << 20  # split-K workspace (32 MB per device)
+_GEMM_EPI = {"none": 0, "resid": 1, "swiglu": 2, "gelu": 3}
+
+
+def gemm(x: torch.Tensor, w, out: torch.Tensor, *, epi: str = "none", bias: Optional[torch.Tensor] = None,
+         residual: Optional[torch.Tensor] = None, fuse_rms: bool = False, eps: float = 1e-5) -> torch.Tensor:
+    """The hand-written LDS-tiled MFMA GEMM (csrc/kernels/gemm.hip) for M > 16 rows:
+    out = epi(rms(x) @ w^T + bias); w a TiledWeight (its single pre-tiled copy) or a row-major bf16
+    [N, K] tensor.  fuse_rms: the per-row 1/rms of x scales the product (gamma folded into w)."""
+    E = ext()
+    rstd = None
+    if fuse_rms:
+        rstd = scratch(x.device, "gemm_rstd", x.shape[0])
+        E.row_rstd(x, rstd, eps)
+    tiled = isinstance(w, TiledWeight)
+    wt = w.t if tiled else w
+    ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
+    E.gemm(x, wt, bias, out, _GEMM_EPI[epi], rstd, residual, tiled, ws)
+    return out
+
+
+def gemm_ok(x: torch.Tensor, w) -> bool:
+    """Shapes the tiled GEMM takes (bf16 weights, N % 16, K % 128, 16-byte aligned rows)."""
+    if isinstance(w, FP8Weight) or not _gpu(x) or x.dtype != torch.bfloat16:
+        return False
+    wt = w.t if isinstance(w, TiledWeight) else w
+    return (wt.dtype == torch.bfloat16 and wt.shape[0] % 16 == 0 and wt.shape[1] % 128 == 0 and x.stride(1) == 1
+            and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0)
+
+
 # ----------------------------------------------------------------------------- GEMM family
 # Rows handled by the MFMA skinny kernels.  Above 16 rows (continuous batching of many sessions)
 # hipBLASLt's GEMM + the HIP epilogue kernels win on every decode shape (tools/bench_kernels.py:
@@ -345,7 +398,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if out is None:
         out = torch.empty((M, w.shape[0]), dtype=dt, device=x.device)
     if isinstance(w, TiledWeight):
-        if _gpu(x) and _stream_ok(x, w) and (ln_c is None or _ln_fold_fits(x, w.w)):
+        if _gpu(x) and _stream_ok(x, w) and (ln_c is None or _ln_fold_fits(x, w)):
             epi = {"none": 0, "gelu": 3}[act]
             if residual is not None:
                 assert act == "none"
@@ -353,7 +406,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
             ext().skinny_gemm(x, w.t, bias, out, epi, fuse_rms and ln_c is None, eps, residual, None, ln_c, True,
                               **mk)
             return out
-        w = w.w
+        if ln_c is not None:
+            return linear(_layernorm_plain(x, eps), w, bias, out=out, residual=residual, act=act, out_dtype=out_dtype)
+        if _gpu(x) and gemm_ok(x, w) and (act == "none" or residual is None) and \
+                (out.dtype == torch.bfloat16 or (residual is None and act == "none")):
+            e = "resid" if residual is not None else ("gelu" if act == "gelu" else "none")
+            return gemm(x, w, out, epi=e, bias=bias, residual=residual, fuse_rms=fuse_rms, eps=eps)
+        w = w.dense()
     if ln_c is not None:
         if _ln_fold_fits(x, w):
             epi = {"none": 0, "gelu": 3}[act] if residual is None else 1
@@ -376,6 +435,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         else:
             E.skinny_gemm(x, w, bias, out, epi, fuse_rms, eps, residual, **mk)
         return out
+    if not fp8 and gemm_ok(x, w) and (act == "none" or residual is None) and \
+            (out.dtype == torch.bfloat16 or (residual is None and act == "none")):
+        e = "resid" if residual is not None else ("gelu" if act == "gelu" else "none")
+        return gemm(x, w, out, epi=e, bias=bias, residual=residual, fuse_rms=fuse_rms, eps=eps)
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
     y = _fp8_matmul(xin, w) if fp8 else torch.matmul(xin, w.t())
     if bias is not None or act != "none" or residual is not None:
@@ -403,7 +466,9 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
         if _gpu(x) and _stream_ok(x, w_gu):
             ext().skinny_gemm_swiglu(x, w_gu.t, None, out, fuse_rms, eps, None, True)
             return out
-        w_gu = w_gu.w
+        if _gpu(x) and gemm_ok(x, w_gu):
+            return gemm(x, w_gu, out, epi="swiglu", fuse_rms=fuse_rms, eps=eps)
+        w_gu = w_gu.dense()
     if not _gpu(x):
         xr, wr, fr = _ref_w8(x, w_gu, fuse_rms, eps)
         return ref.linear_swiglu(xr, wr, fuse_rms=fr, eps=eps, out=out)
@@ -415,6 +480,8 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
         else:
             E.skinny_gemm_swiglu(x, w_gu, None, out, fuse_rms, eps)
         return out
+    if not fp8 and gemm_ok(x, w_gu):
+        return gemm(x, w_gu, out, epi="swiglu", fuse_rms=fuse_rms, eps=eps)
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
     gu = _fp8_matmul(xin, w_gu) if fp8 else torch.matmul(xin, w_gu.t())
     E.swiglu(gu, out)
@@ -429,11 +496,19 @@ def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Te
     ln_c: folded LayerNorm on x (see linear)."""
     M = x.shape[0]
     if isinstance(w_qkv, TiledWeight):
-        if _gpu(x) and _stream_ok(x, w_qkv) and (ln_c is None or _ln_fold_fits(x, w_qkv.w)):
+        if _gpu(x) and _stream_ok(x, w_qkv) and (ln_c is None or _ln_fold_fits(x, w_qkv)):
             ext().skinny_gemm_qkv(x, w_qkv.t, bias, fuse_rms and ln_c is None, eps, n_q_heads, n_kv_heads, head_dim,
                                   rope is not None, positions, slots, rope, q_out, k_cache, v_cache, None, ln_c, True)
             return q_out[:M]
-        w_qkv = w_qkv.w
+        if ln_c is not None:
+            x, ln_c = _layernorm_plain(x, eps), None
+        if _gpu(x) and gemm_ok(x, w_qkv):
+            qkv = scratch(x.device, "qkv", M * w_qkv.shape[0], torch.bfloat16).view(M, w_qkv.shape[0])
+            gemm(x, w_qkv, qkv, bias=bias, fuse_rms=fuse_rms, eps=eps)
+            ext().rope_kv_write(qkv, n_q_heads, n_kv_heads, head_dim, rope is not None, positions, slots, rope, q_out,
+                                k_cache, v_cache)
+            return q_out[:M]
+        w_qkv = w_qkv.dense()
     if ln_c is not None:
         if _ln_fold_fits(x, w_qkv):
             ext().skinny_gemm_qkv(x, w_qkv, bias, False, eps, n_q_heads, n_kv_heads, head_dim, rope is not None,
@@ -449,6 +524,12 @@ def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Te
     E = ext()
     use_rope = rope is not None
     fp8 = isinstance(w_qkv, FP8Weight)
+    if M > SKINNY_MAX_M and not fp8 and gemm_ok(x, w_qkv):
+        qkv = scratch(x.device, "qkv", M * w_qkv.shape[0], torch.bfloat16).view(M, w_qkv.shape[0])
+        gemm(x, w_qkv, qkv, bias=bias, fuse_rms=fuse_rms, eps=eps)
+        E.rope_kv_write(qkv, n_q_heads, n_kv_heads, head_dim, use_rope, positions, slots, rope, q_out, k_cache,
+                        v_cache)
+        return q_out[:M]
     if M <= SKINNY_MAX_M and (not fp8 or _fp8_stream_fits(M, x.shape[1])):
         if fp8:
             E.skinny_gemm_qkv(x, w_qkv.w8, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, use_rope, positions,
@@ -609,20 +690,62 @@ def flash_attention(q: torch.Tensor, kv: KVLayout, *, Sk: int, n_kv_heads: int, 
 def sample(logits: torch.Tensor, *, mask: Optional[torch.Tensor], temperature: Optional[torch.Tensor],
            seed: torch.Tensor, step: torch.Tensor, out_tokens: torch.Tensor,
            part_val: Optional[torch.Tensor] = None, part_idx: Optional[torch.Tensor] = None,
-           n_chunks: int = 64, fail_word: Optional[torch.Tensor] = None) -> torch.Tensor:
+           n_chunks: int = 64, fail_word: Optional[torch.Tensor] = None, v_offset: int = 0, tp=None) -> torch.Tensor:
     """Masked Gumbel-max sampling (greedy without temperature).  ``fail_word``: a device int64
     that, when nonzero at sampling time, turns every output token into -2 (the chained
-    forward's grid-barrier timeout word: the logits of that step are invalid)."""
+    forward's grid-barrier timeout word: the logits of that step are invalid).
+
+    Vocab parallel (``tp`` a TPContext of size > 1): ``logits`` is this rank's shard, column j =
+    token ``v_offset + j``; every rank gets the same tokens, equal to what a TP=1 sampler draws
+    from the full logits (noise and tie-break use global ids).  On GPU TP groups: partial maxima
+    -> one-shot IPC all-gather of [rows, chunks] (value, id) pairs -> merge (sample_tp, no host
+    sync, no RCCL); elsewhere the partial maxima are all-gathered with torch.distributed."""
     rows = logits.shape[0]
+    if tp is not None and getattr(tp, "size", 1) > 1:
+        return _sample_tp(logits, mask=mask, temperature=temperature, seed=seed, step=step, out_tokens=out_tokens,
+                          fail_word=fail_word, v_offset=v_offset, tp=tp)
     if not _gpu(logits):
-        out = ref.sample(logits, mask=mask, temperature=temperature, seed=seed, step=step, out_tokens=out_tokens)
+        out = ref.sample(logits, mask=mask, temperature=temperature, seed=seed, step=step, out_tokens=out_tokens,
+                         v_offset=v_offset)
         if fail_word is not None and int(fail_word.reshape(-1)[0]) != 0:
             out[:rows] = -2
         return out
     if part_val is None:
         part_val = torch.empty((rows * n_chunks,), dtype=torch.float32, device=logits.device)
         part_idx = torch.empty((rows * n_chunks,), dtype=torch.int32, device=logits.device)
-    ext().sample(logits, mask, temperature, seed, step, out_tokens, part_val, part_idx, fail_word)
+    ext().sample(logits, mask, temperature, seed, step, out_tokens, part_val, part_idx, fail_word, v_offset)
+    return out_tokens
+
+
+def tp_sample_chunks(tp_size: int) -> int:
+    """Partial-maximum chunks per row and rank under vocab parallelism (64 over the whole vocab)."""
+    return max(8, 64 // max(1, tp_size))
+
+
+def _sample_tp(logits, *, mask, temperature, seed, step, out_tokens, fail_word, v_offset, tp):
+    import torch.distributed as dist
+
+    rows = logits.shape[0]
+    car = getattr(tp, "custom_ar", None)
+    if _gpu(logits) and car is not None:
+        C = tp_sample_chunks(tp.size)
+        xin, xout = car.sample_buffers(rows * C * 2, logits.device)
+        ext().sample_tp(logits, mask, temperature, seed, step, out_tokens, xin, xout, C, fail_word, v_offset,
+                        car.state, tp.size)
+        return out_tokens
+    vals, idx = ref.sample_partial(logits, mask=mask, temperature=temperature, seed=seed, step=step,
+                                   v_offset=v_offset)
+    dev = logits.device if (_gpu(logits) and dist.get_backend(tp.group) == "nccl") else torch.device("cpu")
+    mine = torch.stack([vals.double(), idx.double()]).to(dev)
+    parts = [torch.empty_like(mine) for _ in range(tp.size)]
+    dist.all_gather(parts, mine, group=tp.group)
+    allv = torch.stack([p[0].cpu() for p in parts])
+    alli = torch.stack([p[1].cpu().long() for p in parts])
+    toks = ref.merge_partials(allv, alli)
+    if fail_word is not None and int(fail_word.reshape(-1)[0]) != 0:
+        toks[:] = -2
+    out_tokens[:rows] = toks.to(out_tokens.dtype).to(out_tokens.device)
+    step.add_(1)
     return out_tokens
 
 

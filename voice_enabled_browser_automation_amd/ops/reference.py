@@ -182,12 +182,13 @@ def _splitmix64(x: int) -> int:
     return x ^ (x >> 31)
 
 
-def gumbel_keys(logits_row: torch.Tensor, T: float, seed: int, step: int, row: int) -> torch.Tensor:
-    """Exact replica of the kernel's counter-based Gumbel noise (vectorised)."""
+def gumbel_keys(logits_row: torch.Tensor, T: float, seed: int, step: int, row: int, v_offset: int = 0) -> torch.Tensor:
+    """Exact replica of the kernel's counter-based Gumbel noise (vectorised); column j is global
+    token id v_offset + j (a vocab shard under tensor parallelism)."""
     m = (1 << 64) - 1
     base = _splitmix64((seed & m) ^ _splitmix64((step * 0x100000001B3 + row) & m))
     V = logits_row.shape[0]
-    v = torch.arange(V, dtype=torch.int64)
+    v = torch.arange(v_offset, v_offset + V, dtype=torch.int64)
     # vectorised splitmix64 on uint64 emulated with python ints is slow; use numpy uint64
     import numpy as np
 
@@ -202,21 +203,47 @@ def gumbel_keys(logits_row: torch.Tensor, T: float, seed: int, step: int, row: i
     return logits_row.float() / T + torch.from_numpy(g.astype(np.float32))
 
 
-def sample(logits, *, mask, temperature, seed, step, out_tokens):
+def sample_partial(logits, *, mask, temperature, seed, step, v_offset=0):
+    """Per-row best (key, global token id) over a logits shard whose column j is token
+    v_offset + j: the kernel's partial stage (no step advance).  (-inf, -1) for an empty row."""
     rows, V = logits.shape
     sd = int(seed.reshape(-1)[0]) & ((1 << 64) - 1)
     st = int(step.reshape(-1)[0])
+    vals = torch.full((rows,), float("-inf"), dtype=torch.float32)
+    idx = torch.full((rows,), -1, dtype=torch.int64)
+    lg = logits.detach().float().cpu()
     for r in range(rows):
         T = float(temperature[r]) if temperature is not None else 0.0
-        key = gumbel_keys(logits[r], T, sd, st, r) if T > 0 else logits[r].float().clone()
+        key = gumbel_keys(lg[r], T, sd, st, r, v_offset) if T > 0 else lg[r].clone()
         if mask is not None:
-            words = mask[r].to(torch.int64) & 0xFFFFFFFF
-            bits = ((words[:, None] >> torch.arange(32)[None, :]) & 1).reshape(-1)[:V].bool()
+            words = mask[r].detach().cpu().to(torch.int64) & 0xFFFFFFFF
+            bits = ((words[:, None] >> torch.arange(32)[None, :]) & 1).reshape(-1)[v_offset : v_offset + V].bool()
             key = key.masked_fill(~bits, float("-inf"))
-        if torch.isinf(key).all() and key.max() < 0:
-            out_tokens[r] = -1
-        else:
-            out_tokens[r] = int(torch.argmax(key))
+        if not (torch.isinf(key).all() and key.max() < 0):
+            j = int(torch.argmax(key))  # first maximum: the lowest id wins ties, as in the kernel
+            vals[r], idx[r] = key[j], v_offset + j
+    return vals, idx
+
+
+def merge_partials(vals: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """[n_src, rows] partial maxima -> token per row (largest key, lowest id on ties; -1 if none)."""
+    n_src, rows = vals.shape
+    out = torch.full((rows,), -1, dtype=torch.int64)
+    for r in range(rows):
+        best_v, best_i = float("-inf"), -1
+        for p in range(n_src):
+            v, i = float(vals[p, r]), int(idx[p, r])
+            if i < 0:
+                continue
+            if best_i < 0 or v > best_v or (v == best_v and i < best_i):
+                best_v, best_i = v, i
+        out[r] = best_i
+    return out
+
+
+def sample(logits, *, mask, temperature, seed, step, out_tokens, v_offset=0):
+    vals, idx = sample_partial(logits, mask=mask, temperature=temperature, seed=seed, step=step, v_offset=v_offset)
+    out_tokens[: logits.shape[0]] = idx.to(out_tokens.dtype).to(out_tokens.device)
     step.add_(1)
     return out_tokens
 

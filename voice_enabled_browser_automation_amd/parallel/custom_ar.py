@@ -34,6 +34,23 @@ class OneShotAllReduce:
                 E.ar_open_peer(self.state, p, torch.frombuffer(bytearray(hb), dtype=torch.uint8))
         dist.barrier(group=ctl_group)
 
+    def sample_buffers(self, words: int, device):
+        """(xin [>= words], xout [>= world * words]) int32 exchange buffers of the vocab-parallel
+        sampler (ops.sample_tp), grown on demand and reused (the calls are stream-ordered)."""
+        have = getattr(self, "_sbuf", None)
+        if have is None or have[0].numel() < words:
+            n = max(words, 4096)
+            self._sbuf = (torch.zeros(n, dtype=torch.int32, device=device),
+                          torch.zeros(self.world * n, dtype=torch.int32, device=device))
+        return self._sbuf
+
+    def gather(self, t: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One-shot all-gather of an int32 [n] tensor -> [world, n] (every rank, rank order)."""
+        if out is None:
+            out = torch.empty((self.world, t.numel()), dtype=torch.int32, device=t.device)
+        ops.ext().ar_gather(self.state, t.contiguous(), out)
+        return out
+
     def fits(self, t: torch.Tensor) -> bool:
         return t.dtype == torch.bfloat16 and t.is_contiguous() and t.numel() <= self.max_elems and t.numel() % 8 == 0
 

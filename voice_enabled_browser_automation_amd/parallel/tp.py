@@ -6,7 +6,9 @@ over gloo.  The LLM needs exactly these collectives:
 * C1/C2  all-reduce of the row-parallel o_proj / down_proj outputs (decode: d*2 bytes per row,
          i.e. 8 KiB for Llama-3-8B -- latency bound; the residual is folded into rank 0's
          GEMM epilogue so the all-reduce result IS the new residual stream);
-* C4     all-gather of the vocab-parallel logits shards (f32);
+* C3     all-reduce of the vocab-parallel embedding rows (one per step);
+* C4     vocab-parallel sampling: each rank's partial (value, id) maxima are exchanged ([B, 2]
+         per chunk, ops.sample / csrc sample_tp over the one-shot IPC all-gather), never logits;
 * C5     broadcast (weights are generated deterministically on every rank, so only the
          random seed needs to agree -- no weight traffic at init);
 * C6     all-gather of per-rank metrics (DP router).
@@ -47,22 +49,17 @@ class TPContext:
                 dist.all_reduce(t, group=self.group)
         return t
 
-    def all_gather_vocab(self, local: torch.Tensor, vocab: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """[n, V/T] shards -> [n, V] (last shard may be short: shards are padded to V/T)."""
+    def all_gather_vocab(self, local: torch.Tensor, vocab: int) -> torch.Tensor:
+        """[n, V_shard] logits shards -> [n, V] (diagnostics / prefill checks only: the decode loop
+        samples vocab-parallel and never gathers logits).  Shards are padded to the common
+        32-aligned shard width for the collective."""
         n, vp = local.shape
-        per = (vocab + self.size - 1) // self.size
-        if vp != per:
-            pad = torch.zeros((n, per), dtype=local.dtype, device=local.device)
-            pad[:, :vp] = local
-            pad[:, vp:] = float("-inf")
-            local = pad
-        parts = [torch.empty((n, per), dtype=local.dtype, device=local.device) for _ in range(self.size)]
-        dist.all_gather(parts, local.contiguous(), group=self.group)
-        full = torch.cat(parts, dim=1)[:, :vocab]
-        if out is not None:
-            out.copy_(full)
-            return out
-        return full.contiguous()
+        per = ((vocab + self.size - 1) // self.size + 31) // 32 * 32
+        pad = torch.full((n, per), float("-inf"), dtype=local.dtype, device=local.device)
+        pad[:, :vp] = local
+        parts = [torch.empty_like(pad) for _ in range(self.size)]
+        dist.all_gather(parts, pad, group=self.group)
+        return torch.cat(parts, dim=1)[:, :vocab].contiguous()
 
     def barrier(self):
         if self.size > 1:

@@ -75,8 +75,7 @@ class StepBuffers:
         self.attn = torch.zeros_like(self.q)
         self.act = torch.zeros(max_rows, model.F, dtype=dt, device=device)
         self.logits_local = torch.zeros(max_rows, model.v_end - model.v_start, dtype=torch.float32, device=device)
-        self.logits = torch.zeros(max_rows, model.cfg.vocab_size, dtype=torch.float32, device=device) \
-            if model.tp.size > 1 else self.logits_local
+        self.logits = self.logits_local  # (vocab-parallel: the decode loop never gathers full logits)
         ns = ops.decode_n_splits(max_ctx)
         self.part_o = torch.zeros(max_rows * ns * model.nq * model.hd, dtype=torch.float32, device=device)
         self.part_ml = torch.zeros(max_rows * ns * model.nq * 2, dtype=torch.float32, device=device)
@@ -337,14 +336,27 @@ class LLMEngine:
         the next run_rows may rewrite the pinned staging rows without a synchronize."""
         self._staging_inflight = False
 
-    def head_logits(self, col_mask: Optional[torch.Tensor] = None, mask_rows: int = 1) -> torch.Tensor:
+    def head_logits(self, col_mask: Optional[torch.Tensor] = None, mask_rows: int = 1,
+                    gather: bool = True) -> torch.Tensor:
         """LM head of the last ``run_rows`` step's selected rows -> f32 logits [rows, V].
         col_mask: the sampler's int32 token bitmask rows (row i <-> logits row i); vocab tiles with
         no admissible token in the first ``mask_rows`` rows are skipped and their logits are stale
-        (read them only through the same mask)."""
+        (read them only through the same mask).  gather=False under TP: this rank's vocab shard
+        (feed it to ``sample``)."""
         hs = self._head_rows
         assert hs is not None, "head_logits() needs a run_rows() step first"
-        return self.model.lm_logits(self.bufs, hs, col_mask=col_mask, mask_rows=mask_rows)
+        if gather:
+            return self.model.lm_logits(self.bufs, hs, col_mask=col_mask, mask_rows=mask_rows)
+        return self.model.lm_logits(self.bufs, hs, col_mask=col_mask, mask_rows=mask_rows, gather=False)
+
+    def sample(self, logits: torch.Tensor, **kw) -> torch.Tensor:
+        """ops.sample over ``head_logits(gather=False)`` output: vocab-parallel under TP (the
+        shard's global offset and the TP group come from the model)."""
+        m = self.model
+        tp = getattr(m, "tp", None)
+        if tp is not None and tp.size > 1:
+            kw.update(v_offset=m.v_start, tp=tp)
+        return ops.sample(logits, **kw)
 
     def _uses_chain(self, M: int) -> bool:
         ok = getattr(self.model, "_chain_ok", None)
