@@ -219,12 +219,18 @@ void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi,
   p.Y = y.data_ptr();
   p.ldy = (int)y.stride(0);
   p.y_f32 = y.scalar_type() == at::kFloat;
+  // (bf16 rows leave the kernel as 16-byte chunks)
+  TORCH_CHECK(y.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(y.data_ptr()) & 15) == 0,
+              "gemm: y rows must be 16-byte aligned");
   if (bias.has_value()) {
     check_bf16(*bias, "bias");
     TORCH_CHECK(bias->numel() == p.N && bias->is_contiguous(), "bias [N]");
     p.bias = bfp(*bias);
   }
   if (epi == 1) {
+    TORCH_CHECK(residual.has_value() && residual->stride(0) % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(residual->data_ptr()) & 15) == 0,
+                "gemm: residual rows must be 16-byte aligned");
     TORCH_CHECK(residual.has_value(), "residual epilogue needs residual");
     check_bf16(*residual, "residual");
     TORCH_CHECK(residual->dim() == 2 && residual->size(0) == p.M && residual->size(1) == p.N &&

@@ -41,77 +41,72 @@ enum Epi { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_GELU = 3 };
 
 constexpr int BM = 128, BN = 128, BKG = 128;
 constexpr int kThreads = 256;
-constexpr int kABytes = BM * BKG * 2;  // 32 KB
-constexpr int kBBytes = BN * BKG * 2;  // 32 KB
+constexpr int kStageBytes = 32768;  // one half k-group (64 deep): A 16 KB + B 16 KB
+constexpr int kLds = 2 * kStageBytes;
 
-struct Stage {
-  uint4 a[8];
-  uint4 b[8];
-};
+// buffer resource over [base, base + bytes): loads past the end return zero (rows >= M, weight
+// tiles >= N), so the stage issue needs no bounds branches
+VWA_DEVICE __amdgpu_buffer_rsrc_t rsrc(const void* base, size_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(bytes < 0x7FFFFFF0ull ? bytes : 0x7FFFFFF0ull), 0x00020000);
+}
 
-// global -> registers for k-group kg
+VWA_DEVICE void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff, 0, 0,
+                                           0);
+}
+
+// Half-stage hs = 2 kg + h (k = 128 kg + 32 g + 16 h + 8 s' + e, s' = 0, 1) of the block's
+// tile, LDS-DMA'd straight into buffer `buf` (no registers): 8 wave-instructions of 1 KB per
+// thread-wave.  Each wave-instruction's LDS destination is lane-linear (base + 16 lane), so the
+// A swizzle is applied on the per-lane SOURCE address (and undone on the read):
+//   A image [128 rows][8 chunks of 16 B], chunk c = 2 g + s' at slot c ^ ((row >> 1) & 7)
+//     -> 16 rows reading one chunk touch 16 distinct (row parity, slot) bank groups
+//   B image [8 tiles][2 s'][64 lanes][16 B]: the tiled weight's fragment blocks verbatim (a
+//     row-major weight gathers each lane's fragment from its row instead)
 template <bool WT>
-VWA_DEVICE void load_stage(const GemmParams& p, int bm, int bn, int kg, Stage& st) {
-  const int t = threadIdx.x;
-  const int c = t & 15;
+VWA_DEVICE void issue_stage(const GemmParams& p, __amdgpu_buffer_rsrc_t rx, __amdgpu_buffer_rsrc_t rw, int bm,
+                            int bn, int hs, char* buf) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int kg = hs >> 1, h = hs & 1;
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int r = it * 16 + (t >> 4);
+  for (int it = 0; it < 4; ++it) {
+    const int q = it * 4 + w;  // wave-instruction index: rows 8q .. 8q + 7
+    const int r = 8 * q + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
     const int m = bm + r;
-    st.a[it] = make_uint4(0u, 0u, 0u, 0u);
-    if (m < p.M) st.a[it] = *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + (size_t)kg * BKG + c * 8);
+    const unsigned off = (unsigned)(((size_t)m * p.ldx + (size_t)kg * BKG + 32 * (c >> 1) + 16 * h + 8 * (c & 1)) * 2);
+    dma16(rx, buf + q * 1024, m < p.M ? off : 0xFFFFFFF0u);
   }
   const int kgn = p.K / BKG;
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
+  for (int it = 0; it < 4; ++it) {
+    const int q = it * 4 + w;  // tile q >> 1, sub-step s' = q & 1
+    const int tile = q >> 1, sp = q & 1;
+    unsigned off;
     if constexpr (WT) {
-      const int T = (bn >> 4) + it;
-      st.b[it] = make_uint4(0u, 0u, 0u, 0u);
-      if (T * 16 < p.N) st.b[it] = *reinterpret_cast<const uint4*>(p.W + ((size_t)T * kgn + kg) * 2048 + t * 8);
+      const int T = (bn >> 4) + tile;
+      off = T * 16 < p.N ? (unsigned)((((size_t)T * kgn + kg) * 2048 + (2 * h + sp) * 512 + lane * 8) * 2) : 0xFFFFFFF0u;
     } else {
-      const int n = bn + it * 16 + (t >> 4);
-      st.b[it] = make_uint4(0u, 0u, 0u, 0u);
-      if (n < p.N) st.b[it] = *reinterpret_cast<const uint4*>(p.W + (size_t)n * p.K + (size_t)kg * BKG + c * 8);
+      const int n = bn + tile * 16 + (lane & 15), g = lane >> 4;
+      off = n < p.N ? (unsigned)(((size_t)n * p.K + (size_t)kg * BKG + 32 * g + 16 * h + 8 * sp) * 2) : 0xFFFFFFF0u;
     }
+    dma16(rw, buf + 16384 + q * 1024, off);
   }
 }
 
-// registers -> LDS (A swizzled, B in fragment order)
-template <bool WT>
-VWA_DEVICE void store_stage(char* lds, const Stage& st) {
-  const int t = threadIdx.x;
-  const int c = t & 15;
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int r = it * 16 + (t >> 4);
-    *reinterpret_cast<uint4*>(lds + r * 256 + ((c ^ (r & 15)) << 4)) = st.a[it];
-  }
-  char* lb = lds + kABytes;
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    if constexpr (WT) {
-      *reinterpret_cast<uint4*>(lb + it * 4096 + t * 16) = st.b[it];
-    } else {
-      // row n_local = it*16 + (t>>4) of the 128-row tile, k chunk c = 4 g + s
-      const int nn = t >> 4, g = c >> 2, s = c & 3;
-      *reinterpret_cast<uint4*>(lb + (it * 4 + s) * 1024 + (16 * g + nn) * 16) = st.b[it];
-    }
-  }
-}
-
-VWA_DEVICE void compute_stage(const char* lds, f32x4 (&acc)[4][4], int wm, int wn) {
+VWA_DEVICE void compute_stage(const char* buf, f32x4 (&acc)[4][4], int wm, int wn) {
   const int l = lane_id();
   const int rl = l & 15, g = l >> 4;
-  const char* la = lds + (wm * 64 + rl) * 256;
-  const char* lb = lds + kABytes + (wn * 4) * 4096 + l * 16;
+  const char* la = buf + (wm * 64 + rl) * 128;
+  const char* lb = buf + 16384 + (wn * 4) * 2048 + l * 16;
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
+  for (int sp = 0; sp < 2; ++sp) {
     bf16x8 a[4], b[4];
-    const int ch = ((4 * g + s) ^ rl) << 4;  // row & 15 == rl for every fragment row
+    const int ch = ((2 * g + sp) ^ (rl >> 1)) << 4;  // ((row >> 1) & 7) == rl >> 1 for every fragment row
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(la + i * 16 * 256 + ch);
+    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(la + i * 16 * 128 + ch);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(lb + j * 4096 + s * 1024);
+    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(lb + j * 2048 + sp * 1024);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -148,21 +143,21 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  Stage st;
-  if (kg0 < kg1) {
-    load_stage<WT>(p, bm, bn, kg0, st);
-    store_stage<WT>(lds, st);
-    __syncthreads();
-    for (int kg = kg0; kg < kg1; ++kg) {
-      const bool more = kg + 1 < kg1;
-      if (more) load_stage<WT>(p, bm, bn, kg + 1, st);  // in flight during the MFMAs
-      compute_stage(lds, acc, wm, wn);
-      __syncthreads();
-      if (more) {
-        store_stage<WT>(lds, st);
-        __syncthreads();
-      }
-    }
+  // pipeline: two LDS buffers, the next half-stage's DMA in flight during this one's MFMAs;
+  // raw barriers with counted vmcnt (a __syncthreads would drain the in-flight DMA)
+  const int h0 = 2 * kg0, nh = 2 * (kg1 - kg0);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(p.X, (size_t)p.M * p.ldx * 2);
+  const __amdgpu_buffer_rsrc_t rw = rsrc(p.W, (size_t)p.N * p.K * 2);
+  if (nh > 0) issue_stage<WT>(p, rx, rw, bm, bn, h0, lds);
+  if (nh > 1) issue_stage<WT>(p, rx, rw, bm, bn, h0 + 1, lds + kStageBytes);
+  for (int i = 0; i < nh; ++i) {
+    if (i + 1 < nh)
+      asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");  // this half-stage landed everywhere
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    compute_stage(lds + (i & 1) * kStageBytes, acc, wm, wn);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done reading it
+    if (i + 2 < nh) issue_stage<WT>(p, rx, rw, bm, bn, h0 + i + 2, lds + (i & 1) * kStageBytes);
   }
   const int l = lane_id();
   const int col0 = bn + wn * 64 + (l & 15);
@@ -183,33 +178,85 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
       }
     return;
   }
+  // per-lane epilogue operands loaded once (no load-or-constant select per element)
+  float bz[4] = {0.f, 0.f, 0.f, 0.f}, rsv[4][4];
+  if (p.bias) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bz[j] = col0 + j * 16 < p.N ? bf2f(p.bias[col0 + j * 16]) : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = row0 + i * 16 + r;
-      if (m >= p.M) continue;
-      const float rs = p.rstd ? p.rstd[m] : 1.f;
-      if constexpr (EPI == EPI_SWIGLU) {
+    for (int r = 0; r < 4; ++r) rsv[i][r] = 1.f;
+  if (p.rstd) {
 #pragma unroll
-        for (int j = 0; j < 4; j += 2) {
-          const int n = col0 + j * 16;  // gate column; its up partner is n + 16
-          if (n >= p.N) continue;
-          const int f = ((n - (l & 15)) >> 5) * 16 + (l & 15);
-          const float gt = acc[i][j][r] * rs, up = acc[i][j + 1][r] * rs;
-          reinterpret_cast<u16*>(p.Y)[(size_t)m * p.ldy + f] = f2bf(silu(gt) * up);
-        }
-      } else {
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rsv[i][r] = row0 + i * 16 + r < p.M ? p.rstd[row0 + i * 16 + r] : 1.f;
+  }
+  if (p.y_f32) {  // f32 logits (rare: prefill LM head rows) -- direct stores
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = row0 + i * 16 + r;
+        if (m >= p.M) continue;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int n = col0 + j * 16;
           if (n >= p.N) continue;
-          float v = acc[i][j][r] * rs + bias_at(p, n);
+          float v = acc[i][j][r] * rsv[i][r] + bz[j];
           if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
-          store_out<EPI>(p, m, n, v);
+          reinterpret_cast<float*>(p.Y)[(size_t)m * p.ldy + n] = v;
+        }
+      }
+    return;
+  }
+  // bf16 out: the wave's tile goes through LDS (padded rows: the four row groups of a store hit
+  // different banks) and leaves as 16-byte row chunks -- coalesced stores, 16-byte residual reads
+  constexpr int NCOL = EPI == EPI_SWIGLU ? 32 : 64;  // output columns of this wave
+  constexpr int RS = EPI == EPI_SWIGLU ? 96 : 144;   // LDS row stride (bytes)
+  char* wl = lds + w * (64 * RS);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rl = i * 16 + 4 * (l >> 4) + r;
+      if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+        for (int j = 0; j < 4; j += 2) {
+          const float gt = acc[i][j][r] * rsv[i][r], up = acc[i][j + 1][r] * rsv[i][r];
+          *reinterpret_cast<u16*>(wl + rl * RS + ((j >> 1) * 16 + (l & 15)) * 2) = f2bf(silu(gt) * up);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float v = acc[i][j][r] * rsv[i][r] + bz[j];
+          if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
+          *reinterpret_cast<u16*>(wl + rl * RS + (j * 16 + (l & 15)) * 2) = f2bf(v);
         }
       }
     }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  constexpr int CPR = NCOL / 8;  // 16-byte chunks per row
+  const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
+  const int cbase = EPI == EPI_SWIGLU ? (bn + wn * 64) / 2 : bn + wn * 64;
+#pragma unroll
+  for (int it = 0; it < 64 * CPR / 64; ++it) {
+    const int idx = it * 64 + l, row = idx / CPR, ch = idx % CPR;
+    const int m = bm + wm * 64 + row, n = cbase + ch * 8;
+    if (m >= p.M || n >= ncols) continue;
+    uint4 v = *reinterpret_cast<const uint4*>(wl + row * RS + ch * 16);
+    if constexpr (EPI == EPI_RESID) {
+      float a[8], b[8];
+      unpack8(v, a);
+      unpack8(*reinterpret_cast<const uint4*>(p.R + (size_t)m * p.ldr + n), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += b[e];
+      v = pack8(a);
+    }
+    *reinterpret_cast<uint4*>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + n) = v;
+  }
 }
 
 // sum of the split-K slabs + epilogue; one thread per output element (SwiGLU: per feature)
@@ -259,7 +306,7 @@ template <int EPI>
 int launch_epi(const GemmParams& p, hipStream_t st) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const dim3 grid(tiles * p.splits);
-  const int lds = kABytes + kBBytes;
+  const int lds = kLds;
   if (p.w_tiled)
     hipLaunchKernelGGL((gemm_kernel<EPI, true>), grid, dim3(kThreads), lds, st, p);
   else

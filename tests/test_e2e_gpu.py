@@ -84,3 +84,67 @@ def test_voice_to_intent_to_execution_on_gpu(tmp_path):
 
     asyncio.run(go())
     torch.cuda.synchronize()
+
+
+def test_eight_concurrent_streaming_sessions_on_gpu():
+    """8 live WebSocket sessions streaming 60 ms PCM packets into the voice service: the ASR
+    batcher (asr/streaming.py) runs every session's recognition pass in shared GPU batches
+    (Whisper-tiny, hipGraph decode); reports speech_to_final_ms p50/p95 per session."""
+    import statistics
+    import time
+
+    from voice_enabled_browser_automation_amd.asr.streaming import AsrBatcher
+
+    ops.ext()
+    eng = AsrEngine(WhisperModel(get_config("whisper-tiny"), device="cuda", seed=0), load_tokenizer("whisper"),
+                    max_sessions=8)
+    batcher = AsrBatcher(eng, max_tokens=24)
+
+    def factory():
+        return StreamingAsrSession(batcher, model_name="whisper-tiny", partial_every_s=0.5, endpoint_silence_s=0.3)
+
+    factory.batcher = batcher
+    lat = {}
+
+    async def client(c, i):
+        ws = await c.ws_connect("/stream")
+        await ws.receive()
+        await ws.receive()
+        pcm = np.concatenate([_speech(1.5 + 0.1 * i), np.zeros(8000, np.int16)]).tobytes()
+        t0 = time.perf_counter()
+        done = asyncio.Event()
+
+        async def reader():
+            while True:
+                msg = await ws.receive()
+                if msg.type != 1:
+                    return
+                if json.loads(msg.data)["type"] == "transcript_final":
+                    lat[i] = (time.perf_counter() - t0) * 1e3
+                    done.set()
+                    return
+
+        rd = asyncio.ensure_future(reader())
+        for j in range(0, len(pcm), 1920):
+            await ws.send_bytes(pcm[j:j + 1920])
+            await asyncio.sleep(0.06)  # real-time pacing, as a microphone
+        await asyncio.wait_for(rd, 60)
+        await ws.close()
+
+    async def go():
+        async with TestClient(TestServer(build_voice(factory, debounce_ms=10))) as c:
+            await asyncio.gather(*(client(c, i) for i in range(8)))
+            return await (await c.get("/metrics")).json()
+
+    try:
+        m = asyncio.run(go())
+    finally:
+        batcher.close()
+    vals = sorted(lat.values())
+    assert len(vals) == 8
+    audio_ms = [(1.5 + 0.1 * i) * 1e3 + 500 for i in range(8)]
+    print(json.dumps({"sessions": 8, "speech_to_final_ms_p50": round(statistics.median(vals), 1),
+                      "speech_to_final_ms_p95": round(vals[-1], 1), "audio_ms_mean": round(sum(audio_ms) / 8, 1),
+                      "asr_rows_per_batch": round(batcher.rows_per_batch(), 2), "batches": batcher.stats["batches"],
+                      "max_batch": batcher.stats["max_batch"]}), flush=True)
+    assert m["asr_batcher"]["max_batch"] > 1 and batcher.rows_per_batch() > 1.0

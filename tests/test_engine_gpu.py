@@ -404,3 +404,48 @@ def test_chained_layer_tail_5_to_16_rows(monkeypatch):
     for a, b in zip(got, ref):
         err = (a - b).abs().max().item()
         assert err < 0.02 * (1 + b.abs().max().item()), err
+
+
+def test_intent_engine_recovers_from_a_failed_chained_step(monkeypatch):
+    """LLMIntentEngine.step's own recovery path: the forward's chained launch "times
+    out" (its error word set in stream order after the forward) -> the zero-copy sampler stores
+    -2 tokens -> recover_step re-runs the rows on the per-kernel path and the same iteration
+    samples again.  The answers equal an engine that never chained; one fallback is counted."""
+    from voice_enabled_browser_automation_amd.brain.intent_engine import LLMIntentEngine
+
+    ops.ext()
+    cfg = LlamaConfig(name="t8r", vocab_size=128256, hidden=1024, n_layers=2, n_heads=8, n_kv_heads=2,
+                      head_dim=128, ffn=2048, max_pos=4096)
+    model = LlamaModel(cfg, device="cuda", seed=6)
+    texts = ["search wireless earbuds", "scroll down"]
+
+    def answers(chain: bool, fail_at: int = -1):
+        monkeypatch.setenv("VWA_CHAIN", "1" if chain else "0")
+        model.enable_chain()
+        eng = LLMEngine(model, max_seqs=2, max_model_len=2048)
+        ie = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=160, temperature=0.1, seed=3)
+        assert ie.zero_copy and ie.spin_wait
+        calls = [0, False]
+        orig = eng.run_rows
+
+        def run_rows(*a, **k):
+            out = orig(*a, **k)
+            calls[0] += 1
+            # the first chained (<= 4-row) sampled step from the fail_at-th call on
+            if fail_at > 0 and calls[0] >= fail_at and not calls[1] and k.get("check") is False:
+                w = eng.step_fail_word()
+                if w is not None:
+                    w.fill_(1)  # what a timed-out barrier spin writes (stream-ordered after the forward)
+                    calls[1] = True
+            return out
+
+        eng.run_rows = run_rows
+        outs = [ie.generate([{"role": "user", "content": t}]) for t in texts]
+        assert fail_at < 0 or calls[1], "no chained step was failed"
+        return outs, eng
+
+    want, _ = answers(False)
+    got, eng = answers(True, fail_at=6)
+    assert got == want
+    assert eng.stats.get("chain_fallbacks") == 1
+    model.enable_chain()

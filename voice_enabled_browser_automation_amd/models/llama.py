@@ -68,7 +68,9 @@ class LlamaModel:
         self.v_end = min(V, self.v_start + self.v_per)
         self.rope = ops.rope_table(cfg.max_pos, cfg.head_dim, cfg.rope_theta, device=self.device)
         self.scale = cfg.head_dim ** -0.5
-        if weights is not None:
+        if self.device.type == "meta":
+            self._init_meta()  # shapes only (memory planning / sharding checks of configs too big to build)
+        elif weights is not None:
             self._load(weights)
         else:
             self._init_random(seed)
@@ -97,6 +99,14 @@ class LlamaModel:
         self.lm_head = q(self.lm_head)
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
+
+    def param_bytes(self) -> int:
+        """Resident bytes of every weight this rank holds (projections, LM head, embedding shard,
+        fp8 scales): one copy each."""
+        ts = [self.lm_head] + [t for L in self.layers for t in (L.qkv, L.o, L.gu, L.down)]
+        n = sum(t.numel() * t.element_size() for t in ts) + self.embed.numel() * self.embed.element_size()
+        n += sum(t.scale.numel() * 4 for t in ts if isinstance(t, ops.FP8Weight))
+        return n
 
     # ------------------------------------------------------------------ weights
     def _shard_layer(self, q, k, v, o, g, u, dn, in_norm, post_norm):
@@ -143,6 +153,15 @@ class LlamaModel:
         del embed, lm
         if self.device.type == "cuda":
             torch.cuda.empty_cache()
+
+    def _init_meta(self):
+        cfg, hd, F = self.cfg, self.hd, self.F
+        e = lambda *shape: torch.empty(*shape, device="meta", dtype=self.dtype)  # noqa: E731
+        self.embed = e(self.v_end - self.v_start, cfg.hidden)
+        self.layers = [LlamaLayerWeights(qkv=e((self.nq + 2 * self.nkv) * hd, cfg.hidden), o=e(cfg.hidden, self.nq * hd),
+                                         gu=e(2 * F, cfg.hidden), down=e(cfg.hidden, F))
+                       for _ in range(cfg.n_layers)]
+        self.lm_head = e(self.v_end - self.v_start, cfg.hidden)
 
     def _vocab_shard(self, embed: torch.Tensor) -> torch.Tensor:
         """This rank's rows [v_start, v_end) of the token embedding (SURVEY.md §2.7 K14 / §2.8 C3:

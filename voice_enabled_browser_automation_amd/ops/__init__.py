@@ -359,13 +359,17 @@ def gemm(x: torch.Tensor, w, out: torch.Tensor, *, epi: str = "none", bias: Opti
     return out
 
 
-def gemm_ok(x: torch.Tensor, w) -> bool:
+def _rows16(t: Optional[torch.Tensor]) -> bool:
+    return t is None or (t.stride(-1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0)
+
+
+def gemm_ok(x: torch.Tensor, w, out: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None) -> bool:
     """Shapes the tiled GEMM takes (bf16 weights, N % 16, K % 128, 16-byte aligned rows)."""
     if isinstance(w, FP8Weight) or not _gpu(x) or x.dtype != torch.bfloat16:
         return False
     wt = w.t if isinstance(w, TiledWeight) else w
-    return (wt.dtype == torch.bfloat16 and wt.shape[0] % 16 == 0 and wt.shape[1] % 128 == 0 and x.stride(1) == 1
-            and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0)
+    return (wt.dtype == torch.bfloat16 and wt.shape[0] % 16 == 0 and wt.shape[1] % 128 == 0 and _rows16(x)
+            and _rows16(out) and _rows16(residual))
 
 
 # ----------------------------------------------------------------------------- GEMM family
@@ -408,7 +412,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
             return out
         if ln_c is not None:
             return linear(_layernorm_plain(x, eps), w, bias, out=out, residual=residual, act=act, out_dtype=out_dtype)
-        if _gpu(x) and gemm_ok(x, w) and (act == "none" or residual is None) and \
+        if _gpu(x) and gemm_ok(x, w, out, residual) and (act == "none" or residual is None) and \
                 (out.dtype == torch.bfloat16 or (residual is None and act == "none")):
             e = "resid" if residual is not None else ("gelu" if act == "gelu" else "none")
             return gemm(x, w, out, epi=e, bias=bias, residual=residual, fuse_rms=fuse_rms, eps=eps)
@@ -435,7 +439,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         else:
             E.skinny_gemm(x, w, bias, out, epi, fuse_rms, eps, residual, **mk)
         return out
-    if not fp8 and gemm_ok(x, w) and (act == "none" or residual is None) and \
+    if not fp8 and gemm_ok(x, w, out, residual) and (act == "none" or residual is None) and \
             (out.dtype == torch.bfloat16 or (residual is None and act == "none")):
         e = "resid" if residual is not None else ("gelu" if act == "gelu" else "none")
         return gemm(x, w, out, epi=e, bias=bias, residual=residual, fuse_rms=fuse_rms, eps=eps)
@@ -466,7 +470,7 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
         if _gpu(x) and _stream_ok(x, w_gu):
             ext().skinny_gemm_swiglu(x, w_gu.t, None, out, fuse_rms, eps, None, True)
             return out
-        if _gpu(x) and gemm_ok(x, w_gu):
+        if _gpu(x) and gemm_ok(x, w_gu, out):
             return gemm(x, w_gu, out, epi="swiglu", fuse_rms=fuse_rms, eps=eps)
         w_gu = w_gu.dense()
     if not _gpu(x):
@@ -480,7 +484,7 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
         else:
             E.skinny_gemm_swiglu(x, w_gu, None, out, fuse_rms, eps)
         return out
-    if not fp8 and gemm_ok(x, w_gu):
+    if not fp8 and gemm_ok(x, w_gu, out):
         return gemm(x, w_gu, out, epi="swiglu", fuse_rms=fuse_rms, eps=eps)
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
     gu = _fp8_matmul(xin, w_gu) if fp8 else torch.matmul(xin, w_gu.t())

@@ -122,6 +122,19 @@ class LLMEngine:
         self.max_model_len = max_model_len
         self.max_seqs = max_seqs
         cfg = model.cfg
+        if kv_blocks is None and kv_gb is None and os.environ.get("VWA_KV_GB", "").strip().lower() == "auto":
+            # size the paged KV from the per-GPU HBM plan (runtime/memory_plan.py): what the weights,
+            # step buffers and workspaces leave of the 288 GB
+            from .memory_plan import plan_memory
+
+            free, _total = torch.cuda.mem_get_info(self.device) if self.device.type == "cuda" else (0, 0)
+            plan = plan_memory(cfg, model.tp.size, wdtype=getattr(model, "wdtype", "bf16"), block_size=block_size,
+                               max_rows=max_rows, max_ctx=max_model_len)
+            kv_blocks = plan.kv_blocks
+            if free:  # never more than the device has free now (other processes, fragmentation)
+                per = PagedKVCache.bytes_per_block(cfg.n_layers, model.nkv, model.hd, block_size)
+                kv_blocks = min(kv_blocks, int(free * 0.9) // per)
+            self.memory_plan = plan
         if kv_blocks is None:
             if kv_gb is None:
                 kv_gb = float(os.environ.get("VWA_KV_GB", "0") or 0)
