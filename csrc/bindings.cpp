@@ -68,7 +68,6 @@ int run_skinny(int epi, const SkinnyParams& p, hipStream_t st) {
 
 SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, bool fuse_rms, double eps,
                          const c10::optional<Tensor>& w_scale = c10::nullopt, bool w_tiled = false) {
-  TORCH_CHECK(!(w_tiled && w_scale.has_value()), "pre-tiled weights are bf16 only");
   check_bf16(x, "x");
   if (w_scale.has_value()) {
     TORCH_CHECK(w.scalar_type() == at::kFloat8_e4m3fn && w.is_cuda(), "fp8 weights must be float8_e4m3fn on the GPU");
@@ -100,13 +99,14 @@ SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<T
   p.w_first = g_w_first == 2 || (g_w_first == 1 && fuse_rms);
   p.w_tiled = w_tiled ? 1 : 0;
   if (w_tiled) TORCH_CHECK(w.size(0) % 16 == 0 && w.size(1) % 128 == 0, "pre-tiled weights need N % 16 == 0, K % 128 == 0");
+  // (fp8 + tiled: the fp8 tiled layout, which only the streaming kernel's W8A8 path reads)
   return p;
 }
 
 // fp8 weights run only on the streaming kernel; a shape it cannot take is an error, never a
 // silent bf16 fallback (the Python layer routes those shapes to the dequantising path).
 int run_skinny_checked(int epi, const SkinnyParams& p, hipStream_t st) {
-  // pre-tiled weights exist only for the streaming kernel (a shape it rejects is an error)
+  // pre-tiled weights (bf16 or fp8) exist only for the streaming kernel (a shape it rejects is an error)
   if (p.w_tiled) return vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
   if (p.w_scale || (p.fuse_rms == 2 && !small_gemm(p))) return vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
   return run_skinny(epi, p, st);
@@ -251,6 +251,68 @@ void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi,
     p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws->numel());
   }
   check_rc(vwa_gemm((int)epi, &p, cur_stream(x)), "gemm");
+}
+
+// W8A8 tiled GEMM (gemm.hip, F8): x8 OCP e4m3 [M, K] with per-row scales sx (quant_fp8_rows),
+// w8 the fp8 tiled layout [N, K] with per-row scales sw.
+void gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> bias, Tensor y, int64_t epi,
+              c10::optional<Tensor> rstd, c10::optional<Tensor> residual, c10::optional<Tensor> ws) {
+  c10::DeviceGuard g(x8.device());
+  TORCH_CHECK(x8.is_cuda() && x8.scalar_type() == at::kFloat8_e4m3fn && x8.dim() == 2 && x8.stride(1) == 1 &&
+                  x8.stride(0) % 16 == 0 && (reinterpret_cast<uintptr_t>(x8.data_ptr()) & 15) == 0,
+              "x8: fp8 e4m3 [M, K] rows 16-byte aligned");
+  TORCH_CHECK(w8.is_cuda() && w8.scalar_type() == at::kFloat8_e4m3fn && w8.is_contiguous() && w8.dim() == 2 &&
+                  w8.size(1) == x8.size(1),
+              "w8: fp8 e4m3 [N, K] (tiled)");
+  TORCH_CHECK(sx.is_cuda() && sx.scalar_type() == at::kFloat && sx.numel() >= x8.size(0), "sx f32 [M]");
+  TORCH_CHECK(sw.is_cuda() && sw.scalar_type() == at::kFloat && sw.numel() == w8.size(0), "sw f32 [N]");
+  TORCH_CHECK(epi >= 0 && epi <= 3, "gemm_fp8: bad epilogue");
+  GemmParams p{};
+  p.X = reinterpret_cast<const uint16_t*>(x8.data_ptr());
+  p.ldx = (int)x8.stride(0);
+  p.W = reinterpret_cast<const uint16_t*>(w8.data_ptr());
+  p.w_tiled = 1;
+  p.M = (int)x8.size(0);
+  p.N = (int)w8.size(0);
+  p.K = (int)w8.size(1);
+  TORCH_CHECK(p.N % 16 == 0 && p.K % 128 == 0, "gemm_fp8: N % 16 == 0 and K % 128 == 0 required");
+  if (epi == 2) TORCH_CHECK(p.N % 32 == 0, "gemm_fp8 SwiGLU: gate/up rows must be a multiple of 32");
+  TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.stride(1) == 1 && y.size(0) == p.M &&
+                  y.size(1) == (epi == 2 ? p.N / 2 : p.N) && y.stride(0) % 8 == 0 &&
+                  (reinterpret_cast<uintptr_t>(y.data_ptr()) & 15) == 0,
+              "y shape / alignment");
+  TORCH_CHECK(y.scalar_type() == at::kBFloat16 || (y.scalar_type() == at::kFloat && epi != 2), "y bf16 (or f32)");
+  p.Y = y.data_ptr();
+  p.ldy = (int)y.stride(0);
+  p.y_f32 = y.scalar_type() == at::kFloat;
+  p.sx = sx.data_ptr<float>();
+  p.sw = sw.data_ptr<float>();
+  if (bias.has_value()) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->numel() == p.N && bias->is_contiguous(), "bias [N]");
+    p.bias = bfp(*bias);
+  }
+  if (epi == 1) {
+    TORCH_CHECK(residual.has_value(), "residual epilogue needs residual");
+    check_bf16(*residual, "residual");
+    TORCH_CHECK(residual->dim() == 2 && residual->size(0) == p.M && residual->size(1) == p.N &&
+                    residual->stride(1) == 1 && residual->stride(0) % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(residual->data_ptr()) & 15) == 0 && !p.y_f32,
+                "residual shape / alignment");
+    p.R = bfp(*residual);
+    p.ldr = (int)residual->stride(0);
+  }
+  if (rstd.has_value()) {
+    TORCH_CHECK(rstd->is_cuda() && rstd->scalar_type() == at::kFloat && rstd->numel() >= p.M, "rstd f32 [M]");
+    p.rstd = rstd->data_ptr<float>();
+  }
+  p.splits = 1;
+  if (ws.has_value()) {
+    TORCH_CHECK(ws->is_cuda() && ws->scalar_type() == at::kFloat && ws->is_contiguous(), "ws f32");
+    p.ws = ws->data_ptr<float>();
+    p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x8), ws->numel());
+  }
+  check_rc(vwa_gemm((int)epi, &p, cur_stream(x8)), "gemm_fp8");
 }
 
 void row_rstd(Tensor x, Tensor rstd, double eps) {
@@ -968,6 +1030,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rstd") = py::none(), py::arg("residual") = py::none(), py::arg("w_tiled") = false,
         py::arg("ws") = py::none());
   m.def("row_rstd", &row_rstd);
+  m.def("gemm_fp8", &gemm_fp8, py::arg("x8"), py::arg("sx"), py::arg("w8"), py::arg("sw"), py::arg("bias"),
+        py::arg("y"), py::arg("epi"), py::arg("rstd") = py::none(), py::arg("residual") = py::none(),
+        py::arg("ws") = py::none());
   m.def("rmsnorm", &rmsnorm);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);

@@ -64,17 +64,24 @@ VWA_DEVICE void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned vo
 //     -> 16 rows reading one chunk touch 16 distinct (row parity, slot) bank groups
 //   B image [8 tiles][2 s'][64 lanes][16 B]: the tiled weight's fragment blocks verbatim (a
 //     row-major weight gathers each lane's fragment from its row instead)
-template <bool WT>
+// F8 (W8A8): one FULL k-group per stage (16 fp8 = 16 B per chunk): A chunk c = 2 g + s2 holds
+// X8[row][128 kg + 32 g + 16 s2 .. + 16), B the fp8 tiled block [s2][lane][16 B] of the tile
+// (ops.tile_weight_fp8) -- the same 32 KB stage images as a bf16 half k-group.
+template <bool WT, bool F8>
 VWA_DEVICE void issue_stage(const GemmParams& p, __amdgpu_buffer_rsrc_t rx, __amdgpu_buffer_rsrc_t rw, int bm,
                             int bn, int hs, char* buf) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int kg = hs >> 1, h = hs & 1;
+  const int kg = F8 ? hs : hs >> 1, h = F8 ? 0 : hs & 1;
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
     const int q = it * 4 + w;  // wave-instruction index: rows 8q .. 8q + 7
     const int r = 8 * q + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
     const int m = bm + r;
-    const unsigned off = (unsigned)(((size_t)m * p.ldx + (size_t)kg * BKG + 32 * (c >> 1) + 16 * h + 8 * (c & 1)) * 2);
+    unsigned off;
+    if constexpr (F8)
+      off = (unsigned)((size_t)m * p.ldx + (size_t)kg * BKG + 32 * (c >> 1) + 16 * (c & 1));
+    else
+      off = (unsigned)(((size_t)m * p.ldx + (size_t)kg * BKG + 32 * (c >> 1) + 16 * h + 8 * (c & 1)) * 2);
     dma16(rx, buf + q * 1024, m < p.M ? off : 0xFFFFFFF0u);
   }
   const int kgn = p.K / BKG;
@@ -83,7 +90,10 @@ VWA_DEVICE void issue_stage(const GemmParams& p, __amdgpu_buffer_rsrc_t rx, __am
     const int q = it * 4 + w;  // tile q >> 1, sub-step s' = q & 1
     const int tile = q >> 1, sp = q & 1;
     unsigned off;
-    if constexpr (WT) {
+    if constexpr (F8) {
+      const int T = (bn >> 4) + tile;
+      off = T * 16 < p.N ? (unsigned)(((size_t)T * kgn + kg) * 2048 + sp * 1024 + lane * 16) : 0xFFFFFFF0u;
+    } else if constexpr (WT) {
       const int T = (bn >> 4) + tile;
       off = T * 16 < p.N ? (unsigned)((((size_t)T * kgn + kg) * 2048 + (2 * h + sp) * 512 + lane * 8) * 2) : 0xFFFFFFF0u;
     } else {
@@ -91,6 +101,26 @@ VWA_DEVICE void issue_stage(const GemmParams& p, __amdgpu_buffer_rsrc_t rx, __am
       off = n < p.N ? (unsigned)(((size_t)n * p.K + (size_t)kg * BKG + 32 * g + 16 * h + 8 * sp) * 2) : 0xFFFFFFF0u;
     }
     dma16(rw, buf + 16384 + q * 1024, off);
+  }
+}
+
+VWA_DEVICE void compute_stage_f8(const char* buf, f32x4 (&acc)[4][4], int wm, int wn) {
+  const int l = lane_id();
+  const int rl = l & 15, g = l >> 4;
+  const char* la = buf + (wm * 64 + rl) * 128;
+  const char* lb = buf + 16384 + (wn * 4) * 2048 + l * 16;
+#pragma unroll
+  for (int sg = 0; sg < 4; ++sg) {  // 32-deep MFMA sub-steps: chunk 2 g + (sg >> 1), half sg & 1
+    long a[4], b[4];
+    const int ch = (((2 * g + (sg >> 1)) ^ (rl >> 1)) << 4) + 8 * (sg & 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const long*>(la + i * 16 * 128 + ch);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const long*>(lb + j * 2048 + (sg >> 1) * 1024 + 8 * (sg & 1));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16_fp8(a[i], b[j], acc[i][j]);
   }
 }
 
@@ -125,7 +155,7 @@ VWA_DEVICE void store_out(const GemmParams& p, int m, int n, float v) {
     reinterpret_cast<u16*>(p.Y)[(size_t)m * p.ldy + n] = f2bf(v);
 }
 
-template <int EPI, bool WT>
+template <int EPI, bool WT, bool F8 = false>
 __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int mb = (p.M + BM - 1) / BM, nb = (p.N + BN - 1) / BN;
@@ -145,19 +175,23 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // pipeline: two LDS buffers, the next half-stage's DMA in flight during this one's MFMAs;
   // raw barriers with counted vmcnt (a __syncthreads would drain the in-flight DMA)
-  const int h0 = 2 * kg0, nh = 2 * (kg1 - kg0);
-  const __amdgpu_buffer_rsrc_t rx = rsrc(p.X, (size_t)p.M * p.ldx * 2);
-  const __amdgpu_buffer_rsrc_t rw = rsrc(p.W, (size_t)p.N * p.K * 2);
-  if (nh > 0) issue_stage<WT>(p, rx, rw, bm, bn, h0, lds);
-  if (nh > 1) issue_stage<WT>(p, rx, rw, bm, bn, h0 + 1, lds + kStageBytes);
+  constexpr int SPG = F8 ? 1 : 2;  // stages per k-group
+  const int h0 = SPG * kg0, nh = SPG * (kg1 - kg0);
+  const __amdgpu_buffer_rsrc_t rx = rsrc(p.X, (size_t)p.M * p.ldx * (F8 ? 1 : 2));
+  const __amdgpu_buffer_rsrc_t rw = rsrc(p.W, (size_t)p.N * p.K * (F8 ? 1 : 2));
+  if (nh > 0) issue_stage<WT, F8>(p, rx, rw, bm, bn, h0, lds);
+  if (nh > 1) issue_stage<WT, F8>(p, rx, rw, bm, bn, h0 + 1, lds + kStageBytes);
   for (int i = 0; i < nh; ++i) {
     if (i + 1 < nh)
       asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");  // this half-stage landed everywhere
     else
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    compute_stage(lds + (i & 1) * kStageBytes, acc, wm, wn);
+    if constexpr (F8)
+      compute_stage_f8(lds + (i & 1) * kStageBytes, acc, wm, wn);
+    else
+      compute_stage(lds + (i & 1) * kStageBytes, acc, wm, wn);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done reading it
-    if (i + 2 < nh) issue_stage<WT>(p, rx, rw, bm, bn, h0 + i + 2, lds + (i & 1) * kStageBytes);
+    if (i + 2 < nh) issue_stage<WT, F8>(p, rx, rw, bm, bn, h0 + i + 2, lds + (i & 1) * kStageBytes);
   }
   const int l = lane_id();
   const int col0 = bn + wn * 64 + (l & 15);
@@ -194,6 +228,16 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) rsv[i][r] = row0 + i * 16 + r < p.M ? p.rstd[row0 + i * 16 + r] : 1.f;
   }
+  // W8A8: acc * sx[m] * sw[n] (SwiGLU: gate / up columns scale before the activation)
+  float cz[4] = {1.f, 1.f, 1.f, 1.f};
+  if constexpr (F8) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rsv[i][r] *= row0 + i * 16 + r < p.M ? p.sx[row0 + i * 16 + r] : 1.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cz[j] = col0 + j * 16 < p.N ? p.sw[col0 + j * 16] : 0.f;
+  }
   if (p.y_f32) {  // f32 logits (rare: prefill LM head rows) -- direct stores
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -205,7 +249,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
         for (int j = 0; j < 4; ++j) {
           const int n = col0 + j * 16;
           if (n >= p.N) continue;
-          float v = acc[i][j][r] * rsv[i][r] + bz[j];
+          float v = acc[i][j][r] * rsv[i][r] * cz[j] + bz[j];
           if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
           reinterpret_cast<float*>(p.Y)[(size_t)m * p.ldy + n] = v;
         }
@@ -225,13 +269,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
       if constexpr (EPI == EPI_SWIGLU) {
 #pragma unroll
         for (int j = 0; j < 4; j += 2) {
-          const float gt = acc[i][j][r] * rsv[i][r], up = acc[i][j + 1][r] * rsv[i][r];
+          const float gt = acc[i][j][r] * rsv[i][r] * cz[j], up = acc[i][j + 1][r] * rsv[i][r] * cz[j + 1];
           *reinterpret_cast<u16*>(wl + rl * RS + ((j >> 1) * 16 + (l & 15)) * 2) = f2bf(silu(gt) * up);
         }
       } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float v = acc[i][j][r] * rsv[i][r] + bz[j];
+          float v = acc[i][j][r] * rsv[i][r] * cz[j] + bz[j];
           if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
           *reinterpret_cast<u16*>(wl + rl * RS + (j * 16 + (l & 15)) * 2) = f2bf(v);
         }
@@ -267,7 +311,7 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmParams p) {
   if (id >= (int64_t)p.M * ncols) return;
   const int m = (int)(id / ncols), c = (int)(id % ncols);
   const size_t slab = (size_t)p.M * p.N;
-  const float rs = p.rstd ? p.rstd[m] : 1.f;
+  const float rs = (p.rstd ? p.rstd[m] : 1.f) * (p.sx ? p.sx[m] : 1.f);
   if constexpr (EPI == EPI_SWIGLU) {
     const int n = (c >> 4) * 32 + (c & 15);
     float gt = 0.f, up = 0.f;
@@ -275,11 +319,15 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmParams p) {
       gt += p.ws[z * slab + (size_t)m * p.N + n];
       up += p.ws[z * slab + (size_t)m * p.N + n + 16];
     }
+    if (p.sw) {
+      gt *= p.sw[n];
+      up *= p.sw[n + 16];
+    }
     reinterpret_cast<u16*>(p.Y)[(size_t)m * p.ldy + c] = f2bf(silu(gt * rs) * (up * rs));
   } else {
     float v = 0.f;
     for (int z = 0; z < p.splits; ++z) v += p.ws[z * slab + (size_t)m * p.N + c];
-    v = v * rs + bias_at(p, c);
+    v = v * rs * (p.sw ? p.sw[c] : 1.f) + bias_at(p, c);
     if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
     store_out<EPI>(p, m, c, v);
   }
@@ -307,7 +355,9 @@ int launch_epi(const GemmParams& p, hipStream_t st) {
   const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   const dim3 grid(tiles * p.splits);
   const int lds = kLds;
-  if (p.w_tiled)
+  if (p.sw)
+    hipLaunchKernelGGL((gemm_kernel<EPI, true, true>), grid, dim3(kThreads), lds, st, p);
+  else if (p.w_tiled)
     hipLaunchKernelGGL((gemm_kernel<EPI, true>), grid, dim3(kThreads), lds, st, p);
   else
     hipLaunchKernelGGL((gemm_kernel<EPI, false>), grid, dim3(kThreads), lds, st, p);
@@ -333,7 +383,9 @@ extern "C" int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats) 
 extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
   GemmParams p = *pp;
   if (p.M < 1 || p.N < 16 || p.N % 16 || p.K < BKG || p.K % BKG) return -10;
-  if (p.ldx % 8 || (reinterpret_cast<uintptr_t>(p.X) & 15) || (reinterpret_cast<uintptr_t>(p.W) & 15)) return -11;
+  if (p.ldx % (p.sw ? 16 : 8) || (reinterpret_cast<uintptr_t>(p.X) & 15) || (reinterpret_cast<uintptr_t>(p.W) & 15))
+    return -11;
+  if (p.sw && (!p.sx || !p.w_tiled)) return -14;  // W8A8: per-row X scales and the fp8 tiled layout
   if (epi == EPI_SWIGLU && (p.N % 32 || p.y_f32)) return -12;
   if (p.splits < 1) p.splits = 1;
   const int KG = p.K / BKG;

@@ -490,10 +490,20 @@ __global__ __launch_bounds__(KS * 64) void skinny_fp8_kernel(SkinnyParams p, int
       const bool ok = (it < n_items) && (kg < ge);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        const unsigned row = (unsigned)(tile * 16 * NT + nt * 16 + nl);
-        const unsigned base = row * (unsigned)K + (unsigned)(kg * 128 + 32 * g);
+        if (p.w_tiled) {
+          // fp8 tiled layout (ops.tile_weight_fp8): the (16-row tile, k-group) block is 2 KB
+          // [s][lane][16 B] -- each load instruction reads 1 KB contiguous, lane (nl, g) gets
+          // W[row][128 kg + 32 g + 16 s .. + 16), the same bytes as the row-major addressing below
+          const unsigned T = (unsigned)(tile * NT + nt);
+          const unsigned base = (T * (unsigned)G + (unsigned)kg) * 2048u + (unsigned)lane * 16u;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) wr[nt][u][s] = bload(rw, ok ? base + 16u * s : kOOB);
+          for (int s = 0; s < 2; ++s) wr[nt][u][s] = bload(rw, ok ? base + 1024u * s : kOOB);
+        } else {
+          const unsigned row = (unsigned)(tile * 16 * NT + nt * 16 + nl);
+          const unsigned base = row * (unsigned)K + (unsigned)(kg * 128 + 32 * g);
+#pragma unroll
+          for (int s = 0; s < 2; ++s) wr[nt][u][s] = bload(rw, ok ? base + 16u * s : kOOB);
+        }
       }
     }
   };

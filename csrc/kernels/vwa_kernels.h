@@ -122,6 +122,9 @@ struct GemmParams {
   const uint16_t* R; int ldr;       // residual (epilogue 1), may alias Y
   const float* rstd;                // [M] per-row scale (RMSNorm with gamma folded into W) or null
   float* ws; int splits; int kg_per_split;  // split-K f32 slabs [splits][M][N] (launcher fills kg_per_split)
+  // W8A8 (sw != null): X is OCP e4m3 bytes [M, ldx] with per-row scales sx, W the fp8 tiled layout
+  // (ops.tile_weight_fp8) with per-row scales sw
+  const float* sx; const float* sw;
 };
 
 struct FlashAttnParams {

@@ -599,3 +599,48 @@ def test_gemm_qkv_rope_kv_write(M):
         res.append((q, kc, vc))
     for a, b in zip(*res):
         close(a, b, 3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 4, 16, 17, 85, 1011])
+def test_fp8_tiled_weights_w8a8(M):
+    """fp8 weights in the fp8 tiled layout (ops.tile_weight_fp8): the W8A8 streaming kernel (<= 16
+    rows) and the W8A8 tiled GEMM (gemm.hip F8, > 16 rows) against the CPU W8A8 emulation, for the
+    store / residual / SwiGLU / QKV epilogues."""
+    K, N = 4096, 1024
+    x = rnd(M, K)
+    w = rnd(N, K, scale=K ** -0.5)
+    wq = ops.FP8Weight.quantize(w, tiled=True)
+    assert wq.tiled and torch.equal(ops.untile_weight_fp8(wq.w8).view(torch.uint8),
+                                    ops.FP8Weight.quantize(w).w8.view(torch.uint8))
+    wc = ops.FP8Weight(wq.rows().cpu(), wq.scale.cpu())
+    out = torch.empty(M, N, dtype=BF, device=DEV)
+    ops.linear(x, wq, out=out, fuse_rms=True)
+    exp = ops.linear(x.cpu(), wc, fuse_rms=True)
+    close(out, exp, 3e-2, 3e-2)
+    res = rnd(M, N)
+    exp = ops.linear(x.cpu(), wc, residual=res.cpu())
+    ops.linear(x, wq, out=res, residual=res)
+    close(res, exp, 3e-2, 3e-2)
+    gu = ops.interleave_gate_up(rnd(512, K, scale=K ** -0.5), rnd(512, K, scale=K ** -0.5))
+    gq = ops.FP8Weight.quantize(gu, tiled=True)
+    got = ops.linear_swiglu(x, gq, fuse_rms=True)
+    exp = ops.linear_swiglu(x.cpu(), ops.FP8Weight(gq.rows().cpu(), gq.scale.cpu()), fuse_rms=True)
+    close(got, exp, 3e-2, 3e-2)
+    nq, nkv, hd = 4, 2, 128
+    wqkv = ops.permute_qkv_rows(rnd((nq + 2 * nkv) * hd, K, scale=K ** -0.5), nq + 2 * nkv, hd)
+    qq = ops.FP8Weight.quantize(wqkv, tiled=True)
+    rope = ops.rope_table(2048, hd, 5e5, device=DEV)
+    pos = torch.arange(M, dtype=torch.int32, device=DEV)
+    slots = torch.arange(M, dtype=torch.int64, device=DEV)
+    outs = []
+    for dev, ww in ((DEV, qq), ("cpu", ops.FP8Weight(qq.rows().cpu(), qq.scale.cpu()))):
+        nb = (M + 15) // 16 + 1
+        kc = torch.zeros(nb, nkv, 16, hd, dtype=BF, device=dev)
+        vc = torch.zeros_like(kc)
+        q = torch.zeros(M, nq * hd, dtype=BF, device=dev)
+        ops.qkv_rope_write(x.to(dev), ww, None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
+                           rope=rope.to(dev), positions=pos.to(dev), slots=slots.to(dev), q_out=q, k_cache=kc,
+                           v_cache=vc)
+        outs.append((q, kc, vc))
+    for a, b in zip(*outs):
+        close(a, b, 4e-2, 4e-2)

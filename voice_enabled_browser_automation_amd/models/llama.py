@@ -93,7 +93,10 @@ class LlamaModel:
         torch.cuda.empty_cache()
 
     def _quantize_fp8(self) -> None:
-        q = ops.FP8Weight.quantize
+        """OCP e4m3 + per-row scales; on the GPU stored once, in the fp8 tiled layout
+        (ops.tile_weight_fp8) the W8A8 streaming kernel and the fp8 GEMM read."""
+        tiled = self.device.type == "cuda" and ops.env_flag("VWA_TILED_WEIGHTS", True)
+        q = lambda w: ops.FP8Weight.quantize(w, tiled=tiled)  # noqa: E731
         for L in self.layers:
             L.qkv, L.o, L.gu, L.down = q(L.qkv), q(L.o), q(L.gu), q(L.down)
         self.lm_head = q(self.lm_head)

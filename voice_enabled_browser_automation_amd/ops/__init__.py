@@ -80,29 +80,52 @@ def _gpu(t: torch.Tensor) -> bool:
 FP8_MAX = 448.0  # OCP e4m3fn
 
 
+def tile_weight_fp8(w8: torch.Tensor) -> torch.Tensor:
+    """fp8 counterpart of tile_weight: per 16-row tile T and 128-wide k-group kg one contiguous
+    2 KB block [s 0..1][lane 0..63][16 B], lane = 16 g + n holding W8[16 T + n][128 kg + 32 g + 16 s
+    .. + 16) -- the W8A8 streaming kernel's per-lane bytes (skinny_fp8_kernel) and the fp8 GEMM's
+    B fragments (gemm.hip F8), so every load instruction reads 1 KB contiguous."""
+    N, K = w8.shape
+    assert N % 16 == 0 and K % 128 == 0, "tile_weight_fp8 needs N % 16 == 0 and K % 128 == 0"
+    t = w8.view(torch.uint8).reshape(N // 16, 16, K // 128, 4, 2, 16)   # [T, n, kg, g, s, e]
+    return t.permute(0, 2, 4, 3, 1, 5).contiguous().view(N, K).view(torch.float8_e4m3fn)
+
+
+def untile_weight_fp8(t: torch.Tensor) -> torch.Tensor:
+    N, K = t.shape
+    u = t.view(torch.uint8).reshape(N // 16, K // 128, 2, 4, 16, 16)     # [T, kg, s, g, n, e]
+    return u.permute(0, 4, 1, 3, 2, 5).contiguous().view(N, K).view(torch.float8_e4m3fn)
+
+
 class FP8Weight:
     """OCP e4m3 weight [N, K] with a per-output-row f32 scale (VWA_DTYPE=fp8).
 
-    Decode GEMMs (<= 16 rows) run the W8A8 streaming kernel: activations are quantised per row
-    on the fly (dynamic amax/448 scale) and multiplied on the fp8 MFMA.  Larger row counts
-    (prefill chunks) use hipBLASLt's fp8 GEMM with row-wise scales when the torch build exposes
-    it, else dequantise.  The CPU reference emulates the same W8A8 rounding.
+    ``tiled``: w8 is in the fp8 tiled layout (tile_weight_fp8), the one copy the GPU kernels read:
+    decode GEMMs (<= 16 rows) run the W8A8 streaming kernel (activations quantised per row on the
+    fly, dynamic amax/448 scale, fp8 MFMA) and larger row counts the W8A8 tiled GEMM (gemm.hip F8,
+    X quantised by one row-quantisation kernel).  The CPU reference emulates the same rounding.
     """
 
-    __slots__ = ("w8", "scale")
+    __slots__ = ("w8", "scale", "tiled")
 
-    def __init__(self, w8: torch.Tensor, scale: torch.Tensor):
-        self.w8, self.scale = w8, scale
+    def __init__(self, w8: torch.Tensor, scale: torch.Tensor, tiled: bool = False):
+        self.w8, self.scale, self.tiled = w8, scale, tiled
 
     @staticmethod
-    def quantize(w: torch.Tensor) -> "FP8Weight":
+    def quantize(w: torch.Tensor, tiled: bool = False) -> "FP8Weight":
         wf = w.float()
         scale = (wf.abs().amax(dim=1) / FP8_MAX).clamp_min(1e-12)
-        w8 = (wf / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn)
-        return FP8Weight(w8.contiguous(), scale.contiguous())
+        w8 = (wf / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).contiguous()
+        if tiled:
+            w8 = tile_weight_fp8(w8)
+        return FP8Weight(w8, scale.contiguous(), tiled)
+
+    def rows(self) -> torch.Tensor:
+        """The row-major e4m3 matrix."""
+        return untile_weight_fp8(self.w8) if self.tiled else self.w8
 
     def dequant(self, dtype=torch.float32) -> torch.Tensor:
-        return (self.w8.float() * self.scale[:, None]).to(dtype)
+        return (self.rows().float() * self.scale[:, None]).to(dtype)
 
     @property
     def shape(self):
@@ -119,7 +142,7 @@ class FP8Weight:
         return 1
 
     def to(self, device) -> "FP8Weight":
-        return FP8Weight(self.w8.to(device), self.scale.to(device))
+        return FP8Weight(self.w8.to(device), self.scale.to(device), self.tiled)
 
 
 def quant_rows_fp8(x: torch.Tensor) -> torch.Tensor:
@@ -150,7 +173,8 @@ _SCALED_MM_OK: Optional[bool] = None
 
 
 def _fp8_matmul(x: torch.Tensor, w: "FP8Weight") -> torch.Tensor:
-    """x [M, K] bf16 @ W8^T for large M: hipBLASLt fp8 GEMM with row-wise scales, or dequantise."""
+    """x [M, K] bf16 @ W8^T for large M with an UNTILED fp8 weight (tiled ones take gemm_fp8):
+    hipBLASLt fp8 GEMM with row-wise scales, or dequantise."""
     global _SCALED_MM_OK
     if _SCALED_MM_OK is not False and hasattr(torch, "_scaled_mm"):
         try:
@@ -363,6 +387,31 @@ def _rows16(t: Optional[torch.Tensor]) -> bool:
     return t is None or (t.stride(-1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0)
 
 
+def gemm_fp8(x: torch.Tensor, w: "FP8Weight", out: torch.Tensor, *, epi: str = "none",
+             bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, fuse_rms: bool = False,
+             eps: float = 1e-5) -> torch.Tensor:
+    """W8A8 tiled MFMA GEMM (gemm.hip F8) for M > 16 rows: x is quantised per row (amax / 448, one
+    kernel), the fp8 MFMA runs on the tiled fp8 weight, both scales (and the RMSNorm 1/rms of the
+    unquantised x) apply in the epilogue."""
+    E = ext()
+    M, K = x.shape
+    x8 = scratch(x.device, "gemm_x8", M * K, torch.uint8).view(torch.float8_e4m3fn).view(M, K)
+    sx = scratch(x.device, "gemm_sx", M)
+    E.quant_fp8_rows(x, x8, sx)
+    rstd = None
+    if fuse_rms:
+        rstd = scratch(x.device, "gemm_rstd", M)
+        E.row_rstd(x, rstd, eps)
+    ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
+    E.gemm_fp8(x8, sx, w.w8, w.scale, bias, out, _GEMM_EPI[epi], rstd, residual, ws)
+    return out
+
+
+def gemm_fp8_ok(x: torch.Tensor, w, out: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None) -> bool:
+    return (isinstance(w, FP8Weight) and w.tiled and _gpu(x) and x.dtype == torch.bfloat16 and w.shape[0] % 16 == 0
+            and w.shape[1] % 128 == 0 and _rows16(x) and _rows16(out) and _rows16(residual))
+
+
 def gemm_ok(x: torch.Tensor, w, out: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None) -> bool:
     """Shapes the tiled GEMM takes (bf16 weights, N % 16, K % 128, 16-byte aligned rows)."""
     if isinstance(w, FP8Weight) or not _gpu(x) or x.dtype != torch.bfloat16:
@@ -435,14 +484,18 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
             assert act == "none"
             epi = 1
         if fp8:
-            E.skinny_gemm(x, w.w8, bias, out, epi, fuse_rms, eps, residual, w.scale)
+            E.skinny_gemm(x, w.w8, bias, out, epi, fuse_rms, eps, residual, w.scale, None, w.tiled)
         else:
             E.skinny_gemm(x, w, bias, out, epi, fuse_rms, eps, residual, **mk)
         return out
-    if not fp8 and gemm_ok(x, w, out, residual) and (act == "none" or residual is None) and \
-            (out.dtype == torch.bfloat16 or (residual is None and act == "none")):
-        e = "resid" if residual is not None else ("gelu" if act == "gelu" else "none")
+    e = "resid" if residual is not None else ("gelu" if act == "gelu" else "none")
+    plain_epi = (act == "none" or residual is None) and (out.dtype == torch.bfloat16 or (residual is None and act == "none"))
+    if fp8 and plain_epi and gemm_fp8_ok(x, w, out, residual):
+        return gemm_fp8(x, w, out, epi=e, bias=bias, residual=residual, fuse_rms=fuse_rms, eps=eps)
+    if not fp8 and plain_epi and gemm_ok(x, w, out, residual):
         return gemm(x, w, out, epi=e, bias=bias, residual=residual, fuse_rms=fuse_rms, eps=eps)
+    if fp8 and w.tiled:
+        w = FP8Weight(w.rows(), w.scale)  # (shapes the tiled kernels reject: dequantising path)
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
     y = _fp8_matmul(xin, w) if fp8 else torch.matmul(xin, w.t())
     if bias is not None or act != "none" or residual is not None:
@@ -480,12 +533,16 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
     fp8 = isinstance(w_gu, FP8Weight)
     if M <= SKINNY_MAX_M and (not fp8 or _fp8_stream_fits(M, x.shape[1], nt=2)):
         if fp8:
-            E.skinny_gemm_swiglu(x, w_gu.w8, None, out, fuse_rms, eps, w_gu.scale)
+            E.skinny_gemm_swiglu(x, w_gu.w8, None, out, fuse_rms, eps, w_gu.scale, w_gu.tiled)
         else:
             E.skinny_gemm_swiglu(x, w_gu, None, out, fuse_rms, eps)
         return out
+    if fp8 and gemm_fp8_ok(x, w_gu, out):
+        return gemm_fp8(x, w_gu, out, epi="swiglu", fuse_rms=fuse_rms, eps=eps)
     if not fp8 and gemm_ok(x, w_gu, out):
         return gemm(x, w_gu, out, epi="swiglu", fuse_rms=fuse_rms, eps=eps)
+    if fp8 and w_gu.tiled:
+        w_gu = FP8Weight(w_gu.rows(), w_gu.scale)
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
     gu = _fp8_matmul(xin, w_gu) if fp8 else torch.matmul(xin, w_gu.t())
     E.swiglu(gu, out)
@@ -528,20 +585,22 @@ def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Te
     E = ext()
     use_rope = rope is not None
     fp8 = isinstance(w_qkv, FP8Weight)
-    if M > SKINNY_MAX_M and not fp8 and gemm_ok(x, w_qkv):
+    if M > SKINNY_MAX_M and (gemm_fp8_ok(x, w_qkv) if fp8 else gemm_ok(x, w_qkv)):
         qkv = scratch(x.device, "qkv", M * w_qkv.shape[0], torch.bfloat16).view(M, w_qkv.shape[0])
-        gemm(x, w_qkv, qkv, bias=bias, fuse_rms=fuse_rms, eps=eps)
+        (gemm_fp8 if fp8 else gemm)(x, w_qkv, qkv, bias=bias, fuse_rms=fuse_rms, eps=eps)
         E.rope_kv_write(qkv, n_q_heads, n_kv_heads, head_dim, use_rope, positions, slots, rope, q_out, k_cache,
                         v_cache)
         return q_out[:M]
     if M <= SKINNY_MAX_M and (not fp8 or _fp8_stream_fits(M, x.shape[1])):
         if fp8:
             E.skinny_gemm_qkv(x, w_qkv.w8, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, use_rope, positions,
-                              slots, rope, q_out, k_cache, v_cache, w_qkv.scale)
+                              slots, rope, q_out, k_cache, v_cache, w_qkv.scale, None, w_qkv.tiled)
         else:
             E.skinny_gemm_qkv(x, w_qkv, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, use_rope, positions,
                               slots, rope, q_out, k_cache, v_cache)
         return q_out[:M]
+    if fp8 and w_qkv.tiled:
+        w_qkv = FP8Weight(w_qkv.rows(), w_qkv.scale)
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
     qkv = _fp8_matmul(xin, w_qkv) if fp8 else torch.matmul(xin, w_qkv.t())
     if bias is not None:
