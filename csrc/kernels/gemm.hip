@@ -39,10 +39,26 @@ namespace {
 
 enum Epi { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_GELU = 3 };
 
-constexpr int BM = 128, BN = 128, BKG = 128;
-constexpr int kThreads = 256;
-constexpr int kStageBytes = 32768;  // one half k-group (64 deep): A 16 KB + B 16 KB
-constexpr int kLds = 2 * kStageBytes;
+constexpr int BKG = 128;
+
+// Workgroup shapes: BM x BN output tile, WM x WN waves, each wave (BM/WM) x (BN/WN).
+//   Cfg<128, 128, 2, 2>: 4 waves of 64 x 64, 64 KB LDS -> 2 workgroups per CU -- the one in use.
+//   (Measured and dropped: Cfg<256, 256, 2, 4>, 8 waves of 128 x 64, which reads 25 % fewer
+//   fragment bytes from LDS per MFMA: 929 vs 915 TF/s on the 1011-row gate/up projection and
+//   2-3x SLOWER on 1011-row o / down -- 64 workgroups cannot fill 256 CUs;
+//   profiles/r3_gemm_bench.md.)
+template <int BM_, int BN_, int WM_, int WN_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NW = WM_ * WN_, THREADS = 64 * NW;
+  static constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // MFMA fragments per wave
+  static constexpr int A_BYTES = BM * 128, STAGE = BM * 128 + BN * 128;
+  static constexpr int NCOL_MAX = BN / WN;
+  static constexpr int EPI_LDS = NW * (FM * 16) * (NCOL_MAX * 2 + 16);
+  static constexpr int LDS = 2 * STAGE > EPI_LDS ? 2 * STAGE : EPI_LDS;
+  static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0 && (BM / 8) / NW + (BN / 8) / NW == 8,
+                "8 LDS-DMA instructions per thread per stage (the counted vmcnt)");
+};
+using CfgS = Cfg<128, 128, 2, 2>;
 
 // buffer resource over [base, base + bytes): loads past the end return zero (rows >= M, weight
 // tiles >= N), so the stage issue needs no bounds branches
@@ -56,25 +72,25 @@ VWA_DEVICE void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned vo
                                            0);
 }
 
-// Half-stage hs = 2 kg + h (k = 128 kg + 32 g + 16 h + 8 s' + e, s' = 0, 1) of the block's
-// tile, LDS-DMA'd straight into buffer `buf` (no registers): 8 wave-instructions of 1 KB per
-// thread-wave.  Each wave-instruction's LDS destination is lane-linear (base + 16 lane), so the
-// A swizzle is applied on the per-lane SOURCE address (and undone on the read):
-//   A image [128 rows][8 chunks of 16 B], chunk c = 2 g + s' at slot c ^ ((row >> 1) & 7)
+// Stage hs of the block's tile (bf16: half k-group hs = 2 kg + h, k = 128 kg + 32 g + 16 h + 8 s'
+// + e, s' = 0, 1), LDS-DMA'd straight into buffer `buf` (no registers): 8 wave-instructions of
+// 1 KB per thread.  Each wave-instruction's LDS destination is lane-linear (base + 16 lane), so
+// the A swizzle is applied on the per-lane SOURCE address (and undone on the read):
+//   A image [BM rows][8 chunks of 16 B], chunk c = 2 g + s' at slot c ^ ((row >> 1) & 7)
 //     -> 16 rows reading one chunk touch 16 distinct (row parity, slot) bank groups
-//   B image [8 tiles][2 s'][64 lanes][16 B]: the tiled weight's fragment blocks verbatim (a
+//   B image [BN/16 tiles][2 s'][64 lanes][16 B]: the tiled weight's fragment blocks verbatim (a
 //     row-major weight gathers each lane's fragment from its row instead)
 // F8 (W8A8): one FULL k-group per stage (16 fp8 = 16 B per chunk): A chunk c = 2 g + s2 holds
 // X8[row][128 kg + 32 g + 16 s2 .. + 16), B the fp8 tiled block [s2][lane][16 B] of the tile
-// (ops.tile_weight_fp8) -- the same 32 KB stage images as a bf16 half k-group.
-template <bool WT, bool F8>
+// (ops.tile_weight_fp8) -- the same stage images as a bf16 half k-group.
+template <class C, bool WT, bool F8>
 VWA_DEVICE void issue_stage(const GemmParams& p, __amdgpu_buffer_rsrc_t rx, __amdgpu_buffer_rsrc_t rw, int bm,
                             int bn, int hs, char* buf) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kg = F8 ? hs : hs >> 1, h = F8 ? 0 : hs & 1;
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int q = it * 4 + w;  // wave-instruction index: rows 8q .. 8q + 7
+  for (int it = 0; it < C::BM / 8 / C::NW; ++it) {
+    const int q = it * C::NW + w;  // wave-instruction index: rows 8q .. 8q + 7
     const int r = 8 * q + (lane >> 3), c = (lane & 7) ^ ((r >> 1) & 7);
     const int m = bm + r;
     unsigned off;
@@ -86,8 +102,8 @@ VWA_DEVICE void issue_stage(const GemmParams& p, __amdgpu_buffer_rsrc_t rx, __am
   }
   const int kgn = p.K / BKG;
 #pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int q = it * 4 + w;  // tile q >> 1, sub-step s' = q & 1
+  for (int it = 0; it < C::BN / 8 / C::NW; ++it) {
+    const int q = it * C::NW + w;  // tile q >> 1, sub-step s' = q & 1
     const int tile = q >> 1, sp = q & 1;
     unsigned off;
     if constexpr (F8) {
@@ -100,47 +116,45 @@ VWA_DEVICE void issue_stage(const GemmParams& p, __amdgpu_buffer_rsrc_t rx, __am
       const int n = bn + tile * 16 + (lane & 15), g = lane >> 4;
       off = n < p.N ? (unsigned)(((size_t)n * p.K + (size_t)kg * BKG + 32 * g + 16 * h + 8 * sp) * 2) : 0xFFFFFFF0u;
     }
-    dma16(rw, buf + 16384 + q * 1024, off);
+    dma16(rw, buf + C::A_BYTES + q * 1024, off);
   }
 }
 
-VWA_DEVICE void compute_stage_f8(const char* buf, f32x4 (&acc)[4][4], int wm, int wn) {
+template <class C, bool F8>
+VWA_DEVICE void compute_stage(const char* buf, f32x4 (&acc)[C::FM][C::FN], int wm, int wn) {
   const int l = lane_id();
   const int rl = l & 15, g = l >> 4;
-  const char* la = buf + (wm * 64 + rl) * 128;
-  const char* lb = buf + 16384 + (wn * 4) * 2048 + l * 16;
+  const char* la = buf + (wm * C::FM * 16 + rl) * 128;
+  const char* lb = buf + C::A_BYTES + (wn * C::FN) * 2048 + l * 16;
+  if constexpr (F8) {
 #pragma unroll
-  for (int sg = 0; sg < 4; ++sg) {  // 32-deep MFMA sub-steps: chunk 2 g + (sg >> 1), half sg & 1
-    long a[4], b[4];
-    const int ch = (((2 * g + (sg >> 1)) ^ (rl >> 1)) << 4) + 8 * (sg & 1);
+    for (int sg = 0; sg < 4; ++sg) {  // 32-deep MFMA sub-steps: chunk 2 g + (sg >> 1), half sg & 1
+      long a[C::FM], b[C::FN];
+      const int ch = (((2 * g + (sg >> 1)) ^ (rl >> 1)) << 4) + 8 * (sg & 1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const long*>(la + i * 16 * 128 + ch);
+      for (int i = 0; i < C::FM; ++i) a[i] = *reinterpret_cast<const long*>(la + i * 16 * 128 + ch);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const long*>(lb + j * 2048 + (sg >> 1) * 1024 + 8 * (sg & 1));
+      for (int j = 0; j < C::FN; ++j)
+        b[j] = *reinterpret_cast<const long*>(lb + j * 2048 + (sg >> 1) * 1024 + 8 * (sg & 1));
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16_fp8(a[i], b[j], acc[i][j]);
-  }
-}
-
-VWA_DEVICE void compute_stage(const char* buf, f32x4 (&acc)[4][4], int wm, int wn) {
-  const int l = lane_id();
-  const int rl = l & 15, g = l >> 4;
-  const char* la = buf + (wm * 64 + rl) * 128;
-  const char* lb = buf + 16384 + (wn * 4) * 2048 + l * 16;
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16_fp8(a[i], b[j], acc[i][j]);
+    }
+  } else {
 #pragma unroll
-  for (int sp = 0; sp < 2; ++sp) {
-    bf16x8 a[4], b[4];
-    const int ch = ((2 * g + sp) ^ (rl >> 1)) << 4;  // ((row >> 1) & 7) == rl >> 1 for every fragment row
+    for (int sp = 0; sp < 2; ++sp) {
+      bf16x8 a[C::FM], b[C::FN];
+      const int ch = ((2 * g + sp) ^ (rl >> 1)) << 4;  // ((row >> 1) & 7) == rl >> 1 for every fragment row
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(la + i * 16 * 128 + ch);
+      for (int i = 0; i < C::FM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(la + i * 16 * 128 + ch);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(lb + j * 2048 + sp * 1024);
+      for (int j = 0; j < C::FN; ++j) b[j] = *reinterpret_cast<const bf16x8*>(lb + j * 2048 + sp * 1024);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+    }
   }
 }
 
@@ -155,57 +169,55 @@ VWA_DEVICE void store_out(const GemmParams& p, int m, int n, float v) {
     reinterpret_cast<u16*>(p.Y)[(size_t)m * p.ldy + n] = f2bf(v);
 }
 
-template <int EPI, bool WT, bool F8 = false>
-__global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
+template <class C, int EPI, bool WT, bool F8 = false>
+__global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int mb = (p.M + BM - 1) / BM, nb = (p.N + BN - 1) / BN;
+  constexpr int FM = C::FM, FN = C::FN;
+  const int mb = (p.M + C::BM - 1) / C::BM, nb = (p.N + C::BN - 1) / C::BN;
   const int tiles = mb * nb;
   const int split = blockIdx.x / tiles;  // split-K slice (blocks of one slice are contiguous)
   // XCD-aware: logical tile order is column-block major, so consecutive logical tiles (same XCD)
   // share the column block's weight tile in L2
   const int lt = xcd_remap((int)(blockIdx.x % tiles), tiles);
-  const int bn = (lt / mb) * BN, bm = (lt % mb) * BM;
+  const int bn = (lt / mb) * C::BN, bm = (lt % mb) * C::BM;
   const int KG = p.K / BKG;
   const int kg0 = split * p.kg_per_split, kg1 = min(KG, kg0 + p.kg_per_split);
-  const int w = threadIdx.x >> 6, wm = w >> 1, wn = w & 1;
-  f32x4 acc[4][4];
+  const int w = threadIdx.x >> 6, wm = w / C::WN, wn = w % C::WN;
+  f32x4 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // pipeline: two LDS buffers, the next half-stage's DMA in flight during this one's MFMAs;
-  // raw barriers with counted vmcnt (a __syncthreads would drain the in-flight DMA)
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // pipeline: two LDS buffers, the next stage's DMA in flight during this one's MFMAs; raw
+  // barriers with counted vmcnt (a __syncthreads would drain the in-flight DMA)
   constexpr int SPG = F8 ? 1 : 2;  // stages per k-group
   const int h0 = SPG * kg0, nh = SPG * (kg1 - kg0);
   const __amdgpu_buffer_rsrc_t rx = rsrc(p.X, (size_t)p.M * p.ldx * (F8 ? 1 : 2));
   const __amdgpu_buffer_rsrc_t rw = rsrc(p.W, (size_t)p.N * p.K * (F8 ? 1 : 2));
-  if (nh > 0) issue_stage<WT, F8>(p, rx, rw, bm, bn, h0, lds);
-  if (nh > 1) issue_stage<WT, F8>(p, rx, rw, bm, bn, h0 + 1, lds + kStageBytes);
+  if (nh > 0) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0, lds);
+  if (nh > 1) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + 1, lds + C::STAGE);
   for (int i = 0; i < nh; ++i) {
     if (i + 1 < nh)
-      asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");  // this half-stage landed everywhere
+      asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");  // this stage landed everywhere
     else
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    if constexpr (F8)
-      compute_stage_f8(lds + (i & 1) * kStageBytes, acc, wm, wn);
-    else
-      compute_stage(lds + (i & 1) * kStageBytes, acc, wm, wn);
+    compute_stage<C, F8>(lds + (i & 1) * C::STAGE, acc, wm, wn);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done reading it
-    if (i + 2 < nh) issue_stage<WT, F8>(p, rx, rw, bm, bn, h0 + i + 2, lds + (i & 1) * kStageBytes);
+    if (i + 2 < nh) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + i + 2, lds + (i & 1) * C::STAGE);
   }
   const int l = lane_id();
-  const int col0 = bn + wn * 64 + (l & 15);
-  const int row0 = bm + wm * 64 + 4 * (l >> 4);
+  const int col0 = bn + wn * FN * 16 + (l & 15);
+  const int row0 = bm + wm * FM * 16 + 4 * (l >> 4);
   if (p.splits > 1) {  // f32 partial slab of this slice; gemm_reduce_kernel applies the epilogue
     float* ws = p.ws + (size_t)split * p.M * p.N;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = row0 + i * 16 + r;
         if (m >= p.M) continue;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < FN; ++j) {
           const int n = col0 + j * 16;
           if (n < p.N) ws[(size_t)m * p.N + n] = acc[i][j][r];
         }
@@ -213,40 +225,44 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
     return;
   }
   // per-lane epilogue operands loaded once (no load-or-constant select per element)
-  float bz[4] = {0.f, 0.f, 0.f, 0.f}, rsv[4][4];
+  float bz[FN], cz[FN], rsv[FM][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    bz[j] = 0.f;
+    cz[j] = 1.f;
+  }
   if (p.bias) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bz[j] = col0 + j * 16 < p.N ? bf2f(p.bias[col0 + j * 16]) : 0.f;
+    for (int j = 0; j < FN; ++j) bz[j] = col0 + j * 16 < p.N ? bf2f(p.bias[col0 + j * 16]) : 0.f;
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) rsv[i][r] = 1.f;
   if (p.rstd) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) rsv[i][r] = row0 + i * 16 + r < p.M ? p.rstd[row0 + i * 16 + r] : 1.f;
   }
   // W8A8: acc * sx[m] * sw[n] (SwiGLU: gate / up columns scale before the activation)
-  float cz[4] = {1.f, 1.f, 1.f, 1.f};
   if constexpr (F8) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) rsv[i][r] *= row0 + i * 16 + r < p.M ? p.sx[row0 + i * 16 + r] : 1.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) cz[j] = col0 + j * 16 < p.N ? p.sw[col0 + j * 16] : 0.f;
+    for (int j = 0; j < FN; ++j) cz[j] = col0 + j * 16 < p.N ? p.sw[col0 + j * 16] : 0.f;
   }
   if (p.y_f32) {  // f32 logits (rare: prefill LM head rows) -- direct stores
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = row0 + i * 16 + r;
         if (m >= p.M) continue;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < FN; ++j) {
           const int n = col0 + j * 16;
           if (n >= p.N) continue;
           float v = acc[i][j][r] * rsv[i][r] * cz[j] + bz[j];
@@ -258,23 +274,24 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
   }
   // bf16 out: the wave's tile goes through LDS (padded rows: the four row groups of a store hit
   // different banks) and leaves as 16-byte row chunks -- coalesced stores, 16-byte residual reads
-  constexpr int NCOL = EPI == EPI_SWIGLU ? 32 : 64;  // output columns of this wave
-  constexpr int RS = EPI == EPI_SWIGLU ? 96 : 144;   // LDS row stride (bytes)
-  char* wl = lds + w * (64 * RS);
+  constexpr int NCOL = EPI == EPI_SWIGLU ? FN * 8 : FN * 16;  // output columns of this wave
+  constexpr int RS = NCOL * 2 + (NCOL == 32 ? 32 : 16);       // LDS row stride (bytes, 16-aligned)
+  constexpr int ROWS = FM * 16;
+  char* wl = lds + w * (ROWS * RS);
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int rl = i * 16 + 4 * (l >> 4) + r;
       if constexpr (EPI == EPI_SWIGLU) {
 #pragma unroll
-        for (int j = 0; j < 4; j += 2) {
+        for (int j = 0; j < FN; j += 2) {
           const float gt = acc[i][j][r] * rsv[i][r] * cz[j], up = acc[i][j + 1][r] * rsv[i][r] * cz[j + 1];
           *reinterpret_cast<u16*>(wl + rl * RS + ((j >> 1) * 16 + (l & 15)) * 2) = f2bf(silu(gt) * up);
         }
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < FN; ++j) {
           float v = acc[i][j][r] * rsv[i][r] * cz[j] + bz[j];
           if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
           *reinterpret_cast<u16*>(wl + rl * RS + (j * 16 + (l & 15)) * 2) = f2bf(v);
@@ -284,11 +301,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_kernel(GemmParams p) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   constexpr int CPR = NCOL / 8;  // 16-byte chunks per row
   const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
-  const int cbase = EPI == EPI_SWIGLU ? (bn + wn * 64) / 2 : bn + wn * 64;
+  const int cbase = EPI == EPI_SWIGLU ? (bn + wn * FN * 16) / 2 : bn + wn * FN * 16;
 #pragma unroll
-  for (int it = 0; it < 64 * CPR / 64; ++it) {
+  for (int it = 0; it < ROWS * CPR / 64; ++it) {
     const int idx = it * 64 + l, row = idx / CPR, ch = idx % CPR;
-    const int m = bm + wm * 64 + row, n = cbase + ch * 8;
+    const int m = bm + wm * ROWS + row, n = cbase + ch * 8;
     if (m >= p.M || n >= ncols) continue;
     uint4 v = *reinterpret_cast<const uint4*>(wl + row * RS + ch * 16);
     if constexpr (EPI == EPI_RESID) {
@@ -350,17 +367,22 @@ __global__ __launch_bounds__(256) void row_rstd_kernel(const u16* __restrict__ x
   if (lane_id() == 0) rstd[row] = rsqrtf(ss / (float)K + eps);
 }
 
+template <class C, int EPI>
+int launch_cfg(const GemmParams& p, hipStream_t st) {
+  const int tiles = ((p.M + C::BM - 1) / C::BM) * ((p.N + C::BN - 1) / C::BN);
+  const dim3 grid(tiles * p.splits);
+  if (p.sw)
+    hipLaunchKernelGGL((gemm_kernel<C, EPI, true, true>), grid, dim3(C::THREADS), C::LDS, st, p);
+  else if (p.w_tiled)
+    hipLaunchKernelGGL((gemm_kernel<C, EPI, true>), grid, dim3(C::THREADS), C::LDS, st, p);
+  else
+    hipLaunchKernelGGL((gemm_kernel<C, EPI, false>), grid, dim3(C::THREADS), C::LDS, st, p);
+  return 0;
+}
+
 template <int EPI>
 int launch_epi(const GemmParams& p, hipStream_t st) {
-  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
-  const dim3 grid(tiles * p.splits);
-  const int lds = kLds;
-  if (p.sw)
-    hipLaunchKernelGGL((gemm_kernel<EPI, true, true>), grid, dim3(kThreads), lds, st, p);
-  else if (p.w_tiled)
-    hipLaunchKernelGGL((gemm_kernel<EPI, true>), grid, dim3(kThreads), lds, st, p);
-  else
-    hipLaunchKernelGGL((gemm_kernel<EPI, false>), grid, dim3(kThreads), lds, st, p);
+  launch_cfg<CfgS, EPI>(p, st);
   if (p.splits > 1) {
     const int64_t n = (int64_t)p.M * (EPI == EPI_SWIGLU ? p.N / 2 : p.N);
     hipLaunchKernelGGL((gemm_reduce_kernel<EPI>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
@@ -373,7 +395,7 @@ int launch_epi(const GemmParams& p, hipStream_t st) {
 // Split-K slices for a shape: enough workgroups to cover the CUs ~2x when the output tiles
 // alone cannot (few rows: weight streaming), bounded by the k-groups and the workspace.
 extern "C" int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats) {
-  const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int tiles = ((M + CfgS::BM - 1) / CfgS::BM) * ((N + CfgS::BN - 1) / CfgS::BN);
   const int KG = K / BKG;
   int s = 1;
   while (tiles * s < cus && s * 2 <= KG && (int64_t)(s * 2) * M * N <= ws_floats) s *= 2;

@@ -536,7 +536,7 @@ def test_tiled_mfma_gemm_epilogues(M, tiled):
     """The LDS-tiled MFMA GEMM (csrc/kernels/gemm.hip) for M > 16 rows -- prefill, many-row decode
     steps, the Whisper encoder -- on pre-tiled and row-major weights, every epilogue, with and
     without split-K (small M x N), against the f32 reference."""
-    for (N, K) in ((384, 384), (1024, 4096)):
+    for (N, K) in ((384, 384), (1024, 4096), (2048, 512)):  # (the last: the 256 x 256 tile from 512 rows)
         x = rnd(M, K)
         w = rnd(N, K, scale=K ** -0.5)
         wt = ops.TiledWeight(w) if tiled else w
@@ -644,3 +644,16 @@ def test_fp8_tiled_weights_w8a8(M):
         outs.append((q, kc, vc))
     for a, b in zip(*outs):
         close(a, b, 4e-2, 4e-2)
+
+
+@pytest.mark.parametrize("M", [600, 1011])
+def test_fp8_gemm_large_tile(M):
+    """W8A8 tiled GEMM on the 256 x 256 workgroup tile (>= 512 rows, N % 256 == 0) vs emulation."""
+    K, N = 1024, 2048
+    x = rnd(M, K)
+    w = rnd(N, K, scale=K ** -0.5)
+    wq = ops.FP8Weight.quantize(w, tiled=True)
+    out = torch.empty(M, N, dtype=BF, device=DEV)
+    ops.linear(x, wq, out=out, fuse_rms=True)
+    exp = ops.linear(x.cpu(), ops.FP8Weight(wq.rows().cpu(), wq.scale.cpu()), fuse_rms=True)
+    close(out, exp, 3e-2, 3e-2)
