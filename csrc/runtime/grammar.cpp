@@ -104,6 +104,22 @@ enum { R_OPEN = 0, R_KEYQ, R_KEY, R_COLON, R_VAL, R_AFTER };
 enum { A_OPEN = 0, A_VAL, A_AFTER, A_COMMA };
 
 inline bool is_digit(unsigned char c) { return c >= '0' && c <= '9'; }
+
+// Digits so far spell the magnitude `mag` (`count` digits, sign `neg`): can appending k >= 0
+// more digits (none after a leading zero, at most 15 in all) give a value in [lo, hi]?
+inline bool int_completable(double mag, int count, bool neg, double lo, double hi) {
+  const double mlo = neg ? std::max(0.0, -hi) : std::max(0.0, lo);
+  const double mhi = neg ? -lo : hi;
+  if (mhi < mlo) return false;
+  const int kmax = (mag == 0 && count >= 1) ? 0 : 15 - count;
+  double scale = 1.0;
+  for (int k = 0; k <= kmax; ++k, scale *= 10.0) {
+    const double a = mag * scale, b = a + scale - 1.0;  // values reachable with k more digits
+    if (a > mhi) return false;
+    if (b >= mlo) return true;
+  }
+  return false;
+}
 inline bool printable(unsigned char c) { return c >= 0x20 && c <= 0x7e; }
 inline void set_first(Node& n, unsigned char c) { n.first[c >> 3] |= (uint8_t)(1u << (c & 7)); }
 inline bool has_first(const Node& n, unsigned char c) { return (n.first[c >> 3] >> (c & 7)) & 1u; }
@@ -496,8 +512,10 @@ bool Grammar::feed(State& s, unsigned char c) const {
         if (c == '-' && f.count == 0 && !neg && n.lo < 0) { f.flag |= 1; return true; }
         if (is_digit(c) && !(f.count == 1 && f.val == 0) && f.count < 15) {
           const double nv = f.val * 10 + (c - '0');
-          const bool ok = neg ? (-nv >= n.lo) : (nv <= n.hi);
-          if (ok) { f.val = nv; f.count++; return true; }
+          // admissible only if some completion of the digits lands in [lo, hi]: a "0" for a
+          // positive integer (timeout_ms >= 1) would otherwise be a dead end -- no digit may
+          // follow a leading zero and 0 itself is out of range
+          if (int_completable(nv, f.count + 1, neg, n.lo, n.hi)) { f.val = nv; f.count++; return true; }
         }
         // not a continuation: terminate the number if complete and re-feed c to the parent
         if (f.count >= 1) {

@@ -113,3 +113,22 @@ def test_generic_json_schema_compiler(tok):
                      ('{"n":01,"ok":true}', False)]:
         m = cg.matcher(1000)
         assert (m.accept_bytes(text.encode()) and m.is_accept()) == ok, text
+
+
+def test_integer_ranges_never_dead_end(g):
+    """timeout_ms is an integer >= 1 (schema.ts: int().positive()): a leading "0" can never be
+    completed (no digit may follow it, 0 is out of range), so the grammar must not admit it --
+    that dead state surfaced as an all-empty mask under concurrent sampling.  Every admitted
+    digit string must still be completable; the bounds are enforced exactly."""
+    pre = b'{"version":"1.0","intents":[{"type":"back","args":{},"priority":0,"requires_confirmation":false,"timeout_ms":'
+    for digits, ok in ((b"0", False), (b"1", True), (b"600000", True), (b"600001", False), (b"60000", True),
+                       (b"9", True), (b"01", False)):
+        m = g.matcher(512)
+        assert m.accept_bytes(pre)
+        assert m.accept_bytes(digits) == ok, digits
+    # retries: 0..3 -> "0" fine, "4" not
+    pre_r = b'{"version":"1.0","intents":[{"type":"back","args":{},"priority":0,"requires_confirmation":false,"retries":'
+    for digits, ok in ((b"0", True), (b"3", True), (b"4", False), (b"10", False)):
+        m = g.matcher(512)
+        assert m.accept_bytes(pre_r)
+        assert m.accept_bytes(digits) == ok, digits

@@ -62,6 +62,7 @@ class IntentRequest:
     text: Optional[str] = None
     error: Optional[BaseException] = None
     future: Any = None
+    diag: Optional[str] = None
 
     def stats(self, t_end: float) -> Dict[str, Any]:
         return dict(prompt_tokens=len(self.ids), cached_prefix_tokens=self.cached,
@@ -277,6 +278,8 @@ class LLMIntentEngine:
         tm["sample_launch_ms"] += (self._t3 - t2) * 1e3
         tm["gpu_wait_ms"] += (t4 - self._t3) * 1e3
         self.batch_stats["sampled"] += n
+        if any(t == -1 for t in toks):
+            self._diagnose(batch, toks, logits, n)
         self._accept(batch, toks, finished)
         if finished:
             self.active = [r for r in self.active if not r.done]
@@ -337,13 +340,30 @@ class LLMIntentEngine:
         self._t3 = t3
         return toks
 
+    def _diagnose(self, batch, toks, logits, n) -> None:
+        """A -1 token means no admissible token had a finite logit: record what the row looked like
+        (mask population, finite admissible logits) in the request's error for the logs."""
+        for i, (r, t) in enumerate(zip(batch, toks)):
+            if t != -1:
+                continue
+            words = torch.from_numpy(self.h_mask_np[i].copy()).to(torch.int64) & 0xFFFFFFFF
+            bits = ((words[:, None] >> torch.arange(32)[None, :]) & 1).reshape(-1).bool()
+            row = logits[i].float().cpu()
+            lo = self.engine.model.v_start if getattr(self.engine.model, "tp", None) and self.engine.model.tp.size > 1 else 0
+            adm = bits[lo : lo + row.shape[0]]
+            vals = row[adm[: row.shape[0]]]
+            r.diag = (f"row {i}/{n}: {int(bits.sum())} admissible tokens, {int(torch.isfinite(vals).sum())} finite "
+                      f"admissible logits, row finite {int(torch.isfinite(row).sum())}/{row.numel()}, step {r.steps}, "
+                      f"out {bytes(r.out[-40:])!r}")
+
     def _accept(self, batch: List[IntentRequest], toks: List[int], finished: List[IntentRequest]) -> None:
         for r, tok in zip(batch, toks):
             r.steps += 1
             m = r.matcher
             if tok < 0 or not m.accept_token(tok):
                 self.batch_stats["rejects"] = self.batch_stats.get("rejects", 0) + 1
-                self._finish(r, IntentEngineError(f"sampler returned a token the grammar rejects ({tok})"))
+                self._finish(r, IntentEngineError(f"sampler returned a token the grammar rejects ({tok})"
+                                                  + (f": {r.diag}" if getattr(r, "diag", None) else "")))
             else:
                 r.out += self.grammar_bytes(tok)
                 if m.is_accept():

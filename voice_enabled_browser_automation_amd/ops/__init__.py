@@ -349,15 +349,19 @@ def rope_table(max_pos: int, head_dim: int, theta: float, device=None, scaling: 
 
 # ----------------------------------------------------------------------------- scratch
 _SCRATCH: dict = {}
+_SCRATCH_RETIRED: list = []
 
 
 def scratch(device, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
-    """A per-device reusable buffer of at least ``numel`` elements (stream-ordered users only;
-    created on the first -- eager -- call, so graph captures after a warm-up reuse it)."""
+    """A per-device reusable buffer of at least ``numel`` elements (stream-ordered users only).
+    A buffer outgrown by a larger request is RETIRED, never freed: a captured hipGraph may still
+    address it (its replays keep using the old address while eager calls move to the new one)."""
     key = (str(device), name, dtype)
     t = _SCRATCH.get(key)
     if t is None or t.numel() < numel:
-        t = torch.empty(max(numel, 1), dtype=dtype, device=device)
+        if t is not None:
+            _SCRATCH_RETIRED.append(t)
+        t = torch.empty(max(numel, 1024), dtype=dtype, device=device)
         _SCRATCH[key] = t
     return t[:numel]
 
