@@ -88,6 +88,34 @@ def main():
     for _ in range(ITERS):
         ops.log_mel(audio, n_frames=3000, window=window, cos_table=cos, mel_fb=fb, out=mel)
     torch.cuda.synchronize()
+    # round 3: the tiled MFMA GEMM (gemm.hip) on the prompt-suffix / cold-prompt gate-up shape,
+    # bf16 and W8A8, and the chained decode layer (chain_kernel) of a Llama-3-8B-shaped model
+    for M in (85, 1011):
+        xg = torch.randn(M, 4096, device=dev).to(torch.bfloat16)
+        wg = ops.TiledWeight((torch.randn(28672, 4096, device=dev) * 0.02).to(torch.bfloat16))
+        hg = torch.empty(M, 14336, device=dev, dtype=torch.bfloat16)
+        for _ in range(ITERS):
+            ops.linear_swiglu(xg, wg, fuse_rms=True, out=hg)
+        del wg
+    wq = ops.FP8Weight.quantize((torch.randn(28672, 4096, device=dev) * 0.02).to(torch.bfloat16), tiled=True)
+    xg = torch.randn(85, 4096, device=dev).to(torch.bfloat16)
+    hg = torch.empty(85, 14336, device=dev, dtype=torch.bfloat16)
+    for _ in range(ITERS):
+        ops.linear_swiglu(xg, wq, fuse_rms=True, out=hg)
+    del wq
+    torch.cuda.synchronize()
+    from voice_enabled_browser_automation_amd.models.config import LlamaConfig
+    from voice_enabled_browser_automation_amd.models.llama import LlamaModel
+    from voice_enabled_browser_automation_amd.runtime.engine import LLMEngine
+
+    cfg = LlamaConfig(name="pmc8b", n_layers=3)  # Llama-3-8B layer shapes (3 layers: 1.3 GB > MALL)
+    m = LlamaModel(cfg, device=dev, seed=1)
+    e = LLMEngine(m, max_seqs=1, max_model_len=2048, use_graphs=False)
+    s = e.new_sequence(list(range(1000, 2100)), use_prefix_cache=False)
+    e.prefill(s)
+    for i in range(ITERS):
+        e.run_rows([(s, 7 + i)])
+    torch.cuda.synchronize()
     print("pmc_kernels done", flush=True)
 
 
