@@ -422,7 +422,9 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                                        int64_t a_st, c10::optional<Tensor> a_ctx, c10::optional<Tensor> a_seq,
                                        double a_scale, int64_t a_n_splits, c10::optional<Tensor> a_part_o,
                                        c10::optional<Tensor> a_part_ml, c10::optional<Tensor> a_counters,
-                                       bool w_tiled, c10::optional<Tensor> a_row_table) {
+                                       bool w_tiled, c10::optional<Tensor> a_row_table,
+                                       c10::optional<Tensor> s_o, c10::optional<Tensor> s_gu,
+                                       c10::optional<Tensor> s_down, c10::optional<Tensor> s_qkv) {
   c10::DeviceGuard g(h.device());
   const int64_t M = h.size(0);
   TORCH_CHECK(att.size(0) == M && act.size(0) == M, "row counts differ");
@@ -433,16 +435,21 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                   (reinterpret_cast<uintptr_t>(bar.data_ptr()) & 127) == 0,
               "bar must be a 128-byte aligned int32[>=384] on the GPU");
   ChainParams cp{};
-  cp.ph[0].p = base_params(att, w_o, c10::nullopt, false, eps, c10::nullopt, w_tiled);
+  // s_*: per-row scales of fp8 tiled weights (ops.tile_weight_fp8) -> the W8A16 chain
+  TORCH_CHECK(s_o.has_value() == s_gu.has_value() && s_o.has_value() == s_down.has_value() &&
+                  (!w_qkv.has_value() || s_qkv.has_value() == s_o.has_value()),
+              "fp8 chain: every phase's weight needs its scales");
+  TORCH_CHECK(!s_o.has_value() || w_tiled, "fp8 chain: tiled fp8 weights only");
+  cp.ph[0].p = base_params(att, w_o, c10::nullopt, false, eps, s_o, w_tiled);
   cp.ph[0].epi = 1;
   set_resid(cp.ph[0].p, h);
-  cp.ph[1].p = base_params(h, w_gu, c10::nullopt, true, eps, c10::nullopt, w_tiled);
+  cp.ph[1].p = base_params(h, w_gu, c10::nullopt, true, eps, s_gu, w_tiled);
   cp.ph[1].epi = 2;
   check_bf16(act, "act");
   TORCH_CHECK(act.stride(1) == 1, "act rows must be contiguous");
   cp.ph[1].p.Y = act.data_ptr();
   cp.ph[1].p.ldy = (int)act.stride(0);
-  cp.ph[2].p = base_params(act, w_down, c10::nullopt, false, eps, c10::nullopt, w_tiled);
+  cp.ph[2].p = base_params(act, w_down, c10::nullopt, false, eps, s_down, w_tiled);
   cp.ph[2].epi = 1;
   set_resid(cp.ph[2].p, h);
   cp.n = 3;
@@ -452,7 +459,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
     TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
                     v_cache.has_value(),
                 "the QKV phase needs positions, slots, q_out and the KV caches");
-    cp.ph[3].p = base_params(h, *w_qkv, c10::nullopt, true, eps, c10::nullopt, w_tiled);
+    cp.ph[3].p = base_params(h, *w_qkv, c10::nullopt, true, eps, s_qkv, w_tiled);
     cp.ph[3].epi = 4;
     set_qkv_epilogue(cp.ph[3].p, *w_qkv, n_q_heads, n_kv_heads, head_dim, rope.has_value(), *positions, *slots, rope,
                      *q_out, *k_cache, *v_cache);
@@ -501,7 +508,8 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   std::memcpy(host.data_ptr(), &cp, sizeof(ChainParams));
   // (bit 24 of the returned LDS size: the down phase streams X with the weights -- chain_run
   // launches that instantiation)
-  return {host.to(h.device()), (int64_t)lds | (cp.n >= 3 && cp.ph[2].xg ? (int64_t)1 << 24 : 0)};
+  return {host.to(h.device()), (int64_t)lds | (cp.n >= 3 && cp.ph[2].xg ? (int64_t)1 << 24 : 0) |
+                                    (s_o.has_value() ? (int64_t)1 << 25 : 0)};
 }
 
 // Whisper decoder chains (skinny_stream.hip chain_kernel SEQ 1 / 2): phase i computes
@@ -603,7 +611,7 @@ void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like, int64_t 
   TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess, "CU count");
   // one workgroup per CU: the barrier needs every workgroup resident
   check_rc(vwa_chain_launch(reinterpret_cast<const ChainParams*>(desc.data_ptr()), (int)seq, (int)n_phases, (int)attn_g,
-                            (int)(lds & 0xFFFFFF), cus, cur_stream(like), (int)((lds >> 24) & 1)),
+                            (int)(lds & 0xFFFFFF), cus, cur_stream(like), (int)((lds >> 24) & 1), (int)((lds >> 25) & 1)),
            "chain");
 }
 
@@ -1016,7 +1024,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_table") = py::none(), py::arg("a_block_size") = 0, py::arg("a_sb") = 0, py::arg("a_sh") = 0,
         py::arg("a_st") = 0, py::arg("a_ctx") = py::none(), py::arg("a_seq") = py::none(), py::arg("a_scale") = 0.0,
         py::arg("a_n_splits") = 0, py::arg("a_part_o") = py::none(), py::arg("a_part_ml") = py::none(),
-        py::arg("a_counters") = py::none(), py::arg("w_tiled") = false, py::arg("a_row_table") = py::none());
+        py::arg("a_counters") = py::none(), py::arg("w_tiled") = false, py::arg("a_row_table") = py::none(),
+        py::arg("s_o") = py::none(), py::arg("s_gu") = py::none(), py::arg("s_down") = py::none(),
+        py::arg("s_qkv") = py::none());
   m.def("set_small_gemm_bytes", &set_small_gemm_bytes);
   m.def("chain_make_seq", &chain_make_seq, py::arg("seq"), py::arg("X"), py::arg("W"), py::arg("bias"),
         py::arg("ln_c"), py::arg("Y"), py::arg("epi"), py::arg("eps"), py::arg("n_heads"), py::arg("head_dim"),

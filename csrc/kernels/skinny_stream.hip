@@ -747,9 +747,14 @@ VWA_DEVICE PhaseRange chain_range(const ChainPhase& ph, int wb0 = 0, int wn = 0)
 // needs no X staging and no more registers
 // wx = false (XG): the weights only -- an item issued before the barrier wait must not read X,
 // which other workgroups are still writing; its X fragments follow after the wait (chain_load_x)
-template <int NT, int U, int WA, int R, bool XG = false>
+// F8 (fp8 tiled weights, ops.tile_weight_fp8): a k-group of a 16-row tile is 2 KB, two 16-byte
+// loads per lane (registers (nt * U + u) * 2 + s2, 16 e4m3 each = k 32 g + 16 s2 .. + 16), so an
+// item of the same 16 registers covers twice the k-groups; chain_phase converts them to bf16
+// fragments in registers (v_cvt_scalef32_pk_bf16_fp8) -- W8A16, half the weight bytes
+template <int NT, int U, int WA, int R, bool XG = false, bool F8 = false>
 VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[R], int it, const PhaseRange& r, bool wx = true) {
-  static_assert(XG ? (NT == 1 && U == 2 && R == 16) : NT * U * 4 == R, "an item fills its register set");
+  static_assert(XG ? (NT == 1 && U == 2 && R == 16 && !F8) : NT * U * (F8 ? 2 : 4) == R,
+                "an item fills its register set");
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.W), (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rxg =
@@ -763,7 +768,13 @@ VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[R], int it
     const bool ok = (it < r.n_items) && (kg < r.ge);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      if (p.w_tiled) {
+      if constexpr (F8) {
+        const unsigned T = (unsigned)(tile * NT + nt);
+        const unsigned base = (T * (unsigned)(p.K / 128) + (unsigned)kg) * 2048u + (unsigned)lane * 16u;
+        const unsigned vb = ok ? base : kOOB2;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) wr[(nt * U + u) * 2 + s2] = bload_w_so<WA>(rw, vb, 1024 * s2);
+      } else if (p.w_tiled) {
         // pre-tiled weights (ops.tile_weight): each load instruction reads 1 KB contiguous.
         // Measured (tools/chain_probe.py, Llama-3-8B layer tail): 89.6 vs 101.4 us at 1 row,
         // 96.3 vs 106.8 us at 4 rows against the row-major [N, K] access
@@ -852,33 +863,33 @@ struct ChainShape {
   static constexpr int R = KS == 16 ? 8 : 16;
 };
 
-template <int EPI, int KS = 8, bool XG = false>
+template <int EPI, int KS = 8, bool XG = false, bool F8 = false>
 struct PhaseShape {
   static constexpr int NT = EPI == EPI_SWIGLU ? 2 : 1;
   // (measured: QKV in half-tile units -- 384 tiles -> 3 units per workgroup, one split tile each --
   // 12.5-13.4 us vs 6.7 median / 11.5 max with whole tiles, also with the split tile processed
   // first and published before the next item's loads under a counted vmcnt)
-  static constexpr int U = XG ? 2 : ChainShape<KS>::R / 4 / NT;
+  static constexpr int U = XG ? 2 : ChainShape<KS>::R / 4 / NT * (F8 ? 2 : 1);
 };
 
 // the phase's first weight item (and with pre2 its second) before the barrier wait: a
 // workgroup that arrives early keeps HBM busy while the grid catches up
-template <int EPI, int KS, int WA, bool XG = false, int R>
+template <int EPI, int KS, int WA, bool XG = false, bool F8 = false, int R>
 VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[R], uint4 (&wr2)[R], int pre2, int wb0 = 0,
                                   int wn = 0) {
-  using S = PhaseShape<EPI, KS, XG>;
+  using S = PhaseShape<EPI, KS, XG, F8>;
   const PhaseRange r = chain_range<KS>(ph, wb0, wn);
   // (issued before the barrier wait: XG items without their X fragments, chain_phase adds them)
-  chain_load<S::NT, S::U, WA, R, XG>(ph.p, ph.nb, wr, 0, r, !XG);
-  if (pre2) chain_load<S::NT, S::U, WA, R, XG>(ph.p, ph.nb, wr2, 1, r, !XG);
+  chain_load<S::NT, S::U, WA, R, XG, F8>(ph.p, ph.nb, wr, 0, r, !XG);
+  if (pre2) chain_load<S::NT, S::U, WA, R, XG, F8>(ph.p, ph.nb, wr2, 1, r, !XG);
 }
 
 // one weight item `it` of a phase into wr (the next phase's item 0 / item 1, see chain_kernel)
-template <int EPI, int KS, int WA, bool XG = false, int R>
+template <int EPI, int KS, int WA, bool XG = false, bool F8 = false, int R>
 VWA_DEVICE void chain_issue_item(const ChainPhase& ph, uint4 (&wr)[R], int it, int wb0 = 0, int wn = 0) {
-  using S = PhaseShape<EPI, KS, XG>;
+  using S = PhaseShape<EPI, KS, XG, F8>;
   const PhaseRange r = chain_range<KS>(ph, wb0, wn);
-  chain_load<S::NT, S::U, WA, R, XG>(ph.p, ph.nb, wr, it, r);
+  chain_load<S::NT, S::U, WA, R, XG, F8>(ph.p, ph.nb, wr, it, r);
 }
 
 // partial tile of a split tile: cross-wave sums of this workgroup's units -> slot (sc1)
@@ -908,10 +919,10 @@ VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
 // queued behind weight loads; the other waves issue their item 1 at once (pre2 == 0: one item at
 // the barrier), which streams while the X rows arrive.  hs = items the staging wave has already
 // issued into (X0, X1).
-template <int EPI, int KS, int WA, bool XG = false, int R>
+template <int EPI, int KS, int WA, bool XG = false, bool F8 = false, int R>
 VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 (&X1)[R], char* smem, int pre2,
                             int hs = 0, int wb0 = 0, int wn = 0) {
-  constexpr int NT = PhaseShape<EPI, KS, XG>::NT, U = PhaseShape<EPI, KS, XG>::U;
+  constexpr int NT = PhaseShape<EPI, KS, XG, F8>::NT, U = PhaseShape<EPI, KS, XG, F8>::U;
   const ChainPhase& ph = cp.ph[i];
   const SkinnyParams& p = ph.p;
   const int nb = ph.nb, M = p.M, K = p.K;
@@ -939,7 +950,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     chain_load_x<U>(p, nb, X0, 0, r);
     if (pre2) chain_load_x<U>(p, nb, X1, 1, r);
   }
-  if (xdma && !stager && !pre2) chain_load<NT, U, WA, R, XG>(p, nb, X1, 1, r);  // streams during the staging
+  if (xdma && !stager && !pre2) chain_load<NT, U, WA, R, XG, F8>(p, nb, X1, 1, r);  // streams during the staging
 
   EpiPre pre;
   if (r.n_items > 0) epi_values<EPI, NT, true>(p, first_tile, threadIdx.x, pre);
@@ -958,11 +969,11 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     asm volatile("" ::: "memory");  // keep the weight loads below younger than the pieces
     int nw = 0;
     if (hs < 1) {
-      chain_load<NT, U, WA, R, XG>(p, nb, X0, 0, r);
+      chain_load<NT, U, WA, R, XG, F8>(p, nb, X0, 0, r);
       ++nw;
     }
     if (hs < 2) {
-      chain_load<NT, U, WA, R, XG>(p, nb, X1, 1, r);
+      chain_load<NT, U, WA, R, XG, F8>(p, nb, X1, 1, r);
       ++nw;
     }
     // the pieces are older than the nw weight items (16 loads each): wait for them only
@@ -1029,7 +1040,22 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
         if constexpr (XG) a = wr[8 + u * 4 + s];
         else if (nl < M) a = *reinterpret_cast<const uint4*>(xs + nl * xstride + kg * 128 + 32 * g + 8 * s);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16(as_bf16x8(a), as_bf16x8(wr[(nt * U + u) * 4 + s]), acc[nt]);
+        for (int nt = 0; nt < NT; ++nt) {
+          if constexpr (F8) {
+            // 8 e4m3 of register (nt, u, s >> 1), half s & 1 -> one bf16 B fragment (k 32 g + 8 s ..);
+            // the per-row scale is applied to the finished column in the epilogue (cs0 / cs1)
+            const uint4 w8 = wr[(nt * U + u) * 2 + (s >> 1)];
+            const unsigned d0 = (s & 1) ? w8.z : w8.x, d1 = (s & 1) ? w8.w : w8.y;
+            uint4 bw;
+            bw.x = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d0, 1.0f, false));
+            bw.y = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d0, 1.0f, true));
+            bw.z = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d1, 1.0f, false));
+            bw.w = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d1, 1.0f, true));
+            acc[nt] = mfma16(as_bf16x8(a), as_bf16x8(bw), acc[nt]);
+          } else {
+            acc[nt] = mfma16(as_bf16x8(a), as_bf16x8(wr[(nt * U + u) * 4 + s]), acc[nt]);
+          }
+        }
       }
     }
   };
@@ -1077,7 +1103,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     if (unit % nb != nb - 1 && it != r.n_items - 1) return false;
     return !(tile * nb >= r.u0 && (tile + 1) * nb <= u1);
   };
-  if (!pre2 && !xdma) chain_load<NT, U, WA, R, XG>(p, nb, X1, 1, r);
+  if (!pre2 && !xdma) chain_load<NT, U, WA, R, XG, F8>(p, nb, X1, 1, r);
   auto ldi = [&](uint4 (&wr)[R], int idx) {
     if (idx == 2 && ((i == 1 && cp.lds_item && w < cp.lds_item_waves) ||
                      (i == 2 && cp.lds_item2 && w < cp.lds_item2_waves))) {  // preloaded (chain_preload)
@@ -1087,7 +1113,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
       for (int k = 0; k < R; ++k) wr[k] = *reinterpret_cast<const uint4*>(src + k * 1024);
       return;
     }
-    chain_load<NT, U, WA, R, XG>(p, nb, wr, idx, r);
+    chain_load<NT, U, WA, R, XG, F8>(p, nb, wr, idx, r);
   };
   for (int it = 0; it < n_pad; it += 2) {
     compute(X0, it);
@@ -1129,7 +1155,7 @@ struct SeqEpi {
 
 // XG2: phase 2 (the down projection) streams its X fragments with the weights (ChainParams
 // ph[2].xg: more rows than its X fits LDS, 5..16 rows, no attention phase)
-template <int KS, int SEQ, int NPH, int AG, int WA, bool XG2 = false>
+template <int KS, int SEQ, int NPH, int AG, int WA, bool XG2 = false, bool F8 = false>
 __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __restrict__ cpp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ChainParams& cp = *cpp;  // device-resident descriptor
@@ -1185,10 +1211,10 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   // swapping the sets per path measured 120 B of VGPR spills)
   auto issue0 = [&](int pre) {
     if (nx) {
-      chain_issue_item<E0, KS, WA>(cp.ph[0], B, 0, ob0, on);
-      chain_issue_item<E1, KS, WA>(cp.ph[1], A, 0);
+      chain_issue_item<E0, KS, WA, false, F8>(cp.ph[0], B, 0, ob0, on);
+      chain_issue_item<E1, KS, WA, false, F8>(cp.ph[1], A, 0);
     } else {
-      chain_issue_first<E0, KS, WA>(cp.ph[0], B, A, pre, ob0, on);
+      chain_issue_first<E0, KS, WA, false, F8>(cp.ph[0], B, A, pre, ob0, on);
     }
   };
   auto preload1 = [&]() {
@@ -1275,12 +1301,12 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   // (hand-off by count: a workgroup without o_proj units skips the phase -- its X rows may not be
   // complete yet, and nothing of it is used)
   if (!(AG > 0 && cp.attn_flag) || chain_range<KS>(cp.ph[0], ob0, on).n_items > 0)
-    chain_phase<E0, KS, WA>(cp, 0, B, A, smem, nx ? 1 : pre0, 2, ob0, on);
+    chain_phase<E0, KS, WA, false, F8>(cp, 0, B, A, smem, nx ? 1 : pre0, 2, ob0, on);
   stamp();
   gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
   if (!stg) {
-    if (nx) chain_issue_item<E1, KS, WA>(cp.ph[1], B, 1);  // phase 1's item 0 is already in A
-    else chain_issue_first<E1, KS, WA>(cp.ph[1], A, B, preb);
+    if (nx) chain_issue_item<E1, KS, WA, false, F8>(cp.ph[1], B, 1);  // phase 1's item 0 is already in A
+    else chain_issue_first<E1, KS, WA, false, F8>(cp.ph[1], A, B, preb);
   }
   chain_wait(bar, gen, cp.bar_mode);
   // every attention output was counted and every waiter released before this barrier: reset the
@@ -1288,11 +1314,11 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   if (AG > 0 && cp.attn_flag && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_store(gp(&bar[kBarAttnDone]), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp();
-  chain_phase<E1, KS, WA>(cp, 1, A, B, smem, nx ? 1 : preb, nx ? 1 : 0);
+  chain_phase<E1, KS, WA, false, F8>(cp, 1, A, B, smem, nx ? 1 : preb, nx ? 1 : 0);
   stamp();
   if constexpr (NPH >= 3) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
-    if (!stg || XG2) chain_issue_first<E2, KS, WA, XG2>(cp.ph[2], A, B, preb);  // (XG2: no staging wave)
+    if (!stg || XG2) chain_issue_first<E2, KS, WA, XG2, F8>(cp.ph[2], A, B, preb);  // (XG2: no staging wave)
     // phase 2's LDS item (down projection): its item 2 streams through the barrier window too
     // (phase 1's LDS use ended at the arrival's __syncthreads; the region lies above phase 2's
     // X rows and scratch, which the staging wave fills after the release)
@@ -1301,15 +1327,15 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                                      chain_range<KS>(cp.ph[2]), 2, smem + cp.lds_item2);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E2, KS, WA, XG2>(cp, 2, A, B, smem, preb, 0);
+    chain_phase<E2, KS, WA, XG2, F8>(cp, 2, A, B, smem, preb, 0);
     stamp();
   }
   if constexpr (NPH >= 4) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
-    if (!stg) chain_issue_first<E3, KS, WA>(cp.ph[3], A, B, preb);
+    if (!stg) chain_issue_first<E3, KS, WA, false, F8>(cp.ph[3], A, B, preb);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E3, KS, WA>(cp, 3, A, B, smem, preb, 0);
+    chain_phase<E3, KS, WA, false, F8>(cp, 3, A, B, smem, preb, 0);
     stamp();
   }
 }
@@ -1339,8 +1365,13 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     // 5..16 rows: only without the attention phase (its row tables hold <= 4 rows), Llama tail; a
     // phase whose X rows do not fit LDS next to the scratch streams X with the weights (xg: the
     // down projection, residual epilogue, pre-tiled weights)
-    const int max_rows = (cp->seq == 0 && cp->attn_g == 0) ? 16 : 4;
-    if (p.M < 1 || p.M > max_rows || p.K % 128 != 0 || p.N % (16 * ph.nt) != 0 || p.w_scale) return -10;
+    // fp8 (W8A16 chain): only the fp8 tiled layout, every phase fp8 (one kernel instantiation),
+    // <= 4 rows (no X streaming with the weights)
+    const bool f8 = p.w_scale != nullptr;
+    if (f8 && (!p.w_tiled || cp->seq != 0)) return -10;
+    if (i > 0 && f8 != (cp->ph[0].p.w_scale != nullptr)) return -10;
+    const int max_rows = (cp->seq == 0 && cp->attn_g == 0 && !f8) ? 16 : 4;
+    if (p.M < 1 || p.M > max_rows || p.K % 128 != 0 || p.N % (16 * ph.nt) != 0) return -10;
     const size_t scratch = (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float);
     const size_t xrows = ((size_t)p.M * (p.K + 8) * 2 + 15) & ~(size_t)15;
     ph.xg = 0;
@@ -1348,7 +1379,8 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
       if (!(cp->seq == 0 && i == 2 && ph.epi == EPI_RESID && p.w_tiled && p.fuse_rms == 0)) return -10;
       ph.xg = 1;
     }
-    const int U = ph.xg ? 2 : R / 4 / ph.nt;
+    if (ph.xg && f8) return -10;
+    const int U = ph.xg ? 2 : R / 4 / ph.nt * (f8 ? 2 : 1);
     if ((size_t)p.N * p.K * 2 >= 0x7FFFFFF0ull || (size_t)p.M * p.ldx * 2 >= 0x7FFFFFF0ull) return -10;
     const int G = p.K / 128;
     const int per_wave = (G + KS - 1) / KS;
@@ -1370,7 +1402,8 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
   // phase 1); the attention's own LDS is free again before the preload
   cp->lds_item = 0;
   cp->lds_item_waves = 0;
-  if (cp->lds_item_req == 1 && cp->seq == 0 && cp->attn_g > 0 && cp->n >= 2 && cp->ph[1].p.w_tiled) {
+  const bool any_f8 = cp->ph[0].p.w_scale != nullptr;  // (LDS items preload the bf16 tiled blocks)
+  if (cp->lds_item_req == 1 && cp->seq == 0 && cp->attn_g > 0 && cp->n >= 2 && cp->ph[1].p.w_tiled && !any_f8) {
     size_t start = 0;
     for (int i = 0; i < 2; ++i) {
       const ChainPhase& ph = cp->ph[i];
@@ -1394,7 +1427,7 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
   // must hold nothing but the X pieces at the release)
   cp->lds_item2 = 0;
   cp->lds_item2_waves = 0;
-  if (cp->lds_item2_req == 1 && cp->seq == 0 && cp->n >= 3 && cp->ph[2].p.w_tiled && !cp->ph[2].xg) {
+  if (cp->lds_item2_req == 1 && cp->seq == 0 && cp->n >= 3 && cp->ph[2].p.w_tiled && !cp->ph[2].xg && !any_f8) {
     const ChainPhase& ph = cp->ph[2];
     const size_t x = ((size_t)ph.p.M * (ph.p.K + 8) * 2 + 15) & ~(size_t)15;
     const size_t start = (x + (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float) + 1023) & ~(size_t)1023;
@@ -1410,16 +1443,30 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
 }
 
 extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid,
-                                hipStream_t st, int xg2) {
+                                hipStream_t st, int xg2, int f8) {
   if (attn_g) lds = lds > (int)MqLds<128, 8>::bytes ? lds : (int)MqLds<128, 8>::bytes;
   if (xg2) {  // Llama tail of 5..16 rows: down projection with X from L2, no attention phase
-    if (seq != 0 || attn_g != 0 || (n_phases != 3 && n_phases != 4)) return -10;
+    if (seq != 0 || attn_g != 0 || f8 || (n_phases != 3 && n_phases != 4)) return -10;
     if (n_phases == 4) hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
     else hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
     return (int)hipGetLastError();
   }
 #define VWA_CHAIN_LAUNCH(S, N, G) \
   hipLaunchKernelGGL((chain_kernel<8, S, N, G, 0>), dim3(grid), dim3(8 * 64), lds, st, d_cp)
+#define VWA_CHAIN_LAUNCH_F8(N, G) \
+  hipLaunchKernelGGL((chain_kernel<8, 0, N, G, 0, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp)
+  if (f8) {  // fp8 tiled weights, W8A16 (Llama tail only)
+    if (seq != 0 || (n_phases != 3 && n_phases != 4)) return -10;
+    const bool q = n_phases == 4;
+    switch (attn_g) {
+      case 0: if (q) VWA_CHAIN_LAUNCH_F8(4, 0); else VWA_CHAIN_LAUNCH_F8(3, 0); break;
+      case 4: if (q) VWA_CHAIN_LAUNCH_F8(4, 4); else VWA_CHAIN_LAUNCH_F8(3, 4); break;
+      case 8: if (q) VWA_CHAIN_LAUNCH_F8(4, 8); else VWA_CHAIN_LAUNCH_F8(3, 8); break;
+      default: return -10;
+    }
+    return (int)hipGetLastError();
+  }
+#undef VWA_CHAIN_LAUNCH_F8
   if (seq == 0) {
     if (n_phases != 3 && n_phases != 4) return -10;
     const bool q = n_phases == 4;

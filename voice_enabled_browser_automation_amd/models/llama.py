@@ -212,9 +212,11 @@ class LlamaModel:
     def _chain_ok(self, M: int) -> bool:
         # 5..16 rows (jump-forward feeds, concurrent sessions): the chain without its attention
         # phase, the down projection streaming X with the weights (skinny_stream.hip XG2)
-        return (M <= ops.env_int("VWA_CHAIN_MAX_ROWS", 4) and self.tp.size == 1 and self.wdtype == "bf16" and self.device.type == "cuda"
-                and not getattr(self, "_chain_disabled", False) and ops.env_flag("VWA_CHAIN", True)
-                and ops.native_available())
+        # fp8: the W8A16 chain over the fp8 tiled weights (<= 4 rows: no X streaming)
+        fp8_ok = self.wdtype == "fp8" and M <= 4 and isinstance(self.layers[0].o, ops.FP8Weight) and self.layers[0].o.tiled
+        return (M <= ops.env_int("VWA_CHAIN_MAX_ROWS", 4) and self.tp.size == 1 and (self.wdtype == "bf16" or fp8_ok)
+                and self.device.type == "cuda" and not getattr(self, "_chain_disabled", False)
+                and ops.env_flag("VWA_CHAIN", True) and ops.native_available())
 
     def disable_chain(self) -> None:
         self._chain_disabled = True
@@ -273,14 +275,18 @@ class LlamaModel:
                      a_sb=lay.sb, a_sh=lay.sh, a_st=lay.st, a_ctx=bufs.ctx_lens, a_seq=bufs.seq_ids,
                      a_scale=self.scale, a_n_splits=ops.decode_n_splits(bufs.max_ctx), a_part_o=bufs.part_o,
                      a_part_ml=bufs.part_ml, a_counters=bufs.attn_cnt, a_row_table=bufs.row_table)
-        tiled = isinstance(L.o, ops.TiledWeight)
-        wsel = (lambda w: w.t) if tiled else (lambda w: w)  # noqa: E731
+        f8 = isinstance(L.o, ops.FP8Weight)
+        tiled = f8 or isinstance(L.o, ops.TiledWeight)
+        wsel = (lambda w: w.w8) if f8 else (lambda w: w.t) if tiled else (lambda w: w)  # noqa: E731
+        sc = {}
+        if f8:  # W8A16 chain: fp8 tiled weights converted to bf16 in registers, per-row scales in the epilogues
+            sc = dict(s_o=L.o.scale, s_gu=L.gu.scale, s_down=L.down.scale, s_qkv=N.qkv.scale if nxt else None)
         desc, lds = ops.ext().chain_make(
             bufs.hidden[:M], bufs.attn[:M], bufs.act[:M], wsel(L.o), wsel(L.gu), wsel(L.down), self.cfg.rms_eps,
             wsel(N.qkv) if nxt else None, self.nq, self.nkv, self.hd,
             bufs.positions if nxt else None, bufs.slots if nxt else None, self.rope if nxt else None,
             bufs.q[:M] if nxt else None, kv.k[li + 1] if nxt else None, kv.v[li + 1] if nxt else None,
-            self._chain_bar, self._chain_work, None, self._chain_bar_mode, **a, w_tiled=tiled)
+            self._chain_bar, self._chain_work, None, self._chain_bar_mode, **a, w_tiled=tiled, **sc)
         cache[key] = (desc, 4 if nxt else 3, lds, self.nq // self.nkv if attn else 0) if desc.numel() else None
         return cache[key]
 
