@@ -830,9 +830,10 @@ VWA_DEVICE void chain_load_x(const SkinnyParams& p, int nb, uint4 (&wr)[R], int 
 // at + 16 l).  Issued during the attention window, when HBM idles behind the latency-bound
 // attention and o_proj; the bandwidth-bound gate/up phase then streams one item less per
 // workgroup (measured: 5.5 us per item, tools/chain_probe.py --diag-skip).  Pre-tiled weights.
-template <int NT, int U, int WA>
+// F8: the fp8 tiled item (chain_load F8: two 1 KB loads per k-group, register (nt * U + u) * 2 + s2)
+template <int NT, int U, int WA, bool F8 = false>
 VWA_DEVICE void chain_preload(const SkinnyParams& p, int nb, const PhaseRange& r, int it, char* dst) {
-  static_assert(NT * U == 4, "an item = 16 loads of 1 KB per wave");
+  static_assert(NT * U == (F8 ? 8 : 4), "an item = 16 loads of 1 KB per wave");
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.W), (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
   const unsigned lane = threadIdx.x & 63;
@@ -846,12 +847,13 @@ VWA_DEVICE void chain_preload(const SkinnyParams& p, int nb, const PhaseRange& r
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
       const unsigned T = (unsigned)(tile * NT + nt);
-      const unsigned base = ((T * (unsigned)(p.K / 128) + (unsigned)kg) * 4u) * 1024u + lane * 16u;
+      constexpr int LPK = F8 ? 2 : 4;  // 1 KB loads per k-group
+      const unsigned base = ((T * (unsigned)(p.K / 128) + (unsigned)kg) * (unsigned)LPK) * 1024u + lane * 16u;
       const unsigned vb = ok ? base : kOOB2;
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+      for (int s = 0; s < LPK; ++s)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rw, (__attribute__((address_space(3))) void*)(wd + ((nt * U + u) * 4 + s) * 1024), 16, vb, 1024 * s, 0, WA);
+            rw, (__attribute__((address_space(3))) void*)(wd + ((nt * U + u) * LPK + s) * 1024), 16, vb, 1024 * s, 0, WA);
     }
   }
 }
@@ -1218,8 +1220,8 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     }
   };
   auto preload1 = [&]() {
-    chain_preload<PhaseShape<E1, KS>::NT, PhaseShape<E1, KS>::U, WA>(cp.ph[1].p, cp.ph[1].nb, chain_range<KS>(cp.ph[1]),
-                                                                     2, smem + cp.lds_item);
+    chain_preload<PhaseShape<E1, KS, false, F8>::NT, PhaseShape<E1, KS, false, F8>::U, WA, F8>(
+        cp.ph[1].p, cp.ph[1].nb, chain_range<KS>(cp.ph[1]), 2, smem + cp.lds_item);
   };
   if constexpr (AG > 0) {
    if (cp.attn_flag) {
@@ -1323,8 +1325,8 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     // (phase 1's LDS use ended at the arrival's __syncthreads; the region lies above phase 2's
     // X rows and scratch, which the staging wave fills after the release)
     if (cp.lds_item2 && (int)(threadIdx.x >> 6) < cp.lds_item2_waves)
-      chain_preload<PhaseShape<E2, KS>::NT, PhaseShape<E2, KS>::U, WA>(cp.ph[2].p, cp.ph[2].nb,
-                                                                     chain_range<KS>(cp.ph[2]), 2, smem + cp.lds_item2);
+      chain_preload<PhaseShape<E2, KS, false, F8>::NT, PhaseShape<E2, KS, false, F8>::U, WA, F8>(
+          cp.ph[2].p, cp.ph[2].nb, chain_range<KS>(cp.ph[2]), 2, smem + cp.lds_item2);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
     chain_phase<E2, KS, WA, XG2, F8>(cp, 2, A, B, smem, preb, 0);
@@ -1402,8 +1404,7 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
   // phase 1); the attention's own LDS is free again before the preload
   cp->lds_item = 0;
   cp->lds_item_waves = 0;
-  const bool any_f8 = cp->ph[0].p.w_scale != nullptr;  // (LDS items preload the bf16 tiled blocks)
-  if (cp->lds_item_req == 1 && cp->seq == 0 && cp->attn_g > 0 && cp->n >= 2 && cp->ph[1].p.w_tiled && !any_f8) {
+  if (cp->lds_item_req == 1 && cp->seq == 0 && cp->attn_g > 0 && cp->n >= 2 && cp->ph[1].p.w_tiled) {
     size_t start = 0;
     for (int i = 0; i < 2; ++i) {
       const ChainPhase& ph = cp->ph[i];
@@ -1427,7 +1428,7 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
   // must hold nothing but the X pieces at the release)
   cp->lds_item2 = 0;
   cp->lds_item2_waves = 0;
-  if (cp->lds_item2_req == 1 && cp->seq == 0 && cp->n >= 3 && cp->ph[2].p.w_tiled && !cp->ph[2].xg && !any_f8) {
+  if (cp->lds_item2_req == 1 && cp->seq == 0 && cp->n >= 3 && cp->ph[2].p.w_tiled && !cp->ph[2].xg) {
     const ChainPhase& ph = cp->ph[2];
     const size_t x = ((size_t)ph.p.M * (ph.p.K + 8) * 2 + 15) & ~(size_t)15;
     const size_t start = (x + (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float) + 1023) & ~(size_t)1023;

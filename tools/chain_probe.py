@@ -34,6 +34,7 @@ def main():
                          "launch (its stamps then show the attention with warm caches / TLB)")
     ap.add_argument("--row-major", dest="tiled", action="store_false",
                     help="row-major [N, K] weights instead of the pre-tiled layout (ops.tile_weight)")
+    ap.add_argument("--fp8", action="store_true", help="fp8 tiled weights (the W8A16 chain, ops.FP8Weight)")
     a = ap.parse_args()
     if a.no_wait:
         a.bar_mode = 5 if a.bar_mode >= 4 else 3
@@ -84,12 +85,20 @@ def main():
         tb = akw["a_table"][0].long()
         p_new = torch.arange(a.ctx, a.ctx + M, device=dev)
         slots = tb[p_new // 16] * 16 + p_new % 16
-    if a.tiled:  # the descriptors hold raw pointers: keep the tiled copies alive in Ws
+    sck = [{} for _ in Ws]
+    if a.fp8:
+        a.tiled = True
+        for w, sc in zip(Ws, sck):
+            for k in ("o", "gu", "down", "qkv"):
+                f = ops.FP8Weight.quantize(w[k], tiled=True)
+                w[k + "_t"], sc["s_" + k] = f.w8, f.scale
+                w[k] = f  # the separate launches run the same fp8 weights
+    elif a.tiled:  # the descriptors hold raw pointers: keep the tiled copies alive in Ws
         for w in Ws:
             w.update({k + "_t": ops.tile_weight(w[k]) for k in ("o", "gu", "down", "qkv")})
     wt = (lambda w, k: w[k + "_t"]) if a.tiled else (lambda w, k: w[k])  # noqa: E731
     descs = [E.chain_make(h, att, act, wt(w, "o"), wt(w, "gu"), wt(w, "down"), 1e-5, wt(w, "qkv"), nq, nkv, hd, pos, slots, rope, q,
-                          kc, vc, bar, work, ts, a.bar_mode, **akw, w_tiled=a.tiled) for w in Ws]
+                          kc, vc, bar, work, ts, a.bar_mode, **akw, w_tiled=a.tiled, **sc) for w, sc in zip(Ws, sck)]
     it = [0]
 
     def chained():
@@ -141,7 +150,7 @@ def main():
             col = col[col > 0]
             if col.numel():
                 extra[nm] = [round(float((col.median() - t0) * 10e-3), 2), round(float((col.max() - t0) * 10e-3), 2)]
-    r = dict(kernel="chain_probe", rows=M, ctx=a.ctx if a.attn else None, warm_kv=a.warm_kv, n_splits=a.n_splits, kv_tok_major=a.kv_tok_major, bar_mode=a.bar_mode, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
+    r = dict(kernel="chain_probe", rows=M, fp8=a.fp8, ctx=a.ctx if a.attn else None, warm_kv=a.warm_kv, n_splits=a.n_splits, kv_tok_major=a.kv_tok_major, bar_mode=a.bar_mode, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
              stamps_med_us=[round(x, 2) for x in med], stamps_min_us=[round(x, 2) for x in mn],
              stamps_max_us=[round(x, 2) for x in mx],
              legend=("start,end_attn," if a.attn else "start,") + "end_o,wait_o,end_gu,wait_gu,end_down,wait_down,end_qkv")
