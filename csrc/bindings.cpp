@@ -379,6 +379,18 @@ void skinny_gemm_qkv(Tensor x, Tensor w_qkv, c10::optional<Tensor> bias, bool fu
   check_rc(run_skinny_checked(4, p, cur_stream(x)), "skinny_gemm_qkv");
 }
 
+// Workgroups of a chained launch: one per CU, or CUs / VWA_CHAIN_GRID_DIV when several processes
+// share one GPU (the two-rank tensor-parallel test on a single device: both ranks' persistent
+// launches must be resident at once, or their in-launch rounds wait for each other until the
+// bounded spin gives up)
+int chain_grid(int dev) {
+  int cus = 0;
+  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess, "CU count");
+  const char* e = std::getenv("VWA_CHAIN_GRID_DIV");
+  const int div = e ? std::atoi(e) : 1;
+  return div > 1 ? cus / div : cus;
+}
+
 // Chained-launch schedule (ChainParams): the measured-best settings of the round-2 A/B runs
 // (profiles/r2_*): two weight items issued ahead of each barrier, phase 1's item 0 in the free
 // register set of a one-item phase 0, X staged by one wave with LDS-DMA, o_proj units only on
@@ -424,7 +436,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                                        c10::optional<Tensor> a_part_ml, c10::optional<Tensor> a_counters,
                                        bool w_tiled, c10::optional<Tensor> a_row_table,
                                        c10::optional<Tensor> s_o, c10::optional<Tensor> s_gu,
-                                       c10::optional<Tensor> s_down, c10::optional<Tensor> s_qkv) {
+                                       c10::optional<Tensor> s_down, c10::optional<Tensor> s_qkv, int64_t tp_ar) {
   c10::DeviceGuard g(h.device());
   const int64_t M = h.size(0);
   TORCH_CHECK(att.size(0) == M && act.size(0) == M, "row counts differ");
@@ -465,6 +477,19 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                      *q_out, *k_cache, *v_cache);
     cp.n = 4;
   }
+  if (tp_ar) {
+    // tensor parallel (o_proj / down row-parallel): the two phases write this rank's f32 partial
+    // rows into its chain regions, the in-launch rounds all-reduce them into h (chain_tp_reduce)
+    TORCH_CHECK(vwa_ar_chain_tp(reinterpret_cast<void*>(tp_ar), &cp.tp) == 0, "chain TP: peers not mapped");
+    TORCH_CHECK(h.stride(1) == 1 && M * h.size(1) <= cp.tp.region, "chain TP: rows exceed the chain region");
+    for (int i : {0, 2}) {
+      SkinnyParams& q = cp.ph[i].p;
+      q.Y = cp.tp.stage[cp.tp.rank] + (i == 2 ? cp.tp.region : 0);
+      q.y_f32 = 1;
+      q.ldy = (int)h.size(1);
+      q.R = nullptr;
+    }
+  }
   cp.bar = reinterpret_cast<unsigned*>(bar.data_ptr<int>());
   cp.bar_mode = (int)bar_mode;
   // work: [0, 8192) u32 split-tile tickets (zeroed, self-resetting) | f32 partial slots
@@ -499,10 +524,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
       cp.attn.rt_stride = (int)rtab.size(1);
     }
   }
-  int cus = 0;
-  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h.device().index()) == hipSuccess,
-              "CU count");
-  const int lds = vwa_chain_prepare(&cp, cus);
+  const int lds = vwa_chain_prepare(&cp, chain_grid(h.device().index()));
   if (lds < 0) return {torch::empty({0}, torch::dtype(torch::kUInt8).device(h.device())), 0};
   Tensor host = torch::empty({(int64_t)sizeof(ChainParams)}, torch::dtype(torch::kUInt8));
   std::memcpy(host.data_ptr(), &cp, sizeof(ChainParams));
@@ -568,10 +590,7 @@ std::tuple<Tensor, int64_t> chain_make_seq(int64_t seq, std::vector<Tensor> X, s
   cp.max_tiles = 8192;
   cp.part = reinterpret_cast<float*>(work.data_ptr<int>() + 8192);
   cp.part_floats = (int)(work.numel() - 8192);
-  int cus = 0;
-  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, X[0].device().index()) == hipSuccess,
-              "CU count");
-  const int lds = vwa_chain_prepare(&cp, cus);
+  const int lds = vwa_chain_prepare(&cp, chain_grid(X[0].device().index()));
   if (lds < 0) return {torch::empty({0}, torch::dtype(torch::kUInt8).device(X[0].device())), 0};
   Tensor host = torch::empty({(int64_t)sizeof(ChainParams)}, torch::dtype(torch::kUInt8));
   std::memcpy(host.data_ptr(), &cp, sizeof(ChainParams));
@@ -607,11 +626,10 @@ Tensor alloc_uncached_i32(int64_t n, Tensor like) {
 void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like, int64_t attn_g, int64_t seq) {
   c10::DeviceGuard g(like.device());
   TORCH_CHECK(desc.is_cuda() && desc.numel() == (int64_t)sizeof(ChainParams), "bad chain descriptor");
-  int dev = like.device().index(), cus = 0;
-  TORCH_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess, "CU count");
   // one workgroup per CU: the barrier needs every workgroup resident
   check_rc(vwa_chain_launch(reinterpret_cast<const ChainParams*>(desc.data_ptr()), (int)seq, (int)n_phases, (int)attn_g,
-                            (int)(lds & 0xFFFFFF), cus, cur_stream(like), (int)((lds >> 24) & 1), (int)((lds >> 25) & 1)),
+                            (int)(lds & 0xFFFFFF), chain_grid(like.device().index()), cur_stream(like),
+                            (int)((lds >> 24) & 1), (int)((lds >> 25) & 1)),
            "chain");
 }
 
@@ -1026,7 +1044,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_n_splits") = 0, py::arg("a_part_o") = py::none(), py::arg("a_part_ml") = py::none(),
         py::arg("a_counters") = py::none(), py::arg("w_tiled") = false, py::arg("a_row_table") = py::none(),
         py::arg("s_o") = py::none(), py::arg("s_gu") = py::none(), py::arg("s_down") = py::none(),
-        py::arg("s_qkv") = py::none());
+        py::arg("s_qkv") = py::none(), py::arg("tp_ar") = 0);
   m.def("set_small_gemm_bytes", &set_small_gemm_bytes);
   m.def("chain_make_seq", &chain_make_seq, py::arg("seq"), py::arg("X"), py::arg("W"), py::arg("bias"),
         py::arg("ln_c"), py::arg("Y"), py::arg("epi"), py::arg("eps"), py::arg("n_heads"), py::arg("head_dim"),

@@ -18,11 +18,15 @@
 //      order (bit-identical result on every rank) into the output.
 // Buffers come from hipMalloc and are shared with hipIpcGetMemHandle / hipIpcOpenMemHandle.
 //
+// Behind the gather region: two f32 regions of the chained decode layer's in-launch all-reduce
+// rounds (skinny_stream.hip chain_tp_reduce; vwa_ar_chain_tp hands the pointers to the chain).
+//
 // The same buffers also carry a one-shot ALL-GATHER of small int32 payloads (vwa_ar_gather: the
 // vocab-parallel sampler's per-rank partial (value, index) maxima, SURVEY.md §2.8 C4 as [B, 2]
 // instead of [B, V/T] logits): a separate double-buffered region behind the all-reduce staging
 // and its own flag / epoch slot (index kMaxBlocks), same protocol, one workgroup.
 #include "common.h"
+#include "vwa_kernels.h"
 
 using namespace vwa;
 
@@ -32,8 +36,10 @@ constexpr int kMaxRanks = 8;
 constexpr int kThreads = 512;
 constexpr int kMaxBlocks = 64;
 constexpr int kGatherSlot = kMaxBlocks;   // flag / epoch slot of the all-gather
-constexpr int kSlots = kMaxBlocks + 1;
+constexpr int kChainSlot = kMaxBlocks + 1;  // flag / epoch slot of the chained layer's in-launch rounds
+constexpr int kSlots = kMaxBlocks + 2;
 constexpr int64_t kGatherWords = 64 * 1024;  // int32 words per rank per call (256 KB)
+constexpr int64_t kChainFloats = 16 * 8192;  // f32 per chain region: 16 rows x hidden 8192 (70B)
 
 struct ArPeers {
   uint16_t* staging[kMaxRanks];  // each rank's staging base (2 x max_elems bf16, then 2 x kGatherWords int32)
@@ -142,7 +148,8 @@ void* vwa_ar_create(int rank, int world, int64_t max_elems) {
   s->rank = rank;
   s->world = world;
   s->max_elems = max_elems;
-  if (hipMalloc(&s->staging, 2 * max_elems * sizeof(uint16_t) + 2 * kGatherWords * sizeof(int)) != hipSuccess ||
+  if (hipMalloc(&s->staging, 2 * max_elems * sizeof(uint16_t) + 2 * kGatherWords * sizeof(int) +
+                                 2 * kChainFloats * sizeof(float)) != hipSuccess ||
       hipMalloc(&s->flags, kSlots * kMaxRanks * sizeof(int)) != hipSuccess ||
       hipMalloc(&s->epochs, kSlots * sizeof(int)) != hipSuccess || hipMalloc(&s->error, sizeof(int)) != hipSuccess) {
     delete s;
@@ -207,6 +214,26 @@ int vwa_ar_gather(void* st, const int* in, int* out, int64_t n, hipStream_t stre
 }
 
 int64_t vwa_ar_gather_max_words() { return kGatherWords; }
+
+// The chained decode layer's view of the group (ChainParams::tp): every rank's two f32 chain
+// regions, the peers' flag words this rank signals, its own flag words and round counter.
+// Returns -1 before every peer is mapped.
+int vwa_ar_chain_tp(void* st, ChainTP* out) {
+  auto* s = static_cast<ArState*>(st);
+  const int64_t off = 2 * s->max_elems * (int64_t)sizeof(uint16_t) + 2 * kGatherWords * (int64_t)sizeof(int);
+  *out = ChainTP{};
+  out->world = s->world;
+  out->rank = s->rank;
+  for (int p = 0; p < s->world; ++p) {
+    if (!s->peers.staging[p] || !s->peers.flags[p]) return -1;
+    out->stage[p] = reinterpret_cast<float*>(reinterpret_cast<char*>(s->peers.staging[p]) + off);
+    out->flag_out[p] = s->peers.flags[p] + kChainSlot * kMaxRanks + s->rank;
+  }
+  out->flag_in = s->flags + kChainSlot * kMaxRanks;
+  out->epoch = s->epochs + kChainSlot;
+  out->region = (int)kChainFloats;
+  return 0;
+}
 
 // Non-zero if a call timed out waiting for a peer (sticky).
 int vwa_ar_error(void* st) {

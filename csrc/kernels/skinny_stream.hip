@@ -105,7 +105,7 @@ VWA_DEVICE void epi_values(const SkinnyParams& p, int tile, int o, EpiPre& e) {
     if (o >= p.M * 16 * NT) return;
     const int m = o / (16 * NT), nn = o % (16 * NT);
     if (p.w_scale) e.cs0 = gld(p.w_scale + n0 + nn);
-    if constexpr (EPI == EPI_RESID) e.r = bf2f(ld_u16<SC1>(p.R + (size_t)m * p.ldr + n0 + nn));
+    if constexpr (EPI == EPI_RESID) e.r = p.R ? bf2f(ld_u16<SC1>(p.R + (size_t)m * p.ldr + n0 + nn)) : 0.f;
   }
 }
 
@@ -708,6 +708,47 @@ VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, i
   __syncthreads();
 }
 
+// Tensor-parallel round (ChainParams::tp, world > 1) after a row-parallel phase whose epilogue
+// wrote this rank's f32 partial rows into stage[rank] + region * tp.region: publish (system-scope
+// release, grid barrier), workgroup 0 signals every peer, every workgroup waits for every peer's
+// signal (bounded: a missing peer raises the error word), then reduces its slice of the M x d rows
+// into h (h += partials summed in rank order: the same bits on every rank).  The caller's next
+// grid barrier orders the slices before any workgroup reads h.
+VWA_DEVICE void chain_tp_reduce(const ChainParams& cp, int region, int target, unsigned long long* bar, int nwg,
+                                unsigned long long& bar_next) {
+  const ChainTP& tp = cp.tp;
+  __threadfence_system();
+  const unsigned long long gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
+  chain_wait(bar, gen, cp.bar_mode);
+  if (blockIdx.x == 0 && (int)threadIdx.x < tp.world)
+    __hip_atomic_store(gp(tp.flag_out[threadIdx.x]), target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if ((int)threadIdx.x < tp.world) {
+    const int* f = tp.flag_in + threadIdx.x;
+    int spins = 0;
+    while (__hip_atomic_load(gp(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target < 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kChainSpinLimit) {
+        __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  const SkinnyParams& hp = cp.ph[1].p;  // gate/up's X: the hidden rows h
+  u16* h = const_cast<u16*>(hp.X);
+  const int d = hp.K, n = hp.M * d;
+  const int per = (n + nwg - 1) / nwg, lo = (int)blockIdx.x * per, hi = min(n, lo + per);
+  for (int i = lo + (int)threadIdx.x; i < hi; i += (int)blockDim.x) {
+    const int m = i / d, c = i - m * d;
+    float acc = 0.f;
+    for (int q = 0; q < tp.world; ++q)
+      acc += __hip_atomic_load(gp(tp.stage[q] + (size_t)region * tp.region + i), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    u16* hp_ = h + (size_t)m * hp.ldx + c;
+    st_u16<true>(hp_, f2bf(bf2f(ld_u16<true>(hp_)) + acc));
+  }
+}
+
 // Work distribution (measured: with whole tiles per workgroup, gate/up's 896 tiles over 256
 // workgroups left half of them a fourth tile -- 65 us max vs 54 us median): a phase is a list of
 // ntiles x nb units (unit = one k-batch of every wave's K slice of a tile) and workgroup b takes
@@ -1161,10 +1202,10 @@ template <int KS, int SEQ, int NPH, int AG, int WA, bool XG2 = false, bool F8 = 
 __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __restrict__ cpp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ChainParams& cp = *cpp;  // device-resident descriptor
-  // Warm the scalar cache with the whole descriptor (21 x 64-byte lines) in ONE round trip: the
+  // Warm the scalar cache with the whole descriptor (24 x 64-byte lines) in ONE round trip: the
   // fields are otherwise fetched behind branches and earlier fields' values, a chain of dependent
   // scalar misses (the attention prologue measured ~6 of them before its first vector load)
-  static_assert(sizeof(ChainParams) <= 21 * 64, "descriptor warm-up covers 21 lines");
+  static_assert(sizeof(ChainParams) <= 24 * 64, "descriptor warm-up covers 24 lines");
   {
     // (non-volatile, no memory clobber: a volatile block counts as a memory write and turns every
     // later descriptor read into a vector load; the never-true test keeps it alive)
@@ -1174,6 +1215,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
         "s_load_dword %0, %1, 0x200\n\t""s_load_dword %0, %1, 0x240\n\t""s_load_dword %0, %1, 0x280\n\t""s_load_dword %0, %1, 0x2c0\n\t"
         "s_load_dword %0, %1, 0x300\n\t""s_load_dword %0, %1, 0x340\n\t""s_load_dword %0, %1, 0x380\n\t""s_load_dword %0, %1, 0x3c0\n\t"
         "s_load_dword %0, %1, 0x400\n\t""s_load_dword %0, %1, 0x440\n\t""s_load_dword %0, %1, 0x480\n\t""s_load_dword %0, %1, 0x4c0\n\t""s_load_dword %0, %1, 0x500\n\t"
+        "s_load_dword %0, %1, 0x540\n\t""s_load_dword %0, %1, 0x580\n\t""s_load_dword %0, %1, 0x5c0\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=&s"(junk)
         : "s"(cpp));
@@ -1186,6 +1228,10 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   unsigned long long gen;
   unsigned long long* bar = reinterpret_cast<unsigned long long*>(cp.bar);
   unsigned long long bar_next = chain_base(bar, nwg, cp.bar_mode);  // mode >= 4: running target
+  // TP rounds of this launch: e0 + 1 (after o_proj), e0 + 2 (after down); every workgroup reads e0
+  // before its first arrival, workgroup 0 advances it after the last round
+  const bool tpr = cp.tp.world > 1;
+  const int e0 = tpr ? __hip_atomic_load(gp(cp.tp.epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   int nts = 0;
   auto stamp = [&]() {
     if (cp.ts && threadIdx.x == 0) *gp(cp.ts + blockIdx.x * 32 + nts) = __builtin_amdgcn_s_memrealtime();
@@ -1305,6 +1351,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   if (!(AG > 0 && cp.attn_flag) || chain_range<KS>(cp.ph[0], ob0, on).n_items > 0)
     chain_phase<E0, KS, WA, false, F8>(cp, 0, B, A, smem, nx ? 1 : pre0, 2, ob0, on);
   stamp();
+  if (SEQ == 0 && tpr) chain_tp_reduce(cp, 0, e0 + 1, bar, nwg, bar_next);
   gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
   if (!stg) {
     if (nx) chain_issue_item<E1, KS, WA, false, F8>(cp.ph[1], B, 1);  // phase 1's item 0 is already in A
@@ -1331,6 +1378,11 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     stamp();
     chain_phase<E2, KS, WA, XG2, F8>(cp, 2, A, B, smem, preb, 0);
     stamp();
+    if (SEQ == 0 && tpr) {
+      chain_tp_reduce(cp, 1, e0 + 2, bar, nwg, bar_next);
+      if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(gp(cp.tp.epoch), e0 + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   if constexpr (NPH >= 4) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);

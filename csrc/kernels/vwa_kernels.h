@@ -76,6 +76,20 @@ struct ChainPhase {
   int epi, nt, nb;
   int xg;  // X fragments streamed with the weights (X rows do not fit LDS; set by vwa_chain_prepare)
 };
+// Tensor-parallel in-launch all-reduce of the chained Llama tail (world 1: off).  The row-parallel
+// phases (o_proj, down) write this rank's f32 partial rows into stage[rank] (region 0 / 1); after
+// a grid barrier workgroup 0 signals every peer (flag_out[p] <- round), every workgroup waits for
+// all peers' signals (flag_in[p]) and reduces its slice h += sum over ranks in rank order (the
+// same bits on every rank), then the next barrier.  Rounds are counted by *epoch (two per launch).
+struct ChainTP {
+  int world, rank;
+  float* stage[8];     // each rank's chain regions (IPC-mapped), 2 x region floats
+  int* flag_out[8];    // peer p's flag word for this rank
+  int* flag_in;        // this rank's flag words [8] (peer p signals [p])
+  int* epoch;          // this rank's round counter (private)
+  int region;          // floats per region (>= M x hidden)
+};
+
 struct ChainParams {
   ChainPhase ph[kChainMaxPhases];
   int n;
@@ -110,6 +124,7 @@ struct ChainParams {
   // adds 1 to a counter (bar u64 word 176, reset after the next barrier); only the workgroups
   // with o_proj units wait for the count
   int attn_flag;
+  ChainTP tp;
 };
 
 // LDS-tiled MFMA GEMM (gemm.hip) for M > 16 rows: Y = epi(rstd[m] * X . W^T (+bias) ...)
@@ -195,6 +210,7 @@ int vwa_ar_open_peer(void* st, int p, const void* in);
 int vwa_ar_allreduce(void* st, const uint16_t* in, uint16_t* out, int64_t n, hipStream_t stream);
 int vwa_ar_gather(void* st, const int* in, int* out, int64_t n, hipStream_t stream);
 int64_t vwa_ar_gather_max_words();
+int vwa_ar_chain_tp(void* st, ChainTP* out);
 int vwa_ar_error(void* st);
 void vwa_ar_destroy(void* st);
 #ifdef __cplusplus

@@ -6,7 +6,9 @@ Every rank builds the TP shard of the same random model (deterministic per-layer
 runs prefill + ragged decode through the engine -- eagerly AND with every decode step replayed
 from a hipGraph -- with the one-shot IPC all-reduce for the vocab-parallel embedding and the
 row-parallel outputs, and compares the (diagnostically gathered) logits with a TP=1 model run
-on the same device.  Then the vocab-parallel sampler (partial maxima -> one-shot IPC all-gather
+on the same device.  Decode steps of <= 4 rows run the chained layer (one launch per layer) with
+the row-parallel all-reduces as in-launch rounds over the same IPC buffers
+(skinny_stream.hip chain_tp_reduce).  Then the vocab-parallel sampler (partial maxima -> one-shot IPC all-gather
 -> merge, ops.sample tp=...) is checked token for token against the TP=1 full-vocab sampler,
 under grammar-like random masks and temperature.  VWA_DIST_BACKEND selects the control /
 large-message backend (gloo when two ranks share one GPU, RCCL needs one GPU per rank); the
@@ -67,6 +69,11 @@ def sample_check(tp, dev, ref_model, tp_model):
 
 def main():
     os.environ.setdefault("VWA_DIST_BACKEND", "gloo")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > torch.cuda.device_count():
+        # ranks share a GPU: each chained (persistent) launch takes 1/world of the CUs so every
+        # rank's launch is resident at once (their in-launch all-reduce rounds wait on each other)
+        os.environ.setdefault("VWA_CHAIN_GRID_DIV", str(world))
     tp = init_distributed()
     dev = torch.device("cuda", torch.cuda.current_device())
     torch.manual_seed(0)
@@ -81,9 +88,14 @@ def main():
         ok &= max(errs) < 0.05 * (1 + max(r.abs().max().item() for r in ref))
         if graphs:
             ok &= e.stats["graph_replays"] >= 5
+        # the 1-row decode steps ran the chained layer with its in-launch all-reduce rounds
+        n_chain = sum(v is not None for v in m.chain_descs())
+        want_chain = tp.custom_ar is not None and os.environ.get("VWA_CHAIN_TP", "1") != "0"
+        ok &= (n_chain > 0) == want_chain and not m.chain_error()
         if tp.rank == 0:
             print(f"graphs={graphs} custom_ar={tp.custom_ar is not None} embed_rows={m.embed.shape[0]} "
-                  f"replays={e.stats['graph_replays']} max_errs={[round(x, 4) for x in errs]}", flush=True)
+                  f"replays={e.stats['graph_replays']} chained_layers={n_chain} chain_error={m.chain_error()} "
+                  f"max_errs={[round(x, 4) for x in errs]}", flush=True)
     s_ok = sample_check(tp, dev, ref_model, m)
     ok &= s_ok
     if tp.custom_ar is not None:

@@ -214,7 +214,9 @@ class LlamaModel:
         # phase, the down projection streaming X with the weights (skinny_stream.hip XG2)
         # fp8: the W8A16 chain over the fp8 tiled weights (<= 4 rows: no X streaming)
         fp8_ok = self.wdtype == "fp8" and M <= 4 and isinstance(self.layers[0].o, ops.FP8Weight) and self.layers[0].o.tiled
-        return (M <= ops.env_int("VWA_CHAIN_MAX_ROWS", 4) and self.tp.size == 1 and (self.wdtype == "bf16" or fp8_ok)
+        # TP > 1: the one-shot all-reduce buffers carry the in-launch rounds (chain_tp_reduce)
+        tp_ok = self.tp.size == 1 or (getattr(self.tp, "custom_ar", None) is not None and ops.env_flag("VWA_CHAIN_TP", True))
+        return (M <= ops.env_int("VWA_CHAIN_MAX_ROWS", 4) and tp_ok and (self.wdtype == "bf16" or fp8_ok)
                 and self.device.type == "cuda" and not getattr(self, "_chain_disabled", False)
                 and ops.env_flag("VWA_CHAIN", True) and ops.native_available())
 
@@ -225,7 +227,10 @@ class LlamaModel:
     def enable_chain(self) -> None:
         """Re-arm the chained launch after a fallback (runtime/engine.py retries with backoff): a
         timed-out launch leaves partial arrivals in the barrier tickets, split-tile tickets and
-        the error word, so they restart from zero (call with no chained launch in flight)."""
+        the error word, so they restart from zero (call with no chained launch in flight).
+        Under TP the ranks' in-launch round counters would no longer agree: never re-armed."""
+        if self.tp.size > 1:
+            return
         for t in (getattr(self, "_chain_bar", None), getattr(self, "_chain_work", None)):
             if t is not None:
                 t.zero_()
@@ -286,7 +291,8 @@ class LlamaModel:
             wsel(N.qkv) if nxt else None, self.nq, self.nkv, self.hd,
             bufs.positions if nxt else None, bufs.slots if nxt else None, self.rope if nxt else None,
             bufs.q[:M] if nxt else None, kv.k[li + 1] if nxt else None, kv.v[li + 1] if nxt else None,
-            self._chain_bar, self._chain_work, None, self._chain_bar_mode, **a, w_tiled=tiled, **sc)
+            self._chain_bar, self._chain_work, None, self._chain_bar_mode, **a, w_tiled=tiled, **sc,
+            tp_ar=self.tp.custom_ar.state if self.tp.size > 1 else 0)
         cache[key] = (desc, 4 if nxt else 3, lds, self.nq // self.nkv if attn else 0) if desc.numel() else None
         return cache[key]
 

@@ -391,6 +391,7 @@ class LLMEngine:
 
         rows, logits_for, pre = self._last_step
         self._last_step = None
+        self._tp_chain_fatal()
         warnings.warn("chained decode launch timed out at a grid barrier; re-running the step with "
                       "per-kernel launches")
         word = self.model.chain_error_word()
@@ -430,11 +431,20 @@ class LLMEngine:
         if err:
             import warnings
 
+            self._tp_chain_fatal()
             warnings.warn("chained decode launch timed out at a grid barrier; using per-kernel launches")
             m.disable_chain()
             self.graphs.clear()
             self.stats["chain_fallbacks"] = self.stats.get("chain_fallbacks", 0) + 1
             self._schedule_chain_retry()
+
+    def _tp_chain_fatal(self) -> None:
+        """Under tensor parallelism a chained launch that timed out (a peer's rounds never came)
+        leaves the ranks' in-launch round counters and K/V in disagreement: no per-rank fallback
+        can restore lockstep, so the step fails loudly (the serving layer restarts the group)."""
+        tp = getattr(self.model, "tp", None)
+        if tp is not None and tp.size > 1:
+            raise RuntimeError("chained TP decode launch timed out waiting for a peer rank")
 
     def _schedule_chain_retry(self) -> None:
         """A chain timeout usually means another kernel held CUs for a while (e.g. the ASR engine
