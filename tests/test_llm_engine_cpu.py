@@ -148,7 +148,7 @@ def _tp_worker(rank, world, port, toks, q):
         e.prefill(s)
         logits = e.run_rows([(s, toks[40]), (s, toks[41])])
         if rank == 0:
-            q.put(logits.float().clone())
+            q.put(logits.float().numpy().copy())  # by value: a torch tensor travels as a shared fd the exiting worker may close first
     finally:
         dist.destroy_process_group()
 
@@ -167,7 +167,7 @@ def test_tensor_parallel_gloo_matches_single():
     procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, toks, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=300)
+    got = torch.from_numpy(q.get(timeout=300))
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
