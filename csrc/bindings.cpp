@@ -930,38 +930,83 @@ void pcm16_to_f32(Tensor pcm, Tensor out, double ratio) {
            "pcm16_to_f32");
 }
 
-void log_mel(Tensor audio, int64_t n_frames, Tensor window, Tensor cos_table, Tensor mel_fb, Tensor mel_scratch,
-             Tensor max_buf, Tensor out) {
+void log_mel(Tensor audio, int64_t n_frames, Tensor window, Tensor basis, Tensor fb_frag, int64_t n_mels,
+             Tensor mel_scratch, Tensor max_buf, Tensor out) {
   c10::DeviceGuard g(audio.device());
   TORCH_CHECK(audio.scalar_type() == at::kFloat && audio.is_contiguous(), "audio f32");
-  TORCH_CHECK(window.numel() == 400 && cos_table.numel() == 400, "n_fft=400 tables");
-  const int n_mels = (int)mel_fb.size(0);
-  TORCH_CHECK(mel_fb.size(1) == 201 && mel_fb.is_contiguous() && mel_fb.scalar_type() == at::kFloat, "mel_fb [n_mels,201]");
+  TORCH_CHECK(window.numel() == 400 && window.scalar_type() == at::kFloat && window.is_contiguous(), "n_fft=400 window");
+  TORCH_CHECK(n_mels >= 1 && n_mels <= 128, "n_mels <= 128");
+  const int64_t mt = (n_mels + 15) / 16;
+  TORCH_CHECK(basis.scalar_type() == at::kFloat && basis.is_contiguous() && basis.numel() == 26 * 25 * 64 * 4,
+              "basis: DFT fragments [26][25][64][4] f32 (ops.logmel_tables)");
+  TORCH_CHECK(fb_frag.scalar_type() == at::kFloat && fb_frag.is_contiguous() && fb_frag.numel() == mt * 13 * 64 * 4,
+              "fb_frag: mel filterbank fragments [n_mels/16][13][64][4] f32 (ops.logmel_tables)");
   TORCH_CHECK(mel_scratch.numel() >= n_frames * n_mels && max_buf.numel() >= 1, "scratch");
   TORCH_CHECK(out.scalar_type() == at::kBFloat16 && out.dim() == 2 && out.size(0) >= n_frames && out.size(1) == n_mels &&
                   out.stride(1) == 1,
               "out bf16 [frames, n_mels]");
   TORCH_CHECK(audio.numel() > 200, "audio too short");
   check_rc(vwa_log_mel(audio.data_ptr<float>(), (int)audio.numel(), (int)n_frames, window.data_ptr<float>(),
-                       cos_table.data_ptr<float>(), nullptr, mel_fb.data_ptr<float>(), n_mels,
-                       mel_scratch.data_ptr<float>(), max_buf.data_ptr<float>(), bfp_mut(out), (int)out.stride(0),
-                       cur_stream(audio)),
+                       basis.data_ptr<float>(), fb_frag.data_ptr<float>(), (int)n_mels, mel_scratch.data_ptr<float>(),
+                       max_buf.data_ptr<float>(), bfp_mut(out), (int)out.stride(0), cur_stream(audio)),
            "log_mel");
 }
 
+// Whisper conv stem (K3): conv1d(k=3, pad=1, stride) + bias + GELU (+ pos) as a batched implicit
+// GEMM on the tiled MFMA GEMM (gemm.hip, row-major weights).  x [B, Tin, Cin] must be a view
+// of a zero-padded channels-last buffer (ops.padded_rows): one zero row in front of and behind
+// every batch's Tin rows, so GEMM row t is the 3*Cin contiguous elements starting at padded
+// row t*stride (ldx = stride*Cin).  w [Cout, 3*Cin] in (kk, ci) order.
 void conv1d_gelu(Tensor x, Tensor w, c10::optional<Tensor> b, c10::optional<Tensor> pos, Tensor y, int64_t stride) {
   c10::DeviceGuard g(x.device());
   check_bf16(x, "x");
   check_bf16(w, "w");
-  TORCH_CHECK(x.dim() == 3 && x.is_contiguous(), "x must be [B, T, Cin] contiguous");
-  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) == 3 * x.size(2), "w must be [Cout, 3*Cin] ([co][kk][ci])");
-  TORCH_CHECK(y.dim() == 3 && y.is_contiguous() && y.size(0) == x.size(0) && y.size(2) == w.size(0), "y [B, Tout, Cout]");
-  const int Tin = (int)x.size(1), Tout = (int)y.size(1);
-  TORCH_CHECK(Tout == (Tin + 2 - 3) / stride + 1, "Tout mismatch");
-  if (pos.has_value()) TORCH_CHECK(pos->dim() == 2 && pos->size(0) >= Tout && pos->size(1) == w.size(0), "pos shape");
-  check_rc(vwa_conv1d_gelu_pos(bfp(x), bfp(w), bfp_opt(b), bfp_opt(pos), bfp_mut(y), (int)x.size(0), (int)x.size(2),
-                               Tin, (int)w.size(0), Tout, (int)stride, cur_stream(x)),
-           "conv1d_gelu");
+  check_bf16(y, "y");
+  TORCH_CHECK(x.dim() == 3 && x.stride(2) == 1 && x.stride(1) == x.size(2), "x must be [B, T, Cin] with contiguous rows");
+  const int64_t B = x.size(0), Tin = x.size(1), Cin = x.size(2);
+  TORCH_CHECK(B == 1 || x.stride(0) >= (Tin + 2) * Cin, "x batches must be (Tin + 2)-row padded slabs");
+  TORCH_CHECK(x.storage_offset() >= Cin &&
+                  (int64_t)(x.storage().nbytes() / 2) >= x.storage_offset() + (B - 1) * x.stride(0) + (Tin + 1) * Cin,
+              "x must be a view of a zero-padded buffer (a pad row before and after each batch)");
+  TORCH_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(1) == 3 * Cin, "w must be [Cout, 3*Cin] ([co][kk][ci])");
+  TORCH_CHECK(stride == 1 || stride == 2, "stride 1 or 2");
+  const int64_t Tout = (Tin + 2 - 3) / stride + 1, Cout = w.size(0);
+  TORCH_CHECK(y.dim() == 3 && y.size(0) == B && y.size(1) == Tout && y.size(2) == Cout && y.stride(2) == 1 &&
+                  y.stride(1) % 8 == 0 && (B == 1 || y.stride(0) % 8 == 0) &&
+                  (reinterpret_cast<uintptr_t>(y.data_ptr()) & 15) == 0,
+              "y [B, Tout, Cout] with 16-byte aligned rows");
+  TORCH_CHECK((3 * Cin) % 128 == 0 && Cout % 16 == 0 && Cin % 8 == 0, "conv: 3*Cin % 128 == 0, Cout % 16 == 0");
+  GemmParams p{};
+  p.X = bfp(x) - Cin;  // the zero row in front
+  p.ldx = (int)(stride * Cin);
+  p.W = bfp(w);
+  p.w_tiled = 0;
+  p.M = (int)Tout;
+  p.N = (int)Cout;
+  p.K = (int)(3 * Cin);
+  p.Y = y.data_ptr();
+  p.ldy = (int)y.stride(1);
+  p.splits = 1;
+  p.nbatch = (int)B;
+  p.bsx = x.stride(0);
+  p.bsy = y.stride(0);
+  if (b.has_value()) {
+    check_bf16(*b, "bias");
+    TORCH_CHECK(b->numel() == Cout && b->is_contiguous(), "bias [Cout]");
+    p.bias = bfp(*b);
+  }
+  int epi = 3;
+  if (pos.has_value()) {
+    check_bf16(*pos, "pos");
+    TORCH_CHECK(pos->dim() == 2 && pos->size(0) >= Tout && pos->size(1) == Cout && pos->stride(1) == 1 &&
+                    pos->stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(pos->data_ptr()) & 15) == 0,
+                "pos [>= Tout, Cout] with 16-byte aligned rows");
+    p.R = bfp(*pos);
+    p.ldr = (int)pos->stride(0);
+    p.bsr = 0;
+    epi = 4;
+  }
+  check_rc(vwa_gemm(epi, &p, cur_stream(x)), "conv1d_gelu");
 }
 
 }  // namespace

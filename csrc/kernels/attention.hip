@@ -285,46 +285,65 @@ int dispatch_mq(const DecodeAttnParams& p, hipStream_t st) {
 int g_attn_impl = 1;  // 1: multi-query MFMA kernel (default), 0: split VALU kernel
 
 // ------------------------------------------------------------------------------------------
-// flash attention forward (MFMA)
+// flash attention forward (MFMA 32x32x16)
 // ------------------------------------------------------------------------------------------
-constexpr int kBQ = 64;   // queries per workgroup (4 waves x 16)
-constexpr int kBK = 64;   // keys per tile
+// v3 (rocprof r3: the 16x16x32 v2 kernel ran at 5-7 % MFMA busy with 23-24 % LDS bank conflicts;
+// 16 queries per wave made every K / V byte read from LDS feed only 16 columns):
+//  * a wave owns 32 queries and computes S^T = K.Q^T with v_mfma_f32_32x32x16_bf16, so each K
+//    fragment read from LDS serves 32 queries and a lane holds 16 keys of ONE query per 32-key block;
+//  * the K rows of a block are read in a permuted order (A row R <- key kb(R)) so that lane half
+//    h's 16 scores are keys {8h..8h+7, 16+8h..16+8h+7}: exactly the B operand (P^T) of
+//    O^T += V^T.P^T for the two 16-key slices -- no lane exchange, no LDS round trip for P;
+//  * K and V tiles both live in the 256-byte-row image (b) (vimg_off): the 32x32x16 row reads of
+//    K and the ds_read_b64_tr_b16 reads of V^T are conflict-free on it;
+//  * online softmax with the running max folded into the MFMA accumulator (S' = K.Q^T - m is
+//    the chain's initial value) and a deferred rescale: the max moves (and O, l are rescaled) only
+//    when a tile's max exceeds it by more than kRescale (log2 units; P <= 2^kRescale, f32 sums);
+//  * 64-key tiles double-buffered in LDS, next tile's global loads issued behind the LDS stores
+//    (one barrier per tile).
+// Grid: 1-D, XCD-remapped so a (batch, head)'s query blocks share an XCD's L2 (K / V reuse);
+// within a head the query blocks run last-first (causal: the longest rows start first).
+constexpr int kFQ = 128;         // queries per workgroup (4 waves x 32)
+constexpr int kFK = 64;          // keys per tile
+constexpr float kRescale = 8.f;  // deferred-max threshold (log2 units)
 
-// v2 (rocprof: v1 spent 39-60% of LDS cycles in bank conflicts and exposed every key tile's global
-// load latency -- 82 us/layer for 84 queries x 1.1k keys):
-//  * K / V of the NEXT 64-key tile are loaded into registers while the current tile computes;
-//  * V is stored row-major in the dual-use image (b) of the guide (256-byte rows, chunk XOR) and
-//    read as the O^T A operand with ds_read_b64_tr_b16 (no 2-byte transposing stores);
-//  * the S^T tiles read K rows in an interleaved key order (A row n of tile t in a 32-key block =
-//    key 8(n>>2) + 4t + (n&3)) so each lane's probabilities are 8 consecutive keys: the two
-//    transposed V reads of a 32-lane half are then 8 rows apart (conflict-free).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+VWA_DEVICE f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256) void flash_attn_kernel(FlashAttnParams p) {
-  constexpr int NCH = D / 8;               // 16-byte chunks per K / V row
-  constexpr int NDS = D / 32;              // MFMA k-steps over head dim
-  constexpr int NDT = D / 16;              // 16-row d tiles of O^T
-  constexpr int LPT = kBK * NCH / 256;     // 16-byte chunks per thread per tile (K and V each)
-  __shared__ __attribute__((aligned(16))) u16 ks[kBK * D];
-  __shared__ __attribute__((aligned(16))) unsigned char vimg[kBK * 256];
+__global__ __launch_bounds__(256, 2) void flash_attn_kernel(FlashAttnParams p) {
+  constexpr int NCH = D / 8;            // 16-byte chunks per K / V row
+  constexpr int NDS = D / 16;           // QK k-steps over the head dim
+  constexpr int NDT = D / 32;           // 32-row d tiles of O^T
+  constexpr int LPT = kFK * NCH / 256;  // 16-byte chunks per thread per tile (K and V each)
+  constexpr int IMG = kFK * 256;        // bytes of one K or V tile image
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2][2][IMG];  // [stage][K, V]
 
-  const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int nqb = (p.Sq + kFQ - 1) / kFQ;
+  const int nwg = nqb * p.n_q_heads * p.B;
+  const int L = xcd_remap((int)blockIdx.x, nwg);
+  const int hb = L / nqb, qb = nqb - 1 - L % nqb;
+  const int h = hb % p.n_q_heads, b = hb / p.n_q_heads;
   const int kvh = h / (p.n_q_heads / p.n_kv_heads);
   const int lane = lane_id(), w = threadIdx.x >> 6;
-  const int ql = lane & 15, g = lane >> 4;
+  const int col = lane & 31, hf = lane >> 5;  // query column, lane half
   const int qoff = p.q_offsets ? p.q_offsets[b] : p.q_offset;
   const int Sk = p.k_lens ? p.k_lens[b] : p.Sk;
-  const int qi = qb * kBQ + w * 16 + ql;  // query index within the batch row
+  const int qw0 = qb * kFQ + w * 32;  // first query of this wave
+  const int qi = qw0 + col;
   const int qpos = qoff + qi;
   const float sl2 = p.scale * 1.4426950408889634f;
 
-  // Q^T fragments (B operand): Q[q][ds*32 + 8g + j], pre-scaled by scale*log2(e)
+  // Q^T fragments (B operand): lane (col, hf) holds Q[qi][16 ds + 8 hf + j], pre-scaled by scale*log2(e)
   bf16x8 qf[NDS];
   {
     const u16* qr = p.q + (int64_t)b * p.q_stride_b + (int64_t)qi * p.q_stride_s + (int64_t)h * p.q_stride_h;
 #pragma unroll
     for (int ds = 0; ds < NDS; ++ds) {
       float f[8];
-      if (qi < p.Sq) unpack8(*reinterpret_cast<const uint4*>(qr + ds * 32 + 8 * g), f);
+      if (qi < p.Sq) unpack8(ld128(qr + ds * 16 + 8 * hf), f);
       else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] = 0.f;
@@ -335,13 +354,16 @@ __global__ __launch_bounds__(256) void flash_attn_kernel(FlashAttnParams p) {
     }
   }
 
-  f32x4 oacc[NDT];
+  f32x16 oacc[NDT];
 #pragma unroll
-  for (int dt = 0; dt < NDT; ++dt) oacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) oacc[dt][i] = 0.f;
+  float m_run = 0.f, l_run = 0.f;
 
   int k_end = Sk;
-  if (CAUSAL) k_end = min(Sk, qoff + qb * kBQ + kBQ);
+  if (CAUSAL) k_end = min(Sk, qoff + qb * kFQ + kFQ);
+  const int nt = (k_end + kFK - 1) / kFK;
 
   uint4 kr[LPT], vr[LPT];
   auto load_tile = [&](int k0) {
@@ -355,107 +377,130 @@ __global__ __launch_bounds__(256) void flash_attn_kernel(FlashAttnParams p) {
         kr[i] = ld128(p.kv.k + off);
         vr[i] = ld128(p.kv.v + off);
       } else {
-        kr[i] = make_uint4(0, 0, 0, 0);
+        kr[i] = make_uint4(0, 0, 0, 0);  // V rows past the end must be finite (0 * NaN = NaN)
         vr[i] = make_uint4(0, 0, 0, 0);
       }
     }
   };
-  if (k_end > 0) load_tile(0);
-  for (int k0 = 0; k0 < k_end; k0 += kBK) {
-    // ---- registers -> LDS (K swizzled rows, V image (b)); then the next tile's loads go out
+  auto store_tile = [&](int stg) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int c = threadIdx.x + i * 256;
       const int r = c / NCH, ch = c % NCH;
-      *reinterpret_cast<uint4*>(&ks[r * D + ((ch ^ (r % NCH)) * 8)]) = kr[i];
-      *reinterpret_cast<uint4*>(vimg + vimg_off(r, ch)) = vr[i];
+      *reinterpret_cast<uint4*>(&lds[stg][0][vimg_off(r, ch)]) = kr[i];
+      *reinterpret_cast<uint4*>(&lds[stg][1][vimg_off(r, ch)]) = vr[i];
     }
-    __syncthreads();
-    if (k0 + kBK < k_end) load_tile(k0 + kBK);
+  };
 
-    // ---- S^T = K . Q^T: 2 blocks of 32 keys x 2 interleaved 16-row tiles
-    f32x4 s[2][2];
+  // A-row permutation of a 32-key block: MFMA row R = (i&3) + 8(i>>2) + 4hf of register i in lane
+  // half hf holds key (i&7) + 16(i>>3) + 8hf; the lane supplying A row `col` reads that key
+  const int a_hi = (col >> 2) & 1, a_r = (col & 3) + 4 * (col >> 3);
+  const int a_key = (a_r & 7) + 16 * (a_r >> 3) + 8 * a_hi;
+  // V^T transposed reads (ds_read_b64_tr_b16): 16-lane group grp covers d 16(grp&1).. of a 32-d
+  // tile and key half grp>>1; lane 4q+p names key row q, d columns 4p..4p+3
+  const int grp = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int v_key = 8 * (grp >> 1) + q4;
+  const int v_ch = 2 * (grp & 1) + (p4 >> 1), v_sub = 8 * (p4 & 1);
+
+  if (nt > 0) {
+    load_tile(0);
+    store_tile(0);
+    if (nt > 1) load_tile(kFK);
+  }
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int k0 = t * kFK;
+    const unsigned char* kimg = lds[t & 1][0];
+    const unsigned char* vimg = lds[t & 1][1];
+    // ---- S'^T = K.Q^T - m_run (the running max is the chain's initial value)
+    f32x16 s[2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        s[kk][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int r = 32 * kk + 8 * (ql >> 2) + 4 * t + (ql & 3);
+      for (int i = 0; i < 16; ++i) s[kk][i] = -m_run;
+      const int row = 32 * kk + a_key;
 #pragma unroll
-        for (int ds = 0; ds < NDS; ++ds) {
-          const int ch = ds * 4 + g;
-          const uint4 a = *reinterpret_cast<const uint4*>(&ks[r * D + ((ch ^ (r % NCH)) * 8)]);
-          s[kk][t] = mfma16(as_bf16x8(a), qf[ds], s[kk][t]);
-        }
+      for (int ds = 0; ds < NDS; ++ds) {
+        const uint4 a = *reinterpret_cast<const uint4*>(kimg + vimg_off(row, 2 * ds + hf));
+        s[kk] = mfma32(as_bf16x8(a), qf[ds], s[kk]);
       }
-    // ---- mask + online softmax (column = this lane's query); lane holds keys 32kk + 8g + 4t + i
+    }
+    // ---- mask (only tiles that reach past Sk or the wave's first causal row)
+    const bool edge = (k0 + kFK > Sk) || (CAUSAL && k0 + kFK - 1 > qoff + qw0);
+    if (edge) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int key = k0 + 32 * kk + (i & 7) + 16 * (i >> 3) + 8 * hf;
+          if (key >= Sk || (CAUSAL && key > qpos)) s[kk][i] = -INFINITY;
+        }
+    }
     float tmax = -INFINITY;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int kidx = k0 + 32 * kk + 8 * g + 4 * t + i;
-          const bool ok = (kidx < Sk) && (!CAUSAL || kidx <= qpos);
-          if (!ok) s[kk][t][i] = -INFINITY;
-          tmax = fmaxf(tmax, s[kk][t][i]);
-        }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 16, 64));
+      for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, s[kk][i]);
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float m_new = fmaxf(m_run, tmax);
-    const float alpha = (m_run == -INFINITY) ? 0.f : exp2f(m_run - m_new);
-    const bool any = (m_new != -INFINITY);
-    float psum = 0.f;
+    // ---- deferred rescale: the first tile sets the max; later ones move it only past kRescale
+    float delta = 0.f;
+    const bool move = (t == 0) || (tmax > kRescale);
+    if (__any(move)) {
+      delta = move ? tmax : 0.f;
+      const float alpha = __builtin_amdgcn_exp2f(-delta);
+      m_run += delta;
+      l_run *= alpha;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float e = (any && s[kk][t][i] != -INFINITY) ? exp2f(s[kk][t][i] - m_new) : 0.f;
-          s[kk][t][i] = e;
-          psum += e;
-        }
-    l_run = l_run * alpha + psum;
-    m_run = m_new;
-#pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) oacc[dt] *= alpha;
-
-    // ---- O^T += V^T . P^T per 32-key block: P^T[keys 8g..8g+7][query column]
-    const int q4 = ql >> 2, p4 = ql & 3;
+      for (int dt = 0; dt < NDT; ++dt) oacc[dt] *= alpha;
+    }
+    // ---- P^T = exp2(S' - delta), packed bf16 per 16-key slice; row sums in f32
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      float pf[8];
+      bf16x8 pb[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        pf[i] = s[kk][0][i];
-        pf[4 + i] = s[kk][1][i];
-      }
-      const bf16x8 pb = as_bf16x8(pack8(pf));
+      for (int ks = 0; ks < 2; ++ks) {
+        float pf[8];
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) {
-        const int ch = 2 * dt + (p4 >> 1), sub = 8 * (p4 & 1);
-        const uint2 lo = lds_tr16(vimg + vimg_off(32 * kk + 8 * g + q4, ch) + sub);
-        const uint2 hi = lds_tr16(vimg + vimg_off(32 * kk + 8 * g + 4 + q4, ch) + sub);
-        oacc[dt] = mfma16(as_bf16x8(make_uint4(lo.x, lo.y, hi.x, hi.y)), pb, oacc[dt]);
+        for (int j = 0; j < 8; ++j) {
+          pf[j] = __builtin_amdgcn_exp2f(s[kk][8 * ks + j] - delta);
+          l_run += pf[j];
+        }
+        pb[ks] = as_bf16x8(pack8(pf));
       }
+      // ---- O^T += V^T.P^T
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int kr0 = 32 * kk + 16 * ks + v_key;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const int ch = 4 * dt + v_ch;
+          const uint2 lo = lds_tr16(vimg + vimg_off(kr0, ch) + v_sub);
+          const uint2 hi = lds_tr16(vimg + vimg_off(kr0 + 4, ch) + v_sub);
+          oacc[dt] = mfma32(as_bf16x8(make_uint4(lo.x, lo.y, hi.x, hi.y)), pb[ks], oacc[dt]);
+        }
+      }
+    }
+    if (t + 1 < nt) {
+      store_tile((t + 1) & 1);
+      if (t + 2 < nt) load_tile(k0 + 2 * kFK);
     }
     __syncthreads();
   }
 
-  float l_tot = l_run + __shfl_xor(l_run, 16, 64);
-  l_tot += __shfl_xor(l_tot, 32, 64);
+  // ---- epilogue: lane (col, hf) holds O^T[d][qi] for d = 32dt + (i&3) + 8(i>>2) + 4hf
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   if (qi < p.Sq) {
     const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
     u16* orow = p.o + (int64_t)b * p.o_stride_b + (int64_t)qi * p.o_stride_s + (int64_t)h * p.o_stride_h;
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt) {
-      uint2 v;
-      v.x = pack2(oacc[dt][0] * inv, oacc[dt][1] * inv);
-      v.y = pack2(oacc[dt][2] * inv, oacc[dt][3] * inv);
-      *reinterpret_cast<uint2*>(orow + dt * 16 + 4 * g) = v;
-    }
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 v;
+        v.x = pack2(oacc[dt][4 * g] * inv, oacc[dt][4 * g + 1] * inv);
+        v.y = pack2(oacc[dt][4 * g + 2] * inv, oacc[dt][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * g + 4 * hf) = v;
+      }
   }
 }
 
@@ -478,7 +523,8 @@ extern "C" int vwa_decode_attention(const DecodeAttnParams* p, hipStream_t st) {
 
 extern "C" int vwa_flash_attention(const FlashAttnParams* p, hipStream_t st) {
   if (p->n_kv_heads <= 0 || p->n_q_heads % p->n_kv_heads) return -1;
-  dim3 grid((p->Sq + kBQ - 1) / kBQ, p->n_q_heads, p->B);
+  if (p->B <= 0 || p->Sq <= 0) return 0;
+  dim3 grid(((p->Sq + kFQ - 1) / kFQ) * p->n_q_heads * p->B);
   if (p->head_dim == 128) {
     if (p->causal) hipLaunchKernelGGL((flash_attn_kernel<128, true>), grid, dim3(256), 0, st, *p);
     else hipLaunchKernelGGL((flash_attn_kernel<128, false>), grid, dim3(256), 0, st, *p);

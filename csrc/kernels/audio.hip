@@ -4,11 +4,10 @@
 //  pcm16_to_f32 : int16 -> f32 (/32768) with optional linear resampling (ratio = in_rate/16000)
 //  log_mel      : Whisper log-mel spectrogram of a (30 s padded) window, computed on device:
 //                 reflect-padded frames (n_fft 400, hop 160) x periodic Hann -> DFT power for
-//                 201 bins (twiddles from a 400-entry cos table in LDS, exact integer phase
-//                 (k*n mod 400)) -> mel filterbank -> log10(max(.,1e-10)); the global max is
-//                 reduced with an order-preserving integer atomicMax; a second pass applies
-//                 max(x, max-8), (x+4)/4 and writes bf16 channels-last [frames][n_mels]
-//                 (the layout the conv1d stem consumes).
+//                 201 bins and the mel projection, both as f32 MFMA GEMMs (logmel_mfma_kernel)
+//                 -> log10(max(.,1e-10)); the global max is reduced with an order-preserving
+//                 integer atomicMax; a second pass applies max(x, max-8), (x+4)/4 and writes
+//                 bf16 channels-last [frames][n_mels] (the layout the conv1d stem consumes).
 #include "common.h"
 #include "vwa_kernels.h"
 
@@ -46,53 +45,119 @@ VWA_DEVICE int f2ord(float f) {
 }
 VWA_DEVICE float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
 
-// one workgroup per frame
-__global__ __launch_bounds__(256) void logmel_frame_kernel(const float* __restrict__ audio, int n_samples,
-                                                           int n_frames, const float* __restrict__ window,
-                                                           const float* __restrict__ cos_table,
-                                                           const float* __restrict__ mel_fb, int n_mels,
-                                                           float* __restrict__ mel_out, int* __restrict__ max_buf) {
-  __shared__ float xs[kNFFT];
-  __shared__ float ct[kNFFT];
-  __shared__ float pw[kBins + 3];
-  __shared__ float red[4];
-  const int f = blockIdx.x;
-  for (int n = threadIdx.x; n < kNFFT; n += 256) {
-    const int idx = reflect(f * kHop + n - kNFFT / 2, n_samples);
-    xs[n] = audio[idx] * window[n];
-    ct[n] = cos_table[n];
+// ---- log-mel power + mel projection on the f32 MFMA (v_mfma_f32_16x16x4_f32: exact f32 in,
+// f32 accumulate -- the spectrum keeps full precision).  One 512-thread workgroup per 16 frames:
+//   frames [16][400] (reflect-padded, Hann-windowed) -> LDS
+//   DFT:  C_cos / C_sin [16 frames][208 bins] = frames . basis   (13 bin tiles of 16, cos and sin
+//         tiles of a bin tile in the same wave: power = c^2 + s^2 in registers) -> LDS
+//   mel:  [16 frames][n_mels] = power . fb^T                     (one 16-mel tile per wave)
+//   log10(max(., 1e-10)) -> f32 scratch + the global max (order-preserving integer atomicMax).
+// The DFT basis (exact-phase cos / sin of 2 pi k n / 400, f64 on the host) and the filterbank are
+// pre-arranged in MFMA fragment order: [tile][k-step / 4][lane][4] -- one 16-byte load per lane
+// per 4 k-steps (ops.logmel_tables).  Replaces a per-bin O(N^2) VALU DFT (138 us per 30 s window,
+// 58 % LDS bank conflicts: profiles/r3_pmc_counters.md row 11).
+constexpr int kLmFrames = 16;        // frames per workgroup (MFMA rows)
+constexpr int kLmBinTiles = 13;      // 208 >= 201 bins
+constexpr int kLmXLd = 404;          // LDS row stride (floats) of the frame / power images:
+constexpr int kLmPLd = 212;          //   404, 212 = 20 (mod 64) -> conflict-free 16 rows x 4 k reads
+constexpr int kLmWaves = 8;
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+VWA_DEVICE f32x4 mfma_f32(float a, float b, const f32x4& c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+__global__ __launch_bounds__(kLmWaves * 64) void logmel_mfma_kernel(const float* __restrict__ audio, int n_samples,
+                                                                   int n_frames, const float* __restrict__ window,
+                                                                   const float4* __restrict__ basis,
+                                                                   const float4* __restrict__ fbf, int n_mels,
+                                                                   float* __restrict__ mel_out, int* __restrict__ max_buf) {
+  __shared__ float xs[kLmFrames * kLmXLd];
+  __shared__ float ps[kLmFrames * kLmPLd];
+  __shared__ float red[kLmWaves];
+  const int f0 = blockIdx.x * kLmFrames;
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int r = lane & 15, kq = lane >> 4;
+  for (int i = threadIdx.x; i < kLmFrames * kNFFT; i += kLmWaves * 64) {
+    const int fr = i / kNFFT, n = i % kNFFT;
+    const int f = f0 + fr;
+    xs[fr * kLmXLd + n] = f < n_frames ? audio[reflect(f * kHop + n - kNFFT / 2, n_samples)] * window[n] : 0.f;
   }
   __syncthreads();
-  for (int k = threadIdx.x; k < kBins; k += 256) {
-    float re = 0.f, im = 0.f;
-    int ph = 0;  // (k*n) mod 400
-    for (int n = 0; n < kNFFT; ++n) {
-      const float x = xs[n];
-      re += x * ct[ph];
-      // sin(2*pi*ph/400) = cos(2*pi*(ph - 100)/400)
-      int ps = ph - 100;
-      if (ps < 0) ps += kNFFT;
-      im -= x * ct[ps];
-      ph += k;
-      if (ph >= kNFFT) ph -= kNFFT;
+
+  // ---- DFT: wave w takes bin tiles w and w + 8 (< 13)
+  {
+    const int nbt = (w + kLmWaves < kLmBinTiles) ? 2 : 1;
+    f32x4 ac[2], as[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      ac[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      as[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    pw[k] = re * re + im * im;
+    const float* xr = xs + r * kLmXLd + kq;
+    for (int s4 = 0; s4 < kNFFT / 16; ++s4) {
+      float4 bc[2], bs[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        if (t < nbt) {
+          const int bt = w + t * kLmWaves;
+          bc[t] = basis[((2 * bt) * (kNFFT / 16) + s4) * 64 + lane];
+          bs[t] = basis[((2 * bt + 1) * (kNFFT / 16) + s4) * 64 + lane];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = xr[(4 * s4 + j) * 4];
+        const float* c0 = reinterpret_cast<const float*>(&bc[0]);
+        const float* s0 = reinterpret_cast<const float*>(&bs[0]);
+        ac[0] = mfma_f32(a, c0[j], ac[0]);
+        as[0] = mfma_f32(a, s0[j], as[0]);
+        if (nbt > 1) {
+          const float* c1 = reinterpret_cast<const float*>(&bc[1]);
+          const float* s1 = reinterpret_cast<const float*>(&bs[1]);
+          ac[1] = mfma_f32(a, c1[j], ac[1]);
+          as[1] = mfma_f32(a, s1[j], as[1]);
+        }
+      }
+    }
+    // power -> LDS: lane holds C[frame 4 kq + i][bin 16 bt + r]
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (t >= nbt) break;
+      const int bt = w + t * kLmWaves;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ps[(4 * kq + i) * kLmPLd + 16 * bt + r] = ac[t][i] * ac[t][i] + as[t][i] * as[t][i];
+    }
   }
   __syncthreads();
+
+  // ---- mel projection: wave w takes mel tile w (n_mels <= 128)
   float lmax = -INFINITY;
-  for (int m = threadIdx.x; m < n_mels; m += 256) {
-    const float* fb = mel_fb + (int64_t)m * kBins;
-    float acc = 0.f;
-    for (int k = 0; k < kBins; ++k) acc += fb[k] * pw[k];
-    const float lv = log10f(fmaxf(acc, 1e-10f));
-    mel_out[(int64_t)f * n_mels + m] = lv;
-    lmax = fmaxf(lmax, lv);
+  if (16 * w < n_mels) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float* pr = ps + r * kLmPLd + kq;
+    for (int s4 = 0; s4 < kLmBinTiles; ++s4) {  // 52 k-steps of 4 bins
+      const float4 b = fbf[(w * kLmBinTiles + s4) * 64 + lane];
+      const float* bb = reinterpret_cast<const float*>(&b);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc = mfma_f32(pr[(4 * s4 + j) * 4], bb[j], acc);
+    }
+    const int m = 16 * w + r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = f0 + 4 * kq + i;
+      if (f < n_frames && m < n_mels) {
+        const float lv = log10f(fmaxf(acc[i], 1e-10f));
+        mel_out[(int64_t)f * n_mels + m] = lv;
+        lmax = fmaxf(lmax, lv);
+      }
+    }
   }
   lmax = wave_max(lmax);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = lmax;
+  if (lane == 0) red[w] = lmax;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    float mx = red[0];
+#pragma unroll
+    for (int i = 1; i < kLmWaves; ++i) mx = fmaxf(mx, red[i]);
     atomicMax(max_buf, f2ord(mx));
   }
 }
@@ -114,15 +179,16 @@ extern "C" int vwa_pcm16_to_f32(const int16_t* pcm, float* out, int n_in, int n_
   return (int)hipGetLastError();
 }
 
-extern "C" int vwa_log_mel(const float* audio, int n_samples, int n_frames, const float* window, const float* dft_cos,
-                           const float* dft_sin, const float* mel_fb, int n_mels, float* mel_out, float* max_buf,
-                           uint16_t* out_bf16, int ld_out, hipStream_t st) {
-  (void)dft_sin;
+extern "C" int vwa_log_mel(const float* audio, int n_samples, int n_frames, const float* window, const float* basis,
+                           const float* fb_frag, int n_mels, float* mel_out, float* max_buf, uint16_t* out_bf16,
+                           int ld_out, hipStream_t st) {
+  if (n_mels < 1 || n_mels > 16 * kLmWaves || n_frames < 1 || n_samples <= kNFFT / 2) return -1;
   int* mb = reinterpret_cast<int*>(max_buf);
   // order-preserving encoding of -inf is a large negative int; reset every call (graph-safe memset node)
   hipMemsetAsync(mb, 0x80, sizeof(int), st);
-  hipLaunchKernelGGL(logmel_frame_kernel, dim3(n_frames), dim3(256), 0, st, audio, n_samples, n_frames, window, dft_cos,
-                     mel_fb, n_mels, mel_out, mb);
+  hipLaunchKernelGGL(logmel_mfma_kernel, dim3((n_frames + kLmFrames - 1) / kLmFrames), dim3(kLmWaves * 64), 0, st,
+                     audio, n_samples, n_frames, window, reinterpret_cast<const float4*>(basis),
+                     reinterpret_cast<const float4*>(fb_frag), n_mels, mel_out, mb);
   const int n = n_frames * n_mels;
   hipLaunchKernelGGL(logmel_norm_kernel, dim3((n + 255) / 256), dim3(256), 0, st, mel_out, mb, out_bf16, n, ld_out,
                      n_mels);

@@ -29,7 +29,12 @@
 //
 // Epilogues (fused, after the optional per-row RMSNorm scale rstd -- gammas are folded into W):
 //   0 store (+bias; bf16 or f32 out)   1 residual add (+bias)   2 SwiGLU over gate/up tiles
-//   interleaved per 16 rows (ops.interleave_gate_up)   3 GELU (+bias)
+//   interleaved per 16 rows (ops.interleave_gate_up)   3 GELU (+bias)   4 GELU (+bias) then a
+//   residual add (the Whisper conv stem's positional embedding: y = gelu(conv + b) + pos)
+//
+// Implicit-GEMM convolution (K3, ops.conv1d_gelu): X rows are ldx apart and K long, so a k=3
+// conv over a zero-padded channels-last buffer is X row t = padded rows t*stride .. t*stride+2
+// (ldx = stride*Cin, K = 3*Cin) -- the A tiles are staged through the same LDS-DMA pipeline.
 #include "common.h"
 #include "vwa_kernels.h"
 
@@ -37,7 +42,9 @@ using namespace vwa;
 
 namespace {
 
-enum Epi { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_GELU = 3 };
+enum Epi { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_GELU = 3, EPI_GELU_RESID = 4 };
+template <int EPI> constexpr bool kResid = EPI == EPI_RESID || EPI == EPI_GELU_RESID;
+template <int EPI> constexpr bool kGelu = EPI == EPI_GELU || EPI == EPI_GELU_RESID;
 
 constexpr int BKG = 128;
 
@@ -173,7 +180,7 @@ VWA_DEVICE float bias_at(const GemmParams& p, int n) { return p.bias ? bf2f(p.bi
 
 template <int EPI>
 VWA_DEVICE void store_out(const GemmParams& p, int m, int n, float v) {
-  if constexpr (EPI == EPI_RESID) v += bf2f(p.R[(size_t)m * p.ldr + n]);
+  if constexpr (kResid<EPI>) v += bf2f(p.R[(size_t)m * p.ldr + n]);
   if (p.y_f32)
     reinterpret_cast<float*>(p.Y)[(size_t)m * p.ldy + n] = v;
   else
@@ -186,7 +193,13 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
   constexpr int FM = C::FM, FN = C::FN;
   const int mb = (p.M + C::BM - 1) / C::BM, nb = (p.N + C::BN - 1) / C::BN;
   const int tiles = mb * nb;
-  const int split = blockIdx.x / tiles;  // split-K slice (blocks of one slice are contiguous)
+  const int split = blockIdx.x / tiles % p.splits;  // split-K slice (blocks of one slice are contiguous)
+  if (p.nbatch > 1) {  // batch z = blockIdx.x / (tiles * splits), splits == 1 (vwa_gemm)
+    const int z = blockIdx.x / tiles;
+    p.X += (size_t)z * p.bsx;
+    p.Y = reinterpret_cast<char*>(p.Y) + (size_t)z * p.bsy * (p.y_f32 ? 4 : 2);
+    if (p.R) p.R += (size_t)z * p.bsr;
+  }
   // XCD-aware: logical tile order is column-block major, so consecutive logical tiles (same XCD)
   // share the column block's weight tile in L2
   const int lt = xcd_remap((int)(blockIdx.x % tiles), tiles);
@@ -203,7 +216,8 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
   // barriers with counted vmcnt (a __syncthreads would drain the in-flight DMA)
   constexpr int SPG = F8 ? 1 : 2;  // stages per k-group
   const int h0 = SPG * kg0, nh = SPG * (kg1 - kg0);
-  const __amdgpu_buffer_rsrc_t rx = rsrc(p.X, (size_t)p.M * p.ldx * (F8 ? 1 : 2));
+  // X extent: the last row starts at (M-1)*ldx and is K long (rows may overlap: conv views)
+  const __amdgpu_buffer_rsrc_t rx = rsrc(p.X, ((size_t)(p.M - 1) * p.ldx + p.K) * (F8 ? 1 : 2));
   const __amdgpu_buffer_rsrc_t rw = rsrc(p.W, (size_t)p.N * p.K * (F8 ? 1 : 2));
   if (nh > 0) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0, lds);
   if (nh > 1) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + 1, lds + C::STAGE);
@@ -277,7 +291,8 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
           const int n = col0 + j * 16;
           if (n >= p.N) continue;
           float v = acc[i][j][r] * rsv[i][r] * cz[j] + bz[j];
-          if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
+          if constexpr (kGelu<EPI>) v = gelu_erf(v);
+          if constexpr (kResid<EPI>) v += bf2f(p.R[(size_t)m * p.ldr + n]);
           reinterpret_cast<float*>(p.Y)[(size_t)m * p.ldy + n] = v;
         }
       }
@@ -304,7 +319,7 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           float v = acc[i][j][r] * rsv[i][r] * cz[j] + bz[j];
-          if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
+          if constexpr (kGelu<EPI>) v = gelu_erf(v);
           *reinterpret_cast<u16*>(wl + rl * RS + (j * 16 + (l & 15)) * 2) = f2bf(v);
         }
       }
@@ -319,7 +334,7 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
     const int m = bm + wm * ROWS + row, n = cbase + ch * 8;
     if (m >= p.M || n >= ncols) continue;
     uint4 v = *reinterpret_cast<const uint4*>(wl + row * RS + ch * 16);
-    if constexpr (EPI == EPI_RESID) {
+    if constexpr (kResid<EPI>) {
       float a[8], b[8];
       unpack8(v, a);
       unpack8(*reinterpret_cast<const uint4*>(p.R + (size_t)m * p.ldr + n), b);
@@ -356,7 +371,7 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmParams p) {
     float v = 0.f;
     for (int z = 0; z < p.splits; ++z) v += p.ws[z * slab + (size_t)m * p.N + c];
     v = v * rs * (p.sw ? p.sw[c] : 1.f) + bias_at(p, c);
-    if constexpr (EPI == EPI_GELU) v = gelu_erf(v);
+    if constexpr (kGelu<EPI>) v = gelu_erf(v);
     store_out<EPI>(p, m, c, v);
   }
 }
@@ -381,7 +396,7 @@ __global__ __launch_bounds__(256) void row_rstd_kernel(const u16* __restrict__ x
 template <class C, int EPI>
 int launch_cfg(const GemmParams& p, hipStream_t st) {
   const int tiles = ((p.M + C::BM - 1) / C::BM) * ((p.N + C::BN - 1) / C::BN);
-  const dim3 grid(tiles * p.splits);
+  const dim3 grid(tiles * p.splits * (p.nbatch > 1 ? p.nbatch : 1));
   if (p.sw)
     hipLaunchKernelGGL((gemm_kernel<C, EPI, true, true>), grid, dim3(C::THREADS), C::LDS, st, p);
   else if (p.w_tiled)
@@ -425,11 +440,13 @@ extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
   p.kg_per_split = (KG + p.splits - 1) / p.splits;
   p.splits = (KG + p.kg_per_split - 1) / p.kg_per_split;  // no empty slice
   if (p.splits > 1 && !p.ws) return -13;
+  if (p.nbatch > 1 && p.splits > 1) return -15;  // batched launches take no split-K
   switch (epi) {
     case EPI_STORE: return launch_epi<EPI_STORE>(p, st);
     case EPI_RESID: return launch_epi<EPI_RESID>(p, st);
     case EPI_SWIGLU: return launch_epi<EPI_SWIGLU>(p, st);
     case EPI_GELU: return launch_epi<EPI_GELU>(p, st);
+    case EPI_GELU_RESID: return launch_epi<EPI_GELU_RESID>(p, st);
     default: return -3;
   }
 }

@@ -140,6 +140,11 @@ struct GemmParams {
   // W8A8 (sw != null): X is OCP e4m3 bytes [M, ldx] with per-row scales sx, W the fp8 tiled layout
   // (ops.tile_weight_fp8) with per-row scales sw
   const float* sx; const float* sw;
+  // batched launch (nbatch > 1, no split-K): batch z reads X + z*bsx, writes Y + z*bsy and reads
+  // R + z*bsr (element strides; bsr 0 = one residual for every batch, e.g. a positional table).
+  // X rows may overlap (ldx < K: the Whisper conv stem as an implicit GEMM, row t = the 3 input
+  // rows t*stride-1 .. t*stride+1 of a zero-padded channels-last buffer)
+  int nbatch; int64_t bsx, bsy, bsr;
 };
 
 struct FlashAttnParams {
@@ -193,11 +198,11 @@ int vwa_sample_partial(const float* logits, int ld, int rows, int V, int v_off, 
 int vwa_sample_final(const float* part_val, const int* part_idx, int n_chunks, int n_src, int64_t src_stride,
                      int* out_tokens, int* step, int rows, const int64_t* fail_word, hipStream_t st);
 int vwa_pcm16_to_f32(const int16_t* pcm, float* out, int n_in, int n_out, float ratio, hipStream_t st);
-int vwa_log_mel(const float* audio, int n_samples, int n_frames, const float* window, const float* dft_cos,
-                const float* dft_sin, const float* mel_fb, int n_mels, float* mel_out, float* max_buf,
-                uint16_t* out_bf16, int ld_out, hipStream_t st);
-int vwa_conv1d_gelu_pos(const uint16_t* x, const uint16_t* w, const uint16_t* b, const uint16_t* pos, uint16_t* y,
-                        int B, int Cin, int Tin, int Cout, int Tout, int stride, hipStream_t st);
+// basis: DFT cos/sin fragments [26 tiles][25][64][4] f32, fb_frag: mel filterbank fragments
+// [n_mels/16][13][64][4] f32 (ops.logmel_tables)
+int vwa_log_mel(const float* audio, int n_samples, int n_frames, const float* window, const float* basis,
+                const float* fb_frag, int n_mels, float* mel_out, float* max_buf, uint16_t* out_bf16, int ld_out,
+                hipStream_t st);
 int vwa_attention_split_tokens();
 int vwa_decode_advance(int* tokens, int* positions, int* ctx_lens, int64_t* slots, const int* sampled,
                        int* out, int* counter, int max_out, int base_block, int block_size, hipStream_t st);

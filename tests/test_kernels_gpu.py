@@ -316,6 +316,39 @@ def test_flash_attention_causal_paged_prefix():
     close(out, exp, 2e-2)
 
 
+@pytest.mark.parametrize("B,S,H,D", [(2, 1500, 6, 64), (1, 1500, 20, 64), (1, 333, 4, 128)])
+def test_flash_attention_encoder_shapes(B, S, H, D):
+    # Whisper encoder shapes (tiny / large-v3) and a ragged 128-dim one, strided q / k / v views of
+    # one fused QKV buffer (the encoder's layout)
+    qkv = rnd(B, S, 3, H, D)
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    table = torch.arange(B, dtype=torch.int32, device=DEV)[:, None]
+    out = ops.flash_attention(q, ops.KVLayout.contiguous(k, v, table), Sk=S, n_kv_heads=H, causal=False,
+                              scale=D ** -0.5)
+    exp = torch.nn.functional.scaled_dot_product_attention(q.float().transpose(1, 2), k.float().transpose(1, 2),
+                                                           v.float().transpose(1, 2)).transpose(1, 2)
+    close(out, exp.cpu(), 2e-2)
+
+
+def test_flash_attention_deferred_rescale():
+    # scores whose running max climbs by more than the deferred-rescale threshold across tiles (keys
+    # scaled up along the sequence) and very negative / very positive rows: the rare rescale branch
+    B, S, H, D = 1, 700, 2, 64
+    q = rnd(B, S, H, D) * 4
+    k = rnd(B, S, H, D) * torch.linspace(0.2, 3.0, S, device=DEV).to(BF)[None, :, None, None]
+    v = rnd(B, S, H, D)
+    q[:, :50] *= 2
+    q[:, 50:100] *= -2
+    table = torch.arange(B, dtype=torch.int32, device=DEV)[:, None]
+    for causal in (False, True):
+        out = ops.flash_attention(q, ops.KVLayout.contiguous(k, v, table), Sk=S, n_kv_heads=H, causal=causal,
+                                  scale=D ** -0.5)
+        exp = torch.nn.functional.scaled_dot_product_attention(q.float().transpose(1, 2), k.float().transpose(1, 2),
+                                                               v.float().transpose(1, 2),
+                                                               is_causal=causal).transpose(1, 2)
+        close(out, exp.cpu(), 3e-2)
+
+
 def test_flash_attention_encoder_contiguous():
     B, S, H, D = 2, 150, 6, 64
     q, k, v = rnd(B, S, H, D), rnd(B, S, H, D), rnd(B, S, H, D)
@@ -375,10 +408,9 @@ def test_audio_frontend_and_conv():
     audio = torch.zeros(n_frames * 160, device=DEV)
     audio[: f.numel()] = f
     window = torch.hann_window(400, periodic=True, device=DEV)
-    cos_table = torch.cos(torch.arange(400, dtype=torch.float64) * 2 * math.pi / 400).float().to(DEV)
     fb = ref.mel_filterbank(n_mels=80).to(DEV)
     out = torch.empty(n_frames, 80, dtype=BF, device=DEV)
-    ops.log_mel(audio, n_frames=n_frames, window=window, cos_table=cos_table, mel_fb=fb, out=out)
+    ops.log_mel(audio, n_frames=n_frames, window=window, mel_fb=fb, out=out)
     exp = ref.log_mel(audio.cpu(), n_frames=n_frames, window=window.cpu(), mel_fb=fb.cpu(),
                       out=torch.empty(n_frames, 80, dtype=BF))
     close(out, exp, 3e-2)
@@ -391,6 +423,38 @@ def test_audio_frontend_and_conv():
     pos = rnd(1500, 384)
     z = ops.conv1d_gelu(y, rnd(384, 3 * 384, scale=0.02), b, stride=2, pos=pos)
     assert z.shape == (1, 1500, 384)
+
+
+def test_log_mel_mfma_128_noise():
+    # large-v3 front end (128 mels) on broadband noise + a tone: every bin and mel tile carries energy
+    n_frames = 3000
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn(n_frames * 160, generator=g) * 0.05
+    a[:32000] += torch.sin(torch.arange(32000) * 2 * math.pi * 1000 / 16000) * 0.3
+    audio = a.to(DEV)
+    window = torch.hann_window(400, periodic=True, device=DEV)
+    fb = ref.mel_filterbank(n_mels=128).to(DEV)
+    out = torch.empty(n_frames, 128, dtype=BF, device=DEV)
+    ops.log_mel(audio, n_frames=n_frames, window=window, mel_fb=fb, out=out)
+    exp = ref.log_mel(audio.cpu(), n_frames=n_frames, window=window.cpu(), mel_fb=fb.cpu(),
+                      out=torch.empty(n_frames, 128, dtype=torch.float32))
+    assert (out.float().cpu() - exp).abs().max().item() < 1.2e-2  # bf16 rounding of values in [-1.5, 1.5]
+
+
+@pytest.mark.parametrize("Cin,Cout,stride,B", [(128, 384, 1, 2), (384, 384, 2, 3), (1280, 1280, 2, 1)])
+def test_conv_stem_implicit_gemm(Cin, Cout, stride, B):
+    # the stem's padded-buffer path (no copy) against F.conv1d: batches are separate zero-padded slabs
+    Tin = 3000
+    _, xv = ops.padded_rows(B, Tin, Cin, dtype=BF, device=DEV)
+    xv.copy_(rnd(B, Tin, Cin))
+    w = rnd(Cout, 3 * Cin, scale=0.03)
+    b = rnd(Cout, scale=0.1)
+    Tout = (Tin - 1) // stride + 1
+    pos = rnd(Tout, Cout) if stride == 2 else None
+    y = ops.conv1d_gelu(xv, w, b, stride=stride, pos=pos, padded=True)
+    exp = ref.conv1d_gelu(xv.cpu(), w.cpu(), b.cpu(), stride=stride, pos=None if pos is None else pos.cpu(),
+                          out=torch.empty(B, Tout, Cout, dtype=torch.float32))
+    close(y, exp, 3e-2)
 
 
 # ----------------------------------------------------------------------------- fp8 (W8A8)

@@ -296,7 +296,7 @@ class AsrEngine:
         slots = [self.free_slots.pop() for _ in range(B)]
         retry = False
         try:
-            mel = torch.stack([m.log_mel(a) for a in audios])
+            mel = m.mel_batch(audios)
             enc = m.encode(mel)
             self.set_cross_batch(slots, enc)
             t_enc = time.perf_counter()

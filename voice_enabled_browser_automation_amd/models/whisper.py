@@ -17,7 +17,7 @@ from __future__ import annotations
 import math
 import weakref
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import List, Optional, Sequence
 
 import torch
 
@@ -120,8 +120,12 @@ class WhisperModel:
         self.fold_decoder_norms()
         # front-end constants
         self.window = torch.hann_window(400, periodic=True, device=self.device)
-        self.cos_table = torch.cos(torch.arange(400, dtype=torch.float64) * 2 * math.pi / 400).float().to(self.device)
         self.mel_fb = ref.mel_filterbank(n_mels=cfg.n_mels).to(self.device)
+        # conv stem on the GEMM path: mel channels zero-padded to a 128 multiple (3*C % 128 == 0),
+        # zero-padded row buffers per batch size (conv padding = the buffers' pad rows)
+        self.mel_ch = ops.conv_channels(cfg.n_mels)
+        self.conv1_wp = ops.pad_conv_weight(self.conv1_w, self.mel_ch)
+        self._stem: dict = {}
 
     def _load(self, w) -> None:
         """HF WhisperForConditionalGeneration names (safetensors, runtime.weights.LazySafetensors)."""
@@ -186,29 +190,52 @@ class WhisperModel:
         self.f_lm = fold(self.lm_head, None, self.dec_ln_w, self.dec_ln_b)
 
     # ------------------------------------------------------------------ encoder
-    def log_mel(self, audio: torch.Tensor, n_frames: int = 3000) -> torch.Tensor:
-        """audio: f32 samples (<= 30 s). Returns [n_frames, n_mels] bf16 (channels-last)."""
+    def log_mel(self, audio: torch.Tensor, n_frames: int = 3000, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """audio: f32 samples (<= 30 s). Returns [n_frames, n_mels] bf16 (channels-last); ``out``: a
+        [n_frames, n_mels] view to write (e.g. a row of mel_batch(), whose rows are mel_ch apart)."""
         pad = torch.zeros(n_frames * 160, dtype=torch.float32, device=self.device)
         n = min(audio.numel(), pad.numel())
         pad[:n] = audio[:n]
-        out = torch.empty(n_frames, self.cfg.n_mels, dtype=self.dtype, device=self.device)
-        return ops.log_mel(pad, n_frames=n_frames, window=self.window, cos_table=self.cos_table, mel_fb=self.mel_fb,
+        if out is None:
+            out = torch.empty(n_frames, self.cfg.n_mels, dtype=self.dtype, device=self.device)
+        return ops.log_mel(pad, n_frames=n_frames, window=self.window, mel_fb=self.mel_fb,
                            out=out)
 
+    def _stem_buffers(self, B: int, T: int):
+        """(mel view [B, T, mel_ch], conv1-output view [B, T, d]) of zero-padded row buffers, cached
+        per (B, T); their pad rows / channels are never written, so they stay zero."""
+        key = (B, T)
+        if key not in self._stem:
+            _, mv = ops.padded_rows(B, T, self.mel_ch, dtype=self.dtype, device=self.device)
+            _, cv = ops.padded_rows(B, T, self.cfg.d_model, dtype=self.dtype, device=self.device)
+            self._stem[key] = (mv, cv)
+        return self._stem[key]
+
+    def mel_batch(self, audios: Sequence[torch.Tensor], n_frames: int = 3000) -> torch.Tensor:
+        """Log-mel of every utterance straight into the conv stem's padded input buffer; returns
+        the [B, n_frames, mel_ch] view encode() takes without a copy."""
+        mv, _ = self._stem_buffers(len(audios), n_frames)
+        for i, a in enumerate(audios):
+            self.log_mel(a, n_frames, out=mv[i, :, : self.cfg.n_mels])
+        return mv
+
     def encode(self, mel: torch.Tensor) -> torch.Tensor:
-        """mel [B, 3000, n_mels] -> encoder states [B, 1500, d]."""
+        """mel [B, 3000, n_mels] (or mel_batch()'s [B, 3000, mel_ch] view) -> encoder states [B, 1500, d]."""
         cfg = self.cfg
-        B = mel.shape[0]
-        x = ops.conv1d_gelu(mel, self.conv1_w, self.conv1_b, stride=1)
-        x = ops.conv1d_gelu(x, self.conv2_w, self.conv2_b, stride=2, pos=self.pos_enc)
+        B, T = mel.shape[0], mel.shape[1]
+        mv, cv = self._stem_buffers(B, T)
+        if mel.data_ptr() != mv.data_ptr() or mel.shape != mv.shape:
+            mv[:, :, : cfg.n_mels] = mel[:, :, : cfg.n_mels]
+        x = ops.conv1d_gelu(mv, self.conv1_wp, self.conv1_b, stride=1, out=cv, padded=True)
+        x = ops.conv1d_gelu(x, self.conv2_w, self.conv2_b, stride=2, pos=self.pos_enc, padded=True)
         T, d = x.shape[1], x.shape[2]
         x = x.reshape(B * T, d)
         table = torch.arange(B, dtype=torch.int32, device=self.device)[:, None]
         for L in self.enc:
             h = ops.layernorm(x, L.ln1_w, L.ln1_b, eps=cfg.ln_eps)
             qkv = ops.linear(h, L.qkv, L.qkv_b).view(B, T, 3, self.H, self.hd)
+            # strided q / k / v views: the flash kernel addresses rows by stride (no copies)
             q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
-            q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
             att = ops.flash_attention(q, ops.KVLayout.contiguous(k, v, table), Sk=T, n_kv_heads=self.H, causal=False,
                                       scale=self.hd ** -0.5)
             x = ops.linear(att.view(B * T, d), L.o, L.o_b, residual=x)

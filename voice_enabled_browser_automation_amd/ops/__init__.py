@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 
@@ -828,9 +828,42 @@ def pcm16_to_f32(pcm: torch.Tensor, in_rate: int = 16000, out: Optional[torch.Te
     return out
 
 
-def log_mel(audio: torch.Tensor, *, n_frames: int, window: torch.Tensor, cos_table: torch.Tensor,
-            mel_fb: torch.Tensor, out: torch.Tensor, scratch: Optional[torch.Tensor] = None,
-            max_buf: Optional[torch.Tensor] = None) -> torch.Tensor:
+_LOGMEL_TABLES: dict = {}
+
+
+def logmel_tables(mel_fb: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """MFMA fragment-ordered constants of the log-mel kernel (audio.hip logmel_mfma_kernel):
+    the DFT basis [26 tiles = 13 bin tiles x (cos, sin)][25][64 lanes][4] with
+    basis[T][s4][l][j] = cos|sin(2 pi n b / 400), n = 4 (4 s4 + j) + (l >> 4), b = 16 (T >> 1) + (l & 15)
+    (0 for b > 200; exact f64 phase), and the filterbank [n_mels / 16][13][64][4] with
+    fbf[t][s4][l][j] = fb[16 t + (l & 15)][4 (4 s4 + j) + (l >> 4)].  Cached per filterbank tensor."""
+    key = (mel_fb.data_ptr(), tuple(mel_fb.shape), str(mel_fb.device))
+    hit = _LOGMEL_TABLES.get(key)
+    if hit is not None:
+        return hit[1], hit[2]
+    lane = torch.arange(64, dtype=torch.float64)
+    ks = (4 * torch.arange(25, dtype=torch.float64)[:, None] + torch.arange(4, dtype=torch.float64)[None, :])  # [25, 4]
+    n = 4 * ks[:, None, :] + torch.floor(lane / 16)[None, :, None]  # [25, 64, 4]
+    tiles = []
+    for bt in range(13):
+        b = 16 * bt + (lane % 16)[None, :, None]
+        ph = 2 * math.pi * torch.remainder(n * b, 400) / 400
+        ok = (b <= 200).to(torch.float64)
+        tiles += [torch.cos(ph) * ok, torch.sin(ph) * ok]
+    basis = torch.stack(tiles).float().contiguous().to(mel_fb.device)
+    n_mels = mel_fb.shape[0]
+    mt = (n_mels + 15) // 16
+    fb = torch.zeros(mt * 16, 208, dtype=torch.float32)
+    fb[:n_mels, :201] = mel_fb.detach().float().cpu()
+    l = torch.arange(64)
+    kidx = (4 * (4 * torch.arange(13)[:, None, None] + torch.arange(4)[None, None, :]) + (l // 16)[None, :, None])
+    fbf = torch.stack([fb[16 * t + (l % 16)[None, :, None], kidx] for t in range(mt)]).contiguous().to(mel_fb.device)
+    _LOGMEL_TABLES[key] = (mel_fb, basis, fbf)  # (keeps mel_fb alive: its data_ptr cannot be reused)
+    return basis, fbf
+
+
+def log_mel(audio: torch.Tensor, *, n_frames: int, window: torch.Tensor, mel_fb: torch.Tensor, out: torch.Tensor,
+            scratch: Optional[torch.Tensor] = None, max_buf: Optional[torch.Tensor] = None) -> torch.Tensor:
     """audio: padded f32 samples (n_frames*160 for Whisper) -> out bf16 [n_frames, n_mels]."""
     if not _gpu(audio):
         return ref.log_mel(audio, n_frames=n_frames, window=window, mel_fb=mel_fb, out=out)
@@ -839,19 +872,54 @@ def log_mel(audio: torch.Tensor, *, n_frames: int, window: torch.Tensor, cos_tab
         scratch = torch.empty((n_frames * n_mels,), dtype=torch.float32, device=audio.device)
     if max_buf is None:
         max_buf = torch.empty((1,), dtype=torch.float32, device=audio.device)
-    ext().log_mel(audio, n_frames, window, cos_table, mel_fb, scratch, max_buf, out)
+    basis, fbf = logmel_tables(mel_fb)
+    ext().log_mel(audio, n_frames, window, basis, fbf, n_mels, scratch, max_buf, out)
     return out
 
 
+def padded_rows(B: int, T: int, C: int, *, dtype, device) -> Tuple[torch.Tensor, torch.Tensor]:
+    """A zero [B, T + 2, C] buffer and its [B, T, C] data view (rows 1..T): the input layout of
+    conv1d_gelu (one zero row in front of and behind every batch's rows = the conv's padding)."""
+    buf = torch.zeros(B, T + 2, C, dtype=dtype, device=device)
+    return buf, buf[:, 1 : T + 1]
+
+
+def conv_channels(cin: int) -> int:
+    """Input channels of the GEMM conv path: 3*C must be a multiple of the GEMM's 128-deep k-group."""
+    return (cin + 127) // 128 * 128
+
+
+def pad_conv_weight(w: torch.Tensor, cp: int) -> torch.Tensor:
+    """[Cout, 3*Cin] ((kk, ci) order) -> [Cout, 3*cp] with zero columns for the padded channels."""
+    cout, k3 = w.shape
+    cin = k3 // 3
+    if cin == cp:
+        return w.contiguous()
+    wp = torch.zeros(cout, 3, cp, dtype=w.dtype, device=w.device)
+    wp[:, :, :cin] = w.view(cout, 3, cin)
+    return wp.view(cout, 3 * cp)
+
+
 def conv1d_gelu(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], *, stride: int,
-                pos: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """x [B, Tin, Cin] channels-last, w [Cout, 3*Cin] ([co][kk][ci]) -> [B, Tout, Cout]."""
+                pos: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+                padded: bool = False) -> torch.Tensor:
+    """x [B, Tin, Cin] channels-last, w [Cout, 3*Cin] ([co][kk][ci]) -> [B, Tout, Cout] =
+    gelu(conv1d(x, k=3, pad=1, stride) + b) (+ pos[:Tout]).
+
+    GPU: a batched implicit GEMM on the tiled MFMA GEMM (gemm.hip).  ``padded=True``: x is the
+    data view of a padded_rows buffer with 3*Cin % 128 == 0 (the model's stem buffers: no copy);
+    otherwise x is copied into one (channels zero-padded to conv_channels(Cin))."""
     B, Tin, Cin = x.shape
     Tout = (Tin + 2 - 3) // stride + 1
     if out is None:
         out = torch.empty((B, Tout, w.shape[0]), dtype=x.dtype, device=x.device)
     if not _gpu(x):
         return ref.conv1d_gelu(x, w, b, stride=stride, pos=pos, out=out)
+    if not padded:
+        cp = conv_channels(Cin)
+        _, xv = padded_rows(B, Tin, cp, dtype=x.dtype, device=x.device)
+        xv[:, :, :Cin] = x
+        x, w = xv, pad_conv_weight(w, cp)
     ext().conv1d_gelu(x, w, b, pos, out, stride)
     return out
 

@@ -130,7 +130,12 @@ def _gather_kv(kv, seq: int, kvh: int, n: int):
     blk = kv.table[seq].long()[t // bs]
     off = blk * kv.sb + kvh * kv.sh + (t % bs) * kv.st
     idx = off[:, None] + torch.arange(D)[None, :]
-    return kv.k.reshape(-1)[idx].float(), kv.v.reshape(-1)[idx].float()
+
+    def flat(x):  # the whole storage (strided views: offsets are relative to the view's first element)
+        n_el = x.untyped_storage().nbytes() // x.element_size()
+        return x.as_strided((n_el,), (1,), 0)[x.storage_offset():]
+
+    return flat(kv.k)[idx].float(), flat(kv.v)[idx].float()
 
 
 def decode_attention(q, kv, ctx_lens, seq_ids, *, n_q_heads, n_kv_heads, head_dim, scale, out):
