@@ -956,8 +956,9 @@ void log_mel(Tensor audio, int64_t n_frames, Tensor window, Tensor basis, Tensor
 // GEMM on the tiled MFMA GEMM (gemm.hip, row-major weights).  x [B, Tin, Cin] must be a view
 // of a zero-padded channels-last buffer (ops.padded_rows): one zero row in front of and behind
 // every batch's Tin rows, so GEMM row t is the 3*Cin contiguous elements starting at padded
-// row t*stride (ldx = stride*Cin).  w [Cout, 3*Cin] in (kk, ci) order.
-void conv1d_gelu(Tensor x, Tensor w, c10::optional<Tensor> b, c10::optional<Tensor> pos, Tensor y, int64_t stride) {
+// row t*stride (ldx = stride*Cin).  w [Cout, 3*Cin] in (kk, ci) order, row-major or pre-tiled.
+void conv1d_gelu(Tensor x, Tensor w, c10::optional<Tensor> b, c10::optional<Tensor> pos, Tensor y, int64_t stride,
+                 bool w_tiled) {
   c10::DeviceGuard g(x.device());
   check_bf16(x, "x");
   check_bf16(w, "w");
@@ -980,7 +981,7 @@ void conv1d_gelu(Tensor x, Tensor w, c10::optional<Tensor> b, c10::optional<Tens
   p.X = bfp(x) - Cin;  // the zero row in front
   p.ldx = (int)(stride * Cin);
   p.W = bfp(w);
-  p.w_tiled = 0;
+  p.w_tiled = w_tiled ? 1 : 0;  // ops.tile_weight layout: 1 KB contiguous B-fragment DMA per instruction
   p.M = (int)Tout;
   p.N = (int)Cout;
   p.K = (int)(3 * Cin);
@@ -994,6 +995,17 @@ void conv1d_gelu(Tensor x, Tensor w, c10::optional<Tensor> b, c10::optional<Tens
     check_bf16(*b, "bias");
     TORCH_CHECK(b->numel() == Cout && b->is_contiguous(), "bias [Cout]");
     p.bias = bfp(*b);
+  }
+  // one utterance: split-K when the output tiles alone cannot fill the CUs (large-v3 conv2: 120
+  // tiles x 30 k-groups); the f32 slabs are summed by gemm_reduce_kernel with the same epilogue
+  Tensor ws;
+  if (B == 1) {
+    const int s = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), (int64_t)1 << 25);
+    if (s > 1) {
+      ws = at::empty({(int64_t)s * p.M * p.N}, x.options().dtype(at::kFloat));
+      p.ws = ws.data_ptr<float>();
+      p.splits = s;
+    }
   }
   int epi = 3;
   if (pos.has_value()) {

@@ -296,16 +296,24 @@ int g_attn_impl = 1;  // 1: multi-query MFMA kernel (default), 0: split VALU ker
 //    O^T += V^T.P^T for the two 16-key slices -- no lane exchange, no LDS round trip for P;
 //  * K and V tiles both live in the 256-byte-row image (b) (vimg_off): the 32x32x16 row reads of
 //    K and the ds_read_b64_tr_b16 reads of V^T are conflict-free on it;
-//  * online softmax with the running max folded into the MFMA accumulator (S' = K.Q^T - m is
-//    the chain's initial value) and a deferred rescale: the max moves (and O, l are rescaled) only
+//  * online softmax with a deferred rescale: the running max moves (and O, l are rescaled) only
 //    when a tile's max exceeds it by more than kRescale (log2 units; P <= 2^kRescale, f32 sums);
-//  * 64-key tiles double-buffered in LDS, next tile's global loads issued behind the LDS stores
-//    (one barrier per tile).
+//  * 8 waves = 4 query waves x 2 key splits: split s takes the 64-key tiles s, s + 2, ... into
+//    its own double-buffered LDS images (the next tile's global loads issued behind the LDS
+//    stores, one barrier per tile pair); the two splits' (m, l, O) merge through LDS at the end.
+//    Two waves per SIMD hide each other's MFMA -> softmax -> MFMA dependency chains, and each
+//    wave's serial tile chain is half as long (the v3 4-wave form measured ~3.6k cycles per tile,
+//    latency-bound at one wave per SIMD);
+//  * the sequence's block-table row is copied to LDS once (no dependent global load per tile).
 // Grid: 1-D, XCD-remapped so a (batch, head)'s query blocks share an XCD's L2 (K / V reuse);
 // within a head the query blocks run last-first (causal: the longest rows start first).
-constexpr int kFQ = 128;         // queries per workgroup (4 waves x 32)
+constexpr int kFQ = 128;         // queries per workgroup (4 query waves x 32)
 constexpr int kFK = 64;          // keys per tile
+constexpr int kFSplit = 2;       // key splits (wave groups) per workgroup
+constexpr int kFTab = 1024;      // block-table entries cached in LDS
 constexpr float kRescale = 8.f;  // deferred-max threshold (log2 units)
+constexpr int kFImg = kFK * 256;                       // bytes of one K or V tile image
+constexpr int kFLds = kFSplit * 2 * 2 * kFImg + kFTab * 4;  // [split][stage][K, V] images + table
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 VWA_DEVICE f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
@@ -313,13 +321,13 @@ VWA_DEVICE f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
 }
 
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(256, 2) void flash_attn_kernel(FlashAttnParams p) {
+__global__ __launch_bounds__(512) void flash_attn_kernel(FlashAttnParams p) {
   constexpr int NCH = D / 8;            // 16-byte chunks per K / V row
   constexpr int NDS = D / 16;           // QK k-steps over the head dim
   constexpr int NDT = D / 32;           // 32-row d tiles of O^T
   constexpr int LPT = kFK * NCH / 256;  // 16-byte chunks per thread per tile (K and V each)
-  constexpr int IMG = kFK * 256;        // bytes of one K or V tile image
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2][2][IMG];  // [stage][K, V]
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int* btab = reinterpret_cast<int*>(smem + kFSplit * 2 * 2 * kFImg);
 
   const int nqb = (p.Sq + kFQ - 1) / kFQ;
   const int nwg = nqb * p.n_q_heads * p.B;
@@ -327,7 +335,9 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(FlashAttnParams p) {
   const int hb = L / nqb, qb = nqb - 1 - L % nqb;
   const int h = hb % p.n_q_heads, b = hb / p.n_q_heads;
   const int kvh = h / (p.n_q_heads / p.n_kv_heads);
-  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  const int w = wid & 3, split = wid >> 2;  // query wave, key split
+  const int stid = threadIdx.x & 255;       // thread index within the split
   const int col = lane & 31, hf = lane >> 5;  // query column, lane half
   const int qoff = p.q_offsets ? p.q_offsets[b] : p.q_offset;
   const int Sk = p.k_lens ? p.k_lens[b] : p.Sk;
@@ -335,6 +345,16 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(FlashAttnParams p) {
   const int qi = qw0 + col;
   const int qpos = qoff + qi;
   const float sl2 = p.scale * 1.4426950408889634f;
+  unsigned char* simg = smem + split * (2 * 2 * kFImg);  // this split's [stage][K, V] images
+
+  int k_end = Sk;
+  if (CAUSAL) k_end = min(Sk, qoff + qb * kFQ + kFQ);
+  const int nt = (k_end + kFK - 1) / kFK;
+  const int k_load = min(Sk, nt * kFK);  // keys the tiles load (the last tile may pass k_end)
+  const int nblk = (k_load + p.kv.block_size - 1) / p.kv.block_size;
+  const bool tab_lds = nblk <= kFTab;
+  if (tab_lds)
+    for (int i = threadIdx.x; i < nblk; i += 512) btab[i] = p.kv.block_table[(int64_t)b * p.kv.table_stride + i];
 
   // Q^T fragments (B operand): lane (col, hf) holds Q[qi][16 ds + 8 hf + j], pre-scaled by scale*log2(e)
   bf16x8 qf[NDS];
@@ -360,20 +380,34 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(FlashAttnParams p) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) oacc[dt][i] = 0.f;
   float m_run = 0.f, l_run = 0.f;
-
-  int k_end = Sk;
-  if (CAUSAL) k_end = min(Sk, qoff + qb * kFQ + kFQ);
-  const int nt = (k_end + kFK - 1) / kFK;
+  __syncthreads();  // block table in LDS
 
   uint4 kr[LPT], vr[LPT];
+  // loader: thread row r_i = (stid + 256 i) / NCH, chunk ch_i.  One block for the whole sequence
+  // (contiguous K / V, e.g. the encoder): a fixed per-thread offset + t * stride_tok; paged with a
+  // power-of-two block size: shifts; otherwise the general division.
+  const int bs = p.kv.block_size;
+  const bool one_block = bs >= k_load;
+  const int lbs = (bs & (bs - 1)) == 0 ? __builtin_ctz(bs) : -1;
+  const int64_t head_off = (int64_t)kvh * p.kv.stride_head;
+  const int64_t blk0_off = one_block ? (int64_t)(tab_lds ? btab[0] : p.kv.block_table[(int64_t)b * p.kv.table_stride]) *
+                                           p.kv.stride_block + head_off
+                                     : 0;
   auto load_tile = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int c = threadIdx.x + i * 256;
+      const int c = stid + i * 256;
       const int r = c / NCH, ch = c % NCH;
       const int t = k0 + r;
       if (t < Sk) {
-        const int64_t off = kv_offset(p.kv, b, kvh, t) + ch * 8;
+        int64_t off;
+        if (one_block) {
+          off = blk0_off + (int64_t)t * p.kv.stride_tok + ch * 8;
+        } else {
+          const int bi = lbs >= 0 ? (t >> lbs) : t / bs, bo = lbs >= 0 ? (t & (bs - 1)) : t % bs;
+          const int blk = tab_lds ? btab[bi] : p.kv.block_table[(int64_t)b * p.kv.table_stride + bi];
+          off = (int64_t)blk * p.kv.stride_block + head_off + (int64_t)bo * p.kv.stride_tok + ch * 8;
+        }
         kr[i] = ld128(p.kv.k + off);
         vr[i] = ld128(p.kv.v + off);
       } else {
@@ -385,10 +419,10 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(FlashAttnParams p) {
   auto store_tile = [&](int stg) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int c = threadIdx.x + i * 256;
+      const int c = stid + i * 256;
       const int r = c / NCH, ch = c % NCH;
-      *reinterpret_cast<uint4*>(&lds[stg][0][vimg_off(r, ch)]) = kr[i];
-      *reinterpret_cast<uint4*>(&lds[stg][1][vimg_off(r, ch)]) = vr[i];
+      *reinterpret_cast<uint4*>(simg + (2 * stg) * kFImg + vimg_off(r, ch)) = kr[i];
+      *reinterpret_cast<uint4*>(simg + (2 * stg + 1) * kFImg + vimg_off(r, ch)) = vr[i];
     }
   };
 
@@ -402,93 +436,129 @@ __global__ __launch_bounds__(256, 2) void flash_attn_kernel(FlashAttnParams p) {
   const int v_key = 8 * (grp >> 1) + q4;
   const int v_ch = 2 * (grp & 1) + (p4 >> 1), v_sub = 8 * (p4 & 1);
 
-  if (nt > 0) {
-    load_tile(0);
+  // split s: tiles s, s + 2, ...; every split runs the same iteration count (block-wide barriers)
+  const int iters = (nt + kFSplit - 1) / kFSplit;
+  if (split < nt) {
+    load_tile(split * kFK);
     store_tile(0);
-    if (nt > 1) load_tile(kFK);
+    if (split + kFSplit < nt) load_tile((split + kFSplit) * kFK);
   }
   __syncthreads();
-  for (int t = 0; t < nt; ++t) {
-    const int k0 = t * kFK;
-    const unsigned char* kimg = lds[t & 1][0];
-    const unsigned char* vimg = lds[t & 1][1];
-    // ---- S'^T = K.Q^T - m_run (the running max is the chain's initial value)
-    f32x16 s[2];
+  bool first = true;
+  for (int it = 0; it < iters; ++it) {
+    const int t = it * kFSplit + split;
+    if (t < nt) {
+      const int k0 = t * kFK;
+      const unsigned char* kimg = simg + (2 * (it & 1)) * kFImg;
+      const unsigned char* vimg = kimg + kFImg;
+      // ---- S^T = K.Q^T
+      f32x16 s[2];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+      for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) s[kk][i] = -m_run;
-      const int row = 32 * kk + a_key;
+        for (int i = 0; i < 16; ++i) s[kk][i] = 0.f;
+        const int row = 32 * kk + a_key;
 #pragma unroll
-      for (int ds = 0; ds < NDS; ++ds) {
-        const uint4 a = *reinterpret_cast<const uint4*>(kimg + vimg_off(row, 2 * ds + hf));
-        s[kk] = mfma32(as_bf16x8(a), qf[ds], s[kk]);
-      }
-    }
-    // ---- mask (only tiles that reach past Sk or the wave's first causal row)
-    const bool edge = (k0 + kFK > Sk) || (CAUSAL && k0 + kFK - 1 > qoff + qw0);
-    if (edge) {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int key = k0 + 32 * kk + (i & 7) + 16 * (i >> 3) + 8 * hf;
-          if (key >= Sk || (CAUSAL && key > qpos)) s[kk][i] = -INFINITY;
-        }
-    }
-    float tmax = -INFINITY;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) tmax = fmaxf(tmax, s[kk][i]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    // ---- deferred rescale: the first tile sets the max; later ones move it only past kRescale
-    float delta = 0.f;
-    const bool move = (t == 0) || (tmax > kRescale);
-    if (__any(move)) {
-      delta = move ? tmax : 0.f;
-      const float alpha = __builtin_amdgcn_exp2f(-delta);
-      m_run += delta;
-      l_run *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) oacc[dt] *= alpha;
-    }
-    // ---- P^T = exp2(S' - delta), packed bf16 per 16-key slice; row sums in f32
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 pb[2];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        float pf[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          pf[j] = __builtin_amdgcn_exp2f(s[kk][8 * ks + j] - delta);
-          l_run += pf[j];
-        }
-        pb[ks] = as_bf16x8(pack8(pf));
-      }
-      // ---- O^T += V^T.P^T
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int kr0 = 32 * kk + 16 * ks + v_key;
-#pragma unroll
-        for (int dt = 0; dt < NDT; ++dt) {
-          const int ch = 4 * dt + v_ch;
-          const uint2 lo = lds_tr16(vimg + vimg_off(kr0, ch) + v_sub);
-          const uint2 hi = lds_tr16(vimg + vimg_off(kr0 + 4, ch) + v_sub);
-          oacc[dt] = mfma32(as_bf16x8(make_uint4(lo.x, lo.y, hi.x, hi.y)), pb[ks], oacc[dt]);
+        for (int ds = 0; ds < NDS; ++ds) {
+          const uint4 a = *reinterpret_cast<const uint4*>(kimg + vimg_off(row, 2 * ds + hf));
+          s[kk] = mfma32(as_bf16x8(a), qf[ds], s[kk]);
         }
       }
-    }
-    if (t + 1 < nt) {
-      store_tile((t + 1) & 1);
-      if (t + 2 < nt) load_tile(k0 + 2 * kFK);
+      // ---- mask (only tiles that reach past Sk or the wave's first causal row)
+      const bool edge = (k0 + kFK > Sk) || (CAUSAL && k0 + kFK - 1 > qoff + qw0);
+      if (edge) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = k0 + 32 * kk + (i & 7) + 16 * (i >> 3) + 8 * hf;
+            if (key >= Sk || (CAUSAL && key > qpos)) s[kk][i] = -INFINITY;
+          }
+      }
+      float tm0 = vmax3(s[0][0], s[0][1], s[0][2]), tm1 = vmax3(s[1][0], s[1][1], s[1][2]);  // two chains
+#pragma unroll
+      for (int i = 3; i < 15; i += 2) {
+        tm0 = vmax3(tm0, s[0][i], s[0][i + 1]);
+        tm1 = vmax3(tm1, s[1][i], s[1][i + 1]);
+      }
+      const float tmax = max_halves(vmax3(tm0, tm1, vmax3(s[0][15], s[1][15], s[1][15])));
+      // ---- deferred rescale: the split's first tile with a visible key sets the max (a causal tile
+      // may leave a row without one: -inf contributes nothing); later tiles move it only when their
+      // max exceeds it by more than kRescale
+      const bool move = (first && tmax != -INFINITY) || (tmax - m_run > kRescale);
+      if (__any(move)) {
+        const float m_new = move ? tmax : m_run;
+        const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+        m_run = m_new;
+        l_run *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) oacc[dt] *= alpha;
+      }
+      first = first && tmax == -INFINITY;  // per lane: until a visible key
+      // ---- P^T = exp2(S - m), packed bf16 per 16-key slice; row sums in f32 (4 partial sums)
+      float ls[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 pb[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          float pf[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            pf[j] = __builtin_amdgcn_exp2f(s[kk][8 * ks + j] - m_run);
+            ls[j & 3] += pf[j];
+          }
+          pb[ks] = as_bf16x8(pack8(pf));
+        }
+        // ---- O^T += V^T.P^T
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int kr0 = 32 * kk + 16 * ks + v_key;
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) {
+            const int ch = 4 * dt + v_ch;
+            const uint2 lo = lds_tr16(vimg + vimg_off(kr0, ch) + v_sub);
+            const uint2 hi = lds_tr16(vimg + vimg_off(kr0 + 4, ch) + v_sub);
+            oacc[dt] = mfma32(as_bf16x8(make_uint4(lo.x, lo.y, hi.x, hi.y)), pb[ks], oacc[dt]);
+          }
+        }
+      }
+      l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+      if (t + kFSplit < nt) {
+        store_tile((it + 1) & 1);
+        if (t + 2 * kFSplit < nt) load_tile((t + 2 * kFSplit) * kFK);
+      }
     }
     __syncthreads();
   }
 
+  // ---- merge the key splits through LDS (the tile images are free after the last barrier):
+  // split 1 publishes (m, l, O^T) per lane, split 0 combines and stores
+  float* mo = reinterpret_cast<float*>(smem) + w * (64 * (NDT * 16 + 2));
+  if (split == 1) {
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) mo[(dt * 16 + i) * 64 + lane] = oacc[dt][i];
+    mo[(NDT * 16) * 64 + lane] = first ? -INFINITY : m_run;  // a split that saw no key adds nothing
+    mo[(NDT * 16 + 1) * 64 + lane] = l_run;
+  }
+  __syncthreads();
+  if (split == 1) return;
+  {
+    const float m1 = mo[(NDT * 16) * 64 + lane], l1 = mo[(NDT * 16 + 1) * 64 + lane];
+    const float m0 = first ? -INFINITY : m_run;
+    const float M = fmaxf(m0, m1);
+    const float a0 = __builtin_amdgcn_exp2f(m0 - M), a1 = __builtin_amdgcn_exp2f(m1 - M);
+    l_run = l_run * a0 + l1 * a1;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) oacc[dt][i] = oacc[dt][i] * a0 + mo[(dt * 16 + i) * 64 + lane] * a1;
+  }
+
   // ---- epilogue: lane (col, hf) holds O^T[d][qi] for d = 32dt + (i&3) + 8(i>>2) + 4hf
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float l_tot = sum_halves(l_run);
   if (qi < p.Sq) {
     const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
     u16* orow = p.o + (int64_t)b * p.o_stride_b + (int64_t)qi * p.o_stride_s + (int64_t)h * p.o_stride_h;
@@ -524,13 +594,13 @@ extern "C" int vwa_decode_attention(const DecodeAttnParams* p, hipStream_t st) {
 extern "C" int vwa_flash_attention(const FlashAttnParams* p, hipStream_t st) {
   if (p->n_kv_heads <= 0 || p->n_q_heads % p->n_kv_heads) return -1;
   if (p->B <= 0 || p->Sq <= 0) return 0;
-  dim3 grid(((p->Sq + kFQ - 1) / kFQ) * p->n_q_heads * p->B);
+  dim3 grid(((p->Sq + kFQ - 1) / kFQ) * p->n_q_heads * p->B), block(64 * 4 * kFSplit);
   if (p->head_dim == 128) {
-    if (p->causal) hipLaunchKernelGGL((flash_attn_kernel<128, true>), grid, dim3(256), 0, st, *p);
-    else hipLaunchKernelGGL((flash_attn_kernel<128, false>), grid, dim3(256), 0, st, *p);
+    if (p->causal) hipLaunchKernelGGL((flash_attn_kernel<128, true>), grid, block, kFLds, st, *p);
+    else hipLaunchKernelGGL((flash_attn_kernel<128, false>), grid, block, kFLds, st, *p);
   } else if (p->head_dim == 64) {
-    if (p->causal) hipLaunchKernelGGL((flash_attn_kernel<64, true>), grid, dim3(256), 0, st, *p);
-    else hipLaunchKernelGGL((flash_attn_kernel<64, false>), grid, dim3(256), 0, st, *p);
+    if (p->causal) hipLaunchKernelGGL((flash_attn_kernel<64, true>), grid, block, kFLds, st, *p);
+    else hipLaunchKernelGGL((flash_attn_kernel<64, false>), grid, block, kFLds, st, *p);
   } else {
     return -3;
   }

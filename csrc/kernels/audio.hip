@@ -58,8 +58,9 @@ VWA_DEVICE float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7ffffff
 // 58 % LDS bank conflicts: profiles/r3_pmc_counters.md row 11).
 constexpr int kLmFrames = 16;        // frames per workgroup (MFMA rows)
 constexpr int kLmBinTiles = 13;      // 208 >= 201 bins
-constexpr int kLmXLd = 404;          // LDS row stride (floats) of the frame / power images:
-constexpr int kLmPLd = 212;          //   404, 212 = 20 (mod 64) -> conflict-free 16 rows x 4 k reads
+constexpr int kLmXLd = 450;          // LDS row strides (floats) of the frame / power images:
+constexpr int kLmPLd = 258;          //   = 2 (mod 64): the A reads (16 rows x 4 k) hit distinct banks
+                                     //   per 32-lane half (20 mod 64 measured 45 % conflicts)
 constexpr int kLmWaves = 8;
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
@@ -76,10 +77,21 @@ __global__ __launch_bounds__(kLmWaves * 64) void logmel_mfma_kernel(const float*
   const int f0 = blockIdx.x * kLmFrames;
   const int lane = lane_id(), w = threadIdx.x >> 6;
   const int r = lane & 15, kq = lane >> 4;
-  for (int i = threadIdx.x; i < kLmFrames * kNFFT; i += kLmWaves * 64) {
-    const int fr = i / kNFFT, n = i % kNFFT;
-    const int f = f0 + fr;
-    xs[fr * kLmXLd + n] = f < n_frames ? audio[reflect(f * kHop + n - kNFFT / 2, n_samples)] * window[n] : 0.f;
+  {  // all 13 gathers of a thread in flight together (a rolled loop waits one round trip each)
+    constexpr int NG = (kLmFrames * kNFFT + kLmWaves * 64 - 1) / (kLmWaves * 64);
+    float v[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int i = threadIdx.x + g * kLmWaves * 64;
+      const int fr = i / kNFFT, n = i % kNFFT, f = f0 + fr;
+      v[g] = (i < kLmFrames * kNFFT && f < n_frames) ? audio[reflect(f * kHop + n - kNFFT / 2, n_samples)] * window[n]
+                                                      : 0.f;
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int i = threadIdx.x + g * kLmWaves * 64;
+      if (i < kLmFrames * kNFFT) xs[(i / kNFFT) * kLmXLd + i % kNFFT] = v[g];
+    }
   }
   __syncthreads();
 
@@ -93,14 +105,33 @@ __global__ __launch_bounds__(kLmWaves * 64) void logmel_mfma_kernel(const float*
       as[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     const float* xr = xs + r * kLmXLd + kq;
+    // basis fragments one 4-step group ahead (an L2 round trip per group otherwise stalls the
+    // MFMA chain: 25 groups x ~600 cycles)
+    const float4* bp[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int bt = min(w + t * kLmWaves, kLmBinTiles - 1);
+      bp[t][0] = basis + (2 * bt) * (kNFFT / 16) * 64 + lane;
+      bp[t][1] = basis + (2 * bt + 1) * (kNFFT / 16) * 64 + lane;
+    }
+    float4 nc[2], ns[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      nc[t] = bp[t][0][0];
+      ns[t] = bp[t][1][0];
+    }
     for (int s4 = 0; s4 < kNFFT / 16; ++s4) {
       float4 bc[2], bs[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        if (t < nbt) {
-          const int bt = w + t * kLmWaves;
-          bc[t] = basis[((2 * bt) * (kNFFT / 16) + s4) * 64 + lane];
-          bs[t] = basis[((2 * bt + 1) * (kNFFT / 16) + s4) * 64 + lane];
+        bc[t] = nc[t];
+        bs[t] = ns[t];
+      }
+      if (s4 + 1 < kNFFT / 16) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          nc[t] = bp[t][0][(s4 + 1) * 64];
+          ns[t] = bp[t][1][(s4 + 1) * 64];
         }
       }
 #pragma unroll
@@ -134,9 +165,12 @@ __global__ __launch_bounds__(kLmWaves * 64) void logmel_mfma_kernel(const float*
   if (16 * w < n_mels) {
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
     const float* pr = ps + r * kLmPLd + kq;
+    float4 fb[kLmBinTiles];  // all 13 filterbank fragments in flight at once
+#pragma unroll
+    for (int s4 = 0; s4 < kLmBinTiles; ++s4) fb[s4] = fbf[(w * kLmBinTiles + s4) * 64 + lane];
+#pragma unroll
     for (int s4 = 0; s4 < kLmBinTiles; ++s4) {  // 52 k-steps of 4 bins
-      const float4 b = fbf[(w * kLmBinTiles + s4) * 64 + lane];
-      const float* bb = reinterpret_cast<const float*>(&b);
+      const float* bb = reinterpret_cast<const float*>(&fb[s4]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc = mfma_f32(pr[(4 * s4 + j) * 4], bb[j], acc);
     }

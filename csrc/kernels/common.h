@@ -45,8 +45,28 @@ VWA_DEVICE u16 f2bf(float f) {
   return __builtin_bit_cast(u16, b);
 }
 
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 VWA_DEVICE uint32_t pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  // one v_cvt_pk_bf16_f32 (RNE) for the pair (two scalar converts + shift/or otherwise)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
+}
+
+// v_max3_f32 without the canonicalising v_max the compiler puts in front of fmaxf on MFMA results
+VWA_DEVICE float vmax3(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// the value of lane l ^ 32 combined with lane l's: v_permlane32_swap (VALU; no LDS round trip)
+VWA_DEVICE float max_halves(float x) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return vmax3(__uint_as_float(s[0]), __uint_as_float(s[1]), __uint_as_float(s[1]));
+}
+VWA_DEVICE float sum_halves(float x) {
+  const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(s[0]) + __uint_as_float(s[1]);
 }
 
 // unpack a 16-byte vector of 8 bf16 into f32

@@ -452,6 +452,8 @@ def test_conv_stem_implicit_gemm(Cin, Cout, stride, B):
     Tout = (Tin - 1) // stride + 1
     pos = rnd(Tout, Cout) if stride == 2 else None
     y = ops.conv1d_gelu(xv, w, b, stride=stride, pos=pos, padded=True)
+    yt = ops.conv1d_gelu(xv, ops.TiledWeight(w), b, stride=stride, pos=pos, padded=True)
+    assert torch.equal(y, yt)  # pre-tiled weights: same products, same order
     exp = ref.conv1d_gelu(xv.cpu(), w.cpu(), b.cpu(), stride=stride, pos=None if pos is None else pos.cpu(),
                           out=torch.empty(B, Tout, Cout, dtype=torch.float32))
     close(y, exp, 3e-2)

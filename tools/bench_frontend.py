@@ -76,8 +76,8 @@ def main():
             _, mv = ops.padded_rows(B, 3000, cp, dtype=BF, device=dev)
             mv.copy_(torch.randn(B, 3000, cp, device=dev).to(BF))
             _, cv = ops.padded_rows(B, 3000, d, dtype=BF, device=dev)
-            w1 = (torch.randn(d, 3 * cp, device=dev) * 0.02).to(BF)
-            w2 = (torch.randn(d, 3 * d, device=dev) * 0.02).to(BF)
+            w1 = ops.TiledWeight((torch.randn(d, 3 * cp, device=dev) * 0.02).to(BF))
+            w2 = ops.TiledWeight((torch.randn(d, 3 * d, device=dev) * 0.02).to(BF))
             b = torch.zeros(d, device=dev, dtype=BF)
             pos = torch.randn(1500, d, device=dev).to(BF)
             y2 = torch.empty(B, 1500, d, device=dev, dtype=BF)
@@ -86,8 +86,8 @@ def main():
                 ops.conv1d_gelu(mv, w1, b, stride=1, out=cv, padded=True)
                 ops.conv1d_gelu(cv, w2, b, stride=2, pos=pos, out=y2, padded=True)
 
-            wt1 = w1.view(d, 3, cp).permute(0, 2, 1).contiguous()
-            wt2 = w2.view(d, 3, d).permute(0, 2, 1).contiguous()
+            wt1 = w1.dense().view(d, 3, cp).permute(0, 2, 1).contiguous()
+            wt2 = w2.dense().view(d, 3, d).permute(0, 2, 1).contiguous()
             xt = mv.transpose(1, 2).contiguous()
 
             def lib():

@@ -126,6 +126,15 @@ class WhisperModel:
         self.mel_ch = ops.conv_channels(cfg.n_mels)
         self.conv1_wp = ops.pad_conv_weight(self.conv1_w, self.mel_ch)
         self._stem: dict = {}
+        # GPU: the encoder-side GEMM weights (conv stem, encoder projections: M = 1500 x sessions
+        # rows on the tiled MFMA GEMM) are kept ONLY in the pre-tiled layout
+        if self.device.type == "cuda":
+            self.conv1_wp = ops.TiledWeight(self.conv1_wp)
+            self.conv2_wt = ops.TiledWeight(self.conv2_w)
+            for L in self.enc:
+                L.qkv, L.o, L.fc1, L.fc2 = (ops.TiledWeight(t) for t in (L.qkv, L.o, L.fc1, L.fc2))
+        else:
+            self.conv2_wt = self.conv2_w
 
     def _load(self, w) -> None:
         """HF WhisperForConditionalGeneration names (safetensors, runtime.weights.LazySafetensors)."""
@@ -227,7 +236,7 @@ class WhisperModel:
         if mel.data_ptr() != mv.data_ptr() or mel.shape != mv.shape:
             mv[:, :, : cfg.n_mels] = mel[:, :, : cfg.n_mels]
         x = ops.conv1d_gelu(mv, self.conv1_wp, self.conv1_b, stride=1, out=cv, padded=True)
-        x = ops.conv1d_gelu(x, self.conv2_w, self.conv2_b, stride=2, pos=self.pos_enc, padded=True)
+        x = ops.conv1d_gelu(x, self.conv2_wt, self.conv2_b, stride=2, pos=self.pos_enc, padded=True)
         T, d = x.shape[1], x.shape[2]
         x = x.reshape(B * T, d)
         table = torch.arange(B, dtype=torch.int32, device=self.device)[:, None]

@@ -914,13 +914,14 @@ def conv1d_gelu(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], *, 
     if out is None:
         out = torch.empty((B, Tout, w.shape[0]), dtype=x.dtype, device=x.device)
     if not _gpu(x):
-        return ref.conv1d_gelu(x, w, b, stride=stride, pos=pos, out=out)
+        return ref.conv1d_gelu(x, plain(w), b, stride=stride, pos=pos, out=out)
     if not padded:
         cp = conv_channels(Cin)
         _, xv = padded_rows(B, Tin, cp, dtype=x.dtype, device=x.device)
         xv[:, :, :Cin] = x
-        x, w = xv, pad_conv_weight(w, cp)
-    ext().conv1d_gelu(x, w, b, pos, out, stride)
+        x, w = xv, pad_conv_weight(plain(w), cp)
+    tiled = isinstance(w, TiledWeight)
+    ext().conv1d_gelu(x, w.t if tiled else w, b, pos, out, stride, tiled)
     return out
 
 
