@@ -999,7 +999,7 @@ void conv1d_gelu(Tensor x, Tensor w, c10::optional<Tensor> b, c10::optional<Tens
   // one utterance: split-K when the output tiles alone cannot fill the CUs (large-v3 conv2: 120
   // tiles x 30 k-groups); the f32 slabs are summed by gemm_reduce_kernel with the same epilogue
   Tensor ws;
-  if (B == 1) {
+  if (B == 1 && p.K >= 1024) {  // (K = 384: the split's f32 reduce costs more than it saves)
     const int s = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), (int64_t)1 << 25);
     if (s > 1) {
       ws = at::empty({(int64_t)s * p.M * p.N}, x.options().dtype(at::kFloat));

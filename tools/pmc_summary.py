@@ -90,6 +90,7 @@ def short(name):
 
 def main():
     dirpath, title = sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "hardware counters"
+    program = sys.argv[3] if len(sys.argv) > 3 else "tools/pmc_kernels.py"
     passes = load(dirpath)
     merged = {}  # chunk index -> {"name", "dur": [...], counters: [...]}
     for disp in passes:
@@ -114,7 +115,7 @@ def main():
 
     print(f"# {title}\n")
     print(f"Source: rocprofv3 `--pmc` passes under `{dirpath}` ({len(passes)} passes), program "
-          "`tools/pmc_kernels.py`; median of launches 2..6 of each shape. Derivations: see "
+          f"`{program}`; median of launches 2..6 of each shape. Derivations: see "
           "`tools/pmc_summary.py` docstring (HBM rd doubles FETCH_SIZE, gfx950 counts half).\n")
     print("| # | kernel | grid | us | HBM rd GB/s (raw) | wr GB/s | L2 hit | MFMA busy | TFLOP/s | "
           "LDS confl | wave wait |")
