@@ -73,3 +73,13 @@ def test_router_balances_proxies_and_fails_over():
             await w.close()
 
     asyncio.run(go())
+
+
+def test_launch_gpu_plan():
+    from voice_enabled_browser_automation_amd.launch import plan_gpus
+
+    assert plan_gpus(8, tp=2) == {"brain": ["0", "1"], "voice": ["2", "3", "4", "5", "6", "7"], "shared": False}
+    assert plan_gpus(2) == {"brain": ["0"], "voice": ["1"], "shared": False}
+    assert plan_gpus(1) == {"brain": ["0"], "voice": ["0"], "shared": True}
+    assert plan_gpus(8, tp=8)["shared"]  # every GPU is a TP rank: the voice worker shares GPU 0
+    assert plan_gpus(8, brain="3", voice="4,5") == {"brain": ["3"], "voice": ["4", "5"], "shared": False}
