@@ -52,6 +52,14 @@ def test_router_balances_proxies_and_fails_over():
             ta, tb = await transcript(a), await transcript(b)
             assert {ta.split(":")[0], tb.split(":")[0]} == {"w0", "w1"}  # one session per worker
             assert ta.endswith(":320") and tb.endswith(":640")  # frames proxied unchanged
+            # C6 metrics gather: after a watchdog round every rank reports its live session + final
+            agg = None
+            for _ in range(40):
+                await asyncio.sleep(0.1)
+                agg = (await (await http.get(router.make_url("/metrics"))).json())["aggregate"]
+                if agg.get("ranks_reporting") == 2 and agg.get("finals") == 2:
+                    break
+            assert agg["ranks_reporting"] == 2 and agg["live_sessions"] == 2 and agg["finals"] == 2, agg
             # kill the worker serving `a`: its session moves to the survivor
             dead = 0 if ta.startswith("w0") else 1
             await workers[dead].close()

@@ -242,6 +242,11 @@ class AsrBatcher:
     def rows_per_batch(self) -> float:
         return self.stats["passes"] / max(1, self.stats["batches"])
 
+    def queue_depth(self) -> int:
+        """Recognition passes waiting for the next GPU batch (the router's load signal)."""
+        with self._cv:
+            return len(self._q)
+
     def _loop(self) -> None:
         if self._cuda_index is not None:
             import torch

@@ -8,6 +8,9 @@ listens on VOICE_PORT with the same ``/health`` and ``/stream`` surface and
 
 * assigns every new WebSocket to the healthy worker with the fewest live sessions;
 * proxies frames both ways unchanged (binary PCM in, JSON events out: byte-compatible);
+* gathers every worker's ``/metrics`` on each watchdog round (per-rank ASR RTF,
+  batcher queue depth, live sessions, speech->final latency) into its own ``/metrics``
+  (``workers[i].stats`` + a node-level ``aggregate``);
 * runs a watchdog that probes every worker's ``/health`` each ``VWA_WATCHDOG_S`` seconds; a
   worker that fails ``VWA_WATCHDOG_FAILS`` probes in a row is taken out of rotation, and the
   sessions it was serving are moved to a healthy worker: the client gets an
@@ -37,6 +40,33 @@ class Worker:
     fails: int = 0
     sessions: int = 0
     clients: set = field(default_factory=set)
+    stats: dict = field(default_factory=dict)  # last gathered /metrics summary
+
+
+def worker_summary(snap: dict) -> dict:
+    """The per-rank fields of a voice worker's /metrics snapshot the router aggregates."""
+    lat = snap.get("latency") or {}
+    bat = snap.get("asr_batcher") or {}
+
+    def p50(k):
+        return (lat.get(k) or {}).get("p50")
+
+    return {"live_sessions": snap.get("live_sessions"), "asr_rtf_p50": p50("asr_rtf"),
+            "asr_push_ms_p50": p50("asr_push_ms"), "speech_to_final_ms_p50": p50("speech_to_final_ms"),
+            "utterance_to_intent_ms_p50": p50("utterance_to_intent_ms"), "queue_depth": bat.get("queue_depth"),
+            "rows_per_batch": bat.get("rows_per_batch"), "finals": (snap.get("counters") or {}).get("finals", 0)}
+
+
+def aggregate(stats: List[dict]) -> dict:
+    """Node-level view over the ranks' summaries (sums of counts, max queue, mean / max RTF)."""
+    def vals(k):
+        return [s[k] for s in stats if s.get(k) is not None]
+
+    rtf = vals("asr_rtf_p50")
+    return {"ranks_reporting": len(stats), "live_sessions": sum(vals("live_sessions")),
+            "finals": sum(vals("finals")), "max_queue_depth": max(vals("queue_depth"), default=0),
+            "asr_rtf_p50_mean": round(sum(rtf) / len(rtf), 6) if rtf else None,
+            "asr_rtf_p50_max": max(rtf, default=None)}
 
 
 def build_router(worker_urls: List[str], *, probe_s: Optional[float] = None,
@@ -58,12 +88,21 @@ def build_router(worker_urls: List[str], *, probe_s: Optional[float] = None,
         except (aiohttp.ClientError, asyncio.TimeoutError):
             return False
 
+    async def gather(w: Worker) -> None:
+        try:
+            async with app["http"].get(w.url + "/metrics", timeout=aiohttp.ClientTimeout(total=probe_s)) as r:
+                if r.status == 200:
+                    w.stats = worker_summary(await r.json())
+        except (aiohttp.ClientError, asyncio.TimeoutError, ValueError):
+            pass
+
     async def watchdog():
         while True:
             await asyncio.sleep(probe_s)
             for w in app["workers"]:
                 ok = await probe(w)
                 if ok:
+                    await gather(w)
                     w.fails = 0
                     if not w.healthy:
                         w.healthy = True
@@ -94,7 +133,9 @@ def build_router(worker_urls: List[str], *, probe_s: Optional[float] = None,
 
     async def metrics(_req):
         snap = app["metrics"].snapshot()
-        snap["workers"] = [{"url": w.url, "healthy": w.healthy, "sessions": w.sessions} for w in app["workers"]]
+        snap["workers"] = [{"url": w.url, "healthy": w.healthy, "sessions": w.sessions, "stats": w.stats}
+                           for w in app["workers"]]
+        snap["aggregate"] = aggregate([w.stats for w in app["workers"] if w.healthy and w.stats])
         return web.json_response(snap)
 
     class _Client:

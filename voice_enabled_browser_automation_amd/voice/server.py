@@ -51,6 +51,7 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
     None = passthrough mode (no recognizer, as the reference without DEEPGRAM_API_KEY)."""
     app = web.Application()
     app["metrics"] = Metrics("voice")
+    app["live"] = 0  # open /stream sessions (reported to the DP router's metrics gather)
     # one worker per live session pass: a session's recognition pass blocks its worker inside the
     # recognizer (asr/streaming.py AsrBatcher), whose single scheduler thread batches the passes
     # of all sessions onto the GPU -- so the pool only needs to be as wide as the session count
@@ -79,7 +80,9 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
         snap = app["metrics"].snapshot()
         batcher = getattr(asr_factory, "batcher", None)
         if batcher is not None:  # cross-session ASR batching: passes per GPU batch
-            snap["asr_batcher"] = dict(batcher.stats, rows_per_batch=round(batcher.rows_per_batch(), 3))
+            snap["asr_batcher"] = dict(batcher.stats, rows_per_batch=round(batcher.rows_per_batch(), 3),
+                                       queue_depth=batcher.queue_depth())
+        snap["live_sessions"] = app["live"]
         return web.json_response(snap)
 
     async def stream(req: web.Request) -> web.WebSocketResponse:
@@ -206,6 +209,7 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                     st["debounce"].cancel()
                 st["debounce"] = asyncio.ensure_future(debounced())
 
+        app["live"] += 1
         try:
             async for msg in ws:
                 if msg.type == WSMsgType.BINARY:
@@ -238,6 +242,7 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                 elif msg.type in (WSMsgType.ERROR, WSMsgType.CLOSE):
                     break
         finally:
+            app["live"] -= 1
             st["closed"] = True
             if st["debounce"] is not None:
                 st["debounce"].cancel()
