@@ -294,26 +294,46 @@ int g_attn_impl = 1;  // 1: multi-query MFMA kernel (default), 0: split VALU ker
 //  * the K rows of a block are read in a permuted order (A row R <- key kb(R)) so that lane half
 //    h's 16 scores are keys {8h..8h+7, 16+8h..16+8h+7}: exactly the B operand (P^T) of
 //    O^T += V^T.P^T for the two 16-key slices -- no lane exchange, no LDS round trip for P;
-//  * K and V tiles both live in the 256-byte-row image (b) (vimg_off): the 32x32x16 row reads of
-//    K and the ds_read_b64_tr_b16 reads of V^T are conflict-free on it;
+//  * K and V tiles both live in one swizzled image (FlashCfg::off): the 32x32x16 row reads of K
+//    and the ds_read_b64_tr_b16 reads of V^T are conflict-free on it;
 //  * online softmax with a deferred rescale: the running max moves (and O, l are rescaled) only
 //    when a tile's max exceeds it by more than kRescale (log2 units; P <= 2^kRescale, f32 sums);
-//  * 8 waves = 4 query waves x 2 key splits: split s takes the 64-key tiles s, s + 2, ... into
-//    its own double-buffered LDS images (the next tile's global loads issued behind the LDS
-//    stores, one barrier per tile pair); the two splits' (m, l, O) merge through LDS at the end.
-//    Two waves per SIMD hide each other's MFMA -> softmax -> MFMA dependency chains, and each
-//    wave's serial tile chain is half as long (the v3 4-wave form measured ~3.6k cycles per tile,
-//    latency-bound at one wave per SIMD);
+//  * 4 query waves x NS key splits (FlashCfg: 2 for D = 128, 3 for D = 64): split s takes the
+//    64-key tiles s, s + NS, ... into its own double-buffered LDS images (the next tile's global
+//    loads issued behind the LDS stores, one barrier per tile round); the splits' (m, l, O) merge
+//    through LDS at the end.  NS waves per SIMD hide each other's MFMA -> softmax -> MFMA
+//    dependency chains, and each wave's serial tile chain is 1/NS as long (the 4-wave form
+//    measured ~3.6k cycles per tile, latency-bound at one wave per SIMD);
 //  * the sequence's block-table row is copied to LDS once (no dependent global load per tile).
 // Grid: 1-D, XCD-remapped so a (batch, head)'s query blocks share an XCD's L2 (K / V reuse);
 // within a head the query blocks run last-first (causal: the longest rows start first).
 constexpr int kFQ = 128;         // queries per workgroup (4 query waves x 32)
 constexpr int kFK = 64;          // keys per tile
-constexpr int kFSplit = 2;       // key splits (wave groups) per workgroup
 constexpr int kFTab = 1024;      // block-table entries cached in LDS
 constexpr float kRescale = 8.f;  // deferred-max threshold (log2 units)
-constexpr int kFImg = kFK * 256;                       // bytes of one K or V tile image
-constexpr int kFLds = kFSplit * 2 * 2 * kFImg + kFTab * 4;  // [split][stage][K, V] images + table
+
+// Per head dim: key splits (wave groups of 4) per workgroup and the K / V tile image.
+//  D = 128: 256-byte rows, image (b) (vimg_off), 16 KB per tile -> 2 splits (8 waves, 128 KB).
+//  D = 64: the guide's image (a) with 128-byte rows -- 8-row x 32-column subtiles of 512 B,
+//  off = 1024 (row >> 3) + 512 (ch >> 2) + 64 (row & 7) + 16 ((ch & 3) ^ ((row >> 2) & 3)): the same
+//  bank pattern as the 256-byte-row form (512 and 1024 are multiples of the 256-byte bank cycle),
+//  so its row and transposed reads stay conflict-free at half the bytes (8 KB per tile) ->
+//  3 splits (12 waves: 3 per SIMD, 96 KB).
+template <int D> struct FlashCfg;
+template <> struct FlashCfg<128> {
+  static constexpr int NS = 2, IMG = kFK * 256;
+  static VWA_DEVICE int off(int r, int ch) { return vimg_off(r, ch); }
+};
+template <> struct FlashCfg<64> {
+  static constexpr int NS = 3, IMG = kFK * 128;
+  static VWA_DEVICE int off(int r, int ch) {
+    return 1024 * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3));
+  }
+};
+template <int D>
+constexpr int flash_lds() {  // [split][stage][K, V] images + block table
+  return FlashCfg<D>::NS * 2 * 2 * FlashCfg<D>::IMG + kFTab * 4;
+}
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 VWA_DEVICE f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
@@ -321,13 +341,15 @@ VWA_DEVICE f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
 }
 
 template <int D, bool CAUSAL>
-__global__ __launch_bounds__(512) void flash_attn_kernel(FlashAttnParams p) {
+__global__ __launch_bounds__(256 * FlashCfg<D>::NS) void flash_attn_kernel(FlashAttnParams p) {
+  using FC = FlashCfg<D>;
+  constexpr int NS = FC::NS, IMG = FC::IMG;
   constexpr int NCH = D / 8;            // 16-byte chunks per K / V row
   constexpr int NDS = D / 16;           // QK k-steps over the head dim
   constexpr int NDT = D / 32;           // 32-row d tiles of O^T
   constexpr int LPT = kFK * NCH / 256;  // 16-byte chunks per thread per tile (K and V each)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  int* btab = reinterpret_cast<int*>(smem + kFSplit * 2 * 2 * kFImg);
+  int* btab = reinterpret_cast<int*>(smem + NS * 2 * 2 * IMG);
 
   const int nqb = (p.Sq + kFQ - 1) / kFQ;
   const int nwg = nqb * p.n_q_heads * p.B;
@@ -345,7 +367,7 @@ __global__ __launch_bounds__(512) void flash_attn_kernel(FlashAttnParams p) {
   const int qi = qw0 + col;
   const int qpos = qoff + qi;
   const float sl2 = p.scale * 1.4426950408889634f;
-  unsigned char* simg = smem + split * (2 * 2 * kFImg);  // this split's [stage][K, V] images
+  unsigned char* simg = smem + split * (2 * 2 * IMG);  // this split's [stage][K, V] images
 
   int k_end = Sk;
   if (CAUSAL) k_end = min(Sk, qoff + qb * kFQ + kFQ);
@@ -354,7 +376,7 @@ __global__ __launch_bounds__(512) void flash_attn_kernel(FlashAttnParams p) {
   const int nblk = (k_load + p.kv.block_size - 1) / p.kv.block_size;
   const bool tab_lds = nblk <= kFTab;
   if (tab_lds)
-    for (int i = threadIdx.x; i < nblk; i += 512) btab[i] = p.kv.block_table[(int64_t)b * p.kv.table_stride + i];
+    for (int i = threadIdx.x; i < nblk; i += 256 * NS) btab[i] = p.kv.block_table[(int64_t)b * p.kv.table_stride + i];
 
   // Q^T fragments (B operand): lane (col, hf) holds Q[qi][16 ds + 8 hf + j], pre-scaled by scale*log2(e)
   bf16x8 qf[NDS];
@@ -421,8 +443,8 @@ __global__ __launch_bounds__(512) void flash_attn_kernel(FlashAttnParams p) {
     for (int i = 0; i < LPT; ++i) {
       const int c = stid + i * 256;
       const int r = c / NCH, ch = c % NCH;
-      *reinterpret_cast<uint4*>(simg + (2 * stg) * kFImg + vimg_off(r, ch)) = kr[i];
-      *reinterpret_cast<uint4*>(simg + (2 * stg + 1) * kFImg + vimg_off(r, ch)) = vr[i];
+      *reinterpret_cast<uint4*>(simg + (2 * stg) * IMG + FC::off(r, ch)) = kr[i];
+      *reinterpret_cast<uint4*>(simg + (2 * stg + 1) * IMG + FC::off(r, ch)) = vr[i];
     }
   };
 
@@ -437,20 +459,20 @@ __global__ __launch_bounds__(512) void flash_attn_kernel(FlashAttnParams p) {
   const int v_ch = 2 * (grp & 1) + (p4 >> 1), v_sub = 8 * (p4 & 1);
 
   // split s: tiles s, s + 2, ...; every split runs the same iteration count (block-wide barriers)
-  const int iters = (nt + kFSplit - 1) / kFSplit;
+  const int iters = (nt + NS - 1) / NS;
   if (split < nt) {
     load_tile(split * kFK);
     store_tile(0);
-    if (split + kFSplit < nt) load_tile((split + kFSplit) * kFK);
+    if (split + NS < nt) load_tile((split + NS) * kFK);
   }
   __syncthreads();
   bool first = true;
   for (int it = 0; it < iters; ++it) {
-    const int t = it * kFSplit + split;
+    const int t = it * NS + split;
     if (t < nt) {
       const int k0 = t * kFK;
-      const unsigned char* kimg = simg + (2 * (it & 1)) * kFImg;
-      const unsigned char* vimg = kimg + kFImg;
+      const unsigned char* kimg = simg + (2 * (it & 1)) * IMG;
+      const unsigned char* vimg = kimg + IMG;
       // ---- S^T = K.Q^T
       f32x16 s[2];
 #pragma unroll
@@ -460,7 +482,7 @@ __global__ __launch_bounds__(512) void flash_attn_kernel(FlashAttnParams p) {
         const int row = 32 * kk + a_key;
 #pragma unroll
         for (int ds = 0; ds < NDS; ++ds) {
-          const uint4 a = *reinterpret_cast<const uint4*>(kimg + vimg_off(row, 2 * ds + hf));
+          const uint4 a = *reinterpret_cast<const uint4*>(kimg + FC::off(row, 2 * ds + hf));
           s[kk] = mfma32(as_bf16x8(a), qf[ds], s[kk]);
         }
       }
@@ -517,25 +539,28 @@ __global__ __launch_bounds__(512) void flash_attn_kernel(FlashAttnParams p) {
 #pragma unroll
           for (int dt = 0; dt < NDT; ++dt) {
             const int ch = 4 * dt + v_ch;
-            const uint2 lo = lds_tr16(vimg + vimg_off(kr0, ch) + v_sub);
-            const uint2 hi = lds_tr16(vimg + vimg_off(kr0 + 4, ch) + v_sub);
+            const uint2 lo = lds_tr16(vimg + FC::off(kr0, ch) + v_sub);
+            const uint2 hi = lds_tr16(vimg + FC::off(kr0 + 4, ch) + v_sub);
             oacc[dt] = mfma32(as_bf16x8(make_uint4(lo.x, lo.y, hi.x, hi.y)), pb[ks], oacc[dt]);
           }
         }
       }
       l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
-      if (t + kFSplit < nt) {
+      if (t + NS < nt) {
         store_tile((it + 1) & 1);
-        if (t + 2 * kFSplit < nt) load_tile((t + 2 * kFSplit) * kFK);
+        if (t + 2 * NS < nt) load_tile((t + 2 * NS) * kFK);
       }
     }
     __syncthreads();
   }
 
   // ---- merge the key splits through LDS (the tile images are free after the last barrier):
-  // split 1 publishes (m, l, O^T) per lane, split 0 combines and stores
-  float* mo = reinterpret_cast<float*>(smem) + w * (64 * (NDT * 16 + 2));
-  if (split == 1) {
+  // splits 1.. publish (m, l, O^T) per lane, split 0 combines and stores
+  constexpr int MO = 64 * (NDT * 16 + 2);  // floats per (split, query wave)
+  static_assert((NS - 1) * 4 * MO * 4 <= NS * 2 * 2 * IMG, "merge area fits the tile images");
+  float* mo_base = reinterpret_cast<float*>(smem) + w * MO;
+  if (split > 0) {
+    float* mo = mo_base + (split - 1) * 4 * MO;
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
@@ -544,17 +569,25 @@ __global__ __launch_bounds__(512) void flash_attn_kernel(FlashAttnParams p) {
     mo[(NDT * 16 + 1) * 64 + lane] = l_run;
   }
   __syncthreads();
-  if (split == 1) return;
+  if (split > 0) return;
   {
-    const float m1 = mo[(NDT * 16) * 64 + lane], l1 = mo[(NDT * 16 + 1) * 64 + lane];
-    const float m0 = first ? -INFINITY : m_run;
-    const float M = fmaxf(m0, m1);
-    const float a0 = __builtin_amdgcn_exp2f(m0 - M), a1 = __builtin_amdgcn_exp2f(m1 - M);
-    l_run = l_run * a0 + l1 * a1;
+    float M = first ? -INFINITY : m_run;
 #pragma unroll
-    for (int dt = 0; dt < NDT; ++dt)
+    for (int sp = 1; sp < NS; ++sp) M = fmaxf(M, mo_base[(sp - 1) * 4 * MO + (NDT * 16) * 64 + lane]);
+    const float a0 = __builtin_amdgcn_exp2f((first ? -INFINITY : m_run) - M);
+    l_run *= a0;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) oacc[dt][i] = oacc[dt][i] * a0 + mo[(dt * 16 + i) * 64 + lane] * a1;
+    for (int dt = 0; dt < NDT; ++dt) oacc[dt] *= a0;
+#pragma unroll
+    for (int sp = 1; sp < NS; ++sp) {
+      const float* mo = mo_base + (sp - 1) * 4 * MO;
+      const float a1 = __builtin_amdgcn_exp2f(mo[(NDT * 16) * 64 + lane] - M);
+      l_run += mo[(NDT * 16 + 1) * 64 + lane] * a1;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) oacc[dt][i] += mo[(dt * 16 + i) * 64 + lane] * a1;
+    }
   }
 
   // ---- epilogue: lane (col, hf) holds O^T[d][qi] for d = 32dt + (i&3) + 8(i>>2) + 4hf
@@ -594,13 +627,15 @@ extern "C" int vwa_decode_attention(const DecodeAttnParams* p, hipStream_t st) {
 extern "C" int vwa_flash_attention(const FlashAttnParams* p, hipStream_t st) {
   if (p->n_kv_heads <= 0 || p->n_q_heads % p->n_kv_heads) return -1;
   if (p->B <= 0 || p->Sq <= 0) return 0;
-  dim3 grid(((p->Sq + kFQ - 1) / kFQ) * p->n_q_heads * p->B), block(64 * 4 * kFSplit);
+  dim3 grid(((p->Sq + kFQ - 1) / kFQ) * p->n_q_heads * p->B);
   if (p->head_dim == 128) {
-    if (p->causal) hipLaunchKernelGGL((flash_attn_kernel<128, true>), grid, block, kFLds, st, *p);
-    else hipLaunchKernelGGL((flash_attn_kernel<128, false>), grid, block, kFLds, st, *p);
+    const dim3 block(256 * FlashCfg<128>::NS);
+    if (p->causal) hipLaunchKernelGGL((flash_attn_kernel<128, true>), grid, block, flash_lds<128>(), st, *p);
+    else hipLaunchKernelGGL((flash_attn_kernel<128, false>), grid, block, flash_lds<128>(), st, *p);
   } else if (p->head_dim == 64) {
-    if (p->causal) hipLaunchKernelGGL((flash_attn_kernel<64, true>), grid, block, kFLds, st, *p);
-    else hipLaunchKernelGGL((flash_attn_kernel<64, false>), grid, block, kFLds, st, *p);
+    const dim3 block(256 * FlashCfg<64>::NS);
+    if (p->causal) hipLaunchKernelGGL((flash_attn_kernel<64, true>), grid, block, flash_lds<64>(), st, *p);
+    else hipLaunchKernelGGL((flash_attn_kernel<64, false>), grid, block, flash_lds<64>(), st, *p);
   } else {
     return -3;
   }
