@@ -317,15 +317,18 @@ constexpr float kRescale = 8.f;  // deferred-max threshold (log2 units)
 //  D = 64: the guide's image (a) with 128-byte rows -- 8-row x 32-column subtiles of 512 B,
 //  off = 1024 (row >> 3) + 512 (ch >> 2) + 64 (row & 7) + 16 ((ch & 3) ^ ((row >> 2) & 3)): the same
 //  bank pattern as the 256-byte-row form (512 and 1024 are multiples of the 256-byte bank cycle),
-//  so its row and transposed reads stay conflict-free at half the bytes (8 KB per tile) ->
-//  3 splits (12 waves: 3 per SIMD, 96 KB).
+//  so its row and transposed reads stay conflict-free at half the bytes (8 KB per tile).
+// DEPTH: tiles in flight in registers per split (global -> register -> LDS staging).  The tile
+// fetch is latency-bound (one 16-32 KB tile per split per iteration, ~9 B/cycle/CU measured with
+// DEPTH 1), so D = 64 keeps two register sets (2 tiles ahead; +16 VGPRs) -- 3 splits at depth 1
+// measured no faster than 2 -- while D = 128 (32 VGPRs per set) has no room for a second.
 template <int D> struct FlashCfg;
 template <> struct FlashCfg<128> {
-  static constexpr int NS = 2, IMG = kFK * 256;
+  static constexpr int NS = 2, DEPTH = 1, IMG = kFK * 256;
   static VWA_DEVICE int off(int r, int ch) { return vimg_off(r, ch); }
 };
 template <> struct FlashCfg<64> {
-  static constexpr int NS = 3, IMG = kFK * 128;
+  static constexpr int NS = 2, DEPTH = 2, IMG = kFK * 128;
   static VWA_DEVICE int off(int r, int ch) {
     return 1024 * (r >> 3) + 512 * (ch >> 2) + 64 * (r & 7) + 16 * ((ch & 3) ^ ((r >> 2) & 3));
   }
@@ -404,7 +407,7 @@ __global__ __launch_bounds__(256 * FlashCfg<D>::NS) void flash_attn_kernel(Flash
   float m_run = 0.f, l_run = 0.f;
   __syncthreads();  // block table in LDS
 
-  uint4 kr[LPT], vr[LPT];
+  uint4 kra[LPT], vra[LPT], krb[LPT], vrb[LPT];  // register sets A, B (B: DEPTH 2 only)
   // loader: thread row r_i = (stid + 256 i) / NCH, chunk ch_i.  One block for the whole sequence
   // (contiguous K / V, e.g. the encoder): a fixed per-thread offset + t * stride_tok; paged with a
   // power-of-two block size: shifts; otherwise the general division.
@@ -415,7 +418,7 @@ __global__ __launch_bounds__(256 * FlashCfg<D>::NS) void flash_attn_kernel(Flash
   const int64_t blk0_off = one_block ? (int64_t)(tab_lds ? btab[0] : p.kv.block_table[(int64_t)b * p.kv.table_stride]) *
                                            p.kv.stride_block + head_off
                                      : 0;
-  auto load_tile = [&](int k0) {
+  auto load_tile = [&](int k0, uint4 (&kr)[LPT], uint4 (&vr)[LPT]) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int c = stid + i * 256;
@@ -438,7 +441,7 @@ __global__ __launch_bounds__(256 * FlashCfg<D>::NS) void flash_attn_kernel(Flash
       }
     }
   };
-  auto store_tile = [&](int stg) {
+  auto store_tile = [&](int stg, const uint4 (&kr)[LPT], const uint4 (&vr)[LPT]) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int c = stid + i * 256;
@@ -459,20 +462,47 @@ __global__ __launch_bounds__(256 * FlashCfg<D>::NS) void flash_attn_kernel(Flash
   const int v_ch = 2 * (grp & 1) + (p4 >> 1), v_sub = 8 * (p4 & 1);
 
   // split s: tiles s, s + 2, ...; every split runs the same iteration count (block-wide barriers)
+  constexpr int DEPTH = FC::DEPTH;
+  constexpr bool PRE = D == 64;  // all of a tile's LDS fragments in registers at once (D = 128: no room)
   const int iters = (nt + NS - 1) / NS;
   if (split < nt) {
-    load_tile(split * kFK);
-    store_tile(0);
-    if (split + NS < nt) load_tile((split + NS) * kFK);
+    load_tile(split * kFK, kra, vra);
+    store_tile(0, kra, vra);
+    if (split + NS < nt) load_tile((split + NS) * kFK, DEPTH == 2 ? krb : kra, DEPTH == 2 ? vrb : vra);
+    if (DEPTH == 2 && split + 2 * NS < nt) load_tile((split + 2 * NS) * kFK, kra, vra);
   }
   __syncthreads();
   bool first = true;
-  for (int it = 0; it < iters; ++it) {
+  // iteration `it` computes this split's local tile it from LDS stage it & 1, then stages local
+  // tile it + 1 (held in register set S) and refills S with local tile it + 1 + DEPTH
+  auto body = [&](int it, uint4 (&SK)[LPT], uint4 (&SV)[LPT]) {
     const int t = it * NS + split;
     if (t < nt) {
       const int k0 = t * kFK;
       const unsigned char* kimg = simg + (2 * (it & 1)) * IMG;
       const unsigned char* vimg = kimg + IMG;
+      // ---- every LDS fragment of the tile requested up front (D = 64: 64 VGPRs of K and V^T
+      // fragments), so no MFMA waits on a read issued right before it (the compiler-scheduled
+      // form waited lgkmcnt(0) before each P.V MFMA)
+      uint4 kf[2][NDS];
+      uint2 vf[2][2][NDT][2];
+      if constexpr (PRE) {
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int ds = 0; ds < NDS; ++ds)
+            kf[kk][ds] = *reinterpret_cast<const uint4*>(kimg + FC::off(32 * kk + a_key, 2 * ds + hf));
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int dt = 0; dt < NDT; ++dt) {
+              const int kr0 = 32 * kk + 16 * ks + v_key, ch = 4 * dt + v_ch;
+              vf[kk][ks][dt][0] = lds_tr16(vimg + FC::off(kr0, ch) + v_sub);
+              vf[kk][ks][dt][1] = lds_tr16(vimg + FC::off(kr0 + 4, ch) + v_sub);
+            }
+      }
       // ---- S^T = K.Q^T
       f32x16 s[2];
 #pragma unroll
@@ -482,7 +512,7 @@ __global__ __launch_bounds__(256 * FlashCfg<D>::NS) void flash_attn_kernel(Flash
         const int row = 32 * kk + a_key;
 #pragma unroll
         for (int ds = 0; ds < NDS; ++ds) {
-          const uint4 a = *reinterpret_cast<const uint4*>(kimg + FC::off(row, 2 * ds + hf));
+          const uint4 a = PRE ? kf[kk][ds] : *reinterpret_cast<const uint4*>(kimg + FC::off(row, 2 * ds + hf));
           s[kk] = mfma32(as_bf16x8(a), qf[ds], s[kk]);
         }
       }
@@ -539,19 +569,27 @@ __global__ __launch_bounds__(256 * FlashCfg<D>::NS) void flash_attn_kernel(Flash
 #pragma unroll
           for (int dt = 0; dt < NDT; ++dt) {
             const int ch = 4 * dt + v_ch;
-            const uint2 lo = lds_tr16(vimg + FC::off(kr0, ch) + v_sub);
-            const uint2 hi = lds_tr16(vimg + FC::off(kr0 + 4, ch) + v_sub);
+            const uint2 lo = PRE ? vf[kk][ks][dt][0] : lds_tr16(vimg + FC::off(kr0, ch) + v_sub);
+            const uint2 hi = PRE ? vf[kk][ks][dt][1] : lds_tr16(vimg + FC::off(kr0 + 4, ch) + v_sub);
             oacc[dt] = mfma32(as_bf16x8(make_uint4(lo.x, lo.y, hi.x, hi.y)), pb[ks], oacc[dt]);
           }
         }
       }
       l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
       if (t + NS < nt) {
-        store_tile((it + 1) & 1);
-        if (t + 2 * NS < nt) load_tile((t + 2 * NS) * kFK);
+        store_tile((it + 1) & 1, SK, SV);
+        if (t + (DEPTH + 1) * NS < nt) load_tile((t + (DEPTH + 1) * NS) * kFK, SK, SV);
       }
     }
     __syncthreads();
+  };
+  if constexpr (DEPTH == 2) {
+    for (int it = 0; it < iters; it += 2) {  // local tile it + 1 sits in B when it is even
+      body(it, krb, vrb);
+      if (it + 1 < iters) body(it + 1, kra, vra);
+    }
+  } else {
+    for (int it = 0; it < iters; ++it) body(it, kra, vra);
   }
 
   // ---- merge the key splits through LDS (the tile images are free after the last barrier):
