@@ -57,3 +57,59 @@ def test_streaming_with_real_engine_emits_deepgram_events():
     e = [e for e in evs if e["is_final"]][0]
     assert set(e) >= {"type", "is_final", "speech_final", "channel", "start", "duration"}
     assert isinstance(e["channel"]["alternatives"][0]["transcript"], str)
+
+
+def test_logmel_fragment_tables_match_direct_dft():
+    """ops.logmel_tables lays the DFT basis and the filterbank out in the f32-MFMA fragment order
+    audio.hip logmel_mfma_kernel reads (A: lane l -> row l & 15, k-step 4 s4 + j, sample 4 ks + l >> 4;
+    B: the same k, column l & 15): rebuilt from the fragments, they must be the plain matrices."""
+    import math
+
+    import numpy as np
+
+    from voice_enabled_browser_automation_amd import ops
+    from voice_enabled_browser_automation_amd.ops import reference as ref
+
+    for n_mels in (80, 128):
+        fb = ref.mel_filterbank(n_mels=n_mels)
+        basis, fbf = ops.logmel_tables(fb)
+        basis, fbf = basis.numpy(), fbf.numpy()
+        cos = np.zeros((400, 208))
+        sin = np.zeros((400, 208))
+        for T in range(26):
+            for s4 in range(25):
+                for lane in range(64):
+                    for j in range(4):
+                        n, b = 4 * (4 * s4 + j) + (lane >> 4), 16 * (T >> 1) + (lane & 15)
+                        (cos if T % 2 == 0 else sin)[n, b] = basis[T, s4, lane, j]
+        nn, bb = np.arange(400)[:, None], np.arange(201)[None, :]
+        assert np.allclose(cos[:, :201], np.cos(2 * math.pi * nn * bb / 400), atol=1e-6)
+        assert np.allclose(sin[:, :201], np.sin(2 * math.pi * nn * bb / 400), atol=1e-6)
+        assert not cos[:, 201:].any() and not sin[:, 201:].any()
+        fbm = np.zeros((fbf.shape[0] * 16, 208))
+        for t in range(fbf.shape[0]):
+            for s4 in range(13):
+                for lane in range(64):
+                    for j in range(4):
+                        fbm[16 * t + (lane & 15), 4 * (4 * s4 + j) + (lane >> 4)] = fbf[t, s4, lane, j]
+        assert np.allclose(fbm[:n_mels, :201], fb.numpy(), atol=0)
+        assert not fbm[n_mels:].any() and not fbm[:, 201:].any()
+
+
+def test_conv_padded_path_matches_plain_on_cpu():
+    """The stem's padded-row buffers (ops.padded_rows) + channel-padded weights give the plain
+    conv1d_gelu result (CPU reference path: the same contract the GPU implicit GEMM relies on)."""
+    import torch
+
+    from voice_enabled_browser_automation_amd import ops
+
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 50, 80, generator=g).to(torch.bfloat16)
+    w = (torch.randn(64, 3 * 80, generator=g) * 0.05).to(torch.bfloat16)
+    b = torch.randn(64, generator=g).to(torch.bfloat16)
+    plain = ops.conv1d_gelu(x, w, b, stride=1)
+    cp = ops.conv_channels(80)
+    _, xv = ops.padded_rows(2, 50, cp, dtype=torch.bfloat16, device="cpu")
+    xv[:, :, :80] = x
+    padded = ops.conv1d_gelu(xv, ops.pad_conv_weight(w, cp), b, stride=1, padded=True)
+    assert torch.allclose(plain.float(), padded.float(), atol=2e-2)
