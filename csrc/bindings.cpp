@@ -249,7 +249,9 @@ void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi,
     TORCH_CHECK(ws->is_cuda() && ws->scalar_type() == at::kFloat && ws->is_contiguous(), "ws f32");
     p.ws = ws->data_ptr<float>();
     p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws->numel());
+    p.ws_cap = ws->numel();
   }
+  p.cus = device_cus(x);
   check_rc(vwa_gemm((int)epi, &p, cur_stream(x)), "gemm");
 }
 
@@ -1103,6 +1105,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("s_o") = py::none(), py::arg("s_gu") = py::none(), py::arg("s_down") = py::none(),
         py::arg("s_qkv") = py::none(), py::arg("tp_ar") = 0);
   m.def("set_small_gemm_bytes", &set_small_gemm_bytes);
+  m.def("gemm_set_p8", [](int64_t mode) { vwa_gemm_set_p8((int)mode); });
   m.def("chain_make_seq", &chain_make_seq, py::arg("seq"), py::arg("X"), py::arg("W"), py::arg("bias"),
         py::arg("ln_c"), py::arg("Y"), py::arg("epi"), py::arg("eps"), py::arg("n_heads"), py::arg("head_dim"),
         py::arg("positions"), py::arg("slots"), py::arg("k_cache"), py::arg("v_cache"), py::arg("bar"),

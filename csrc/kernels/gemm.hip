@@ -176,6 +176,64 @@ VWA_DEVICE void compute_stage(const char* buf, f32x4 (&acc)[C::FM][C::FN], int w
   }
 }
 
+// ---- 256 x 256 tile, 8 waves (2 x 4, each 128 x 64), 8-phase software pipeline (the guide's
+// "256^2 8-phase template": the 128^2 two-barrier loop above is capped near 900 TF/s because each
+// stage's DMA is drained by the barrier that publishes it).  A stage (one bf16 half k-group, 64
+// deep) is four half-tile images of 16 KB -- A-lo (rows 0-127), A-hi (rows 128-255), B-lo
+// (n-tiles 0-7), B-hi (8-15) -- in the same layouts as the 128^2 kernel.  Each stage runs 4
+// phases of 16 MFMAs per wave (one C quadrant: 4 row x 2 column fragments x 2 k-substeps):
+//   P0 reads A 0-3 + B 0-1, P1 B 2-3, P2 A 4-7, P3 B 0-1 (A stays in registers across P0/P1 and
+//   P2/P3), with the next stages' half-tiles DMA'd behind them: P0 A-hi + B-lo and P1 B-hi of
+//   stage s+1 (into the other buffer, free since the end of stage s-1), P3 A-lo of stage s+2
+//   (into this buffer: its A halves were last read in P2).  The only wait on the DMA is a counted
+//   vmcnt in P3 (A-lo of s+2 stays in flight).  The two wave groups (M halves) run one barrier
+//   apart, so one group's LDS reads overlap the other group's MFMAs; every phase retires its reads
+//   (lgkmcnt) before its first barrier, so a restage issued after that barrier by the other group
+//   cannot overwrite bytes still being read, and every staged byte is read after a barrier that
+//   follows every issuing wave's counted wait.
+constexpr int kP8Half = 16384;
+using CfgP8 = Cfg<256, 256, 2, 4>;
+
+// half-tile `which` (0 A-lo, 1 A-hi, 2 B-lo, 3 B-hi) of stage hs into the stage image `st`:
+// 16 wave-instructions of 1 KB = 2 per wave (tiled bf16 weights only)
+VWA_DEVICE void p8_issue(const GemmParams& p, __amdgpu_buffer_rsrc_t rx, __amdgpu_buffer_rsrc_t rw, int bm, int bn,
+                         int hs, int which, char* st) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int kg = hs >> 1, h = hs & 1;
+  const int kgn = p.K / BKG;
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int q = it * 8 + w;
+    if (which < 2) {
+      const int qa = 16 * which + q;  // rows 8 qa .. 8 qa + 7
+      const int r = 8 * qa + (lane >> 3), c = (lane & 7) ^ swz((r >> 1) & 7);
+      const int m = bm + r;
+      const unsigned off =
+          (unsigned)(((size_t)m * p.ldx + (size_t)kg * BKG + 32 * (c >> 1) + 16 * h + 8 * (c & 1)) * 2);
+      dma16(rx, st + qa * 1024, m < p.M ? off : 0xFFFFFFF0u);
+    } else {
+      const int tile = 8 * (which - 2) + (q >> 1), sp = q & 1;
+      const int T = (bn >> 4) + tile;
+      const unsigned off =
+          T * 16 < p.N ? (unsigned)((((size_t)T * kgn + kg) * 2048 + (2 * h + sp) * 512 + lane * 8) * 2) : 0xFFFFFFF0u;
+      dma16(rw, st + CfgP8::A_BYTES + (2 * tile + sp) * 1024, off);
+    }
+  }
+}
+
+// one phase: 16 MFMAs acc[i0 .. i0+3][j0 .. j0+1] over both k-substeps of the stage
+template <int I0, int J0>
+VWA_DEVICE void p8_mfma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2], const bf16x8 (&b)[2][2]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int sp = 0; sp < 2; ++sp)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[I0 + i][J0 + j] = mfma16(a[i][sp], b[j][sp], acc[I0 + i][J0 + j]);
+  __builtin_amdgcn_s_setprio(0);
+}
+
 VWA_DEVICE float bias_at(const GemmParams& p, int n) { return p.bias ? bf2f(p.bias[n]) : 0.f; }
 
 template <int EPI>
@@ -187,7 +245,7 @@ VWA_DEVICE void store_out(const GemmParams& p, int m, int n, float v) {
     reinterpret_cast<u16*>(p.Y)[(size_t)m * p.ldy + n] = f2bf(v);
 }
 
-template <class C, int EPI, bool WT, bool F8 = false>
+template <class C, int EPI, bool WT, bool F8 = false, bool P8 = false>
 __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   constexpr int FM = C::FM, FN = C::FN;
@@ -219,6 +277,82 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
   // X extent: the last row starts at (M-1)*ldx and is K long (rows may overlap: conv views)
   const __amdgpu_buffer_rsrc_t rx = rsrc(p.X, ((size_t)(p.M - 1) * p.ldx + p.K) * (F8 ? 1 : 2));
   const __amdgpu_buffer_rsrc_t rw = rsrc(p.W, (size_t)p.N * p.K * (F8 ? 1 : 2));
+  if constexpr (P8) {
+    static_assert(C::BM == 256 && C::BN == 256 && C::NW == 8 && WT && !F8, "8-phase pipeline: CfgP8, tiled bf16");
+    const int l = lane_id(), rl = l & 15, g = l >> 4;
+    auto stage = [&](int s) { return lds + (s & 1) * C::STAGE; };
+    if (nh > 0) {
+#pragma unroll
+      for (int hq = 0; hq < 4; ++hq) p8_issue(p, rx, rw, bm, bn, h0, hq, stage(0));
+    }
+    if (nh > 1) p8_issue(p, rx, rw, bm, bn, h0 + 1, 0, stage(1));
+    if (nh > 1) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    bf16x8 a[4][2], b[2][2];
+    if (wm == 1) asm volatile("s_barrier" ::: "memory");  // group 1 runs one barrier behind group 0
+    for (int s = 0; s < nh; ++s) {
+      const char* st = stage(s);
+      const char* la = st + (wm * 128 + rl) * 128;
+      const char* lb = st + C::A_BYTES + (wn * 4) * 2048 + l * 16;
+      auto read_a = [&](int i0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int sp = 0; sp < 2; ++sp)
+            a[i][sp] = *reinterpret_cast<const bf16x8*>(la + (i0 + i) * 16 * 128 + (((2 * g + sp) ^ swz(rl >> 1)) << 4));
+      };
+      auto read_b = [&](int j0) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int sp = 0; sp < 2; ++sp) b[j][sp] = *reinterpret_cast<const bf16x8*>(lb + (j0 + j) * 2048 + sp * 1024);
+      };
+      const bool n1 = s + 1 < nh, n2 = s + 2 < nh;
+      // phase = operand reads (+ DMA issue) ; lgkmcnt(0) ; barrier ; 16 MFMAs ; barrier.  The two
+      // wave groups (wm) run one barrier apart, so one group's reads overlap the other's MFMAs, and
+      // a buffer's reads are retired (lgkmcnt) before the barrier that lets the other group restage it
+      // P0
+      read_a(0);
+      read_b(0);
+      if (n1) {
+        p8_issue(p, rx, rw, bm, bn, h0 + s + 1, 1, stage(s + 1));
+        p8_issue(p, rx, rw, bm, bn, h0 + s + 1, 2, stage(s + 1));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      p8_mfma<0, 0>(acc, a, b);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_barrier" ::: "memory");
+      // P1
+      read_b(2);
+      if (n1) p8_issue(p, rx, rw, bm, bn, h0 + s + 1, 3, stage(s + 1));
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      p8_mfma<0, 2>(acc, a, b);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_barrier" ::: "memory");
+      // P2
+      read_a(4);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      p8_mfma<4, 2>(acc, a, b);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_barrier" ::: "memory");
+      // P3 (A-lo of this buffer was last read in P2: restage it with stage s + 2).  Stage s + 1 has
+      // landed for this wave (only A-lo of s + 2 may stay in flight) before this phase's first
+      // barrier; with the groups a barrier apart every wave has waited by the barrier that ends the
+      // phase, and the next stage is read only after it
+      read_b(0);
+      if (n2) p8_issue(p, rx, rw, bm, bn, h0 + s + 2, 0, stage(s + 2));
+      __builtin_amdgcn_sched_barrier(0);
+      if (n2) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      p8_mfma<4, 0>(acc, a, b);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_barrier" ::: "memory");
+    }
+    if (wm == 0) asm volatile("s_barrier" ::: "memory");  // (group 1 started one barrier later)
+  } else {
   if (nh > 0) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0, lds);
   if (nh > 1) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + 1, lds + C::STAGE);
   for (int i = 0; i < nh; ++i) {
@@ -229,6 +363,7 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
     compute_stage<C, F8>(lds + (i & 1) * C::STAGE, acc, wm, wn);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done reading it
     if (i + 2 < nh) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + i + 2, lds + (i & 1) * C::STAGE);
+  }
   }
   const int l = lane_id();
   const int col0 = bn + wn * FN * 16 + (l & 15);
@@ -406,9 +541,22 @@ int launch_cfg(const GemmParams& p, hipStream_t st) {
   return 0;
 }
 
+int g_p8_mode = 2;  // 0: never, 1: every eligible shape, 2: the measured rule (p8_auto)
+
+// Shapes the 8-phase 256^2 kernel takes: tiled bf16 weights, N % 256, one batch
+bool p8_eligible(const GemmParams& p) {
+  return p.w_tiled && !p.sw && p.N % 256 == 0 && p.nbatch <= 1 && p.M >= 256;
+}
+
 template <int EPI>
-int launch_epi(const GemmParams& p, hipStream_t st) {
-  launch_cfg<CfgS, EPI>(p, st);
+int launch_epi(const GemmParams& p, hipStream_t st, bool p8) {
+  if (p8) {
+    const int tiles = ((p.M + 255) / 256) * (p.N / 256);
+    hipLaunchKernelGGL((gemm_kernel<CfgP8, EPI, true, false, true>), dim3(tiles * p.splits), dim3(CfgP8::THREADS),
+                       CfgP8::LDS, st, p);
+  } else {
+    launch_cfg<CfgS, EPI>(p, st);
+  }
   if (p.splits > 1) {
     const int64_t n = (int64_t)p.M * (EPI == EPI_SWIGLU ? p.N / 2 : p.N);
     hipLaunchKernelGGL((gemm_reduce_kernel<EPI>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
@@ -428,6 +576,8 @@ extern "C" int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats) 
   return s;
 }
 
+extern "C" void vwa_gemm_set_p8(int mode) { g_p8_mode = mode; }
+
 extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
   GemmParams p = *pp;
   if (p.M < 1 || p.N < 16 || p.N % 16 || p.K < BKG || p.K % BKG) return -10;
@@ -436,17 +586,31 @@ extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
   if (p.sw && (!p.sx || !p.w_tiled)) return -14;  // W8A8: per-row X scales and the fp8 tiled layout
   if (epi == EPI_SWIGLU && (p.N % 32 || p.y_f32)) return -12;
   if (p.splits < 1) p.splits = 1;
+  // 8-phase 256^2 kernel: the prompt-sized shapes whose 256^2 tiles alone fill the CUs (mode 2:
+  // >= 256 tiles, e.g. the 1011-row gate/up; tools/bench_gemm.py), any eligible shape in mode 1
+  // (split-K as for the 128^2 kernel when the workspace allows)
+  bool p8 = false;
+  if (g_p8_mode && p8_eligible(p)) {
+    const int tiles8 = ((p.M + 255) / 256) * (p.N / 256);
+    if (g_p8_mode == 1 || tiles8 >= 256) {
+      p8 = true;
+      int s = 1;
+      const int KGs = p.K / BKG;
+      while (p.ws && tiles8 * s < p.cus && s * 2 <= KGs && (int64_t)(s * 2) * p.M * p.N <= p.ws_cap) s *= 2;
+      p.splits = s;
+    }
+  }
   const int KG = p.K / BKG;
   p.kg_per_split = (KG + p.splits - 1) / p.splits;
   p.splits = (KG + p.kg_per_split - 1) / p.kg_per_split;  // no empty slice
   if (p.splits > 1 && !p.ws) return -13;
   if (p.nbatch > 1 && p.splits > 1) return -15;  // batched launches take no split-K
   switch (epi) {
-    case EPI_STORE: return launch_epi<EPI_STORE>(p, st);
-    case EPI_RESID: return launch_epi<EPI_RESID>(p, st);
-    case EPI_SWIGLU: return launch_epi<EPI_SWIGLU>(p, st);
-    case EPI_GELU: return launch_epi<EPI_GELU>(p, st);
-    case EPI_GELU_RESID: return launch_epi<EPI_GELU_RESID>(p, st);
+    case EPI_STORE: return launch_epi<EPI_STORE>(p, st, p8);
+    case EPI_RESID: return launch_epi<EPI_RESID>(p, st, p8);
+    case EPI_SWIGLU: return launch_epi<EPI_SWIGLU>(p, st, p8);
+    case EPI_GELU: return launch_epi<EPI_GELU>(p, st, p8);
+    case EPI_GELU_RESID: return launch_epi<EPI_GELU_RESID>(p, st, p8);
     default: return -3;
   }
 }

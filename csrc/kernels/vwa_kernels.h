@@ -145,6 +145,7 @@ struct GemmParams {
   // X rows may overlap (ldx < K: the Whisper conv stem as an implicit GEMM, row t = the 3 input
   // rows t*stride-1 .. t*stride+1 of a zero-padded channels-last buffer)
   int nbatch; int64_t bsx, bsy, bsr;
+  int cus; int64_t ws_cap;  // CU count and workspace floats (split-K choice of the 256^2 kernel)
 };
 
 struct FlashAttnParams {
@@ -169,6 +170,7 @@ int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g,
                      int xg2 = 0, int f8 = 0);
 int vwa_gemm(int epi, const GemmParams* p, hipStream_t st);
 int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats);
+void vwa_gemm_set_p8(int mode);  // 0: 128^2 kernel only, 1: 256^2 8-phase wherever eligible, 2: measured rule
 int vwa_row_rstd(const uint16_t* x, int ldx, int M, int K, float eps, float* rstd, hipStream_t st);
 int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,
                 uint16_t* y, int rows, int D, int ldx, float eps, hipStream_t st);

@@ -632,6 +632,41 @@ def test_tiled_mfma_gemm_epilogues(M, tiled):
     close(got, exp, 2e-2)
 
 
+@pytest.mark.parametrize("M", [256, 300, 1011])
+def test_gemm_8phase_256_tile(M):
+    """The 256 x 256 8-phase pipelined GEMM (gemm.hip P8; forced on every eligible shape) on
+    pre-tiled weights: every epilogue, split-K (few tiles) and a partial last row block, against
+    the f32 reference -- then back to the measured routing."""
+    E = ops.ext()
+    E.gemm_set_p8(1)
+    try:
+        for (N, K) in ((512, 4096), (4096, 1024), (2048, 512)):
+            x = rnd(M, K)
+            w = rnd(N, K, scale=K ** -0.5)
+            wt = ops.TiledWeight(w)
+            b = rnd(N, scale=0.1)
+            xc, wc, bc = x.cpu(), w.cpu(), b.cpu()
+            for act, fuse in (("none", False), ("gelu", True)):
+                out = torch.empty(M, N, dtype=BF, device=DEV)
+                ops.linear(x, wt, b, out=out, act=act, fuse_rms=fuse)
+                exp = torch.empty(M, N, dtype=BF)
+                ref.linear(xc, wc, bc, out=exp, act=act, fuse_rms=fuse)
+                close(out, exp, 2e-2)
+            res = rnd(M, N)
+            exp = torch.empty(M, N, dtype=BF)
+            ref.linear(xc, wc, None, out=exp, residual=res.cpu())
+            ops.linear(x, wt, out=res, residual=res)
+            close(res, exp, 3e-2)
+        gu = ops.interleave_gate_up(rnd(1024, 1024, scale=0.03), rnd(1024, 1024, scale=0.03))
+        x = rnd(M, 1024)
+        got = ops.linear_swiglu(x, ops.TiledWeight(gu), fuse_rms=True)
+        exp = torch.empty(M, 1024, dtype=BF)
+        ref.linear_swiglu(x.cpu(), gu.cpu(), fuse_rms=True, out=exp)
+        close(got, exp, 2e-2)
+    finally:
+        E.gemm_set_p8(2)
+
+
 def test_gemm_replaces_hipblaslt(monkeypatch):
     """No projection of > 16 rows reaches torch.matmul (hipBLASLt) any more."""
     def boom(*a, **k):

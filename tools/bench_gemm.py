@@ -54,11 +54,17 @@ def main():
         tw = ops.TiledWeight(w)
         out = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
         t_ref = timeit(lambda: torch.matmul(x, w.t()))
+        ops.ext().gemm_set_p8(0)
+        t_128 = timeit(lambda: ops.gemm(x, tw, out))
+        ops.ext().gemm_set_p8(1)
+        t_p8 = timeit(lambda: ops.gemm(x, tw, out)) if M >= 256 and N % 256 == 0 else None
+        ops.ext().gemm_set_p8(2)
         t_own = timeit(lambda: ops.gemm(x, tw, out))
         ref = torch.matmul(x.float(), w.float().t())
         err = (out.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
         fl = 2.0 * M * N * K
         r = dict(shape=name, M=M, N=N, K=K, hipblaslt_us=round(t_ref, 1), gemm_us=round(t_own, 1),
+                 tile128_us=round(t_128, 1), tile256_8phase_us=None if t_p8 is None else round(t_p8, 1),
                  speedup=round(t_ref / t_own, 3), gemm_tflops=round(fl / t_own / 1e6, 1),
                  gemm_weight_tbps=round(N * K * 2 / t_own / 1e6, 2), rel_err=round(err, 5))
         rows.append(r)
