@@ -54,6 +54,9 @@ def ext():
         impl = os.environ.get("VWA_ATTN_IMPL")
         if impl:
             m.set_attention_impl(ATTENTION_IMPLS[impl])
+        p8 = os.environ.get("VWA_GEMM_P8")  # 0: 128x128 GEMM only, 1: 256x256 8-phase wherever eligible
+        if p8 not in (None, ""):
+            m.gemm_set_p8(int(p8))
         _EXT = m
         return m
     except BaseException as e:  # noqa: BLE001
