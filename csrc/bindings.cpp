@@ -39,7 +39,7 @@ void check_rc(int rc, const char* what) { TORCH_CHECK(rc == 0, what, " launch fa
 // skinny GEMM dispatch: 1 = persistent streaming kernel when the shape fits (default), 0 = one-tile kernel
 int g_skinny_mode = 1;
 int g_grid_cap = 256;
-int g_ks = 8;
+int g_ks = 0;  // K-split waves of the streaming kernel; 0 = by shape (skinny_ks)
 int g_w_first = 2;  // 0: never, 1: only with the fused RMSNorm prologue, 2: always (measured best)
 void set_skinny_mode(int64_t mode, int64_t grid_cap, int64_t ks, int64_t w_first) {
   g_skinny_mode = (int)mode;
@@ -54,13 +54,19 @@ size_t g_small_bytes = 4u << 20;
 void set_small_gemm_bytes(int64_t n) { g_small_bytes = (size_t)(n > 0 ? n : 0); }
 // Also every K < 1024: the streaming kernel splits K over its 8 waves in 128-wide groups, so
 // with fewer than 8 groups most of its waves idle (Whisper-tiny's 40 MB LM head, K = 384).
+// Streaming-kernel K split: 4 waves when K < 2048, else 8.  Its waves take 128-wide k-groups, so
+// at K = 1280 (Whisper-large-v3's decoder) 8 waves leave 6 idle in the second round; measured
+// (tools/bench_whisper_decode.py, tiled weights, HBM-resident) 6.45 vs 6.83 us for QKV, 8.33 vs
+// 8.97 for fc1, 27.9 vs 34.2 for the 133 MB LM head; K >= 4096 (Llama) stays at 8.
+int skinny_ks(const SkinnyParams& p) { return g_ks ? g_ks : (p.K < 2048 ? 4 : 8); }
+
 bool small_gemm(const SkinnyParams& p) {
   return !p.w_scale && g_small_bytes && p.M <= 16 && ((size_t)p.N * p.K * 2 <= g_small_bytes || p.K < 1024);
 }
 
 int run_skinny(int epi, const SkinnyParams& p, hipStream_t st) {
   if (g_skinny_mode == 1 && !small_gemm(p)) {
-    const int r = vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
+    const int r = vwa_skinny_stream(epi, &p, g_grid_cap, skinny_ks(p), st);
     if (r != -10) return r;
   }
   return vwa_skinny_gemm(epi, &p, st);
@@ -107,8 +113,8 @@ SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<T
 // silent bf16 fallback (the Python layer routes those shapes to the dequantising path).
 int run_skinny_checked(int epi, const SkinnyParams& p, hipStream_t st) {
   // pre-tiled weights (bf16 or fp8) exist only for the streaming kernel (a shape it rejects is an error)
-  if (p.w_tiled) return vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
-  if (p.w_scale || (p.fuse_rms == 2 && !small_gemm(p))) return vwa_skinny_stream(epi, &p, g_grid_cap, g_ks, st);
+  if (p.w_tiled) return vwa_skinny_stream(epi, &p, g_grid_cap, skinny_ks(p), st);
+  if (p.w_scale || (p.fuse_rms == 2 && !small_gemm(p))) return vwa_skinny_stream(epi, &p, g_grid_cap, skinny_ks(p), st);
   return run_skinny(epi, p, st);
 }
 
@@ -545,7 +551,7 @@ std::tuple<Tensor, int64_t> chain_make_seq(int64_t seq, std::vector<Tensor> X, s
                                            std::vector<int64_t> epi, double eps, int64_t n_heads, int64_t head_dim,
                                            c10::optional<Tensor> positions, c10::optional<Tensor> slots,
                                            c10::optional<Tensor> k_cache, c10::optional<Tensor> v_cache, Tensor bar,
-                                           Tensor work, int64_t bar_mode) {
+                                           Tensor work, int64_t bar_mode, bool w_tiled) {
   const size_t n = X.size();
   TORCH_CHECK(n >= 2 && n <= (size_t)kChainMaxPhases && W.size() == n && bias.size() == n && ln_c.size() == n &&
                   Y.size() == n && epi.size() == n,
@@ -562,7 +568,7 @@ std::tuple<Tensor, int64_t> chain_make_seq(int64_t seq, std::vector<Tensor> X, s
   for (size_t i = 0; i < n; ++i) {
     TORCH_CHECK(X[i].size(0) == M && Y[i].size(0) == M, "row counts differ");
     SkinnyParams& p = cp.ph[i].p;
-    p = base_params(X[i], W[i], bias[i], false, eps);
+    p = base_params(X[i], W[i], bias[i], false, eps, c10::nullopt, w_tiled);
     cp.ph[i].epi = (int)epi[i];
     set_ln_fold(p, ln_c[i], (int)epi[i]);
     if (epi[i] == 4) {
@@ -1109,7 +1115,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("chain_make_seq", &chain_make_seq, py::arg("seq"), py::arg("X"), py::arg("W"), py::arg("bias"),
         py::arg("ln_c"), py::arg("Y"), py::arg("epi"), py::arg("eps"), py::arg("n_heads"), py::arg("head_dim"),
         py::arg("positions"), py::arg("slots"), py::arg("k_cache"), py::arg("v_cache"), py::arg("bar"),
-        py::arg("work"), py::arg("bar_mode") = 1);
+        py::arg("work"), py::arg("bar_mode") = 1, py::arg("w_tiled") = false);
   m.def("chain_run", &chain_run, py::arg("desc"), py::arg("n_phases"), py::arg("lds"), py::arg("like"),
         py::arg("attn_g") = 0, py::arg("seq") = 0);
   m.def("alloc_uncached_i32", &alloc_uncached_i32);
@@ -1136,7 +1142,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pcm16_to_f32", &pcm16_to_f32);
   m.def("log_mel", &log_mel);
   m.def("conv1d_gelu", &conv1d_gelu);
-  m.def("set_skinny_mode", &set_skinny_mode, py::arg("mode"), py::arg("grid_cap") = 256, py::arg("ks") = 8,
+  m.def("set_skinny_mode", &set_skinny_mode, py::arg("mode"), py::arg("grid_cap") = 256, py::arg("ks") = 0,
         py::arg("w_first") = 2);
   m.def("attention_split_tokens", []() { return vwa_attention_split_tokens(); });
   m.def("set_attention_impl", [](int64_t impl) { vwa_set_attention_impl((int)impl); });

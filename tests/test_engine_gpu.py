@@ -336,6 +336,39 @@ def test_whisper_chained_decoder_matches_per_kernel_path(name, monkeypatch):
         assert err < 0.02 * (1 + b.abs().max().item()), err
 
 
+@pytest.mark.parametrize("chain", [False, True])
+def test_whisper_tiled_decoder_matches_row_major(chain, monkeypatch):
+    """Decode-step weights in the pre-tiled layout (large models: WhisperModel._tile_decoder; the
+    streaming kernel with the 4-wave K split at K = 1280) give the logits of the row-major
+    decoder on the same weights -- per-kernel path and chained launches."""
+    import dataclasses
+
+    from voice_enabled_browser_automation_amd.asr.engine import WhisperRunner
+
+    ops.ext()
+    cfg = dataclasses.replace(get_config("whisper-large-v3"), n_enc_layers=1, n_dec_layers=2)
+    m_rm = WhisperModel(cfg, device="cuda", seed=5, tile_decoder=False)
+    m_t = WhisperModel(cfg, device="cuda", seed=5, tile_decoder=True)
+    assert m_t.dec_tiled and not m_rm.dec_tiled and isinstance(m_t.dec[0].fc2, ops.TiledWeight)
+    torch.manual_seed(2)
+    enc = torch.randn(1, cfg.n_audio_ctx, cfg.d_model, device="cuda").to(torch.bfloat16)
+    runners = []
+
+    def run(m, ch):
+        monkeypatch.setenv("VWA_CHAIN_ASR", "1" if ch else "0")
+        r = WhisperRunner(m, max_sessions=1, use_graphs=False)
+        runners.append(r)
+        r.set_cross(0, enc)
+        return [r.step([(0, (11 * p) % 1000, p)]).float().cpu().clone() for p in range(4)]
+
+    ref = run(m_rm, False)
+    got = run(m_t, chain)
+    assert not m_t.chain_error()
+    for a, b in zip(got, ref):
+        err = (a - b).abs().max().item()
+        assert err < 0.02 * (1 + b.abs().max().item()), err
+
+
 def test_chain_is_rearmed_after_backoff(monkeypatch):
     """After a fallback the engine re-arms the chained launch (fresh barrier counters) once the
     backoff has passed; the re-armed chained steps match an engine that never chained."""

@@ -39,7 +39,7 @@ def skinny_mode(request):
     ops.ext().set_skinny_mode(*request.param)
     ops.ext().set_small_gemm_bytes(0)  # every shape on the selected kernel (no small-weight routing)
     yield request.param
-    ops.ext().set_skinny_mode(1, 256, 8, 2)
+    ops.ext().set_skinny_mode(1, 256, 0, 2)
     ops.ext().set_small_gemm_bytes(4 << 20)
 
 

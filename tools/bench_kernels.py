@@ -67,7 +67,7 @@ def main():
             for mode, cap, ks in ((0, 256, 8), (1, 256, 8), (1, 512, 4), (1, 768, 4)):
                 ops.ext().set_skinny_mode(mode, cap, ks)
                 variants[f"m{mode}_g{cap}_k{ks}"] = round(timeit(ours), 2)
-            ops.ext().set_skinny_mode(1, 256, 8)
+            ops.ext().set_skinny_mode(1, 256, 0)
 
             def blas():
                 it[0] = (it[0] + 1) % ncopy
@@ -96,7 +96,7 @@ def main():
             ops.ext().set_skinny_mode(mode, cap, ks)
             variants[f"m{mode}_g{cap}_k{ks}"] = round(timeit(lambda: ops.ext().skinny_gemm(x, w, None, y, 0, False,
                                                                                              1e-5, None)), 2)
-        ops.ext().set_skinny_mode(1, 256, 8)
+        ops.ext().set_skinny_mode(1, 256, 0)
         ops.ext().set_small_gemm_bytes(4 << 20)
         r = dict(kernel="skinny_small", shape=name, M=1, N=N, K=K, variants=variants)
         print(json.dumps(r), flush=True)
@@ -126,7 +126,7 @@ def main():
                         ops.ext().skinny_gemm(x, ws[it[0]], None, y, 0, rms, 1e-5, None)
                     ops.ext().set_skinny_mode(1, 256, 8, wf)
                     out[f"rms{int(rms)}_wf{wf}"] = round(timeit(f), 2)
-            ops.ext().set_skinny_mode(1, 256, 8, 2)
+            ops.ext().set_skinny_mode(1, 256, 0, 2)
             del ws
             r = dict(kernel="prologue_order", shape=name, M=M, **out)
             print(json.dumps(r), flush=True)

@@ -38,7 +38,7 @@ def main():
             res.setdefault(name, {}).setdefault(str(cap), []).append(round(us, 2))
         del ws
         torch.cuda.empty_cache()
-    E.set_skinny_mode(1, 256, 8, 2)
+    E.set_skinny_mode(1, 256, 0, 2)
     print(json.dumps({"kernel": "grid_probe", "us": res}))
 
 

@@ -65,7 +65,7 @@ class DecLayer:
 
 class WhisperModel:
     def __init__(self, cfg: WhisperConfig, *, device="cpu", dtype=torch.bfloat16, seed: int = 0,
-                 weights=None):
+                 weights=None, tile_decoder: Optional[bool] = None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
@@ -135,6 +135,16 @@ class WhisperModel:
                 L.qkv, L.o, L.fc1, L.fc2 = (ops.TiledWeight(t) for t in (L.qkv, L.o, L.fc1, L.fc2))
         else:
             self.conv2_wt = self.conv2_w
+        # decode-step weights in the pre-tiled layout when they stream from HBM (more than the
+        # 256 MB Infinity Cache per token: large-v3's 1.5 GB); cache-resident small models keep the
+        # row-major layout for the one-tile kernel.  Measured per layer at M = 1 (tools/
+        # bench_whisper_decode.py, K = 1280): QKV 8.1 -> 6.5 us, fc1 11.2 -> 8.3, fc2 12.3 -> 9.6,
+        # LM head 43 -> 28 (tiled + the 4-wave K split).
+        if tile_decoder is None:
+            tile_decoder = self.decoder_bytes() > (256 << 20)
+        self.dec_tiled = bool(tile_decoder) and self.device.type == "cuda"
+        if self.dec_tiled:
+            self._tile_decoder()
 
     def _load(self, w) -> None:
         """HF WhisperForConditionalGeneration names (safetensors, runtime.weights.LazySafetensors)."""
@@ -197,6 +207,22 @@ class WhisperModel:
             L.f_xq = fold(L.xq, L.xq_b, L.lnx_w, L.lnx_b)
             L.f_fc1 = fold(L.fc1, L.fc1_b, L.ln2_w, L.ln2_b)
         self.f_lm = fold(self.lm_head, None, self.dec_ln_w, self.dec_ln_b)
+
+    def decoder_bytes(self) -> int:
+        """Weight bytes one decode step streams (decoder projections + LM head)."""
+        n = sum(t.numel() for L in self.dec for t in (L.qkv, L.o, L.xq, L.xo, L.fc1, L.fc2))
+        return (n + self.lm_head.numel()) * self.lm_head.element_size()
+
+    def _tile_decoder(self) -> None:
+        """Decode-path projections -> TiledWeight (the folded QKV / cross-query / fc1 / LM head
+        copies and the out-proj / fc2 weights); the unfolded copies stay row-major for the
+        prompt-sized paths and checkpoint round trips."""
+        T = ops.TiledWeight
+        for L in self.dec:
+            L.o, L.xo, L.fc2 = T(L.o), T(L.xo), T(L.fc2)
+            L.f_qkv, L.f_xq, L.f_fc1 = ((T(w), b, c) for (w, b, c) in (L.f_qkv, L.f_xq, L.f_fc1))
+        w, b, c = self.f_lm
+        self.f_lm = (T(w), b, c)
 
     # ------------------------------------------------------------------ encoder
     def log_mel(self, audio: torch.Tensor, n_frames: int = 3000, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -313,13 +339,16 @@ class WhisperModel:
         common = dict(eps=eps, n_heads=self.H, head_dim=self.hd, bar=self._chain_bar, work=self._chain_work,
                       bar_mode=self._chain_bar_mode)
         (wq, bq, cq), (w1, b1, c1) = L.f_xq, L.f_fc1
-        mid = ops.ext().chain_make_seq(2, [att, x], [L.o, wq], [L.o_b, bq], [None, cq], [x, q], [1, 0],
+        common["w_tiled"] = self.dec_tiled
+        wt = lambda t: t.t if isinstance(t, ops.TiledWeight) else t  # noqa: E731
+        mid = ops.ext().chain_make_seq(2, [att, x], [wt(L.o), wt(wq)], [L.o_b, bq], [None, cq], [x, q], [1, 0],
                                        positions=None, slots=None, k_cache=None, v_cache=None, **common)
-        X, W, B, C, Y, E = [att, x, f], [L.xo, w1, L.fc2], [L.xo_b, b1, L.fc2_b], [None, c1, None], [x, f, x], [1, 3, 1]
+        X, W, B, C, Y, E = ([att, x, f], [wt(L.xo), wt(w1), wt(L.fc2)], [L.xo_b, b1, L.fc2_b], [None, c1, None],
+                            [x, f, x], [1, 3, 1])
         nxt = li + 1 < len(self.dec)
         if nxt:
             wn, bn, cn = self.dec[li + 1].f_qkv
-            X, W, B, C, Y, E = X + [x], W + [wn], B + [bn], C + [cn], Y + [q], E + [4]
+            X, W, B, C, Y, E = X + [x], W + [wt(wn)], B + [bn], C + [cn], Y + [q], E + [4]
         tail = ops.ext().chain_make_seq(1, X, W, B, C, Y, E, positions=bufs.positions if nxt else None,
                                         slots=bufs.slots if nxt else None,
                                         k_cache=bufs.k_cache[li + 1] if nxt else None,
