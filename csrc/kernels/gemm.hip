@@ -586,17 +586,19 @@ extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
   if (p.sw && (!p.sx || !p.w_tiled)) return -14;  // W8A8: per-row X scales and the fp8 tiled layout
   if (epi == EPI_SWIGLU && (p.N % 32 || p.y_f32)) return -12;
   if (p.splits < 1) p.splits = 1;
-  // 8-phase 256^2 kernel: the prompt-sized shapes whose 256^2 tiles alone fill the CUs (mode 2:
-  // >= 256 tiles, e.g. the 1011-row gate/up; tools/bench_gemm.py), any eligible shape in mode 1
-  // (split-K as for the 128^2 kernel when the workspace allows)
+  // 8-phase 256^2 kernel (mode 2, measured rule, tools/bench_gemm.py): the prompt-sized shapes
+  // whose 256^2 tiles alone fill the CUs (>= 256 tiles, e.g. the 1011-row gate/up), or fill them
+  // with split-K slices of >= 2048 K each (the 1011-row down projection, K = 14336: 4 slices,
+  // 118.5 vs 140.4 us on the 128^2 kernel and 122.5 for hipBLASLt; shorter slices lose to the
+  // f32 partial traffic: o / QKV at K = 4096 58 / 92 vs 45 / 60 us).  Mode 1: every eligible shape.
   bool p8 = false;
   if (g_p8_mode && p8_eligible(p)) {
     const int tiles8 = ((p.M + 255) / 256) * (p.N / 256);
-    if (g_p8_mode == 1 || tiles8 >= 256) {
+    int s = 1;
+    const int KGs = p.K / BKG;
+    while (p.ws && tiles8 * s < p.cus && s * 2 <= KGs && (int64_t)(s * 2) * p.M * p.N <= p.ws_cap) s *= 2;
+    if (g_p8_mode == 1 || tiles8 >= 256 || (p.cus > 0 && tiles8 * s >= p.cus && p.K / s >= 2048)) {
       p8 = true;
-      int s = 1;
-      const int KGs = p.K / BKG;
-      while (p.ws && tiles8 * s < p.cus && s * 2 <= KGs && (int64_t)(s * 2) * p.M * p.N <= p.ws_cap) s *= 2;
       p.splits = s;
     }
   }

@@ -369,7 +369,7 @@ def scratch(device, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
     return t[:numel]
 
 
-GEMM_WS_FLOATS = 8 << 20  # split-K workspace (32 MB per device)
+GEMM_WS_FLOATS = 32 << 20  # split-K workspace (128 MB per device: 4 f32 slices of a 1k x 4096 output)
 _GEMM_EPI = {"none": 0, "resid": 1, "swiglu": 2, "gelu": 3}
 
 
