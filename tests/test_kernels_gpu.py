@@ -667,6 +667,19 @@ def test_gemm_8phase_256_tile(M):
         E.gemm_set_p8(2)
 
 
+def test_gemm_8phase_split_k_down_projection():
+    """Measured routing (mode 2): the 1011-row Llama-3-8B down projection (K = 14336) runs the
+    8-phase kernel in 4 split-K slices with the residual applied by the reduce kernel -- against
+    an f32 reference (GPU fp32 matmul of the same bf16 operands)."""
+    M, N, K = 1011, 4096, 14336
+    x = rnd(M, K)
+    w = rnd(N, K, scale=K ** -0.5)
+    res = rnd(M, N)
+    exp = (x.float() @ w.float().t() + res.float())
+    ops.linear(x, ops.TiledWeight(w), out=res, residual=res)
+    close(res, exp, 3e-2)
+
+
 def test_gemm_replaces_hipblaslt(monkeypatch):
     """No projection of > 16 rows reaches torch.matmul (hipBLASLt) any more."""
     def boom(*a, **k):
