@@ -58,7 +58,16 @@ class StepBuffers:
         # needs a single H2D copy: [tokens | positions | seq_ids | ctx_lens | slots (int64) | sel]
         # (sel = the rows whose logits the step returns: one per sequence, not one per token row)
         R = max_rows
-        self.meta = torch.zeros(7 * R, **i32)
+        # per-ROW copy of each row's sequence block table (chained attention: read in the same round
+        # trip as seq_ids / ctx_lens instead of a dependent table load); <= 128 blocks per sequence.
+        # It sits right behind the step metadata in ONE buffer (device and pinned host alike), so a
+        # step's upload is one copy node (measured in the bench trace: two copies were 2 + 3 us of
+        # GPU time plus a 4 us scheduling gap per decode step)
+        self.rt_cols = max_blocks_per_seq if max_blocks_per_seq <= 128 and max_blocks_per_seq % 2 == 0 else 0
+        C = max(2, self.rt_cols)
+        T = (7 * R + 15) // 16 * 16  # row table at a 64-byte aligned offset
+        self.meta_all = torch.zeros(T + R * C, **i32)
+        self.meta = self.meta_all[: 7 * R]
         self.tokens = self.meta[0:R]
         self.positions = self.meta[R : 2 * R]
         self.seq_ids = self.meta[2 * R : 3 * R]
@@ -81,15 +90,13 @@ class StepBuffers:
         self.part_ml = torch.zeros(max_rows * ns * model.nq * 2, dtype=torch.float32, device=device)
         self.attn_cnt = torch.zeros(max_rows * model.nkv, dtype=torch.int32, device=device)  # chunk tickets
         pin = torch.device(device).type == "cuda"
-        self.h_meta = torch.zeros(7 * R, dtype=torch.int32, pin_memory=pin)
+        self.h_meta_all = torch.zeros(T + R * C, dtype=torch.int32, pin_memory=pin)
+        self.h_meta = self.h_meta_all[: 7 * R]
         self.h_i32 = self.h_meta[: 4 * R].view(4, R)
         self.h_slots = self.h_meta[4 * R : 6 * R].view(torch.int64)
         self.h_sel = self.h_meta[6 * R :]
-        # per-ROW copy of each row's sequence block table (chained attention: read in the same round
-        # trip as seq_ids / ctx_lens instead of a dependent table load); <= 128 blocks per sequence
-        self.rt_cols = max_blocks_per_seq if max_blocks_per_seq <= 128 and max_blocks_per_seq % 2 == 0 else 0
-        self.row_table = torch.zeros(max_rows, max(2, self.rt_cols), **i32)
-        self.h_row_table = torch.zeros(max_rows, max(2, self.rt_cols), dtype=torch.int32, pin_memory=pin)
+        self.row_table = self.meta_all[T:].view(R, C)
+        self.h_row_table = self.h_meta_all[T:].view(R, C)
         self.np_row_table = self.h_row_table.numpy()
         self.h_i32[3].fill_(1)  # the same inert rows as the device copy (captured graphs upload it)
         self.h_slots.fill_(-1)
@@ -211,9 +218,10 @@ class LLMEngine:
         if upload_meta:
             # inside a captured graph: the pinned -> device metadata copy is the graph's first node,
             # so a replay is one host call instead of a copy + a replay
-            self.bufs.meta.copy_(self.bufs.h_meta, non_blocking=True)
-            if self.bufs.rt_cols and M <= 4:
-                self.bufs.row_table[:M].copy_(self.bufs.h_row_table[:M], non_blocking=True)
+            b = self.bufs
+            n = (b.meta_all.numel() - b.row_table.numel() + M * b.row_table.shape[1]) if b.rt_cols and M <= 4 \
+                else b.meta.numel()
+            b.meta_all[:n].copy_(b.h_meta_all[:n], non_blocking=True)
         return self.model.forward(self.bufs, M, self.kv, n_sel=None if L == M else L, head=False)
 
     def _capture(self, M: int, L: int):
