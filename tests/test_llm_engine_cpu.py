@@ -203,3 +203,51 @@ def test_sampler_fail_word_marks_every_row():
     assert out.tolist() == logits.argmax(-1).tolist()
     ops.sample(logits, fail_word=torch.ones(1, dtype=torch.int64), **kw)
     assert out.tolist() == [-2, -2, -2]
+
+
+def test_reference_attention_matches_per_head_loops():
+    """The CPU attention (ops/reference.py: every head of a row in one batched product, one K/V
+    gather per sequence) equals plain per-(row, head) softmax(q K^T) V over the paged cache --
+    GQA, ragged contexts, rows of one sequence at different positions, a contiguous-layout
+    causal prefill."""
+    import math
+
+    import torch
+
+    from voice_enabled_browser_automation_amd import ops
+    from voice_enabled_browser_automation_amd.ops import reference as ref
+
+    g = torch.Generator().manual_seed(0)
+    nq, nkv, D, bs, nblk = 8, 2, 32, 4, 40
+    kc = torch.randn(nblk, nkv, bs, D, generator=g)
+    vc = torch.randn(nblk, nkv, bs, D, generator=g)
+    table = torch.randperm(nblk, generator=g)[:24].view(2, 12).to(torch.int32)
+    kv = ops.KVLayout.paged(kc, vc, table)
+    ctx = torch.tensor([5, 6, 7, 30, 1], dtype=torch.int32)
+    sid = torch.tensor([0, 0, 0, 1, 1], dtype=torch.int32)
+    q = torch.randn(5, nq * D, generator=g)
+    out = torch.empty_like(q)
+    ref.decode_attention(q, kv, ctx, sid, n_q_heads=nq, n_kv_heads=nkv, head_dim=D, scale=D ** -0.5, out=out)
+    G = nq // nkv
+    for r in range(5):
+        n, s = int(ctx[r]), int(sid[r])
+        toks = [(int(table[s, t // bs]), t % bs) for t in range(n)]
+        for h in range(nq):
+            K = torch.stack([kc[b, h // G, o] for b, o in toks])
+            V = torch.stack([vc[b, h // G, o] for b, o in toks])
+            p = torch.softmax(K @ q[r, h * D:(h + 1) * D] / math.sqrt(D), 0)
+            assert torch.allclose(out[r, h * D:(h + 1) * D], p @ V, atol=1e-5)
+    # contiguous [B, S, H, D] layout, causal with a query offset
+    B, S, Sq = 2, 9, 4
+    k = torch.randn(B, S, nkv, D, generator=g)
+    v = torch.randn(B, S, nkv, D, generator=g)
+    qq = torch.randn(B, Sq, nq, D, generator=g)
+    o = torch.empty_like(qq)
+    ref.flash_attention(qq, ops.KVLayout.contiguous(k, v, torch.arange(B, dtype=torch.int32)[:, None]), Sk=S,
+                        n_kv_heads=nkv, causal=True, scale=D ** -0.5, q_offset=S - Sq, out=o)
+    for b in range(B):
+        for i in range(Sq):
+            for h in range(nq):
+                n = S - Sq + i + 1
+                p = torch.softmax(k[b, :n, h // G] @ qq[b, i, h] / math.sqrt(D), 0)
+                assert torch.allclose(o[b, i, h], p @ v[b, :n, h // G], atol=1e-5)

@@ -280,11 +280,17 @@ def permute_qkv_rows(w: torch.Tensor, n_heads_total: int, head_dim: int) -> torc
     return w[full].contiguous()
 
 
+_UNPERM: dict = {}
+
+
 def unpermute_qkv_cols(y: torch.Tensor, n_heads_total: int, head_dim: int) -> torch.Tensor:
-    perm = qkv_row_perm(head_dim).to(y.device)
-    inv = torch.empty_like(perm)
-    inv[perm] = torch.arange(head_dim, device=y.device)
-    full = torch.cat([inv + h * head_dim for h in range(n_heads_total)])
+    key = (n_heads_total, head_dim, str(y.device))
+    full = _UNPERM.get(key)
+    if full is None:  # (a pure function of the sizes: built once, the CPU decode calls it per layer)
+        perm = qkv_row_perm(head_dim)
+        inv = torch.empty_like(perm)
+        inv[perm] = torch.arange(head_dim)
+        full = _UNPERM[key] = torch.cat([inv + h * head_dim for h in range(n_heads_total)]).to(y.device)
     return y[..., full]
 
 

@@ -120,41 +120,53 @@ def embedding(ids, table, *, pos_table=None, positions=None, vocab_start=0, out)
     return out
 
 
-def _gather_kv(kv, seq: int, kvh: int, n: int):
-    """Return K, V [n, D] (f32) for tokens 0..n-1 of table row `seq`, kv head kvh."""
-    if n == 0:
-        return None, None
+def _flat(x):
+    """The whole storage of x as a 1-D view (strided views: offsets are relative to x's first element)."""
+    n_el = x.untyped_storage().nbytes() // x.element_size()
+    return x.as_strided((n_el,), (1,), 0)[x.storage_offset():]
+
+
+def _gather_kv_heads(kv, seq: int, n: int, heads: int):
+    """K, V [heads, n, D] (f32) for tokens 0..n-1 of table row `seq`, every kv head at once: the
+    cache storage viewed as [blocks, heads, block_size, D] (the layout's strides), the sequence's
+    blocks picked with one index_select."""
     bs = kv.block_size
     D = kv.k.shape[-1]
-    t = torch.arange(n)
-    blk = kv.table[seq].long()[t // bs]
-    off = blk * kv.sb + kvh * kv.sh + (t % bs) * kv.st
-    idx = off[:, None] + torch.arange(D)[None, :]
+    nb = (n + bs - 1) // bs
+    blk = kv.table[seq][:nb].long()
 
-    def flat(x):  # the whole storage (strided views: offsets are relative to the view's first element)
-        n_el = x.untyped_storage().nbytes() // x.element_size()
-        return x.as_strided((n_el,), (1,), 0)[x.storage_offset():]
+    def g(x):
+        n_el = x.untyped_storage().nbytes() // x.element_size() - x.storage_offset()
+        nblocks = (n_el - (heads - 1) * kv.sh - (bs - 1) * kv.st - D) // kv.sb + 1
+        v = x.as_strided((nblocks, heads, bs, D), (kv.sb, kv.sh, kv.st, 1), x.storage_offset())
+        return v.index_select(0, blk).permute(1, 0, 2, 3).reshape(heads, nb * bs, D)[:, :n].float()
 
-    return flat(kv.k)[idx].float(), flat(kv.v)[idx].float()
+    return g(kv.k), g(kv.v)
 
 
 def decode_attention(q, kv, ctx_lens, seq_ids, *, n_q_heads, n_kv_heads, head_dim, scale, out):
+    """Per row: softmax(q K^T * scale) V over the row's first ctx_len cached tokens, every head of
+    the row in one batched product (GQA: G query heads per kv head).  Rows of one sequence share
+    one gather of its K/V (the longest context among them)."""
     rows = q.shape[0]
     G = n_q_heads // n_kv_heads
+    ctx = [int(c) for c in ctx_lens[:rows]]
+    sids = [int(s) for s in seq_ids[:rows]]
+    cache = {}
     for r in range(rows):
-        n = int(ctx_lens[r])
-        seq = int(seq_ids[r])
-        for kvh in range(n_kv_heads):
-            K, V = _gather_kv(kv, seq, kvh, n)
-            for g in range(G):
-                h = kvh * G + g
-                qv = q[r, h * head_dim : (h + 1) * head_dim].float()
-                if K is None:
-                    o = torch.zeros(head_dim)
-                else:
-                    p = torch.softmax((K @ qv) * scale, dim=0)
-                    o = p @ V
-                out[r, h * head_dim : (h + 1) * head_dim] = o.to(out.dtype)
+        n, seq = ctx[r], sids[r]
+        if n == 0:
+            out[r, : n_q_heads * head_dim] = 0
+            continue
+        if seq not in cache:
+            nmax = max(c for c, s in zip(ctx, sids) if s == seq)
+            cache[seq] = _gather_kv_heads(kv, seq, nmax, n_kv_heads)
+        K, V = cache[seq]
+        K, V = K[:, :n], V[:, :n]
+        qv = q[r, : n_q_heads * head_dim].float().view(n_kv_heads, G, head_dim)
+        p = torch.softmax(torch.einsum("hgd,hnd->hgn", qv, K) * scale, dim=-1)
+        o = torch.einsum("hgn,hnd->hgd", p, V)
+        out[r, : n_q_heads * head_dim] = o.reshape(-1).to(out.dtype)
     return out
 
 
@@ -164,18 +176,16 @@ def flash_attention(q, kv, *, Sk, n_kv_heads, causal, scale, q_offset=0, out, k_
     for b in range(B):
         sk = int(k_lens[b]) if k_lens is not None else Sk
         qo = int(q_offsets[b]) if q_offsets is not None else q_offset
-        for kvh in range(n_kv_heads):
-            K, V = _gather_kv(kv, b, kvh, sk)
-            for g in range(G):
-                h = kvh * G + g
-                qq = q[b, :, h, :].float()
-                s = (qq @ K.t()) * scale
-                if causal:
-                    qi = torch.arange(Sq)[:, None] + qo
-                    kj = torch.arange(sk)[None, :]
-                    s = s.masked_fill(kj > qi, float("-inf"))
-                p = torch.softmax(s, dim=-1)
-                out[b, :, h, :] = (p @ V).to(out.dtype)
+        K, V = _gather_kv_heads(kv, b, sk, n_kv_heads)  # [Hkv, sk, D]
+        qq = q[b].float().view(Sq, n_kv_heads, G, D)
+        s = torch.einsum("qhgd,hkd->hgqk", qq, K) * scale
+        if causal:
+            qi = torch.arange(Sq)[:, None] + qo
+            kj = torch.arange(sk)[None, :]
+            s = s.masked_fill(kj > qi, float("-inf"))
+        p = torch.softmax(s, dim=-1)
+        o = torch.einsum("hgqk,hkd->qhgd", p, V)
+        out[b] = o.reshape(Sq, Hq, D).to(out.dtype)
     return out
 
 
