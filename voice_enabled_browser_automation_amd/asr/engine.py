@@ -158,7 +158,7 @@ class AsrEngine:
         # device-resident single-session decode loop (graphs keyed by (slot, eot allowed))
         self.loop_out = torch.zeros(max(448, cfg.n_text_ctx), dtype=torch.int32, device=dev)
         self.loop_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.loop_graphs: Dict[Tuple[int, bool], torch.cuda.CUDAGraph] = {}
+        self.loop_graphs: Dict[Tuple[int, bool, int], torch.cuda.CUDAGraph] = {}
         self.device_loop = self.runner.use_graphs and ops.env_flag("VWA_ASR_DEVICE_LOOP", True)
         self.last_stats: Dict[str, float] = {}
         self.free_slots = list(range(max_sessions - 1, -1, -1))
@@ -198,8 +198,10 @@ class AsrEngine:
         ops.ext().decode_advance(b.tokens, b.positions, b.ctx_lens, b.slots, self.d_tok, self.loop_out,
                                  self.loop_cnt, 1 + slot * self.runner.bps, self.runner.bs)
 
-    def _loop_graph(self, slot: int, allow_eot: bool) -> "torch.cuda.CUDAGraph":
-        key = (slot, allow_eot)
+    LOOP_STEPS = 4  # decode steps per replayed loop graph (graph-to-graph launch gap ~10 us per replay)
+
+    def _loop_graph(self, slot: int, allow_eot: bool, steps: int = 1) -> "torch.cuda.CUDAGraph":
+        key = (slot, allow_eot, steps)
         g = self.loop_graphs.get(key)
         if g is None:
             r = self.runner
@@ -218,7 +220,8 @@ class AsrEngine:
             if r.pool is None:
                 r.pool = torch.cuda.graph_pool_handle()
             with torch.cuda.graph(g, pool=r.pool):
-                self._loop_step(slot, allow_eot)
+                for _ in range(steps):  # identical steps: each reads what the previous advanced
+                    self._loop_step(slot, allow_eot)
             self.loop_graphs[key] = g
         return g
 
@@ -234,6 +237,8 @@ class AsrEngine:
         if n_max <= 0:
             return []
         g = self._loop_graph(slot, not exact)
+        K = self.LOOP_STEPS
+        gk = self._loop_graph(slot, not exact, K) if K > 1 else None
         # row 0 = this session at the last prompt position; the first advance moves it to P
         b.seq_ids[:1].fill_(slot)
         b.positions[:1].fill_(P - 1)
@@ -243,7 +248,12 @@ class AsrEngine:
         done = 1
         chunk = n_max if exact else 8
         while True:
-            for _ in range(min(chunk, n_max - done)):
+            todo = min(chunk, n_max - done)
+            while gk is not None and todo >= K:  # K steps per replay (never past n_max)
+                gk.replay()
+                done += K
+                todo -= K
+            for _ in range(todo):
                 g.replay()
                 done += 1
             toks = self.loop_out[:done].tolist()
