@@ -1433,7 +1433,9 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
       if (!(cp->seq == 0 && i == 2 && ph.epi == EPI_RESID && p.w_tiled && p.fuse_rms == 0)) return -10;
       ph.xg = 1;
     }
-    if (ph.xg && f8) return -10;
+    // (X streaming has only the attention-less instantiation: a 70B down projection at 3-4 rows
+    // -- 28672-wide X rows -- is chained with the decode attention as its own launch instead)
+    if (ph.xg && (f8 || cp->attn_g > 0)) return -10;
     const int U = ph.xg ? 2 : R / 4 / ph.nt * (f8 ? 2 : 1);
     if ((size_t)p.N * p.K * 2 >= 0x7FFFFFF0ull || (size_t)p.M * p.ldx * 2 >= 0x7FFFFFF0ull) return -10;
     const int G = p.K / 128;

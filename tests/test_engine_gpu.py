@@ -195,6 +195,44 @@ def test_chained_layer_tail_matches_per_kernel_path(cfg, monkeypatch):
         assert err < 0.02 * (1 + b.abs().max().item()), err
 
 
+def test_llama70b_shape_chained_layers_match_f32_reference():
+    """Llama-3-70B layer shapes (hidden 8192, 64 q / 8 kv heads -> GQA 8:1, FFN 28672; BASELINE
+    config 4 at TP=1) through the chained decode launch -- decode attention as phase 0 at 1-2
+    rows, the tail alone with a separate attention launch at 3-4 rows, where the 28672-wide down
+    rows no longer fit LDS next to the attention -- against the CPU f32 reference engine on the
+    same bf16 weights (2 layers, small vocab)."""
+    import copy
+
+    ops.ext()
+    torch.manual_seed(0)
+    cfg = LlamaConfig(name="t70", vocab_size=4096, hidden=8192, n_layers=2, n_heads=64, n_kv_heads=8, head_dim=128,
+                      ffn=28672, max_pos=2048)
+    toks = torch.randint(0, cfg.vocab_size, (40,)).tolist()
+    cpu = LlamaModel(cfg, device="cpu", seed=3)
+    gpu = copy.deepcopy(cpu)
+    move_model(gpu, "cuda")
+    gpu._tile_weights()
+
+    def run(model):
+        e = LLMEngine(model, max_seqs=2, max_model_len=256, kv_blocks=20, block_size=16)
+        s = e.new_sequence(toks[:30], use_prefix_cache=False)
+        out, i = [e.prefill(s).float().cpu().clone()], 30
+        for n in (1, 2, 3, 4):
+            out.append(e.run_rows([(s, t) for t in toks[i:i + n]]).float().cpu().clone())
+            i += n
+        return out, e
+
+    ref, _ = run(cpu)
+    got, e = run(gpu)
+    assert not gpu.chain_error()
+    descs = gpu.chain_descs()
+    assert descs and all(v is not None for v in descs), "a 70B-shape step left the chained launch"
+    assert any(v[3] == 8 for v in descs), "no step chained the GQA-8 decode attention"
+    for i, (a, b) in enumerate(zip(got, ref)):
+        err = (a - b).abs().max().item()
+        assert err < 0.03 * (1 + b.abs().max().item()), (i, err)
+
+
 def test_chain_timeout_falls_back_to_per_kernel_launches():
     """A grid-barrier timeout (error word set by the chained kernel) switches the model to the
     per-kernel path and drops the captured graphs (runtime/engine.py _check_chain)."""

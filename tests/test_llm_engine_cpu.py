@@ -251,3 +251,43 @@ def test_reference_attention_matches_per_head_loops():
                 n = S - Sq + i + 1
                 p = torch.softmax(k[b, :n, h // G] @ qq[b, i, h] / math.sqrt(D), 0)
                 assert torch.allclose(o[b, i, h], p @ v[b, :n, h // G], atol=1e-5)
+
+
+def test_batched_admission_prefill_matches_serial_prefill():
+    """runtime/engine.py prefill_batch: several requests' prompt suffixes behind a cached prefix in
+    ONE ragged forward (> 64 rows: eager scratch forward, attention in 64-row slices; <= 64 rows:
+    a step bucket) leave the same K/V -- and hence the same next-token logits -- as one prefill per
+    request; a cold prompt among them takes the single-sequence path."""
+    torch.manual_seed(0)
+    m = LlamaModel(SMALL, device="cpu", seed=3)
+    head = torch.randint(0, 512, (64,)).tolist()
+    tails = [torch.randint(0, 512, (n,)).tolist() for n in (40, 33, 27)]
+    cold = torch.randint(0, 512, (80,)).tolist()
+
+    def make():
+        e = LLMEngine(m, max_seqs=5, max_model_len=256, kv_blocks=120, block_size=16)
+        s0 = e.new_sequence(head)
+        e.prefill(s0)
+        e.free_sequence(s0)  # publishes the shared head to the prefix cache
+        seqs = [e.new_sequence(head + t) for t in tails] + [e.new_sequence(cold)]
+        assert all(s.n_computed == 64 for s in seqs[:3]) and seqs[3].n_computed == 0
+        return e, seqs
+
+    def next_logits(e, seqs):
+        return [e.run_rows([(s, 7)]).float().clone() for s in seqs]
+
+    eA, sA = make()
+    for s in sA:
+        eA.prefill(s)
+    want = next_logits(eA, sA)
+    eB, sB = make()
+    eB.prefill_batch([(s, len(s.tokens)) for s in sB])  # 100 suffix rows + one cold prompt
+    assert [s.n_computed for s in sB] == [len(s.tokens) for s in sB]
+    assert eB.stats["batched_prefills"] == 1
+    got = next_logits(eB, sB)
+    for a, b in zip(got, want):
+        assert torch.allclose(a, b, atol=2e-2, rtol=2e-2), (a - b).abs().max()
+    eC, sC = make()
+    eC.prefill_batch([(s, len(s.tokens)) for s in sC[1:3]])  # 60 rows: one step-bucket forward
+    for a, b in zip(next_logits(eC, sC[1:3]), want[1:3]):
+        assert torch.allclose(a, b, atol=2e-2, rtol=2e-2), (a - b).abs().max()

@@ -2,6 +2,7 @@
 
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29556 \
         tools/tp_check.py
+    VWA_TP_CHECK_CFG=70b VWA_TP_CHECK_LAYERS=2 python -m torch.distributed.run --nproc-per-node 8 ... tools/tp_check.py
 Every rank builds the TP shard of the same random model (deterministic per-layer generator),
 runs prefill + ragged decode through the engine -- eagerly AND with every decode step replayed
 from a hipGraph -- with the one-shot IPC all-reduce for the vocab-parallel embedding and the
@@ -27,8 +28,19 @@ from voice_enabled_browser_automation_amd.models.llama import LlamaModel  # noqa
 from voice_enabled_browser_automation_amd.parallel.tp import TPContext, init_distributed  # noqa: E402
 from voice_enabled_browser_automation_amd.runtime.engine import LLMEngine  # noqa: E402
 
-CFG = LlamaConfig(name="tp", vocab_size=4096, hidden=512, n_layers=3, n_heads=8, n_kv_heads=4, head_dim=64,
-                  ffn=1024, max_pos=1024)
+CFGS = {
+    "small": LlamaConfig(name="tp", vocab_size=4096, hidden=512, n_layers=3, n_heads=8, n_kv_heads=4, head_dim=64,
+                         ffn=1024, max_pos=1024),
+    # Llama-3-70B layer shapes (hidden 8192, 64 q / 8 kv heads, FFN 28672, vocab 128256): at TP=8
+    # every rank holds 8 q heads, 1 kv head, an FFN slice of 3584 and a 16032-token vocab shard
+    "70b": LlamaConfig(name="tp70b", vocab_size=128256, hidden=8192, n_layers=3, n_heads=64, n_kv_heads=8,
+                       head_dim=128, ffn=28672, max_pos=1024),
+}
+CFG = CFGS[os.environ.get("VWA_TP_CHECK_CFG", "small")]
+if os.environ.get("VWA_TP_CHECK_LAYERS"):
+    import dataclasses
+
+    CFG = dataclasses.replace(CFG, n_layers=int(os.environ["VWA_TP_CHECK_LAYERS"]))
 
 
 def run(model, toks, graphs):

@@ -164,20 +164,29 @@ class LLMIntentEngine:
             r.feed += ftoks
 
     def _admit(self, r: IntentRequest) -> None:
+        """Admit one request on its own (prefill included)."""
+        self._admit_begin(r)
+        self.engine.prefill(r.seq, upto=len(r.ids) - 1)
+        self._admit_end(r)
+
+    def _admit_begin(self, r: IntentRequest) -> None:
+        """Prompt -> sequence (prefix-cache match) + grammar matcher; the prefill is left to the
+        caller (batched over every request admitted in the same iteration)."""
         eng = self.engine
         r.t_start = time.perf_counter()
         r.ids = self._encode_prompt(r.messages)
-        r.seq = eng.new_sequence(r.ids)
-        r.cached = r.seq.n_computed
-        if r.cached >= len(r.ids):  # whole prompt cached: recompute its last token for logits
-            r.seq.n_computed = r.cached = len(r.ids) - 1
-        eng.prefill(r.seq, upto=len(r.ids) - 1)  # the last prompt token joins the batched step
-        r.t_first = time.perf_counter()
         r.matcher = self.grammar.matcher(self.budget_chars)
         if r.matcher.min_completion() > self.budget_chars:
             raise IntentEngineError(f"budget_chars={self.budget_chars} is below the shortest schema-valid "
                                     f"answer ({r.matcher.min_completion()} chars)")
-        r.feed = [r.ids[-1]]
+        r.seq = eng.new_sequence(r.ids)
+        r.cached = r.seq.n_computed
+        if r.cached >= len(r.ids):  # whole prompt cached: recompute its last token for logits
+            r.seq.n_computed = r.cached = len(r.ids) - 1
+
+    def _admit_end(self, r: IntentRequest) -> None:
+        r.t_first = time.perf_counter()
+        r.feed = [r.ids[-1]]  # the last prompt token joins the batched step
         self._jump_forward(r)
 
     def _finish(self, r: IntentRequest, error: Optional[BaseException] = None) -> None:
@@ -212,17 +221,33 @@ class LLMIntentEngine:
     def step(self) -> List[IntentRequest]:
         """One scheduler iteration; returns the requests that finished in it."""
         finished: List[IntentRequest] = []
-        while len(self.active) < self.max_active:
+        admitted: List[IntentRequest] = []
+        while len(self.active) + len(admitted) < self.max_active:
             with self._lock:
                 if not self.waiting:
                     break
                 r = self.waiting.popleft()
             try:
-                self._admit(r)
-                self.active.append(r)
+                self._admit_begin(r)
+                admitted.append(r)
             except Exception as e:  # noqa: BLE001
                 self._finish(r, e)
                 finished.append(r)
+        if admitted:
+            # ONE batched prefill of every admitted request's prompt suffix (all but its last
+            # token, which joins the decode step below)
+            try:
+                self.engine.prefill_batch([(r.seq, len(r.ids) - 1) for r in admitted])
+            except Exception as e:  # noqa: BLE001
+                if getattr(getattr(self.engine.model, "tp", None), "size", 1) > 1:
+                    raise  # TP: lockstep is lost -- brain/tp_engine.py ends the group
+                for r in admitted:
+                    self._finish(r, e)
+                    finished.append(r)
+                admitted = []
+            for r in admitted:
+                self._admit_end(r)
+                self.active.append(r)
         if not self.active:
             return finished
         # rows: each request's pending tokens; requests that do not fit wait one iteration, a

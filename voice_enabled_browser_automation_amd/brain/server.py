@@ -28,6 +28,7 @@ from ..contracts import ParseRequest, ParseResponse, safe_parse
 from ..utils.context import cap_context
 from ..utils.metrics import Metrics
 from .prompt import messages_for
+from .tp_engine import TPIntentEngine  # noqa: F401  (re-exported: the TP control plane)
 
 SERVICE_NAME = "brain-ts"  # byte-compatible /health payload (apps/brain/src/server.ts:87)
 
@@ -41,6 +42,9 @@ def build_app(engine: Any = None) -> web.Application:
     app["metrics"] = Metrics("brain")
 
     async def health(_req: web.Request) -> web.Response:
+        failed = getattr(app["engine"], "failed", None)
+        if failed is not None:  # a TP group that lost lockstep: the process is about to exit
+            return web.json_response({"status": "error", "service": SERVICE_NAME, "detail": str(failed)}, status=503)
         return web.json_response({"status": "ok", "service": SERVICE_NAME})
 
     async def metrics(_req: web.Request) -> web.Response:
@@ -159,55 +163,6 @@ def build_llm_engine(model_name: Optional[str] = None, device: Optional[str] = N
     eng.capture_all()
     ie = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=budget, chat_format=llama3_chat)
     return TPIntentEngine(ie, tp) if tp.size > 1 else ie
-
-
-class TPIntentEngine:
-    """Control plane for a tensor-parallel brain: rank 0 serves HTTP and broadcasts every request
-    (chat messages) to the TP workers over a CPU (gloo) group; all ranks then run the identical,
-    deterministic decode loop in lockstep (identical all-gathered logits + seeds -> identical
-    tokens), so the RCCL collectives inside each step always match up."""
-
-    def __init__(self, inner, tp):
-        import torch.distributed as dist
-
-        self.inner = inner
-        self.tp = tp
-        self.ctl = dist.new_group(backend="gloo")
-        self.last_stats = {}
-
-    def _bcast(self, obj):
-        import torch.distributed as dist
-
-        box = [obj]
-        dist.broadcast_object_list(box, src=0, group=self.ctl)
-        return box[0]
-
-    def __call__(self, messages):
-        self._bcast(messages)
-        out = self.inner(messages)
-        self.last_stats = self.inner.last_stats
-        return out
-
-    def parse(self, request, repair: bool = False):
-        return self(messages_for(request, repair=repair))
-
-    def stop(self):
-        """Rank 0: release the TP workers from worker_loop."""
-        self._bcast(None)
-
-    def worker_loop(self):
-        """TP ranks != 0: follow rank 0's requests until stop(); returns the answers decoded here
-        (identical to rank 0's: lockstep decode, vocab-parallel sampling)."""
-        outs = []
-        while True:
-            messages = self._bcast(None)
-            if messages is None:
-                return outs
-            try:
-                outs.append(self.inner(messages))
-            except Exception as e:  # noqa: BLE001  (rank 0 reports the error to the client)
-                print(f"[brain worker {self.tp.rank}] {e}", flush=True)
-                outs.append(None)
 
 
 def main():

@@ -8,9 +8,9 @@ GPU placement on one node (plan_gpus): the brain (LLM) takes GPUs 0..TP-1 and th
 (ASR) every remaining GPU, one voice worker per GPU behind the session router (session DP);
 VWA_BRAIN_GPUS / VWA_VOICE_GPUS (comma lists) override.  With VWA_TP>1 the brain is launched
 through torch.distributed.run with one process per GPU.  When only one GPU is visible the two
-share it: the brain then runs without the chained decode launch (VWA_CHAIN=0) -- that kernel keeps
-one workgroup resident on every CU behind grid barriers, which a co-located ASR would starve
-(it would time out and fall back per step).
+share it (shared_gpu_env: the chained decode launch stays on, bounded waits + fallback).  The
+brain is restartable: a TP group that loses lockstep exits and is started again in fresh
+processes while the other services keep serving (Supervisor).
 """
 from __future__ import annotations
 
@@ -23,28 +23,125 @@ import time
 PKG = "voice_enabled_browser_automation_amd"
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 def _spawn(module: str, env_extra: dict, torchrun_nproc: int = 0) -> subprocess.Popen:
     env = dict(os.environ)
     env.update(env_extra)
     if torchrun_nproc > 1:
+        # a fresh rendezvous port per (re)start: the previous group's port may still be in TIME_WAIT
+        port = env.get("VWA_MASTER_PORT") or str(_free_port())
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={torchrun_nproc}",
-               "--master-addr", "127.0.0.1", "--master-port", env.get("VWA_MASTER_PORT", "29611"), "-m", module]
+               "--master-addr", "127.0.0.1", "--master-port", port, "-m", module]
     else:
         cmd = [sys.executable, "-m", module]
     return subprocess.Popen(cmd, env=env)
+
+
+class Supervisor:
+    """Keeps the services running.  A service marked restartable (the brain: its TP group exits
+    with brain/tp_engine.FATAL_EXIT_CODE when it loses lockstep, and any brain crash is an LLM
+    failure the reference survives with 500s, apps/brain/src/server.ts:122-126) is started again
+    in FRESH processes -- never re-exec'd from a process that touched the GPU -- with exponential
+    backoff, at most ``max_restarts`` times per ``window_s``; the other services keep running
+    meanwhile (voice answers brain errors as the reference does).  Any other exit, or a restart
+    budget spent, stops everything."""
+
+    def __init__(self, spawn=None, max_restarts: int = 5, window_s: float = 600.0, backoff_s: float = 1.0,
+                 clock=time.monotonic, sleep=time.sleep, log=print):
+        self.spawn = spawn or _spawn
+        self.max_restarts = max_restarts
+        self.window_s = window_s
+        self.backoff_s = backoff_s
+        self.clock = clock
+        self.sleep = sleep
+        self.log = log
+        self.services = []  # [name, args, restartable, proc, restart times]
+
+    def add(self, name: str, module: str, env_extra: dict, torchrun_nproc: int = 0, restartable: bool = False):
+        proc = self.spawn(module, env_extra, torchrun_nproc)
+        self.services.append([name, (module, env_extra, torchrun_nproc), restartable, proc, []])
+        return proc
+
+    def procs(self):
+        return [s[3] for s in self.services]
+
+    def poll_once(self) -> bool:
+        """Check every service once; restart what may be restarted.  False = stop everything."""
+        for svc in self.services:
+            name, args, restartable, proc, times = svc
+            rc = proc.poll()
+            if rc is None:
+                continue
+            now = self.clock()
+            times[:] = [t for t in times if now - t < self.window_s]
+            if not restartable or len(times) >= self.max_restarts:
+                self.log(f"[launch] {name} exited with {rc}; stopping" +
+                         (f" ({len(times)} restarts in {self.window_s:.0f} s)" if restartable else ""))
+                return False
+            delay = self.backoff_s * (2 ** len(times))
+            self.log(f"[launch] {name} exited with {rc}; restarting it in fresh processes in {delay:.1f} s "
+                     f"(restart {len(times) + 1}/{self.max_restarts})")
+            self.sleep(delay)
+            times.append(now)
+            svc[3] = self.spawn(*args)
+        return True
+
+    def stop(self) -> None:
+        for p in self.procs():
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in self.procs():
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
 
 
 def _ids(v: str) -> list:
     return [g.strip() for g in v.split(",") if g.strip()]
 
 
-def plan_gpus(n_gpus: int, tp: int = 1, brain: str = "", voice: str = "") -> dict:
+def plan_gpus(n_gpus: int, tp: int = 1, brain: str = "", voice: str = "", parent_visible: str = "") -> dict:
     """-> {"brain": [ids], "voice": [ids], "shared": bool}: the brain on GPUs 0..tp-1, the voice
-    workers on the rest (or explicit lists); shared = a brain GPU also hosts a voice worker."""
+    workers on the rest (or explicit lists); shared = a brain GPU also hosts a voice worker.
+    ``parent_visible`` (the launcher's own HIP_VISIBLE_DEVICES list): the planned ordinals index
+    into it, so a launcher given GPUs 4,5 places its children on 4 and 5 -- a child's
+    HIP_VISIBLE_DEVICES replaces the inherited mask rather than narrowing it."""
     n = max(1, n_gpus)
     b = _ids(brain) or [str(i) for i in range(min(tp, n))]
     v = _ids(voice) or ([str(i) for i in range(n) if str(i) not in b] or [b[0]])
-    return {"brain": b, "voice": v, "shared": bool(set(b) & set(v))}
+    shared = bool(set(b) & set(v))
+    par = _ids(parent_visible)
+    if par:
+        m = lambda ids: [par[int(i)] if i.isdigit() and int(i) < len(par) else i for i in ids]  # noqa: E731
+        b, v = m(b), m(v)
+    return {"brain": b, "voice": v, "shared": shared}
+
+
+def _parent_visible() -> str:
+    return os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES") or ""
+
+
+def shared_gpu_env(env) -> dict:
+    """Brain settings when it shares its GPU with a voice worker.  The chained decode launch stays
+    on: its persistent workgroups wait (bounded) for the ASR's short kernels to drain from the CUs
+    they need, and a launch that still times out falls back to per-kernel launches and is re-armed
+    after a backoff (runtime/engine.py).  VWA_SHARED_CHAIN=0 restores the per-kernel brain;
+    VWA_SHARED_CHAIN_GRID_DIV=k gives the chain CUs/k workgroups."""
+    out = {"VWA_CHAIN": env.get("VWA_CHAIN", env.get("VWA_SHARED_CHAIN", "1"))}
+    div = env.get("VWA_SHARED_CHAIN_GRID_DIV")
+    if div:
+        out["VWA_CHAIN_GRID_DIV"] = div
+    return out
 
 
 def _visible_gpus() -> int:
@@ -58,41 +155,34 @@ def _visible_gpus() -> int:
 
 def main():
     tp = int(os.environ.get("VWA_TP", "1") or 1)
-    plan = plan_gpus(_visible_gpus(), tp, os.environ.get("VWA_BRAIN_GPUS", ""), os.environ.get("VWA_VOICE_GPUS", ""))
+    plan = plan_gpus(_visible_gpus(), tp, os.environ.get("VWA_BRAIN_GPUS", ""), os.environ.get("VWA_VOICE_GPUS", ""),
+                     parent_visible=_parent_visible())
     voice_gpus = plan["voice"]
     benv = {"HIP_VISIBLE_DEVICES": ",".join(plan["brain"])}
     if plan["shared"]:
-        benv["VWA_CHAIN"] = os.environ.get("VWA_CHAIN", "0")
-    procs = [_spawn(f"{PKG}.brain.server", benv, tp)]
+        benv.update(shared_gpu_env(os.environ))
+    sup = Supervisor(max_restarts=int(os.environ.get("VWA_BRAIN_MAX_RESTARTS", "5")))
+    sup.add("brain", f"{PKG}.brain.server", benv, tp, restartable=True)
     if len(voice_gpus) > 1:
         # ASR session-DP: one voice worker per GPU behind the router on VOICE_PORT (voice/router.py)
         base = int(os.environ.get("VWA_VOICE_BASE_PORT", "7100"))
         for i, g in enumerate(voice_gpus):
-            procs.append(_spawn(f"{PKG}.voice.server", {"HIP_VISIBLE_DEVICES": g, "VOICE_PORT": str(base + i)}))
-        procs.append(_spawn(f"{PKG}.voice.router", {"VWA_DP": str(len(voice_gpus))}))
+            sup.add(f"voice{i}", f"{PKG}.voice.server", {"HIP_VISIBLE_DEVICES": g, "VOICE_PORT": str(base + i)})
+        sup.add("router", f"{PKG}.voice.router", {"VWA_DP": str(len(voice_gpus))})
     else:
-        procs.append(_spawn(f"{PKG}.voice.server", {"HIP_VISIBLE_DEVICES": voice_gpus[0] if voice_gpus else "0"}))
-    procs += [_spawn(f"{PKG}.executor.server", {}), _spawn(f"{PKG}.web.server", {})]
+        sup.add("voice", f"{PKG}.voice.server", {"HIP_VISIBLE_DEVICES": voice_gpus[0] if voice_gpus else "0"})
+    sup.add("executor", f"{PKG}.executor.server", {})
+    sup.add("web", f"{PKG}.web.server", {})
 
     def stop(*_a):
-        for p in procs:
-            if p.poll() is None:
-                p.send_signal(signal.SIGTERM)
-        for p in procs:
-            try:
-                p.wait(timeout=10)
-            except subprocess.TimeoutExpired:
-                p.kill()
+        sup.stop()
         sys.exit(0)
 
     signal.signal(signal.SIGINT, stop)
     signal.signal(signal.SIGTERM, stop)
-    while True:
-        for p in procs:
-            if p.poll() is not None:
-                print(f"[launch] a service exited with {p.returncode}; stopping", flush=True)
-                stop()
+    while sup.poll_once():
         time.sleep(1.0)
+    stop()
 
 
 if __name__ == "__main__":

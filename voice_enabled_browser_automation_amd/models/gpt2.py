@@ -149,7 +149,7 @@ class GPT2Model:
                                    slots=bufs.slots, q_out=qbuf, k_cache=kc, v_cache=vc)
             if prefill_seq is None:
                 attn = bufs.attn[:M]
-                ops.decode_attention(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens, bufs.seq_ids,
+                ops.decode_attention_rows(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens, bufs.seq_ids,
                                      n_q_heads=self.nq, n_kv_heads=self.nkv, head_dim=self.hd, scale=self.scale,
                                      max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o, part_ml=bufs.part_ml,
                                      counters=bufs.attn_cnt)

@@ -286,13 +286,22 @@ class LlamaModel:
         sc = {}
         if f8:  # W8A16 chain: fp8 tiled weights converted to bf16 in registers, per-row scales in the epilogues
             sc = dict(s_o=L.o.scale, s_gu=L.gu.scale, s_down=L.down.scale, s_qkv=N.qkv.scale if nxt else None)
-        desc, lds = ops.ext().chain_make(
-            bufs.hidden[:M], bufs.attn[:M], bufs.act[:M], wsel(L.o), wsel(L.gu), wsel(L.down), self.cfg.rms_eps,
-            wsel(N.qkv) if nxt else None, self.nq, self.nkv, self.hd,
-            bufs.positions if nxt else None, bufs.slots if nxt else None, self.rope if nxt else None,
-            bufs.q[:M] if nxt else None, kv.k[li + 1] if nxt else None, kv.v[li + 1] if nxt else None,
-            self._chain_bar, self._chain_work, None, self._chain_bar_mode, **a, w_tiled=tiled, **sc,
-            tp_ar=self.tp.custom_ar.state if self.tp.size > 1 else 0)
+        def make(a):
+            return ops.ext().chain_make(
+                bufs.hidden[:M], bufs.attn[:M], bufs.act[:M], wsel(L.o), wsel(L.gu), wsel(L.down), self.cfg.rms_eps,
+                wsel(N.qkv) if nxt else None, self.nq, self.nkv, self.hd,
+                bufs.positions if nxt else None, bufs.slots if nxt else None, self.rope if nxt else None,
+                bufs.q[:M] if nxt else None, kv.k[li + 1] if nxt else None, kv.v[li + 1] if nxt else None,
+                self._chain_bar, self._chain_work, None, self._chain_bar_mode, **a, w_tiled=tiled, **sc,
+                tp_ar=self.tp.custom_ar.state if self.tp.size > 1 else 0)
+
+        desc, lds = make(a)
+        if not desc.numel() and attn:
+            # shapes the attention phase cannot share a launch with (Llama-3-70B at 3-4 rows: the
+            # 28672-wide down-projection X rows exceed LDS, and X streaming has no attention
+            # instantiation): chain the tail, the decode attention as its own launch
+            attn = False
+            desc, lds = make({})
         cache[key] = (desc, 4 if nxt else 3, lds, self.nq // self.nkv if attn else 0) if desc.numel() else None
         return cache[key]
 
@@ -357,8 +366,10 @@ class LlamaModel:
                 continue
             chain = False  # shapes the chain cannot take: per-kernel path from here on
             if prefill_seq is None:
+                # (ragged rows: a decode step, or the batched admission prefill of several requests'
+                # prompt suffixes -- runtime/engine.py prefill_batch -- in 64-row attention slices)
                 attn = bufs.attn[:M]
-                ops.decode_attention(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens, bufs.seq_ids,
+                ops.decode_attention_rows(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens, bufs.seq_ids,
                                      n_q_heads=self.nq, n_kv_heads=self.nkv, head_dim=self.hd, scale=self.scale,
                                      max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o, part_ml=bufs.part_ml,
                                      counters=bufs.attn_cnt)

@@ -748,6 +748,21 @@ def decode_attention(q: torch.Tensor, kv: KVLayout, ctx_lens: torch.Tensor, seq_
     return out
 
 
+def decode_attention_rows(q: torch.Tensor, kv: KVLayout, ctx_lens: torch.Tensor, seq_ids: torch.Tensor, *,
+                          out: torch.Tensor, slice_rows: int = 64, **kw) -> torch.Tensor:
+    """decode_attention over any number of ragged rows (each row: its own sequence and causal
+    context): the multi-query MFMA kernel takes <= 64 rows per launch (its row-group scan), so
+    longer row sets -- batched admission prefill of several requests' prompt suffixes -- run in
+    64-row slices that reuse the same partial buffers (stream-ordered)."""
+    M = q.shape[0]
+    if M <= slice_rows or not _gpu(q):
+        return decode_attention(q, kv, ctx_lens, seq_ids, out=out, **kw)
+    for i in range(0, M, slice_rows):
+        j = min(M, i + slice_rows)
+        decode_attention(q[i:j], kv, ctx_lens[i:j], seq_ids[i:j], out=out[i:j], **kw)
+    return out
+
+
 def flash_attention(q: torch.Tensor, kv: KVLayout, *, Sk: int, n_kv_heads: int, causal: bool, scale: float,
                     q_offset: int = 0, out: Optional[torch.Tensor] = None,
                     k_lens: Optional[torch.Tensor] = None, q_offsets: Optional[torch.Tensor] = None) -> torch.Tensor:

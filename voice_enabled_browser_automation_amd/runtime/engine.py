@@ -30,6 +30,12 @@ from .kv_cache import BlockManager, PagedKVCache
 BUCKETS = (1, 2, 4, 8, 16, 32, 64)
 
 
+class TPGroupFailure(RuntimeError):
+    """A tensor-parallel decode step lost lockstep (a chained launch timed out waiting for a peer
+    rank's in-launch all-reduce round): this process's KV cache and round counters can no longer
+    be trusted, so the whole TP group must be restarted (brain/tp_engine.py)."""
+
+
 def bucket_for(n: int) -> int:
     for b in BUCKETS:
         if n <= b:
@@ -449,10 +455,11 @@ class LLMEngine:
     def _tp_chain_fatal(self) -> None:
         """Under tensor parallelism a chained launch that timed out (a peer's rounds never came)
         leaves the ranks' in-launch round counters and K/V in disagreement: no per-rank fallback
-        can restore lockstep, so the step fails loudly (the serving layer restarts the group)."""
+        can restore lockstep, so the step fails loudly: brain/tp_engine.py fails the in-flight
+        requests and exits the process, and the launcher restarts the TP group."""
         tp = getattr(self.model, "tp", None)
         if tp is not None and tp.size > 1:
-            raise RuntimeError("chained TP decode launch timed out waiting for a peer rank")
+            raise TPGroupFailure("chained TP decode launch timed out waiting for a peer rank")
 
     def _schedule_chain_retry(self) -> None:
         """A chain timeout usually means another kernel held CUs for a while (e.g. the ASR engine
@@ -475,6 +482,80 @@ class LLMEngine:
         self.model.enable_chain()
         self.graphs.clear()
         self.stats["chain_rearms"] = self.stats.get("chain_rearms", 0) + 1
+
+    def prefill_batch(self, items: List[Tuple[Sequence_, int]], chunk: int = 2048) -> None:
+        """Admission prefill of several requests in as few forwards as possible: the K/V of every
+        ``seq.tokens[n_computed:upto]`` for each (seq, upto).  Sequences whose uncached part is
+        longer than what sits before it (a cold prompt: its own self-attention dominates) take the
+        single-sequence path (flash attention); the others -- prompt suffixes behind the cached
+        static prefix, ~85 tokens each for the intent prompt -- are concatenated into ONE ragged
+        row set (each row: its sequence, position, KV slot, causal context), run through the
+        step graphs when they fit a decode bucket and otherwise as eager forwards of up to
+        ``chunk`` rows: the projections then run as prompt-sized MFMA GEMMs (gemm.hip) shared by
+        every request instead of one weight pass per request (reference: each /parse sends its
+        prompt independently, apps/brain/src/server.ts:98-105).  No logits are computed."""
+        rows: List[Tuple[Sequence_, int]] = []
+        for seq, upto in items:
+            end = min(upto, len(seq.tokens))
+            todo = end - seq.n_computed
+            if todo <= 0:
+                continue
+            if todo > seq.n_computed and todo > self.bufs.max_rows:
+                self.prefill(seq, upto=end)
+                continue
+            rows += [(seq, t) for t in seq.tokens[seq.n_computed:end]]
+        if not rows:
+            return
+        self.stats["prefill_tokens"] += len(rows)
+        self.stats["batched_prefills"] = self.stats.get("batched_prefills", 0) + 1
+        if len(rows) <= self.bufs.max_rows:
+            self.run_rows(rows, logits_for=[len(rows) - 1], check=True, defer_head=True)
+            self._head_rows = None
+            return
+        if self._staging_inflight and self.device.type == "cuda":
+            torch.cuda.current_stream().synchronize()
+            self._staging_inflight = False
+        for i in range(0, len(rows), chunk):
+            self._ragged_forward(rows[i : i + chunk])
+
+    def _ragged_forward(self, rows: List[Tuple[Sequence_, int]]) -> None:
+        """One eager forward of ragged rows (more than the step buckets hold): the decode-mode
+        model forward over scratch buffers sized for them; attention in 64-row slices."""
+        n = len(rows)
+        bs = self.block_size
+        pending: Dict[int, int] = {}
+        toks, poss, sids, slots = [], [], [], []
+        for seq, tok in rows:
+            pos = pending.get(seq.sid, seq.n_computed)
+            if pos // bs >= len(seq.blocks):
+                self._ensure_blocks(seq, pos + 1)
+            toks.append(tok)
+            poss.append(pos)
+            sids.append(seq.sid)
+            slots.append(seq.blocks[pos // bs] * bs + pos % bs)
+            pending[seq.sid] = pos + 1
+        if self.bufs.table_dirty:
+            self.bufs.block_table.copy_(self.bufs.h_table, non_blocking=self.device.type == "cuda")
+            self.bufs.table_dirty = False
+        dev, m = self.device, self.model
+        i32 = dict(dtype=torch.int32)
+        meta = torch.tensor([toks, poss, sids, [p + 1 for p in poss]], **i32)
+        if dev.type == "cuda":
+            meta = meta.pin_memory().to(dev, non_blocking=True)
+        d = m.cfg.hidden
+        scratch = SimpleNamespace(
+            tokens=meta[0], positions=meta[1], seq_ids=meta[2], ctx_lens=meta[3],
+            slots=torch.tensor(slots, dtype=torch.int64).to(dev, non_blocking=dev.type == "cuda"),
+            block_table=self.bufs.block_table, max_ctx=self.bufs.max_ctx,
+            hidden=torch.empty(n, d, dtype=m.dtype, device=dev),
+            q=torch.empty(n, m.nq * m.hd, dtype=m.dtype, device=dev),
+            attn=torch.empty(n, m.nq * m.hd, dtype=m.dtype, device=dev),
+            act=torch.empty(n, getattr(m, "F", getattr(m.cfg, "ffn", d)), dtype=m.dtype, device=dev),
+            part_o=self.bufs.part_o, part_ml=self.bufs.part_ml, attn_cnt=self.bufs.attn_cnt,
+            logits_local=self.bufs.logits_local, logits=self.bufs.logits)
+        m.forward(scratch, n, self.kv, head=False)
+        for sid, ln in pending.items():
+            self.seqs[sid].n_computed = ln
 
     def prefill(self, seq: Sequence_, chunk: int = 2048, upto: Optional[int] = None) -> Optional[torch.Tensor]:
         """Compute K/V for seq.tokens[n_computed:upto] (default: all tokens); returns f32 logits
