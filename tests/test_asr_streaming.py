@@ -105,3 +105,30 @@ def test_eight_concurrent_websocket_sessions_batch_their_passes(engine):
     assert batcher.rows_per_batch() > 1.0, batcher.stats
     assert m["asr_batcher"]["max_batch"] > 1
     assert m["counters"]["finals"] == n_sess
+
+
+def test_utterance_buffer_is_appended_in_place():
+    """The session's utterance buffer is preallocated and appended in place (no per-frame copy of
+    the whole utterance); recognition passes see exactly the samples pushed so far."""
+    seen = []
+    s = StreamingAsrSession(lambda pcm: seen.append(pcm.copy()) or "x", partial_every_s=1.0)
+    store = s._pcm
+    pcm = _speech(3.0, 200)
+    for i in range(0, len(pcm), 960):  # 60 ms packets
+        s.push(pcm[i : i + 960].tobytes())
+    assert s._pcm is store and s._n == len(pcm)
+    assert np.array_equal(s.buf, pcm)
+    assert seen and all(np.array_equal(a, pcm[: len(a)]) for a in seen)
+
+
+def test_recognizer_builds_hypotheses_on_the_prefix_it_forced(engine):
+    """A committed prefix longer than the decoder's position cap is cut before decoding, and the
+    hypothesis is that cut prefix + the continuation (never longer-prefix + tokens
+    decoded after a shorter one)."""
+    cap = engine.max_prefix()
+    long_prefix = list(range(400, 400 + cap + 25))
+    for rec in (EngineRecognizer(engine, max_tokens=3), AsrBatcher(engine, max_tokens=3)):
+        hyp = rec.recognize(_speech(1.0, 220), long_prefix)
+        assert hyp.tokens[:cap] == long_prefix[:cap] and len(hyp.tokens) <= cap + 3
+        if hasattr(rec, "close"):
+            rec.close()

@@ -102,7 +102,7 @@ def test_skinny_swiglu(M, skinny_mode):
     xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5)
     exp = torch.nn.functional.silu(xf @ wg.float().cpu().t()) * (xf @ wu.float().cpu().t())
     close(out, exp, 2e-2)
-    # prefill path (hipBLASLt + swiglu kernel)
+    # prefill-sized rows: the tiled MFMA GEMM (gemm.hip) with the SwiGLU epilogue
     x2 = rnd(80, K)
     out2 = ops.linear_swiglu(x2, wgu)
     exp2 = torch.nn.functional.silu(x2.float().cpu() @ wg.float().cpu().t()) * (x2.float().cpu() @ wu.float().cpu().t())
@@ -771,3 +771,41 @@ def test_fp8_gemm_large_tile(M):
     ops.linear(x, wq, out=out, fuse_rms=True)
     exp = ops.linear(x.cpu(), ops.FP8Weight(wq.rows().cpu(), wq.scale.cpu()), fuse_rms=True)
     close(out, exp, 3e-2, 3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 4, 8])
+def test_llama70b_tp8_per_rank_decode_shapes(M):
+    """One rank's decode projections of Llama-3-70B at TP=8 (BASELINE config 4): o_proj
+    [8192, 1024] and down [8192, 3584] (row-parallel, residual epilogue), gate/up [2 x 3584, 8192]
+    (SwiGLU) and QKV [(8 + 2) x 128, 8192] (1 kv head: RoPE + paged-KV write) on pre-tiled weights
+    through the streaming kernel, against the f32 reference."""
+    d, F, nq, nkv, hd = 8192, 3584, 8, 1, 128
+    x = rnd(M, d)
+    res = rnd(M, d)
+    for N, K in ((d, nq * hd), (d, F)):
+        xi, w = rnd(M, K), rnd(N, K, scale=0.02)
+        out = res.clone()
+        ops.linear(xi, ops.TiledWeight(w), out=out, residual=out)
+        want = ref.linear(xi.cpu(), w.cpu(), None, out=res.clone().cpu(), residual=res.cpu())
+        close(out, want, 2e-2)
+    gu = ops.interleave_gate_up(rnd(F, d, scale=0.02), rnd(F, d, scale=0.02))
+    a = ops.linear_swiglu(x, ops.TiledWeight(gu), fuse_rms=True)
+    b = ref.linear_swiglu(x.cpu(), gu.cpu(), fuse_rms=True, eps=1e-5, out=torch.empty(M, F, dtype=BF))
+    close(a, b, 2e-2)
+    H = nq + 2 * nkv
+    wq = ops.permute_qkv_rows(rnd(H * hd, d, scale=0.02), H, hd)
+    rope = ops.rope_table(512, hd, 5e5, device=DEV)
+    pos = torch.arange(7, 7 + M, dtype=torch.int32, device=DEV)
+    slots = torch.arange(M, dtype=torch.int64, device=DEV) + 3
+    kc = torch.zeros(4, nkv, 16, hd, dtype=BF, device=DEV)
+    vc = torch.zeros_like(kc)
+    q = torch.zeros(M, nq * hd, dtype=BF, device=DEV)
+    ops.qkv_rope_write(x, ops.TiledWeight(wq), None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv,
+                       head_dim=hd, rope=rope, positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc)
+    kc2, vc2 = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q2 = torch.zeros(M, nq * hd, dtype=BF)
+    ref.qkv_rope_write(x.cpu(), wq.cpu(), None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
+                       rope=rope.cpu(), positions=pos.cpu(), slots=slots.cpu(), q_out=q2, k_cache=kc2, v_cache=vc2)
+    for a, b in ((q, q2), (kc, kc2), (vc, vc2)):
+        assert torch.isfinite(a.float()).all()
+        close(a, b, 3e-2)

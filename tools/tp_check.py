@@ -15,6 +15,7 @@ under grammar-like random masks and temperature.  VWA_DIST_BACKEND selects the c
 large-message backend (gloo when two ranks share one GPU, RCCL needs one GPU per rank); the
 decode step itself contains no torch.distributed call, so it is graph-captured either way.
 """
+import math
 import os
 import sys
 
@@ -79,6 +80,28 @@ def sample_check(tp, dev, ref_model, tp_model):
     return ok
 
 
+def ar_self_check(tp, dev):
+    """The one-shot all-reduce alone (bf16, decode row counts 1..64 of this config's hidden size):
+    rank r contributes (r + 1) * x, the sum is (world (world + 1) / 2) * x on every rank."""
+    if tp.custom_ar is None:
+        return True
+    ok = True
+    g = torch.Generator(device="cpu").manual_seed(3)
+    for rows in (1, 2, 8, 64):
+        x = (torch.randn(rows, CFG.hidden, generator=g) * 0.1).to(torch.bfloat16)
+        t = (x.float() * (tp.rank + 1)).to(torch.bfloat16).to(dev)
+        want = sum((x.float() * (r + 1)).to(torch.bfloat16).float() for r in range(tp.size))
+        for _ in range(3):
+            t2 = t.clone()
+            tp.all_reduce(t2)
+            torch.cuda.synchronize()
+            err = (t2.float().cpu() - want).abs().max().item()
+            ok &= math.isfinite(err) and err < 0.02 * (1 + want.abs().max().item())
+        if tp.rank == 0:
+            print(f"oneshot_allreduce rows={rows} err={err:.4g} error_word={tp.custom_ar.error()}", flush=True)
+    return ok
+
+
 def main():
     os.environ.setdefault("VWA_DIST_BACKEND", "gloo")
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -88,6 +111,7 @@ def main():
         os.environ.setdefault("VWA_CHAIN_GRID_DIV", str(world))
     tp = init_distributed()
     dev = torch.device("cuda", torch.cuda.current_device())
+    ar_ok = ar_self_check(tp, dev)
     torch.manual_seed(0)
     toks = torch.randint(0, CFG.vocab_size, (110,)).tolist()
     ref_model = LlamaModel(CFG, device=dev, seed=7, tp=TPContext.single())
@@ -97,6 +121,7 @@ def main():
         m = LlamaModel(CFG, device=dev, seed=7, tp=tp)
         got, e = run(m, toks, graphs=graphs)
         errs = [(a - b).abs().max().item() for a, b in zip(got, ref)]
+        ok &= all(math.isfinite(x) for x in errs)  # (max() would skip a NaN after the first entry)
         ok &= max(errs) < 0.05 * (1 + max(r.abs().max().item() for r in ref))
         if graphs:
             ok &= e.stats["graph_replays"] >= 5
@@ -109,7 +134,7 @@ def main():
                   f"replays={e.stats['graph_replays']} chained_layers={n_chain} chain_error={m.chain_error()} "
                   f"max_errs={[round(x, 4) for x in errs]}", flush=True)
     s_ok = sample_check(tp, dev, ref_model, m)
-    ok &= s_ok
+    ok &= s_ok and ar_ok
     if tp.custom_ar is not None:
         ok &= not tp.custom_ar.error()
     if tp.rank == 0:

@@ -287,12 +287,19 @@ class AsrEngine:
         toks = self.decode_many(audios, max_tokens=max_tokens, min_tokens=min_tokens, exact_tokens=exact_tokens)
         return [self.tok.decode(o) for o in toks]
 
+    def max_prefix(self) -> int:
+        """Longest forced text prefix decode_many keeps (the decoder's position cap minus the SOT
+        prompt and one decoded token); longer prefixes are cut to this length."""
+        r = self.runner
+        return max(0, r.bps * r.bs - len(self.prompt) - 1)
+
     def decode_many(self, audios: List[torch.Tensor], prefixes: Optional[Sequence[Sequence[int]]] = None, *,
                     max_tokens: int = 96, min_tokens: int = 0, exact_tokens: Optional[int] = None) -> List[List[int]]:
         """Token ids decoded for each utterance.  ``prefixes[i]``: text tokens forced after the
         SOT sequence (a streaming session's committed transcript -- asr/streaming.py local
         agreement): they are prefilled in the same ragged prompt step as the SOT tokens and only
-        the continuation is decoded; the result EXCLUDES the prefix."""
+        the continuation is decoded; the result EXCLUDES the prefix.  A prefix longer than
+        ``max_prefix()`` is cut to that length (callers build hypotheses from the cut prefix)."""
         t0 = time.perf_counter()
         m = self.model
         B = len(audios)

@@ -94,7 +94,10 @@ class StreamingAsrSession:
         self.min_speech = int(min_speech_s * rate)
         self.local_agreement = local_agreement
         self.frame = rate // 50  # 20 ms
-        self.buf = np.zeros(0, dtype=np.int16)
+        # the utterance buffer: preallocated to the window (+ one packet), appended in place --
+        # no per-frame re-concatenation of the whole utterance
+        self._pcm = np.zeros(self.max_window + 4 * rate, dtype=np.int16)
+        self._n = 0
         self._carry = b""
         self.t_offset = 0.0          # stream time of buf[0]
         self.speech = 0              # speech samples in the utterance
@@ -107,6 +110,17 @@ class StreamingAsrSession:
                                         "committed_tokens": 0}
 
     # ------------------------------------------------------------------ internals
+    @property
+    def buf(self) -> np.ndarray:
+        """The current utterance's samples (a view of the preallocated buffer)."""
+        return self._pcm[: self._n]
+
+    def _append(self, fr: np.ndarray) -> None:
+        if self._n + len(fr) > len(self._pcm):  # (never with the window cut; a safety net)
+            self._pcm = np.concatenate([self._pcm, np.zeros(max(len(fr), len(self._pcm) // 2), dtype=np.int16)])
+        self._pcm[self._n : self._n + len(fr)] = fr
+        self._n += len(fr)
+
     def _run(self) -> Hypothesis:
         t0 = time.perf_counter()
         hyp = self.rec.recognize(self.buf, self.committed if self.local_agreement else ())
@@ -115,8 +129,8 @@ class StreamingAsrSession:
         return hyp
 
     def _reset_utterance(self) -> None:
-        self.t_offset += len(self.buf) / self.rate
-        self.buf = np.zeros(0, dtype=np.int16)
+        self.t_offset += self._n / self.rate
+        self._n = 0
         self.speech = self.trailing_silence = self.since_partial = 0
         self.last_partial = ""
         self.committed = []
@@ -161,7 +175,7 @@ class StreamingAsrSession:
             fr = pcm[i : i + self.frame]
             if len(fr) == 0:
                 continue
-            self.buf = np.concatenate([self.buf, fr])
+            self._append(fr)
             rms = float(np.sqrt(np.mean(fr.astype(np.float32) ** 2)))
             if rms >= self.thresh:
                 self.speech += len(fr)
@@ -176,8 +190,8 @@ class StreamingAsrSession:
                 events += self._final()
             elif self.speech == 0 and self.trailing_silence >= self.endpoint:
                 # leading silence: drop it, keep the stream clock
-                self.t_offset += len(self.buf) / self.rate
-                self.buf = np.zeros(0, dtype=np.int16)
+                self.t_offset += self._n / self.rate
+                self._n = 0
                 self.trailing_silence = 0
         if self.speech >= self.min_speech and self.since_partial >= self.partial_every:
             self.since_partial = 0
@@ -200,8 +214,9 @@ class EngineRecognizer:
         self.max_tokens = max_tokens
 
     def recognize(self, pcm: np.ndarray, prefix: Sequence[int] = ()) -> Hypothesis:
-        toks = self.eng.decode_many([self.eng.pcm_to_audio(pcm)], [list(prefix)], max_tokens=self.max_tokens)[0]
-        full = list(prefix) + toks
+        prefix = list(prefix)[: self.eng.max_prefix()]  # the prefix the decoder actually forces
+        toks = self.eng.decode_many([self.eng.pcm_to_audio(pcm)], [prefix], max_tokens=self.max_tokens)[0]
+        full = prefix + toks
         return Hypothesis(full, self.eng.tok.decode(full).strip())
 
 
@@ -235,7 +250,8 @@ class AsrBatcher:
         with self._cv:
             if self._stop:
                 raise RuntimeError("ASR batcher stopped")
-            self._q.append((np.array(pcm, dtype=np.int16, copy=True), list(prefix), fut))
+            # (cut to what the decoder forces: the hypothesis is built on the prefix it really used)
+            self._q.append((np.array(pcm, dtype=np.int16, copy=True), list(prefix)[: self.eng.max_prefix()], fut))
             self._cv.notify()
         return fut.result()
 

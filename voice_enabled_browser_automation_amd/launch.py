@@ -137,7 +137,9 @@ def shared_gpu_env(env) -> dict:
     they need, and a launch that still times out falls back to per-kernel launches and is re-armed
     after a backoff (runtime/engine.py).  VWA_SHARED_CHAIN=0 restores the per-kernel brain;
     VWA_SHARED_CHAIN_GRID_DIV=k gives the chain CUs/k workgroups."""
-    out = {"VWA_CHAIN": env.get("VWA_CHAIN", env.get("VWA_SHARED_CHAIN", "1"))}
+    out = {"VWA_CHAIN": env.get("VWA_CHAIN", env.get("VWA_SHARED_CHAIN", "1")),
+           # HBM the voice worker's ASR keeps (the brain's auto KV sizing leaves it free)
+           "VWA_SHARED_GB": env.get("VWA_SHARED_GB", "24")}
     div = env.get("VWA_SHARED_CHAIN_GRID_DIV")
     if div:
         out["VWA_CHAIN_GRID_DIV"] = div

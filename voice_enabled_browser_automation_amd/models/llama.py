@@ -12,8 +12,10 @@ gamma folded into the LM head.  A decode layer is therefore 5 kernels:
 Tensor parallelism (one process per GPU, torch.distributed over RCCL/xGMI):
 column-parallel QKV (heads split) and gate/up, row-parallel o/down with ONE all-reduce each
 (rank 0 adds the residual in its epilogue, the others contribute their partial product, the
-all-reduce then produces h_new = h + sum_r partial_r in place), vocab-parallel LM head with an
-all-gather of the logits.  Weights are generated (or loaded) full-size per layer with a
+all-reduce then produces h_new = h + sum_r partial_r in place; decode steps of <= 4 rows do
+both all-reduces as in-launch rounds of the chained layer), vocab-parallel embedding (one
+all-reduce) and LM head whose logits stay sharded: the sampler exchanges per-rank partial maxima,
+never logits (ops.sample tp=...).  Weights are generated (or loaded) full-size per layer with a
 deterministic generator and sliced, so a TP model is numerically the same model as TP=1.
 """
 from __future__ import annotations
@@ -66,6 +68,9 @@ class LlamaModel:
         self.v_per = ((V + T - 1) // T + 31) // 32 * 32
         self.v_start = self.tp.rank * self.v_per
         self.v_end = min(V, self.v_start + self.v_per)
+        # (32-aligned shards can leave the last ranks past the end of a small vocabulary: refuse)
+        if (T - 1) * self.v_per >= V:
+            raise ValueError(f"vocab {V} cannot be split into {T} 32-aligned shards (last shard empty)")
         self.rope = ops.rope_table(cfg.max_pos, cfg.head_dim, cfg.rope_theta, device=self.device)
         self.scale = cfg.head_dim ** -0.5
         if self.device.type == "meta":

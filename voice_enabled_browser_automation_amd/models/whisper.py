@@ -2,7 +2,7 @@
 
 Encoder (one pass per 30 s window, batch of sessions = DP):
     log_mel (HIP, K2) -> conv1d+GELU (HIP MFMA implicit GEMM, K3) -> conv1d/s2+GELU+pos (K3)
-    -> L x [layernorm (K4) -> QKV GEMM (hipBLASLt) + bias -> flash attention (HIP MFMA, K5)
+    -> L x [layernorm (K4) -> QKV GEMM (gemm.hip tiled MFMA) + bias -> flash attention (HIP MFMA, K5)
             -> out-proj + bias + residual (K-epilogue) -> layernorm -> fc1 + bias + GELU -> fc2 + residual]
     -> layernorm -> cross-attention K/V for every decoder layer (computed once per window).
 Decoder (per token, hipGraph-captured per batch bucket):

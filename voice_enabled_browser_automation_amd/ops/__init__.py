@@ -435,9 +435,8 @@ def gemm_ok(x: torch.Tensor, w, out: Optional[torch.Tensor] = None, residual: Op
 
 
 # ----------------------------------------------------------------------------- GEMM family
-# Rows handled by the MFMA skinny kernels.  Above 16 rows (continuous batching of many sessions)
-# hipBLASLt's GEMM + the HIP epilogue kernels win on every decode shape (tools/bench_kernels.py:
-# M=32 qkv 15 vs 31 us, gate_up 54 vs 101 us, LM head 187 vs 446 us).
+# Rows handled by the MFMA streaming (skinny) kernels; above this the hand-written LDS-tiled MFMA
+# GEMM (gemm.hip) takes the step (continuous batching of many sessions, prefill).
 SKINNY_MAX_M = 16
 
 
@@ -447,8 +446,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
            col_mask: Optional[torch.Tensor] = None, col_mask_off: int = 0, mask_rows: int = 1) -> torch.Tensor:
     """y = act(rms(x) @ w^T + bias) [+ residual].
 
-    GPU: rows <= 64 -> MFMA skinny GEMM with fused epilogue (decode); otherwise hipBLASLt
-    (torch.matmul) for the plain GEMM + HIP epilogue kernels (prefill).
+    GPU: decode rows (<= SKINNY_MAX_M) -> the MFMA streaming GEMM with fused epilogue; more rows
+    -> the LDS-tiled MFMA GEMM (gemm.hip) with the same epilogues.  torch.matmul + the HIP
+    epilogue kernels only for shapes neither kernel takes.
     ln_c (from fold_layernorm): x goes through a LayerNorm whose affine is folded into (w, bias);
     decode rows compute its mean/rstd inside the streaming GEMM, other shapes normalise first.
     col_mask (int32 token bitmask rows, the sampler's grammar mask; plain store epilogue): the

@@ -9,8 +9,10 @@ the row bucket M.  Each bucket (1, 2, 4, ..., 64) is captured once into a hipGra
 (torch.cuda.CUDAGraph on ROCm) and replayed: the ~165 kernels of a Llama-3-8B step are
 then one graph launch instead of ~165 Python-driven launches.
 
-Longer prompt chunks (> 64 rows) go through the prefill path (hipBLASLt GEMMs + flash
-attention over the paged cache with a causal query offset), eagerly.
+Longer prompt chunks (> 64 rows) go through the prefill path eagerly: the hand-written tiled
+MFMA GEMM (csrc/kernels/gemm.hip) and flash attention over the paged cache with a causal query
+offset for a cold prompt; several requests' suffixes behind a cached prefix are batched into one
+ragged forward (``prefill_batch``).
 
 Sampling runs after the forward on the same stream so the CPU can compute the grammar mask
 for this step while the GPU is busy with the forward (see brain.intent_engine).
@@ -141,12 +143,19 @@ class LLMEngine:
             from .memory_plan import plan_memory
 
             free, _total = torch.cuda.mem_get_info(self.device) if self.device.type == "cuda" else (0, 0)
+            # VWA_SHARED_GB: HBM a co-located service keeps (launch.py sets it when the voice
+            # worker's ASR shares this GPU)
+            shared = float(os.environ.get("VWA_SHARED_GB", "0") or 0)
             plan = plan_memory(cfg, model.tp.size, wdtype=getattr(model, "wdtype", "bf16"), block_size=block_size,
-                               max_rows=max_rows, max_ctx=max_model_len)
+                               max_rows=max_rows, max_ctx=max_model_len, shared_gb=shared)
             kv_blocks = plan.kv_blocks
-            if free:  # never more than the device has free now (other processes, fragmentation)
+            if free:
+                # never more than the device has free now (other processes, fragmentation), minus
+                # headroom for what is allocated after the KV: step buffers, graph pools, GEMM and
+                # prefill scratch, and the co-located service
                 per = PagedKVCache.bytes_per_block(cfg.n_layers, model.nkv, model.hd, block_size)
-                kv_blocks = min(kv_blocks, int(free * 0.9) // per)
+                head = plan.step_buffers + plan.workspace + int(4e9) + int(shared * 1e9)
+                kv_blocks = min(kv_blocks, max(0, int(free * 0.95) - head) // per)
             self.memory_plan = plan
         if kv_blocks is None:
             if kv_gb is None:

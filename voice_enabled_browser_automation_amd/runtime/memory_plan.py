@@ -54,9 +54,17 @@ def _shard(n: int, t: int, align: int = 1) -> int:
 
 def plan_memory(cfg, tp: int = 1, *, wdtype: str = "bf16", kv_gb: Optional[float] = None, block_size: int = 16,
                 max_rows: int = 64, max_ctx: int = 4096, hbm: int = HBM_BYTES_MI355X,
-                reserve_frac: float = 0.06, gemm_ws_floats: int = 8 << 20, ar_max_elems: int = 64 * 8192) -> MemoryPlan:
+                reserve_frac: float = 0.06, gemm_ws_floats: Optional[int] = None, ar_max_elems: int = 64 * 8192,
+                shared_gb: float = 0.0, prefill_rows: int = 2048) -> MemoryPlan:
     """Bytes per rank.  ``kv_gb`` None: all remaining HBM after the rest (minus the reserve)
-    becomes KV; otherwise that many GB (capped at what remains)."""
+    becomes KV; otherwise that many GB (capped at what remains).  ``shared_gb``: HBM left to a
+    co-located service (the voice worker's ASR on a shared single GPU).  The workspace counts the
+    GEMM split-K workspace (ops.GEMM_WS_FLOATS), the batched-prefill scratch rows and, under TP,
+    the one-shot all-reduce staging + all-gather + chained-layer regions (allreduce.hip)."""
+    if gemm_ws_floats is None:
+        from .. import ops
+
+        gemm_ws_floats = ops.GEMM_WS_FLOATS
     assert cfg.n_heads % tp == 0 and cfg.n_kv_heads % tp == 0, "TP must divide the head counts"
     d, hd, L = cfg.hidden, cfg.head_dim, cfg.n_layers
     nq, nkv, F = cfg.n_heads // tp, cfg.n_kv_heads // tp, cfg.ffn // tp
@@ -71,9 +79,11 @@ def plan_memory(cfg, tp: int = 1, *, wdtype: str = "bf16", kv_gb: Optional[float
     n_splits = -(-max_ctx // 128)
     step = max_rows * (2 * d + 2 * nq * hd + F) * 2 + max_rows * v_per * 4 \
         + max_rows * n_splits * nq * (hd + 2) * 4
-    workspace = gemm_ws_floats * 4 + (2 * ar_max_elems * 2 + 2 * 64 * 1024 * 4 if tp > 1 else 0)
+    prefill = prefill_rows * (2 * d + 2 * nq * hd + F) * 2  # runtime/engine.py _ragged_forward scratch
+    ar = 2 * ar_max_elems * 2 + 2 * 64 * 1024 * 4 + 2 * 16 * 8192 * 4  # staging, gather, chain regions
+    workspace = gemm_ws_floats * 4 + prefill + (ar if tp > 1 else 0)
     kv_tok = 2 * L * nkv * hd * 2
-    reserve = int(hbm * reserve_frac)
+    reserve = int(hbm * reserve_frac) + int(shared_gb * 1e9)
     free = hbm - weights - embedding - step - workspace - reserve
     want = free if kv_gb is None else min(free, int(kv_gb * 1e9))
     per_block = kv_tok * block_size

@@ -221,8 +221,11 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                         events = await asr_call(asr.push, msg.data)
                         dt = time.perf_counter() - t_push
                         m.observe("asr_push_ms", dt * 1e3)
-                        if events:  # a recognition pass ran: real-time factor of this packet's work
-                            m.observe("asr_rtf", dt / max(1e-6, len(msg.data) / 2 / 16000.0))
+                        # a recognition pass ran: real-time factor = pass time over the seconds of
+                        # audio that pass recognised (the utterance buffer it covered)
+                        covered = max((float(ev.get("duration") or 0.0) for ev in events), default=0.0)
+                        if covered > 0:
+                            m.observe("asr_rtf", dt / covered)
                         await handle_events(events)
                 elif msg.type == WSMsgType.TEXT:
                     try:
