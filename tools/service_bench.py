@@ -1,0 +1,267 @@
+"""Product-path latency through the services (VERDICT r3 missing #4): speech end ->
+``intent`` frame over WS ``/stream``, with the brain and voice services as separate processes on
+the GPU(s) they would get from launch.py and a stub executor.
+
+    python tools/service_bench.py --sessions 1,8 --debounce 0,1000 --chain 1,0 --json out.jsonl
+
+Per (chain, debounce, sessions): every session opens ``/stream``, sets the page context, then
+streams utterances of ``--audio-s`` seconds of synthetic speech as 60 ms PCM16 packets paced in
+real time (a microphone, apps/web/src/App.tsx:279-288), followed by silence packets until the
+``intent`` frame arrives.  Reported per utterance:
+
+* speech_end_to_final_ms -- last speech packet sent -> ``transcript_final`` (the VAD endpoint,
+  ``endpoint_silence_s`` = 0.6 s, plus the final recognition pass);
+* final_to_intent_ms -- ``transcript_final`` -> ``intent`` (the debounce, the HTTP hop to the
+  brain, the grammar-constrained parse, the reply);
+* speech_end_to_intent_ms -- the sum: what a user waits after they stop speaking.
+
+The brain and the voice worker share GPU 0 (launch.py's single-GPU placement) unless
+``--brain-gpu`` / ``--voice-gpu`` say otherwise; ``--chain`` toggles the brain's chained decode
+launch (VWA_CHAIN), which then runs beside the live ASR kernels.  Random-init weights: the ASR runs
+in fixed-work mode (VWA_ASR_TOKENS_PER_S, 4 tokens per second of audio, as bench.py).
+"""
+import argparse
+import asyncio
+import json
+import os
+import socket
+import statistics
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = "voice_enabled_browser_automation_amd"
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def synth_speech(seconds: float, seed: int, rate: int = 16000) -> np.ndarray:
+    """Voiced syllables with short pauses (< the 0.6 s VAD endpoint), as bench.py's generator."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(int(seconds * rate)) / rate
+    f0 = 110 + 30 * np.sin(2 * np.pi * 0.3 * t + rng.uniform(0, 6))
+    phase = 2 * np.pi * np.cumsum(f0) / rate
+    sig = np.zeros(len(t))
+    for k, a in enumerate((1.0, 0.5, 0.25)):
+        sig += a * np.sin(phase * (k + 1) + rng.uniform(0, 6))
+    env = 0.35 + 0.65 * np.clip(np.sin(2 * np.pi * 4.0 * t + rng.uniform(0, 6)), 0, None) ** 0.5
+    sig = sig * env
+    sig = sig / (np.abs(sig).max() + 1e-9) * 0.6
+    return (sig * 32767).astype(np.int16)
+
+
+def spawn(module: str, env_extra: dict, log: str) -> subprocess.Popen:
+    env = dict(os.environ, **env_extra)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.Popen([sys.executable, "-u", "-m", module], env=env, cwd=ROOT,
+                            stdout=open(log, "w"), stderr=subprocess.STDOUT)
+
+
+async def wait_health(url: str, proc: subprocess.Popen, timeout: float) -> None:
+    import aiohttp
+
+    t0 = time.time()
+    async with aiohttp.ClientSession() as s:
+        while time.time() - t0 < timeout:
+            if proc.poll() is not None:
+                raise RuntimeError(f"{url}: service exited with {proc.returncode}")
+            try:
+                async with s.get(url) as r:
+                    if r.status == 200:
+                        return
+            except aiohttp.ClientError:
+                pass
+            await asyncio.sleep(0.5)
+    raise TimeoutError(url)
+
+
+async def start_stub_executor():
+    """/execute stub (the executor service's contract without a browser): {session_id, results}."""
+    from aiohttp import web
+
+    async def execute(req):
+        body = await req.json()
+        return web.json_response({"session_id": body.get("session_id") or "bench",
+                                  "results": [{"intent": i, "ok": True} for i in body.get("intents", [])],
+                                  "artifacts": {"dir": ""}})
+
+    async def health(_r):
+        return web.json_response({"status": "ok", "service": "executor"})
+
+    app = web.Application()
+    app.router.add_post("/execute", execute)
+    app.router.add_get("/health", health)
+    runner = web.AppRunner(app)
+    await runner.setup()
+    port = free_port()
+    await web.TCPSite(runner, "127.0.0.1", port).start()
+    return runner, port
+
+
+async def session(url: str, idx: int, n_utt: int, audio_s: float, out: list) -> None:
+    import aiohttp
+
+    pkt = 960  # 60 ms at 16 kHz
+    silence = np.zeros(pkt, np.int16).tobytes()
+    async with aiohttp.ClientSession() as s:
+        async with s.ws_connect(url, max_msg_size=0) as ws:
+            await ws.send_str(json.dumps({"type": "context_update", "payload": {"url": "https://www.bestbuy.com"}}))
+            marks: dict = {}
+            got = asyncio.Event()
+
+            async def reader():
+                async for msg in ws:
+                    if msg.type != aiohttp.WSMsgType.TEXT:
+                        continue
+                    f = json.loads(msg.data)
+                    now = time.perf_counter()
+                    if f["type"] == "transcript_final" and "final" not in marks:
+                        marks["final"] = now
+                    elif f["type"] == "intent":
+                        marks["intent"] = now
+                        marks["valid"] = isinstance(f.get("payload"), dict) and "intents" in f["payload"]
+                        got.set()
+
+            rd = asyncio.ensure_future(reader())
+            t_next = time.perf_counter()
+            for u in range(n_utt):
+                pcm = synth_speech(audio_s, seed=1000 * idx + u)
+                marks.clear()
+                got.clear()
+                for i in range(0, len(pcm), pkt):
+                    await ws.send_bytes(pcm[i : i + pkt].tobytes())
+                    t_next += pkt / 16000
+                    await asyncio.sleep(max(0.0, t_next - time.perf_counter()))
+                t_end = time.perf_counter()
+                deadline = t_end + 30.0
+                while not got.is_set() and time.perf_counter() < deadline:  # the mic keeps sending silence
+                    await ws.send_bytes(silence)
+                    t_next += pkt / 16000
+                    await asyncio.sleep(max(0.0, t_next - time.perf_counter()))
+                if got.is_set():
+                    fin = marks.get("final", marks["intent"])
+                    out.append({"session": idx, "utt": u, "valid": marks.get("valid", False),
+                                "speech_end_to_final_ms": (fin - t_end) * 1e3,
+                                "final_to_intent_ms": (marks["intent"] - fin) * 1e3,
+                                "speech_end_to_intent_ms": (marks["intent"] - t_end) * 1e3})
+                else:
+                    out.append({"session": idx, "utt": u, "timeout": True})
+                for _ in range(8):  # ~0.5 s of silence between utterances
+                    await ws.send_bytes(silence)
+                    t_next += pkt / 16000
+                    await asyncio.sleep(max(0.0, t_next - time.perf_counter()))
+            await ws.send_str(json.dumps({"type": "close"}))
+            rd.cancel()
+
+
+def pct(v, q):
+    return round(float(np.percentile(v, q)), 1) if v else None
+
+
+async def run_matrix(a) -> list:
+    import aiohttp
+
+    logs = os.path.join(ROOT, "gpurun_out", "service_bench")
+    os.makedirs(logs, exist_ok=True)
+    ex_runner, ex_port = await start_stub_executor()
+    results = []
+    try:
+        for chain in a.chain:
+            bport = free_port()
+            benv = {"VWA_BRAIN_ENGINE": a.brain_engine, "VWA_LLM_MODEL": a.llm, "BRAIN_PORT": str(bport),
+                    "VWA_CHAIN": chain, "HIP_VISIBLE_DEVICES": a.brain_gpu, "VWA_MAX_SESSIONS": str(max(a.sessions)),
+                    "VWA_DTYPE": a.dtype, "VWA_SHARED_GB": "24"}
+            brain = spawn(f"{PKG}.brain.server", benv, os.path.join(logs, f"brain_chain{chain}.log"))
+            try:
+                t0 = time.time()
+                await wait_health(f"http://127.0.0.1:{bport}/health", brain, a.load_timeout)
+                brain_load_s = time.time() - t0
+                for deb in a.debounce:
+                    vport = free_port()
+                    venv = {"VWA_ASR_ENGINE": a.asr_engine, "VWA_ASR_MODEL": a.asr, "VOICE_PORT": str(vport),
+                            "BRAIN_URL": f"http://127.0.0.1:{bport}/parse",
+                            "EXECUTOR_URL": f"http://127.0.0.1:{ex_port}", "VWA_DEBOUNCE_MS": deb,
+                            "HIP_VISIBLE_DEVICES": a.voice_gpu, "VWA_MAX_SESSIONS": str(max(a.sessions)),
+                            "VWA_ASR_TOKENS_PER_S": str(a.asr_tokens_per_s)}
+                    voice = spawn(f"{PKG}.voice.server", venv, os.path.join(logs, f"voice_chain{chain}_deb{deb}.log"))
+                    try:
+                        await wait_health(f"http://127.0.0.1:{vport}/health", voice, a.load_timeout)
+                        url = f"http://127.0.0.1:{vport}/stream"
+                        # warm-up: one utterance (graph captures, prefix cache of the prompt head)
+                        await session(url, 99, 1, a.audio_s, [])
+                        for n in a.sessions:
+                            out: list = []
+                            t0 = time.perf_counter()
+                            await asyncio.gather(*(session(url, i, a.utterances, a.audio_s, out) for i in range(n)))
+                            wall = time.perf_counter() - t0
+                            ok = [r for r in out if not r.get("timeout")]
+                            e2i = [r["speech_end_to_intent_ms"] for r in ok]
+                            rec = {"what": "service_latency", "chain": chain, "debounce_ms": float(deb), "sessions": n,
+                                   "utterances": len(out), "timeouts": len(out) - len(ok),
+                                   "valid_intents": f"{sum(r['valid'] for r in ok)}/{len(out)}",
+                                   "audio_s": a.audio_s, "asr": a.asr, "llm": a.llm, "dtype": a.dtype,
+                                   "speech_end_to_intent_p50_ms": pct(e2i, 50),
+                                   "speech_end_to_intent_p95_ms": pct(e2i, 95),
+                                   "speech_end_to_final_p50_ms": pct([r["speech_end_to_final_ms"] for r in ok], 50),
+                                   "final_to_intent_p50_ms": pct([r["final_to_intent_ms"] for r in ok], 50),
+                                   "final_to_intent_p95_ms": pct([r["final_to_intent_ms"] for r in ok], 95),
+                                   "wall_s": round(wall, 2), "brain_load_s": round(brain_load_s, 1)}
+                            async with aiohttp.ClientSession() as s:
+                                async with s.get(f"http://127.0.0.1:{bport}/metrics") as r:
+                                    bm = await r.json()
+                            eng = bm.get("engine", {})
+                            rec["brain_chain_fallbacks"] = eng.get("chain_fallbacks", 0)
+                            rec["brain_rows_per_iteration"] = eng.get("rows_per_iteration")
+                            print(json.dumps(rec), flush=True)
+                            results.append(rec)
+                    finally:
+                        voice.terminate()
+                        voice.wait(timeout=30)
+            finally:
+                brain.terminate()
+                brain.wait(timeout=60)
+    finally:
+        await ex_runner.cleanup()
+    return results
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sessions", default="1,8")
+    ap.add_argument("--debounce", default="0,1000")
+    ap.add_argument("--chain", default="1,0")
+    ap.add_argument("--utterances", type=int, default=4)
+    ap.add_argument("--audio-s", type=float, default=5.0)
+    ap.add_argument("--asr", default="whisper-tiny")
+    ap.add_argument("--asr-engine", default="whisper")
+    ap.add_argument("--asr-tokens-per-s", type=float, default=4.0)
+    ap.add_argument("--llm", default="llama3-8b")
+    ap.add_argument("--brain-engine", default="llm")
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--brain-gpu", default="0")
+    ap.add_argument("--voice-gpu", default="0")
+    ap.add_argument("--load-timeout", type=float, default=600)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    a.sessions = [int(x) for x in a.sessions.split(",")]
+    a.debounce = a.debounce.split(",")
+    a.chain = a.chain.split(",")
+    res = asyncio.run(run_matrix(a))
+    if a.json:
+        with open(a.json, "a") as f:
+            for r in res:
+                f.write(json.dumps(r) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -80,6 +80,34 @@ def sample_check(tp, dev, ref_model, tp_model):
     return ok
 
 
+def install_nan_trace(tp):
+    """VWA_TP_CHECK_TRACE=1: every kernel wrapper the Llama forward calls synchronises and checks
+    its output; the first non-finite result is printed (rank, op, shapes) once."""
+    state = {"done": False, "n": 0}
+
+    def wrap(name, fn, pick):
+        def run(*a, **k):
+            r = fn(*a, **k)
+            state["n"] += 1
+            if not state["done"]:
+                t = pick(a, k, r)
+                torch.cuda.synchronize()
+                if t is not None and not torch.isfinite(t.float()).all():
+                    state["done"] = True
+                    ins = [tuple(x.shape) for x in a if isinstance(x, torch.Tensor)]
+                    fin = [bool(torch.isfinite(x.float()).all()) for x in a if isinstance(x, torch.Tensor)]
+                    print(f"[rank {tp.rank}] first non-finite output: op #{state['n']} {name} in={ins} "
+                          f"inputs_finite={fin} out={tuple(t.shape)}", flush=True)
+            return r
+        return run
+
+    out_of = lambda a, k, r: r if isinstance(r, torch.Tensor) else k.get("out")  # noqa: E731
+    for name in ("qkv_rope_write", "decode_attention_rows", "linear", "linear_swiglu", "embedding"):
+        setattr(ops, name, wrap(name, getattr(ops, name), out_of))
+    ar = tp.all_reduce
+    tp.all_reduce = wrap("tp.all_reduce", ar, lambda a, k, r: r)
+
+
 def ar_self_check(tp, dev):
     """The one-shot all-reduce alone (bf16, decode row counts 1..64 of this config's hidden size):
     rank r contributes (r + 1) * x, the sum is (world (world + 1) / 2) * x on every rank."""
@@ -112,6 +140,8 @@ def main():
     tp = init_distributed()
     dev = torch.device("cuda", torch.cuda.current_device())
     ar_ok = ar_self_check(tp, dev)
+    if os.environ.get("VWA_TP_CHECK_TRACE") == "1":
+        install_nan_trace(tp)
     torch.manual_seed(0)
     toks = torch.randint(0, CFG.vocab_size, (110,)).tolist()
     ref_model = LlamaModel(CFG, device=dev, seed=7, tp=TPContext.single())

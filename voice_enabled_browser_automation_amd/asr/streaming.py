@@ -228,9 +228,14 @@ class AsrBatcher:
     engine's free session slots -- and runs them as one ``decode_many`` batch.  While a batch is
     on the GPU the next one accumulates, so under load each GPU pass serves many sessions."""
 
-    def __init__(self, asr_engine, *, max_tokens: int = 96, max_batch: Optional[int] = None):
+    def __init__(self, asr_engine, *, max_tokens: int = 96, max_batch: Optional[int] = None,
+                 tokens_per_s: Optional[float] = None):
+        """tokens_per_s: fixed-work mode for benchmarks on random-init weights (which emit EOT at
+        random): every pass decodes exactly round(audio seconds x tokens_per_s) transcript tokens
+        in all (committed prefix included), as bench.py's ``exact_tokens``."""
         self.eng = asr_engine
         self.max_tokens = max_tokens
+        self.tokens_per_s = tokens_per_s
         self.max_batch = max_batch or len(asr_engine.free_slots)
         self._q: List[tuple] = []
         self._cv = threading.Condition()
@@ -278,7 +283,11 @@ class AsrBatcher:
             t0 = time.perf_counter()
             try:
                 audios = [self.eng.pcm_to_audio(p) for p, _, _ in batch]
-                toks = self.eng.decode_many(audios, [pre for _, pre, _ in batch], max_tokens=self.max_tokens)
+                kw = dict(max_tokens=self.max_tokens)
+                if self.tokens_per_s:
+                    kw = dict(exact_tokens=max(1, min(self.max_tokens, max(
+                        int(round(len(p) / 16000 * self.tokens_per_s)) - len(pre) for p, pre, _ in batch))))
+                toks = self.eng.decode_many(audios, [pre for _, pre, _ in batch], **kw)
                 for (_, pre, fut), t in zip(batch, toks):
                     full = pre + t
                     fut.set_result(Hypothesis(full, self.eng.tok.decode(full).strip()))

@@ -280,7 +280,9 @@ def asr_factory_from_env() -> Optional[Callable[[], Any]]:
     model = WhisperModel(get_config(name), device=dev, weights=LazySafetensors(wpath) if wpath else None)
     eng = AsrEngine(model, load_tokenizer("whisper"),
                     max_sessions=int(os.environ.get("VWA_MAX_SESSIONS", "8")))
-    batcher = AsrBatcher(eng)
+    # VWA_ASR_TOKENS_PER_S: fixed-work transcripts for benchmarks on random-init weights
+    tps = float(os.environ.get("VWA_ASR_TOKENS_PER_S", "0") or 0) or None
+    batcher = AsrBatcher(eng, tokens_per_s=tps)
     every = float(os.environ.get("VWA_PARTIAL_EVERY_S", "1.0"))
 
     def factory():
