@@ -115,6 +115,16 @@ VWA_DEVICE f32x4 mfma16_fp8(long a, long b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
 }
 
+// OCP fp8 e4m3 on the block-scaled MX MFMA, 16x16x128 (v_mfma_scale_f32_16x16x128_f8f6f4): 32 fp8
+// per lane per operand; unit E8M0 block scales (127 = 2^0) -- the per-row scales are applied in
+// the epilogue.  Twice the bf16 MFMA rate per clock (MI355X_MICROARCH.md: the non-scaled 16x16x32
+// fp8 form only runs at the bf16 rate) and a quarter of the instructions.  A and B take the same
+// (lane, byte) -> k assignment, so any k order the operands share gives the full dot product.
+using i32x8 = __attribute__((ext_vector_type(8))) int;
+VWA_DEVICE f32x4 mfma16x128_fp8(const i32x8& a, const i32x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
 // two f32 -> two OCP e4m3 bytes (round to nearest even, saturating at +-448 via the caller's scale)
 VWA_DEVICE uint32_t cvt_pk_fp8(float a, float b) {
   return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xFFFFu;

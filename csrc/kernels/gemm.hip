@@ -140,25 +140,30 @@ VWA_DEVICE void compute_stage(const char* buf, f32x4 (&acc)[C::FM][C::FN], int w
   const char* la = buf + (wm * C::FM * 16 + rl) * 128;
   const char* lb = buf + C::A_BYTES + (wn * C::FN) * 2048 + l * 16;
   if constexpr (F8) {
+    // one 128-deep MX MFMA per fragment pair: lane (row / column, g) supplies the 32 fp8 of
+    // k 32 g .. 32 g + 32 -- A chunks 2 g and 2 g + 1 of the swizzled image, B blocks s2 = 0, 1 of
+    // the fp8 tiled layout -- each read with one ds_read_b128 (conflict-free, as the bf16 path).
+    // (The earlier 16x16x32 form read 8-byte halves, which the compiler merged into
+    // ds_read2st64_b64 -- 16-lane groups on 32 banks: 49.8 % LDS bank conflicts,
+    // profiles/r3_pmc_fp8_chain.md -- and ran at the bf16 MFMA rate.)
+    i32x8 a[C::FM], b[C::FN];
+    const int c0 = ((2 * g) ^ swz(rl >> 1)) << 4, c1 = ((2 * g + 1) ^ swz(rl >> 1)) << 4;
 #pragma unroll
-    for (int sg = 0; sg < 4; ++sg) {
-      // 32-deep MFMA sub-steps: chunk 2 g + (sg >> 1), 8-byte half (sg & 1) ^ (g & 1) -- the odd
-      // k-columns take the halves in the other order (the same permutation on A and B, so every
-      // k pair still meets once), which puts the two columns of a ds_read_b64 lane group on
-      // different banks
-      long a[C::FM], b[C::FN];
-      const int hs8 = 8 * ((sg & 1) ^ (g & 1));
-      const int ch = (((2 * g + (sg >> 1)) ^ swz(rl >> 1)) << 4) + hs8;
-#pragma unroll
-      for (int i = 0; i < C::FM; ++i) a[i] = *reinterpret_cast<const long*>(la + i * 16 * 128 + ch);
-#pragma unroll
-      for (int j = 0; j < C::FN; ++j)
-        b[j] = *reinterpret_cast<const long*>(lb + j * 2048 + (sg >> 1) * 1024 + hs8);
-#pragma unroll
-      for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16_fp8(a[i], b[j], acc[i][j]);
+    for (int i = 0; i < C::FM; ++i) {
+      const uint4 lo = *reinterpret_cast<const uint4*>(la + i * 16 * 128 + c0);
+      const uint4 hi = *reinterpret_cast<const uint4*>(la + i * 16 * 128 + c1);
+      a[i] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
     }
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+      const uint4 lo = *reinterpret_cast<const uint4*>(lb + j * 2048);
+      const uint4 hi = *reinterpret_cast<const uint4*>(lb + j * 2048 + 1024);
+      b[j] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x128_fp8(a[i], b[j], acc[i][j]);
   } else {
 #pragma unroll
     for (int sp = 0; sp < 2; ++sp) {
