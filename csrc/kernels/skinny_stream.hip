@@ -113,23 +113,27 @@ VWA_DEVICE void epi_values(const SkinnyParams& p, int tile, int o, EpiPre& e) {
 // / LayerNorm rstd and, on the fp8 path, the activation quantisation scale); mus[m] (folded
 // LayerNorm only, else null): row mean, removed as mean * ln_c[n]; column scales (fp8) come
 // with the epilogue operands (`pre` when this is the workgroup's first tile).
-template <int EPI, int NT, int KS, bool SC1 = false>
+// MT: 16-row MFMA row fragments per tile (M <= 16 MT; MT > 1 only in the streaming kernel's
+// many-row form, skinny_stream_kernel); red = [KS][NT][MT][4][64] partial sums.
+template <int EPI, int NT, int KS, bool SC1 = false, int MT = 1>
 VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs, const float* mus, int tile,
-                              f32x4 (&acc)[NT], int w, int lane, const EpiPre& pre, bool first,
+                              f32x4 (&acc)[NT * MT], int w, int lane, const EpiPre& pre, bool first,
                               const float* partner = nullptr) {
   const int M = p.M;
   const int n0 = tile * 16 * NT;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) red[((w * NT + nt) * 4 + i) * 64 + lane] = acc[nt][i];
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(((w * NT + nt) * MT + mt) * 4 + i) * 64 + lane] = acc[nt * MT + mt][i];
   __syncthreads();
   auto red_at = [&](int m, int nn) -> float {
-    const int nt = nn >> 4, q = nn & 15;
-    const int ln = q + 16 * (m >> 2), i = m & 3;
+    const int nt = nn >> 4, q = nn & 15, mt = MT > 1 ? m >> 4 : 0, mm = m & 15;
+    const int ln = q + 16 * (mm >> 2), i = mm & 3;
     float s = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < KS; ++ww) s += red[((ww * NT + nt) * 4 + i) * 64 + ln];
+    for (int ww = 0; ww < KS; ++ww) s += red[(((ww * NT + nt) * MT + mt) * 4 + i) * 64 + ln];
     // split tile (chain kernel): the other workgroup's partial sums, published with sc1 stores
     if (partner) s += __hip_atomic_load(gp(partner + m * 16 * NT + nn), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return s;
@@ -204,19 +208,24 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
   }
   __syncthreads();
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < NT * MT; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-template <int EPI, int NT, int KS, bool XG>
+// MT > 1 (17..64 rows: continuous batching of many sessions): every weight fragment meets MT
+// X row fragments, so a step of up to 64 rows streams the weights ONCE in one persistent launch
+// with the fused epilogues (instead of split-K GEMM launches + reduce + epilogue kernels).
+template <int EPI, int NT, int KS, bool XG, int MT = 1>
 __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, int nb, int xstride) {
-  constexpr int U = XG ? 2 : 4 / NT;  // k-groups (128 wide) per item
+  // k-groups (128 wide) per item; MT > 1: one (the X fragments of MT row tiles share the
+  // register budget of the item's weights)
+  constexpr int U = MT > 1 ? 1 : XG ? 2 : 4 / NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int M = p.M, K = p.K, N = p.N;
   u16* xs = reinterpret_cast<u16*>(smem);
   const int xbytes = XG ? 0 : ((M * xstride * 2) + 15) & ~15;
-  float* red = reinterpret_cast<float*>(smem + xbytes);  // [KS][NT][4][64]
-  float* rs = red + KS * NT * 4 * 64;                     // [16] row scales (1/rms, LayerNorm rstd)
-  float* mu = rs + 16;                                    // [16] row means (folded LayerNorm)
+  float* red = reinterpret_cast<float*>(smem + xbytes);  // [KS][NT][MT][4][64]
+  float* rs = red + KS * NT * MT * 4 * 64;                // [16 MT] row scales (1/rms, LayerNorm rstd)
+  float* mu = rs + 16 * MT;                               // [16 MT] row means (folded LayerNorm)
   const float* mus = (p.fuse_rms == 2) ? mu : nullptr;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nl = lane & 15, g = lane >> 4;
@@ -253,16 +262,18 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
   const int n_items = n_live * nb;
   auto tile_of = [&](int it) { return masked ? __shfl(live_tile, it / nb, 64) : (int)blockIdx.x + (it / nb) * (int)gridDim.x; };
 
-  auto load_x = [&](uint4 (&xr)[U][4], int it) {
+  auto load_x = [&](uint4 (&xr)[MT][U][4], int it) {
     const int b = it % nb;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kg = gb + b * U + u;
-      const bool ok = (it < n_items) && (kg < ge) && (nl < M);
-      const unsigned base = ((unsigned)nl * (unsigned)p.ldx + (unsigned)(kg * 128 + 32 * g)) * 2u;
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) xr[u][s] = bload(rx, ok ? base + 16u * s : kOOB);
-    }
+      for (int u = 0; u < U; ++u) {
+        const int kg = gb + b * U + u, row = 16 * mt + nl;
+        const bool ok = (it < n_items) && (kg < ge) && (row < M);
+        const unsigned base = ((unsigned)row * (unsigned)p.ldx + (unsigned)(kg * 128 + 32 * g)) * 2u;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) xr[mt][u][s] = bload(rx, ok ? base + 16u * s : kOOB);
+      }
   };
 
   auto load_item = [&](uint4 (&wr)[NT][U][4], int it) {
@@ -289,11 +300,11 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
     }
   };
 
-  f32x4 acc[NT];
+  f32x4 acc[NT * MT];
 #pragma unroll
-  for (int nt = 0; nt < NT; ++nt) acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < NT * MT; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto compute_item = [&](const uint4 (&wr)[NT][U][4], const uint4 (&xr)[U][4], int it) {
+  auto compute_item = [&](const uint4 (&wr)[NT][U][4], const uint4 (&xr)[MT][U][4], int it) {
     const int b = it % nb;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -301,21 +312,26 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
       if (kg >= ge) break;  // wave-uniform
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        uint4 a = make_uint4(0, 0, 0, 0);
-        if constexpr (XG) a = xr[u][s];
-        else if (nl < M) a = *reinterpret_cast<const uint4*>(xs + nl * xstride + kg * 128 + 32 * g + 8 * s);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[nt] = mfma16(as_bf16x8(a), as_bf16x8(wr[nt][u][s]), acc[nt]);
+        for (int mt = 0; mt < MT; ++mt) {
+          uint4 a = make_uint4(0, 0, 0, 0);
+          if constexpr (XG) a = xr[mt][u][s];
+          else if (16 * mt + nl < M)
+            a = *reinterpret_cast<const uint4*>(xs + (16 * mt + nl) * xstride + kg * 128 + 32 * g + 8 * s);
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            acc[nt * MT + mt] = mfma16(as_bf16x8(a), as_bf16x8(wr[nt][u][s]), acc[nt * MT + mt]);
+        }
       }
     }
   };
 
   auto finish_tile = [&](int it) {
-    tile_epilogue<EPI, NT, KS>(p, red, rs, mus, tile_of(it), acc, w, lane, pre, !masked && it < nb);
+    tile_epilogue<EPI, NT, KS, false, MT>(p, red, rs, mus, tile_of(it), acc, w, lane, pre, !masked && it < nb);
   };
 
   uint4 A[NT][U][4], B[NT][U][4];
-  uint4 XA[U][4], XB[U][4];  // XG only (dead otherwise)
+  uint4 XA[MT][U][4], XB[MT][U][4];  // XG only (dead otherwise)
   // w_first: issue the first weight item before staging X (its round trip then overlaps the X
   // staging + fused-RMSNorm statistics); otherwise stage X first (the X round trip is short).
   if (p.w_first) {
@@ -332,7 +348,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
     }
   }
   __syncthreads();
-  for (int m = w; m < 16; m += KS) {
+  for (int m = w; m < 16 * MT; m += KS) {
     float sc = 1.f, mean = 0.f;
     if (p.fuse_rms && m < M) {
       float s = 0.f, s1 = 0.f;
@@ -382,15 +398,15 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
   }
 }
 
-template <int EPI, int NT, int KS, bool XG>
+template <int EPI, int NT, int KS, bool XG, int MT = 1>
 int launch_v(const SkinnyParams& p, hipStream_t st, int grid_cap, size_t lds, int xstride) {
-  constexpr int U = XG ? 2 : 4 / NT;
+  constexpr int U = MT > 1 ? 1 : XG ? 2 : 4 / NT;
   const int G = p.K / 128;
   const int per_wave = (G + KS - 1) / KS;
   const int nb = (per_wave + U - 1) / U;
   const int ntiles = p.N / (16 * NT);
   const int grid = ntiles < grid_cap ? ntiles : grid_cap;
-  hipLaunchKernelGGL((skinny_stream_kernel<EPI, NT, KS, XG>), dim3(grid), dim3(KS * 64), lds, st, p, nb, xstride);
+  hipLaunchKernelGGL((skinny_stream_kernel<EPI, NT, KS, XG, MT>), dim3(grid), dim3(KS * 64), lds, st, p, nb, xstride);
   return 0;
 }
 
@@ -398,6 +414,19 @@ template <int EPI, int NT, int KS>
 int launch(const SkinnyParams& p0, hipStream_t st, int grid_cap) {
   SkinnyParams p = p0;
   const int xstride = p.K + 8;
+  if (p.M > 16) {
+    // 17..64 rows: X fragments stream with the weights (XG; the rows no longer fit LDS at the
+    // decode shapes), 2 or 4 row fragments per weight fragment; no folded LayerNorm, no mask
+    if constexpr (KS == 8) {
+      if (p.fuse_rms == 2 || p.M > 64 || (size_t)p.M * p.ldx * 2 >= 0x7FFFFFF0ull) return -10;
+      p.col_mask = nullptr;
+      if (p.M <= 32)
+        return launch_v<EPI, NT, KS, true, 2>(p, st, grid_cap, (size_t)(KS * NT * 2 * 4 * 64 + 64) * 4, xstride);
+      return launch_v<EPI, NT, KS, true, 4>(p, st, grid_cap, (size_t)(KS * NT * 4 * 4 * 64 + 128) * 4, xstride);
+    } else {
+      return -10;
+    }
+  }
   const size_t xbytes = ((size_t)p.M * xstride * 2 + 15) & ~(size_t)15;
   const size_t red = (size_t)(KS * NT * 4 * 64 + 32) * sizeof(float);  // + row scales + row means
   const bool lds_x = xbytes + red <= 160 * 1024;
@@ -1573,7 +1602,7 @@ int dispatch_ks(int epi, const SkinnyParams& p, int grid_cap, hipStream_t st) {
 // Returns -10 when this shape does not fit the streaming kernel (caller falls back).
 // ks = waves per workgroup splitting K (4 or 8); grid_cap = max persistent workgroups.
 extern "C" int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st) {
-  if (p->M < 1 || p->M > 16 || p->K % 128 != 0) return -10;
+  if (p->M < 1 || p->M > 64 || p->K % 128 != 0) return -10;
   if ((size_t)p->N * p->K * (p->w_scale ? 1 : 2) >= 0x7FFFFFF0ull) return -10;
   const int r = (ks == 4) ? dispatch_ks<4>(epi, *p, grid_cap, st) : dispatch_ks<8>(epi, *p, grid_cap, st);
   if (r) return r;

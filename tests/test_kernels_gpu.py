@@ -809,3 +809,43 @@ def test_llama70b_tp8_per_rank_decode_shapes(M):
     for a, b in ((q, q2), (kc, kc2), (vc, vc2)):
         assert torch.isfinite(a.float()).all()
         close(a, b, 3e-2)
+
+
+@pytest.mark.parametrize("M", [17, 24, 32, 33, 48, 64])
+def test_streaming_kernel_many_rows(M):
+    """17..64 decode rows (continuous batching) on the streaming kernel with pre-tiled weights
+    (skinny_stream.hip MT = 2 / 4 row fragments per weight fragment, X streamed with the weights):
+    store (f32 out + fused RMSNorm, the LM head), residual (the down shape, K = 14336), SwiGLU
+    and QKV + RoPE + paged-KV write, against the f32 reference."""
+    assert ops.STREAM_MAX_M >= 64
+    K, N = 4096, 1024
+    x = rnd(M, K)
+    w = rnd(N, K, scale=0.02)
+    y = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    ops.linear(x, ops.TiledWeight(w), out=y, fuse_rms=True)
+    close(y, ref.linear(x.cpu(), w.cpu(), None, out=torch.empty(M, N), fuse_rms=True), 2e-3, 2e-3)
+    xd, wd, res = rnd(M, 14336), rnd(512, 14336, scale=0.01), rnd(M, 512)
+    out = res.clone()
+    ops.linear(xd, ops.TiledWeight(wd), out=out, residual=out)
+    close(out, ref.linear(xd.cpu(), wd.cpu(), None, out=torch.empty(M, 512, dtype=BF), residual=res.cpu()), 2e-2)
+    F = 768
+    gu = ops.interleave_gate_up(rnd(F, K, scale=0.02), rnd(F, K, scale=0.02))
+    a = ops.linear_swiglu(x, ops.TiledWeight(gu), fuse_rms=True)
+    close(a, ref.linear_swiglu(x.cpu(), gu.cpu(), fuse_rms=True, eps=1e-5, out=torch.empty(M, F, dtype=BF)), 2e-2)
+    nq, nkv, hd = 8, 2, 128
+    H = nq + 2 * nkv
+    wq = ops.permute_qkv_rows(rnd(H * hd, K, scale=0.02), H, hd)
+    rope = ops.rope_table(512, hd, 5e5, device=DEV)
+    pos = torch.randint(0, 400, (M,), dtype=torch.int32, device=DEV)
+    slots = torch.randperm(16 * 8, device=DEV)[:M].to(torch.int64)
+    kc = torch.zeros(8, nkv, 16, hd, dtype=BF, device=DEV)
+    vc = torch.zeros_like(kc)
+    q = torch.zeros(M, nq * hd, dtype=BF, device=DEV)
+    ops.qkv_rope_write(x, ops.TiledWeight(wq), None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
+                       rope=rope, positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc)
+    kc2, vc2 = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    q2 = torch.zeros(M, nq * hd, dtype=BF)
+    ref.qkv_rope_write(x.cpu(), wq.cpu(), None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
+                       rope=rope.cpu(), positions=pos.cpu(), slots=slots.cpu(), q_out=q2, k_cache=kc2, v_cache=vc2)
+    for a_, b_ in ((q, q2), (kc, kc2), (vc, vc2)):
+        close(a_, b_, 3e-2)

@@ -256,8 +256,10 @@ class TiledWeight:
 
 
 def _stream_ok(x: torch.Tensor, w) -> bool:
-    """Decode rows the streaming kernel takes with a pre-tiled weight."""
-    return x.shape[0] <= SKINNY_MAX_M and x.shape[1] % 128 == 0 and w.shape[0] % 16 == 0
+    """Decode rows the streaming kernel takes with a pre-tiled weight: up to STREAM_MAX_M (64) --
+    above 16 rows with 2 or 4 X row fragments per streamed weight fragment (skinny_stream.hip MT),
+    one persistent launch with the fused epilogue instead of split-K GEMM + reduce launches."""
+    return x.shape[0] <= STREAM_MAX_M and x.shape[1] % 128 == 0 and w.shape[0] % 16 == 0
 
 
 def plain(w):
@@ -438,6 +440,9 @@ def gemm_ok(x: torch.Tensor, w, out: Optional[torch.Tensor] = None, residual: Op
 # Rows handled by the MFMA streaming (skinny) kernels; above this the hand-written LDS-tiled MFMA
 # GEMM (gemm.hip) takes the step (continuous batching of many sessions, prefill).
 SKINNY_MAX_M = 16
+# Rows the streaming kernel takes with PRE-TILED bf16 weights (the models' decode weights):
+# many-row continuous-batching steps stay on it (VWA_STREAM_MAX_M=16 restores the tiled GEMM).
+STREAM_MAX_M = max(16, min(64, int(os.environ.get("VWA_STREAM_MAX_M", "64"))))
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, out: Optional[torch.Tensor] = None,
