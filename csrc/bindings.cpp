@@ -58,7 +58,8 @@ void set_small_gemm_bytes(int64_t n) { g_small_bytes = (size_t)(n > 0 ? n : 0); 
 // at K = 1280 (Whisper-large-v3's decoder) 8 waves leave 6 idle in the second round; measured
 // (tools/bench_whisper_decode.py, tiled weights, HBM-resident) 6.45 vs 6.83 us for QKV, 8.33 vs
 // 8.97 for fc1, 27.9 vs 34.2 for the 133 MB LM head; K >= 4096 (Llama) stays at 8.
-int skinny_ks(const SkinnyParams& p) { return g_ks ? g_ks : (p.K < 2048 ? 4 : 8); }
+// (> 16 rows: the many-row form exists for 8 waves only)
+int skinny_ks(const SkinnyParams& p) { return g_ks ? g_ks : (p.K < 2048 && p.M <= 16 ? 4 : 8); }
 
 bool small_gemm(const SkinnyParams& p) {
   return !p.w_scale && g_small_bytes && p.M <= 16 && ((size_t)p.N * p.K * 2 <= g_small_bytes || p.K < 1024);

@@ -1378,7 +1378,13 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   // (hand-off by count: a workgroup without o_proj units skips the phase -- its X rows may not be
   // complete yet, and nothing of it is used)
   if (!(AG > 0 && cp.attn_flag) || chain_range<KS>(cp.ph[0], ob0, on).n_items > 0)
-    chain_phase<E0, KS, WA, false, F8>(cp, 0, B, A, smem, nx ? 1 : pre0, 2, ob0, on);
+    // hs: items the staging wave already holds -- 2 (items 0 and 1, or with nx item 0 and phase
+    // 1's item 0), but only item 0 when this workgroup ran an attention item (pre0 = 0: its
+    // register set A was live in the attention until then).  (A fixed 2 here left the staging
+    // wave's item 1 unloaded whenever an attention workgroup also had >= 2 o_proj items -- more
+    // attention items than half the grid: several sessions' rows, or a grid cut by
+    // VWA_CHAIN_GRID_DIV -- and its MFMAs read stale registers: NaN / wrong o_proj tiles.)
+    chain_phase<E0, KS, WA, false, F8>(cp, 0, B, A, smem, nx ? 1 : pre0, nx ? 2 : 1 + (pre0 ? 1 : 0), ob0, on);
   stamp();
   if (SEQ == 0 && tpr) chain_tp_reduce(cp, 0, e0 + 1, bar, nwg, bar_next);
   gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);

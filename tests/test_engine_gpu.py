@@ -204,31 +204,37 @@ def test_chained_layer_tail_matches_per_kernel_path(cfg, grid_div, monkeypatch):
         assert err < 0.02 * (1 + b.abs().max().item()), err
 
 
-def test_llama70b_shape_chained_layers_match_f32_reference():
+@pytest.mark.parametrize("grid_div,max_len", [(1, 256), (8, 512)], ids=["full-grid", "griddiv8"])
+def test_llama70b_shape_chained_layers_match_f32_reference(grid_div, max_len, monkeypatch):
     """Llama-3-70B layer shapes (hidden 8192, 64 q / 8 kv heads -> GQA 8:1, FFN 28672; BASELINE
     config 4 at TP=1) through the chained decode launch -- decode attention as phase 0 at 1-2
     rows, the tail alone with a separate attention launch at 3-4 rows, where the 28672-wide down
     rows no longer fit LDS next to the attention -- against the CPU f32 reference engine on the
-    same bf16 weights (2 layers, small vocab)."""
+    same bf16 weights (2 layers, small vocab), with rows of one and of two sessions.  griddiv8:
+    32 workgroups (eight ranks sharing a GPU), where every workgroup runs an attention item AND
+    several o_proj items (the path whose staging wave once computed an unloaded item: NaN)."""
     import copy
 
     ops.ext()
+    monkeypatch.setenv("VWA_CHAIN_GRID_DIV", str(grid_div))
     torch.manual_seed(0)
     cfg = LlamaConfig(name="t70", vocab_size=4096, hidden=8192, n_layers=2, n_heads=64, n_kv_heads=8, head_dim=128,
                       ffn=28672, max_pos=2048)
-    toks = torch.randint(0, cfg.vocab_size, (40,)).tolist()
+    toks = torch.randint(0, cfg.vocab_size, (60,)).tolist()
     cpu = LlamaModel(cfg, device="cpu", seed=3)
     gpu = copy.deepcopy(cpu)
     move_model(gpu, "cuda")
     gpu._tile_weights()
 
     def run(model):
-        e = LLMEngine(model, max_seqs=2, max_model_len=256, kv_blocks=20, block_size=16)
+        e = LLMEngine(model, max_seqs=3, max_model_len=max_len, kv_blocks=60, block_size=16)
         s = e.new_sequence(toks[:30], use_prefix_cache=False)
-        out, i = [e.prefill(s).float().cpu().clone()], 30
-        for n in (1, 2, 3, 4):
-            out.append(e.run_rows([(s, t) for t in toks[i:i + n]]).float().cpu().clone())
-            i += n
+        s2 = e.new_sequence(toks[10:37], use_prefix_cache=False)
+        out = [e.prefill(s).float().cpu().clone(), e.prefill(s2).float().cpu().clone()]
+        for rows in ([(s, toks[40])], [(s, toks[41]), (s2, toks[42])], [(s, toks[43]), (s, toks[44])],
+                     [(s, toks[45]), (s, toks[46]), (s2, toks[47])],
+                     [(s, toks[48]), (s, toks[49]), (s2, toks[50]), (s2, toks[51])]):
+            out.append(e.run_rows(rows).float().cpu().clone())
         return out, e
 
     ref, _ = run(cpu)
@@ -239,7 +245,7 @@ def test_llama70b_shape_chained_layers_match_f32_reference():
     assert any(v[3] == 8 for v in descs), "no step chained the GQA-8 decode attention"
     for i, (a, b) in enumerate(zip(got, ref)):
         err = (a - b).abs().max().item()
-        assert err < 0.03 * (1 + b.abs().max().item()), (i, err)
+        assert math.isfinite(err) and err < 0.03 * (1 + b.abs().max().item()), (i, err)
 
 
 def test_chain_timeout_falls_back_to_per_kernel_launches():

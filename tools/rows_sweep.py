@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--prefix", type=int, default=1024)
     ap.add_argument("--suffix", type=int, default=85)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--no-prefill-bench", action="store_true", help="skip the admission prefill comparison")
     a = ap.parse_args()
     ops.ext()
     dev = torch.device("cuda")
@@ -52,7 +53,7 @@ def main():
 
     # ---- admission prefill: R requests' suffixes, batched vs one by one
     suf = [torch.randint(1000, 100000, (a.suffix,), generator=g).tolist() for _ in range(R)]
-    for mode in ("serial", "batched", "serial", "batched"):
+    for mode in (() if a.no_prefill_bench else ("serial", "batched", "serial", "batched")):
         seqs = [e.new_sequence(head + s) for s in suf]
         torch.cuda.synchronize()
         t0 = time.perf_counter()

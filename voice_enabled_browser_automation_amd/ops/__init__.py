@@ -440,9 +440,11 @@ def gemm_ok(x: torch.Tensor, w, out: Optional[torch.Tensor] = None, residual: Op
 # Rows handled by the MFMA streaming (skinny) kernels; above this the hand-written LDS-tiled MFMA
 # GEMM (gemm.hip) takes the step (continuous batching of many sessions, prefill).
 SKINNY_MAX_M = 16
-# Rows the streaming kernel takes with PRE-TILED bf16 weights (the models' decode weights):
-# many-row continuous-batching steps stay on it (VWA_STREAM_MAX_M=16 restores the tiled GEMM).
-STREAM_MAX_M = max(16, min(64, int(os.environ.get("VWA_STREAM_MAX_M", "64"))))
+# Rows the streaming kernel takes with PRE-TILED bf16 weights.  17..64 rows are supported
+# (skinny_stream.hip MT = 2 / 4, X streamed with the weights) but measured slower than the tiled
+# GEMM for whole decode steps (Llama-3-8B, tools/rows_sweep.py, profiles/r4_rows_sweep_*: 32 rows
+# 6.89 vs 5.65 ms, 64 rows 11.0 vs 6.9 ms): opt-in with VWA_STREAM_MAX_M.
+STREAM_MAX_M = max(16, min(64, int(os.environ.get("VWA_STREAM_MAX_M", "16"))))
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, out: Optional[torch.Tensor] = None,
