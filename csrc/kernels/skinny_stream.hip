@@ -765,16 +765,36 @@ VWA_DEVICE void chain_tp_reduce(const ChainParams& cp, int region, int target, u
   __syncthreads();
   const SkinnyParams& hp = cp.ph[1].p;  // gate/up's X: the hidden rows h
   u16* h = const_cast<u16*>(hp.X);
-  const int d = hp.K, n = hp.M * d;
-  const int per = (n + nwg - 1) / nwg, lo = (int)blockIdx.x * per, hi = min(n, lo + per);
+  const int d = hp.K, n4 = hp.M * d / 4;  // (d % 128 == 0: a 4-float group never crosses a row)
+  const int per = (n4 + nwg - 1) / nwg, lo = (int)blockIdx.x * per, hi = min(n4, lo + per);
+  // every peer's partials of this 16-byte group: one system-coherent 16-byte load each (sc0 sc1,
+  // the system-scope atomic load's cache bits) -- a quarter of the transactions of per-float
+  // atomic loads over xGMI -- all issued before any is summed, rank order kept (identical bits)
+  constexpr int kMaxW = 8;
+  __amdgpu_buffer_rsrc_t rs[kMaxW];
+#pragma unroll
+  for (int q = 0; q < kMaxW; ++q)
+    rs[q] = __builtin_amdgcn_make_buffer_rsrc(q < tp.world ? tp.stage[q] + (size_t)region * tp.region : tp.stage[0],
+                                              (short)0, (int)(tp.region * sizeof(float)), 0x00020000);
   for (int i = lo + (int)threadIdx.x; i < hi; i += (int)blockDim.x) {
-    const int m = i / d, c = i - m * d;
-    float acc = 0.f;
-    for (int q = 0; q < tp.world; ++q)
-      acc += __hip_atomic_load(gp(tp.stage[q] + (size_t)region * tp.region + i), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
+    const int m = (4 * i) / d, c = 4 * i - m * d;
+    u32x4 part[kMaxW];
+#pragma unroll
+    for (int q = 0; q < kMaxW; ++q)
+      if (q < tp.world) part[q] = __builtin_amdgcn_raw_buffer_load_b128(rs[q], 16 * i, 0, 17);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < kMaxW; ++q)
+      if (q < tp.world) {
+        const float4 f = __builtin_bit_cast(float4, part[q]);
+        acc[0] += f.x;
+        acc[1] += f.y;
+        acc[2] += f.z;
+        acc[3] += f.w;
+      }
     u16* hp_ = h + (size_t)m * hp.ldx + c;
-    st_u16<true>(hp_, f2bf(bf2f(ld_u16<true>(hp_)) + acc));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st_u16<true>(hp_ + j, f2bf(bf2f(ld_u16<true>(hp_ + j)) + acc[j]));
   }
 }
 

@@ -1,6 +1,6 @@
 """fp8 decode step (W8A16 chained layer over the fp8 tiled weights, fp8 LM head) of a
 Llama-3-8B-shaped model, launched ITERS times eagerly: the rocprofv3 --pmc target for the fp8
-decode's HBM bytes and MFMA use (tools/gpu_pmc_fp8.sh, summary by tools/pmc_summary.py).
+decode's HBM bytes and MFMA use (tools/gpu_recipes.sh pmc, summary by tools/pmc_summary.py).
 
 3 layers (0.65 GB of fp8 weights > the 256 MB Infinity Cache, as the full model's 7.5 GB per
 token), 1 row at ~1.1k context, the bench's shape.

@@ -1,5 +1,5 @@
 """ASR front-end kernels, each launched ITERS times eagerly: the target program of rocprofv3
-hardware-counter passes (tools/gpu_pmc_frontend.sh; summary: tools/pmc_summary.py).
+hardware-counter passes (tools/gpu_recipes.sh frontend; summary: tools/pmc_summary.py).
 
 Shapes: log-mel (80 / 128 mels, one 30 s window), the conv stem of whisper-tiny and large-v3
 (padded-buffer path: the batched implicit GEMM), flash attention for the whisper-tiny / large-v3
