@@ -609,6 +609,9 @@ int launch_fp8(const SkinnyParams& p, hipStream_t st, int grid_cap) {
 // co-resident: the grid is one workgroup per CU.
 // ------------------------------------------------------------------------------------------
 constexpr int kChainSpinLimit = 1 << 18;  // ~0.3 s: a lost workgroup ends the launch, not the GPU
+// the in-launch TP rounds wait for PEER PROCESSES, whose host-side skew (graph capture, Python,
+// eight ranks sharing one GPU) can exceed the intra-launch bound: ~4 s before a peer is declared lost
+constexpr int kChainTpSpinLimit = 1 << 22;
 
 // Grid barrier on monotonic 64-bit tickets (no reset, no generation word, never wraps): a
 // workgroup's ticket t on its counter tells it which barrier instance it is in, so it can wait for
@@ -756,7 +759,7 @@ VWA_DEVICE void chain_tp_reduce(const ChainParams& cp, int region, int target, u
     int spins = 0;
     while (__hip_atomic_load(gp(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target < 0) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > kChainSpinLimit) {
+      if (++spins > kChainTpSpinLimit) {
         __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }

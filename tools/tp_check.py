@@ -48,6 +48,9 @@ def run(model, toks, graphs):
     e = LLMEngine(model, max_seqs=2, max_model_len=512, kv_blocks=80, use_graphs=graphs)
     if graphs:
         e.capture_all()
+    torch.cuda.synchronize()
+    if model.tp.size > 1:  # (as the serving control plane does per iteration: ranks start aligned)
+        dist.barrier()
     s = e.new_sequence(toks[:100], use_prefix_cache=False)
     out = [e.prefill(s).float().cpu().clone()]
     for t in toks[100:104]:
