@@ -37,3 +37,10 @@ def test_oneshot_allreduce_two_ranks():
 def test_tensor_parallel_llama_two_ranks():
     rc, out = _torchrun("tp_check.py", {"VWA_DIST_BACKEND": "gloo"})
     assert rc == 0 and "TP_CHECK PASS" in out, out[-3000:]
+
+
+def test_tp_brain_continuous_batching_two_ranks():
+    """brain/tp_engine.py on the GPU kernels: 4 concurrent requests on a TP=2 group decode together
+    in lockstep (chained layers with in-launch all-reduce rounds, vocab-parallel sampling)."""
+    rc, out = _torchrun("tp_brain_check.py", {"VWA_DIST_BACKEND": "gloo"}, timeout=280)
+    assert rc == 0 and "TP_BRAIN_CHECK PASS" in out, out[-3000:]
