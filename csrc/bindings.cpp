@@ -201,8 +201,16 @@ int device_cus(const Tensor& t) {
 // add (+bias), 2 SwiGLU over interleaved gate/up tiles (y [M, N/2]), 3 GELU (+bias).  rstd: f32
 // [M] per-row RMSNorm scale applied to the product (gammas folded into w).  ws: f32 split-K
 // workspace (the launcher splits K only when the output tiles alone cannot fill the CUs).
+static void set_tickets(GemmParams& p, const c10::optional<Tensor>& tickets) {
+  if (!tickets.has_value()) return;
+  TORCH_CHECK(tickets->is_cuda() && tickets->scalar_type() == at::kInt && tickets->is_contiguous(),
+              "tickets: zeroed int32 counters");
+  p.tickets = tickets->data_ptr<int>();
+  p.n_tickets = (int)tickets->numel();
+}
+
 void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi, c10::optional<Tensor> rstd,
-          c10::optional<Tensor> residual, bool w_tiled, c10::optional<Tensor> ws) {
+          c10::optional<Tensor> residual, bool w_tiled, c10::optional<Tensor> ws, c10::optional<Tensor> tickets) {
   c10::DeviceGuard g(x.device());
   check_bf16(x, "x");
   check_bf16(w, "w");
@@ -258,6 +266,7 @@ void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi,
     p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws->numel());
     p.ws_cap = ws->numel();
   }
+  set_tickets(p, tickets);
   p.cus = device_cus(x);
   check_rc(vwa_gemm((int)epi, &p, cur_stream(x)), "gemm");
 }
@@ -265,7 +274,8 @@ void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi,
 // W8A8 tiled GEMM (gemm.hip, F8): x8 OCP e4m3 [M, K] with per-row scales sx (quant_fp8_rows),
 // w8 the fp8 tiled layout [N, K] with per-row scales sw.
 void gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> bias, Tensor y, int64_t epi,
-              c10::optional<Tensor> rstd, c10::optional<Tensor> residual, c10::optional<Tensor> ws) {
+              c10::optional<Tensor> rstd, c10::optional<Tensor> residual, c10::optional<Tensor> ws,
+              c10::optional<Tensor> tickets) {
   c10::DeviceGuard g(x8.device());
   TORCH_CHECK(x8.is_cuda() && x8.scalar_type() == at::kFloat8_e4m3fn && x8.dim() == 2 && x8.stride(1) == 1 &&
                   x8.stride(0) % 16 == 0 && (reinterpret_cast<uintptr_t>(x8.data_ptr()) & 15) == 0,
@@ -321,7 +331,88 @@ void gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> 
     p.ws = ws->data_ptr<float>();
     p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x8), ws->numel());
   }
+  set_tickets(p, tickets);
   check_rc(vwa_gemm((int)epi, &p, cur_stream(x8)), "gemm_fp8");
+}
+
+void check_cache(const Tensor& c, const char* name);
+
+// QKV projection on the tiled GEMM with the rotary + paged-KV write in its epilogue (gemm.hip
+// EPI_QKV; > 16 rows): x bf16 (sx null) or fp8 codes x8 with per-row scales sx (W8A8, w fp8 tiled
+// with row scales sw).  Replaces gemm -> qkv scratch -> rope_kv_write.
+void gemm_qkv(Tensor x, c10::optional<Tensor> sx, Tensor w, c10::optional<Tensor> sw, c10::optional<Tensor> bias,
+              c10::optional<Tensor> rstd, bool w_tiled, Tensor ws, c10::optional<Tensor> tickets, int64_t n_q_heads,
+              int64_t n_kv_heads, int64_t head_dim, bool use_rope, Tensor positions, Tensor slots,
+              c10::optional<Tensor> rope, Tensor q_out, Tensor k_cache, Tensor v_cache) {
+  c10::DeviceGuard g(x.device());
+  const bool f8 = sx.has_value();
+  GemmParams p{};
+  if (f8) {
+    TORCH_CHECK(x.scalar_type() == at::kFloat8_e4m3fn && x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 16 == 0 &&
+                    (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0,
+                "x8: fp8 e4m3 [M, K] rows 16-byte aligned");
+    TORCH_CHECK(sw.has_value() && w.scalar_type() == at::kFloat8_e4m3fn && w_tiled, "W8A8: fp8 tiled w + scales");
+    TORCH_CHECK(sx->scalar_type() == at::kFloat && sx->numel() >= x.size(0), "sx f32 [M]");
+    TORCH_CHECK(sw->scalar_type() == at::kFloat && sw->numel() == w.size(0), "sw f32 [N]");
+    p.sx = sx->data_ptr<float>();
+    p.sw = sw->data_ptr<float>();
+  } else {
+    check_bf16(x, "x");
+    check_contig_rows(x, "x");
+    check_bf16(w, "w");
+  }
+  TORCH_CHECK(w.is_contiguous() && w.dim() == 2 && w.size(1) == x.size(1), "w [N, K] with x's K");
+  p.X = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  p.ldx = (int)x.stride(0);
+  p.W = reinterpret_cast<const uint16_t*>(w.data_ptr());
+  p.w_tiled = w_tiled ? 1 : 0;
+  p.M = (int)x.size(0);
+  p.N = (int)w.size(0);
+  p.K = (int)w.size(1);
+  TORCH_CHECK(p.N == (n_q_heads + 2 * n_kv_heads) * head_dim && head_dim % 16 == 0 && p.K % 128 == 0, "qkv shape");
+  if (bias.has_value()) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->numel() == p.N && bias->is_contiguous(), "bias [N]");
+    p.bias = bfp(*bias);
+  }
+  if (rstd.has_value()) {
+    TORCH_CHECK(rstd->is_cuda() && rstd->scalar_type() == at::kFloat && rstd->numel() >= p.M, "rstd f32 [M]");
+    p.rstd = rstd->data_ptr<float>();
+  }
+  TORCH_CHECK(positions.scalar_type() == at::kInt && positions.numel() >= p.M, "positions");
+  TORCH_CHECK(slots.scalar_type() == at::kLong && slots.numel() >= p.M, "slots");
+  TORCH_CHECK(q_out.dim() == 2 && q_out.size(0) >= p.M && q_out.size(1) == n_q_heads * head_dim && q_out.stride(1) == 1 &&
+                  q_out.stride(0) % 8 == 0 && (reinterpret_cast<uintptr_t>(q_out.data_ptr()) & 15) == 0,
+              "q_out rows 16-byte aligned");
+  check_cache(k_cache, "k_cache");
+  check_cache(v_cache, "v_cache");
+  TORCH_CHECK(k_cache.stride(0) % 8 == 0 && k_cache.stride(1) % 8 == 0 && k_cache.stride(2) % 8 == 0 &&
+                  k_cache.strides() == v_cache.strides() && (reinterpret_cast<uintptr_t>(k_cache.data_ptr()) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(v_cache.data_ptr()) & 15) == 0,
+              "caches: 16-byte aligned token rows");
+  if (use_rope) TORCH_CHECK(rope.has_value() && rope->scalar_type() == at::kFloat && rope->is_contiguous(), "rope table");
+  p.n_q_heads = (int)n_q_heads;
+  p.n_kv_heads = (int)n_kv_heads;
+  p.head_dim = (int)head_dim;
+  p.use_rope = use_rope ? 1 : 0;
+  p.positions = positions.data_ptr<int>();
+  p.slots = slots.data_ptr<int64_t>();
+  p.rope = use_rope ? rope->data_ptr<float>() : nullptr;
+  p.q_out = bfp_mut(q_out);
+  p.ldq = (int)q_out.stride(0);
+  p.k_cache = bfp_mut(k_cache);
+  p.v_cache = bfp_mut(v_cache);
+  p.block_size = (int)k_cache.size(2);
+  p.cache_sb = k_cache.stride(0);
+  p.cache_sh = k_cache.stride(1);
+  p.cache_st = k_cache.stride(2);
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous(), "ws f32");
+  p.ws = ws.data_ptr<float>();
+  p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws.numel());
+  p.ws_cap = ws.numel();
+  set_tickets(p, tickets);
+  p.cus = device_cus(x);
+  check_rc(vwa_gemm(5, &p, cur_stream(x)), "gemm_qkv");
 }
 
 void row_rstd(Tensor x, Tensor rstd, double eps) {
@@ -784,10 +875,16 @@ DecodeAttnParams decode_params(const Tensor& q, const Tensor& k, const Tensor& v
 void decode_attention(Tensor q, Tensor k, Tensor v, Tensor table, int64_t block_size, int64_t sb, int64_t sh,
                       int64_t stok, Tensor ctx_lens, Tensor seq_ids, int64_t n_q_heads, int64_t n_kv_heads,
                       int64_t head_dim, double scale, int64_t n_splits, Tensor part_o, Tensor part_ml,
-                      Tensor counters, Tensor out) {
+                      Tensor counters, Tensor out, c10::optional<Tensor> shared) {
   c10::DeviceGuard g(q.device());
   DecodeAttnParams p = decode_params(q, k, v, table, block_size, sb, sh, stok, ctx_lens, seq_ids, n_q_heads,
                                      n_kv_heads, head_dim, scale, n_splits, part_o, part_ml, counters, out);
+  if (shared.has_value()) {
+    TORCH_CHECK(shared->is_cuda() && shared->scalar_type() == at::kInt && shared->numel() >= 2 &&
+                    shared->is_contiguous(),
+                "shared: int32 [P, n_real] on the device");
+    p.shared = shared->data_ptr<int>();
+  }
   check_rc(vwa_decode_attention(&p, cur_stream(q)), "decode_attention");
 }
 
@@ -1032,14 +1129,17 @@ void conv1d_gelu(Tensor x, Tensor w, c10::optional<Tensor> b, c10::optional<Tens
 
 }  // namespace
 
-void quant_fp8_rows(Tensor x, Tensor q, Tensor scale) {
+void quant_fp8_rows(Tensor x, Tensor q, Tensor scale, c10::optional<Tensor> rstd, double eps) {
   c10::DeviceGuard g(x.device());
   check_bf16(x, "x");
   check_contig_rows(x, "x");
   TORCH_CHECK(q.scalar_type() == at::kFloat8_e4m3fn && q.is_contiguous() && q.sizes() == x.sizes(), "q fp8 [rows, D]");
   TORCH_CHECK(scale.scalar_type() == at::kFloat && scale.numel() >= x.size(0), "scale f32 [rows]");
+  if (rstd.has_value())
+    TORCH_CHECK(rstd->scalar_type() == at::kFloat && rstd->numel() >= x.size(0), "rstd f32 [rows]");
   check_rc(vwa_quant_fp8_rows(bfp(x), (int)x.stride(0), (int)x.size(0), (int)x.size(1),
-                              reinterpret_cast<uint8_t*>(q.data_ptr()), scale.data_ptr<float>(), cur_stream(x)),
+                              reinterpret_cast<uint8_t*>(q.data_ptr()), scale.data_ptr<float>(),
+                              rstd.has_value() ? rstd->data_ptr<float>() : nullptr, (float)eps, cur_stream(x)),
            "quant_fp8_rows");
 }
 
@@ -1080,7 +1180,8 @@ int64_t ar_error(int64_t st) { return vwa_ar_error(reinterpret_cast<void*>(st));
 void ar_destroy(int64_t st) { vwa_ar_destroy(reinterpret_cast<void*>(st)); }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
-  m.def("quant_fp8_rows", &quant_fp8_rows);
+  m.def("quant_fp8_rows", &quant_fp8_rows, py::arg("x"), py::arg("q"), py::arg("scale"),
+        py::arg("rstd") = py::none(), py::arg("eps") = 1e-5);
   m.def("ar_create", &ar_create);
   m.def("ar_handles", &ar_handles);
   m.def("ar_open_peer", &ar_open_peer);
@@ -1123,11 +1224,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_advance", &decode_advance);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
         py::arg("rstd") = py::none(), py::arg("residual") = py::none(), py::arg("w_tiled") = false,
-        py::arg("ws") = py::none());
+        py::arg("ws") = py::none(), py::arg("tickets") = py::none());
   m.def("row_rstd", &row_rstd);
+  m.def("gemm_qkv", &gemm_qkv);
   m.def("gemm_fp8", &gemm_fp8, py::arg("x8"), py::arg("sx"), py::arg("w8"), py::arg("sw"), py::arg("bias"),
         py::arg("y"), py::arg("epi"), py::arg("rstd") = py::none(), py::arg("residual") = py::none(),
-        py::arg("ws") = py::none());
+        py::arg("ws") = py::none(), py::arg("tickets") = py::none());
   m.def("rmsnorm", &rmsnorm);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);

@@ -223,26 +223,40 @@ __global__ __launch_bounds__(256) void embedding_kernel(const int* __restrict__ 
 }
 
 // Per-row dynamic fp8 quantisation of activations for the large-M fp8 GEMM path (prefill):
-// amax over the row -> scale = amax/448 -> e4m3 bytes.  One workgroup per row.
+// amax over the row -> scale = amax/448 -> e4m3 bytes.  One workgroup per row.  With rstd: the
+// same pass also sums the squares (the RMSNorm 1/rms of a projection whose gamma is folded into
+// W) -- one launch instead of quant + row_rstd (profiles/r4_prof_fp8_c32_kernel_stats.md: the two
+// row kernels were 10.7 % of the 32-session fp8 GPU time, ~5 us each).
 __global__ __launch_bounds__(256) void quant_fp8_rows_kernel(const u16* __restrict__ x, int ldx, int D,
-                                                             uint8_t* __restrict__ q, float* __restrict__ scale) {
-  __shared__ float red[4];
+                                                             uint8_t* __restrict__ q, float* __restrict__ scale,
+                                                             float* __restrict__ rstd, float eps) {
+  __shared__ float red[4], red2[4];
   const int row = blockIdx.x;
   const u16* xr = x + (size_t)row * ldx;
-  float am = 0.f;
+  float am = 0.f, ss = 0.f;
   for (int c = threadIdx.x * 8; c < D; c += 256 * 8) {
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(xr + c), f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) am = fmaxf(am, fabsf(f[j]));
+    for (int j = 0; j < 8; ++j) {
+      am = fmaxf(am, fabsf(f[j]));
+      ss += f[j] * f[j];
+    }
   }
   am = wave_max(am);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+  if (rstd) ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) {
+    red[threadIdx.x >> 6] = am;
+    red2[threadIdx.x >> 6] = ss;
+  }
   __syncthreads();
   am = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   const float sx = am > 0.f ? am * (1.f / 448.f) : 1.f;
   const float iv = 1.f / sx;
-  if (threadIdx.x == 0) scale[row] = sx;
+  if (threadIdx.x == 0) {
+    scale[row] = sx;
+    if (rstd) rstd[row] = rsqrtf((red2[0] + red2[1] + red2[2] + red2[3]) / (float)D + eps);
+  }
   for (int c = threadIdx.x * 8; c < D; c += 256 * 8) {
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(xr + c), f);
@@ -258,9 +272,9 @@ inline int nblk(int64_t n, int b) { return (int)((n + b - 1) / b); }
 }  // namespace
 
 extern "C" int vwa_quant_fp8_rows(const uint16_t* x, int ldx, int rows, int D, uint8_t* q, float* scale,
-                                  hipStream_t st) {
+                                  float* rstd, float eps, hipStream_t st) {
   if (D % 8) return -1;
-  hipLaunchKernelGGL(quant_fp8_rows_kernel, dim3(rows), dim3(256), 0, st, x, ldx, D, q, scale);
+  hipLaunchKernelGGL(quant_fp8_rows_kernel, dim3(rows), dim3(256), 0, st, x, ldx, D, q, scale, rstd, eps);
   return (int)hipGetLastError();
 }
 

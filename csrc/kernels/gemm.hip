@@ -42,7 +42,7 @@ using namespace vwa;
 
 namespace {
 
-enum Epi { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_GELU = 3, EPI_GELU_RESID = 4 };
+enum Epi { EPI_STORE = 0, EPI_RESID = 1, EPI_SWIGLU = 2, EPI_GELU = 3, EPI_GELU_RESID = 4, EPI_QKV = 5 };
 template <int EPI> constexpr bool kResid = EPI == EPI_RESID || EPI == EPI_GELU_RESID;
 template <int EPI> constexpr bool kGelu = EPI == EPI_GELU || EPI == EPI_GELU_RESID;
 
@@ -250,6 +250,139 @@ VWA_DEVICE void store_out(const GemmParams& p, int m, int n, float v) {
     reinterpret_cast<u16*>(p.Y)[(size_t)m * p.ldy + n] = f2bf(v);
 }
 
+// EPI_QKV: output chunk n .. n+7 (o) of row m and its rotation partner n^8 (q) -> rotary (q / k
+// heads) -> q_out or the paged K / V caches, 16-byte stores.  Within a head (permuted rows) the
+// chunk at column 16 t + 8 hi holds dims hi * hd/2 + 8 t .. + 8, its partner the other half.
+VWA_DEVICE void qkv_store(const GemmParams& p, int m, int n, const float (&o)[8], const float (&q)[8]) {
+  const int hd = p.head_dim, half = hd >> 1;
+  const int head = n / hd, wc = n % hd;
+  const int t = wc >> 4;
+  const bool hi = (wc & 8) != 0;
+  const bool is_v = head >= p.n_q_heads + p.n_kv_heads;
+  float y[8];
+  if (p.use_rope && !is_v) {
+    const float4* cs = reinterpret_cast<const float4*>(p.rope + ((size_t)p.positions[m] * half + 8 * t) * 2);
+#pragma unroll
+    for (int e2 = 0; e2 < 4; ++e2) {
+      const float4 v = cs[e2];  // (cos, sin) of dims 2 e2, 2 e2 + 1
+      const int e = 2 * e2;
+      y[e] = hi ? o[e] * v.x + q[e] * v.y : o[e] * v.x - q[e] * v.y;
+      y[e + 1] = hi ? o[e + 1] * v.z + q[e + 1] * v.w : o[e + 1] * v.z - q[e + 1] * v.w;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) y[e] = o[e];
+  }
+  const int d = (hi ? half : 0) + 8 * t;
+  if (head < p.n_q_heads) {
+    *reinterpret_cast<uint4*>(p.q_out + (size_t)m * p.ldq + head * hd + d) = pack8(y);
+    return;
+  }
+  const int64_t slot = p.slots[m];
+  if (slot < 0) return;
+  const int kvh = is_v ? head - p.n_q_heads - p.n_kv_heads : head - p.n_q_heads;
+  const int64_t idx = (slot / p.block_size) * p.cache_sb + kvh * p.cache_sh + (slot % p.block_size) * p.cache_st;
+  *reinterpret_cast<uint4*>((is_v ? p.v_cache : p.k_cache) + idx + d) = pack8(y);
+}
+
+// f32 partial slabs of the one-launch split-K: write-through (sc1) stores / L2-missing (sc1) loads
+// -- the slices of a tile may run on different XCDs, whose L2s are not coherent with each other
+VWA_DEVICE void st_wt_f32(__amdgpu_buffer_rsrc_t r, size_t idx, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)(idx * 4), 0, 16);
+}
+// AUX 16: sc1 (the one-launch split-K's cross-XCD hand-off); 0: plain (the reduce kernel, after
+// the GEMM launch's end made the slabs visible)
+template <int AUX>
+VWA_DEVICE float4 ld_f4(__amdgpu_buffer_rsrc_t r, size_t idx) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, AUX));
+}
+
+VWA_DEVICE void add8(float (&v)[8], const float4& a, const float4& b) {
+  v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+}
+
+// One output item of a split-K GEMM: row m, output columns c .. c+7 -- the sum of every slice's
+// f32 partial (slice order: the result does not depend on which slice finished last) and the
+// epilogue (SwiGLU: features c .. c+7 from the interleaved gate / up columns; QKV: also the
+// rotation partner chunk c^8, then rotary + q / KV stores), 16-byte stores.  Slices are loaded
+// in batches of 4 (all of a batch's loads in flight before any is used).
+template <int EPI, int AUX>
+VWA_DEVICE void reduce_item(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int m, int c) {
+  constexpr bool SW = EPI == EPI_SWIGLU, QK = EPI == EPI_QKV;
+  const size_t slab = (size_t)p.M * p.N;
+  const float rs = (p.rstd ? p.rstd[m] : 1.f) * (p.sx ? p.sx[m] : 1.f);
+  // the two 8-column source chunks: SwiGLU gate n0 / up n0 + 16; QKV own c / partner c ^ 8
+  const int n0 = SW ? (c >> 4) * 32 + (c & 15) : c;
+  const int n1 = SW ? n0 + 16 : (c ^ 8);
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int z0 = 0; z0 < p.splits; z0 += 4) {
+    float4 x[4][2], y[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      // slices past the last read past the slab range: the buffer returns zeros
+      const size_t base = (size_t)(z0 + u) * slab + (size_t)m * p.N;
+      x[u][0] = ld_f4<AUX>(rws, base + n0);
+      x[u][1] = ld_f4<AUX>(rws, base + n0 + 4);
+      if constexpr (SW || QK) {
+        y[u][0] = ld_f4<AUX>(rws, base + n1);
+        y[u][1] = ld_f4<AUX>(rws, base + n1 + 4);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      add8(a, x[u][0], x[u][1]);
+      if constexpr (SW || QK) add8(b, y[u][0], y[u][1]);
+    }
+  }
+  float v[8];
+  if constexpr (SW) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gs = p.sw ? p.sw[n0 + e] : 1.f, us = p.sw ? p.sw[n1 + e] : 1.f;
+      v[e] = silu(a[e] * gs * rs) * (b[e] * us * rs);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = a[e] * rs * (p.sw ? p.sw[c + e] : 1.f) + bias_at(p, c + e);
+      if constexpr (kGelu<EPI>) v[e] = gelu_erf(v[e]);
+    }
+    if constexpr (QK) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) b[e] = b[e] * rs * (p.sw ? p.sw[n1 + e] : 1.f) + bias_at(p, n1 + e);
+      qkv_store(p, m, c, v, b);
+      return;
+    }
+  }
+  if (p.y_f32) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) store_out<EPI>(p, m, c + e, v[e]);
+    return;
+  }
+  if constexpr (kResid<EPI>) {
+    float r[8];
+    unpack8(*reinterpret_cast<const uint4*>(p.R + (size_t)m * p.ldr + c), r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += r[e];
+  }
+  *reinterpret_cast<uint4*>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + c) = pack8(v);
+}
+
+// The last-arriving slice of output tile (bm, bn) (one-launch split-K): every item of the tile's
+// valid rows
+template <int EPI>
+VWA_DEVICE void split_reduce_tile(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int bm, int bn, int BM, int BN,
+                                  int nthreads) {
+  constexpr bool SW = EPI == EPI_SWIGLU;
+  const int cpr = (SW ? BN / 2 : BN) / 8;  // 8-wide output chunks per tile row
+  const int rows = min(BM, p.M - bm);
+  const int ncols = SW ? p.N / 2 : p.N;
+  for (int it = threadIdx.x; it < rows * cpr; it += nthreads) {
+    const int c = (SW ? bn / 2 : bn) + (it % cpr) * 8;
+    if (c < ncols) reduce_item<EPI, 16>(p, rws, bm + it / cpr, c);
+  }
+}
+
 template <class C, int EPI, bool WT, bool F8 = false, bool P8 = false>
 __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -373,6 +506,39 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
   const int l = lane_id();
   const int col0 = bn + wn * FN * 16 + (l & 15);
   const int row0 = bm + wm * FM * 16 + 4 * (l >> 4);
+  if (p.splits > 1 && p.tickets != nullptr) {
+    // one-launch split-K: partial slab written through to memory, then one arrival count per
+    // tile; the last slice (any XCD) reads the slabs back past its L2 and runs the epilogue
+    const __amdgpu_buffer_rsrc_t rws = rsrc(p.ws, (size_t)p.splits * p.M * p.N * 4);
+    const size_t zb = (size_t)split * p.M * p.N;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = row0 + i * 16 + r;
+        if (m >= p.M) continue;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int n = col0 + j * 16;
+          if (n < p.N) st_wt_f32(rws, zb + (size_t)m * p.N + n, acc[i][j][r]);
+        }
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partials reached memory
+    __syncthreads();
+    int* s_last = reinterpret_cast<int*>(lds);  // the stage images are dead (the k loop's last barrier)
+    if (threadIdx.x == 0) {
+      int* t = p.tickets + lt;
+      const int ticket = __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = ticket == p.splits - 1;
+      if (last) __hip_atomic_store(t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *s_last = last;
+    }
+    __syncthreads();
+    if (!*s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // only orders the slab loads after the ticket
+    split_reduce_tile<EPI>(p, rws, bm, bn, C::BM, C::BN, C::THREADS);
+    return;
+  }
   if (p.splits > 1) {  // f32 partial slab of this slice; gemm_reduce_kernel applies the epilogue
     float* ws = p.ws + (size_t)split * p.M * p.N;
 #pragma unroll
@@ -474,6 +640,13 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
     const int m = bm + wm * ROWS + row, n = cbase + ch * 8;
     if (m >= p.M || n >= ncols) continue;
     uint4 v = *reinterpret_cast<const uint4*>(wl + row * RS + ch * 16);
+    if constexpr (EPI == EPI_QKV) {  // (bf16-rounded like the stored projection it replaces)
+      float o[8], q[8];
+      unpack8(v, o);
+      unpack8(*reinterpret_cast<const uint4*>(wl + row * RS + (ch ^ 1) * 16), q);
+      qkv_store(p, m, n, o, q);
+      continue;
+    }
     if constexpr (kResid<EPI>) {
       float a[8], b[8];
       unpack8(v, a);
@@ -486,34 +659,14 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
   }
 }
 
-// sum of the split-K slabs + epilogue; one thread per output element (SwiGLU: per feature)
+// sum of the split-K slabs + epilogue (two-launch split-K): one thread per (row, 8 output columns)
 template <int EPI>
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmParams p) {
+  const int cpr = (EPI == EPI_SWIGLU ? p.N / 2 : p.N) / 8;
   const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
-  if (id >= (int64_t)p.M * ncols) return;
-  const int m = (int)(id / ncols), c = (int)(id % ncols);
-  const size_t slab = (size_t)p.M * p.N;
-  const float rs = (p.rstd ? p.rstd[m] : 1.f) * (p.sx ? p.sx[m] : 1.f);
-  if constexpr (EPI == EPI_SWIGLU) {
-    const int n = (c >> 4) * 32 + (c & 15);
-    float gt = 0.f, up = 0.f;
-    for (int z = 0; z < p.splits; ++z) {
-      gt += p.ws[z * slab + (size_t)m * p.N + n];
-      up += p.ws[z * slab + (size_t)m * p.N + n + 16];
-    }
-    if (p.sw) {
-      gt *= p.sw[n];
-      up *= p.sw[n + 16];
-    }
-    reinterpret_cast<u16*>(p.Y)[(size_t)m * p.ldy + c] = f2bf(silu(gt * rs) * (up * rs));
-  } else {
-    float v = 0.f;
-    for (int z = 0; z < p.splits; ++z) v += p.ws[z * slab + (size_t)m * p.N + c];
-    v = v * rs * (p.sw ? p.sw[c] : 1.f) + bias_at(p, c);
-    if constexpr (kGelu<EPI>) v = gelu_erf(v);
-    store_out<EPI>(p, m, c, v);
-  }
+  if (id >= (int64_t)p.M * cpr) return;
+  const __amdgpu_buffer_rsrc_t rws = rsrc(p.ws, (size_t)p.splits * p.M * p.N * 4);
+  reduce_item<EPI, 0>(p, rws, (int)(id / cpr), (int)(id % cpr) * 8);
 }
 
 // per-row 1/rms of X (the RMSNorm of a projection whose gamma is folded into W)
@@ -562,8 +715,8 @@ int launch_epi(const GemmParams& p, hipStream_t st, bool p8) {
   } else {
     launch_cfg<CfgS, EPI>(p, st);
   }
-  if (p.splits > 1) {
-    const int64_t n = (int64_t)p.M * (EPI == EPI_SWIGLU ? p.N / 2 : p.N);
+  if (p.splits > 1 && p.tickets == nullptr) {
+    const int64_t n = (int64_t)p.M * (EPI == EPI_SWIGLU ? p.N / 2 : p.N) / 8;
     hipLaunchKernelGGL((gemm_reduce_kernel<EPI>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
   }
   return (int)hipGetLastError();
@@ -590,6 +743,9 @@ extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
     return -11;
   if (p.sw && (!p.sx || !p.w_tiled)) return -14;  // W8A8: per-row X scales and the fp8 tiled layout
   if (epi == EPI_SWIGLU && (p.N % 32 || p.y_f32)) return -12;
+  if (epi == EPI_QKV && (p.y_f32 || p.head_dim % 16 || p.N != (p.n_q_heads + 2 * p.n_kv_heads) * p.head_dim ||
+                         !p.q_out || !p.k_cache || !p.v_cache || !p.slots || (p.use_rope && (!p.rope || !p.positions))))
+    return -16;
   if (p.splits < 1) p.splits = 1;
   // 8-phase 256^2 kernel (mode 2, measured rule, tools/bench_gemm.py): the prompt-sized shapes
   // whose 256^2 tiles alone fill the CUs (>= 256 tiles, e.g. the 1011-row gate/up), or fill them
@@ -611,6 +767,9 @@ extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
   p.kg_per_split = (KG + p.splits - 1) / p.splits;
   p.splits = (KG + p.kg_per_split - 1) / p.kg_per_split;  // no empty slice
   if (p.splits > 1 && !p.ws) return -13;
+  // one-launch split-K: the 128^2 kernel, a counter per output tile
+  if (p8 || p.splits == 1 || (int64_t)((p.M + CfgS::BM - 1) / CfgS::BM) * ((p.N + CfgS::BN - 1) / CfgS::BN) > p.n_tickets)
+    p.tickets = nullptr;
   if (p.nbatch > 1 && p.splits > 1) return -15;  // batched launches take no split-K
   switch (epi) {
     case EPI_STORE: return launch_epi<EPI_STORE>(p, st, p8);
@@ -618,6 +777,7 @@ extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
     case EPI_SWIGLU: return launch_epi<EPI_SWIGLU>(p, st, p8);
     case EPI_GELU: return launch_epi<EPI_GELU>(p, st, p8);
     case EPI_GELU_RESID: return launch_epi<EPI_GELU_RESID>(p, st, p8);
+    case EPI_QKV: return launch_epi<EPI_QKV>(p, st, p8);
     default: return -3;
   }
 }

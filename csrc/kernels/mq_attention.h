@@ -189,6 +189,11 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
         __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.ctx_lens), (short)0, p.rows * 4, 0x00020000);
     s_meta[512 + lane] = (int)__builtin_amdgcn_raw_buffer_load_b32(r_sid, lane * 4, 0, 0);
     s_meta[576 + lane] = (int)__builtin_amdgcn_raw_buffer_load_b32(r_ctx, lane * 4, 0, 0);
+    if constexpr (!FINE) {
+      const __amdgpu_buffer_rsrc_t r_sh =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.shared), (short)0, p.shared ? 8 : 0, 0x00020000);
+      if (lane < 2) s_meta[640 + lane] = (int)__builtin_amdgcn_raw_buffer_load_b32(r_sh, lane * 4, 0, 0);
+    }
   }
   __syncthreads();
   stamp(12);  // (diagnostic: step metadata in LDS)
@@ -199,7 +204,20 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   const int cl = lane < p.rows ? s_meta[576 + lane] : 0;
   stamp(16);
   const int sp = __shfl(sl, lane > 0 ? lane - 1 : 0, 64);
-  const unsigned long long run_starts = __ballot(lane < p.rows && (lane == 0 || sl != sp));
+  const unsigned long long seq_starts = __ballot(lane < p.rows && (lane == 0 || sl != sp));
+  // shared cached prefix (p.shared): rows 0 .. n_real-1 are grouped RG at a time regardless of
+  // sequence (their first P keys are the same blocks), the padded rows behind them by sequence
+  int P = 0, n_real = p.rows;
+  if constexpr (!FINE) {
+    P = s_meta[640];
+    n_real = min(p.rows, s_meta[641]);
+  }
+  const bool cascade = !FINE && P > 0 && n_real > 0 && p.n_splits > RG;
+  unsigned long long run_starts = seq_starts;
+  if (cascade) {
+    const unsigned long long real = n_real >= 64 ? ~0ull : ((1ull << n_real) - 1ull);
+    run_starts = 1ull | (n_real < p.rows ? (1ull << n_real) : 0ull) | (seq_starts & ~real);
+  }
   const int run0 = 63 - __builtin_clzll(run_starts & ((2ull << lane) - 1ull));  // lane 0 always starts a run
   const unsigned long long leaders = __ballot(lane < p.rows && (lane - run0) % RG == 0);
   const int n_groups = __builtin_popcountll(leaders);
@@ -207,7 +225,10 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   // chunks per (group, kv head): spread the work over the grid (one item per workgroup when it
   // fits), never more than the partial buffers hold
   static_assert(!FINE || NW == 8, "the FINE merge pairs two threads per (column, slice): 512 threads");
-  const int n_eff = max(1, min(FINE ? min(p.n_splits, 16) : p.n_splits, grid / max(1, n_groups * nkv)));
+  // cascade: n_pc prefix chunks + up to RG own-key chunks (one per sequence run of the group) per
+  // group -- the partial slots 0 .. n_pc + RG - 1
+  const int n_pc = cascade ? max(1, min(p.n_splits - RG, grid / max(1, n_groups * nkv) - RG)) : 0;
+  const int n_eff = cascade ? n_pc + RG : max(1, min(FINE ? min(p.n_splits, 16) : p.n_splits, grid / max(1, n_groups * nkv)));
   const int n_items = n_groups * nkv * n_eff;
   if (n_items_out) *n_items_out = n_items;
   if (n_final_out) *n_final_out = n_groups * nkv;
@@ -245,19 +266,62 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   for (int o = 1; o < 64; o <<= 1) ctxmax = max(ctxmax, __shfl_xor(ctxmax, o, 64));
   if (item == bid) stamp(19);
   const int rho = n / G;                     // group row of this lane's query column
-  const int ctx_n = __shfl(c_own, rho, 64);  // its context (0 for padded columns)
+  int ctx_n = __shfl(c_own, rho, 64);        // its context (0 for padded columns)
 
-  // ---- this item's chunk of the group's keys (NW waves x CL/NW keys)
-  const int CL = ((ctxmax + n_eff - 1) / n_eff + kChunk - 1) / kChunk * kChunk;
-  const int kbeg = chunk * CL;
-  if (kbeg >= ctxmax) continue;
-  const int nact = (ctxmax + CL - 1) / CL;
+  // ---- this item's chunk of the group's keys (NW waves x CL/NW keys): [kbeg, kend), partial slot
+  int CL, kbeg, kend, nact, slot = chunk, kv_seq = seq;
+  if (cascade && r0 < n_real) {
+    // prefix chunks (slots 0 .. npa-1) over [0, P) for every row of the group; then one chunk per
+    // sequence run j of the group with keys past P: [P, max ctx of the run), the other runs'
+    // columns masked (slot npa + its rank among such runs)
+    const unsigned long long gm = (nr >= 64 ? ~0ull : ((1ull << nr) - 1ull)) << r0;
+    const unsigned long long subs = (seq_starts & gm) | (1ull << r0);
+    const int run_of = __builtin_popcountll(subs & ((2ull << min(r0 + lane, 63)) - 1ull)) - 1;  // lane < nr
+    const int nruns = __builtin_popcountll(subs);
+    int own_mask = 0, my_max = 0;  // runs with own keys; this item's run's max context
+    const int j = chunk - n_pc;
+    for (int rr = 0; rr < nruns; ++rr) {
+      int cm = (lane < nr && run_of == rr) ? c_src : 0;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) cm = max(cm, __shfl_xor(cm, o, 64));
+      if (cm > P) own_mask |= 1 << rr;
+      if (rr == j) my_max = cm;
+    }
+    CL = ((P + n_pc - 1) / n_pc + kChunk - 1) / kChunk * kChunk;
+    const int npa = (P + CL - 1) / CL;
+    nact = npa + __builtin_popcount(own_mask);
+    if (chunk < n_pc) {
+      kbeg = chunk * CL;
+      if (kbeg >= P) continue;
+      kend = min(P, kbeg + CL);
+    } else {
+      if (j >= nruns || !((own_mask >> j) & 1)) continue;
+      unsigned long long sb = subs;
+      for (int t = 0; t < j; ++t) sb &= sb - 1ull;  // drop the first j run starts
+      const int a = __builtin_ctzll(sb);
+      sb &= sb - 1ull;
+      const int b = sb ? __builtin_ctzll(sb) : r0 + nr;
+      kbeg = P;
+      kend = my_max;
+      CL = (kend - kbeg + kChunk - 1) / kChunk * kChunk;
+      slot = npa + __builtin_popcount(own_mask & ((1 << j) - 1));
+      kv_seq = __shfl(sl, a, 64);
+      if (rho < a - r0 || rho >= b - r0) ctx_n = 0;  // other runs' columns: no keys in this chunk
+    }
+  } else {
+    CL = ((ctxmax + n_eff - 1) / n_eff + kChunk - 1) / kChunk * kChunk;
+    if (cascade) CL = (ctxmax + kChunk - 1) / kChunk * kChunk;  // padded rows: one chunk
+    kbeg = chunk * CL;
+    if (kbeg >= ctxmax) continue;
+    kend = min(ctxmax, kbeg + CL);
+    nact = (ctxmax + CL - 1) / CL;
+  }
   // non-FINE: wave w takes the contiguous CL / NW keys from wb; FINE: the chunk's 32-key steps
   // round-robin over the waves (step s of the chunk -> wave s % NW)
   const int wb = FINE ? kbeg : kbeg + w * (CL / kWv);
-  const int we = FINE ? min(ctxmax, kbeg + CL) : min(ctxmax, wb + CL / kWv);
+  const int we = FINE ? kend : min(kend, wb + CL / kWv);
   const int nsteps = we > wb ? (we - wb + kMqStep - 1) / kMqStep : 0;
-  const int kmax = ctxmax - 1;  // keys past the context are clamped (finite data, masked scores)
+  const int kmax = kend - 1;  // keys past the chunk are clamped (finite data, masked scores)
   if (item == bid) stamp(20);
 
   // ---- Q^T fragments (B operand): Q[column n][dims 32ks + 8g ..], pre-scaled by scale*log2(e)
@@ -308,7 +372,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
       const int st = (int)p.kv.stride_tok;
       offsets([&](int key) -> int64_t { return ((key & 16) ? bB : bA) + hoff + (key & 15) * st; });
     } else {
-      offsets([&](int key) -> int64_t { return kv_offset(p.kv, seq, kvh, key); });
+      offsets([&](int key) -> int64_t { return kv_offset(p.kv, kv_seq, kvh, key); });
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -443,7 +507,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
       for (int j = 0; j < 8; ++j) acc[j] *= inv;
       store_out<SC1OUT>(p.out + (int64_t)crow * p.ldo + ch * D + 8 * dc, pack8(acc));
     } else {
-      const int64_t base = ((int64_t)crow * p.n_splits + chunk) * nq + ch;
+      const int64_t base = ((int64_t)crow * p.n_splits + slot) * nq + ch;
       st_sc1_f4(r_o, base * D + 8 * dc, acc);
       st_sc1_f4(r_o, base * D + 8 * dc + 4, acc + 4);
       if (dc == 0) st_sc1_f2(r_ml, base * 2, M, L);

@@ -64,6 +64,11 @@ struct DecodeAttnParams {
   // optional (chained attention, <= 4 rows): the block table of each ROW's sequence, [rows][rt_stride
   // <= 128] -- read in the same round trip as seq_ids / ctx_lens (no dependent table load)
   const int* row_table; int rt_stride;
+  // optional (multi-query kernel, non-chained): [P, n_real] on the device -- the first P keys (a
+  // multiple of 32) of rows 0 .. n_real-1 are the SAME physical K/V (the prefix-cached prompt every
+  // session shares), so those rows are grouped RG at a time across sequences for keys < P (one
+  // K/V read per group instead of per sequence) and by sequence for their own keys >= P.
+  const int* shared;
 };
 
 // Chained decode GEMM phases in one persistent launch (skinny_stream.hip, vwa_chain): each phase
@@ -146,6 +151,18 @@ struct GemmParams {
   // rows t*stride-1 .. t*stride+1 of a zero-padded channels-last buffer)
   int nbatch; int64_t bsx, bsy, bsr;
   int cus; int64_t ws_cap;  // CU count and workspace floats (split-K choice of the 256^2 kernel)
+  // split-K in one launch (128^2 kernel): per-tile arrival counters (zeroed once, reset by the last
+  // arriver) -- the slices publish their f32 partials write-through and the LAST slice of a tile
+  // sums them and runs the epilogue (no gemm_reduce launch).  null: the two-launch form.
+  int* tickets; int n_tickets;
+  // epilogue 5 (QKV): rotary embedding + paged-KV write of a QKV projection with permuted head rows
+  // (ops.permute_qkv_rows: each 16-column tile holds the rotation pairs (c, c + 8)) -- q heads go
+  // to q_out in natural dim order, k / v heads to the caches at slots[m] (< 0: not written);
+  // Y is not written.  No separate rope_kv_write launch.
+  int n_q_heads, n_kv_heads, head_dim, use_rope;
+  const int* positions; const int64_t* slots; const float* rope;
+  uint16_t* q_out; int ldq; uint16_t* k_cache; uint16_t* v_cache; int block_size;
+  int64_t cache_sb, cache_sh, cache_st;
 };
 
 struct FlashAttnParams {
@@ -208,7 +225,8 @@ int vwa_log_mel(const float* audio, int n_samples, int n_frames, const float* wi
 int vwa_attention_split_tokens();
 int vwa_decode_advance(int* tokens, int* positions, int* ctx_lens, int64_t* slots, const int* sampled,
                        int* out, int* counter, int max_out, int base_block, int block_size, hipStream_t st);
-int vwa_quant_fp8_rows(const uint16_t* x, int ldx, int rows, int D, uint8_t* q, float* scale, hipStream_t st);
+int vwa_quant_fp8_rows(const uint16_t* x, int ldx, int rows, int D, uint8_t* q, float* scale, float* rstd, float eps,
+                       hipStream_t st);
 // one-shot peer-to-peer all-reduce (allreduce.hip)
 void* vwa_ar_create(int rank, int world, int64_t max_elems);
 int vwa_ar_handles(void* st, void* out);

@@ -849,3 +849,160 @@ def test_streaming_kernel_many_rows(M, monkeypatch):
                        rope=rope.cpu(), positions=pos.cpu(), slots=slots.cpu(), q_out=q2, k_cache=kc2, v_cache=vc2)
     for a_, b_ in ((q, q2), (kc, kc2), (vc, vc2)):
         close(a_, b_, 3e-2)
+
+
+@pytest.mark.parametrize("M", [17, 32, 64])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_gemm_one_launch_split_k(M, fp8, monkeypatch):
+    """Many-row decode shapes (Llama-3-8B widths, split-K because 17..64 rows give too few output
+    tiles): the one-launch split-K (each tile's last slice reduces the write-through slabs and
+    runs the epilogue) is bit-identical to GEMM + gemm_reduce and matches the f32 reference, for
+    the residual / SwiGLU / store epilogues; the tile counters stay zero between launches."""
+    K = 4096
+    x = rnd(M, K)
+    res0 = rnd(M, 4096)
+    w_o = rnd(4096, K, scale=K ** -0.5)
+    gu = ops.interleave_gate_up(rnd(1024, K, scale=K ** -0.5), rnd(1024, K, scale=K ** -0.5))
+    w_q = rnd(1536, K, scale=K ** -0.5)
+    if fp8:
+        W = [ops.FP8Weight.quantize(w, tiled=True) for w in (w_o, gu, w_q)]
+        C = [ops.FP8Weight(w.rows().cpu(), w.scale.cpu()) for w in W]
+    else:
+        W = [ops.TiledWeight(w) for w in (w_o, gu, w_q)]
+        C = [w.cpu() for w in (w_o, gu, w_q)]
+
+    def run():
+        res = res0.clone()
+        ops.linear(x, W[0], out=res, residual=res, fuse_rms=True)
+        sw = ops.linear_swiglu(x, W[1], fuse_rms=True)
+        q = torch.empty(M, 1536, dtype=BF, device=DEV)
+        ops.linear(x, W[2], out=q, fuse_rms=True)
+        torch.cuda.synchronize()
+        return res, sw, q
+
+    monkeypatch.setattr(ops, "GEMM_ONE_LAUNCH", True)
+    one = run()
+    one2 = run()  # counters were reset by the last arrivers: a second launch is identical
+    assert int(ops.gemm_tickets(DEV).abs().sum()) == 0
+    monkeypatch.setattr(ops, "GEMM_ONE_LAUNCH", False)
+    two = run()
+    for a, b, c in zip(one, one2, two):
+        assert torch.equal(a, b) and torch.equal(a, c)
+    xc = x.cpu()
+    exp = ops.linear(xc, C[0], residual=res0.cpu(), fuse_rms=True)
+    close(one[0], exp, 3e-2, 3e-2)
+    close(one[1], ops.linear_swiglu(xc, C[1], fuse_rms=True), 3e-2, 3e-2)
+    close(one[2], ops.linear(xc, C[2], fuse_rms=True), 3e-2, 3e-2)
+
+
+def test_quant_fp8_rows_with_rstd():
+    """The fp8 row quantiser's optional RMSNorm output (one row pass for the W8A8 GEMM's two row
+    statistics) equals row_rstd, and the codes / scales are unchanged by it."""
+    E = ops.ext()
+    for M, K in ((33, 4096), (64, 14336)):
+        x = rnd(M, K)
+        q1 = torch.empty(M, K, dtype=torch.float8_e4m3fn, device=DEV)
+        q2 = torch.empty_like(q1)
+        s1 = torch.empty(M, device=DEV)
+        s2 = torch.empty(M, device=DEV)
+        r1 = torch.empty(M, device=DEV)
+        r2 = torch.empty(M, device=DEV)
+        E.quant_fp8_rows(x, q1, s1)
+        E.quant_fp8_rows(x, q2, s2, r2, 1e-5)
+        E.row_rstd(x, r1, 1e-5)
+        assert torch.equal(q1.view(torch.uint8), q2.view(torch.uint8)) and torch.equal(s1, s2)
+        exp = torch.rsqrt(x.float().pow(2).mean(-1) + 1e-5)
+        torch.testing.assert_close(r2, exp, rtol=1e-4, atol=0)
+        torch.testing.assert_close(r2, r1, rtol=1e-5, atol=0)
+
+
+@pytest.mark.parametrize("M", [17, 48, 300])
+@pytest.mark.parametrize("kind", ["bf16", "fp8", "rowmajor"])
+def test_gemm_qkv_epilogue_fused(M, kind, monkeypatch):
+    """The QKV projection with the rotary + paged-KV write in the tiled GEMM's epilogue (EPI_QKV:
+    one-launch split-K at few rows, the plain / 256^2 epilogue at 300) == GEMM + rope_kv_write and
+    the f32 reference, Llama-3-8B head geometry; a negative slot writes no cache row."""
+    K, nq, nkv, hd = 4096, 32, 8, 128
+    w = ops.permute_qkv_rows(rnd((nq + 2 * nkv) * hd, K, scale=K ** -0.5), nq + 2 * nkv, hd)
+    ww = {"bf16": lambda: ops.TiledWeight(w), "fp8": lambda: ops.FP8Weight.quantize(w, tiled=True),
+          "rowmajor": lambda: w}[kind]()
+    x = rnd(M, K)
+    rope = ops.rope_table(2048, hd, 5e5, device=DEV)
+    pos = torch.arange(100, 100 + M, dtype=torch.int32, device=DEV)
+    slots = torch.randperm(40 * 16, device=DEV)[:M].to(torch.int64)
+    slots[M // 2] = -1
+
+    def run(fused):
+        monkeypatch.setattr(ops, "GEMM_QKV_FUSED", fused)
+        kc = torch.zeros(40, nkv, 16, hd, dtype=BF, device=DEV)
+        vc = torch.zeros_like(kc)
+        q = torch.zeros(M, nq * hd, dtype=BF, device=DEV)
+        ops.qkv_rope_write(x, ww, None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd, rope=rope,
+                           positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc)
+        torch.cuda.synchronize()
+        return q, kc, vc
+
+    fused, plain = run(True), run(False)
+    for a, b in zip(fused, plain):
+        close(a, b, 3e-2, 3e-2)
+    if kind != "fp8":
+        kc = torch.zeros(40, nkv, 16, hd, dtype=BF)
+        vc = torch.zeros_like(kc)
+        q = torch.zeros(M, nq * hd, dtype=BF)
+        ops.qkv_rope_write(x.cpu(), w.cpu(), None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
+                           rope=rope.cpu(), positions=pos.cpu(), slots=slots.cpu(), q_out=q, k_cache=kc, v_cache=vc)
+        for a, b in zip(fused, (q, kc, vc)):
+            close(a, b, 3e-2, 3e-2)
+
+
+@pytest.mark.parametrize("hd,nq,nkv", [(128, 32, 8), (128, 8, 1), (64, 8, 4)])
+@pytest.mark.parametrize("n_sess,P", [(3, 128), (8, 1024), (32, 1024), (61, 512)])
+def test_decode_attention_shared_prefix(hd, nq, nkv, n_sess, P):
+    """Sessions over one prefix-cached prompt (the same physical blocks for the first P keys): the
+    multi-query kernel's shared-prefix grouping ([P, n_real] words) == the reference and == the
+    per-session grouping; runs of jump-forward rows, a session whose own keys end exactly at P,
+    padded rows behind the real ones (seq 0, one key), counters left zero."""
+    bs, per = 16, 100
+    blocks = 8 + n_sess * per
+    kc = rnd(blocks, nkv, bs, hd)
+    vc = rnd(blocks, nkv, bs, hd)
+    table = (torch.randperm(blocks - 8, device=DEV)[: n_sess * per] + 8).to(torch.int32).view(n_sess, per).contiguous()
+    table[:, : P // bs] = table[0, : P // bs]
+    seqs, ctx = [], []
+    g = torch.Generator().manual_seed(n_sess)
+    for s in range(n_sess):
+        if s == 1:
+            own = [0]  # own keys end exactly at P
+        else:
+            own = [int(torch.randint(1, 300, (1,), generator=g))]
+        if s % 5 == 2:  # a jump-forward run of consecutive positions
+            own = [own[0] + i for i in range(int(torch.randint(2, 6, (1,), generator=g)))]
+        for o in own:
+            if len(seqs) < 64:
+                seqs.append(s)
+                ctx.append(P + o if o else P)
+    n_real = len(seqs)
+    pad = min(64, n_real + 3) - n_real
+    seqs += [0] * pad
+    ctx += [1] * pad
+    rows = len(seqs)
+    seq_ids = torch.tensor(seqs, dtype=torch.int32, device=DEV)
+    ctx_lens = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    q = rnd(rows, nq * hd)
+    kv = ops.KVLayout.paged(kc, vc, table)
+    cnt = torch.zeros(rows * nkv, dtype=torch.int32, device=DEV)
+    shared = torch.tensor([P, n_real], dtype=torch.int32, device=DEV)
+    outs = []
+    for sh in (shared, None, shared):
+        out = torch.empty_like(q)
+        ops.decode_attention(q, kv, ctx_lens, seq_ids, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd, scale=hd ** -0.5,
+                             max_ctx=per * bs, out=out, counters=cnt, shared=sh)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert int(cnt.abs().sum()) == 0
+    exp = ref.decode_attention(q.cpu(), ops.KVLayout.paged(kc.cpu(), vc.cpu(), table.cpu()), ctx_lens.cpu(),
+                               seq_ids.cpu(), n_q_heads=nq, n_kv_heads=nkv, head_dim=hd, scale=hd ** -0.5,
+                               out=torch.empty(rows, nq * hd, dtype=BF))
+    close(outs[0][:n_real], exp[:n_real], 2e-2)
+    close(outs[1][:n_real], exp[:n_real], 2e-2)
+    assert torch.equal(outs[0], outs[2])

@@ -21,7 +21,7 @@ import voice_enabled_browser_automation_amd.ops as ops  # noqa: E402
 from bench_kernels import timeit  # noqa: E402
 
 
-def case(rows, ctx, same_seq, nq=32, nkv=8, hd=128, bs=16, max_ctx=2048):
+def case(rows, ctx, same_seq, nq=32, nkv=8, hd=128, bs=16, max_ctx=2048, shared=0):
     dev = "cuda"
     n_seq = 1 if same_seq else rows
     per = (max_ctx + bs - 1) // bs
@@ -31,6 +31,8 @@ def case(rows, ctx, same_seq, nq=32, nkv=8, hd=128, bs=16, max_ctx=2048):
     # shuffled physical blocks: the layout the block manager produces after churn
     perm = torch.randperm(blocks - 1, device=dev)[: n_seq * per].to(torch.int32) + 1
     table = perm.view(n_seq, per).contiguous()
+    if shared:  # sessions over one cached prompt prefix: the same physical blocks (prefix cache)
+        table[:, : shared // bs] = table[0, : shared // bs]
     q = torch.randn(rows, nq * hd, device=dev).to(torch.bfloat16)
     out = torch.empty_like(q)
     if same_seq:
@@ -56,8 +58,9 @@ def case(rows, ctx, same_seq, nq=32, nkv=8, hd=128, bs=16, max_ctx=2048):
                                          sid.cpu(), n_q_heads=nq, n_kv_heads=nkv, head_dim=hd, scale=hd ** -0.5,
                                          out=torch.empty(q.shape, dtype=q.dtype))
     err = (out.cpu().float() - ref.float()).abs().max().item()
-    kv_mb = n_seq * ctx * nkv * hd * 2 * 2 / 1e6
-    return dict(kernel="decode_attention", rows=rows, ctx=ctx, same_seq=same_seq, heads=f"{nq}/{nkv}x{hd}",
+    kv_mb = (n_seq * ctx - (n_seq - 1) * shared) * nkv * hd * 2 * 2 / 1e6
+    return dict(kernel="decode_attention", rows=rows, ctx=ctx, same_seq=same_seq, shared=shared,
+                heads=f"{nq}/{nkv}x{hd}",
                 us=round(t, 2), kv_mb=round(kv_mb, 2), max_err=round(err, 4))
 
 
@@ -65,6 +68,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
     ap.add_argument("--impls", default="mq,split")
+    ap.add_argument("--only-llama", action="store_true", help="skip the Whisper / 70B shapes")
     args = ap.parse_args()
     torch.manual_seed(0)
     res = []
@@ -72,6 +76,9 @@ def main():
               dict(rows=4, ctx=1100, same_seq=True), dict(rows=8, ctx=1100, same_seq=True),
               dict(rows=21, ctx=1100, same_seq=True), dict(rows=64, ctx=1100, same_seq=True),
               dict(rows=8, ctx=1100, same_seq=False), dict(rows=32, ctx=1100, same_seq=False),
+              # sessions sharing the cached 1k-token intent prompt prefix (the serving case)
+              dict(rows=8, ctx=1200, same_seq=False, shared=1024), dict(rows=16, ctx=1200, same_seq=False, shared=1024),
+              dict(rows=32, ctx=1200, same_seq=False, shared=1024), dict(rows=64, ctx=1200, same_seq=False, shared=1024),
               dict(rows=1, ctx=300, same_seq=True), dict(rows=1, ctx=2000, same_seq=True),
               # Whisper decoder: cross-attention over the 1500-frame window, self-attention
               dict(rows=1, ctx=1500, same_seq=True, nq=6, nkv=6, hd=64),
@@ -79,6 +86,8 @@ def main():
               dict(rows=1, ctx=44, same_seq=True, nq=20, nkv=20, hd=64, max_ctx=448),
               # Llama-3-70B at TP=8: one kv head, 8 q heads per rank
               dict(rows=1, ctx=1100, same_seq=True, nq=8, nkv=1, hd=128)]
+    if args.only_llama:
+        shapes = [s for s in shapes if s.get("nq", 32) == 32]
     for impl in args.impls.split(","):
         ops.set_attention_impl(impl)
         for sh in shapes:

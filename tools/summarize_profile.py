@@ -37,9 +37,9 @@ def main():
     print("| kernel | calls | total ms | avg us | % |" + (" vgpr/agpr/sgpr/lds/scratch |" if res else ""))
     print("|---|---:|---:|---:|---:|" + ("---|" if res else ""))
     for name, calls, total, avg, pct, footprint in rows[:30]:
-        name = name.replace("|", "/")
-        if len(name) > 95:
-            name = name[:95] + "..."
+        name = name.replace("|", "/").replace("(anonymous namespace)::", "")
+        if len(name) > 110:
+            name = name[:110] + "..."
         print(f"| `{name}` | {calls} | {total / 1e6:.2f} | {avg / 1e3:.2f} | {pct:.2f} |"
               + (f" {footprint} |" if res else ""))
 

@@ -366,7 +366,8 @@ class LlamaModel:
                     ops.decode_attention(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens,
                                          bufs.seq_ids, n_q_heads=self.nq, n_kv_heads=self.nkv, head_dim=self.hd,
                                          scale=self.scale, max_ctx=bufs.max_ctx, out=bufs.attn[:M],
-                                         part_o=bufs.part_o, part_ml=bufs.part_ml, counters=bufs.attn_cnt)
+                                         part_o=bufs.part_o, part_ml=bufs.part_ml, counters=bufs.attn_cnt,
+                                         shared=getattr(bufs, "shared", None))
                 ops.ext().chain_run(d[0], d[1], d[2], h, d[3])
                 continue
             chain = False  # shapes the chain cannot take: per-kernel path from here on
@@ -377,7 +378,7 @@ class LlamaModel:
                 ops.decode_attention_rows(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens, bufs.seq_ids,
                                      n_q_heads=self.nq, n_kv_heads=self.nkv, head_dim=self.hd, scale=self.scale,
                                      max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o, part_ml=bufs.part_ml,
-                                     counters=bufs.attn_cnt)
+                                     counters=bufs.attn_cnt, shared=getattr(bufs, "shared", None))
             elif pf_slices is not None:
                 attn = pf_out
                 lay = ops.KVLayout.paged(kc, vc, bufs.block_table)

@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import Optional, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 
@@ -378,6 +378,28 @@ def scratch(device, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
 
 
 GEMM_WS_FLOATS = 32 << 20  # split-K workspace (128 MB per device: 4 f32 slices of a 1k x 4096 output)
+# One-launch split-K (gemm.hip, opt-in VWA_GEMM_ONE_LAUNCH=1): the last slice of each output tile
+# reduces the slabs and runs the epilogue, so a split GEMM is one kernel instead of GEMM +
+# gemm_reduce.  Per-tile arrival counters, zeroed once and reset by each tile's last arriver.
+# Measured NOT faster at 32 decode rows (profiles/r4_gemm_one_launch_ab.md): the tail -- write-through
+# partial stores drained, the ticket, the L2-missing partial loads -- costs about what the reduce
+# launch does (fp8 o / down 26.3 vs 20.2 + 5.2 us).
+GEMM_ONE_LAUNCH = os.environ.get("VWA_GEMM_ONE_LAUNCH", "0") == "1"
+_GEMM_TICKETS: Dict[str, torch.Tensor] = {}
+
+
+def gemm_tickets(device) -> Optional[torch.Tensor]:
+    if not GEMM_ONE_LAUNCH:
+        return None
+    dev = torch.device(device)
+    if dev.type == "cuda" and dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    t = _GEMM_TICKETS.get(str(dev))
+    if t is None:
+        t = _GEMM_TICKETS[str(dev)] = torch.zeros(1 << 14, dtype=torch.int32, device=dev)
+    return t
+
+
 _GEMM_EPI = {"none": 0, "resid": 1, "swiglu": 2, "gelu": 3}
 
 
@@ -394,7 +416,7 @@ def gemm(x: torch.Tensor, w, out: torch.Tensor, *, epi: str = "none", bias: Opti
     tiled = isinstance(w, TiledWeight)
     wt = w.t if tiled else w
     ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
-    E.gemm(x, wt, bias, out, _GEMM_EPI[epi], rstd, residual, tiled, ws)
+    E.gemm(x, wt, bias, out, _GEMM_EPI[epi], rstd, residual, tiled, ws, gemm_tickets(x.device))
     return out
 
 
@@ -406,19 +428,16 @@ def gemm_fp8(x: torch.Tensor, w: "FP8Weight", out: torch.Tensor, *, epi: str = "
              bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, fuse_rms: bool = False,
              eps: float = 1e-5) -> torch.Tensor:
     """W8A8 tiled MFMA GEMM (gemm.hip F8) for M > 16 rows: x is quantised per row (amax / 448, one
-    kernel), the fp8 MFMA runs on the tiled fp8 weight, both scales (and the RMSNorm 1/rms of the
+    kernel that also yields the RMSNorm 1/rms), the fp8 MFMA runs on the tiled fp8 weight, both scales (and the RMSNorm 1/rms of the
     unquantised x) apply in the epilogue."""
     E = ext()
     M, K = x.shape
     x8 = scratch(x.device, "gemm_x8", M * K, torch.uint8).view(torch.float8_e4m3fn).view(M, K)
     sx = scratch(x.device, "gemm_sx", M)
-    E.quant_fp8_rows(x, x8, sx)
-    rstd = None
-    if fuse_rms:
-        rstd = scratch(x.device, "gemm_rstd", M)
-        E.row_rstd(x, rstd, eps)
+    rstd = scratch(x.device, "gemm_rstd", M) if fuse_rms else None
+    E.quant_fp8_rows(x, x8, sx, rstd, eps)  # one row pass: amax -> e4m3 codes (+ 1/rms)
     ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
-    E.gemm_fp8(x8, sx, w.w8, w.scale, bias, out, _GEMM_EPI[epi], rstd, residual, ws)
+    E.gemm_fp8(x8, sx, w.w8, w.scale, bias, out, _GEMM_EPI[epi], rstd, residual, ws, gemm_tickets(x.device))
     return out
 
 
@@ -569,6 +588,34 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
     return out
 
 
+# > 16-row QKV projections with the rotary + paged-KV write in the tiled GEMM's epilogue (gemm.hip
+# EPI_QKV; with split-K: in the slab reduction) -- no qkv scratch round trip, no rope_kv_write
+# launch.  VWA_GEMM_QKV=0: GEMM -> qkv scratch -> rope_kv_write
+GEMM_QKV_FUSED = os.environ.get("VWA_GEMM_QKV", "1") != "0"
+
+
+def _gemm_qkv(x, w, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, rope, positions, slots, q_out, k_cache,
+              v_cache) -> None:
+    E = ext()
+    M, K = x.shape
+    ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
+    tk = gemm_tickets(x.device)
+    common = (n_q_heads, n_kv_heads, head_dim, rope is not None, positions, slots, rope, q_out, k_cache, v_cache)
+    if isinstance(w, FP8Weight):
+        x8 = scratch(x.device, "gemm_x8", M * K, torch.uint8).view(torch.float8_e4m3fn).view(M, K)
+        sx = scratch(x.device, "gemm_sx", M)
+        rstd = scratch(x.device, "gemm_rstd", M) if fuse_rms else None
+        E.quant_fp8_rows(x, x8, sx, rstd, eps)
+        E.gemm_qkv(x8, sx, w.w8, w.scale, bias, rstd, True, ws, tk, *common)
+        return
+    rstd = None
+    if fuse_rms:
+        rstd = scratch(x.device, "gemm_rstd", M)
+        E.row_rstd(x, rstd, eps)
+    tiled = isinstance(w, TiledWeight)
+    E.gemm_qkv(x, None, w.t if tiled else w, None, bias, rstd, tiled, ws, tk, *common)
+
+
 def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Tensor], *, fuse_rms: bool, eps: float,
                    n_q_heads: int, n_kv_heads: int, head_dim: int, rope: Optional[torch.Tensor],
                    positions: torch.Tensor, slots: torch.Tensor, q_out: torch.Tensor, k_cache: torch.Tensor,
@@ -583,6 +630,10 @@ def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Te
             return q_out[:M]
         if ln_c is not None:
             x, ln_c = _layernorm_plain(x, eps), None
+        if _gpu(x) and gemm_ok(x, w_qkv) and GEMM_QKV_FUSED:
+            _gemm_qkv(x, w_qkv, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, rope, positions, slots, q_out,
+                      k_cache, v_cache)
+            return q_out[:M]
         if _gpu(x) and gemm_ok(x, w_qkv):
             qkv = scratch(x.device, "qkv", M * w_qkv.shape[0], torch.bfloat16).view(M, w_qkv.shape[0])
             gemm(x, w_qkv, qkv, bias=bias, fuse_rms=fuse_rms, eps=eps)
@@ -605,6 +656,10 @@ def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Te
     E = ext()
     use_rope = rope is not None
     fp8 = isinstance(w_qkv, FP8Weight)
+    if M > SKINNY_MAX_M and (gemm_fp8_ok(x, w_qkv) if fp8 else gemm_ok(x, w_qkv)) and GEMM_QKV_FUSED:
+        _gemm_qkv(x, w_qkv, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, rope, positions, slots, q_out,
+                  k_cache, v_cache)
+        return q_out[:M]
     if M > SKINNY_MAX_M and (gemm_fp8_ok(x, w_qkv) if fp8 else gemm_ok(x, w_qkv)):
         qkv = scratch(x.device, "qkv", M * w_qkv.shape[0], torch.bfloat16).view(M, w_qkv.shape[0])
         (gemm_fp8 if fp8 else gemm)(x, w_qkv, qkv, bias=bias, fuse_rms=fuse_rms, eps=eps)
@@ -736,9 +791,13 @@ def decode_n_splits(max_ctx: int) -> int:
 def decode_attention(q: torch.Tensor, kv: KVLayout, ctx_lens: torch.Tensor, seq_ids: torch.Tensor, *,
                      n_q_heads: int, n_kv_heads: int, head_dim: int, scale: float, max_ctx: int,
                      out: torch.Tensor, part_o: Optional[torch.Tensor] = None,
-                     part_ml: Optional[torch.Tensor] = None, counters: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     part_ml: Optional[torch.Tensor] = None, counters: Optional[torch.Tensor] = None,
+                     shared: Optional[torch.Tensor] = None) -> torch.Tensor:
     """One query row per token; ``max_ctx`` bounds every row's context (fixes the grid, so the
-    launch is graph-capturable while contexts grow)."""
+    launch is graph-capturable while contexts grow).  ``shared``: int32 [P, n_real] on the device
+    (the step buffers' shared-prefix words, runtime/engine.py): the first P keys of rows
+    0 .. n_real-1 are the same physical K/V blocks (the cached prompt every session shares), so the
+    multi-query kernel reads them once per group of rows across sessions."""
     n_splits = decode_n_splits(max_ctx)
     if not _gpu(q):
         return ref.decode_attention(q, kv, ctx_lens, seq_ids, n_q_heads=n_q_heads, n_kv_heads=n_kv_heads,
@@ -751,7 +810,7 @@ def decode_attention(q: torch.Tensor, kv: KVLayout, ctx_lens: torch.Tensor, seq_
     if counters is None:
         counters = split_counters(q.device, q.shape[0] * n_kv_heads)
     ext().decode_attention(q, kv.k, kv.v, kv.table, kv.block_size, kv.sb, kv.sh, kv.st, ctx_lens, seq_ids, n_q_heads,
-                           n_kv_heads, head_dim, scale, n_splits, part_o, part_ml, counters, out)
+                           n_kv_heads, head_dim, scale, n_splits, part_o, part_ml, counters, out, shared)
     return out
 
 
@@ -764,6 +823,7 @@ def decode_attention_rows(q: torch.Tensor, kv: KVLayout, ctx_lens: torch.Tensor,
     M = q.shape[0]
     if M <= slice_rows or not _gpu(q):
         return decode_attention(q, kv, ctx_lens, seq_ids, out=out, **kw)
+    kw.pop("shared", None)  # (the shared-prefix words describe the whole row set)
     for i in range(0, M, slice_rows):
         j = min(M, i + slice_rows)
         decode_attention(q[i:j], kv, ctx_lens[i:j], seq_ids[i:j], out=out[i:j], **kw)

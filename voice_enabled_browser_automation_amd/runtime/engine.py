@@ -19,6 +19,7 @@ for this step while the GPU is busy with the forward (see brain.intent_engine).
 """
 from __future__ import annotations
 
+import itertools
 import os
 from dataclasses import dataclass, field
 from types import SimpleNamespace
@@ -45,6 +46,14 @@ def bucket_for(n: int) -> int:
     raise ValueError(f"{n} rows exceed the largest decode bucket")
 
 
+_SEQ_UIDS = itertools.count()
+
+# Decode attention reads the prompt prefix the step's sessions share (the same prefix-cached
+# blocks) once per group of rows across sessions (attention.hip / mq_attention.h cascade);
+# VWA_SHARED_ATTN=0: once per session
+SHARED_ATTN = os.environ.get("VWA_SHARED_ATTN", "1") != "0"
+
+
 @dataclass
 class Sequence_:
     sid: int                     # block-table row
@@ -52,6 +61,7 @@ class Sequence_:
     blocks: List[int] = field(default_factory=list)
     n_computed: int = 0          # tokens whose K/V are in the cache
     n_cached_prefix: int = 0     # tokens served from the prefix cache
+    uid: int = field(default_factory=lambda: next(_SEQ_UIDS))  # unique for the process lifetime
 
 
 class StepBuffers:
@@ -63,8 +73,10 @@ class StepBuffers:
         self.max_rows = max_rows
         self.max_ctx = max_ctx
         # all per-row metadata lives in ONE device buffer (and one pinned host mirror) so a step
-        # needs a single H2D copy: [tokens | positions | seq_ids | ctx_lens | slots (int64) | sel]
-        # (sel = the rows whose logits the step returns: one per sequence, not one per token row)
+        # needs a single H2D copy: [tokens | positions | seq_ids | ctx_lens | slots (int64) | sel |
+        # shared] (sel = the rows whose logits the step returns: one per sequence, not one per token
+        # row; shared = [P, n_real]: the first P keys of the step's real rows are the same cached
+        # prompt blocks -- the decode attention reads them once per group of sessions)
         R = max_rows
         # per-ROW copy of each row's sequence block table (chained attention: read in the same round
         # trip as seq_ids / ctx_lens instead of a dependent table load); <= 128 blocks per sequence.
@@ -73,15 +85,16 @@ class StepBuffers:
         # GPU time plus a 4 us scheduling gap per decode step)
         self.rt_cols = max_blocks_per_seq if max_blocks_per_seq <= 128 and max_blocks_per_seq % 2 == 0 else 0
         C = max(2, self.rt_cols)
-        T = (7 * R + 15) // 16 * 16  # row table at a 64-byte aligned offset
+        T = (7 * R + 2 + 15) // 16 * 16  # row table at a 64-byte aligned offset
         self.meta_all = torch.zeros(T + R * C, **i32)
-        self.meta = self.meta_all[: 7 * R]
+        self.meta = self.meta_all[: 7 * R + 2]
         self.tokens = self.meta[0:R]
         self.positions = self.meta[R : 2 * R]
         self.seq_ids = self.meta[2 * R : 3 * R]
         self.ctx_lens = self.meta[3 * R : 4 * R]
         self.slots = self.meta[4 * R : 6 * R].view(torch.int64)
         self.sel = self.meta[6 * R : 7 * R]
+        self.shared = self.meta[7 * R : 7 * R + 2]
         self.ctx_lens.fill_(1)
         self.slots.fill_(-1)
         self.block_table = torch.zeros(max_seqs, max_blocks_per_seq, **i32)
@@ -99,10 +112,11 @@ class StepBuffers:
         self.attn_cnt = torch.zeros(max_rows * model.nkv, dtype=torch.int32, device=device)  # chunk tickets
         pin = torch.device(device).type == "cuda"
         self.h_meta_all = torch.zeros(T + R * C, dtype=torch.int32, pin_memory=pin)
-        self.h_meta = self.h_meta_all[: 7 * R]
+        self.h_meta = self.h_meta_all[: 7 * R + 2]
         self.h_i32 = self.h_meta[: 4 * R].view(4, R)
         self.h_slots = self.h_meta[4 * R : 6 * R].view(torch.int64)
-        self.h_sel = self.h_meta[6 * R :]
+        self.h_sel = self.h_meta[6 * R : 7 * R]
+        self.np_shared = self.h_meta[7 * R : 7 * R + 2].numpy()
         self.row_table = self.meta_all[T:].view(R, C)
         self.h_row_table = self.h_meta_all[T:].view(R, C)
         self.np_row_table = self.h_row_table.numpy()
@@ -183,6 +197,7 @@ class LLMEngine:
         # replayed graph -- so the next step may only rewrite them once it has executed
         self._staging_inflight = False
         self._head_rows: Optional[torch.Tensor] = None  # the last step's hidden rows for head_logits()
+        self._shared_cache: Dict[tuple, int] = {}  # sequences of a step -> shared prefix blocks
 
     # ------------------------------------------------------------------ sequences
     def new_sequence(self, tokens: Sequence[int], use_prefix_cache: bool = True) -> Sequence_:
@@ -224,6 +239,31 @@ class LLMEngine:
         row[:] = 0
         row[: len(seq.blocks)] = seq.blocks
         self.bufs.table_dirty = True
+
+    def _shared_prefix(self, rows: List[Tuple[Sequence_, int]], min_ctx: int) -> int:
+        """Keys (a multiple of 32) that every row of the step reads from the SAME physical blocks:
+        the prefix-cached prompt the sessions share (decode attention reads them once per group of
+        rows across sessions).  0 below 128 keys or for a single sequence.  Cached per set of
+        sequences (it changes only when a session joins or leaves)."""
+        if not SHARED_ATTN:
+            return 0
+        seqs = {}
+        for seq, _ in rows:
+            seqs.setdefault(seq.sid, seq)
+        if len(seqs) < 2:
+            return 0
+        key = tuple(s.uid for s in seqs.values())
+        nb = self._shared_cache.get(key)
+        if nb is None:
+            lim = min(len(s.blocks) for s in seqs.values())
+            t = self.bufs.np_table[list(seqs)][:, :lim]
+            eq = (t == t[0]).all(0)
+            nb = int(lim if eq.all() else eq.argmin())
+            if len(self._shared_cache) > 256:
+                self._shared_cache.clear()
+            self._shared_cache[key] = nb
+        P = min(nb * self.block_size, min_ctx) // 32 * 32
+        return P if P >= 128 else 0
 
     def slot_of(self, seq: Sequence_, pos: int) -> int:
         return seq.blocks[pos // self.block_size] * self.block_size + pos % self.block_size
@@ -333,6 +373,8 @@ class LLMEngine:
         hi[2, :n] = sids
         hi[3, :n] = hi[1, :n] + 1
         b.np_slots[:n] = slots
+        b.np_shared[0] = self._shared_prefix(rows, min(poss) + 1)
+        b.np_shared[1] = n
         if M > n:  # padded rows: no KV write, 1-token context on scratch block 0
             hi[0:3, n:M] = 0
             hi[3, n:M] = 1
