@@ -273,9 +273,12 @@ void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi,
 
 // W8A8 tiled GEMM (gemm.hip, F8): x8 OCP e4m3 [M, K] with per-row scales sx (quant_fp8_rows),
 // w8 the fp8 tiled layout [N, K] with per-row scales sw.
-void gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> bias, Tensor y, int64_t epi,
+// q8 / q_sx / q_rstd (optional): the output rows quantised for the next W8A8 GEMM in the split-K
+// reduce (gemm_reduce_rowq_kernel); returns whether that happened (no split: the caller quantises).
+bool gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> bias, Tensor y, int64_t epi,
               c10::optional<Tensor> rstd, c10::optional<Tensor> residual, c10::optional<Tensor> ws,
-              c10::optional<Tensor> tickets) {
+              c10::optional<Tensor> tickets, c10::optional<Tensor> q8, c10::optional<Tensor> q_sx,
+              c10::optional<Tensor> q_rstd, double q_eps) {
   c10::DeviceGuard g(x8.device());
   TORCH_CHECK(x8.is_cuda() && x8.scalar_type() == at::kFloat8_e4m3fn && x8.dim() == 2 && x8.stride(1) == 1 &&
                   x8.stride(0) % 16 == 0 && (reinterpret_cast<uintptr_t>(x8.data_ptr()) & 15) == 0,
@@ -332,7 +335,26 @@ void gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> 
     p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x8), ws->numel());
   }
   set_tickets(p, tickets);
-  check_rc(vwa_gemm((int)epi, &p, cur_stream(x8)), "gemm_fp8");
+  if (q8.has_value()) {
+    const int64_t nout = epi == 2 ? p.N / 2 : p.N;
+    TORCH_CHECK(q8->is_cuda() && q8->scalar_type() == at::kFloat8_e4m3fn && q8->dim() == 2 && q8->size(0) == p.M &&
+                    q8->size(1) == nout && q8->stride(1) == 1 && q8->stride(0) % 16 == 0 &&
+                    (reinterpret_cast<uintptr_t>(q8->data_ptr()) & 15) == 0,
+                "q8: fp8 [M, output columns], 16-byte aligned rows");
+    TORCH_CHECK(q_sx.has_value() && q_sx->scalar_type() == at::kFloat && q_sx->numel() >= p.M, "q_sx f32 [M]");
+    p.q8 = reinterpret_cast<uint8_t*>(q8->data_ptr());
+    p.ldq8 = (int)q8->stride(0);
+    p.q_sx = q_sx->data_ptr<float>();
+    if (q_rstd.has_value()) {
+      TORCH_CHECK(q_rstd->scalar_type() == at::kFloat && q_rstd->numel() >= p.M, "q_rstd f32 [M]");
+      p.q_rstd = q_rstd->data_ptr<float>();
+    }
+    p.q_eps = (float)q_eps;
+  }
+  const int rc = vwa_gemm((int)epi, &p, cur_stream(x8));
+  if (rc == 2) return true;
+  check_rc(rc, "gemm_fp8");
+  return false;
 }
 
 void check_cache(const Tensor& c, const char* name);
@@ -1214,6 +1236,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("s_qkv") = py::none(), py::arg("tp_ar") = 0);
   m.def("set_small_gemm_bytes", &set_small_gemm_bytes);
   m.def("gemm_set_p8", [](int64_t mode) { vwa_gemm_set_p8((int)mode); });
+  m.def("gemm_set_nb", [](int64_t nb) { vwa_gemm_set_nb((int)nb); });
   m.def("chain_make_seq", &chain_make_seq, py::arg("seq"), py::arg("X"), py::arg("W"), py::arg("bias"),
         py::arg("ln_c"), py::arg("Y"), py::arg("epi"), py::arg("eps"), py::arg("n_heads"), py::arg("head_dim"),
         py::arg("positions"), py::arg("slots"), py::arg("k_cache"), py::arg("v_cache"), py::arg("bar"),
@@ -1229,7 +1252,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_qkv", &gemm_qkv);
   m.def("gemm_fp8", &gemm_fp8, py::arg("x8"), py::arg("sx"), py::arg("w8"), py::arg("sw"), py::arg("bias"),
         py::arg("y"), py::arg("epi"), py::arg("rstd") = py::none(), py::arg("residual") = py::none(),
-        py::arg("ws") = py::none(), py::arg("tickets") = py::none());
+        py::arg("ws") = py::none(), py::arg("tickets") = py::none(), py::arg("q8") = py::none(),
+        py::arg("q_sx") = py::none(), py::arg("q_rstd") = py::none(), py::arg("q_eps") = 1e-5);
   m.def("rmsnorm", &rmsnorm);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);

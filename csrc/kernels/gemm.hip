@@ -307,7 +307,7 @@ VWA_DEVICE void add8(float (&v)[8], const float4& a, const float4& b) {
 // rotation partner chunk c^8, then rotary + q / KV stores), 16-byte stores.  Slices are loaded
 // in batches of 4 (all of a batch's loads in flight before any is used).
 template <int EPI, int AUX>
-VWA_DEVICE void reduce_item(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int m, int c) {
+VWA_DEVICE void reduce_item(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int m, int c, float* keep = nullptr) {
   constexpr bool SW = EPI == EPI_SWIGLU, QK = EPI == EPI_QKV;
   const size_t slab = (size_t)p.M * p.N;
   const float rs = (p.rstd ? p.rstd[m] : 1.f) * (p.sx ? p.sx[m] : 1.f);
@@ -365,7 +365,9 @@ VWA_DEVICE void reduce_item(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += r[e];
   }
-  *reinterpret_cast<uint4*>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + c) = pack8(v);
+  const uint4 packed = pack8(v);
+  *reinterpret_cast<uint4*>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + c) = packed;
+  if (keep) unpack8(packed, keep);  // the stored (bf16-rounded) values, for the row quantisation
 }
 
 // The last-arriving slice of output tile (bm, bn) (one-launch split-K): every item of the tile's
@@ -383,7 +385,11 @@ VWA_DEVICE void split_reduce_tile(const GemmParams& p, __amdgpu_buffer_rsrc_t rw
   }
 }
 
-template <class C, int EPI, bool WT, bool F8 = false, bool P8 = false>
+// NB (128^2 kernel): LDS stage buffers.  2: the next stage's DMA in flight during this one's MFMAs
+// (2 workgroups per CU -- prompt-sized GEMMs).  4: up to four stages in flight -- few-row GEMMs
+// (one row block, weight streaming) whose short split-K slices are latency-bound with two (a
+// 4-stage slice of the 32-row fp8 o_proj measured 2 TB/s); 128 KB LDS, one workgroup per CU.
+template <class C, int EPI, bool WT, bool F8 = false, bool P8 = false, int NB = 2>
 __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   constexpr int FM = C::FM, FN = C::FN;
@@ -490,6 +496,23 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
       asm volatile("s_barrier" ::: "memory");
     }
     if (wm == 0) asm volatile("s_barrier" ::: "memory");  // (group 1 started one barrier later)
+  } else if constexpr (NB > 2) {
+    static_assert(NB <= 4, "vmcnt cases below");
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if (i < nh) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + i, lds + i * C::STAGE);
+    for (int i = 0; i < nh; ++i) {
+      // stage i landed everywhere: the stages issued after it (8 DMA instructions each) may stay
+      // in flight
+      const int ahead = min(NB - 1, nh - 1 - i);
+      if (ahead >= 3) asm volatile("s_waitcnt vmcnt(24)\n\ts_barrier" ::: "memory");
+      else if (ahead == 2) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      compute_stage<C, F8>(lds + (i % NB) * C::STAGE, acc, wm, wn);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done reading it
+      if (i + NB < nh) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + i + NB, lds + (i % NB) * C::STAGE);
+    }
   } else {
   if (nh > 0) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0, lds);
   if (nh > 1) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + 1, lds + C::STAGE);
@@ -669,6 +692,60 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmParams p) {
   reduce_item<EPI, 0>(p, rws, (int)(id / cpr), (int)(id % cpr) * 8);
 }
 
+// Two-launch split-K reduce with the NEXT W8A8 GEMM's input quantisation fused (fp8 decode steps
+// of > 16 rows): one workgroup per output row -- sum + epilogue + bf16 store of each of the row's
+// chunks (kept in registers), then the row's amax (-> e4m3 codes, scale) and sum of squares (->
+// the RMSNorm 1/rms) over the stored bf16 values: the same chunk -> thread mapping and order as
+// quant_fp8_rows_kernel on the stored row, so the same codes / scale / 1/rms.  One launch instead
+// of gemm_reduce + quant_fp8_rows (~5 us each at 32 rows, profiles/r4_rows32_fp8_kernel_stats_v2.md).
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_reduce_rowq_kernel(GemmParams p) {
+  constexpr int MAXC = 8;  // 8-column chunks per thread: output rows of up to 16384 columns
+  __shared__ float red[2][4];
+  const int m = blockIdx.x;
+  const int nch = (EPI == EPI_SWIGLU ? p.N / 2 : p.N) / 8;
+  const __amdgpu_buffer_rsrc_t rws = rsrc(p.ws, (size_t)p.splits * p.M * p.N * 4);
+  float v[MAXC][8];
+  float am = 0.f, ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int ch = threadIdx.x + i * 256;
+    if (ch < nch) {
+      reduce_item<EPI, 0>(p, rws, m, ch * 8, v[i]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        am = fmaxf(am, fabsf(v[i][e]));
+        ss += v[i][e] * v[i][e];
+      }
+    }
+  }
+  am = wave_max(am);
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = am;
+    red[1][threadIdx.x >> 6] = ss;
+  }
+  __syncthreads();
+  am = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+  const float sx = am > 0.f ? am * (1.f / 448.f) : 1.f;
+  const float iv = 1.f / sx;
+  if (threadIdx.x == 0) {
+    p.q_sx[m] = sx;
+    if (p.q_rstd) p.q_rstd[m] = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)(nch * 8) + p.q_eps);
+  }
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int ch = threadIdx.x + i * 256;
+    if (ch < nch) {
+      const float* f = v[i];
+      uint2 o;
+      o.x = cvt_pk_fp8(f[0] * iv, f[1] * iv) | (cvt_pk_fp8(f[2] * iv, f[3] * iv) << 16);
+      o.y = cvt_pk_fp8(f[4] * iv, f[5] * iv) | (cvt_pk_fp8(f[6] * iv, f[7] * iv) << 16);
+      *reinterpret_cast<uint2*>(p.q8 + (size_t)m * p.ldq8 + ch * 8) = o;
+    }
+  }
+}
+
 // per-row 1/rms of X (the RMSNorm of a projection whose gamma is folded into W)
 __global__ __launch_bounds__(256) void row_rstd_kernel(const u16* __restrict__ x, int ldx, int M, int K, float eps,
                                                        float* __restrict__ rstd) {
@@ -686,16 +763,27 @@ __global__ __launch_bounds__(256) void row_rstd_kernel(const u16* __restrict__ x
   if (lane_id() == 0) rstd[row] = rsqrtf(ss / (float)K + eps);
 }
 
+int g_gemm_nb = 4;  // stage buffers of the 128^2 kernel for one-row-block GEMMs (2 or 4)
+
+template <class C, int EPI, int NB>
+void launch_nb(const GemmParams& p, dim3 grid, hipStream_t st) {
+  const int lds = NB * C::STAGE > C::LDS ? NB * C::STAGE : C::LDS;
+  if (p.sw)
+    hipLaunchKernelGGL((gemm_kernel<C, EPI, true, true, false, NB>), grid, dim3(C::THREADS), lds, st, p);
+  else if (p.w_tiled)
+    hipLaunchKernelGGL((gemm_kernel<C, EPI, true, false, false, NB>), grid, dim3(C::THREADS), lds, st, p);
+  else
+    hipLaunchKernelGGL((gemm_kernel<C, EPI, false, false, false, NB>), grid, dim3(C::THREADS), lds, st, p);
+}
+
 template <class C, int EPI>
 int launch_cfg(const GemmParams& p, hipStream_t st) {
   const int tiles = ((p.M + C::BM - 1) / C::BM) * ((p.N + C::BN - 1) / C::BN);
   const dim3 grid(tiles * p.splits * (p.nbatch > 1 ? p.nbatch : 1));
-  if (p.sw)
-    hipLaunchKernelGGL((gemm_kernel<C, EPI, true, true>), grid, dim3(C::THREADS), C::LDS, st, p);
-  else if (p.w_tiled)
-    hipLaunchKernelGGL((gemm_kernel<C, EPI, true>), grid, dim3(C::THREADS), C::LDS, st, p);
+  if (g_gemm_nb == 4 && p.M <= C::BM && p.nbatch <= 1)
+    launch_nb<C, EPI, 4>(p, grid, st);
   else
-    hipLaunchKernelGGL((gemm_kernel<C, EPI, false>), grid, dim3(C::THREADS), C::LDS, st, p);
+    launch_nb<C, EPI, 2>(p, grid, st);
   return 0;
 }
 
@@ -715,11 +803,21 @@ int launch_epi(const GemmParams& p, hipStream_t st, bool p8) {
   } else {
     launch_cfg<CfgS, EPI>(p, st);
   }
+  bool rowq = false;
   if (p.splits > 1 && p.tickets == nullptr) {
-    const int64_t n = (int64_t)p.M * (EPI == EPI_SWIGLU ? p.N / 2 : p.N) / 8;
-    hipLaunchKernelGGL((gemm_reduce_kernel<EPI>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
+    if constexpr (EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_SWIGLU) {
+      if (p.q8) {
+        hipLaunchKernelGGL((gemm_reduce_rowq_kernel<EPI>), dim3(p.M), dim3(256), 0, st, p);
+        rowq = true;
+      }
+    }
+    if (!rowq) {
+      const int64_t n = (int64_t)p.M * (EPI == EPI_SWIGLU ? p.N / 2 : p.N) / 8;
+      hipLaunchKernelGGL((gemm_reduce_kernel<EPI>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
+    }
   }
-  return (int)hipGetLastError();
+  const int e = (int)hipGetLastError();
+  return e ? e : rowq ? 2 : 0;
 }
 
 }  // namespace
@@ -735,6 +833,7 @@ extern "C" int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats) 
 }
 
 extern "C" void vwa_gemm_set_p8(int mode) { g_p8_mode = mode; }
+extern "C" void vwa_gemm_set_nb(int nb) { g_gemm_nb = nb == 4 ? 4 : 2; }
 
 extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
   GemmParams p = *pp;
@@ -743,6 +842,7 @@ extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
     return -11;
   if (p.sw && (!p.sx || !p.w_tiled)) return -14;  // W8A8: per-row X scales and the fp8 tiled layout
   if (epi == EPI_SWIGLU && (p.N % 32 || p.y_f32)) return -12;
+  if (p.q8 && (p.y_f32 || !p.q_sx || (epi == EPI_SWIGLU ? p.N / 2 : p.N) > 16384 || p.ldq8 % 8)) return -17;
   if (epi == EPI_QKV && (p.y_f32 || p.head_dim % 16 || p.N != (p.n_q_heads + 2 * p.n_kv_heads) * p.head_dim ||
                          !p.q_out || !p.k_cache || !p.v_cache || !p.slots || (p.use_rope && (!p.rope || !p.positions))))
     return -16;

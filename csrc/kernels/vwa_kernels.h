@@ -163,6 +163,10 @@ struct GemmParams {
   const int* positions; const int64_t* slots; const float* rope;
   uint16_t* q_out; int ldq; uint16_t* k_cache; uint16_t* v_cache; int block_size;
   int64_t cache_sb, cache_sh, cache_st;
+  // optional row quantisation of the OUTPUT for the next W8A8 GEMM (epilogues 0 / 1 / 2 with the
+  // two-launch split-K): e4m3 codes q8 [M, ldq8], per-row scales q_sx (amax / 448) and, if q_rstd,
+  // the RMSNorm 1/rms (eps q_eps) of the stored bf16 rows; vwa_gemm returns 2 when it did so
+  uint8_t* q8; int ldq8; float* q_sx; float* q_rstd; float q_eps;
 };
 
 struct FlashAttnParams {
@@ -187,6 +191,7 @@ int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g,
                      int xg2 = 0, int f8 = 0);
 int vwa_gemm(int epi, const GemmParams* p, hipStream_t st);
 int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats);
+void vwa_gemm_set_nb(int nb);  // 128^2 kernel stage buffers for one-row-block GEMMs: 4 (default) or 2
 void vwa_gemm_set_p8(int mode);  // 0: 128^2 kernel only, 1: 256^2 8-phase wherever eligible, 2: measured rule
 int vwa_row_rstd(const uint16_t* x, int ldx, int M, int K, float eps, float* rstd, hipStream_t st);
 int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,

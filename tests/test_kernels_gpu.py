@@ -1006,3 +1006,40 @@ def test_decode_attention_shared_prefix(hd, nq, nkv, n_sess, P):
     close(outs[0][:n_real], exp[:n_real], 2e-2)
     close(outs[1][:n_real], exp[:n_real], 2e-2)
     assert torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("M", [17, 40, 64])
+def test_fp8_row_quant_handoff(M):
+    """W8A8 GEMM chain of a Llama layer at > 16 rows (o_proj -> gate/up -> down -> next QKV): with
+    the row-quantisation hand-off each split-K reduce quantises its output for the next GEMM
+    (no quant_fp8_rows launches in between) -- bit-identical to quantising every input."""
+    d, F, nq, nkv, hd = 1024, 2048, 8, 2, 128
+    W = dict(o=rnd(d, nq * hd, scale=0.03), gu=ops.interleave_gate_up(rnd(F, d, scale=0.03), rnd(F, d, scale=0.03)),
+             down=rnd(d, F, scale=0.02), qkv=ops.permute_qkv_rows(rnd((nq + 2 * nkv) * hd, d, scale=0.03),
+                                                                nq + 2 * nkv, hd))
+    W8 = {k: ops.FP8Weight.quantize(v, tiled=True) for k, v in W.items()}
+    attn0, h0 = rnd(M, nq * hd), rnd(M, d)
+    rope = ops.rope_table(512, hd, 5e5, device=DEV)
+    pos = torch.arange(M, dtype=torch.int32, device=DEV)
+    slots = torch.arange(M, dtype=torch.int64, device=DEV)
+
+    def layer(on):
+        ops.row_quant_handoff(on)
+        try:
+            h = h0.clone()
+            ops.linear(attn0, W8["o"], out=h, residual=h)
+            act = ops.linear_swiglu(h, W8["gu"], fuse_rms=True)
+            ops.linear(act, W8["down"], out=h, residual=h)
+            kc = torch.zeros((M + 15) // 16 + 1, nkv, 16, hd, dtype=BF, device=DEV)
+            vc = torch.zeros_like(kc)
+            q = torch.zeros(M, nq * hd, dtype=BF, device=DEV)
+            ops.qkv_rope_write(h, W8["qkv"], None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
+                               rope=rope, positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc)
+            torch.cuda.synchronize()
+            return h, act, q, kc, vc
+        finally:
+            ops.row_quant_handoff(False)
+
+    with_h, without = layer(True), layer(False)
+    for a, b in zip(with_h, without):
+        assert torch.equal(a, b)

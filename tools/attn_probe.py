@@ -21,7 +21,8 @@ import voice_enabled_browser_automation_amd.ops as ops  # noqa: E402
 from bench_kernels import timeit  # noqa: E402
 
 
-def case(rows, ctx, same_seq, nq=32, nkv=8, hd=128, bs=16, max_ctx=2048, shared=0):
+def case(rows, ctx, same_seq, nq=32, nkv=8, hd=128, bs=16, max_ctx=2048, shared=0, use_shared=True,
+         n_splits=None):
     dev = "cuda"
     n_seq = 1 if same_seq else rows
     per = (max_ctx + bs - 1) // bs
@@ -47,9 +48,12 @@ def case(rows, ctx, same_seq, nq=32, nkv=8, hd=128, bs=16, max_ctx=2048, shared=
     pm = torch.empty(rows * ns * nq * 2, device=dev)
     cnt = torch.zeros(rows * nkv, dtype=torch.int32, device=dev)
 
+    sh = torch.tensor([shared, rows], dtype=torch.int32, device=dev) if shared and use_shared else None
+
     def f():
         ops.decode_attention(q, kv, cl, sid, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd, scale=hd ** -0.5,
-                             max_ctx=max_ctx, out=out, part_o=po, part_ml=pm, counters=cnt)
+                             max_ctx=max_ctx, out=out, part_o=po, part_ml=pm, counters=cnt, shared=sh,
+                             n_splits=n_splits)
 
     t = timeit(f)
     f()
@@ -60,6 +64,7 @@ def case(rows, ctx, same_seq, nq=32, nkv=8, hd=128, bs=16, max_ctx=2048, shared=
     err = (out.cpu().float() - ref.float()).abs().max().item()
     kv_mb = (n_seq * ctx - (n_seq - 1) * shared) * nkv * hd * 2 * 2 / 1e6
     return dict(kernel="decode_attention", rows=rows, ctx=ctx, same_seq=same_seq, shared=shared,
+                grouped=bool(sh is not None), n_splits=n_splits,
                 heads=f"{nq}/{nkv}x{hd}",
                 us=round(t, 2), kv_mb=round(kv_mb, 2), max_err=round(err, 4))
 
@@ -69,6 +74,8 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--impls", default="mq,split")
     ap.add_argument("--only-llama", action="store_true", help="skip the Whisper / 70B shapes")
+    ap.add_argument("--split-sweep", action="store_true",
+                    help="sessions over a shared prefix: chunk cap x shared-prefix grouping on / off")
     args = ap.parse_args()
     torch.manual_seed(0)
     res = []
@@ -86,6 +93,9 @@ def main():
               dict(rows=1, ctx=44, same_seq=True, nq=20, nkv=20, hd=64, max_ctx=448),
               # Llama-3-70B at TP=8: one kv head, 8 q heads per rank
               dict(rows=1, ctx=1100, same_seq=True, nq=8, nkv=1, hd=128)]
+    if args.split_sweep:
+        shapes = [dict(rows=r, ctx=1200, same_seq=False, shared=1024, use_shared=u, n_splits=ns)
+                  for r in (8, 16, 32, 64) for u in (True, False) for ns in (None, 8, 4, 2, 1)]
     if args.only_llama:
         shapes = [s for s in shapes if s.get("nq", 32) == 32]
     for impl in args.impls.split(","):

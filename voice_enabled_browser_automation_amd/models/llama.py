@@ -351,6 +351,9 @@ class LlamaModel:
             pf_sid = torch.full((M,), prefill_seq, **i32)
             pf_slices = [(i, min(M, i + 64)) for i in range(0, M, 64)]
             pf_out = torch.empty((M, self.nq * self.hd), dtype=self.dtype, device=self.device)
+        # fp8 rows > 16 (TP = 1: h is written only by the GEMM epilogues inside the loop): each W8A8
+        # GEMM's split-K reduce also quantises its output rows for the next one (ops.row_quant_handoff)
+        ops.row_quant_handoff(self.wdtype == "fp8" and self.tp.size == 1)
         for li, L in enumerate(self.layers):
             kc, vc = kv.k[li], kv.v[li]
             if chain and li > 0:
@@ -398,6 +401,7 @@ class LlamaModel:
             act = bufs.act[:M] if M <= bufs.act.shape[0] else None
             act = ops.linear_swiglu(h, L.gu, fuse_rms=True, eps=cfg.rms_eps, out=act)
             self._row_parallel(act, L.down, h)
+        ops.row_quant_handoff(False)
         if n_sel is not None:
             hs = torch.index_select(h, 0, bufs.sel[:n_sel], out=bufs.hidden_sel[:n_sel])
         else:

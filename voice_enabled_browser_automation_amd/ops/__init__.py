@@ -57,6 +57,9 @@ def ext():
         p8 = os.environ.get("VWA_GEMM_P8")  # 0: 128x128 GEMM only, 1: 256x256 8-phase wherever eligible
         if p8 not in (None, ""):
             m.gemm_set_p8(int(p8))
+        nb = os.environ.get("VWA_GEMM_NB")  # stage buffers of few-row (one row block) GEMMs: 4 / 2
+        if nb not in (None, ""):
+            m.gemm_set_nb(int(nb))
         _EXT = m
         return m
     except BaseException as e:  # noqa: BLE001
@@ -424,20 +427,77 @@ def _rows16(t: Optional[torch.Tensor]) -> bool:
     return t is None or (t.stride(-1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0)
 
 
+# Row-quantisation hand-off between consecutive W8A8 GEMMs on the same rows (the fp8 decode step
+# of > 16 rows): a GEMM whose split-K reduce can also quantise its output rows (gemm.hip
+# gemm_reduce_rowq_kernel) leaves the e4m3 codes / scales / 1/rms in the next GEMM's input staging
+# buffers, and the next GEMM reading that output skips its quant_fp8_rows launch.  Enabled only
+# around a model's layer loop (models/llama.py), where the hand-off tensor (the residual stream /
+# the SwiGLU output) is written by nothing but those GEMMs; the key is (pointer, shape, row stride).
+_QHAND = {"on": False, "key": None, "eps": None, "n": 0}
+
+
+def row_quant_handoff(enabled: bool) -> None:
+    _QHAND.update(on=bool(enabled) and os.environ.get("VWA_ROWQ_HANDOFF", "1") != "0", key=None, eps=None)
+
+
+def _qhand_guard(fn):
+    """A projection that wrote the hand-off tensor by any other path (not gemm_fp8) invalidates it."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapped(*a, **k):
+        n0 = _QHAND["n"]
+        y = fn(*a, **k)
+        key = _QHAND["key"]
+        if key is not None and _QHAND["n"] == n0 and isinstance(y, torch.Tensor) and y.data_ptr() == key[0]:
+            _QHAND["key"] = None
+        return y
+
+    return wrapped
+
+
+def _qkey(t: torch.Tensor):
+    return (t.data_ptr(), tuple(t.shape), t.stride(0))
+
+
+def _fp8_staging(x: torch.Tensor, K: int, n_out: int = 0):
+    M = x.shape[0]
+    x8 = scratch(x.device, "gemm_x8", M * max(K, n_out), torch.uint8).view(torch.float8_e4m3fn)
+    return x8, scratch(x.device, "gemm_sx", M), scratch(x.device, "gemm_rstd", M)
+
+
+def _fp8_input(x: torch.Tensor, fuse_rms: bool, eps: float):
+    """(x8 [M, K], sx, rstd or None) of x: the hand-off of the GEMM that wrote x, or one row pass."""
+    M, K = x.shape
+    x8, sx, rs = _fp8_staging(x, K)
+    if not (_QHAND["on"] and _QHAND["key"] == _qkey(x) and _QHAND["eps"] == eps):
+        E = ext()
+        E.quant_fp8_rows(x, x8[: M * K].view(M, K), sx, rs if fuse_rms else None, eps)
+    return x8[: M * K].view(M, K), sx, (rs if fuse_rms else None)
+
+
 def gemm_fp8(x: torch.Tensor, w: "FP8Weight", out: torch.Tensor, *, epi: str = "none",
              bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, fuse_rms: bool = False,
              eps: float = 1e-5) -> torch.Tensor:
     """W8A8 tiled MFMA GEMM (gemm.hip F8) for M > 16 rows: x is quantised per row (amax / 448, one
-    kernel that also yields the RMSNorm 1/rms), the fp8 MFMA runs on the tiled fp8 weight, both scales (and the RMSNorm 1/rms of the
-    unquantised x) apply in the epilogue."""
+    kernel that also yields the RMSNorm 1/rms -- or the previous GEMM's hand-off), the fp8 MFMA runs
+    on the tiled fp8 weight, both scales (and the RMSNorm 1/rms of the unquantised x) apply in the
+    epilogue.  Inside row_quant_handoff: the output rows are quantised for the next GEMM too."""
     E = ext()
     M, K = x.shape
-    x8 = scratch(x.device, "gemm_x8", M * K, torch.uint8).view(torch.float8_e4m3fn).view(M, K)
-    sx = scratch(x.device, "gemm_sx", M)
-    rstd = scratch(x.device, "gemm_rstd", M) if fuse_rms else None
-    E.quant_fp8_rows(x, x8, sx, rstd, eps)  # one row pass: amax -> e4m3 codes (+ 1/rms)
+    x8, sx, rstd = _fp8_input(x, fuse_rms, eps)
     ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
-    E.gemm_fp8(x8, sx, w.w8, w.scale, bias, out, _GEMM_EPI[epi], rstd, residual, ws, gemm_tickets(x.device))
+    tk = gemm_tickets(x.device)
+    if not _QHAND["on"] or out.dtype != torch.bfloat16:
+        E.gemm_fp8(x8, sx, w.w8, w.scale, bias, out, _GEMM_EPI[epi], rstd, residual, ws, tk)
+        return out
+    n_out = out.shape[1]
+    q8, qs, qr = _fp8_staging(x, K, n_out)
+    q8 = q8[: M * n_out].view(M, n_out)
+    # (the output's codes overwrite this GEMM's input codes -- in stream order, after it read them)
+    if not E.gemm_fp8(x8, sx, w.w8, w.scale, bias, out, _GEMM_EPI[epi], rstd, residual, ws, tk, q8, qs, qr, eps):
+        E.quant_fp8_rows(out, q8, qs, qr, eps)  # (no split-K reduce to fold it into)
+    _QHAND.update(key=_qkey(out), eps=eps, n=_QHAND["n"] + 1)
     return out
 
 
@@ -466,6 +526,7 @@ SKINNY_MAX_M = 16
 STREAM_MAX_M = max(16, min(64, int(os.environ.get("VWA_STREAM_MAX_M", "16"))))
 
 
+@_qhand_guard
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, out: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, act: str = "none", fuse_rms: bool = False, eps: float = 1e-5,
            out_dtype: Optional[torch.dtype] = None, ln_c: Optional[torch.Tensor] = None,
@@ -552,6 +613,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return out
 
 
+@_qhand_guard
 def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False, eps: float = 1e-5,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
     M = x.shape[0]
@@ -602,10 +664,7 @@ def _gemm_qkv(x, w, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, rope, 
     tk = gemm_tickets(x.device)
     common = (n_q_heads, n_kv_heads, head_dim, rope is not None, positions, slots, rope, q_out, k_cache, v_cache)
     if isinstance(w, FP8Weight):
-        x8 = scratch(x.device, "gemm_x8", M * K, torch.uint8).view(torch.float8_e4m3fn).view(M, K)
-        sx = scratch(x.device, "gemm_sx", M)
-        rstd = scratch(x.device, "gemm_rstd", M) if fuse_rms else None
-        E.quant_fp8_rows(x, x8, sx, rstd, eps)
+        x8, sx, rstd = _fp8_input(x, fuse_rms, eps)
         E.gemm_qkv(x8, sx, w.w8, w.scale, bias, rstd, True, ws, tk, *common)
         return
     rstd = None
@@ -792,13 +851,14 @@ def decode_attention(q: torch.Tensor, kv: KVLayout, ctx_lens: torch.Tensor, seq_
                      n_q_heads: int, n_kv_heads: int, head_dim: int, scale: float, max_ctx: int,
                      out: torch.Tensor, part_o: Optional[torch.Tensor] = None,
                      part_ml: Optional[torch.Tensor] = None, counters: Optional[torch.Tensor] = None,
-                     shared: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     shared: Optional[torch.Tensor] = None, n_splits: Optional[int] = None) -> torch.Tensor:
     """One query row per token; ``max_ctx`` bounds every row's context (fixes the grid, so the
     launch is graph-capturable while contexts grow).  ``shared``: int32 [P, n_real] on the device
     (the step buffers' shared-prefix words, runtime/engine.py): the first P keys of rows
     0 .. n_real-1 are the same physical K/V blocks (the cached prompt every session shares), so the
-    multi-query kernel reads them once per group of rows across sessions."""
-    n_splits = decode_n_splits(max_ctx)
+    multi-query kernel reads them once per group of rows across sessions.  ``n_splits`` (tuning
+    probes): cap on the key chunks (partial slots) per row group, default max_ctx / 128."""
+    n_splits = min(n_splits or 1 << 30, decode_n_splits(max_ctx))
     if not _gpu(q):
         return ref.decode_attention(q, kv, ctx_lens, seq_ids, n_q_heads=n_q_heads, n_kv_heads=n_kv_heads,
                                     head_dim=head_dim, scale=scale, out=out)
