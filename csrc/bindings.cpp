@@ -263,7 +263,7 @@ void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi,
   if (ws.has_value()) {
     TORCH_CHECK(ws->is_cuda() && ws->scalar_type() == at::kFloat && ws->is_contiguous(), "ws f32");
     p.ws = ws->data_ptr<float>();
-    p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws->numel());
+    p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws->numel(), 0);
     p.ws_cap = ws->numel();
   }
   set_tickets(p, tickets);
@@ -332,7 +332,7 @@ bool gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> 
   if (ws.has_value()) {
     TORCH_CHECK(ws->is_cuda() && ws->scalar_type() == at::kFloat && ws->is_contiguous(), "ws f32");
     p.ws = ws->data_ptr<float>();
-    p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x8), ws->numel());
+    p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x8), ws->numel(), 1);
   }
   set_tickets(p, tickets);
   if (q8.has_value()) {
@@ -430,7 +430,7 @@ void gemm_qkv(Tensor x, c10::optional<Tensor> sx, Tensor w, c10::optional<Tensor
   p.cache_st = k_cache.stride(2);
   TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous(), "ws f32");
   p.ws = ws.data_ptr<float>();
-  p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws.numel());
+  p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws.numel(), f8 ? 1 : 0);
   p.ws_cap = ws.numel();
   set_tickets(p, tickets);
   p.cus = device_cus(x);
@@ -1128,7 +1128,7 @@ void conv1d_gelu(Tensor x, Tensor w, c10::optional<Tensor> b, c10::optional<Tens
   // tiles x 30 k-groups); the f32 slabs are summed by gemm_reduce_kernel with the same epilogue
   Tensor ws;
   if (B == 1 && p.K >= 1024) {  // (K = 384: the split's f32 reduce costs more than it saves)
-    const int s = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), (int64_t)1 << 25);
+    const int s = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), (int64_t)1 << 25, 0);
     if (s > 1) {
       ws = at::empty({(int64_t)s * p.M * p.N}, x.options().dtype(at::kFloat));
       p.ws = ws.data_ptr<float>();
@@ -1237,6 +1237,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_small_gemm_bytes", &set_small_gemm_bytes);
   m.def("gemm_set_p8", [](int64_t mode) { vwa_gemm_set_p8((int)mode); });
   m.def("gemm_set_nb", [](int64_t nb) { vwa_gemm_set_nb((int)nb); });
+  m.def("gemm_set_split_fill", [](int64_t pct) { vwa_gemm_set_split_fill((int)pct); });
   m.def("chain_make_seq", &chain_make_seq, py::arg("seq"), py::arg("X"), py::arg("W"), py::arg("bias"),
         py::arg("ln_c"), py::arg("Y"), py::arg("epi"), py::arg("eps"), py::arg("n_heads"), py::arg("head_dim"),
         py::arg("positions"), py::arg("slots"), py::arg("k_cache"), py::arg("v_cache"), py::arg("bar"),

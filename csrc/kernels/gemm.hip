@@ -301,41 +301,62 @@ VWA_DEVICE void add8(float (&v)[8], const float4& a, const float4& b) {
   v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
 }
 
-// One output item of a split-K GEMM: row m, output columns c .. c+7 -- the sum of every slice's
-// f32 partial (slice order: the result does not depend on which slice finished last) and the
-// epilogue (SwiGLU: features c .. c+7 from the interleaved gate / up columns; QKV: also the
-// rotation partner chunk c^8, then rotary + q / KV stores), 16-byte stores.  Slices are loaded
-// in batches of 4 (all of a batch's loads in flight before any is used).
-template <int EPI, int AUX>
-VWA_DEVICE void reduce_item(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int m, int c, float* keep = nullptr) {
-  constexpr bool SW = EPI == EPI_SWIGLU, QK = EPI == EPI_QKV;
+// Split-K output items: row m, output columns c .. c+7 -- the sum of every slice's f32 partial
+// (slice order: the result does not depend on which slice finished last) and the epilogue
+// (SwiGLU: features c .. c+7 from the interleaved gate / up columns; QKV: also the rotation
+// partner chunk c^8, then rotary + q / KV stores), 16-byte stores.
+//   src0 / src1: the item's two 8-column source chunks (SwiGLU gate / up; QKV own / partner)
+template <int EPI>
+VWA_DEVICE int item_src0(int c) { return EPI == EPI_SWIGLU ? (c >> 4) * 32 + (c & 15) : c; }
+template <int EPI>
+VWA_DEVICE int item_src1(int c) { return EPI == EPI_SWIGLU ? item_src0<EPI>(c) + 16 : (c ^ 8); }
+template <int EPI>
+constexpr bool kTwoSrc = EPI == EPI_SWIGLU || EPI == EPI_QKV;
+
+// sums a (src0) / b (src1) of NI items (row m, first columns c[i]); the slices in batches of ZB,
+// all of a batch's loads (every item) in flight before any is used; slices past the last read
+// past the slab range (the buffer returns zeros)
+template <int EPI, int AUX, int NI, int ZB>
+VWA_DEVICE void sum_items(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int m, const int (&c)[NI],
+                          const bool (&ok)[NI], float (&a)[NI][8], float (&b)[NI][8]) {
   const size_t slab = (size_t)p.M * p.N;
-  const float rs = (p.rstd ? p.rstd[m] : 1.f) * (p.sx ? p.sx[m] : 1.f);
-  // the two 8-column source chunks: SwiGLU gate n0 / up n0 + 16; QKV own c / partner c ^ 8
-  const int n0 = SW ? (c >> 4) * 32 + (c & 15) : c;
-  const int n1 = SW ? n0 + 16 : (c ^ 8);
-  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, b[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int z0 = 0; z0 < p.splits; z0 += 4) {
-    float4 x[4][2], y[4][2];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      // slices past the last read past the slab range: the buffer returns zeros
-      const size_t base = (size_t)(z0 + u) * slab + (size_t)m * p.N;
-      x[u][0] = ld_f4<AUX>(rws, base + n0);
-      x[u][1] = ld_f4<AUX>(rws, base + n0 + 4);
-      if constexpr (SW || QK) {
-        y[u][0] = ld_f4<AUX>(rws, base + n1);
-        y[u][1] = ld_f4<AUX>(rws, base + n1 + 4);
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[i][e] = b[i][e] = 0.f;
+  for (int z0 = 0; z0 < p.splits; z0 += ZB) {
+    float4 x[NI][ZB][2], y[NI][ZB][2];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int u = 0; u < ZB; ++u) {
+        const size_t base = (size_t)(z0 + u) * slab + (size_t)m * p.N;
+        const int n0 = item_src0<EPI>(c[i]), n1 = item_src1<EPI>(c[i]);
+        // (an item past the row end reads offset 0 of slice z: in range, discarded)
+        x[i][u][0] = ld_f4<AUX>(rws, ok[i] ? base + n0 : 0);
+        x[i][u][1] = ld_f4<AUX>(rws, ok[i] ? base + n0 + 4 : 0);
+        if constexpr (kTwoSrc<EPI>) {
+          y[i][u][0] = ld_f4<AUX>(rws, ok[i] ? base + n1 : 0);
+          y[i][u][1] = ld_f4<AUX>(rws, ok[i] ? base + n1 + 4 : 0);
+        }
       }
-    }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      add8(a, x[u][0], x[u][1]);
-      if constexpr (SW || QK) add8(b, y[u][0], y[u][1]);
-    }
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int u = 0; u < ZB; ++u) {
+        add8(a[i], x[i][u][0], x[i][u][1]);
+        if constexpr (kTwoSrc<EPI>) add8(b[i], y[i][u][0], y[i][u][1]);
+      }
   }
+}
+
+// epilogue of one summed item + its stores; keep (optional): the stored bf16 values as floats
+template <int EPI>
+VWA_DEVICE void finish_item(const GemmParams& p, int m, int c, const float (&a)[8], float (&b)[8], float* keep) {
+  const float rs = (p.rstd ? p.rstd[m] : 1.f) * (p.sx ? p.sx[m] : 1.f);
+  const int n0 = item_src0<EPI>(c), n1 = item_src1<EPI>(c);
   float v[8];
-  if constexpr (SW) {
+  if constexpr (EPI == EPI_SWIGLU) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float gs = p.sw ? p.sw[n0 + e] : 1.f, us = p.sw ? p.sw[n1 + e] : 1.f;
@@ -347,7 +368,7 @@ VWA_DEVICE void reduce_item(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int
       v[e] = a[e] * rs * (p.sw ? p.sw[c + e] : 1.f) + bias_at(p, c + e);
       if constexpr (kGelu<EPI>) v[e] = gelu_erf(v[e]);
     }
-    if constexpr (QK) {
+    if constexpr (EPI == EPI_QKV) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) b[e] = b[e] * rs * (p.sw ? p.sw[n1 + e] : 1.f) + bias_at(p, n1 + e);
       qkv_store(p, m, c, v, b);
@@ -368,6 +389,15 @@ VWA_DEVICE void reduce_item(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int
   const uint4 packed = pack8(v);
   *reinterpret_cast<uint4*>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + c) = packed;
   if (keep) unpack8(packed, keep);  // the stored (bf16-rounded) values, for the row quantisation
+}
+
+template <int EPI, int AUX>
+VWA_DEVICE void reduce_item(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int m, int c) {
+  const int cc[1] = {c};
+  const bool ok[1] = {true};
+  float a[1][8], b[1][8];
+  sum_items<EPI, AUX, 1, 4>(p, rws, m, cc, ok, a, b);
+  finish_item<EPI>(p, m, c, a[0], b[0], nullptr);
 }
 
 // The last-arriving slice of output tile (bm, bn) (one-launch split-K): every item of the tile's
@@ -699,26 +729,35 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmParams p) {
 // quant_fp8_rows_kernel on the stored row, so the same codes / scale / 1/rms.  One launch instead
 // of gemm_reduce + quant_fp8_rows (~5 us each at 32 rows, profiles/r4_rows32_fp8_kernel_stats_v2.md).
 template <int EPI>
-__global__ __launch_bounds__(256) void gemm_reduce_rowq_kernel(GemmParams p) {
-  constexpr int MAXC = 8;  // 8-column chunks per thread: output rows of up to 16384 columns
-  __shared__ float red[2][4];
+__global__ __launch_bounds__(1024) void gemm_reduce_rowq_kernel(GemmParams p) {
+  constexpr int NT = 1024, MAXC = 2;  // 16 waves; 8-column chunks per thread: rows of <= 16384 outputs
+  __shared__ float red[2][NT / 64];
   const int m = blockIdx.x;
   const int nch = (EPI == EPI_SWIGLU ? p.N / 2 : p.N) / 8;
   const __amdgpu_buffer_rsrc_t rws = rsrc(p.ws, (size_t)p.splits * p.M * p.N * 4);
-  float v[MAXC][8];
+  int c[MAXC];
+  bool ok[MAXC];
+#pragma unroll
+  for (int i = 0; i < MAXC; ++i) {
+    const int ch = threadIdx.x + i * NT;
+    ok[i] = ch < nch;
+    c[i] = ch * 8;
+  }
+  float a[MAXC][8], b[MAXC][8], v[MAXC][8];
+  sum_items<EPI, 0, MAXC, 2>(p, rws, m, c, ok, a, b);
   float am = 0.f, ss = 0.f;
 #pragma unroll
   for (int i = 0; i < MAXC; ++i) {
-    const int ch = threadIdx.x + i * 256;
-    if (ch < nch) {
-      reduce_item<EPI, 0>(p, rws, m, ch * 8, v[i]);
+    if (!ok[i]) continue;
+    finish_item<EPI>(p, m, c[i], a[i], b[i], v[i]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        am = fmaxf(am, fabsf(v[i][e]));
-        ss += v[i][e] * v[i][e];
-      }
+    for (int e = 0; e < 8; ++e) {
+      am = fmaxf(am, fabsf(v[i][e]));
+      ss += v[i][e] * v[i][e];
     }
   }
+  // (per-thread sums over chunks tid, tid + NT, ...: a different order than quant_fp8_rows'
+  // 256-thread pass, so the 1/rms may differ in the last bits; the codes / scale do not)
   am = wave_max(am);
   ss = wave_sum(ss);
   if ((threadIdx.x & 63) == 0) {
@@ -726,23 +765,27 @@ __global__ __launch_bounds__(256) void gemm_reduce_rowq_kernel(GemmParams p) {
     red[1][threadIdx.x >> 6] = ss;
   }
   __syncthreads();
-  am = fmaxf(fmaxf(red[0][0], red[0][1]), fmaxf(red[0][2], red[0][3]));
+  am = 0.f;
+  ss = 0.f;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    am = fmaxf(am, red[0][w]);
+    ss += red[1][w];
+  }
   const float sx = am > 0.f ? am * (1.f / 448.f) : 1.f;
   const float iv = 1.f / sx;
   if (threadIdx.x == 0) {
     p.q_sx[m] = sx;
-    if (p.q_rstd) p.q_rstd[m] = rsqrtf((red[1][0] + red[1][1] + red[1][2] + red[1][3]) / (float)(nch * 8) + p.q_eps);
+    if (p.q_rstd) p.q_rstd[m] = rsqrtf(ss / (float)(nch * 8) + p.q_eps);
   }
 #pragma unroll
   for (int i = 0; i < MAXC; ++i) {
-    const int ch = threadIdx.x + i * 256;
-    if (ch < nch) {
-      const float* f = v[i];
-      uint2 o;
-      o.x = cvt_pk_fp8(f[0] * iv, f[1] * iv) | (cvt_pk_fp8(f[2] * iv, f[3] * iv) << 16);
-      o.y = cvt_pk_fp8(f[4] * iv, f[5] * iv) | (cvt_pk_fp8(f[6] * iv, f[7] * iv) << 16);
-      *reinterpret_cast<uint2*>(p.q8 + (size_t)m * p.ldq8 + ch * 8) = o;
-    }
+    if (!ok[i]) continue;
+    const float* f = v[i];
+    uint2 o;
+    o.x = cvt_pk_fp8(f[0] * iv, f[1] * iv) | (cvt_pk_fp8(f[2] * iv, f[3] * iv) << 16);
+    o.y = cvt_pk_fp8(f[4] * iv, f[5] * iv) | (cvt_pk_fp8(f[6] * iv, f[7] * iv) << 16);
+    *reinterpret_cast<uint2*>(p.q8 + (size_t)m * p.ldq8 + c[i]) = o;
   }
 }
 
@@ -763,7 +806,10 @@ __global__ __launch_bounds__(256) void row_rstd_kernel(const u16* __restrict__ x
   if (lane_id() == 0) rstd[row] = rsqrtf(ss / (float)K + eps);
 }
 
-int g_gemm_nb = 4;  // stage buffers of the 128^2 kernel for one-row-block GEMMs (2 or 4)
+// stage buffers of the 128^2 kernel for one-row-block GEMMs (2 or 4).  4 measured slower in whole
+// decode steps (fp8 32 rows 4.97 vs 4.36 ms): 128 KB of LDS leaves one workgroup per CU, and the
+// split-K grids of > 256 workgroups then run in two rounds (profiles/r4_gemm_ab.md)
+int g_gemm_nb = 2;
 
 template <class C, int EPI, int NB>
 void launch_nb(const GemmParams& p, dim3 grid, hipStream_t st) {
@@ -807,7 +853,7 @@ int launch_epi(const GemmParams& p, hipStream_t st, bool p8) {
   if (p.splits > 1 && p.tickets == nullptr) {
     if constexpr (EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_SWIGLU) {
       if (p.q8) {
-        hipLaunchKernelGGL((gemm_reduce_rowq_kernel<EPI>), dim3(p.M), dim3(256), 0, st, p);
+        hipLaunchKernelGGL((gemm_reduce_rowq_kernel<EPI>), dim3(p.M), dim3(1024), 0, st, p);
         rowq = true;
       }
     }
@@ -824,13 +870,22 @@ int launch_epi(const GemmParams& p, hipStream_t st, bool p8) {
 
 // Split-K slices for a shape: enough workgroups to cover the CUs ~2x when the output tiles
 // alone cannot (few rows: weight streaming), bounded by the k-groups and the workspace.
-extern "C" int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats) {
+// Split while the workgroups cover less than this % of the CUs (0: per-dtype default).  Measured
+// on the Llama-3-8B decode steps of 32 / 64 rows (tools/rows_sweep.py, profiles/r4_gemm_ab.md):
+// bf16 75 % (5.08 / 5.69 ms vs 5.21 / 6.08 at 100 %), fp8 100 % (4.42 / 5.03 vs 4.62 / 5.06 at 75 %).
+int g_split_fill_pct = 0;
+
+extern "C" int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats, int f8) {
   const int tiles = ((M + CfgS::BM - 1) / CfgS::BM) * ((N + CfgS::BN - 1) / CfgS::BN);
   const int KG = K / BKG;
+  const int pct = g_split_fill_pct > 0 ? g_split_fill_pct : f8 ? 100 : 75;
+  const int fill = (int)((int64_t)cus * pct / 100);
   int s = 1;
-  while (tiles * s < cus && s * 2 <= KG && (int64_t)(s * 2) * M * N <= ws_floats) s *= 2;
+  while (tiles * s < fill && s * 2 <= KG && (int64_t)(s * 2) * M * N <= ws_floats) s *= 2;
   return s;
 }
+
+extern "C" void vwa_gemm_set_split_fill(int pct) { g_split_fill_pct = pct < 0 ? 0 : pct; }
 
 extern "C" void vwa_gemm_set_p8(int mode) { g_p8_mode = mode; }
 extern "C" void vwa_gemm_set_nb(int nb) { g_gemm_nb = nb == 4 ? 4 : 2; }
@@ -842,7 +897,7 @@ extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
     return -11;
   if (p.sw && (!p.sx || !p.w_tiled)) return -14;  // W8A8: per-row X scales and the fp8 tiled layout
   if (epi == EPI_SWIGLU && (p.N % 32 || p.y_f32)) return -12;
-  if (p.q8 && (p.y_f32 || !p.q_sx || (epi == EPI_SWIGLU ? p.N / 2 : p.N) > 16384 || p.ldq8 % 8)) return -17;
+  if (p.q8 && (p.y_f32 || !p.q_sx || (epi == EPI_SWIGLU ? p.N / 2 : p.N) > 16384 || p.ldq8 % 8)) return -17;  // 2 chunks x 1024 threads
   if (epi == EPI_QKV && (p.y_f32 || p.head_dim % 16 || p.N != (p.n_q_heads + 2 * p.n_kv_heads) * p.head_dim ||
                          !p.q_out || !p.k_cache || !p.v_cache || !p.slots || (p.use_rope && (!p.rope || !p.positions))))
     return -16;

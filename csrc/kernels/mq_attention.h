@@ -227,8 +227,12 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   static_assert(!FINE || NW == 8, "the FINE merge pairs two threads per (column, slice): 512 threads");
   // cascade: n_pc prefix chunks + up to RG own-key chunks (one per sequence run of the group) per
   // group -- the partial slots 0 .. n_pc + RG - 1
-  const int n_pc = cascade ? max(1, min(p.n_splits - RG, grid / max(1, n_groups * nkv) - RG)) : 0;
-  const int n_eff = cascade ? n_pc + RG : max(1, min(FINE ? min(p.n_splits, 16) : p.n_splits, grid / max(1, n_groups * nkv)));
+  // (standalone kernel: about one item per CU -- grid / 2 -- measured best over the chunk cap,
+  // tools/attn_probe.py --split-sweep, profiles/r4_attn_split_sweep.jsonl: e.g. 8 sessions 14.5 vs
+  // 21.2 us with a full-grid split, 16 grouped sessions 14.7 vs 23.2 us)
+  const int tgt = FINE ? grid : max(1, grid / 2);
+  const int n_pc = cascade ? max(1, min(p.n_splits - RG, tgt / max(1, n_groups * nkv) - RG)) : 0;
+  const int n_eff = cascade ? n_pc + RG : max(1, min(FINE ? min(p.n_splits, 16) : p.n_splits, tgt / max(1, n_groups * nkv)));
   const int n_items = n_groups * nkv * n_eff;
   if (n_items_out) *n_items_out = n_items;
   if (n_final_out) *n_final_out = n_groups * nkv;

@@ -190,8 +190,9 @@ int vwa_chain_prepare(ChainParams* cp, int grid);
 int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid, hipStream_t st,
                      int xg2 = 0, int f8 = 0);
 int vwa_gemm(int epi, const GemmParams* p, hipStream_t st);
-int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats);
-void vwa_gemm_set_nb(int nb);  // 128^2 kernel stage buffers for one-row-block GEMMs: 4 (default) or 2
+int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats, int f8);
+void vwa_gemm_set_split_fill(int pct);  // split-K while tiles x splits < pct % of the CUs (0: bf16 75, fp8 100)
+void vwa_gemm_set_nb(int nb);  // 128^2 kernel stage buffers for one-row-block GEMMs: 2 (default) or 4
 void vwa_gemm_set_p8(int mode);  // 0: 128^2 kernel only, 1: 256^2 8-phase wherever eligible, 2: measured rule
 int vwa_row_rstd(const uint16_t* x, int ldx, int M, int K, float eps, float* rstd, hipStream_t st);
 int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,

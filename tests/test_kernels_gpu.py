@@ -1009,10 +1009,11 @@ def test_decode_attention_shared_prefix(hd, nq, nkv, n_sess, P):
 
 
 @pytest.mark.parametrize("M", [17, 40, 64])
-def test_fp8_row_quant_handoff(M):
+def test_fp8_row_quant_handoff(M, monkeypatch):
     """W8A8 GEMM chain of a Llama layer at > 16 rows (o_proj -> gate/up -> down -> next QKV): with
     the row-quantisation hand-off each split-K reduce quantises its output for the next GEMM
-    (no quant_fp8_rows launches in between) -- bit-identical to quantising every input."""
+    (no quant_fp8_rows launches in between) -- the same as quantising every input (the fused
+    1/rms sums in another order: last-bit differences only)."""
     d, F, nq, nkv, hd = 1024, 2048, 8, 2, 128
     W = dict(o=rnd(d, nq * hd, scale=0.03), gu=ops.interleave_gate_up(rnd(F, d, scale=0.03), rnd(F, d, scale=0.03)),
              down=rnd(d, F, scale=0.02), qkv=ops.permute_qkv_rows(rnd((nq + 2 * nkv) * hd, d, scale=0.03),
@@ -1024,6 +1025,7 @@ def test_fp8_row_quant_handoff(M):
     slots = torch.arange(M, dtype=torch.int64, device=DEV)
 
     def layer(on):
+        monkeypatch.setenv("VWA_ROWQ_HANDOFF", "1" if on else "0")
         ops.row_quant_handoff(on)
         try:
             h = h0.clone()
@@ -1042,4 +1044,5 @@ def test_fp8_row_quant_handoff(M):
 
     with_h, without = layer(True), layer(False)
     for a, b in zip(with_h, without):
-        assert torch.equal(a, b)
+        close(a, b, 2e-2, 2e-2)
+    assert torch.equal(with_h[0], without[0])  # o_proj output: no 1/rms involved yet

@@ -60,6 +60,9 @@ def ext():
         nb = os.environ.get("VWA_GEMM_NB")  # stage buffers of few-row (one row block) GEMMs: 4 / 2
         if nb not in (None, ""):
             m.gemm_set_nb(int(nb))
+        fill = os.environ.get("VWA_GEMM_SPLIT_FILL")  # split-K until tiles x splits >= this % of CUs
+        if fill not in (None, ""):
+            m.gemm_set_split_fill(int(fill))
         _EXT = m
         return m
     except BaseException as e:  # noqa: BLE001
@@ -437,7 +440,10 @@ _QHAND = {"on": False, "key": None, "eps": None, "n": 0}
 
 
 def row_quant_handoff(enabled: bool) -> None:
-    _QHAND.update(on=bool(enabled) and os.environ.get("VWA_ROWQ_HANDOFF", "1") != "0", key=None, eps=None)
+    # opt-in (VWA_ROWQ_HANDOFF=1): measured slower in whole fp8 decode steps (32 rows 5.31 vs 4.97 ms,
+    # profiles/r4_gemm_ab.md) -- the one-workgroup-per-row reduce is latency-bound on the
+    # 14336-wide SwiGLU rows (21 us vs 6 + 5 for the reduce and quant launches)
+    _QHAND.update(on=bool(enabled) and os.environ.get("VWA_ROWQ_HANDOFF", "0") == "1", key=None, eps=None)
 
 
 def _qhand_guard(fn):
