@@ -1,0 +1,7 @@
+set -e
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u tools/rows_sweep.py --rows 24,32,48,64 --no-prefill-bench --dtype fp8 --json gpurun_out/rows_w_fp8.jsonl > gpurun_out/rows_w.log 2>&1
+timeout -k 10 500 python -u bench.py --dtype fp8 --concurrent 32 --steps 10 --warmup 3 > gpurun_out/bench_w_c32.log 2>&1
+timeout -k 10 500 python -u bench.py --concurrent 8 --steps 10 --warmup 3 > gpurun_out/bench_w_c8.log 2>&1

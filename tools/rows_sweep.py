@@ -71,7 +71,7 @@ def main():
     # ---- decode step vs rows
     seqs = [e.new_sequence(head + s) for s in suf]
     e.prefill_batch([(s, len(s.tokens)) for s in seqs])
-    e.capture_all(buckets=tuple(b for b in (1, 2, 4, 8, 16, 32, 64) if b <= R), logit_buckets=())
+    e.capture_all(buckets=tuple(b for b in (1, 2, 4, 8, 16, 32, 48, 64) if b <= R), logit_buckets=())
     for M in rows_list:
         rows = lambda: [(seqs[i], 7) for i in range(M)]  # noqa: E731
         for _ in range(3):

@@ -30,7 +30,11 @@ import torch
 from .. import ops
 from .kv_cache import BlockManager, PagedKVCache
 
-BUCKETS = (1, 2, 4, 8, 16, 32, 64)
+# Row buckets of the captured step graphs.  48 between the powers of two: a 44-row step of 32
+# concurrent sessions (+ jump-forward rows) pays for 48 rows, not 64 -- fp8 4.71 vs 5.05 ms, 32
+# sessions p50 447 vs 459 ms (attention, LM head and the GEMMs' rows scale with the bucket).  (24
+# measured the same as 32: the one 128-row GEMM tile and the attention floor dominate there.)
+BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64)
 
 
 class TPGroupFailure(RuntimeError):
