@@ -589,3 +589,43 @@ def test_fp8_chained_layer_is_w8a16(cfg, monkeypatch):
     for a, b in zip(got, ref):
         err = (a - b).abs().max().item()
         assert err < 0.02 * (1 + b.abs().max().item()), err
+
+
+@pytest.mark.parametrize("flash", ["1", "0"])
+def test_batched_admission_prefill_gpu(flash, monkeypatch):
+    """GPU batched admission prefill (runtime/engine.py prefill_batch, > 64 ragged rows): the
+    per-request runs' causal attention as ONE batched flash launch per layer (VWA_PREFILL_FLASH=1,
+    the default) or the decode kernel over 64-row slices -- the same K/V, hence the same next-token
+    logits, as one prefill per request."""
+    import voice_enabled_browser_automation_amd.runtime.engine as eng_mod
+
+    monkeypatch.setattr(eng_mod, "PREFILL_FLASH", flash == "1")
+    torch.manual_seed(0)
+    m = LlamaModel(CFG, device="cuda", seed=3)
+    head = torch.randint(0, 4096, (200,)).tolist()
+    tails = [torch.randint(0, 4096, (n,)).tolist() for n in (40, 33, 27, 85, 60)]
+
+    def make():
+        e = LLMEngine(m, max_seqs=6, max_model_len=512, kv_blocks=200, block_size=16)
+        s0 = e.new_sequence(head)
+        e.prefill(s0)
+        e.free_sequence(s0)
+        return e, [e.new_sequence(head + t) for t in tails]
+
+    def next_logits(e, seqs):
+        return [e.run_rows([(s, 7)]).float().clone() for s in seqs]
+
+    eA, sA = make()
+    for s in sA:
+        eA.prefill(s)
+    want = next_logits(eA, sA)
+    eB, sB = make()
+    calls = []
+    orig = ops.flash_attention_runs
+    monkeypatch.setattr(ops, "flash_attention_runs", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    eB.prefill_batch([(s, len(s.tokens)) for s in sB])  # 245 suffix rows behind the cached head
+    assert bool(calls) == (flash == "1")
+    got = next_logits(eB, sB)
+    for a, b in zip(got, want):
+        assert torch.isfinite(a).all()
+        assert torch.allclose(a, b, atol=3e-2, rtol=3e-2), (a - b).abs().max()

@@ -378,10 +378,16 @@ class LlamaModel:
                 # (ragged rows: a decode step, or the batched admission prefill of several requests'
                 # prompt suffixes -- runtime/engine.py prefill_batch -- in 64-row attention slices)
                 attn = bufs.attn[:M]
-                ops.decode_attention_rows(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens, bufs.seq_ids,
-                                     n_q_heads=self.nq, n_kv_heads=self.nkv, head_dim=self.hd, scale=self.scale,
-                                     max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o, part_ml=bufs.part_ml,
-                                     counters=bufs.attn_cnt, shared=getattr(bufs, "shared", None))
+                fl = getattr(bufs, "flash", None)
+                if fl is not None:  # whole per-request runs (batched admission prefill)
+                    ops.flash_attention_runs(q, kc, vc, fl, n_q_heads=self.nq, n_kv_heads=self.nkv,
+                                             head_dim=self.hd, scale=self.scale, out=attn)
+                else:
+                    ops.decode_attention_rows(q, ops.KVLayout.paged(kc, vc, bufs.block_table), bufs.ctx_lens,
+                                              bufs.seq_ids, n_q_heads=self.nq, n_kv_heads=self.nkv, head_dim=self.hd,
+                                              scale=self.scale, max_ctx=bufs.max_ctx, out=attn, part_o=bufs.part_o,
+                                              part_ml=bufs.part_ml, counters=bufs.attn_cnt,
+                                              shared=getattr(bufs, "shared", None))
             elif pf_slices is not None:
                 attn = pf_out
                 lay = ops.KVLayout.paged(kc, vc, bufs.block_table)

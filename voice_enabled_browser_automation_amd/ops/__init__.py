@@ -896,6 +896,22 @@ def decode_attention_rows(q: torch.Tensor, kv: KVLayout, ctx_lens: torch.Tensor,
     return out
 
 
+def flash_attention_runs(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, runs, *, n_q_heads: int,
+                         n_kv_heads: int, head_dim: int, scale: float, out: torch.Tensor) -> torch.Tensor:
+    """Causal attention of ragged rows that are whole per-sequence runs (runtime/engine.py
+    _ragged_flash: B runs of <= S consecutive positions, run b at absolute offset q_offsets[b] over
+    its own block-table row): scattered into a [B, S] query block, one batched flash-attention
+    launch, gathered back.  The padding queries of short runs compute rows nobody reads."""
+    B, S, hq = runs.B, runs.S, n_q_heads * head_dim
+    qp = scratch(q.device, "runs_q", B * S * hq, q.dtype).view(B * S, hq)
+    op = scratch(q.device, "runs_o", B * S * hq, q.dtype).view(B * S, hq)
+    qp.index_copy_(0, runs.dst, q)
+    flash_attention(qp.view(B, S, n_q_heads, head_dim), KVLayout.paged(k_cache, v_cache, runs.table), Sk=runs.max_k,
+                    n_kv_heads=n_kv_heads, causal=True, scale=scale, out=op.view(B, S, n_q_heads, head_dim),
+                    k_lens=runs.k_lens, q_offsets=runs.q_offsets)
+    return torch.index_select(op, 0, runs.dst, out=out)
+
+
 def flash_attention(q: torch.Tensor, kv: KVLayout, *, Sk: int, n_kv_heads: int, causal: bool, scale: float,
                     q_offset: int = 0, out: Optional[torch.Tensor] = None,
                     k_lens: Optional[torch.Tensor] = None, q_offsets: Optional[torch.Tensor] = None) -> torch.Tensor:

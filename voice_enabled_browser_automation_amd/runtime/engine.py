@@ -56,6 +56,9 @@ _SEQ_UIDS = itertools.count()
 # blocks) once per group of rows across sessions (attention.hip / mq_attention.h cascade);
 # VWA_SHARED_ATTN=0: once per session
 SHARED_ATTN = os.environ.get("VWA_SHARED_ATTN", "1") != "0"
+# Batched admission prefill: causal flash attention over [requests x longest suffix] instead of the
+# decode-attention kernel in 64-row slices (VWA_PREFILL_FLASH=0: slices)
+PREFILL_FLASH = os.environ.get("VWA_PREFILL_FLASH", "1") != "0"
 
 
 @dataclass
@@ -607,10 +610,37 @@ class LLMEngine:
             attn=torch.empty(n, m.nq * m.hd, dtype=m.dtype, device=dev),
             act=torch.empty(n, getattr(m, "F", getattr(m.cfg, "ffn", d)), dtype=m.dtype, device=dev),
             part_o=self.bufs.part_o, part_ml=self.bufs.part_ml, attn_cnt=self.bufs.attn_cnt,
-            logits_local=self.bufs.logits_local, logits=self.bufs.logits)
+            logits_local=self.bufs.logits_local, logits=self.bufs.logits,
+            flash=self._ragged_flash(sids, poss) if dev.type == "cuda" else None)
         m.forward(scratch, n, self.kv, head=False)
         for sid, ln in pending.items():
             self.seqs[sid].n_computed = ln
+
+    def _ragged_flash(self, sids: List[int], poss: List[int]) -> Optional[SimpleNamespace]:
+        """Ragged rows made of whole per-sequence runs (consecutive positions, one run per
+        sequence -- the batched admission prefill): the batched causal flash attention layout for
+        them ([B runs, S = longest run] queries at absolute offsets, each run's own block-table row)
+        -- one launch per layer instead of the decode kernel over 64-row slices."""
+        if not PREFILL_FLASH:
+            return None
+        runs: List[List[int]] = []  # [sid, first row, rows, first position]
+        for i, (sid, pos) in enumerate(zip(sids, poss)):
+            if runs and runs[-1][0] == sid and pos == poss[i - 1] + 1:
+                runs[-1][2] += 1
+            else:
+                runs.append([sid, i, 1, pos])
+        if len(runs) < 2 or len({r[0] for r in runs}) != len(runs):
+            return None
+        B, S = len(runs), max(r[2] for r in runs)
+        dst = torch.empty(len(sids), dtype=torch.int64)
+        for b, (_, i0, cnt, _) in enumerate(runs):
+            dst[i0 : i0 + cnt] = torch.arange(b * S, b * S + cnt)
+        dev = self.device
+        meta = torch.tensor([[r[3] for r in runs], [r[3] + r[2] for r in runs], [r[0] for r in runs]],
+                            dtype=torch.int32).pin_memory().to(dev, non_blocking=True)
+        return SimpleNamespace(B=B, S=S, dst=dst.pin_memory().to(dev, non_blocking=True), q_offsets=meta[0],
+                               k_lens=meta[1], table=self.bufs.block_table.index_select(0, meta[2]),
+                               max_k=max(r[3] + r[2] for r in runs))
 
     def prefill(self, seq: Sequence_, chunk: int = 2048, upto: Optional[int] = None) -> Optional[torch.Tensor]:
         """Compute K/V for seq.tokens[n_computed:upto] (default: all tokens); returns f32 logits
