@@ -69,11 +69,14 @@ def run_concurrent(args, C, asr, brain, utterances, asr_tokens, world):
     """C voice sessions arriving together on every rank: one batched ASR pass, then all C intent
     parses decoded with continuous batching.  Per-session latency = ASR batch + that session's
     parse completion.  Not part of the headline value."""
+    asr_ms = []
+
     def round_(k):
         pcms = [utterances[(k * C + j) % len(utterances)] for j in range(C)]
         t0 = time.perf_counter()
         texts = asr.transcribe_many([asr.pcm_to_audio(p) for p in pcms], exact_tokens=asr_tokens)
         t_asr = (time.perf_counter() - t0) * 1e3
+        asr_ms.append(t_asr)
         reqs = [{"text": t if t.strip() else COMMANDS[j % len(COMMANDS)], "context": {"url": "https://www.bestbuy.com"}}
                 for j, t in enumerate(texts)]
         outs = brain.parse_many(reqs)
@@ -87,6 +90,8 @@ def run_concurrent(args, C, asr, brain, utterances, asr_tokens, world):
     t0 = time.perf_counter()
     lat, ok = [], 0
     it0 = dict(brain.batch_stats)
+    tm0 = dict(getattr(brain, "timing", {}))
+    asr_ms.clear()
     for k in range(args.steps):
         l, o = round_(k + 1)
         lat += l
@@ -107,7 +112,13 @@ def run_concurrent(args, C, asr, brain, utterances, asr_tokens, world):
             "throughput_utt_per_s": round(len(all_lat) / (el_max / 1e3), 3),
             "valid_intents": f"{sum(int(a[1]) for a in allt)}/{len(all_lat)}",
             "rows_per_iteration": round(bs["rows"] / max(1, bs["iterations"]), 2),
-            "samples_per_iteration": round(bs["sampled"] / max(1, bs["iterations"]), 2)}
+            "samples_per_iteration": round(bs["sampled"] / max(1, bs["iterations"]), 2),
+            "iterations_per_round": round(bs["iterations"] / max(1, args.steps), 1),
+            "asr_batch_ms_mean": round(statistics.mean(asr_ms), 2) if asr_ms else None,
+            # per scheduler iteration, host-side clock (ms): launch of the step, grammar masks
+            # (overlapping the GPU), head + sampler launch, waiting for the tokens, accept / jump-forward
+            "iteration_ms": {k: round((v - tm0.get(k, 0.0)) / max(1, bs["iterations"]), 3)
+                             for k, v in getattr(brain, "timing", {}).items()}}
 
 
 def _free_port() -> int:

@@ -131,7 +131,8 @@ class LLMIntentEngine:
         self.last_batch: List[Dict[str, Any]] = []
         self.batch_stats = dict(iterations=0, rows=0, sampled=0, max_active=0)
         # host-side time per scheduler phase (where a decode step's wall time goes)
-        self.timing = dict(build_launch_ms=0.0, mask_ms=0.0, sample_launch_ms=0.0, gpu_wait_ms=0.0, post_ms=0.0)
+        self.timing = dict(build_launch_ms=0.0, mask_ms=0.0, sample_launch_ms=0.0, gpu_wait_ms=0.0, post_ms=0.0,
+                           admit_prefill_ms=0.0)
         self._prefix_ids: Dict[str, List[int]] = {}
         self._head_len = 0
         self.waiting: Deque[IntentRequest] = deque()
@@ -236,8 +237,10 @@ class LLMIntentEngine:
         if admitted:
             # ONE batched prefill of every admitted request's prompt suffix (all but its last
             # token, which joins the decode step below)
+            ta = time.perf_counter()
             try:
                 self.engine.prefill_batch([(r.seq, len(r.ids) - 1) for r in admitted])
+                self.timing["admit_prefill_ms"] += (time.perf_counter() - ta) * 1e3
             except Exception as e:  # noqa: BLE001
                 if getattr(getattr(self.engine.model, "tp", None), "size", 1) > 1:
                     raise  # TP: lockstep is lost -- brain/tp_engine.py ends the group
