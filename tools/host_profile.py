@@ -22,22 +22,33 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--llm", default="llama3-8b")
     ap.add_argument("--n", type=int, default=6)
+    ap.add_argument("--concurrent", type=int, default=0, help="profile rounds of C requests decoded together")
     a = ap.parse_args()
     ops.ext()
     m = LlamaModel(get_config(a.llm), device="cuda", seed=2)
-    eng = LLMEngine(m, max_seqs=4, max_model_len=2048)
+    eng = LLMEngine(m, max_seqs=max(4, a.concurrent), max_model_len=2048)
     brain = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=512, temperature=0.1, seed=1234)
     eng.capture_all()
     for i in range(2):
         brain.parse({"text": COMMANDS[i], "context": {"url": "https://www.bestbuy.com"}})
     torch.cuda.synchronize()
+    reqs = [{"text": COMMANDS[i % len(COMMANDS)], "context": {"url": "https://www.bestbuy.com"}}
+            for i in range(max(1, a.concurrent))]
+    if a.concurrent:
+        brain.parse_many(reqs)
     pr = cProfile.Profile()
     pr.enable()
     for i in range(a.n):
-        brain.parse({"text": COMMANDS[i % len(COMMANDS)], "context": {"url": "https://www.bestbuy.com"}})
+        if a.concurrent:
+            brain.parse_many(reqs)
+        else:
+            brain.parse(reqs[i % len(reqs)])
     pr.disable()
+    it = brain.batch_stats["iterations"]
+    print("iterations", it, "timing_ms", {k: round(v, 1) for k, v in brain.timing.items()})
     st = pstats.Stats(pr)
-    st.sort_stats("tottime").print_stats(30)
+    st.sort_stats("tottime").print_stats(40)
+    st.sort_stats("cumulative").print_stats(40)
 
 
 if __name__ == "__main__":

@@ -78,15 +78,19 @@ def main():
             e.run_rows(rows(), check=False)
         torch.cuda.synchronize()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        ts = []
+        ts, hs = [], []
         for _ in range(a.iters):
+            rr = rows()
             ev[0].record()
-            e.run_rows(rows(), check=False, defer_head=True)
+            h0 = time.perf_counter()
+            e.run_rows(rr, check=False, defer_head=True)
+            hs.append((time.perf_counter() - h0) * 1e6)
             ev[1].record()
             torch.cuda.synchronize()
             e.host_synced()
             ts.append(ev[0].elapsed_time(ev[1]))
         fwd = sorted(ts)[len(ts) // 2]
+        host_us = sorted(hs)[len(hs) // 2]  # CPU time of building + launching the step
         ts = []
         for _ in range(a.iters):
             ev[0].record()
@@ -97,7 +101,7 @@ def main():
             ts.append(ev[0].elapsed_time(ev[1]))
         full = sorted(ts)[len(ts) // 2]
         emit({"what": "decode_step", "model": a.model, "dtype": a.dtype, "rows": M, "chained": m._chain_ok(M),
-              "layers_ms": round(fwd, 3), "with_lm_head_ms": round(full, 3),
+              "layers_ms": round(fwd, 3), "with_lm_head_ms": round(full, 3), "host_launch_us": round(host_us, 1),
               "weight_GB": round(m.weight_bytes() / 1e9, 2), "ctx": len(seqs[0].tokens)})
     if a.json:
         with open(a.json, "a") as f:
