@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import voice_enabled_browser_automation_amd.ops as ops  # noqa: E402
 from voice_enabled_browser_automation_amd.models.config import get_config  # noqa: E402
 from voice_enabled_browser_automation_amd.models.llama import LlamaModel  # noqa: E402
-from voice_enabled_browser_automation_amd.runtime.engine import LLMEngine  # noqa: E402
+from voice_enabled_browser_automation_amd.runtime.engine import BUCKETS, LLMEngine  # noqa: E402
 
 
 def main():
@@ -71,7 +71,7 @@ def main():
     # ---- decode step vs rows
     seqs = [e.new_sequence(head + s) for s in suf]
     e.prefill_batch([(s, len(s.tokens)) for s in seqs])
-    e.capture_all(buckets=tuple(b for b in (1, 2, 4, 8, 16, 32, 48, 64) if b <= R), logit_buckets=())
+    e.capture_all(buckets=tuple(b for b in BUCKETS if b <= R), logit_buckets=())
     for M in rows_list:
         rows = lambda: [(seqs[i], 7) for i in range(M)]  # noqa: E731
         for _ in range(3):

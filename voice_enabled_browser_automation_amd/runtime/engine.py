@@ -30,11 +30,13 @@ import torch
 from .. import ops
 from .kv_cache import BlockManager, PagedKVCache
 
-# Row buckets of the captured step graphs.  48 between the powers of two: a 44-row step of 32
-# concurrent sessions (+ jump-forward rows) pays for 48 rows, not 64 -- fp8 4.71 vs 5.05 ms, 32
-# sessions p50 447 vs 459 ms (attention, LM head and the GEMMs' rows scale with the bucket).  (24
-# measured the same as 32: the one 128-row GEMM tile and the attention floor dominate there.)
-BUCKETS = (1, 2, 4, 8, 16, 32, 48, 64)
+# Row buckets of the captured step graphs (VWA_ROW_BUCKETS overrides).  48 between the powers of
+# two: a 44-row step of 32 concurrent sessions (+ jump-forward rows) pays for 48 rows, not 64 --
+# fp8 4.71 vs 5.05 ms, 32 sessions p50 447 vs 459 ms.  12: the 8-session steps (~13 rows) -- the
+# streaming GEMMs' X staging makes 8..16-row steps cost ~72 us per row (8: 4.04, 12: 4.36, 16:
+# 4.61 ms bf16, profiles/r4_rows_buckets_8_16.jsonl).  (24 measured the same as 32: the one
+# 128-row GEMM tile and the attention floor dominate there.)
+BUCKETS = tuple(int(b) for b in os.environ.get("VWA_ROW_BUCKETS", "1,2,4,8,12,16,32,48,64").split(","))
 
 
 class TPGroupFailure(RuntimeError):
