@@ -410,6 +410,10 @@ int launch_v(const SkinnyParams& p, hipStream_t st, int grid_cap, size_t lds, in
   return 0;
 }
 
+// Rows from which the <= 16-row streaming GEMM streams X fragments with the weights (XG) instead
+// of staging all of X in LDS (99: never; tuning knob, vwa_skinny_set_xg_rows)
+int g_xg_rows = 99;
+
 template <int EPI, int NT, int KS>
 int launch(const SkinnyParams& p0, hipStream_t st, int grid_cap) {
   SkinnyParams p = p0;
@@ -429,7 +433,7 @@ int launch(const SkinnyParams& p0, hipStream_t st, int grid_cap) {
   }
   const size_t xbytes = ((size_t)p.M * xstride * 2 + 15) & ~(size_t)15;
   const size_t red = (size_t)(KS * NT * 4 * 64 + 32) * sizeof(float);  // + row scales + row means
-  const bool lds_x = xbytes + red <= 160 * 1024;
+  const bool lds_x = xbytes + red <= 160 * 1024 && (p.M < g_xg_rows || p.fuse_rms == 2 || p.col_mask);
   if (p.col_mask) {  // the masked tile list: NT 1, EPI store, LDS-staged X, <= 64 tiles per workgroup
     const int ntiles = p.N / (16 * NT), grid = ntiles < grid_cap ? ntiles : grid_cap;
     if (EPI != EPI_STORE || NT != 1 || !lds_x || (ntiles + grid - 1) / grid > 64 || p.col_mask_rows < 1)
@@ -1630,6 +1634,8 @@ int dispatch_ks(int epi, const SkinnyParams& p, int grid_cap, hipStream_t st) {
 
 // Returns -10 when this shape does not fit the streaming kernel (caller falls back).
 // ks = waves per workgroup splitting K (4 or 8); grid_cap = max persistent workgroups.
+extern "C" void vwa_skinny_set_xg_rows(int rows) { g_xg_rows = rows; }
+
 extern "C" int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st) {
   if (p->M < 1 || p->M > 64 || p->K % 128 != 0) return -10;
   if ((size_t)p->N * p->K * (p->w_scale ? 1 : 2) >= 0x7FFFFFF0ull) return -10;

@@ -187,8 +187,8 @@ def test_plan_gpus_maps_through_the_parent_mask():
     assert plan_gpus(4, 2, parent_visible="") == {"brain": ["0", "1"], "voice": ["2", "3"], "shared": False}
     p = plan_gpus(1, 1, parent_visible="6")
     assert p == {"brain": ["6"], "voice": ["6"], "shared": True}
-    assert shared_gpu_env({})["VWA_CHAIN"] == "1"
-    assert shared_gpu_env({"VWA_SHARED_CHAIN": "0"})["VWA_CHAIN"] == "0"
+    assert shared_gpu_env({})["VWA_CHAIN"] == "0"
+    assert shared_gpu_env({"VWA_SHARED_CHAIN": "1"})["VWA_CHAIN"] == "1"
 
 
 def test_brain_health_reports_a_failed_tp_group():

@@ -222,6 +222,9 @@ async def run_matrix(a) -> list:
                             eng = bm.get("engine", {})
                             rec["brain_chain_fallbacks"] = eng.get("chain_fallbacks", 0)
                             rec["brain_rows_per_iteration"] = eng.get("rows_per_iteration")
+                            rec["brain_chained_steps"] = eng.get("chained_steps", 0)
+                            rec["brain_steps"] = eng.get("steps", 0)
+                            rec["brain_host_ms"] = eng.get("host_ms")
                             print(json.dumps(rec), flush=True)
                             results.append(rec)
                     finally:

@@ -8,8 +8,8 @@ GPU placement on one node (plan_gpus): the brain (LLM) takes GPUs 0..TP-1 and th
 (ASR) every remaining GPU, one voice worker per GPU behind the session router (session DP);
 VWA_BRAIN_GPUS / VWA_VOICE_GPUS (comma lists) override.  With VWA_TP>1 the brain is launched
 through torch.distributed.run with one process per GPU.  When only one GPU is visible the two
-share it (shared_gpu_env: the chained decode launch stays on, bounded waits + fallback).  The
-brain is restartable: a TP group that loses lockstep exits and is started again in fresh
+share it (shared_gpu_env: per-kernel decode launches beside the ASR -- measured faster than the
+chained launch there).  The brain is restartable: a TP group that loses lockstep exits and is started again in fresh
 processes while the other services keep serving (Supervisor).
 """
 from __future__ import annotations
@@ -132,12 +132,14 @@ def _parent_visible() -> str:
 
 
 def shared_gpu_env(env) -> dict:
-    """Brain settings when it shares its GPU with a voice worker.  The chained decode launch stays
-    on: its persistent workgroups wait (bounded) for the ASR's short kernels to drain from the CUs
-    they need, and a launch that still times out falls back to per-kernel launches and is re-armed
-    after a backoff (runtime/engine.py).  VWA_SHARED_CHAIN=0 restores the per-kernel brain;
-    VWA_SHARED_CHAIN_GRID_DIV=k gives the chain CUs/k workgroups."""
-    out = {"VWA_CHAIN": env.get("VWA_CHAIN", env.get("VWA_SHARED_CHAIN", "1")),
+    """Brain settings when it shares its GPU with a voice worker.  Per-kernel decode launches by
+    default: under live streaming-ASR load the chained launch's persistent workgroups wait for the
+    ASR kernels to drain from their CUs, and the step measured 3.72-3.76 ms of GPU wait vs
+    3.61-3.62 ms per-kernel (tools/service_bench.py, two alternating runs each,
+    profiles/r4_service_chain_ab.jsonl; a first round-4 run had measured the chain ahead).
+    VWA_SHARED_CHAIN=1 keeps the chain (bounded waits, fallback + re-arm in runtime/engine.py);
+    VWA_SHARED_CHAIN_GRID_DIV=k gives it CUs/k workgroups."""
+    out = {"VWA_CHAIN": env.get("VWA_CHAIN", env.get("VWA_SHARED_CHAIN", "0")),
            # HBM the voice worker's ASR keeps (the brain's auto KV sizing leaves it free)
            "VWA_SHARED_GB": env.get("VWA_SHARED_GB", "24")}
     div = env.get("VWA_SHARED_CHAIN_GRID_DIV")

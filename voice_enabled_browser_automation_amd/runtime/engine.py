@@ -392,6 +392,8 @@ class LLMEngine:
         if rtab is not None and not self.use_graphs:
             b.row_table[:M].copy_(b.h_row_table[:M], non_blocking=True)
         chained = self._uses_chain(M)
+        if chained:
+            self.stats["chained_steps"] = self.stats.get("chained_steps", 0) + 1
         self._last_step = (list(rows), logits_for, {sid: self.seqs[sid].n_computed for sid in pending}) \
             if chained else None
         if self.use_graphs:
