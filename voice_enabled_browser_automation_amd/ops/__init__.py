@@ -497,7 +497,9 @@ def gemm_fp8(x: torch.Tensor, w: "FP8Weight", out: torch.Tensor, *, epi: str = "
     x8, sx, rstd = _fp8_input(x, fuse_rms, eps)
     ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
     tk = gemm_tickets(x.device)
-    if not _QHAND["on"] or out.dtype != torch.bfloat16:
+    # (residual epilogues only: the 4096-wide residual rows reduce + quantise in one pass faster than
+    # the two launches; the 14336-wide SwiGLU rows do not -- profiles/r4_gemm_ab.md)
+    if not _QHAND["on"] or out.dtype != torch.bfloat16 or epi != "resid":
         E.gemm_fp8(x8, sx, w.w8, w.scale, bias, out, _GEMM_EPI[epi], rstd, residual, ws, tk)
         return out
     n_out = out.shape[1]
