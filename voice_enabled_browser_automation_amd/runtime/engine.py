@@ -636,6 +636,8 @@ class LLMEngine:
         if len(runs) < 2 or len({r[0] for r in runs}) != len(runs):
             return None
         B, S = len(runs), max(r[2] for r in runs)
+        if B * S > 2 * len(sids):  # one long run among short ones: mostly padding queries -- slices
+            return None
         dst = torch.empty(len(sids), dtype=torch.int64)
         for b, (_, i0, cnt, _) in enumerate(runs):
             dst[i0 : i0 + cnt] = torch.arange(b * S, b * S + cnt)
