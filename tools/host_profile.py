@@ -48,6 +48,7 @@ def main():
     print("iterations", it, "timing_ms", {k: round(v, 1) for k, v in brain.timing.items()})
     st = pstats.Stats(pr)
     st.sort_stats("tottime").print_stats(40)
+    st.print_callees("run_rows")
     st.sort_stats("cumulative").print_stats(40)
 
 

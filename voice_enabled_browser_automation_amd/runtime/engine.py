@@ -126,6 +126,12 @@ class StepBuffers:
         self.h_slots = self.h_meta[4 * R : 6 * R].view(torch.int64)
         self.h_sel = self.h_meta[6 * R : 7 * R]
         self.np_shared = self.h_meta[7 * R : 7 * R + 2].numpy()
+        # rows whose hidden state feeds the LM head when the step computed every row (L == M):
+        # gathered on the device through a pinned staging copy (a torch.tensor(list, device=...)
+        # here was a pageable, host-blocking copy that waited for the whole step -- measured: 9 of
+        # 172 iterations at 32 sessions stalled ~4.6 ms each)
+        self.h_head_idx = torch.zeros(R, dtype=torch.int64, pin_memory=pin)
+        self.head_idx = torch.zeros(R, dtype=torch.int64, device=device)
         self.row_table = self.meta_all[T:].view(R, C)
         self.h_row_table = self.h_meta_all[T:].view(R, C)
         self.np_row_table = self.h_row_table.numpy()
@@ -415,7 +421,13 @@ class LLMEngine:
             if self.model.chain_error():
                 self._head_rows = None
                 return self.recover_step()
-        self._head_rows = hs[torch.tensor(logits_for, device=hs.device)] if L == M and nl != n else hs[:nl]
+        if L == M and nl != n:
+            b.h_head_idx[:nl] = torch.as_tensor(logits_for, dtype=torch.int64)
+            idx = b.head_idx[:nl]
+            idx.copy_(b.h_head_idx[:nl], non_blocking=hs.device.type == "cuda")
+            self._head_rows = hs.index_select(0, idx)
+        else:
+            self._head_rows = hs[:nl]
         if defer_head:
             return None
         return self.head_logits()
