@@ -7,6 +7,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 import torch
 
@@ -24,9 +25,30 @@ def main():
     ap.add_argument("--asr", default="whisper-tiny")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tokens", type=int, default=40)
+    ap.add_argument("--batch", default="", help="also time transcribe_many over B utterances (comma list)")
     a = ap.parse_args()
     ops.ext()
     m = WhisperModel(get_config(a.asr), device="cuda", seed=0)
+    if a.batch:  # concurrent sessions' batched pass (bench.py --concurrent: one per round)
+        sizes = [int(x) for x in a.batch.split(",")]
+        eng = AsrEngine(m, load_tokenizer("whisper"), max_sessions=max(sizes))
+        for B in sizes:
+            audios = [eng.pcm_to_audio(synth_speech(10.0, seed=100 + j)) for j in range(B)]
+            for _ in range(2):
+                eng.transcribe_many(audios, exact_tokens=a.tokens)
+            ts, enc, dec = [], [], []
+            for _ in range(a.reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                eng.transcribe_many(audios, exact_tokens=a.tokens)
+                ts.append((time.perf_counter() - t0) * 1e3)
+                s = getattr(eng, "last_stats", {}) or {}
+                enc.append(s.get("encode_ms", 0.0))
+                dec.append(s.get("decode_ms", 0.0))
+            print(json.dumps(dict(tool="asr_timing", asr=a.asr, batch=B, tokens=a.tokens,
+                                  total_ms=round(statistics.median(ts), 2), encode_ms=round(statistics.median(enc), 2),
+                                  decode_ms=round(statistics.median(dec), 2))), flush=True)
+        return
     audio = None
     texts = {}
     for chain in ("0", "1"):
