@@ -558,7 +558,8 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                                        c10::optional<Tensor> a_part_ml, c10::optional<Tensor> a_counters,
                                        bool w_tiled, c10::optional<Tensor> a_row_table,
                                        c10::optional<Tensor> s_o, c10::optional<Tensor> s_gu,
-                                       c10::optional<Tensor> s_down, c10::optional<Tensor> s_qkv, int64_t tp_ar) {
+                                       c10::optional<Tensor> s_down, c10::optional<Tensor> s_qkv, int64_t tp_ar,
+                                       int64_t tail_n) {
   c10::DeviceGuard g(h.device());
   const int64_t M = h.size(0);
   TORCH_CHECK(att.size(0) == M && act.size(0) == M, "row counts differ");
@@ -589,6 +590,11 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   cp.n = 3;
   cp.seq = 0;
   chain_schedule(cp);
+  // tail_n == 2: o_proj -> gate/up only (5..16 rows: both X row blocks fit LDS; the down
+  // projection, whose 14336-wide X does not, stays a streaming launch)
+  TORCH_CHECK(tail_n == 0 || (tail_n == 2 && !w_qkv.has_value() && !tp_ar && !s_o.has_value()),
+              "chain tail_n: 0 or 2 (bf16, no QKV, no TP)");
+  if (tail_n == 2) cp.n = 2;
   if (w_qkv.has_value()) {
     TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
                     v_cache.has_value(),
@@ -1233,7 +1239,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_n_splits") = 0, py::arg("a_part_o") = py::none(), py::arg("a_part_ml") = py::none(),
         py::arg("a_counters") = py::none(), py::arg("w_tiled") = false, py::arg("a_row_table") = py::none(),
         py::arg("s_o") = py::none(), py::arg("s_gu") = py::none(), py::arg("s_down") = py::none(),
-        py::arg("s_qkv") = py::none(), py::arg("tp_ar") = 0);
+        py::arg("s_qkv") = py::none(), py::arg("tp_ar") = 0, py::arg("tail_n") = 0);
   m.def("set_small_gemm_bytes", &set_small_gemm_bytes);
   m.def("gemm_set_p8", [](int64_t mode) { vwa_gemm_set_p8((int)mode); });
   m.def("gemm_set_nb", [](int64_t nb) { vwa_gemm_set_nb((int)nb); });

@@ -1471,7 +1471,8 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
   static const int kSeq[3][kChainMaxPhases] = {{EPI_RESID, EPI_SWIGLU, EPI_RESID, EPI_QKV},
                                                {EPI_RESID, EPI_GELU, EPI_RESID, EPI_QKV},
                                                {EPI_RESID, EPI_STORE, -1, -1}};
-  if (cp->seq < 0 || cp->seq > 2 || (cp->seq == 2 ? cp->n != 2 : cp->n < 3)) return -10;
+  if (cp->seq < 0 || cp->seq > 2 || (cp->seq == 2 ? cp->n != 2 : cp->n < (cp->seq == 0 ? 2 : 3))) return -10;
+  if (cp->seq == 0 && cp->n == 2 && (cp->attn_g || cp->tp.world > 1)) return -10;  // o -> gate/up only: no attention, no TP
   size_t lds = 0;
   for (int i = 0; i < cp->n; ++i) {
     ChainPhase& ph = cp->ph[i];
@@ -1584,7 +1585,10 @@ extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, 
     return (int)hipGetLastError();
   }
 #undef VWA_CHAIN_LAUNCH_F8
-  if (seq == 0) {
+  if (seq == 0 && n_phases == 2) {  // o_proj -> gate/up (5..16 rows, no attention phase)
+    if (attn_g) return -10;
+    VWA_CHAIN_LAUNCH(0, 2, 0);
+  } else if (seq == 0) {
     if (n_phases != 3 && n_phases != 4) return -10;
     const bool q = n_phases == 4;
     switch (attn_g) {

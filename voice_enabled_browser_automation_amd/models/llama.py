@@ -225,6 +225,37 @@ class LlamaModel:
                 and self.device.type == "cuda" and not getattr(self, "_chain_disabled", False)
                 and ops.env_flag("VWA_CHAIN", True) and ops.native_available())
 
+    def _chain2_ok(self, M: int) -> bool:
+        """5..16 rows (VWA_CHAIN2=1): o_proj -> gate/up as ONE chained launch (both X row blocks fit
+        LDS), attention / down / QKV as their own launches (skinny_stream.hip chain_kernel NPH 2)."""
+        return (5 <= M <= 16 and self.tp.size == 1 and self.wdtype == "bf16" and self.device.type == "cuda"
+                and isinstance(self.layers[0].o, ops.TiledWeight) and not getattr(self, "_chain_disabled", False)
+                and ops.env_flag("VWA_CHAIN", True) and ops.env_flag("VWA_CHAIN2", False) and ops.native_available())
+
+    def _chain_any(self, M: int) -> bool:
+        """Whether a step of M rows runs a chained launch (either form): the engine then checks the
+        launch's barrier error word and re-runs a timed-out step on the per-kernel path."""
+        return self._chain_ok(M) or self._chain2_ok(M)
+
+    def _chain2_desc(self, bufs, M: int, li: int):
+        """(descriptor, lds) of layer li's chained o_proj -> gate/up for this engine's buffers (None if
+        the shapes do not fit), cached like _chain_desc."""
+        if not isinstance(getattr(self, "_chains", None), weakref.WeakKeyDictionary):
+            self.reset_chains()
+        cache = self._chains.setdefault(bufs, {})
+        key = ("c2", M, li)
+        if key in cache:
+            return cache[key]
+        if getattr(self, "_chain_bar", None) is None:
+            self._chain_bar, self._chain_bar_mode, self._chain_work = ops.chain_buffers(self.device)
+        L = self.layers[li]
+        desc, lds = ops.ext().chain_make(
+            bufs.hidden[:M], bufs.attn[:M], bufs.act[:M], L.o.t, L.gu.t, L.down.t, self.cfg.rms_eps, None, self.nq,
+            self.nkv, self.hd, None, None, None, None, None, None, self._chain_bar, self._chain_work, None,
+            self._chain_bar_mode, w_tiled=True, tail_n=2)
+        cache[key] = (desc, lds) if desc.numel() else None
+        return cache[key]
+
     def disable_chain(self) -> None:
         self._chain_disabled = True
         self.reset_chains()
@@ -403,9 +434,15 @@ class LlamaModel:
                 ops.flash_attention(q4, ops.KVLayout.paged(kc, vc, table), Sk=q_offset + M, n_kv_heads=self.nkv,
                                     causal=True, scale=self.scale, q_offset=q_offset, out=attn4)
                 attn = attn4.view(M, self.nq * self.hd)
-            self._row_parallel(attn, L.o, h)
-            act = bufs.act[:M] if M <= bufs.act.shape[0] else None
-            act = ops.linear_swiglu(h, L.gu, fuse_rms=True, eps=cfg.rms_eps, out=act)
+            # (the chained o_proj reads bufs.attn: the decode-attention output of the step buffers)
+            d2 = self._chain2_desc(bufs, M, li) if prefill_seq is None and self._chain2_ok(M) else None
+            if d2 is not None:  # chained o_proj -> gate/up (5..16 rows)
+                ops.ext().chain_run(d2[0], 2, d2[1], h)
+                act = bufs.act[:M]
+            else:
+                self._row_parallel(attn, L.o, h)
+                act = bufs.act[:M] if M <= bufs.act.shape[0] else None
+                act = ops.linear_swiglu(h, L.gu, fuse_rms=True, eps=cfg.rms_eps, out=act)
             self._row_parallel(act, L.down, h)
         ops.row_quant_handoff(False)
         if n_sel is not None:

@@ -460,7 +460,7 @@ class LLMEngine:
         return ops.sample(logits, **kw)
 
     def _uses_chain(self, M: int) -> bool:
-        ok = getattr(self.model, "_chain_ok", None)
+        ok = getattr(self.model, "_chain_any", None) or getattr(self.model, "_chain_ok", None)
         return bool(ok is not None and ok(M))
 
     def step_fail_word(self) -> Optional[torch.Tensor]:
