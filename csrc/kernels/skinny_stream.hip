@@ -398,6 +398,11 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
   }
 }
 
+// One workgroup per tile when the tiles exceed the cap by at most 2x and two workgroups fit a CU's
+// LDS (VWA_SKINNY_GRID_ADAPT=1): no second, serial tile for a quarter of the workgroups (e.g.
+// Whisper-large-v3's fc1, 320 tiles; Llama's QKV, 384)
+int g_grid_adapt = 0;
+
 template <int EPI, int NT, int KS, bool XG, int MT = 1>
 int launch_v(const SkinnyParams& p, hipStream_t st, int grid_cap, size_t lds, int xstride) {
   constexpr int U = MT > 1 ? 1 : XG ? 2 : 4 / NT;
@@ -405,7 +410,8 @@ int launch_v(const SkinnyParams& p, hipStream_t st, int grid_cap, size_t lds, in
   const int per_wave = (G + KS - 1) / KS;
   const int nb = (per_wave + U - 1) / U;
   const int ntiles = p.N / (16 * NT);
-  const int grid = ntiles < grid_cap ? ntiles : grid_cap;
+  int grid = ntiles < grid_cap ? ntiles : grid_cap;
+  if (g_grid_adapt && ntiles > grid_cap && ntiles <= 2 * grid_cap && 2 * lds <= 160 * 1024 && !p.col_mask) grid = ntiles;
   hipLaunchKernelGGL((skinny_stream_kernel<EPI, NT, KS, XG, MT>), dim3(grid), dim3(KS * 64), lds, st, p, nb, xstride);
   return 0;
 }
@@ -594,7 +600,8 @@ int launch_fp8(const SkinnyParams& p, hipStream_t st, int grid_cap) {
   const size_t lds = xbytes + (size_t)(KS * NT * 4 * 64 + 32) * sizeof(float);
   if (lds > 160 * 1024) return -10;
   const int ntiles = p.N / (16 * NT);
-  const int grid = ntiles < grid_cap ? ntiles : grid_cap;
+  int grid = ntiles < grid_cap ? ntiles : grid_cap;
+  if (g_grid_adapt && ntiles > grid_cap && ntiles <= 2 * grid_cap && 2 * lds <= 160 * 1024) grid = ntiles;
   hipLaunchKernelGGL((skinny_fp8_kernel<EPI, NT, KS>), dim3(grid), dim3(KS * 64), lds, st, p, nb, xstride);
   return 0;
 }
@@ -1639,6 +1646,7 @@ int dispatch_ks(int epi, const SkinnyParams& p, int grid_cap, hipStream_t st) {
 // Returns -10 when this shape does not fit the streaming kernel (caller falls back).
 // ks = waves per workgroup splitting K (4 or 8); grid_cap = max persistent workgroups.
 extern "C" void vwa_skinny_set_xg_rows(int rows) { g_xg_rows = rows; }
+extern "C" void vwa_skinny_set_grid_adapt(int on) { g_grid_adapt = on; }
 
 extern "C" int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st) {
   if (p->M < 1 || p->M > 64 || p->K % 128 != 0) return -10;

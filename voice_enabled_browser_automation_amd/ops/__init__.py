@@ -60,6 +60,9 @@ def ext():
         nb = os.environ.get("VWA_GEMM_NB")  # stage buffers of few-row (one row block) GEMMs: 4 / 2
         if nb not in (None, ""):
             m.gemm_set_nb(int(nb))
+        ga = os.environ.get("VWA_SKINNY_GRID_ADAPT")  # one workgroup per tile up to 2x the grid cap
+        if ga not in (None, ""):
+            m.skinny_set_grid_adapt(int(ga))
         xg = os.environ.get("VWA_SKINNY_XG_ROWS")  # <= 16-row streaming GEMM: X streamed from this many rows
         if xg not in (None, ""):
             m.skinny_set_xg_rows(int(xg))
