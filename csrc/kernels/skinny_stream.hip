@@ -1620,9 +1620,38 @@ extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, 
 namespace {
 }  // namespace
 
+// Plain epilogues (store / residual / GELU) of >= g_nt2_rows rows (<= 16, no grammar mask): two
+// adjacent 16-column tiles per workgroup tile, so every X fragment read from LDS (or streamed,
+// XG) feeds two MFMAs -- half the X traffic per weight byte, half the tiles.  99: never (tuning
+// knob, vwa_skinny_set_nt2_rows).
+int g_nt2_rows = 99;
+
+template <int KS>
+bool use_nt2(int epi, const SkinnyParams& p) {
+  if (p.M < g_nt2_rows || p.M > 16 || p.N % 32 != 0 || p.col_mask) return false;
+  if (epi != EPI_STORE && epi != EPI_RESID && epi != EPI_GELU) return false;
+  if (p.w_scale)  // the fp8 kernel stages X in LDS: the NT 2 reduction buffer must fit beside it
+    return ((size_t)p.M * (p.K + 16) + 15) / 16 * 16 + (size_t)(KS * 2 * 4 * 64 + 32) * 4 <= 160 * 1024;
+  return true;
+}
+
 // Returns -10 when this shape does not fit the streaming kernel (caller falls back).
 template <int KS>
 int dispatch_ks(int epi, const SkinnyParams& p, int grid_cap, hipStream_t st) {
+  if (use_nt2<KS>(epi, p)) {
+    if (p.w_scale) {
+      switch (epi) {
+        case EPI_STORE: return launch_fp8<EPI_STORE, 2, KS>(p, st, grid_cap);
+        case EPI_RESID: return launch_fp8<EPI_RESID, 2, KS>(p, st, grid_cap);
+        default: return launch_fp8<EPI_GELU, 2, KS>(p, st, grid_cap);
+      }
+    }
+    switch (epi) {
+      case EPI_STORE: return launch<EPI_STORE, 2, KS>(p, st, grid_cap);
+      case EPI_RESID: return launch<EPI_RESID, 2, KS>(p, st, grid_cap);
+      default: return launch<EPI_GELU, 2, KS>(p, st, grid_cap);
+    }
+  }
   if (p.w_scale) {
     switch (epi) {
       case EPI_STORE: return launch_fp8<EPI_STORE, 1, KS>(p, st, grid_cap);
@@ -1647,6 +1676,7 @@ int dispatch_ks(int epi, const SkinnyParams& p, int grid_cap, hipStream_t st) {
 // ks = waves per workgroup splitting K (4 or 8); grid_cap = max persistent workgroups.
 extern "C" void vwa_skinny_set_xg_rows(int rows) { g_xg_rows = rows; }
 extern "C" void vwa_skinny_set_grid_adapt(int on) { g_grid_adapt = on; }
+extern "C" void vwa_skinny_set_nt2_rows(int rows) { g_nt2_rows = rows; }
 
 extern "C" int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st) {
   if (p->M < 1 || p->M > 64 || p->K % 128 != 0) return -10;

@@ -1046,3 +1046,48 @@ def test_fp8_row_quant_handoff(M, monkeypatch):
     for a, b in zip(with_h, without):
         close(a, b, 2e-2, 2e-2)
     assert torch.equal(with_h[0], without[0])  # o_proj output: no 1/rms involved yet
+
+
+@pytest.mark.parametrize("M", [5, 8, 16])
+def test_skinny_nt2_tiles_match_reference(M):
+    """Two 16-column tiles per workgroup tile for the plain epilogues (skinny_stream.hip use_nt2,
+    VWA_SKINNY_NT2_ROWS): bf16 tiled weights with X in LDS (K 4096) and streamed (K 14336, XG),
+    fp8 tiled weights (W8A8), store + fused RMSNorm, residual and GELU, against the fp32 CPU
+    reference; the NT 2 launch is checked to differ from no launch at all by comparing with NT 1."""
+    m = ops.ext()
+    K, N = 4096, 1024
+    x, xd = rnd(M, K), rnd(M, 14336)
+    w, wd = rnd(N, K, scale=0.02), rnd(512, 14336, scale=0.01)
+    wq = ops.FP8Weight.quantize(rnd(N, K, scale=K ** -0.5), tiled=True)
+    wc = ops.FP8Weight(wq.rows().cpu(), wq.scale.cpu())
+    res, resd = rnd(M, N), rnd(M, 512)
+    results = {}
+    try:
+        for nt2 in (99, 1):
+            m.skinny_set_nt2_rows(nt2)
+            a = torch.empty(M, N, dtype=torch.float32, device=DEV)
+            ops.linear(x, ops.TiledWeight(w), out=a, fuse_rms=True)
+            b = resd.clone()
+            ops.linear(xd, ops.TiledWeight(wd), out=b, residual=b)
+            c = ops.linear(x, ops.TiledWeight(w), act="gelu")
+            d = res.clone()
+            ops.linear(x, wq, out=d, residual=d)
+            torch.cuda.synchronize()
+            results[nt2] = (a, b, c, d)
+    finally:
+        m.skinny_set_nt2_rows(99)
+    xc, xdc = x.cpu().float(), xd.cpu().float()
+    xn = xc * torch.rsqrt(xc.pow(2).mean(-1, keepdim=True) + 1e-5)
+    exp_a = xn @ w.cpu().float().t()
+    exp_b = resd.cpu().float() + xdc @ wd.cpu().float().t()
+    exp_c = torch.nn.functional.gelu(xc @ w.cpu().float().t())
+    exp_d = ops.linear(x.cpu(), wc, residual=res.cpu())
+    for nt2 in (99, 1):
+        a, b, c, d = results[nt2]
+        close(a, exp_a, 1e-2, 1e-2)
+        close(b, exp_b, 3e-2, 3e-2)
+        close(c, exp_c, 2e-2, 2e-2)
+        close(d, exp_d, 3e-2, 3e-2)
+    # same summation order per column (the K split over waves is unchanged): identical results
+    for u, v in zip(results[99], results[1]):
+        assert torch.equal(u, v)

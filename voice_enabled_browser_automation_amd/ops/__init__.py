@@ -63,6 +63,9 @@ def ext():
         ga = os.environ.get("VWA_SKINNY_GRID_ADAPT")  # one workgroup per tile up to 2x the grid cap
         if ga not in (None, ""):
             m.skinny_set_grid_adapt(int(ga))
+        nt2 = os.environ.get("VWA_SKINNY_NT2_ROWS")  # store/resid/GELU GEMMs: 32-column tiles from this many rows
+        if nt2 not in (None, ""):
+            m.skinny_set_nt2_rows(int(nt2))
         xg = os.environ.get("VWA_SKINNY_XG_ROWS")  # <= 16-row streaming GEMM: X streamed from this many rows
         if xg not in (None, ""):
             m.skinny_set_xg_rows(int(xg))
