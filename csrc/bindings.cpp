@@ -1246,6 +1246,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("skinny_set_xg_rows", [](int64_t rows) { vwa_skinny_set_xg_rows((int)rows); });
   m.def("skinny_set_grid_adapt", [](int64_t on) { vwa_skinny_set_grid_adapt((int)on); });
   m.def("skinny_set_nt2_rows", [](int64_t rows) { vwa_skinny_set_nt2_rows((int)rows); });
+  m.def("skinny_set_x_skew", [](int64_t skew) { vwa_skinny_set_x_skew((int)skew); });
   m.def("gemm_set_split_fill", [](int64_t pct) { vwa_gemm_set_split_fill((int)pct); });
   m.def("chain_make_seq", &chain_make_seq, py::arg("seq"), py::arg("X"), py::arg("W"), py::arg("bias"),
         py::arg("ln_c"), py::arg("Y"), py::arg("epi"), py::arg("eps"), py::arg("n_heads"), py::arg("head_dim"),

@@ -215,15 +215,20 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
 // X row fragments, so a step of up to 64 rows streams the weights ONCE in one persistent launch
 // with the fused epilogues (instead of split-K GEMM launches + reduce + epilogue kernels).
 template <int EPI, int NT, int KS, bool XG, int MT = 1>
-__global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, int nb, int xstride) {
+__global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, int nb, int xstride, int xskew) {
   // k-groups (128 wide) per item; MT > 1: one (the X fragments of MT row tiles share the
   // register budget of the item's weights)
   constexpr int U = MT > 1 ? 1 : XG ? 2 : 4 / NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int M = p.M, K = p.K, N = p.N;
   u16* xs = reinterpret_cast<u16*>(smem);
-  const int xbytes = XG ? 0 : ((M * xstride * 2) + 15) & ~15;
+  // LDS-staged X: row m at m * xstride + (m / 4) * xskew elements.  xstride = K + 8 puts row m+1
+  // one 16-B bank slot after row m; the extra 64-B skew every 4 rows (xskew 32) makes each
+  // ds_read_b128 lane group ({0-3,12-15,20-27}, ...: rows nl, k-quarters g) hit 16 distinct slots
+  // -- without it lanes (nl, g) and (nl + 4, g - 1)... share slots, a 2-way conflict on every read.
+  const int xbytes = XG ? 0 : ((M * xstride * 2) + 4 * xskew * 2 + 15) & ~15;
   float* red = reinterpret_cast<float*>(smem + xbytes);  // [KS][NT][MT][4][64]
+  auto xrow = [&](int m) { return m * xstride + (m >> 2) * xskew; };
   float* rs = red + KS * NT * MT * 4 * 64;                // [16 MT] row scales (1/rms, LayerNorm rstd)
   float* mu = rs + 16 * MT;                               // [16 MT] row means (folded LayerNorm)
   const float* mus = (p.fuse_rms == 2) ? mu : nullptr;
@@ -317,7 +322,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
           uint4 a = make_uint4(0, 0, 0, 0);
           if constexpr (XG) a = xr[mt][u][s];
           else if (16 * mt + nl < M)
-            a = *reinterpret_cast<const uint4*>(xs + (16 * mt + nl) * xstride + kg * 128 + 32 * g + 8 * s);
+            a = *reinterpret_cast<const uint4*>(xs + xrow(16 * mt + nl) + kg * 128 + 32 * g + 8 * s);
 #pragma unroll
           for (int nt = 0; nt < NT; ++nt)
             acc[nt * MT + mt] = mfma16(as_bf16x8(a), as_bf16x8(wr[nt][u][s]), acc[nt * MT + mt]);
@@ -343,7 +348,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
   if constexpr (!XG) {
     for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
       const int m = c / k8, kk = c % k8;
-      *reinterpret_cast<uint4*>(xs + m * xstride + kk * 8) =
+      *reinterpret_cast<uint4*>(xs + xrow(m) + kk * 8) =
           *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8);
     }
   }
@@ -355,7 +360,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
       for (int kk = lane; kk < k8; kk += 64) {
         float f[8];
         unpack8(XG ? *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8)
-                   : *reinterpret_cast<const uint4*>(xs + m * xstride + kk * 8), f);
+                   : *reinterpret_cast<const uint4*>(xs + xrow(m) + kk * 8), f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           s += f[j] * f[j];
@@ -402,6 +407,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
 // LDS (VWA_SKINNY_GRID_ADAPT=1): no second, serial tile for a quarter of the workgroups (e.g.
 // Whisper-large-v3's fc1, 320 tiles; Llama's QKV, 384)
 int g_grid_adapt = 0;
+int g_x_skew = 32;  // LDS X row skew (elements per 4 rows; 0: none -- A/B knob, vwa_skinny_set_x_skew)
 
 template <int EPI, int NT, int KS, bool XG, int MT = 1>
 int launch_v(const SkinnyParams& p, hipStream_t st, int grid_cap, size_t lds, int xstride) {
@@ -412,7 +418,8 @@ int launch_v(const SkinnyParams& p, hipStream_t st, int grid_cap, size_t lds, in
   const int ntiles = p.N / (16 * NT);
   int grid = ntiles < grid_cap ? ntiles : grid_cap;
   if (g_grid_adapt && ntiles > grid_cap && ntiles <= 2 * grid_cap && 2 * lds <= 160 * 1024 && !p.col_mask) grid = ntiles;
-  hipLaunchKernelGGL((skinny_stream_kernel<EPI, NT, KS, XG, MT>), dim3(grid), dim3(KS * 64), lds, st, p, nb, xstride);
+  hipLaunchKernelGGL((skinny_stream_kernel<EPI, NT, KS, XG, MT>), dim3(grid), dim3(KS * 64), lds, st, p, nb, xstride,
+                     XG ? 0 : g_x_skew);
   return 0;
 }
 
@@ -437,7 +444,7 @@ int launch(const SkinnyParams& p0, hipStream_t st, int grid_cap) {
       return -10;
     }
   }
-  const size_t xbytes = ((size_t)p.M * xstride * 2 + 15) & ~(size_t)15;
+  const size_t xbytes = ((size_t)p.M * xstride * 2 + 4 * g_x_skew * 2 + 15) & ~(size_t)15;
   const size_t red = (size_t)(KS * NT * 4 * 64 + 32) * sizeof(float);  // + row scales + row means
   const bool lds_x = xbytes + red <= 160 * 1024 && (p.M < g_xg_rows || p.fuse_rms == 2 || p.col_mask);
   if (p.col_mask) {  // the masked tile list: NT 1, EPI store, LDS-staged X, <= 64 tiles per workgroup
@@ -1677,6 +1684,7 @@ int dispatch_ks(int epi, const SkinnyParams& p, int grid_cap, hipStream_t st) {
 extern "C" void vwa_skinny_set_xg_rows(int rows) { g_xg_rows = rows; }
 extern "C" void vwa_skinny_set_grid_adapt(int on) { g_grid_adapt = on; }
 extern "C" void vwa_skinny_set_nt2_rows(int rows) { g_nt2_rows = rows; }
+extern "C" void vwa_skinny_set_x_skew(int skew) { g_x_skew = skew == 0 ? 0 : 32; }
 
 extern "C" int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st) {
   if (p->M < 1 || p->M > 64 || p->K % 128 != 0) return -10;

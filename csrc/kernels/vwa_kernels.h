@@ -188,6 +188,7 @@ int vwa_skinny_gemm(int epi, const SkinnyParams* p, hipStream_t st);
 int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st);
 void vwa_skinny_set_xg_rows(int rows);  // X streamed with the weights from this many rows (99: never)
 void vwa_skinny_set_grid_adapt(int on);  // one workgroup per tile up to 2x the grid cap (LDS permitting)
+void vwa_skinny_set_x_skew(int skew);  // LDS-staged X rows: 64-B skew every 4 rows (default) or none (0)
 void vwa_skinny_set_nt2_rows(int rows);  // two 16-column tiles per workgroup tile from this many rows (99: never)
 int vwa_chain_prepare(ChainParams* cp, int grid);
 int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid, hipStream_t st,

@@ -66,6 +66,9 @@ def ext():
         nt2 = os.environ.get("VWA_SKINNY_NT2_ROWS")  # store/resid/GELU GEMMs: 32-column tiles from this many rows
         if nt2 not in (None, ""):
             m.skinny_set_nt2_rows(int(nt2))
+        xsk = os.environ.get("VWA_SKINNY_X_SKEW")  # LDS-staged X rows: 64-B skew every 4 rows (1) / none (0)
+        if xsk not in (None, ""):
+            m.skinny_set_x_skew(int(xsk))
         xg = os.environ.get("VWA_SKINNY_XG_ROWS")  # <= 16-row streaming GEMM: X streamed from this many rows
         if xg not in (None, ""):
             m.skinny_set_xg_rows(int(xg))
