@@ -526,6 +526,28 @@ void chain_schedule(ChainParams& cp) {
   cp.lds_item_req = 1;
   cp.lds_item2_req = 1;
   cp.attn_flag = 1;
+  // diagnostic override of the schedule (tools/chain_probe.py A/B runs): "name=value,..."
+  if (const char* e = std::getenv("VWA_CHAIN_SCHED")) {
+    std::string s(e);
+    size_t at = 0;
+    while (at < s.size()) {
+      const size_t comma = s.find(',', at), eq = s.find('=', at);
+      const size_t end = comma == std::string::npos ? s.size() : comma;
+      if (eq != std::string::npos && eq < end) {
+        const std::string k = s.substr(at, eq - at);
+        const int v = std::atoi(s.substr(eq + 1, end - eq - 1).c_str());
+        if (k == "pre2") cp.pre2 = v;
+        else if (k == "next0") cp.next0 = v;
+        else if (k == "xdma") cp.xdma = v;
+        else if (k == "osub") cp.osub = v;
+        else if (k == "lds1") cp.lds_item_req = v;
+        else if (k == "lds2") cp.lds_item2_req = v;
+        else if (k == "aflag") cp.attn_flag = v;
+        else if (k == "pre_mask") cp.pre_mask = v;
+      }
+      at = end + 1;
+    }
+  }
 }
 
 // ---- chained decode layer tail (skinny_stream.hip, vwa_chain_*): descriptor built once on the
@@ -628,7 +650,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   cp.part = reinterpret_cast<float*>(work.data_ptr<int>() + 8192);
   cp.part_floats = (int)(work.numel() - 8192);
   if (ts.has_value()) {
-    TORCH_CHECK(ts->is_cuda() && ts->scalar_type() == at::kLong && ts->numel() >= 1024 * 32, "ts must be int64[>=32768]");
+    TORCH_CHECK(ts->is_cuda() && ts->scalar_type() == at::kLong && ts->numel() >= 1024 * 64, "ts must be int64[>=65536] (64 stamp slots per workgroup)");
     cp.ts = reinterpret_cast<unsigned long long*>(ts->data_ptr<int64_t>());
   }
   if (a_q.has_value()) {  // decode attention as the launch's first phase (its output is `att`)

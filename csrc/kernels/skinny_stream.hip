@@ -599,6 +599,9 @@ __global__ __launch_bounds__(KS * 64) void skinny_fp8_kernel(SkinnyParams p, int
 template <int EPI, int NT, int KS>
 int launch_fp8(const SkinnyParams& p, hipStream_t st, int grid_cap) {
   constexpr int U = 8 / NT;
+  // skinny_fp8_kernel holds 16 rows (rs[16], one MFMA row fragment): more rows must go to the
+  // tiled GEMM, never to silently wrong rows 16+
+  if (p.M > 16) return -10;
   const int G = p.K / 128;
   const int per_wave = (G + KS - 1) / KS;
   const int nb = (per_wave + U - 1) / U;
@@ -640,6 +643,9 @@ constexpr int kChainTpSpinLimit = 1 << 22;
 // arrival to release (four dependent agent-scope round trips).  A flat counter polled with scalar loads
 // on uncached memory (256 same-address atomics) measured 121 us per chained layer vs 99.6 two-level.
 constexpr int kBarTop = 128, kBarErr = 160, kBarAttnDone = 176;
+// diagnostic stamp slots per workgroup (ChainParams::ts): 0..8 phase edges, 9..21 attention,
+// 22..53 in-phase (chain_phase pst)
+constexpr int kTsStride = 64;
 
 // Sum of the 8 group counters (mode 4/5), read with scalar loads past the scalar cache: one
 // round trip for all eight (they complete on lgkmcnt, not behind the wave's weight loads).
@@ -1052,11 +1058,11 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
   const PhaseRange r = chain_range<KS>(ph, wb0, wn);
   const int first_tile = r.u0 / nb;
   const bool xdma = cp.xdma != 0, stager = xdma && w == KS - 1 && !XG;
-  // diagnostic in-phase stamps (tools/chain_probe.py, wave 0): phase 0 -> slots 22..28, phase 1
-  // -> 29..31 (entry, X staged, row scales, item 0 computed, ...)
+  // diagnostic in-phase stamps (tools/chain_probe.py, wave 0): phase i -> slots 22 + 8 i + k
+  // (entry, X staged, row scales, item 0 computed, tile 0 finished, item 1, tile 1 finished)
   auto pst = [&](int k) {
-    const int slot = i == 0 ? 22 + k : i == 1 && k < 3 ? 29 + k : -1;
-    if (cp.ts && threadIdx.x == 0 && slot >= 0) *gp(cp.ts + blockIdx.x * 32 + slot) = __builtin_amdgcn_s_memrealtime();
+    const int slot = k < 8 ? 22 + 8 * i + k : -1;
+    if (cp.ts && threadIdx.x == 0 && slot >= 0) *gp(cp.ts + blockIdx.x * kTsStride + slot) = __builtin_amdgcn_s_memrealtime();
   };
   pst(0);
   if constexpr (XG) {  // X fragments of the items issued before the barrier wait (weights only)
@@ -1304,7 +1310,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   const int e0 = tpr ? __hip_atomic_load(gp(cp.tp.epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   int nts = 0;
   auto stamp = [&]() {
-    if (cp.ts && threadIdx.x == 0) *gp(cp.ts + blockIdx.x * 32 + nts) = __builtin_amdgcn_s_memrealtime();
+    if (cp.ts && threadIdx.x == 0) *gp(cp.ts + blockIdx.x * kTsStride + nts) = __builtin_amdgcn_s_memrealtime();
     ++nts;
   };
   stamp();
@@ -1353,7 +1359,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                         }, &n_attn, [&](int k) {
                                                           if ((k == 15 || k == 10) && cp.ts) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                                                           if (cp.ts && threadIdx.x == 0)
-                                                            *gp(cp.ts + blockIdx.x * 32 + k) = __builtin_amdgcn_s_memrealtime();
+                                                            *gp(cp.ts + blockIdx.x * kTsStride + k) = __builtin_amdgcn_s_memrealtime();
                                                         }, done, &n_final);
     if (!idle) setup0(n_attn);
     stamp();
@@ -1391,7 +1397,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                         }, &n_attn, [&](int k) {
                                                           if ((k == 15 || k == 10) && cp.ts) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                                                           if (cp.ts && threadIdx.x == 0)
-                                                            *gp(cp.ts + blockIdx.x * 32 + k) = __builtin_amdgcn_s_memrealtime();
+                                                            *gp(cp.ts + blockIdx.x * kTsStride + k) = __builtin_amdgcn_s_memrealtime();
                                                         });
     if (!idle) setup0(n_attn);
     stamp();
@@ -1416,6 +1422,8 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   // (their second follows right at the release)
   const bool stg = cp.xdma && (threadIdx.x >> 6) == KS - 1;
   const int preb = cp.xdma ? 0 : cp.pre2;
+  // per-barrier override (cp.pre_mask bit i): two items issued ahead of phase i even with xdma
+  auto preb_of = [&](int i) { return ((cp.pre_mask >> i) & 1) ? 1 : preb; };
   // (hand-off by count: a workgroup without o_proj units skips the phase -- its X rows may not be
   // complete yet, and nothing of it is used)
   if (!(AG > 0 && cp.attn_flag) || chain_range<KS>(cp.ph[0], ob0, on).n_items > 0)
@@ -1431,7 +1439,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
   if (!stg) {
     if (nx) chain_issue_item<E1, KS, WA, false, F8>(cp.ph[1], B, 1);  // phase 1's item 0 is already in A
-    else chain_issue_first<E1, KS, WA, false, F8>(cp.ph[1], A, B, preb);
+    else chain_issue_first<E1, KS, WA, false, F8>(cp.ph[1], A, B, preb_of(1));
   }
   chain_wait(bar, gen, cp.bar_mode);
   // every attention output was counted and every waiter released before this barrier: reset the
@@ -1439,11 +1447,11 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   if (AG > 0 && cp.attn_flag && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_store(gp(&bar[kBarAttnDone]), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp();
-  chain_phase<E1, KS, WA, false, F8>(cp, 1, A, B, smem, nx ? 1 : preb, nx ? 1 : 0);
+  chain_phase<E1, KS, WA, false, F8>(cp, 1, A, B, smem, nx ? 1 : preb_of(1), nx ? 1 : 0);
   stamp();
   if constexpr (NPH >= 3) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
-    if (!stg || XG2) chain_issue_first<E2, KS, WA, XG2, F8>(cp.ph[2], A, B, preb);  // (XG2: no staging wave)
+    if (!stg || XG2) chain_issue_first<E2, KS, WA, XG2, F8>(cp.ph[2], A, B, preb_of(2));  // (XG2: no staging wave)
     // phase 2's LDS item (down projection): its item 2 streams through the barrier window too
     // (phase 1's LDS use ended at the arrival's __syncthreads; the region lies above phase 2's
     // X rows and scratch, which the staging wave fills after the release)
@@ -1452,7 +1460,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
           cp.ph[2].p, cp.ph[2].nb, chain_range<KS>(cp.ph[2]), 2, smem + cp.lds_item2);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E2, KS, WA, XG2, F8>(cp, 2, A, B, smem, preb, 0);
+    chain_phase<E2, KS, WA, XG2, F8>(cp, 2, A, B, smem, preb_of(2), 0);
     stamp();
     if (SEQ == 0 && tpr) {
       chain_tp_reduce(cp, 1, e0 + 2, bar, nwg, bar_next);
@@ -1462,10 +1470,10 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   }
   if constexpr (NPH >= 4) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
-    if (!stg) chain_issue_first<E3, KS, WA, false, F8>(cp.ph[3], A, B, preb);
+    if (!stg) chain_issue_first<E3, KS, WA, false, F8>(cp.ph[3], A, B, preb_of(3));
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E3, KS, WA, false, F8>(cp, 3, A, B, smem, preb, 0);
+    chain_phase<E3, KS, WA, false, F8>(cp, 3, A, B, smem, preb_of(3), 0);
     stamp();
   }
 }

@@ -129,6 +129,7 @@ struct ChainParams {
   // adds 1 to a counter (bar u64 word 176, reset after the next barrier); only the workgroups
   // with o_proj units wait for the count
   int attn_flag;
+  int pre_mask;  // bit i: two weight items issued ahead of the barrier before phase i (xdma issues one)
   ChainTP tp;
 };
 

@@ -111,6 +111,62 @@ def test_full_flow_with_fake_brain_and_executor():
     asyncio.run(go())
 
 
+def test_execution_does_not_block_the_brain_path():
+    """A slow browser run (3 s fake executor) must not hold back the next utterance's intent frame
+    or this utterance's confirmation_required (reference server.ts:186-224 fires /execute without
+    awaiting it); executions still run in order with the chained session id."""
+    exec_calls = []
+
+    async def brain(req):
+        await req.json()
+        return web.json_response({"version": "1.0", "intents": [
+            {"type": "search", "args": {"query": "earbuds"}, "priority": 0, "requires_confirmation": False,
+             "retries": 1},
+            {"type": "upload", "args": {"fileRef": "resume://latest"}, "priority": 1, "requires_confirmation": True,
+             "retries": 1}], "context_updates": {}, "confidence": 0.9})
+
+    async def execute(req):
+        body = await req.json()
+        exec_calls.append(body)
+        await asyncio.sleep(3.0)
+        return web.json_response({"session_id": f"sess-{len(exec_calls)}", "results": [], "artifacts": {}})
+
+    async def go():
+        bapp = web.Application()
+        bapp.router.add_post("/parse", brain)
+        eapp = web.Application()
+        eapp.router.add_post("/execute", execute)
+        async with TestServer(bapp) as bs, TestServer(eapp) as es:
+            vapp = build_app(lambda: FakeAsr(), brain_url=str(bs.make_url("/parse")),
+                             executor_url=str(es.make_url("")).rstrip("/"), debounce_ms=10)
+            async with TestClient(TestServer(vapp)) as c:
+                ws = await c.ws_connect("/stream")
+                await ws.receive()
+                await ws.receive()
+                loop = asyncio.get_running_loop()
+                t0 = loop.time()
+                await ws.send_str(json.dumps({"type": "flush"}))
+                got = await _recv_types(ws, ["intent", "confirmation_required"])
+                assert loop.time() - t0 < 1.5, "confirmation_required waited for the browser run"
+                assert "execution_result" not in [g["type"] for g in got]
+                t1 = loop.time()
+                await ws.send_str(json.dumps({"type": "flush"}))
+                got2 = await _recv_types(ws, ["intent"])
+                assert loop.time() - t1 < 1.5, "the second intent frame waited for the first execution"
+                rest = await _recv_types(ws, ["execution_result"], timeout=10.0)
+                results = [g for g in got + got2 + rest if g["type"] == "execution_result"]
+                while len(results) < 2:
+                    msg = json.loads((await asyncio.wait_for(ws.receive(), 10.0)).data)
+                    if msg["type"] == "execution_result":
+                        results.append(msg)
+                assert results[0]["payload"].endswith("Session: sess-1")
+                assert results[1]["payload"].endswith("Session: sess-2")
+                assert "session_id" not in exec_calls[0] and exec_calls[1]["session_id"] == "sess-1"
+                await ws.close()
+
+    asyncio.run(go())
+
+
 def test_streaming_session_vad_partials_finals():
     calls = []
 

@@ -54,7 +54,7 @@ def main():
     rope = ops.rope_table(4096, hd, 5e5, device=dev)
     bar = E.alloc_uncached_i32(512, torch.empty(1, device=dev)) if a.bar_mode >= 2 else \
         torch.zeros(512, dtype=torch.int32, device=dev)
-    ts = torch.zeros(1024 * 32, dtype=torch.int64, device=dev)
+    ts = torch.zeros(1024 * 64, dtype=torch.int64, device=dev)  # 64 stamp slots per workgroup
     work = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
     akw, ag = {}, 0
     if a.attn:  # the layer's attention over a 1100-token paged context as phase 0
@@ -134,13 +134,13 @@ def main():
     # stamps of the last launch: [start, end0, wait0, end1, wait1, end2, wait2, end3]
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     ns_ = 9 if a.attn else 8
-    st = ts.view(-1, 32)[:cus, :ns_].double().cpu()
+    st = ts.view(-1, 64)[:cus, :ns_].double().cpu()
     st = (st - st[:, :1].min()) * 10e-3  # us
     med = st.median(dim=0).values.tolist()
     mx = st.max(dim=0).values.tolist()
     mn = st.min(dim=0).values.tolist()
     if a.attn:  # in-attention stamps 9..14 of the attention workgroups (slots stay 0 elsewhere)
-        full = ts.view(-1, 32)[:cus].double().cpu()
+        full = ts.view(-1, 64)[:cus].double().cpu()
         t0 = full[:, 0].min()
         att = full[full[:, 9] > 0]
         names = ["ctx_known", "q_ready", "pre_sync", "meta_landed", "kv_issue", "merged", "kv_landed", "meta_regs", "n_items", "loop_top", "ctxmax", "chunk_known", "pre_loop"]
@@ -167,8 +167,10 @@ def main():
                 # in-phase stamps (chain_phase pst): o_proj entry, X staged, scales, item0, fin0,
                 # item1, fin1 | gate/up entry, X staged, scales
                 ph = {}
-                for j, pn in enumerate(["o_entry", "o_xstaged", "o_scales", "o_item0", "o_fin0", "o_item1",
-                                        "o_fin1", "gu_entry", "gu_xstaged", "gu_scales"]):
+                # chain_phase pst: phase i at slots 22 + 8 i + k
+                kn = ["entry", "xstaged", "scales", "item0", "fin0", "item1", "fin1"]
+                for j, pn in [(8 * i + k, f"{pre}_{n}") for i, pre in enumerate(["o", "gu", "down", "qkv"])
+                              for k, n in enumerate(kn)]:
                     col = full[sel, 22 + j]
                     col = col[col > 0]
                     if col.numel():

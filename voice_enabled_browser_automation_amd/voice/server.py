@@ -13,9 +13,12 @@ Per connection:
   * JSON control frames: ``{"type":"close"}``, ``{"type":"context_update","payload":{...}}``,
     and ``{"type":"flush"}`` (end of utterance: finalise without waiting for silence).
 
-Races of the reference fixed here: brain calls and executor calls of one
-connection are serialised by a per-connection lock, so the executor session id is assigned in
-order; sends after a client disconnect are dropped.
+Races of the reference fixed here: brain calls of one connection are serialised
+by a per-connection lock (context updates apply in utterance order), and its executor calls run
+one at a time from a per-connection queue, so the executor session id is assigned in order; sends
+after a client disconnect are dropped.  As in the reference (server.ts:186-224) the execution is
+NOT awaited on the brain path: ``intent``, ``tts`` and ``confirmation_required`` go out as soon as
+the brain answers, and the next utterance's brain call does not wait for a browser run.
 """
 from __future__ import annotations
 
@@ -58,6 +61,7 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
     app["asr_pool"] = ThreadPoolExecutor(max_workers=int(os.environ.get("VWA_MAX_SESSIONS", "32")) + 4,
                                          thread_name_prefix="asr")
     app["asr_factory"] = asr_factory
+    app["exec_tasks"] = set()  # executor queues still draining after their connection closed
     brain_url = brain_url or os.environ.get("BRAIN_URL", "http://127.0.0.1:8090/parse")
     executor_url = executor_url or os.environ.get("EXECUTOR_URL", "http://127.0.0.1:7081")
     if debounce_ms is None:
@@ -67,6 +71,8 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
         app_["http"] = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=120))
 
     async def on_cleanup(app_):
+        for t in list(app_["exec_tasks"]):
+            t.cancel()
         await app_["http"].close()
         app_["asr_pool"].shutdown(wait=False)
 
@@ -147,6 +153,19 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                 await send({"type": "execution_error", "payload": f"Execution failed: {e}"})
                 m.inc("execution_errors")
 
+        # executor calls of this connection, in order, off the brain path (the reference fires
+        # /execute without awaiting it, server.ts:186-219; one at a time here so session ids chain)
+        exec_q: asyncio.Queue = asyncio.Queue()
+
+        async def exec_worker():
+            while True:
+                safe = await exec_q.get()
+                if safe is None:
+                    return
+                await run_executor(safe)
+
+        exec_task = asyncio.ensure_future(exec_worker())
+
         async def process(combined: str):
             async with lock:
                 t0 = time.perf_counter()
@@ -174,7 +193,7 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                     safe = [i for i in intents if not (isinstance(i, dict) and i.get("requires_confirmation"))]
                     risky = [i for i in intents if isinstance(i, dict) and i.get("requires_confirmation")]
                     if safe:
-                        await run_executor(safe)
+                        exec_q.put_nowait(safe)
                     if risky:
                         await send({"type": "confirmation_required",
                                     "payload": f"{len(risky)} risky actions require manual confirmation"})
@@ -251,6 +270,11 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                 st["debounce"].cancel()
             if asr is not None and hasattr(asr, "close"):
                 asr.close()
+            # queued executions still run (the reference's fire-and-forget promises do); their
+            # frames are dropped once the socket is closed
+            exec_q.put_nowait(None)
+            app["exec_tasks"].add(exec_task)
+            exec_task.add_done_callback(app["exec_tasks"].discard)
         return ws
 
     app.router.add_get("/health", health)
