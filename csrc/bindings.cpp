@@ -526,6 +526,10 @@ void chain_schedule(ChainParams& cp) {
   cp.lds_item_req = 1;
   cp.lds_item2_req = 1;
   cp.attn_flag = 1;
+  // round 5 (profiles/r5_chain_xwait.md): nothing but the X pieces in a CU's memory queue until X is
+  // in LDS -- chained layer 103.2-103.6 vs 105.6 us, bench GPU wait 3462-3471 vs 3558 us per step
+  cp.xfirst = 1;
+  cp.xwait = 1;
   // diagnostic override of the schedule (tools/chain_probe.py A/B runs): "name=value,..."
   if (const char* e = std::getenv("VWA_CHAIN_SCHED")) {
     std::string s(e);
@@ -544,6 +548,11 @@ void chain_schedule(ChainParams& cp) {
         else if (k == "lds2") cp.lds_item2_req = v;
         else if (k == "aflag") cp.attn_flag = v;
         else if (k == "pre_mask") cp.pre_mask = v;
+        else if (k == "pre_waves") cp.pre_waves = v;
+        else if (k == "xfirst") cp.xfirst = v;
+        else if (k == "xwait") cp.xwait = v;
+        else if (k == "xw_late") cp.xw_late = v;
+        else if (k == "poll_free") cp.poll_free = v;
       }
       at = end + 1;
     }

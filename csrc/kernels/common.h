@@ -92,6 +92,15 @@ VWA_DEVICE uint4 load_nt(const void* p) {
 
 VWA_DEVICE bf16x8 as_bf16x8(const uint4& v) { return __builtin_bit_cast(bf16x8, v); }
 
+// Workgroup barrier for LDS (and control-flow) hand-offs only: this wave's LDS / scalar operations
+// complete first (lgkmcnt), its VECTOR memory operations stay in flight.  __syncthreads()' workgroup
+// release fence makes the compiler put s_waitcnt vmcnt(0) in front of the barrier whenever a store
+// may be outstanding -- and gfx9 counts loads and stores on one in-order counter, so that drains
+// every weight load a streaming kernel keeps in flight (measured: the chained layer's X staging
+// "took" 6-9 us because its barrier waited for 256 KB of prefetched weights per CU).  Callers that
+// need their global stores performed before the barrier wait for them explicitly.
+VWA_DEVICE void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 VWA_DEVICE float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

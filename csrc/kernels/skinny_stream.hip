@@ -127,7 +127,7 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) red[(((w * NT + nt) * MT + mt) * 4 + i) * 64 + lane] = acc[nt * MT + mt][i];
-  __syncthreads();
+  lds_sync();
   auto red_at = [&](int m, int nn) -> float {
     const int nt = nn >> 4, q = nn & 15, mt = MT > 1 ? m >> 4 : 0, mm = m & 15;
     const int ln = q + 16 * (mm >> 2), i = mm & 3;
@@ -206,7 +206,7 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
       else st_u16<SC1>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + n, f2bf(v));
     }
   }
-  __syncthreads();
+  lds_sync();
 #pragma unroll
   for (int k = 0; k < NT * MT; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
           *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8);
     }
   }
-  __syncthreads();
+  lds_sync();
   for (int m = w; m < 16 * MT; m += KS) {
     float sc = 1.f, mean = 0.f;
     if (p.fuse_rms && m < M) {
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
       mu[m] = mean;
     }
   }
-  __syncthreads();
+  lds_sync();
 
   if (!p.w_first) {
     load_item(A, 0);
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_fp8_kernel(SkinnyParams p, int
       inv[m] = iv;
     }
   }
-  __syncthreads();
+  lds_sync();
   // ---- quantise X rows into LDS (e4m3, 8 values -> 8 bytes)
   for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
     const int m = c / k8, kk = c % k8;
@@ -517,7 +517,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_fp8_kernel(SkinnyParams p, int
     q.y = cvt_pk_fp8(f[4] * iv, f[5] * iv) | (cvt_pk_fp8(f[6] * iv, f[7] * iv) << 16);
     *reinterpret_cast<uint2*>(xs + m * xstride + kk * 8) = q;
   }
-  __syncthreads();
+  lds_sync();
 
   const int G = K / 128;
   const int gb = (G * w) / KS, ge = (G * (w + 1)) / KS;
@@ -680,7 +680,7 @@ VWA_DEVICE unsigned long long chain_base(const unsigned long long* bar, int nwg,
 
 VWA_DEVICE unsigned long long chain_arrive(unsigned long long* bar, int nwg, int mode, unsigned long long& next) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are performed
-  __syncthreads();
+  lds_sync();
   if (mode >= 4) {
     if (threadIdx.x == 0) __hip_atomic_fetch_add(gp(&bar[16 * (blockIdx.x & 7)]), 1ull, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
@@ -708,7 +708,7 @@ VWA_DEVICE unsigned long long chain_arrive(unsigned long long* bar, int nwg, int
 
 VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, int mode) {
   if (mode == 3 || mode == 5) {  // DIAGNOSTIC ONLY (tools/chain_probe.py --no-wait): arrive, never
-    __syncthreads();             // wait -> wrong results; what the phases cost without dependencies
+    lds_sync();             // wait -> wrong results; what the phases cost without dependencies
     return;
   }
   if (mode == 4) {
@@ -724,7 +724,7 @@ VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, i
         }
       }
     }
-    __syncthreads();
+    lds_sync();
     return;
   }
   if (mode == 2) {
@@ -747,7 +747,7 @@ VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, i
         }
       }
     }
-    __syncthreads();
+    lds_sync();
     return;
   }
   if (threadIdx.x == 0) {
@@ -761,7 +761,7 @@ VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, i
       }
     }
   }
-  __syncthreads();
+  lds_sync();
 }
 
 // Tensor-parallel round (ChainParams::tp, world > 1) after a row-parallel phase whose epilogue
@@ -1019,7 +1019,7 @@ VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[((w * NT + nt) * 4 + i) * 64 + lane] = acc[nt][i];
-  __syncthreads();
+  lds_sync();
   for (int o = threadIdx.x; o < M * 16 * NT; o += KS * 64) {
     const int m = o / (16 * NT), nn = o % (16 * NT);
     const int nt = nn >> 4, q = nn & 15;
@@ -1029,7 +1029,7 @@ VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
     for (int ww = 0; ww < KS; ++ww) v += red[((ww * NT + nt) * 4 + i) * 64 + ln];
     st_f32<true>(slot + o, v);
   }
-  __syncthreads();
+  lds_sync();
 }
 
 // One phase.  X0 holds this phase's item 0 (issued before the barrier wait), X1 item 1 when pre2.
@@ -1040,7 +1040,7 @@ VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
 // issued into (X0, X1).
 template <int EPI, int KS, int WA, bool XG = false, bool F8 = false, int R>
 VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 (&X1)[R], char* smem, int pre2,
-                            int hs = 0, int wb0 = 0, int wn = 0) {
+                            int hs = 0, int wb0 = 0, int wn = 0, bool has0 = true) {
   constexpr int NT = PhaseShape<EPI, KS, XG, F8>::NT, U = PhaseShape<EPI, KS, XG, F8>::U;
   const ChainPhase& ph = cp.ph[i];
   const SkinnyParams& p = ph.p;
@@ -1069,10 +1069,6 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     chain_load_x<U>(p, nb, X0, 0, r);
     if (pre2) chain_load_x<U>(p, nb, X1, 1, r);
   }
-  if (xdma && !stager && !pre2) chain_load<NT, U, WA, R, XG, F8>(p, nb, X1, 1, r);  // streams during the staging
-
-  EpiPre pre;
-  if (r.n_items > 0) epi_values<EPI, NT, true>(p, first_tile, threadIdx.x, pre);
   // ---- stage X (written by the previous phase: sc1 loads) + RMSNorm row scales
   const int k8 = K / 8;
   const __amdgpu_buffer_rsrc_t rx =
@@ -1086,6 +1082,28 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
             rx, (__attribute__((address_space(3))) void*)(xs + m * xstride + j * 512), 16,
             (unsigned)(((size_t)m * p.ldx + j * 512) * 2 + lane * 16), 0, 0, 16);
     asm volatile("" ::: "memory");  // keep the weight loads below younger than the pieces
+  }
+  // cp.xfirst: a CU's vector memory requests are served in order (measured, tools/
+  // crit_latency_probe.hip: a load behind 112-224 KB of the same CU's weight loads takes 2-4 us,
+  // 0.12 us on a CU whose own queue is empty while the others stream) -- so the other waves issue
+  // their next weight item only after the staging wave's X pieces are in the queue
+  // cp.xwait: the CU's memory pipe is SHARED by its waves (measured: one wave's 28 KB of X pieces
+  // land in 1.1 us on a quiet CU, 5.6 us while 7 other waves stream weights) -- so no wave issues
+  // weights until the X rows are in LDS; the items pre-issued at the barrier arrival have had the
+  // barrier window to land
+  const bool xw = xdma && cp.xwait;
+  if (xdma && cp.xfirst && !xw) lds_sync();
+  auto issue_rest = [&]() {
+    if (xdma && !stager && !has0) chain_load<NT, U, WA, R, XG, F8>(p, nb, X0, 0, r);  // (not issued at the barrier)
+    if (xdma && !stager && (!pre2 || !has0)) chain_load<NT, U, WA, R, XG, F8>(p, nb, X1, 1, r);  // streams during the staging
+  };
+  if (!xw) issue_rest();
+
+  EpiPre pre;
+  if (r.n_items > 0 && !xw) epi_values<EPI, NT, true>(p, first_tile, threadIdx.x, pre);
+  if (stager && xw) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pieces (the staging wave issued nothing else)
+  } else if (stager) {
     int nw = 0;
     if (hs < 1) {
       chain_load<NT, U, WA, R, XG, F8>(p, nb, X0, 0, r);
@@ -1113,8 +1131,19 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
       *reinterpret_cast<uint4*>(xs + m * xstride + kk * 8) = make_uint4(v.x, v.y, v.z, v.w);
     }
   }
-  __syncthreads();
+  lds_sync();
   pst(1);
+  // X is in LDS: the weights (and the first tile's epilogue operands) go out after the row scales
+  // -- a wave whose issue blocks on a full memory queue would hold the scales barrier
+  auto issue_xw = [&]() {
+    issue_rest();
+    if (stager) {
+      if (hs < 1) chain_load<NT, U, WA, R, XG, F8>(p, nb, X0, 0, r);
+      if (hs < 2) chain_load<NT, U, WA, R, XG, F8>(p, nb, X1, 1, r);
+    }
+    if (r.n_items > 0) epi_values<EPI, NT, true>(p, first_tile, threadIdx.x, pre);
+  };
+  if (xw && !cp.xw_late) issue_xw();
   for (int m = w; m < 16; m += KS) {
     float sc = 1.f, mean = 0.f;
     if (p.fuse_rms && m < M && !XG) {  // (the host never folds a norm into an XG phase)
@@ -1141,7 +1170,8 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
       mu[m] = mean;
     }
   }
-  __syncthreads();
+  lds_sync();
+  if (xw && cp.xw_late) issue_xw();
   pst(2);
 
   f32x4 acc[NT];
@@ -1194,14 +1224,14 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     float* slots = cp.part + (size_t)tile * 2 * per;
     tile_publish<NT, KS>(M, red, acc, slots + mine * per);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    lds_sync();
     if (threadIdx.x == 0) {
       const unsigned t = __hip_atomic_fetch_add(gp(&cp.tickets[tile]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = t == 1u;
       if (last) __hip_atomic_store(gp(&cp.tickets[tile]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *s_flag = last;
     }
-    __syncthreads();
+    lds_sync();
     if (*s_flag) {
       tile_epilogue<EPI, NT, KS, true>(p, red, rs, mus, tile, acc, w, lane, pre, false,
                                        slots + (1 - mine) * per);
@@ -1225,8 +1255,11 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
   if (!pre2 && !xdma) chain_load<NT, U, WA, R, XG, F8>(p, nb, X1, 1, r);
   auto ldi = [&](uint4 (&wr)[R], int idx) {
     if (idx == 2 && ((i == 1 && cp.lds_item && w < cp.lds_item_waves) ||
-                     (i == 2 && cp.lds_item2 && w < cp.lds_item2_waves))) {  // preloaded (chain_preload)
+                     (i == 2 && cp.lds_item2 && w < cp.lds_item2_waves && !(cp.poll_free && w == 0)))) {  // preloaded (chain_preload)
       static_assert(R == 16, "LDS item: 16 loads of 1 KB per wave");
+      // this wave's LDS-DMA of the item must have landed (no barrier drains vmcnt any more, and
+      // the compiler does not order LDS-DMA writes before these reads)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const char* src = smem + (i == 1 ? cp.lds_item : cp.lds_item2) + w * 16384 + lane * 16;
 #pragma unroll
       for (int k = 0; k < R; ++k) wr[k] = *reinterpret_cast<const uint4*>(src + k * 1024);
@@ -1363,7 +1396,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                         }, done, &n_final);
     if (!idle) setup0(n_attn);
     stamp();
-    __syncthreads();  // the attention's LDS readers are done (idle workgroups: the metadata's)
+    lds_sync();  // the attention's LDS readers are done (idle workgroups: the metadata's)
     if (!idle) {
       pre0 = 0;
       issue0(0);
@@ -1384,7 +1417,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
           }
         }
       }
-      __syncthreads();
+      lds_sync();
     }
    } else {
     // idle workgroups (no attention item) issue their o_proj weights at once; the others after
@@ -1437,9 +1470,13 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   stamp();
   if (SEQ == 0 && tpr) chain_tp_reduce(cp, 0, e0 + 1, bar, nwg, bar_next);
   gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
+  // cp.pre_waves (> 0): only waves below it issue the next phase's items at the barrier; the others
+  // issue theirs after the release, behind the X pieces (chain_phase has0 = false)
+  const int wv = (int)(threadIdx.x >> 6);
+  const bool prew = (cp.pre_waves == 0 || wv < cp.pre_waves) && !(cp.poll_free && wv == 0);
   if (!stg) {
     if (nx) chain_issue_item<E1, KS, WA, false, F8>(cp.ph[1], B, 1);  // phase 1's item 0 is already in A
-    else chain_issue_first<E1, KS, WA, false, F8>(cp.ph[1], A, B, preb_of(1));
+    else if (prew) chain_issue_first<E1, KS, WA, false, F8>(cp.ph[1], A, B, preb_of(1));
   }
   chain_wait(bar, gen, cp.bar_mode);
   // every attention output was counted and every waiter released before this barrier: reset the
@@ -1447,20 +1484,20 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   if (AG > 0 && cp.attn_flag && blockIdx.x == 0 && threadIdx.x == 0)
     __hip_atomic_store(gp(&bar[kBarAttnDone]), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp();
-  chain_phase<E1, KS, WA, false, F8>(cp, 1, A, B, smem, nx ? 1 : preb_of(1), nx ? 1 : 0);
+  chain_phase<E1, KS, WA, false, F8>(cp, 1, A, B, smem, nx ? 1 : preb_of(1), nx ? 1 : 0, 0, 0, nx || prew);
   stamp();
   if constexpr (NPH >= 3) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
-    if (!stg || XG2) chain_issue_first<E2, KS, WA, XG2, F8>(cp.ph[2], A, B, preb_of(2));  // (XG2: no staging wave)
+    if ((!stg && prew) || XG2) chain_issue_first<E2, KS, WA, XG2, F8>(cp.ph[2], A, B, preb_of(2));  // (XG2: no staging wave)
     // phase 2's LDS item (down projection): its item 2 streams through the barrier window too
     // (phase 1's LDS use ended at the arrival's __syncthreads; the region lies above phase 2's
     // X rows and scratch, which the staging wave fills after the release)
-    if (cp.lds_item2 && (int)(threadIdx.x >> 6) < cp.lds_item2_waves)
+    if (cp.lds_item2 && wv < cp.lds_item2_waves && !(cp.poll_free && wv == 0))
       chain_preload<PhaseShape<E2, KS, false, F8>::NT, PhaseShape<E2, KS, false, F8>::U, WA, F8>(
           cp.ph[2].p, cp.ph[2].nb, chain_range<KS>(cp.ph[2]), 2, smem + cp.lds_item2);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E2, KS, WA, XG2, F8>(cp, 2, A, B, smem, preb_of(2), 0);
+    chain_phase<E2, KS, WA, XG2, F8>(cp, 2, A, B, smem, preb_of(2), 0, 0, 0, prew || XG2);
     stamp();
     if (SEQ == 0 && tpr) {
       chain_tp_reduce(cp, 1, e0 + 2, bar, nwg, bar_next);
@@ -1470,10 +1507,10 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   }
   if constexpr (NPH >= 4) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
-    if (!stg) chain_issue_first<E3, KS, WA, false, F8>(cp.ph[3], A, B, preb_of(3));
+    if (!stg && prew) chain_issue_first<E3, KS, WA, false, F8>(cp.ph[3], A, B, preb_of(3));
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E3, KS, WA, false, F8>(cp, 3, A, B, smem, preb_of(3), 0);
+    chain_phase<E3, KS, WA, false, F8>(cp, 3, A, B, smem, preb_of(3), 0, 0, 0, prew);
     stamp();
   }
 }

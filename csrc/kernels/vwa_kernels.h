@@ -130,6 +130,11 @@ struct ChainParams {
   // with o_proj units wait for the count
   int attn_flag;
   int pre_mask;  // bit i: two weight items issued ahead of the barrier before phase i (xdma issues one)
+  int pre_waves;  // > 0: only waves below it issue the next phase's items at a barrier (0: all)
+  int xfirst;     // the staging wave's X pieces enter the CU's memory queue before the others' next items
+  int xwait;      // no wave issues weights between a barrier's release and its X rows landing in LDS
+  int xw_late;    // (xwait) the weights go out after the row scales, not before
+  int poll_free;  // wave 0 (the barrier poller) issues nothing ahead of a barrier wait
   ChainTP tp;
 };
 

@@ -147,23 +147,31 @@ def test_supervisor_restarts_only_the_brain():
 
     spawned = []
 
-    def spawn(module, env, nproc):
+    def spawn(module, env, nproc, restart=0):
         p = _FakeProc(module)
-        spawned.append((module, nproc, p))
+        spawned.append((module, nproc, p, restart))
         return p
 
     t = [0.0]
     sup = Supervisor(spawn=spawn, max_restarts=2, window_s=100.0, backoff_s=0.5, clock=lambda: t[0],
-                     sleep=lambda s: t.__setitem__(0, t[0] + s), log=lambda *_: None)
+                     log=lambda *_: None)
     brain = sup.add("brain", "pkg.brain.server", {}, 2, restartable=True)
     voice = sup.add("voice", "pkg.voice.server", {})
     assert sup.poll_once()
     brain.rc = FATAL_EXIT_CODE  # the TP group exited after losing lockstep
+    assert sup.poll_once() and sup.pending_restarts() == 1 and len(spawned) == 2  # scheduled, not slept
+    voice.rc = None
+    t[0] += 0.25
+    assert sup.poll_once() and len(spawned) == 2  # backoff (0.5 s) not over: others still watched
+    t[0] += 0.3
     assert sup.poll_once()
     assert len(spawned) == 3 and spawned[-1][:2] == ("pkg.brain.server", 2)  # a fresh torchrun group
+    assert spawned[-1][3] == 1  # a restart: the launcher picks a fresh rendezvous port
     assert sup.procs()[1] is voice and voice.rc is None and not voice.signals
     sup.procs()[0].rc = FATAL_EXIT_CODE
-    assert sup.poll_once()  # second restart (backoff doubled)
+    assert sup.poll_once()
+    t[0] += 1.0  # second restart (backoff doubled)
+    assert sup.poll_once() and len(spawned) == 4 and spawned[-1][3] == 2
     sup.procs()[0].rc = FATAL_EXIT_CODE
     assert not sup.poll_once()  # restart budget spent: stop everything
     sup.stop()
@@ -173,7 +181,7 @@ def test_supervisor_restarts_only_the_brain():
 def test_supervisor_stops_on_a_non_restartable_exit():
     from voice_enabled_browser_automation_amd.launch import Supervisor
 
-    sup = Supervisor(spawn=lambda m, e, n: _FakeProc(m), log=lambda *_: None)
+    sup = Supervisor(spawn=lambda m, e, n, restart=0: _FakeProc(m), log=lambda *_: None)
     sup.add("brain", "b", {}, restartable=True)
     ex = sup.add("executor", "e", {})
     ex.rc = 1
@@ -208,3 +216,53 @@ def test_brain_health_reports_a_failed_tp_group():
 
     status, body = asyncio.run(go())
     assert status == 503 and body["status"] == "error"
+
+
+def _idle_worker(rank, world, port, q):
+    import datetime
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tp = TPContext(rank=rank, size=world, group=dist.group.WORLD)
+    # a control group whose collectives time out after 2 s: without the leader's heartbeat the
+    # worker's broadcast raises during the idle period below and the group would be restarted
+    ctl = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=2))
+
+    def fatal(e):
+        q.put(("fatal", rank, repr(e)))
+        os._exit(FATAL_EXIT_CODE)
+
+    tpe = TPIntentEngine(_engine(tp), tp, ctl_group=ctl, on_fatal=fatal, heartbeat_s=0.3)
+    if rank == 0:
+        tpe.start()
+        time.sleep(4.0)  # idle for twice the control group's timeout
+        outs = tpe.parse_many(_reqs()[:1])
+        q.put(("beats", rank, tpe.heartbeats))
+        tpe.stop()
+    else:
+        outs = tpe.worker_loop()
+    q.put(("outs", rank, outs))
+    dist.destroy_process_group()
+
+
+def test_idle_tp_group_survives_past_the_control_timeout():
+    """an idle leader must keep the workers' control broadcast alive (heartbeat), so
+    a quiet period longer than the gloo timeout is not turned into a fatal group restart."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_idle_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    msgs = []
+    while not q.empty():
+        msgs.append(q.get())
+    assert [p.exitcode for p in procs] == [0, 0], msgs
+    assert not [m for m in msgs if m[0] == "fatal"], msgs
+    beats = next(m[2] for m in msgs if m[0] == "beats")
+    assert beats >= 5, msgs
+    outs = {r: o for kind, r, o in msgs if kind == "outs"}
+    assert outs[0] == outs[1] and safe_parse(ParseResponse, outs[0][0]).success

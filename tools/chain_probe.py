@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--row-major", dest="tiled", action="store_false",
                     help="row-major [N, K] weights instead of the pre-tiled layout (ops.tile_weight)")
     ap.add_argument("--fp8", action="store_true", help="fp8 tiled weights (the W8A16 chain, ops.FP8Weight)")
+    ap.add_argument("--no-stamps", action="store_true",
+                    help="launch without the per-phase stamps (their stores and waits slow the phases slightly)")
     a = ap.parse_args()
     if a.no_wait:
         a.bar_mode = 5 if a.bar_mode >= 4 else 3
@@ -98,7 +100,8 @@ def main():
             w.update({k + "_t": ops.tile_weight(w[k]) for k in ("o", "gu", "down", "qkv")})
     wt = (lambda w, k: w[k + "_t"]) if a.tiled else (lambda w, k: w[k])  # noqa: E731
     descs = [E.chain_make(h, att, act, wt(w, "o"), wt(w, "gu"), wt(w, "down"), 1e-5, wt(w, "qkv"), nq, nkv, hd, pos, slots, rope, q,
-                          kc, vc, bar, work, ts, a.bar_mode, **akw, w_tiled=a.tiled, **sc) for w, sc in zip(Ws, sck)]
+                          kc, vc, bar, work, None if a.no_stamps else ts, a.bar_mode, **akw, w_tiled=a.tiled, **sc)
+             for w, sc in zip(Ws, sck)]
     it = [0]
 
     def chained():
@@ -178,6 +181,7 @@ def main():
                                   int(col.numel())]
                 r[nm + "_phase"] = ph
     r["env"] = {k: v for k, v in os.environ.items() if k.startswith("VWA_CHAIN")}
+    r["layer_us"] = round(float(mx[-1]), 2)
     print(json.dumps(r), flush=True)
     if a.json:
         with open(a.json, "a") as f:

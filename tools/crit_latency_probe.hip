@@ -171,6 +171,53 @@ __global__ __launch_bounds__(512) void crit_loader(const char* W, size_t wbytes,
   if (acc == 0x12345678u) sink[1] = (int)acc;
 }
 
+// X staging as the chained layer does it: wave 0 of every workgroup LDS-DMAs `pieces` 1 KB pieces
+// (one row of K = 512 * pieces bf16) with cache bits AUX, all in flight, and times their landing.
+// copies: how many distinct copies of X the 256 workgroups spread over (1: all read the SAME bytes,
+// 8: one copy per XCD by block id mod 8, 256: private).  Waves 1..nstream stream weights meanwhile.
+__global__ __launch_bounds__(512) void xstage(const char* W, size_t wbytes, int nstream, const char* X, int pieces,
+                                              int copies, int aux, unsigned long long* out, int* sink) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (w >= 1 && w <= nstream) {
+    const unsigned nwaves = gridDim.x * nstream, wid = blockIdx.x * nstream + (w - 1);
+    const unsigned per = (unsigned)(wbytes / 16384) / nwaves;
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(W), (short)0, (int)wbytes, 0x00020000);
+    const unsigned b0 = wid * per * 16384u + lane * 16u;
+    u32x4 v[16];
+    unsigned acc = 0;
+    for (unsigned it = 0; it < per; ++it) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(b0 + it * 16384u + i * 1024u), 0, 0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc ^= v[i].x ^ v[i].w;
+    }
+    if (acc == 0x12345678u) sink[0] = (int)acc;
+    return;
+  }
+  if (w != 0) return;
+  const unsigned long long t_start = now();
+  if (nstream) while (now() - t_start < 300) __builtin_amdgcn_s_sleep(8);
+  const int copy = copies == 1 ? 0 : copies == 8 ? (blockIdx.x & 7) : blockIdx.x;
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(X), (short)0, 256 * 64 * 1024, 0x00020000);
+  const unsigned base = (unsigned)copy * 64u * 1024u;
+  const unsigned long long t0 = now();
+  for (int j = 0; j < pieces; ++j) {
+    if (aux == 16)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(lds + j * 1024), 16,
+                                               base + j * 1024 + lane * 16, 0, 0, 16);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (__attribute__((address_space(3))) void*)(lds + j * 1024), 16,
+                                               base + j * 1024 + lane * 16, 0, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long t1 = now();
+  if (lane == 0) out[blockIdx.x] = t1 - t0;
+  if (lds[lane] == 123 && lds[1000 + lane] == 77) sink[2] = 1;
+}
+
 int main() {
   const size_t wbytes = (size_t)1 << 30, cold_bytes = (size_t)256 << 20;
   char *W, *cold;
@@ -193,7 +240,7 @@ int main() {
   const char* mnames[] = {"sc1_peer_line", "cold_hbm_line", "scalar_uncached_poll", "atomic_uncached_ticket",
                           "scalar_uncached_fresh_line", "scalar_cached_fresh_line"};
   std::vector<unsigned long long> h(256 * kProbes);
-  for (int sets = 1; sets <= 2; ++sets)
+  for (int sets = 1; sets <= 0; ++sets)
     for (int ns : {0, 2, 4, 7})
       for (int mode = 0; mode < 6; ++mode) {
         if ((ns == 0 && sets == 2) || mode == 2 || mode == 3 || mode == 5 || ns == 2) continue;
@@ -220,6 +267,29 @@ int main() {
                     v.back(), ms * 1e3, ns ? wbytes / (ms * 1e-3) / 1e12 : 0.0);
         std::fflush(stdout);
       }
+  {  // X staging: hot spot of 256 CUs reading the same bytes?
+    char* Xs;
+    CK(hipMalloc(&Xs, 256 * 64 * 1024));
+    CK(hipMemset(Xs, 3, 256 * 64 * 1024));
+    for (int ns : {0, 7})
+      for (int pieces : {8, 28})
+        for (int copies : {1, 8, 256})
+          for (int aux : {16, 0}) {
+            hipLaunchKernelGGL(xstage, dim3(256), dim3(512), 64 * 1024, 0, W, wbytes, ns, Xs, pieces, copies, aux, out, sink);
+            hipLaunchKernelGGL(xstage, dim3(256), dim3(512), 64 * 1024, 0, W, wbytes, ns, Xs, pieces, copies, aux, out, sink);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(h.data(), out, 256 * 8, hipMemcpyDeviceToHost));
+            std::vector<double> v(256);
+            for (int b = 0; b < 256; ++b) v[b] = h[b] * 0.01;
+            std::sort(v.begin(), v.end());
+            std::printf("{\"xstage\": true, \"stream_waves\": %d, \"pieces_kb\": %d, \"copies\": %d, \"sc1\": %d, "
+                        "\"us_p10_p50_p90_max\": [%.2f, %.2f, %.2f, %.2f]}\n", ns, pieces, copies, aux == 16,
+                        v[25], v[128], v[230], v[255]);
+            std::fflush(stdout);
+          }
+    CK(hipFree(Xs));
+  }
+  return 0;
   // loader-wave streaming (LDS-DMA ring), in-flight cap per CU, probes from a busy / a quiet CU
   for (int infl : {32, 48, 63})
     for (int quiet : {0, 1})

@@ -38,6 +38,10 @@ from typing import Any, Callable, Deque, List, Optional, Tuple
 from .prompt import messages_for
 
 FATAL_EXIT_CODE = 70  # EX_SOFTWARE: the TP group must be restarted as a whole
+# An idle leader sends an empty control message this often: the workers block in a gloo broadcast
+# between iterations, and a broadcast that waits past the group's timeout (torch default 30 min)
+# raises -- which the failure policy would turn into a needless group restart.
+HEARTBEAT_S = float(os.environ.get("VWA_TP_HEARTBEAT_S", "5"))
 
 
 def _default_fatal(exc: BaseException) -> None:
@@ -53,7 +57,8 @@ class TPIntentEngine:
 
     name = "llm-tp"
 
-    def __init__(self, inner, tp, ctl_group=None, on_fatal: Optional[Callable[[BaseException], None]] = None):
+    def __init__(self, inner, tp, ctl_group=None, on_fatal: Optional[Callable[[BaseException], None]] = None,
+                 heartbeat_s: Optional[float] = None):
         import torch.distributed as dist
 
         self.inner = inner
@@ -67,6 +72,8 @@ class TPIntentEngine:
         self._stop = False
         self.iterations = 0
         self.control_msgs = 0
+        self.heartbeats = 0
+        self.heartbeat_s = HEARTBEAT_S if heartbeat_s is None else heartbeat_s
 
     # ------------------------------------------------------------------ shared
     @property
@@ -159,8 +166,13 @@ class TPIntentEngine:
             torch.cuda.set_device(inner._cuda_index)
         while True:
             with self._cv:
+                idle = False
                 while not self._stop and not self._incoming and not inner.has_work():
-                    self._cv.wait()
+                    if not self._cv.wait(timeout=self.heartbeat_s):
+                        idle = True  # nothing arrived for a heartbeat period: keep the workers' wait short
+                        break
+                if idle and not self._stop and not self._incoming and not inner.has_work():
+                    self.heartbeats += 1
                 # admit at most what fits next to the active set; the rest waits for later iterations
                 room = max(0, inner.max_active - len(inner.active) - len(inner.waiting))
                 new = [self._incoming.popleft() for _ in range(min(room, len(self._incoming)))]

@@ -33,12 +33,13 @@ def _free_port() -> int:
     return port
 
 
-def _spawn(module: str, env_extra: dict, torchrun_nproc: int = 0) -> subprocess.Popen:
+def _spawn(module: str, env_extra: dict, torchrun_nproc: int = 0, restart: int = 0) -> subprocess.Popen:
     env = dict(os.environ)
     env.update(env_extra)
     if torchrun_nproc > 1:
-        # a fresh rendezvous port per (re)start: the previous group's port may still be in TIME_WAIT
-        port = env.get("VWA_MASTER_PORT") or str(_free_port())
+        # VWA_MASTER_PORT only for the first start: a restarted group gets a fresh rendezvous port
+        # (the previous group's port may still be in TIME_WAIT)
+        port = (env.get("VWA_MASTER_PORT") if restart == 0 else None) or str(_free_port())
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={torchrun_nproc}",
                "--master-addr", "127.0.0.1", "--master-port", port, "-m", module]
     else:
@@ -53,35 +54,47 @@ class Supervisor:
     in FRESH processes -- never re-exec'd from a process that touched the GPU -- with exponential
     backoff, at most ``max_restarts`` times per ``window_s``; the other services keep running
     meanwhile (voice answers brain errors as the reference does).  Any other exit, or a restart
-    budget spent, stops everything."""
+    budget spent, stops everything.  The backoff is a scheduled restart time, not a sleep: the
+    other services (and SIGTERM) are still watched while a restart is pending."""
 
     def __init__(self, spawn=None, max_restarts: int = 5, window_s: float = 600.0, backoff_s: float = 1.0,
-                 clock=time.monotonic, sleep=time.sleep, log=print):
+                 clock=time.monotonic, log=print):
         self.spawn = spawn or _spawn
         self.max_restarts = max_restarts
         self.window_s = window_s
         self.backoff_s = backoff_s
         self.clock = clock
-        self.sleep = sleep
         self.log = log
-        self.services = []  # [name, args, restartable, proc, restart times]
+        # [name, args, restartable, proc, restart times, restart due at (None: running), restarts]
+        self.services = []
 
     def add(self, name: str, module: str, env_extra: dict, torchrun_nproc: int = 0, restartable: bool = False):
         proc = self.spawn(module, env_extra, torchrun_nproc)
-        self.services.append([name, (module, env_extra, torchrun_nproc), restartable, proc, []])
+        self.services.append([name, (module, env_extra, torchrun_nproc), restartable, proc, [], None, 0])
         return proc
 
     def procs(self):
         return [s[3] for s in self.services]
 
+    def pending_restarts(self) -> int:
+        return sum(1 for s in self.services if s[5] is not None)
+
     def poll_once(self) -> bool:
-        """Check every service once; restart what may be restarted.  False = stop everything."""
+        """Check every service once; schedule / perform the restarts that are allowed.  Never blocks.
+        False = stop everything."""
+        now = self.clock()
         for svc in self.services:
-            name, args, restartable, proc, times = svc
+            name, args, restartable, proc, times, due, n = svc
+            if due is not None:
+                if now >= due:
+                    svc[5] = None
+                    svc[6] = n + 1
+                    times.append(now)
+                    svc[3] = self.spawn(*args, restart=n + 1)
+                continue
             rc = proc.poll()
             if rc is None:
                 continue
-            now = self.clock()
             times[:] = [t for t in times if now - t < self.window_s]
             if not restartable or len(times) >= self.max_restarts:
                 self.log(f"[launch] {name} exited with {rc}; stopping" +
@@ -90,12 +103,12 @@ class Supervisor:
             delay = self.backoff_s * (2 ** len(times))
             self.log(f"[launch] {name} exited with {rc}; restarting it in fresh processes in {delay:.1f} s "
                      f"(restart {len(times) + 1}/{self.max_restarts})")
-            self.sleep(delay)
-            times.append(now)
-            svc[3] = self.spawn(*args)
+            svc[5] = now + delay
         return True
 
     def stop(self) -> None:
+        for svc in self.services:
+            svc[5] = None  # (a pending restart is cancelled)
         for p in self.procs():
             if p.poll() is None:
                 p.send_signal(signal.SIGTERM)
