@@ -12,8 +12,10 @@ ENGINE latency (audio fully received -> validated intent); `parity_p50_ms` adds 
 reference's fixed 1000 ms debounce (apps/voice/src/server.ts:229).
 
 Multi-GPU (torchrun, one process per GPU, RCCL): weak scaling -- every rank serves its own
-voice sessions (ASR data-parallel, one LLM replica per rank, or TP groups with --tp);
-the reported p50 is over ALL sessions of all ranks.
+voice sessions (ASR data-parallel, one LLM replica per rank), or with --tp every TP group serves
+them through the served control plane (brain/tp_engine.TPIntentEngine: the group leader runs the
+sessions, its peers follow the leader's scheduler iterations in lockstep); the reported p50 is
+over ALL sessions of all ranks / groups.
 
 Data: synthetic speech-like audio, random-init weights of the named architectures.
 """
@@ -37,6 +39,7 @@ from voice_enabled_browser_automation_amd import ops  # noqa: E402
 from voice_enabled_browser_automation_amd.asr.engine import AsrEngine  # noqa: E402
 from voice_enabled_browser_automation_amd.brain.intent_engine import LLMIntentEngine  # noqa: E402
 from voice_enabled_browser_automation_amd.brain.prompt import COMMANDS  # noqa: E402
+from voice_enabled_browser_automation_amd.brain.tp_engine import TPIntentEngine  # noqa: E402
 from voice_enabled_browser_automation_amd.contracts import ParseResponse, safe_parse  # noqa: E402
 from voice_enabled_browser_automation_amd.models.config import get_config  # noqa: E402
 from voice_enabled_browser_automation_amd.models.llama import LlamaModel  # noqa: E402
@@ -44,6 +47,7 @@ from voice_enabled_browser_automation_amd.models.whisper import WhisperModel  # 
 from voice_enabled_browser_automation_amd.parallel.tp import init_distributed  # noqa: E402
 from voice_enabled_browser_automation_amd.runtime.engine import LLMEngine  # noqa: E402
 from voice_enabled_browser_automation_amd.tokenizer import load_tokenizer  # noqa: E402
+from voice_enabled_browser_automation_amd.utils.env import knob  # noqa: E402
 
 METRIC = "voice-to-intent p50 latency (ms) + ASR RTF; 10s utterance; Llama-3-8B brain"
 
@@ -65,7 +69,48 @@ def synth_speech(seconds: float, seed: int, rate: int = 16000) -> np.ndarray:
     return (sig * 32767).astype(np.int16)
 
 
-def run_concurrent(args, C, asr, brain, utterances, asr_tokens, world):
+def _sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
+def drive_sessions(brain, tp, world: int, n: int, one, start: int = 0):
+    """Run n voice commands through ``one(i)`` between world barriers, as the served deployment
+    does: without TP every rank runs its own; with TP (``brain`` a TPIntentEngine) the group
+    leader runs them and its peers follow the leader's scheduler iterations in lockstep
+    (``worker_loop``) until the leader stops the group.  -> (results of the leader / every DP
+    rank, wall-clock ms between the barriers)."""
+    follower = tp.size > 1 and tp.rank != 0
+    _sync()
+    if world > 1:
+        torch.distributed.barrier()
+    _sync()
+    t0 = time.perf_counter()
+    out = []
+    if follower:
+        brain.worker_loop()
+    else:
+        for i in range(n):
+            out.append(one(start + i))
+        if tp.size > 1:
+            brain.stop()
+    _sync()
+    if world > 1:
+        torch.distributed.barrier()
+    _sync()
+    return out, (time.perf_counter() - t0) * 1e3
+
+
+def gather(obj, world: int):
+    """Every rank's object (rank order); followers contribute empty results."""
+    if world == 1:
+        return [obj]
+    out = [None] * world
+    torch.distributed.all_gather_object(out, obj)
+    return out
+
+
+def run_concurrent(args, C, asr, brain, utterances, asr_tokens, world, tp):
     """C voice sessions arriving together on every rank: one batched ASR pass, then all C intent
     parses decoded with continuous batching.  Per-session latency = ASR batch + that session's
     parse completion.  Not part of the headline value."""
@@ -83,34 +128,21 @@ def run_concurrent(args, C, asr, brain, utterances, asr_tokens, world):
         ok = sum(safe_parse(ParseResponse, o).success for o in outs)
         return [t_asr + b["latency_ms"] for b in brain.last_batch], ok
 
-    round_(0)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    t0 = time.perf_counter()
-    lat, ok = [], 0
+    drive_sessions(brain, tp, world, 1, round_)  # warm-up round
     it0 = dict(brain.batch_stats)
     tm0 = dict(getattr(brain, "timing", {}))
     asr_ms.clear()
-    for k in range(args.steps):
-        l, o = round_(k + 1)
-        lat += l
-        ok += o
-    torch.cuda.synchronize()
-    el = (time.perf_counter() - t0) * 1e3
+    rounds, el = drive_sessions(brain, tp, world, args.steps, round_, start=1)
+    lat = [x for l, _o in rounds for x in l]
+    ok = sum(o for _l, o in rounds)
     bs = {k: brain.batch_stats[k] - it0.get(k, 0) for k in ("iterations", "rows", "sampled")}
-    t = torch.tensor([el, float(ok)] + lat, dtype=torch.float64, device=torch.device("cuda", torch.cuda.current_device()))
-    if world > 1:
-        allt = [torch.zeros_like(t) for _ in range(world)]
-        torch.distributed.all_gather(allt, t)
-    else:
-        allt = [t]
-    all_lat = [float(x) for a in allt for x in a[2:]]
-    el_max = max(float(a[0]) for a in allt)
+    allr = gather({"el": el, "ok": ok, "lat": lat}, world)
+    all_lat = [x for a in allr for x in a["lat"]]
+    el_max = max(a["el"] for a in allr)
     return {"sessions_per_rank": C, "p50_ms": round(statistics.median(all_lat), 3),
             "p90_ms": round(float(np.percentile(all_lat, 90)), 3),
             "throughput_utt_per_s": round(len(all_lat) / (el_max / 1e3), 3),
-            "valid_intents": f"{sum(int(a[1]) for a in allt)}/{len(all_lat)}",
+            "valid_intents": f"{sum(a['ok'] for a in allr)}/{len(all_lat)}",
             "rows_per_iteration": round(bs["rows"] / max(1, bs["iterations"]), 2),
             "samples_per_iteration": round(bs["sampled"] / max(1, bs["iterations"]), 2),
             "iterations_per_round": round(bs["iterations"] / max(1, args.steps), 1),
@@ -148,21 +180,23 @@ def spawn_ranks(n: int) -> int:
 
 
 def main():
+    # strict native mode: an op that would fall back to a vendor library raises (ops.vendor_fallback)
+    os.environ.setdefault("VWA_STRICT_NATIVE", "1")
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--asr", default=os.environ.get("VWA_ASR_MODEL", "whisper-tiny"))
-    ap.add_argument("--llm", default=os.environ.get("VWA_LLM_MODEL", "llama3-8b"))
-    ap.add_argument("--tp", type=int, default=int(os.environ.get("VWA_TP", "1")))
+    ap.add_argument("--asr", default=knob("VWA_ASR_MODEL"))
+    ap.add_argument("--llm", default=knob("VWA_LLM_MODEL"))
+    ap.add_argument("--tp", type=int, default=knob("VWA_TP"))
     ap.add_argument("--audio-s", type=float, default=10.0)
     ap.add_argument("--asr-tokens-per-s", type=float, default=4.0)
     ap.add_argument("--budget-chars", type=int, default=512)
     ap.add_argument("--debounce-ms", type=float, default=1000.0, help="reference debounce added for parity_p50_ms")
-    ap.add_argument("--concurrent", type=int, default=int(os.environ.get("VWA_BENCH_CONCURRENT", "0")),
+    ap.add_argument("--concurrent", type=int, default=knob("VWA_BENCH_CONCURRENT"),
                     help="also measure C concurrent voice sessions per rank (batched ASR + continuous-batched "
                          "intent decoding); reported under 'concurrent', outside the headline value")
-    ap.add_argument("--dtype", default=os.environ.get("VWA_DTYPE", "bf16"), choices=("bf16", "fp8"),
+    ap.add_argument("--dtype", default=knob("VWA_DTYPE"), choices=("bf16", "fp8"),
                     help="LLM weight dtype: bf16 (headline config) or fp8 (W8A8 on the fp8 MFMA, config 5)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--verbose", action="store_true")
@@ -180,7 +214,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (MI355X)")
-    if os.environ.get("VWA_DIST_BACKEND", "nccl") != "nccl":
+    if (knob("VWA_DIST_BACKEND") or "nccl") != "nccl":
         local = local % torch.cuda.device_count()  # gloo rehearsal on fewer GPUs than ranks
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -197,6 +231,8 @@ def main():
     brain = LLMIntentEngine(engine, load_tokenizer("llama3"), budget_chars=args.budget_chars, temperature=0.1,
                             seed=1234)  # every replica does the same work (weak scaling; TP lockstep)
     engine.capture_all()
+    if tp.size > 1:  # the served TP control plane (brain/server.py uses the same engine)
+        brain = TPIntentEngine(brain, tp)
     torch.cuda.synchronize()
     load_s = time.time() - t_load
 
@@ -219,41 +255,30 @@ def main():
         t1 = time.perf_counter()
         return (t1 - t0) * 1e3, (t_asr - t0) * 1e3, ok
 
-    for i in range(args.warmup):
-        one(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    lat, asr_ms, oks, llm_stats = [], [], [], []
+    drive_sessions(brain, tp, world, args.warmup, one)
     tm0, it0 = dict(brain.timing), brain.batch_stats["iterations"]
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        l, a, ok = one(args.warmup + i)
-        lat.append(l)
-        asr_ms.append(a)
-        oks.append(ok)
-        llm_stats.append(dict(brain.last_stats))
+
+    def timed_one(i):
+        r = one(i)
+        stats = dict(brain.last_stats)
         if args.verbose and rank == 0:
-            print(json.dumps({"step": i, "latency_ms": round(l, 2), "asr_ms": round(a, 2), **brain.last_stats}),
-                  flush=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    elapsed = (time.perf_counter() - t_start) * 1e3
+            print(json.dumps({"step": i - args.warmup, "latency_ms": round(r[0], 2), "asr_ms": round(r[1], 2),
+                              **stats}), flush=True)
+        return r + (stats,)
+
+    res_steps, elapsed = drive_sessions(brain, tp, world, args.steps, timed_one, start=args.warmup)
+    lat = [r[0] for r in res_steps]
+    asr_ms = [r[1] for r in res_steps]
+    oks = [r[2] for r in res_steps]
+    llm_stats = [r[3] for r in res_steps]
     n_it = max(1, brain.batch_stats["iterations"] - it0)
     host_us = {k.replace("_ms", "_us"): round((brain.timing[k] - tm0[k]) * 1e3 / n_it, 1) for k in tm0}
 
-    conc = run_concurrent(args, C, asr, brain, utterances, asr_tokens, world) if C > 1 else None
+    conc = run_concurrent(args, C, asr, brain, utterances, asr_tokens, world, tp) if C > 1 else None
 
-    # gather every session's latency across ranks (weak scaling: p50 over all sessions)
-    local_t = torch.tensor([elapsed] + lat + asr_ms + [float(sum(oks))], dtype=torch.float64, device=dev)
-    if world > 1:
-        allt = [torch.zeros_like(local_t) for _ in range(world)]
-        torch.distributed.all_gather(allt, local_t)
-    else:
-        allt = [local_t]
+    # gather every session's latency across ranks (weak scaling: p50 over all sessions; TP
+    # followers ran no sessions of their own)
+    allr = gather({"el": elapsed, "lat": lat, "asr": asr_ms, "ok": int(sum(oks))}, world)
     # evidence that the collective backend really saw every rank on its own GPU
     rccl_world, n_devices, backend = 1, 1, None
     if world > 1:
@@ -266,10 +291,10 @@ def main():
         torch.distributed.all_gather(ids, ident)
         n_devices = len({tuple(a.tolist()) for a in ids})
     K = args.steps
-    elapsed_max = max(float(t[0]) for t in allt)
-    all_lat = [float(x) for t in allt for x in t[1 : 1 + K]]
-    all_asr = [float(x) for t in allt for x in t[1 + K : 1 + 2 * K]]
-    n_ok = sum(int(t[-1]) for t in allt)
+    elapsed_max = max(a["el"] for a in allr)
+    all_lat = [x for a in allr for x in a["lat"]]
+    all_asr = [x for a in allr for x in a["asr"]]
+    n_ok = sum(a["ok"] for a in allr)
     if rank == 0:
         p50 = statistics.median(all_lat)
         rtf = statistics.median(all_asr) / (args.audio_s * 1e3)

@@ -86,7 +86,7 @@ SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<T
   check_contig_rows(x, "x");
   TORCH_CHECK(w.is_contiguous() && w.dim() == 2, "w must be contiguous [N, K]");
   TORCH_CHECK(x.size(1) == w.size(1), "K mismatch: x ", x.sizes(), " w ", w.sizes());
-  TORCH_CHECK(x.size(0) >= 1 && x.size(0) <= 64, "skinny_gemm supports 1..64 rows, got ", x.size(0));
+  TORCH_CHECK(x.size(0) >= 1 && x.size(0) <= 16, "skinny_gemm supports 1..16 rows (more: the tiled GEMM), got ", x.size(0));
   TORCH_CHECK(w.size(1) % 128 == 0, "K must be a multiple of 128");
   if (bias.has_value()) {
     check_bf16(*bias, "bias");
@@ -201,16 +201,8 @@ int device_cus(const Tensor& t) {
 // add (+bias), 2 SwiGLU over interleaved gate/up tiles (y [M, N/2]), 3 GELU (+bias).  rstd: f32
 // [M] per-row RMSNorm scale applied to the product (gammas folded into w).  ws: f32 split-K
 // workspace (the launcher splits K only when the output tiles alone cannot fill the CUs).
-static void set_tickets(GemmParams& p, const c10::optional<Tensor>& tickets) {
-  if (!tickets.has_value()) return;
-  TORCH_CHECK(tickets->is_cuda() && tickets->scalar_type() == at::kInt && tickets->is_contiguous(),
-              "tickets: zeroed int32 counters");
-  p.tickets = tickets->data_ptr<int>();
-  p.n_tickets = (int)tickets->numel();
-}
-
 void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi, c10::optional<Tensor> rstd,
-          c10::optional<Tensor> residual, bool w_tiled, c10::optional<Tensor> ws, c10::optional<Tensor> tickets) {
+          c10::optional<Tensor> residual, bool w_tiled, c10::optional<Tensor> ws) {
   c10::DeviceGuard g(x.device());
   check_bf16(x, "x");
   check_bf16(w, "w");
@@ -266,19 +258,14 @@ void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi,
     p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws->numel(), 0);
     p.ws_cap = ws->numel();
   }
-  set_tickets(p, tickets);
   p.cus = device_cus(x);
   check_rc(vwa_gemm((int)epi, &p, cur_stream(x)), "gemm");
 }
 
 // W8A8 tiled GEMM (gemm.hip, F8): x8 OCP e4m3 [M, K] with per-row scales sx (quant_fp8_rows),
 // w8 the fp8 tiled layout [N, K] with per-row scales sw.
-// q8 / q_sx / q_rstd (optional): the output rows quantised for the next W8A8 GEMM in the split-K
-// reduce (gemm_reduce_rowq_kernel); returns whether that happened (no split: the caller quantises).
-bool gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> bias, Tensor y, int64_t epi,
-              c10::optional<Tensor> rstd, c10::optional<Tensor> residual, c10::optional<Tensor> ws,
-              c10::optional<Tensor> tickets, c10::optional<Tensor> q8, c10::optional<Tensor> q_sx,
-              c10::optional<Tensor> q_rstd, double q_eps) {
+void gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> bias, Tensor y, int64_t epi,
+              c10::optional<Tensor> rstd, c10::optional<Tensor> residual, c10::optional<Tensor> ws) {
   c10::DeviceGuard g(x8.device());
   TORCH_CHECK(x8.is_cuda() && x8.scalar_type() == at::kFloat8_e4m3fn && x8.dim() == 2 && x8.stride(1) == 1 &&
                   x8.stride(0) % 16 == 0 && (reinterpret_cast<uintptr_t>(x8.data_ptr()) & 15) == 0,
@@ -334,27 +321,7 @@ bool gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> 
     p.ws = ws->data_ptr<float>();
     p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x8), ws->numel(), 1);
   }
-  set_tickets(p, tickets);
-  if (q8.has_value()) {
-    const int64_t nout = epi == 2 ? p.N / 2 : p.N;
-    TORCH_CHECK(q8->is_cuda() && q8->scalar_type() == at::kFloat8_e4m3fn && q8->dim() == 2 && q8->size(0) == p.M &&
-                    q8->size(1) == nout && q8->stride(1) == 1 && q8->stride(0) % 16 == 0 &&
-                    (reinterpret_cast<uintptr_t>(q8->data_ptr()) & 15) == 0,
-                "q8: fp8 [M, output columns], 16-byte aligned rows");
-    TORCH_CHECK(q_sx.has_value() && q_sx->scalar_type() == at::kFloat && q_sx->numel() >= p.M, "q_sx f32 [M]");
-    p.q8 = reinterpret_cast<uint8_t*>(q8->data_ptr());
-    p.ldq8 = (int)q8->stride(0);
-    p.q_sx = q_sx->data_ptr<float>();
-    if (q_rstd.has_value()) {
-      TORCH_CHECK(q_rstd->scalar_type() == at::kFloat && q_rstd->numel() >= p.M, "q_rstd f32 [M]");
-      p.q_rstd = q_rstd->data_ptr<float>();
-    }
-    p.q_eps = (float)q_eps;
-  }
-  const int rc = vwa_gemm((int)epi, &p, cur_stream(x8));
-  if (rc == 2) return true;
-  check_rc(rc, "gemm_fp8");
-  return false;
+  check_rc(vwa_gemm((int)epi, &p, cur_stream(x8)), "gemm_fp8");
 }
 
 void check_cache(const Tensor& c, const char* name);
@@ -363,7 +330,7 @@ void check_cache(const Tensor& c, const char* name);
 // EPI_QKV; > 16 rows): x bf16 (sx null) or fp8 codes x8 with per-row scales sx (W8A8, w fp8 tiled
 // with row scales sw).  Replaces gemm -> qkv scratch -> rope_kv_write.
 void gemm_qkv(Tensor x, c10::optional<Tensor> sx, Tensor w, c10::optional<Tensor> sw, c10::optional<Tensor> bias,
-              c10::optional<Tensor> rstd, bool w_tiled, Tensor ws, c10::optional<Tensor> tickets, int64_t n_q_heads,
+              c10::optional<Tensor> rstd, bool w_tiled, Tensor ws, int64_t n_q_heads,
               int64_t n_kv_heads, int64_t head_dim, bool use_rope, Tensor positions, Tensor slots,
               c10::optional<Tensor> rope, Tensor q_out, Tensor k_cache, Tensor v_cache) {
   c10::DeviceGuard g(x.device());
@@ -432,7 +399,6 @@ void gemm_qkv(Tensor x, c10::optional<Tensor> sx, Tensor w, c10::optional<Tensor
   p.ws = ws.data_ptr<float>();
   p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws.numel(), f8 ? 1 : 0);
   p.ws_cap = ws.numel();
-  set_tickets(p, tickets);
   p.cus = device_cus(x);
   check_rc(vwa_gemm(5, &p, cur_stream(x)), "gemm_qkv");
 }
@@ -589,8 +555,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                                        c10::optional<Tensor> a_part_ml, c10::optional<Tensor> a_counters,
                                        bool w_tiled, c10::optional<Tensor> a_row_table,
                                        c10::optional<Tensor> s_o, c10::optional<Tensor> s_gu,
-                                       c10::optional<Tensor> s_down, c10::optional<Tensor> s_qkv, int64_t tp_ar,
-                                       int64_t tail_n) {
+                                       c10::optional<Tensor> s_down, c10::optional<Tensor> s_qkv, int64_t tp_ar) {
   c10::DeviceGuard g(h.device());
   const int64_t M = h.size(0);
   TORCH_CHECK(att.size(0) == M && act.size(0) == M, "row counts differ");
@@ -621,11 +586,6 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   cp.n = 3;
   cp.seq = 0;
   chain_schedule(cp);
-  // tail_n == 2: o_proj -> gate/up only (5..16 rows: both X row blocks fit LDS; the down
-  // projection, whose 14336-wide X does not, stays a streaming launch)
-  TORCH_CHECK(tail_n == 0 || (tail_n == 2 && !w_qkv.has_value() && !tp_ar && !s_o.has_value()),
-              "chain tail_n: 0 or 2 (bf16, no QKV, no TP)");
-  if (tail_n == 2) cp.n = 2;
   if (w_qkv.has_value()) {
     TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
                     v_cache.has_value(),
@@ -1270,13 +1230,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_n_splits") = 0, py::arg("a_part_o") = py::none(), py::arg("a_part_ml") = py::none(),
         py::arg("a_counters") = py::none(), py::arg("w_tiled") = false, py::arg("a_row_table") = py::none(),
         py::arg("s_o") = py::none(), py::arg("s_gu") = py::none(), py::arg("s_down") = py::none(),
-        py::arg("s_qkv") = py::none(), py::arg("tp_ar") = 0, py::arg("tail_n") = 0);
+        py::arg("s_qkv") = py::none(), py::arg("tp_ar") = 0);
   m.def("set_small_gemm_bytes", &set_small_gemm_bytes);
   m.def("gemm_set_p8", [](int64_t mode) { vwa_gemm_set_p8((int)mode); });
-  m.def("gemm_set_nb", [](int64_t nb) { vwa_gemm_set_nb((int)nb); });
-  m.def("skinny_set_xg_rows", [](int64_t rows) { vwa_skinny_set_xg_rows((int)rows); });
-  m.def("skinny_set_grid_adapt", [](int64_t on) { vwa_skinny_set_grid_adapt((int)on); });
-  m.def("skinny_set_nt2_rows", [](int64_t rows) { vwa_skinny_set_nt2_rows((int)rows); });
   m.def("skinny_set_x_skew", [](int64_t skew) { vwa_skinny_set_x_skew((int)skew); });
   m.def("gemm_set_split_fill", [](int64_t pct) { vwa_gemm_set_split_fill((int)pct); });
   m.def("chain_make_seq", &chain_make_seq, py::arg("seq"), py::arg("X"), py::arg("W"), py::arg("bias"),
@@ -1289,13 +1245,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_advance", &decode_advance);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
         py::arg("rstd") = py::none(), py::arg("residual") = py::none(), py::arg("w_tiled") = false,
-        py::arg("ws") = py::none(), py::arg("tickets") = py::none());
+        py::arg("ws") = py::none());
   m.def("row_rstd", &row_rstd);
   m.def("gemm_qkv", &gemm_qkv);
   m.def("gemm_fp8", &gemm_fp8, py::arg("x8"), py::arg("sx"), py::arg("w8"), py::arg("sw"), py::arg("bias"),
         py::arg("y"), py::arg("epi"), py::arg("rstd") = py::none(), py::arg("residual") = py::none(),
-        py::arg("ws") = py::none(), py::arg("tickets") = py::none(), py::arg("q8") = py::none(),
-        py::arg("q_sx") = py::none(), py::arg("q_rstd") = py::none(), py::arg("q_eps") = 1e-5);
+        py::arg("ws") = py::none());
   m.def("rmsnorm", &rmsnorm);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);

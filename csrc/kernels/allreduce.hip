@@ -16,7 +16,12 @@
 //      raises an error word instead of hanging the GPU);
 //   4. acquire (system-scope fence) and sum the chunk of all ranks' staging buffers in rank
 //      order (bit-identical result on every rank) into the output.
-// Buffers come from hipMalloc and are shared with hipIpcGetMemHandle / hipIpcOpenMemHandle.
+// The IPC-shared buffers (staging, gather, chain regions, flags) are allocated L2-UNCACHED
+// (hipExtMallocWithFlags hipDeviceMallocUncached; vwa_ar_create checks the type with
+// hipPointerGetAttributes): a peer GPU reads them over xGMI while this GPU's L2 could otherwise
+// still hold the newest stores -- with uncached memory every store and flag goes to HBM, and no
+// correctness argument leans on the system-scope fences' L2 write-back.  Shared with
+// hipIpcGetMemHandle / hipIpcOpenMemHandle (dmabuf).
 //
 // Behind the gather region: two f32 regions of the chained decode layer's in-launch all-reduce
 // rounds (skinny_stream.hip chain_tp_reduce; vwa_ar_chain_tp hands the pointers to the chain).
@@ -139,6 +144,20 @@ struct ArState {
 
 }  // namespace
 
+// L2-uncached device memory for the cross-device hand-offs, its type asserted
+static int alloc_uncached(void** p, size_t bytes) {
+  *p = nullptr;
+  if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached) != hipSuccess) return -1;
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, *p) != hipSuccess || a.type != hipMemoryTypeDevice ||
+      (a.allocationFlags & hipDeviceMallocUncached) != hipDeviceMallocUncached) {
+    (void)hipFree(*p);
+    *p = nullptr;
+    return -2;
+  }
+  return 0;
+}
+
 extern "C" {
 
 // Allocate the local IPC-shareable buffers; returns an opaque state pointer (nullptr on error).
@@ -148,13 +167,19 @@ void* vwa_ar_create(int rank, int world, int64_t max_elems) {
   s->rank = rank;
   s->world = world;
   s->max_elems = max_elems;
-  if (hipMalloc(&s->staging, 2 * max_elems * sizeof(uint16_t) + 2 * kGatherWords * sizeof(int) +
-                                 2 * kChainFloats * sizeof(float)) != hipSuccess ||
-      hipMalloc(&s->flags, kSlots * kMaxRanks * sizeof(int)) != hipSuccess ||
+  void* stg = nullptr;
+  void* flg = nullptr;
+  if (alloc_uncached(&stg, 2 * max_elems * sizeof(uint16_t) + 2 * kGatherWords * sizeof(int) +
+                               2 * kChainFloats * sizeof(float)) != 0 ||
+      alloc_uncached(&flg, kSlots * kMaxRanks * sizeof(int)) != 0 ||
       hipMalloc(&s->epochs, kSlots * sizeof(int)) != hipSuccess || hipMalloc(&s->error, sizeof(int)) != hipSuccess) {
+    if (stg) (void)hipFree(stg);
+    if (flg) (void)hipFree(flg);
     delete s;
     return nullptr;
   }
+  s->staging = static_cast<uint16_t*>(stg);
+  s->flags = static_cast<int*>(flg);
   (void)hipMemset(s->flags, 0, kSlots * kMaxRanks * sizeof(int));
   (void)hipMemset(s->epochs, 0, kSlots * sizeof(int));
   (void)hipMemset(s->error, 0, sizeof(int));

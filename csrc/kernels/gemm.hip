@@ -285,13 +285,8 @@ VWA_DEVICE void qkv_store(const GemmParams& p, int m, int n, const float (&o)[8]
   *reinterpret_cast<uint4*>((is_v ? p.v_cache : p.k_cache) + idx + d) = pack8(y);
 }
 
-// f32 partial slabs of the one-launch split-K: write-through (sc1) stores / L2-missing (sc1) loads
-// -- the slices of a tile may run on different XCDs, whose L2s are not coherent with each other
-VWA_DEVICE void st_wt_f32(__amdgpu_buffer_rsrc_t r, size_t idx, float v) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)(idx * 4), 0, 16);
-}
-// AUX 16: sc1 (the one-launch split-K's cross-XCD hand-off); 0: plain (the reduce kernel, after
-// the GEMM launch's end made the slabs visible)
+// f32 partial slab loads of the split-K reduce (AUX: buffer cache bits; the reduce runs after the
+// GEMM launch's end made the slabs visible, so plain loads)
 template <int AUX>
 VWA_DEVICE float4 ld_f4(__amdgpu_buffer_rsrc_t r, size_t idx) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(idx * 4), 0, AUX));
@@ -350,9 +345,9 @@ VWA_DEVICE void sum_items(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int m
   }
 }
 
-// epilogue of one summed item + its stores; keep (optional): the stored bf16 values as floats
+// epilogue of one summed item + its stores
 template <int EPI>
-VWA_DEVICE void finish_item(const GemmParams& p, int m, int c, const float (&a)[8], float (&b)[8], float* keep) {
+VWA_DEVICE void finish_item(const GemmParams& p, int m, int c, const float (&a)[8], float (&b)[8]) {
   const float rs = (p.rstd ? p.rstd[m] : 1.f) * (p.sx ? p.sx[m] : 1.f);
   const int n0 = item_src0<EPI>(c), n1 = item_src1<EPI>(c);
   float v[8];
@@ -386,9 +381,7 @@ VWA_DEVICE void finish_item(const GemmParams& p, int m, int c, const float (&a)[
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += r[e];
   }
-  const uint4 packed = pack8(v);
-  *reinterpret_cast<uint4*>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + c) = packed;
-  if (keep) unpack8(packed, keep);  // the stored (bf16-rounded) values, for the row quantisation
+  *reinterpret_cast<uint4*>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + c) = pack8(v);
 }
 
 template <int EPI, int AUX>
@@ -397,29 +390,13 @@ VWA_DEVICE void reduce_item(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int
   const bool ok[1] = {true};
   float a[1][8], b[1][8];
   sum_items<EPI, AUX, 1, 4>(p, rws, m, cc, ok, a, b);
-  finish_item<EPI>(p, m, c, a[0], b[0], nullptr);
+  finish_item<EPI>(p, m, c, a[0], b[0]);
 }
 
-// The last-arriving slice of output tile (bm, bn) (one-launch split-K): every item of the tile's
-// valid rows
-template <int EPI>
-VWA_DEVICE void split_reduce_tile(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int bm, int bn, int BM, int BN,
-                                  int nthreads) {
-  constexpr bool SW = EPI == EPI_SWIGLU;
-  const int cpr = (SW ? BN / 2 : BN) / 8;  // 8-wide output chunks per tile row
-  const int rows = min(BM, p.M - bm);
-  const int ncols = SW ? p.N / 2 : p.N;
-  for (int it = threadIdx.x; it < rows * cpr; it += nthreads) {
-    const int c = (SW ? bn / 2 : bn) + (it % cpr) * 8;
-    if (c < ncols) reduce_item<EPI, 16>(p, rws, bm + it / cpr, c);
-  }
-}
-
-// NB (128^2 kernel): LDS stage buffers.  2: the next stage's DMA in flight during this one's MFMAs
-// (2 workgroups per CU -- prompt-sized GEMMs).  4: up to four stages in flight -- few-row GEMMs
-// (one row block, weight streaming) whose short split-K slices are latency-bound with two (a
-// 4-stage slice of the 32-row fp8 o_proj measured 2 TB/s); 128 KB LDS, one workgroup per CU.
-template <class C, int EPI, bool WT, bool F8 = false, bool P8 = false, int NB = 2>
+// (round 4's 4-stage variant for one-row-block GEMMs measured slower in whole decode steps -- 128 KB
+// of LDS leaves one workgroup per CU, so split-K grids above 256 workgroups ran in two rounds:
+// fp8 32 rows 4.97 vs 4.36 ms, profiles/r4_gemm_ab.md -- and was removed in round 5)
+template <class C, int EPI, bool WT, bool F8 = false, bool P8 = false>
 __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   constexpr int FM = C::FM, FN = C::FN;
@@ -526,23 +503,6 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
       asm volatile("s_barrier" ::: "memory");
     }
     if (wm == 0) asm volatile("s_barrier" ::: "memory");  // (group 1 started one barrier later)
-  } else if constexpr (NB > 2) {
-    static_assert(NB <= 4, "vmcnt cases below");
-#pragma unroll
-    for (int i = 0; i < NB; ++i)
-      if (i < nh) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + i, lds + i * C::STAGE);
-    for (int i = 0; i < nh; ++i) {
-      // stage i landed everywhere: the stages issued after it (8 DMA instructions each) may stay
-      // in flight
-      const int ahead = min(NB - 1, nh - 1 - i);
-      if (ahead >= 3) asm volatile("s_waitcnt vmcnt(24)\n\ts_barrier" ::: "memory");
-      else if (ahead == 2) asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      compute_stage<C, F8>(lds + (i % NB) * C::STAGE, acc, wm, wn);
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done reading it
-      if (i + NB < nh) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + i + NB, lds + (i % NB) * C::STAGE);
-    }
   } else {
   if (nh > 0) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0, lds);
   if (nh > 1) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + 1, lds + C::STAGE);
@@ -559,39 +519,6 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
   const int l = lane_id();
   const int col0 = bn + wn * FN * 16 + (l & 15);
   const int row0 = bm + wm * FM * 16 + 4 * (l >> 4);
-  if (p.splits > 1 && p.tickets != nullptr) {
-    // one-launch split-K: partial slab written through to memory, then one arrival count per
-    // tile; the last slice (any XCD) reads the slabs back past its L2 and runs the epilogue
-    const __amdgpu_buffer_rsrc_t rws = rsrc(p.ws, (size_t)p.splits * p.M * p.N * 4);
-    const size_t zb = (size_t)split * p.M * p.N;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = row0 + i * 16 + r;
-        if (m >= p.M) continue;
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int n = col0 + j * 16;
-          if (n < p.N) st_wt_f32(rws, zb + (size_t)m * p.N + n, acc[i][j][r]);
-        }
-      }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partials reached memory
-    __syncthreads();
-    int* s_last = reinterpret_cast<int*>(lds);  // the stage images are dead (the k loop's last barrier)
-    if (threadIdx.x == 0) {
-      int* t = p.tickets + lt;
-      const int ticket = __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = ticket == p.splits - 1;
-      if (last) __hip_atomic_store(t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *s_last = last;
-    }
-    __syncthreads();
-    if (!*s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // only orders the slab loads after the ticket
-    split_reduce_tile<EPI>(p, rws, bm, bn, C::BM, C::BN, C::THREADS);
-    return;
-  }
   if (p.splits > 1) {  // f32 partial slab of this slice; gemm_reduce_kernel applies the epilogue
     float* ws = p.ws + (size_t)split * p.M * p.N;
 #pragma unroll
@@ -722,73 +649,6 @@ __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmParams p) {
   reduce_item<EPI, 0>(p, rws, (int)(id / cpr), (int)(id % cpr) * 8);
 }
 
-// Two-launch split-K reduce with the NEXT W8A8 GEMM's input quantisation fused (fp8 decode steps
-// of > 16 rows): one workgroup per output row -- sum + epilogue + bf16 store of each of the row's
-// chunks (kept in registers), then the row's amax (-> e4m3 codes, scale) and sum of squares (->
-// the RMSNorm 1/rms) over the stored bf16 values: the same chunk -> thread mapping and order as
-// quant_fp8_rows_kernel on the stored row, so the same codes / scale / 1/rms.  One launch instead
-// of gemm_reduce + quant_fp8_rows (~5 us each at 32 rows, profiles/r4_rows32_fp8_kernel_stats_v2.md).
-template <int EPI>
-__global__ __launch_bounds__(1024) void gemm_reduce_rowq_kernel(GemmParams p) {
-  constexpr int NT = 1024, MAXC = 2;  // 16 waves; 8-column chunks per thread: rows of <= 16384 outputs
-  __shared__ float red[2][NT / 64];
-  const int m = blockIdx.x;
-  const int nch = (EPI == EPI_SWIGLU ? p.N / 2 : p.N) / 8;
-  const __amdgpu_buffer_rsrc_t rws = rsrc(p.ws, (size_t)p.splits * p.M * p.N * 4);
-  int c[MAXC];
-  bool ok[MAXC];
-#pragma unroll
-  for (int i = 0; i < MAXC; ++i) {
-    const int ch = threadIdx.x + i * NT;
-    ok[i] = ch < nch;
-    c[i] = ch * 8;
-  }
-  float a[MAXC][8], b[MAXC][8], v[MAXC][8];
-  sum_items<EPI, 0, MAXC, 2>(p, rws, m, c, ok, a, b);
-  float am = 0.f, ss = 0.f;
-#pragma unroll
-  for (int i = 0; i < MAXC; ++i) {
-    if (!ok[i]) continue;
-    finish_item<EPI>(p, m, c[i], a[i], b[i], v[i]);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      am = fmaxf(am, fabsf(v[i][e]));
-      ss += v[i][e] * v[i][e];
-    }
-  }
-  // (per-thread sums over chunks tid, tid + NT, ...: a different order than quant_fp8_rows'
-  // 256-thread pass, so the 1/rms may differ in the last bits; the codes / scale do not)
-  am = wave_max(am);
-  ss = wave_sum(ss);
-  if ((threadIdx.x & 63) == 0) {
-    red[0][threadIdx.x >> 6] = am;
-    red[1][threadIdx.x >> 6] = ss;
-  }
-  __syncthreads();
-  am = 0.f;
-  ss = 0.f;
-#pragma unroll
-  for (int w = 0; w < NT / 64; ++w) {
-    am = fmaxf(am, red[0][w]);
-    ss += red[1][w];
-  }
-  const float sx = am > 0.f ? am * (1.f / 448.f) : 1.f;
-  const float iv = 1.f / sx;
-  if (threadIdx.x == 0) {
-    p.q_sx[m] = sx;
-    if (p.q_rstd) p.q_rstd[m] = rsqrtf(ss / (float)(nch * 8) + p.q_eps);
-  }
-#pragma unroll
-  for (int i = 0; i < MAXC; ++i) {
-    if (!ok[i]) continue;
-    const float* f = v[i];
-    uint2 o;
-    o.x = cvt_pk_fp8(f[0] * iv, f[1] * iv) | (cvt_pk_fp8(f[2] * iv, f[3] * iv) << 16);
-    o.y = cvt_pk_fp8(f[4] * iv, f[5] * iv) | (cvt_pk_fp8(f[6] * iv, f[7] * iv) << 16);
-    *reinterpret_cast<uint2*>(p.q8 + (size_t)m * p.ldq8 + c[i]) = o;
-  }
-}
-
 // per-row 1/rms of X (the RMSNorm of a projection whose gamma is folded into W)
 __global__ __launch_bounds__(256) void row_rstd_kernel(const u16* __restrict__ x, int ldx, int M, int K, float eps,
                                                        float* __restrict__ rstd) {
@@ -806,30 +666,17 @@ __global__ __launch_bounds__(256) void row_rstd_kernel(const u16* __restrict__ x
   if (lane_id() == 0) rstd[row] = rsqrtf(ss / (float)K + eps);
 }
 
-// stage buffers of the 128^2 kernel for one-row-block GEMMs (2 or 4).  4 measured slower in whole
-// decode steps (fp8 32 rows 4.97 vs 4.36 ms): 128 KB of LDS leaves one workgroup per CU, and the
-// split-K grids of > 256 workgroups then run in two rounds (profiles/r4_gemm_ab.md)
-int g_gemm_nb = 2;
-
-template <class C, int EPI, int NB>
-void launch_nb(const GemmParams& p, dim3 grid, hipStream_t st) {
-  const int lds = NB * C::STAGE > C::LDS ? NB * C::STAGE : C::LDS;
-  if (p.sw)
-    hipLaunchKernelGGL((gemm_kernel<C, EPI, true, true, false, NB>), grid, dim3(C::THREADS), lds, st, p);
-  else if (p.w_tiled)
-    hipLaunchKernelGGL((gemm_kernel<C, EPI, true, false, false, NB>), grid, dim3(C::THREADS), lds, st, p);
-  else
-    hipLaunchKernelGGL((gemm_kernel<C, EPI, false, false, false, NB>), grid, dim3(C::THREADS), lds, st, p);
-}
-
 template <class C, int EPI>
 int launch_cfg(const GemmParams& p, hipStream_t st) {
   const int tiles = ((p.M + C::BM - 1) / C::BM) * ((p.N + C::BN - 1) / C::BN);
   const dim3 grid(tiles * p.splits * (p.nbatch > 1 ? p.nbatch : 1));
-  if (g_gemm_nb == 4 && p.M <= C::BM && p.nbatch <= 1)
-    launch_nb<C, EPI, 4>(p, grid, st);
+  const int lds = 2 * C::STAGE > C::LDS ? 2 * C::STAGE : C::LDS;  // two stage buffers
+  if (p.sw)
+    hipLaunchKernelGGL((gemm_kernel<C, EPI, true, true>), grid, dim3(C::THREADS), lds, st, p);
+  else if (p.w_tiled)
+    hipLaunchKernelGGL((gemm_kernel<C, EPI, true, false>), grid, dim3(C::THREADS), lds, st, p);
   else
-    launch_nb<C, EPI, 2>(p, grid, st);
+    hipLaunchKernelGGL((gemm_kernel<C, EPI, false, false>), grid, dim3(C::THREADS), lds, st, p);
   return 0;
 }
 
@@ -849,21 +696,11 @@ int launch_epi(const GemmParams& p, hipStream_t st, bool p8) {
   } else {
     launch_cfg<CfgS, EPI>(p, st);
   }
-  bool rowq = false;
-  if (p.splits > 1 && p.tickets == nullptr) {
-    if constexpr (EPI == EPI_STORE || EPI == EPI_RESID || EPI == EPI_SWIGLU) {
-      if (p.q8) {
-        hipLaunchKernelGGL((gemm_reduce_rowq_kernel<EPI>), dim3(p.M), dim3(1024), 0, st, p);
-        rowq = true;
-      }
-    }
-    if (!rowq) {
-      const int64_t n = (int64_t)p.M * (EPI == EPI_SWIGLU ? p.N / 2 : p.N) / 8;
-      hipLaunchKernelGGL((gemm_reduce_kernel<EPI>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
-    }
+  if (p.splits > 1) {
+    const int64_t n = (int64_t)p.M * (EPI == EPI_SWIGLU ? p.N / 2 : p.N) / 8;
+    hipLaunchKernelGGL((gemm_reduce_kernel<EPI>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p);
   }
-  const int e = (int)hipGetLastError();
-  return e ? e : rowq ? 2 : 0;
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -888,7 +725,6 @@ extern "C" int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats, 
 extern "C" void vwa_gemm_set_split_fill(int pct) { g_split_fill_pct = pct < 0 ? 0 : pct; }
 
 extern "C" void vwa_gemm_set_p8(int mode) { g_p8_mode = mode; }
-extern "C" void vwa_gemm_set_nb(int nb) { g_gemm_nb = nb == 4 ? 4 : 2; }
 
 extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
   GemmParams p = *pp;
@@ -897,7 +733,6 @@ extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
     return -11;
   if (p.sw && (!p.sx || !p.w_tiled)) return -14;  // W8A8: per-row X scales and the fp8 tiled layout
   if (epi == EPI_SWIGLU && (p.N % 32 || p.y_f32)) return -12;
-  if (p.q8 && (p.y_f32 || !p.q_sx || (epi == EPI_SWIGLU ? p.N / 2 : p.N) > 16384 || p.ldq8 % 8)) return -17;  // 2 chunks x 1024 threads
   if (epi == EPI_QKV && (p.y_f32 || p.head_dim % 16 || p.N != (p.n_q_heads + 2 * p.n_kv_heads) * p.head_dim ||
                          !p.q_out || !p.k_cache || !p.v_cache || !p.slots || (p.use_rope && (!p.rope || !p.positions))))
     return -16;
@@ -922,9 +757,6 @@ extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
   p.kg_per_split = (KG + p.splits - 1) / p.splits;
   p.splits = (KG + p.kg_per_split - 1) / p.kg_per_split;  // no empty slice
   if (p.splits > 1 && !p.ws) return -13;
-  // one-launch split-K: the 128^2 kernel, a counter per output tile
-  if (p8 || p.splits == 1 || (int64_t)((p.M + CfgS::BM - 1) / CfgS::BM) * ((p.N + CfgS::BN - 1) / CfgS::BN) > p.n_tickets)
-    p.tickets = nullptr;
   if (p.nbatch > 1 && p.splits > 1) return -15;  // batched launches take no split-K
   switch (epi) {
     case EPI_STORE: return launch_epi<EPI_STORE>(p, st, p8);

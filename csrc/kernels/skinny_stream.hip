@@ -211,9 +211,8 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
   for (int k = 0; k < NT * MT; ++k) acc[k] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-// MT > 1 (17..64 rows: continuous batching of many sessions): every weight fragment meets MT
-// X row fragments, so a step of up to 64 rows streams the weights ONCE in one persistent launch
-// with the fused epilogues (instead of split-K GEMM launches + reduce + epilogue kernels).
+// MT: 16-row MFMA row fragments per weight fragment (only MT = 1 is instantiated since round 5: the
+// 17..64-row form measured slower than the tiled GEMM and was removed).
 template <int EPI, int NT, int KS, bool XG, int MT = 1>
 __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, int nb, int xstride, int xskew) {
   // k-groups (128 wide) per item; MT > 1: one (the X fragments of MT row tiles share the
@@ -403,10 +402,6 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
   }
 }
 
-// One workgroup per tile when the tiles exceed the cap by at most 2x and two workgroups fit a CU's
-// LDS (VWA_SKINNY_GRID_ADAPT=1): no second, serial tile for a quarter of the workgroups (e.g.
-// Whisper-large-v3's fc1, 320 tiles; Llama's QKV, 384)
-int g_grid_adapt = 0;
 int g_x_skew = 32;  // LDS X row skew (elements per 4 rows; 0: none -- A/B knob, vwa_skinny_set_x_skew)
 
 template <int EPI, int NT, int KS, bool XG, int MT = 1>
@@ -416,37 +411,25 @@ int launch_v(const SkinnyParams& p, hipStream_t st, int grid_cap, size_t lds, in
   const int per_wave = (G + KS - 1) / KS;
   const int nb = (per_wave + U - 1) / U;
   const int ntiles = p.N / (16 * NT);
-  int grid = ntiles < grid_cap ? ntiles : grid_cap;
-  if (g_grid_adapt && ntiles > grid_cap && ntiles <= 2 * grid_cap && 2 * lds <= 160 * 1024 && !p.col_mask) grid = ntiles;
+  const int grid = ntiles < grid_cap ? ntiles : grid_cap;
   hipLaunchKernelGGL((skinny_stream_kernel<EPI, NT, KS, XG, MT>), dim3(grid), dim3(KS * 64), lds, st, p, nb, xstride,
                      XG ? 0 : g_x_skew);
   return 0;
 }
 
-// Rows from which the <= 16-row streaming GEMM streams X fragments with the weights (XG) instead
-// of staging all of X in LDS (99: never; tuning knob, vwa_skinny_set_xg_rows)
-int g_xg_rows = 99;
-
 template <int EPI, int NT, int KS>
 int launch(const SkinnyParams& p0, hipStream_t st, int grid_cap) {
   SkinnyParams p = p0;
   const int xstride = p.K + 8;
-  if (p.M > 16) {
-    // 17..64 rows: X fragments stream with the weights (XG; the rows no longer fit LDS at the
-    // decode shapes), 2 or 4 row fragments per weight fragment; no folded LayerNorm, no mask
-    if constexpr (KS == 8) {
-      if (p.fuse_rms == 2 || p.M > 64 || (size_t)p.M * p.ldx * 2 >= 0x7FFFFFF0ull) return -10;
-      p.col_mask = nullptr;
-      if (p.M <= 32)
-        return launch_v<EPI, NT, KS, true, 2>(p, st, grid_cap, (size_t)(KS * NT * 2 * 4 * 64 + 64) * 4, xstride);
-      return launch_v<EPI, NT, KS, true, 4>(p, st, grid_cap, (size_t)(KS * NT * 4 * 4 * 64 + 128) * 4, xstride);
-    } else {
-      return -10;
-    }
-  }
+  // (round 4's 17..64-row form -- X streamed next to the weights, 2 / 4 row fragments per weight
+  // fragment -- measured slower than the tiled GEMM for whole decode steps and was removed in round
+  // 5: more than 16 rows are the tiled GEMM's, gemm.hip)
+  if (p.M > 16) return -10;
   const size_t xbytes = ((size_t)p.M * xstride * 2 + 4 * g_x_skew * 2 + 15) & ~(size_t)15;
   const size_t red = (size_t)(KS * NT * 4 * 64 + 32) * sizeof(float);  // + row scales + row means
-  const bool lds_x = xbytes + red <= 160 * 1024 && (p.M < g_xg_rows || p.fuse_rms == 2 || p.col_mask);
+  // X rows staged in LDS when they fit next to the reduction scratch; otherwise (the down
+  // projection's 14336-wide rows at more than ~5 rows) streamed from L2 with the weights (XG)
+  const bool lds_x = xbytes + red <= 160 * 1024;
   if (p.col_mask) {  // the masked tile list: NT 1, EPI store, LDS-staged X, <= 64 tiles per workgroup
     const int ntiles = p.N / (16 * NT), grid = ntiles < grid_cap ? ntiles : grid_cap;
     if (EPI != EPI_STORE || NT != 1 || !lds_x || (ntiles + grid - 1) / grid > 64 || p.col_mask_rows < 1)
@@ -610,8 +593,7 @@ int launch_fp8(const SkinnyParams& p, hipStream_t st, int grid_cap) {
   const size_t lds = xbytes + (size_t)(KS * NT * 4 * 64 + 32) * sizeof(float);
   if (lds > 160 * 1024) return -10;
   const int ntiles = p.N / (16 * NT);
-  int grid = ntiles < grid_cap ? ntiles : grid_cap;
-  if (g_grid_adapt && ntiles > grid_cap && ntiles <= 2 * grid_cap && 2 * lds <= 160 * 1024) grid = ntiles;
+  const int grid = ntiles < grid_cap ? ntiles : grid_cap;
   hipLaunchKernelGGL((skinny_fp8_kernel<EPI, NT, KS>), dim3(grid), dim3(KS * 64), lds, st, p, nb, xstride);
   return 0;
 }
@@ -1531,7 +1513,7 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
                                                {EPI_RESID, EPI_GELU, EPI_RESID, EPI_QKV},
                                                {EPI_RESID, EPI_STORE, -1, -1}};
   if (cp->seq < 0 || cp->seq > 2 || (cp->seq == 2 ? cp->n != 2 : cp->n < (cp->seq == 0 ? 2 : 3))) return -10;
-  if (cp->seq == 0 && cp->n == 2 && (cp->attn_g || cp->tp.world > 1)) return -10;  // o -> gate/up only: no attention, no TP
+  if (cp->seq == 0 && cp->n == 2) return -10;  // (round 4's o_proj -> gate/up chain: removed in round 5)
   size_t lds = 0;
   for (int i = 0; i < cp->n; ++i) {
     ChainPhase& ph = cp->ph[i];
@@ -1644,10 +1626,7 @@ extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, 
     return (int)hipGetLastError();
   }
 #undef VWA_CHAIN_LAUNCH_F8
-  if (seq == 0 && n_phases == 2) {  // o_proj -> gate/up (5..16 rows, no attention phase)
-    if (attn_g) return -10;
-    VWA_CHAIN_LAUNCH(0, 2, 0);
-  } else if (seq == 0) {
+  if (seq == 0) {
     if (n_phases != 3 && n_phases != 4) return -10;
     const bool q = n_phases == 4;
     switch (attn_g) {
@@ -1669,41 +1648,12 @@ extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, 
   return (int)hipGetLastError();
 }
 
-namespace {
-}  // namespace
-
-// Plain epilogues (store / residual / GELU) of >= g_nt2_rows rows (<= 16, no grammar mask): two
-// adjacent 16-column tiles per workgroup tile, so every X fragment read from LDS (or streamed,
-// XG) feeds two MFMAs -- half the X traffic per weight byte, half the tiles.  99: never (tuning
-// knob, vwa_skinny_set_nt2_rows).
-int g_nt2_rows = 99;
-
-template <int KS>
-bool use_nt2(int epi, const SkinnyParams& p) {
-  if (p.M < g_nt2_rows || p.M > 16 || p.N % 32 != 0 || p.col_mask) return false;
-  if (epi != EPI_STORE && epi != EPI_RESID && epi != EPI_GELU) return false;
-  if (p.w_scale)  // the fp8 kernel stages X in LDS: the NT 2 reduction buffer must fit beside it
-    return ((size_t)p.M * (p.K + 16) + 15) / 16 * 16 + (size_t)(KS * 2 * 4 * 64 + 32) * 4 <= 160 * 1024;
-  return true;
-}
+// (round 4's 32-column tiles for the plain epilogues measured slower at
+// 8 / 16 rows, profiles/r4_skinny_nt2_rows.jsonl, and were removed in round 5)
 
 // Returns -10 when this shape does not fit the streaming kernel (caller falls back).
 template <int KS>
 int dispatch_ks(int epi, const SkinnyParams& p, int grid_cap, hipStream_t st) {
-  if (use_nt2<KS>(epi, p)) {
-    if (p.w_scale) {
-      switch (epi) {
-        case EPI_STORE: return launch_fp8<EPI_STORE, 2, KS>(p, st, grid_cap);
-        case EPI_RESID: return launch_fp8<EPI_RESID, 2, KS>(p, st, grid_cap);
-        default: return launch_fp8<EPI_GELU, 2, KS>(p, st, grid_cap);
-      }
-    }
-    switch (epi) {
-      case EPI_STORE: return launch<EPI_STORE, 2, KS>(p, st, grid_cap);
-      case EPI_RESID: return launch<EPI_RESID, 2, KS>(p, st, grid_cap);
-      default: return launch<EPI_GELU, 2, KS>(p, st, grid_cap);
-    }
-  }
   if (p.w_scale) {
     switch (epi) {
       case EPI_STORE: return launch_fp8<EPI_STORE, 1, KS>(p, st, grid_cap);
@@ -1726,13 +1676,10 @@ int dispatch_ks(int epi, const SkinnyParams& p, int grid_cap, hipStream_t st) {
 
 // Returns -10 when this shape does not fit the streaming kernel (caller falls back).
 // ks = waves per workgroup splitting K (4 or 8); grid_cap = max persistent workgroups.
-extern "C" void vwa_skinny_set_xg_rows(int rows) { g_xg_rows = rows; }
-extern "C" void vwa_skinny_set_grid_adapt(int on) { g_grid_adapt = on; }
-extern "C" void vwa_skinny_set_nt2_rows(int rows) { g_nt2_rows = rows; }
 extern "C" void vwa_skinny_set_x_skew(int skew) { g_x_skew = skew == 0 ? 0 : 32; }
 
 extern "C" int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st) {
-  if (p->M < 1 || p->M > 64 || p->K % 128 != 0) return -10;
+  if (p->M < 1 || p->M > 16 || p->K % 128 != 0) return -10;
   if ((size_t)p->N * p->K * (p->w_scale ? 1 : 2) >= 0x7FFFFFF0ull) return -10;
   const int r = (ks == 4) ? dispatch_ks<4>(epi, *p, grid_cap, st) : dispatch_ks<8>(epi, *p, grid_cap, st);
   if (r) return r;

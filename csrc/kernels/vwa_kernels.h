@@ -157,10 +157,6 @@ struct GemmParams {
   // rows t*stride-1 .. t*stride+1 of a zero-padded channels-last buffer)
   int nbatch; int64_t bsx, bsy, bsr;
   int cus; int64_t ws_cap;  // CU count and workspace floats (split-K choice of the 256^2 kernel)
-  // split-K in one launch (128^2 kernel): per-tile arrival counters (zeroed once, reset by the last
-  // arriver) -- the slices publish their f32 partials write-through and the LAST slice of a tile
-  // sums them and runs the epilogue (no gemm_reduce launch).  null: the two-launch form.
-  int* tickets; int n_tickets;
   // epilogue 5 (QKV): rotary embedding + paged-KV write of a QKV projection with permuted head rows
   // (ops.permute_qkv_rows: each 16-column tile holds the rotation pairs (c, c + 8)) -- q heads go
   // to q_out in natural dim order, k / v heads to the caches at slots[m] (< 0: not written);
@@ -169,10 +165,6 @@ struct GemmParams {
   const int* positions; const int64_t* slots; const float* rope;
   uint16_t* q_out; int ldq; uint16_t* k_cache; uint16_t* v_cache; int block_size;
   int64_t cache_sb, cache_sh, cache_st;
-  // optional row quantisation of the OUTPUT for the next W8A8 GEMM (epilogues 0 / 1 / 2 with the
-  // two-launch split-K): e4m3 codes q8 [M, ldq8], per-row scales q_sx (amax / 448) and, if q_rstd,
-  // the RMSNorm 1/rms (eps q_eps) of the stored bf16 rows; vwa_gemm returns 2 when it did so
-  uint8_t* q8; int ldq8; float* q_sx; float* q_rstd; float q_eps;
 };
 
 struct FlashAttnParams {
@@ -192,17 +184,13 @@ extern "C" {
 #endif
 int vwa_skinny_gemm(int epi, const SkinnyParams* p, hipStream_t st);
 int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st);
-void vwa_skinny_set_xg_rows(int rows);  // X streamed with the weights from this many rows (99: never)
-void vwa_skinny_set_grid_adapt(int on);  // one workgroup per tile up to 2x the grid cap (LDS permitting)
 void vwa_skinny_set_x_skew(int skew);  // LDS-staged X rows: 64-B skew every 4 rows (default) or none (0)
-void vwa_skinny_set_nt2_rows(int rows);  // two 16-column tiles per workgroup tile from this many rows (99: never)
 int vwa_chain_prepare(ChainParams* cp, int grid);
 int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid, hipStream_t st,
                      int xg2 = 0, int f8 = 0);
 int vwa_gemm(int epi, const GemmParams* p, hipStream_t st);
 int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats, int f8);
 void vwa_gemm_set_split_fill(int pct);  // split-K while tiles x splits < pct % of the CUs (0: bf16 75, fp8 100)
-void vwa_gemm_set_nb(int nb);  // 128^2 kernel stage buffers for one-row-block GEMMs: 2 (default) or 4
 void vwa_gemm_set_p8(int mode);  // 0: 128^2 kernel only, 1: 256^2 8-phase wherever eligible, 2: measured rule
 int vwa_row_rstd(const uint16_t* x, int ldx, int M, int K, float eps, float* rstd, hipStream_t st);
 int vwa_rmsnorm(const uint16_t* x, const uint16_t* residual, uint16_t* residual_out, const uint16_t* w,

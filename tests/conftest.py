@@ -11,6 +11,7 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU and the native kernel library")
     config.addinivalue_line("markers", "slow: long-running test")
+    config.addinivalue_line("markers", "allow_vendor: a GPU test that exercises a vendor-library fallback on purpose")
 
 
 def pytest_collection_modifyitems(config, items):
@@ -22,6 +23,16 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _strict_native_on_gpu(request, monkeypatch):
+    """GPU tests run in strict native mode: an op that would leave the hand-written kernels for a
+    vendor library (torch.matmul / _scaled_mm on a GPU tensor) raises instead (ops.vendor_fallback).
+    A test that exercises such a path on purpose marks itself ``allow_vendor``."""
+    if "gpu" in request.keywords and "allow_vendor" not in request.keywords:
+        monkeypatch.setenv("VWA_STRICT_NATIVE", "1")
+    yield
 
 
 def pytest_sessionstart(session):

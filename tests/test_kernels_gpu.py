@@ -811,90 +811,6 @@ def test_llama70b_tp8_per_rank_decode_shapes(M):
         close(a, b, 3e-2)
 
 
-@pytest.mark.parametrize("M", [17, 24, 32, 33, 48, 64])
-def test_streaming_kernel_many_rows(M, monkeypatch):
-    """17..64 decode rows (continuous batching) on the streaming kernel with pre-tiled weights
-    (skinny_stream.hip MT = 2 / 4 row fragments per weight fragment, X streamed with the weights):
-    store (f32 out + fused RMSNorm, the LM head), residual (the down shape, K = 14336), SwiGLU
-    and QKV + RoPE + paged-KV write, against the f32 reference."""
-    monkeypatch.setattr(ops, "STREAM_MAX_M", 64)  # (opt-in outside this test: VWA_STREAM_MAX_M)
-    K, N = 4096, 1024
-    x = rnd(M, K)
-    w = rnd(N, K, scale=0.02)
-    y = torch.empty(M, N, dtype=torch.float32, device=DEV)
-    ops.linear(x, ops.TiledWeight(w), out=y, fuse_rms=True)
-    close(y, ref.linear(x.cpu(), w.cpu(), None, out=torch.empty(M, N), fuse_rms=True), 2e-3, 2e-3)
-    xd, wd, res = rnd(M, 14336), rnd(512, 14336, scale=0.01), rnd(M, 512)
-    out = res.clone()
-    ops.linear(xd, ops.TiledWeight(wd), out=out, residual=out)
-    close(out, ref.linear(xd.cpu(), wd.cpu(), None, out=torch.empty(M, 512, dtype=BF), residual=res.cpu()), 2e-2)
-    F = 768
-    gu = ops.interleave_gate_up(rnd(F, K, scale=0.02), rnd(F, K, scale=0.02))
-    a = ops.linear_swiglu(x, ops.TiledWeight(gu), fuse_rms=True)
-    close(a, ref.linear_swiglu(x.cpu(), gu.cpu(), fuse_rms=True, eps=1e-5, out=torch.empty(M, F, dtype=BF)), 2e-2)
-    nq, nkv, hd = 8, 2, 128
-    H = nq + 2 * nkv
-    wq = ops.permute_qkv_rows(rnd(H * hd, K, scale=0.02), H, hd)
-    rope = ops.rope_table(512, hd, 5e5, device=DEV)
-    pos = torch.randint(0, 400, (M,), dtype=torch.int32, device=DEV)
-    slots = torch.randperm(16 * 8, device=DEV)[:M].to(torch.int64)
-    kc = torch.zeros(8, nkv, 16, hd, dtype=BF, device=DEV)
-    vc = torch.zeros_like(kc)
-    q = torch.zeros(M, nq * hd, dtype=BF, device=DEV)
-    ops.qkv_rope_write(x, ops.TiledWeight(wq), None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
-                       rope=rope, positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc)
-    kc2, vc2 = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
-    q2 = torch.zeros(M, nq * hd, dtype=BF)
-    ref.qkv_rope_write(x.cpu(), wq.cpu(), None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
-                       rope=rope.cpu(), positions=pos.cpu(), slots=slots.cpu(), q_out=q2, k_cache=kc2, v_cache=vc2)
-    for a_, b_ in ((q, q2), (kc, kc2), (vc, vc2)):
-        close(a_, b_, 3e-2)
-
-
-@pytest.mark.parametrize("M", [17, 32, 64])
-@pytest.mark.parametrize("fp8", [False, True])
-def test_gemm_one_launch_split_k(M, fp8, monkeypatch):
-    """Many-row decode shapes (Llama-3-8B widths, split-K because 17..64 rows give too few output
-    tiles): the one-launch split-K (each tile's last slice reduces the write-through slabs and
-    runs the epilogue) is bit-identical to GEMM + gemm_reduce and matches the f32 reference, for
-    the residual / SwiGLU / store epilogues; the tile counters stay zero between launches."""
-    K = 4096
-    x = rnd(M, K)
-    res0 = rnd(M, 4096)
-    w_o = rnd(4096, K, scale=K ** -0.5)
-    gu = ops.interleave_gate_up(rnd(1024, K, scale=K ** -0.5), rnd(1024, K, scale=K ** -0.5))
-    w_q = rnd(1536, K, scale=K ** -0.5)
-    if fp8:
-        W = [ops.FP8Weight.quantize(w, tiled=True) for w in (w_o, gu, w_q)]
-        C = [ops.FP8Weight(w.rows().cpu(), w.scale.cpu()) for w in W]
-    else:
-        W = [ops.TiledWeight(w) for w in (w_o, gu, w_q)]
-        C = [w.cpu() for w in (w_o, gu, w_q)]
-
-    def run():
-        res = res0.clone()
-        ops.linear(x, W[0], out=res, residual=res, fuse_rms=True)
-        sw = ops.linear_swiglu(x, W[1], fuse_rms=True)
-        q = torch.empty(M, 1536, dtype=BF, device=DEV)
-        ops.linear(x, W[2], out=q, fuse_rms=True)
-        torch.cuda.synchronize()
-        return res, sw, q
-
-    monkeypatch.setattr(ops, "GEMM_ONE_LAUNCH", True)
-    one = run()
-    one2 = run()  # counters were reset by the last arrivers: a second launch is identical
-    assert int(ops.gemm_tickets(DEV).abs().sum()) == 0
-    monkeypatch.setattr(ops, "GEMM_ONE_LAUNCH", False)
-    two = run()
-    for a, b, c in zip(one, one2, two):
-        assert torch.equal(a, b) and torch.equal(a, c)
-    xc = x.cpu()
-    exp = ops.linear(xc, C[0], residual=res0.cpu(), fuse_rms=True)
-    close(one[0], exp, 3e-2, 3e-2)
-    close(one[1], ops.linear_swiglu(xc, C[1], fuse_rms=True), 3e-2, 3e-2)
-    close(one[2], ops.linear(xc, C[2], fuse_rms=True), 3e-2, 3e-2)
-
-
 def test_quant_fp8_rows_with_rstd():
     """The fp8 row quantiser's optional RMSNorm output (one row pass for the W8A8 GEMM's two row
     statistics) equals row_rstd, and the codes / scales are unchanged by it."""
@@ -1007,87 +923,3 @@ def test_decode_attention_shared_prefix(hd, nq, nkv, n_sess, P):
     close(outs[1][:n_real], exp[:n_real], 2e-2)
     assert torch.equal(outs[0], outs[2])
 
-
-@pytest.mark.parametrize("M", [17, 40, 64])
-def test_fp8_row_quant_handoff(M, monkeypatch):
-    """W8A8 GEMM chain of a Llama layer at > 16 rows (o_proj -> gate/up -> down -> next QKV): with
-    the row-quantisation hand-off each split-K reduce quantises its output for the next GEMM
-    (no quant_fp8_rows launches in between) -- the same as quantising every input (the fused
-    1/rms sums in another order: last-bit differences only)."""
-    d, F, nq, nkv, hd = 1024, 2048, 8, 2, 128
-    W = dict(o=rnd(d, nq * hd, scale=0.03), gu=ops.interleave_gate_up(rnd(F, d, scale=0.03), rnd(F, d, scale=0.03)),
-             down=rnd(d, F, scale=0.02), qkv=ops.permute_qkv_rows(rnd((nq + 2 * nkv) * hd, d, scale=0.03),
-                                                                nq + 2 * nkv, hd))
-    W8 = {k: ops.FP8Weight.quantize(v, tiled=True) for k, v in W.items()}
-    attn0, h0 = rnd(M, nq * hd), rnd(M, d)
-    rope = ops.rope_table(512, hd, 5e5, device=DEV)
-    pos = torch.arange(M, dtype=torch.int32, device=DEV)
-    slots = torch.arange(M, dtype=torch.int64, device=DEV)
-
-    def layer(on):
-        monkeypatch.setenv("VWA_ROWQ_HANDOFF", "1" if on else "0")
-        ops.row_quant_handoff(on)
-        try:
-            h = h0.clone()
-            ops.linear(attn0, W8["o"], out=h, residual=h)
-            act = ops.linear_swiglu(h, W8["gu"], fuse_rms=True)
-            ops.linear(act, W8["down"], out=h, residual=h)
-            kc = torch.zeros((M + 15) // 16 + 1, nkv, 16, hd, dtype=BF, device=DEV)
-            vc = torch.zeros_like(kc)
-            q = torch.zeros(M, nq * hd, dtype=BF, device=DEV)
-            ops.qkv_rope_write(h, W8["qkv"], None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
-                               rope=rope, positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc)
-            torch.cuda.synchronize()
-            return h, act, q, kc, vc
-        finally:
-            ops.row_quant_handoff(False)
-
-    with_h, without = layer(True), layer(False)
-    for a, b in zip(with_h, without):
-        close(a, b, 2e-2, 2e-2)
-    assert torch.equal(with_h[0], without[0])  # o_proj output: no 1/rms involved yet
-
-
-@pytest.mark.parametrize("M", [5, 8, 16])
-def test_skinny_nt2_tiles_match_reference(M):
-    """Two 16-column tiles per workgroup tile for the plain epilogues (skinny_stream.hip use_nt2,
-    VWA_SKINNY_NT2_ROWS): bf16 tiled weights with X in LDS (K 4096) and streamed (K 14336, XG),
-    fp8 tiled weights (W8A8), store + fused RMSNorm, residual and GELU, against the fp32 CPU
-    reference; the NT 2 launch is checked to differ from no launch at all by comparing with NT 1."""
-    m = ops.ext()
-    K, N = 4096, 1024
-    x, xd = rnd(M, K), rnd(M, 14336)
-    w, wd = rnd(N, K, scale=0.02), rnd(512, 14336, scale=0.01)
-    wq = ops.FP8Weight.quantize(rnd(N, K, scale=K ** -0.5), tiled=True)
-    wc = ops.FP8Weight(wq.rows().cpu(), wq.scale.cpu())
-    res, resd = rnd(M, N), rnd(M, 512)
-    results = {}
-    try:
-        for nt2 in (99, 1):
-            m.skinny_set_nt2_rows(nt2)
-            a = torch.empty(M, N, dtype=torch.float32, device=DEV)
-            ops.linear(x, ops.TiledWeight(w), out=a, fuse_rms=True)
-            b = resd.clone()
-            ops.linear(xd, ops.TiledWeight(wd), out=b, residual=b)
-            c = ops.linear(x, ops.TiledWeight(w), act="gelu")
-            d = res.clone()
-            ops.linear(x, wq, out=d, residual=d)
-            torch.cuda.synchronize()
-            results[nt2] = (a, b, c, d)
-    finally:
-        m.skinny_set_nt2_rows(99)
-    xc, xdc = x.cpu().float(), xd.cpu().float()
-    xn = xc * torch.rsqrt(xc.pow(2).mean(-1, keepdim=True) + 1e-5)
-    exp_a = xn @ w.cpu().float().t()
-    exp_b = resd.cpu().float() + xdc @ wd.cpu().float().t()
-    exp_c = torch.nn.functional.gelu(xc @ w.cpu().float().t())
-    exp_d = ops.linear(x.cpu(), wc, residual=res.cpu())
-    for nt2 in (99, 1):
-        a, b, c, d = results[nt2]
-        close(a, exp_a, 1e-2, 1e-2)
-        close(b, exp_b, 3e-2, 3e-2)
-        close(c, exp_c, 2e-2, 2e-2)
-        close(d, exp_d, 3e-2, 3e-2)
-    # same summation order per column (the K split over waves is unchanged): identical results
-    for u, v in zip(results[99], results[1]):
-        assert torch.equal(u, v)

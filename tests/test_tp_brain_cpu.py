@@ -266,3 +266,50 @@ def test_idle_tp_group_survives_past_the_control_timeout():
     assert beats >= 5, msgs
     outs = {r: o for kind, r, o in msgs if kind == "outs"}
     assert outs[0] == outs[1] and safe_parse(ParseResponse, outs[0][0]).success
+
+
+def _bench_worker(rank, world, port, q):
+    """bench.py's session driver over the served TP control plane: rank 0 runs
+    the sessions through TPIntentEngine, rank 1 follows in lockstep, world barriers around."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank), VWA_DIST_BACKEND="gloo")
+    torch.set_num_threads(2)
+    import bench
+    from voice_enabled_browser_automation_amd.parallel.tp import init_distributed
+
+    tp = init_distributed(tp_size=2)
+    assert tp.size == 2 and tp.ctl is not None
+    brain = TPIntentEngine(_engine(tp), tp)
+    reqs = _reqs()
+
+    def one(i):
+        out = brain.parse(reqs[i % len(reqs)])
+        return safe_parse(ParseResponse, out).success, out
+
+    bench.drive_sessions(brain, tp, world, 1, one)  # warm-up
+    res, el = bench.drive_sessions(brain, tp, world, 3, one, start=1)
+    allr = bench.gather({"rank": rank, "n": len(res), "ok": sum(r[0] for r in res),
+                         "outs": [r[1] for r in res], "it": brain.iterations}, world)
+    q.put(("done", rank, allr, el))
+    dist.destroy_process_group()
+
+
+def test_bench_tp_control_path_over_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+    assert [p.exitcode for p in procs] == [0, 0]
+    msgs = {}
+    while not q.empty():
+        kind, r, allr, el = q.get()
+        msgs[r] = (allr, el)
+    allr = msgs[0][0]
+    assert allr[0]["n"] == 3 and allr[0]["ok"] == 3  # the leader ran the sessions, all valid
+    assert allr[1]["n"] == 0  # the follower ran none of its own...
+    assert allr[1]["it"] == allr[0]["it"] > 0  # ...but every scheduler iteration in lockstep
+    assert all(safe_parse(ParseResponse, o).success for o in allr[0]["outs"])

@@ -10,7 +10,8 @@ real time (a microphone, apps/web/src/App.tsx:279-288), followed by silence pack
 ``intent`` frame arrives.  Reported per utterance:
 
 * speech_end_to_final_ms -- last speech packet sent -> ``transcript_final`` (the VAD endpoint,
-  ``endpoint_silence_s`` = 0.6 s, plus the final recognition pass);
+  ``--endpoint-ms`` = VWA_ENDPOINT_MS; the final recognition pass runs speculatively from
+  ``--spec-ms`` of trailing silence on, so it is normally done by the endpoint);
 * final_to_intent_ms -- ``transcript_final`` -> ``intent`` (the debounce, the HTTP hop to the
   brain, the grammar-constrained parse, the reply);
 * speech_end_to_intent_ms -- the sum: what a user waits after they stop speaking.
@@ -35,6 +36,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PKG = "voice_enabled_browser_automation_amd"
+from voice_enabled_browser_automation_amd.utils.env import knob  # noqa: E402
 
 
 def free_port() -> int:
@@ -192,7 +194,8 @@ async def run_matrix(a) -> list:
                             "BRAIN_URL": f"http://127.0.0.1:{bport}/parse",
                             "EXECUTOR_URL": f"http://127.0.0.1:{ex_port}", "VWA_DEBOUNCE_MS": deb,
                             "HIP_VISIBLE_DEVICES": a.voice_gpu, "VWA_MAX_SESSIONS": str(max(a.sessions)),
-                            "VWA_ASR_TOKENS_PER_S": str(a.asr_tokens_per_s)}
+                            "VWA_ASR_TOKENS_PER_S": str(a.asr_tokens_per_s),
+                            "VWA_ENDPOINT_MS": str(a.endpoint_ms), "VWA_SPEC_FINAL_MS": str(a.spec_ms)}
                     voice = spawn(f"{PKG}.voice.server", venv, os.path.join(logs, f"voice_chain{chain}_deb{deb}.log"))
                     try:
                         await wait_health(f"http://127.0.0.1:{vport}/health", voice, a.load_timeout)
@@ -210,6 +213,7 @@ async def run_matrix(a) -> list:
                                    "utterances": len(out), "timeouts": len(out) - len(ok),
                                    "valid_intents": f"{sum(r['valid'] for r in ok)}/{len(out)}",
                                    "audio_s": a.audio_s, "asr": a.asr, "llm": a.llm, "dtype": a.dtype,
+                                   "endpoint_ms": a.endpoint_ms, "spec_final_ms": a.spec_ms,
                                    "speech_end_to_intent_p50_ms": pct(e2i, 50),
                                    "speech_end_to_intent_p95_ms": pct(e2i, 95),
                                    "speech_end_to_final_p50_ms": pct([r["speech_end_to_final_ms"] for r in ok], 50),
@@ -242,8 +246,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sessions", default="1,8")
     ap.add_argument("--debounce", default="0,1000")
-    ap.add_argument("--chain", default="1,0")
-    ap.add_argument("--utterances", type=int, default=4)
+    ap.add_argument("--chain", default="0", help="brain VWA_CHAIN (the single-GPU deployment default: 0)")
+    ap.add_argument("--utterances", type=int, default=20, help="utterances per session per point")
+    ap.add_argument("--endpoint-ms", type=float, default=knob("VWA_ENDPOINT_MS"))
+    ap.add_argument("--spec-ms", type=float, default=knob("VWA_SPEC_FINAL_MS"))
     ap.add_argument("--audio-s", type=float, default=5.0)
     ap.add_argument("--asr", default="whisper-tiny")
     ap.add_argument("--asr-engine", default="whisper")

@@ -78,7 +78,7 @@ class WhisperRunner:
         self.h_i32 = torch.zeros(4, R, dtype=torch.int32, pin_memory=pin)
         self.h_slots = torch.full((R,), -1, dtype=torch.int64, pin_memory=pin)
         if use_graphs is None:
-            use_graphs = ops.env_flag("VWA_HIPGRAPH", True)
+            use_graphs = ops.env_flag("VWA_HIPGRAPH")
         self.use_graphs = bool(use_graphs) and dev.type == "cuda"
         self.graphs: Dict[int, Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
         self.pool = None
@@ -159,7 +159,7 @@ class AsrEngine:
         self.loop_out = torch.zeros(max(448, cfg.n_text_ctx), dtype=torch.int32, device=dev)
         self.loop_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
         self.loop_graphs: Dict[Tuple[int, bool, int], torch.cuda.CUDAGraph] = {}
-        self.device_loop = self.runner.use_graphs and ops.env_flag("VWA_ASR_DEVICE_LOOP", True)
+        self.device_loop = self.runner.use_graphs and ops.env_flag("VWA_ASR_DEVICE_LOOP")
         self.last_stats: Dict[str, float] = {}
         self.free_slots = list(range(max_sessions - 1, -1, -1))
 

@@ -11,9 +11,18 @@ apps/web/src/App.tsx:279-288).  A session keeps the current utterance buffer and
   *committed* -- later passes force it as the decoder prefix (prefilled in one ragged step with
   the SOT tokens) and decode only the continuation, so a long utterance does not re-decode its
   whole transcript at every partial, and the committed words never flicker;
-* on an endpoint (``endpoint_silence_s`` of silence after speech), on ``flush()`` (client
-  end-of-utterance) or when the 30 s Whisper window is full, it emits a final result
-  (``is_final: true, speech_final: true``) and starts a new utterance.
+* on an endpoint (``endpoint_silence_s`` of silence after speech, ``VWA_ENDPOINT_MS``), on
+  ``flush()`` (client end-of-utterance) or when the 30 s Whisper window is full, it emits a final
+  result (``is_final: true, speech_final: true``) and starts a new utterance;
+* **speculative final**: once the trailing silence reaches ``spec_silence_s``
+  (``VWA_SPEC_FINAL_MS``, shorter than the endpoint) the final recognition pass is started in the
+  background on the utterance so far; if the silence lasts to the endpoint its result IS the final
+  (no pass after the endpoint), if speech resumes it is discarded -- so the final costs the
+  endpoint wait alone, not endpoint + a recognition pass (Deepgram's live endpointing finalises
+  without a client-side wait, deepgram.ts:36-45);
+* the VAD threshold adapts to the noise floor (``max(energy_threshold, noise_mult x floor)``; the
+  floor is bootstrapped from a stationary mic-open period and kept by the non-speech frames), so a
+  noisy microphone still endpoints.
 
 Recognition passes go through a *recognizer* (``recognize(pcm, prefix) -> Hypothesis``).
 ``AsrBatcher`` is the serving recognizer: one scheduler thread per GPU engine that gathers the
@@ -72,6 +81,19 @@ def _as_recognizer(r: Any):
     return r if hasattr(r, "recognize") else TextRecognizer(r)
 
 
+def recognize_async(rec: Any, pcm: np.ndarray, prefix: Sequence[int] = ()) -> Future:
+    """A recognition pass that runs in the background when the recognizer can (AsrBatcher: queued
+    for the next GPU batch), else synchronously into an already completed Future."""
+    if hasattr(rec, "recognize_async"):
+        return rec.recognize_async(pcm, prefix)
+    fut: Future = Future()
+    try:
+        fut.set_result(rec.recognize(pcm, prefix))
+    except BaseException as e:  # noqa: BLE001
+        fut.set_exception(e)
+    return fut
+
+
 def common_prefix(a: Sequence[int], b: Sequence[int]) -> int:
     n = min(len(a), len(b))
     i = 0
@@ -82,14 +104,28 @@ def common_prefix(a: Sequence[int], b: Sequence[int]) -> int:
 
 class StreamingAsrSession:
     def __init__(self, recognizer: Any, *, rate: int = 16000, model_name: str = "whisper",
-                 partial_every_s: float = 1.0, endpoint_silence_s: float = 0.6, energy_threshold: float = 300.0,
-                 max_window_s: float = 30.0, min_speech_s: float = 0.2, local_agreement: bool = True):
+                 partial_every_s: float = 1.0, endpoint_silence_s: Optional[float] = None,
+                 energy_threshold: Optional[float] = None, max_window_s: float = 30.0, min_speech_s: float = 0.2,
+                 local_agreement: bool = True, spec_silence_s: Optional[float] = None,
+                 noise_mult: Optional[float] = None):
+        from ..utils.env import knob
+
         self.rec = _as_recognizer(recognizer)
         self.rate = rate
         self.model_name = model_name
         self.partial_every = int(partial_every_s * rate)
+        if endpoint_silence_s is None:
+            endpoint_silence_s = knob("VWA_ENDPOINT_MS") / 1000.0
+        if spec_silence_s is None:
+            spec_silence_s = knob("VWA_SPEC_FINAL_MS") / 1000.0
         self.endpoint = int(endpoint_silence_s * rate)
-        self.thresh = energy_threshold
+        # speculative final pass after this much trailing silence (0: off; never later than the endpoint)
+        self.spec_at = min(int(spec_silence_s * rate), self.endpoint) if spec_silence_s > 0 else 0
+        self.thresh = knob("VWA_VAD_THRESHOLD") if energy_threshold is None else energy_threshold
+        self.noise_mult = knob("VWA_VAD_NOISE_MULT") if noise_mult is None else noise_mult
+        self.noise_floor = 0.0  # tracked non-speech frame RMS (0: not known)
+        self._boot: Optional[List[float]] = []  # frame RMS of the stream's first 300 ms
+        self._spec: Optional[Future] = None  # the speculative final pass in flight
         self.max_window = int(max_window_s * rate)
         self.min_speech = int(min_speech_s * rate)
         self.local_agreement = local_agreement
@@ -107,7 +143,8 @@ class StreamingAsrSession:
         self.committed: List[int] = []   # agreed token prefix of the current utterance
         self.prev_tokens: List[int] = []  # previous interim hypothesis
         self.stats: Dict[str, float] = {"partials": 0, "finals": 0, "asr_ms": 0.0, "passes": 0,
-                                        "committed_tokens": 0}
+                                        "committed_tokens": 0, "spec_started": 0, "spec_used": 0,
+                                        "spec_discarded": 0}
 
     # ------------------------------------------------------------------ internals
     @property
@@ -128,6 +165,21 @@ class StreamingAsrSession:
         self.stats["passes"] += 1
         return hyp
 
+    def _track_floor(self, rms: float) -> None:
+        """Bootstrap the noise floor from the stream's first 300 ms (the mic-open moment) when that
+        audio is stationary (frame RMS within 2x: hiss, hum -- not a speech onset) and quiet enough
+        (mult x level <= 10 x the fixed threshold); afterwards the non-speech frames maintain it."""
+        if self._boot is None or self.noise_mult <= 0.0:
+            return
+        self._boot.append(rms)
+        if len(self._boot) < 15:
+            return
+        lo, hi = min(self._boot), max(self._boot)
+        med = float(np.median(self._boot))
+        if hi <= 2.0 * max(lo, 1e-6) and self.noise_mult * med <= 10.0 * self.thresh:
+            self.noise_floor = max(self.noise_floor, med)
+        self._boot = None
+
     def _reset_utterance(self) -> None:
         self.t_offset += self._n / self.rate
         self._n = 0
@@ -135,11 +187,34 @@ class StreamingAsrSession:
         self.last_partial = ""
         self.committed = []
         self.prev_tokens = []
+        self._drop_spec()
 
-    def _final(self) -> List[Dict]:
+    def _drop_spec(self) -> None:
+        if self._spec is not None:
+            self.stats["spec_discarded"] += 1
+            self._spec = None
+
+    def _start_spec(self) -> None:
+        """The final pass, started during the trailing silence (see module docstring)."""
+        self.stats["spec_started"] += 1
+        self._spec_t0 = time.perf_counter()
+        self._spec = recognize_async(self.rec, self.buf.copy(), self.committed if self.local_agreement else ())
+
+    def _final(self, use_spec: bool = True) -> List[Dict]:
         out: List[Dict] = []
         if self.speech >= self.min_speech and len(self.buf):
-            hyp = self._run()
+            hyp = None
+            if use_spec and self._spec is not None:
+                try:
+                    hyp = self._spec.result()
+                    self.stats["spec_used"] += 1
+                    self.stats["asr_ms"] += (time.perf_counter() - self._spec_t0) * 1e3
+                    self.stats["passes"] += 1
+                    self._spec = None
+                except Exception:  # noqa: BLE001  (a failed background pass: run the final now)
+                    self._drop_spec()
+            if hyp is None:
+                hyp = self._run()
             out.append(results_event(hyp.text, is_final=True, start=self.t_offset, duration=len(self.buf) / self.rate,
                                      model=self.model_name))
             self.stats["finals"] += 1
@@ -177,17 +252,26 @@ class StreamingAsrSession:
                 continue
             self._append(fr)
             rms = float(np.sqrt(np.mean(fr.astype(np.float32) ** 2)))
-            if rms >= self.thresh:
+            self._track_floor(rms)
+            if rms >= max(self.thresh, self.noise_mult * self.noise_floor):
                 self.speech += len(fr)
                 self.trailing_silence = 0
+                self._drop_spec()  # speech resumed: the speculative final no longer covers the utterance
             else:
                 self.trailing_silence += len(fr)
+                # non-speech frames: the floor falls fast to quieter frames, rises slowly (0.3 % / frame)
+                if self.noise_floor > 0.0:
+                    self.noise_floor = (0.8 * self.noise_floor + 0.2 * rms if rms < self.noise_floor
+                                        else min(rms, self.noise_floor * 1.003))
             if self.speech > 0:
                 self.since_partial += len(fr)
             if self.speech >= self.min_speech and self.trailing_silence >= self.endpoint:
                 events += self._final()
             elif len(self.buf) >= self.max_window:
-                events += self._final()
+                events += self._final(use_spec=False)
+            elif (self.spec_at and self._spec is None and self.speech >= self.min_speech
+                  and self.trailing_silence >= self.spec_at):
+                self._start_spec()
             elif self.speech == 0 and self.trailing_silence >= self.endpoint:
                 # leading silence: drop it, keep the stream clock
                 self.t_offset += self._n / self.rate
@@ -199,7 +283,7 @@ class StreamingAsrSession:
         return events
 
     def flush(self) -> List[Dict]:
-        return self._final()
+        return self._final()  # (a speculative pass in flight covers the utterance: speech since would have dropped it)
 
     def close(self) -> None:
         pass
@@ -251,6 +335,10 @@ class AsrBatcher:
         self._thread.start()
 
     def recognize(self, pcm: np.ndarray, prefix: Sequence[int] = ()) -> Hypothesis:
+        return self.recognize_async(pcm, prefix).result()
+
+    def recognize_async(self, pcm: np.ndarray, prefix: Sequence[int] = ()) -> Future:
+        """Queue a pass for the next GPU batch; the Future resolves to its Hypothesis."""
         fut: Future = Future()
         with self._cv:
             if self._stop:
@@ -258,7 +346,7 @@ class AsrBatcher:
             # (cut to what the decoder forces: the hypothesis is built on the prefix it really used)
             self._q.append((np.array(pcm, dtype=np.int16, copy=True), list(prefix)[: self.eng.max_prefix()], fut))
             self._cv.notify()
-        return fut.result()
+        return fut
 
     def rows_per_batch(self) -> float:
         return self.stats["passes"] / max(1, self.stats["batches"])

@@ -117,14 +117,14 @@ class LLMIntentEngine:
         # wait for the sampled tokens by polling the pinned readback buffer (sentinel -> token)
         # instead of a stream synchronize: the GPU idles from the sampler's end until the host
         # has posted the next step, so the wake-up latency is on the critical path
-        self.spin_wait = pin and ops.env_flag("VWA_SPIN_WAIT", True)
+        self.spin_wait = pin and ops.env_flag("VWA_SPIN_WAIT")
         # LM head under the grammar mask (LLMEngine.head_logits): the vocab tiles no row may sample
         # are skipped -- 42 % of the tiles live per step on average on the intent grammar
-        self.masked_head = ops.env_flag("VWA_MASKED_HEAD", True)
+        self.masked_head = ops.env_flag("VWA_MASKED_HEAD")
         # zero-copy host buffers (GPU): the LM head and the sampler read the grammar masks straight
         # from the pinned host rows and the sampler stores the tokens into pinned host memory -- no
         # H2D mask copy and no D2H token copy per step (each a DMA start on the critical path)
-        self.zero_copy = pin and ops.env_flag("VWA_ZERO_COPY", True)
+        self.zero_copy = pin and ops.env_flag("VWA_ZERO_COPY")
         self.part_val = torch.zeros(R * 64, dtype=torch.float32, device=dev)
         self.part_idx = torch.zeros(R * 64, dtype=torch.int32, device=dev)
         self.last_stats: Dict[str, Any] = {}

@@ -29,6 +29,7 @@ from ..utils.context import cap_context
 from ..utils.metrics import Metrics
 from .prompt import messages_for
 from .tp_engine import TPIntentEngine  # noqa: F401  (re-exported: the TP control plane)
+from ..utils.env import knob
 
 SERVICE_NAME = "brain-ts"  # byte-compatible /health payload (apps/brain/src/server.ts:87)
 
@@ -118,7 +119,7 @@ def build_app(engine: Any = None) -> web.Application:
 
 
 def make_engine_from_env():
-    kind = os.environ.get("VWA_BRAIN_ENGINE", "keyword")
+    kind = knob("VWA_BRAIN_ENGINE")
     if kind == "keyword":
         from .intent_engine import FakeIntentEngine, keyword_intents
 
@@ -144,21 +145,21 @@ def build_llm_engine(model_name: Optional[str] = None, device: Optional[str] = N
     from .intent_engine import LLMIntentEngine
     from .prompt import llama3_chat, plain_chat
 
-    name = model_name or os.environ.get("VWA_LLM_MODEL", "llama3-8b")
+    name = model_name or knob("VWA_LLM_MODEL")
     cfg = get_config(name)
-    seed = int(os.environ.get("VWA_SEED", "0"))
+    seed = knob("VWA_SEED")
     dev = device or ("cuda" if torch.cuda.is_available() else "cpu")
-    sessions = int(os.environ.get("VWA_MAX_SESSIONS", "8"))
-    budget = int(os.environ.get("VWA_BUDGET_CHARS", "512"))
-    wpath = os.environ.get("VWA_LLM_WEIGHTS") or None  # safetensors checkpoint (HF names)
+    sessions = knob("VWA_MAX_SESSIONS")
+    budget = knob("VWA_BUDGET_CHARS")
+    wpath = knob("VWA_LLM_WEIGHTS") or None  # safetensors checkpoint (HF names)
     if isinstance(cfg, GPT2Config):
         model = load_llm(name, device=dev, seed=seed, weights_path=wpath)
         eng = LLMEngine(model, max_seqs=sessions, max_model_len=cfg.max_pos)
         eng.capture_all()
         return LLMIntentEngine(eng, load_tokenizer("gpt2"), budget_chars=budget, chat_format=plain_chat)
-    tp = init_distributed(tp_size=int(os.environ.get("VWA_TP", "1") or 1))
+    tp = init_distributed(tp_size=knob("VWA_TP"))
     model = load_llm(name, device=dev, tp=tp, seed=seed, weights_path=wpath,
-                     wdtype=os.environ.get("VWA_DTYPE", "bf16"))
+                     wdtype=knob("VWA_DTYPE"))
     eng = LLMEngine(model, max_seqs=sessions, max_model_len=4096)
     eng.capture_all()
     ie = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=budget, chat_format=llama3_chat)
@@ -169,7 +170,7 @@ def main():
     from ..utils.env import load_dotenv
 
     load_dotenv()
-    port = int(os.environ.get("BRAIN_PORT", "8090"))
+    port = knob("BRAIN_PORT")
     engine = make_engine_from_env()
     if isinstance(engine, TPIntentEngine) and engine.tp.rank != 0:
         engine.worker_loop()  # TP worker: no HTTP, follows rank 0's requests

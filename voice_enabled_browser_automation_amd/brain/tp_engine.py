@@ -36,12 +36,13 @@ from concurrent.futures import Future
 from typing import Any, Callable, Deque, List, Optional, Tuple
 
 from .prompt import messages_for
+from ..utils.env import knob
 
 FATAL_EXIT_CODE = 70  # EX_SOFTWARE: the TP group must be restarted as a whole
 # An idle leader sends an empty control message this often: the workers block in a gloo broadcast
 # between iterations, and a broadcast that waits past the group's timeout (torch default 30 min)
 # raises -- which the failure policy would turn into a needless group restart.
-HEARTBEAT_S = float(os.environ.get("VWA_TP_HEARTBEAT_S", "5"))
+HEARTBEAT_S = knob("VWA_TP_HEARTBEAT_S")
 
 
 def _default_fatal(exc: BaseException) -> None:
@@ -63,7 +64,9 @@ class TPIntentEngine:
 
         self.inner = inner
         self.tp = tp
-        self.ctl = ctl_group if ctl_group is not None else dist.new_group(backend="gloo")
+        # the TP group's own gloo group (parallel/tp.py init_distributed); a world-wide one only for
+        # a context built by hand with a single TP group
+        self.ctl = ctl_group if ctl_group is not None else (getattr(tp, "ctl", None) or dist.new_group(backend="gloo"))
         self.on_fatal = on_fatal or _default_fatal
         self.failed: Optional[BaseException] = None
         self._incoming: Deque[Tuple[List[dict], Future]] = deque()
@@ -83,6 +86,14 @@ class TPIntentEngine:
     @property
     def batch_stats(self):
         return self.inner.batch_stats
+
+    @property
+    def timing(self):
+        return self.inner.timing
+
+    @property
+    def last_batch(self):
+        return self.inner.last_batch
 
     def engine_stats(self):
         out = dict(self.inner.engine_stats())

@@ -27,12 +27,13 @@ from typing import Any, Dict, List, Optional
 
 from .artifacts import screenshot_path, write_csv, write_json
 from .dom_analyzer import DOMAnalyzer, best_search_element, find_by_selector, find_by_text
+from ..utils.env import knob
 
 DEFAULT_TIMEOUT_MS = 15000
 SEARCH_WAIT_MS = 5000
 LEGACY_SEARCH_SELECTORS = ['input[name="q"]', 'input[type="search"]', 'input[aria-label*="Search" i]',
                            'input[placeholder*="Search" i]', "#search", 'input[name*="search" i]']
-UPLOAD_DIR = os.environ.get("UPLOAD_DIR", ".uploads")
+UPLOAD_DIR = knob("UPLOAD_DIR")
 
 EXTRACT_JS = r"""
 ([sel, limit, columns]) => {

@@ -9,10 +9,11 @@ import os
 from typing import Any, Dict
 
 import aiohttp
+from ..utils.env import knob
 
 
 async def create_browserbase_session(api_key: str, project_id: str, api_base: str = "") -> Dict[str, Any]:
-    base = api_base or os.environ.get("BROWSERBASE_API_BASE", "https://api.browserbase.com/v1")
+    base = api_base or knob("BROWSERBASE_API_BASE")
     async with aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=60)) as s:
         async with s.post(f"{base}/sessions", json={"projectId": project_id},
                           headers={"X-BB-API-Key": api_key, "Content-Type": "application/json"}) as r:

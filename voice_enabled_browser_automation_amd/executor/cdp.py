@@ -36,6 +36,7 @@ import threading
 from typing import Any, Dict, List, Optional
 
 import aiohttp
+from ..utils.env import knob
 
 # Keys Input.dispatchKeyEvent needs spelled out (Playwright key names)
 _KEYS = {
@@ -456,7 +457,7 @@ class CdpPage:
 
 # ---------------------------------------------------------------------- endpoints
 def find_chrome() -> Optional[str]:
-    p = os.environ.get("CHROME_PATH")
+    p = knob("CHROME_PATH")
     if p and os.path.isfile(p):
         return p
     for name in ("google-chrome", "google-chrome-stable", "chromium", "chromium-browser", "chrome"):

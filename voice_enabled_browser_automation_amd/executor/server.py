@@ -20,6 +20,7 @@ from ..contracts import ExecuteRequest, safe_parse
 from ..utils.metrics import Metrics
 from .actions import run_intents
 from .session import SessionManager
+from ..utils.env import knob
 
 
 @web.middleware
@@ -39,7 +40,7 @@ async def cors(request: web.Request, handler):
 def build_app(sessions: Optional[SessionManager] = None, upload_dir: Optional[str] = None) -> web.Application:
     app = web.Application(middlewares=[cors], client_max_size=64 * 1024 * 1024)
     app["sessions"] = sessions or SessionManager()
-    app["upload_dir"] = upload_dir or os.environ.get("UPLOAD_DIR", ".uploads")
+    app["upload_dir"] = upload_dir or knob("UPLOAD_DIR")
     app["metrics"] = Metrics("executor")
 
     async def health(_req):
@@ -113,7 +114,7 @@ def main():
     from ..utils.env import load_dotenv
 
     load_dotenv()
-    port = int(os.environ.get("EXECUTOR_PORT", "7081"))
+    port = knob("EXECUTOR_PORT")
     print(f"[executor] listening on http://127.0.0.1:{port}", flush=True)
     web.run_app(build_app(), host="127.0.0.1", port=port, print=None)
 

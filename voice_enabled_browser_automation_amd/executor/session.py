@@ -21,6 +21,7 @@ import os
 import uuid
 from dataclasses import dataclass, field
 from typing import Any, Awaitable, Callable, Dict, Optional
+from ..utils.env import knob
 
 
 @dataclass
@@ -38,7 +39,7 @@ PageFactory = Callable[[str], Awaitable[Session]]
 
 
 def artifacts_dir() -> str:
-    return os.environ.get("ARTIFACTS_DIR", ".artifacts")
+    return knob("ARTIFACTS_DIR")
 
 
 async def _cdp_factory(sid: str) -> Session:
@@ -48,22 +49,22 @@ async def _cdp_factory(sid: str) -> Session:
 
     d = os.path.join(artifacts_dir(), sid)
     os.makedirs(d, exist_ok=True)
-    bb_key, bb_proj = os.environ.get("BROWSERBASE_API_KEY"), os.environ.get("BROWSERBASE_PROJECT_ID")
-    if os.environ.get("CDP_URL"):
-        conn = await cdp.connect(os.environ["CDP_URL"])
+    bb_key, bb_proj = knob("BROWSERBASE_API_KEY"), knob("BROWSERBASE_PROJECT_ID")
+    if knob("CDP_URL"):
+        conn = await cdp.connect(knob("CDP_URL"))
     elif bb_key and bb_proj:
         from .browserbase import create_browserbase_session
 
         conn = await cdp.connect((await create_browserbase_session(bb_key, bb_proj))["connectUrl"])
     else:
-        conn = await cdp.launch_chrome(headless=os.environ.get("EXECUTOR_HEADLESS", "false") == "true")
+        conn = await cdp.launch_chrome(headless=knob("EXECUTOR_HEADLESS"))
     page = await conn.new_page()
     return Session(id=sid, page=page, dir=d, browser=conn)
 
 
 def _driver() -> str:
     """``VWA_BROWSER_DRIVER``: playwright | cdp | auto (default: Playwright when importable)."""
-    want = os.environ.get("VWA_BROWSER_DRIVER", "auto")
+    want = knob("VWA_BROWSER_DRIVER")
     if want != "auto":
         return want
     try:
@@ -80,7 +81,7 @@ async def _playwright_factory(sid: str) -> Session:
     d = os.path.join(artifacts_dir(), sid)
     os.makedirs(d, exist_ok=True)
     pw = await async_playwright().start()
-    bb_key, bb_proj = os.environ.get("BROWSERBASE_API_KEY"), os.environ.get("BROWSERBASE_PROJECT_ID")
+    bb_key, bb_proj = knob("BROWSERBASE_API_KEY"), knob("BROWSERBASE_PROJECT_ID")
     if bb_key and bb_proj:
         from .browserbase import create_browserbase_session
 
@@ -88,7 +89,7 @@ async def _playwright_factory(sid: str) -> Session:
         browser = await pw.chromium.connect_over_cdp(bb["connectUrl"])
         context = browser.contexts[0] if browser.contexts else await browser.new_context()
     else:
-        headless = os.environ.get("EXECUTOR_HEADLESS", "false") == "true"
+        headless = knob("EXECUTOR_HEADLESS")
         try:
             browser = await pw.chromium.launch(channel="chrome", headless=headless)
         except Exception:  # noqa: BLE001  (no branded Chrome: bundled chromium, as the legacy session.js)

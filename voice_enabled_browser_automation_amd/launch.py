@@ -19,6 +19,7 @@ import signal
 import subprocess
 import sys
 import time
+from .utils.env import knob
 
 PKG = "voice_enabled_browser_automation_amd"
 
@@ -171,18 +172,18 @@ def _visible_gpus() -> int:
 
 
 def main():
-    tp = int(os.environ.get("VWA_TP", "1") or 1)
-    plan = plan_gpus(_visible_gpus(), tp, os.environ.get("VWA_BRAIN_GPUS", ""), os.environ.get("VWA_VOICE_GPUS", ""),
+    tp = knob("VWA_TP")
+    plan = plan_gpus(_visible_gpus(), tp, knob("VWA_BRAIN_GPUS"), knob("VWA_VOICE_GPUS"),
                      parent_visible=_parent_visible())
     voice_gpus = plan["voice"]
     benv = {"HIP_VISIBLE_DEVICES": ",".join(plan["brain"])}
     if plan["shared"]:
         benv.update(shared_gpu_env(os.environ))
-    sup = Supervisor(max_restarts=int(os.environ.get("VWA_BRAIN_MAX_RESTARTS", "5")))
+    sup = Supervisor(max_restarts=knob("VWA_BRAIN_MAX_RESTARTS"))
     sup.add("brain", f"{PKG}.brain.server", benv, tp, restartable=True)
     if len(voice_gpus) > 1:
         # ASR session-DP: one voice worker per GPU behind the router on VOICE_PORT (voice/router.py)
-        base = int(os.environ.get("VWA_VOICE_BASE_PORT", "7100"))
+        base = knob("VWA_VOICE_BASE_PORT")
         for i, g in enumerate(voice_gpus):
             sup.add(f"voice{i}", f"{PKG}.voice.server", {"HIP_VISIBLE_DEVICES": g, "VOICE_PORT": str(base + i)})
         sup.add("router", f"{PKG}.voice.router", {"VWA_DP": str(len(voice_gpus))})

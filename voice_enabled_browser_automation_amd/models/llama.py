@@ -83,7 +83,7 @@ class LlamaModel:
             self._quantize_fp8()
         elif wdtype != "bf16":
             raise ValueError(f"unsupported weight dtype {wdtype!r} (bf16 | fp8)")
-        elif self.device.type == "cuda" and dtype == torch.bfloat16 and ops.env_flag("VWA_TILED_WEIGHTS", True):
+        elif self.device.type == "cuda" and dtype == torch.bfloat16 and ops.env_flag("VWA_TILED_WEIGHTS"):
             self._tile_weights()
 
     def _tile_weights(self) -> None:
@@ -100,7 +100,7 @@ class LlamaModel:
     def _quantize_fp8(self) -> None:
         """OCP e4m3 + per-row scales; on the GPU stored once, in the fp8 tiled layout
         (ops.tile_weight_fp8) the W8A8 streaming kernel and the fp8 GEMM read."""
-        tiled = self.device.type == "cuda" and ops.env_flag("VWA_TILED_WEIGHTS", True)
+        tiled = self.device.type == "cuda" and ops.env_flag("VWA_TILED_WEIGHTS")
         q = lambda w: ops.FP8Weight.quantize(w, tiled=tiled)  # noqa: E731
         for L in self.layers:
             L.qkv, L.o, L.gu, L.down = q(L.qkv), q(L.o), q(L.gu), q(L.down)
@@ -220,41 +220,17 @@ class LlamaModel:
         # fp8: the W8A16 chain over the fp8 tiled weights (<= 4 rows: no X streaming)
         fp8_ok = self.wdtype == "fp8" and M <= 4 and isinstance(self.layers[0].o, ops.FP8Weight) and self.layers[0].o.tiled
         # TP > 1: the one-shot all-reduce buffers carry the in-launch rounds (chain_tp_reduce)
-        tp_ok = self.tp.size == 1 or (getattr(self.tp, "custom_ar", None) is not None and ops.env_flag("VWA_CHAIN_TP", True))
-        return (M <= ops.env_int("VWA_CHAIN_MAX_ROWS", 4) and tp_ok and (self.wdtype == "bf16" or fp8_ok)
+        tp_ok = self.tp.size == 1 or (getattr(self.tp, "custom_ar", None) is not None and ops.env_flag("VWA_CHAIN_TP"))
+        return (M <= ops.env_int("VWA_CHAIN_MAX_ROWS") and tp_ok and (self.wdtype == "bf16" or fp8_ok)
                 and self.device.type == "cuda" and not getattr(self, "_chain_disabled", False)
-                and ops.env_flag("VWA_CHAIN", True) and ops.native_available())
-
-    def _chain2_ok(self, M: int) -> bool:
-        """5..16 rows (VWA_CHAIN2=1): o_proj -> gate/up as ONE chained launch (both X row blocks fit
-        LDS), attention / down / QKV as their own launches (skinny_stream.hip chain_kernel NPH 2)."""
-        return (5 <= M <= 16 and self.tp.size == 1 and self.wdtype == "bf16" and self.device.type == "cuda"
-                and isinstance(self.layers[0].o, ops.TiledWeight) and not getattr(self, "_chain_disabled", False)
-                and ops.env_flag("VWA_CHAIN", True) and ops.env_flag("VWA_CHAIN2", False) and ops.native_available())
+                and ops.env_flag("VWA_CHAIN") and ops.native_available())
 
     def _chain_any(self, M: int) -> bool:
-        """Whether a step of M rows runs a chained launch (either form): the engine then checks the
-        launch's barrier error word and re-runs a timed-out step on the per-kernel path."""
-        return self._chain_ok(M) or self._chain2_ok(M)
-
-    def _chain2_desc(self, bufs, M: int, li: int):
-        """(descriptor, lds) of layer li's chained o_proj -> gate/up for this engine's buffers (None if
-        the shapes do not fit), cached like _chain_desc."""
-        if not isinstance(getattr(self, "_chains", None), weakref.WeakKeyDictionary):
-            self.reset_chains()
-        cache = self._chains.setdefault(bufs, {})
-        key = ("c2", M, li)
-        if key in cache:
-            return cache[key]
-        if getattr(self, "_chain_bar", None) is None:
-            self._chain_bar, self._chain_bar_mode, self._chain_work = ops.chain_buffers(self.device)
-        L = self.layers[li]
-        desc, lds = ops.ext().chain_make(
-            bufs.hidden[:M], bufs.attn[:M], bufs.act[:M], L.o.t, L.gu.t, L.down.t, self.cfg.rms_eps, None, self.nq,
-            self.nkv, self.hd, None, None, None, None, None, None, self._chain_bar, self._chain_work, None,
-            self._chain_bar_mode, w_tiled=True, tail_n=2)
-        cache[key] = (desc, lds) if desc.numel() else None
-        return cache[key]
+        """Whether a step of M rows runs a chained launch: the engine then checks the launch's
+        barrier error word and re-runs a timed-out step on the per-kernel path.  (Round 4's 2-phase
+        o_proj -> gate/up chain for 5..16 rows measured no faster -- its barrier cost what the saved
+        launch gap did, profiles/r4_chain2_o_gu_rows.jsonl -- and was removed in round 5.)"""
+        return self._chain_ok(M)
 
     def disable_chain(self) -> None:
         self._chain_disabled = True
@@ -306,7 +282,7 @@ class LlamaModel:
         # (the chained attention addresses K/V through per-row copies of the block table, which
         # the step buffers keep for contexts of <= 128 blocks, in 16-token blocks: otherwise the
         # separate launch)
-        attn = (M <= 4 and self.hd == 128 and self.nq // self.nkv in (4, 8) and ops.env_flag("VWA_CHAIN_ATTN", True)
+        attn = (M <= 4 and self.hd == 128 and self.nq // self.nkv in (4, 8) and ops.env_flag("VWA_CHAIN_ATTN")
                 and ops.decode_n_splits(bufs.max_ctx) > 1 and getattr(bufs, "rt_cols", 0) > 0
                 and kv.k[li].shape[2] == 16)
         a = {}
@@ -376,15 +352,12 @@ class LlamaModel:
         # for 84 queries over 1.1k keys: 64 workgroups each walking every key tile)
         pf_slices = None
         if (prefill_seq is not None and q_offset >= M and M <= 256 and self.device.type == "cuda"
-                and ops.env_flag("VWA_PREFILL_DECODE_ATTN", True)):
+                and ops.env_flag("VWA_PREFILL_DECODE_ATTN")):
             i32 = dict(dtype=torch.int32, device=self.device)
             pf_ctx = torch.arange(q_offset + 1, q_offset + M + 1, **i32)
             pf_sid = torch.full((M,), prefill_seq, **i32)
             pf_slices = [(i, min(M, i + 64)) for i in range(0, M, 64)]
             pf_out = torch.empty((M, self.nq * self.hd), dtype=self.dtype, device=self.device)
-        # fp8 rows > 16 (TP = 1: h is written only by the GEMM epilogues inside the loop): each W8A8
-        # GEMM's split-K reduce also quantises its output rows for the next one (ops.row_quant_handoff)
-        ops.row_quant_handoff(self.wdtype == "fp8" and self.tp.size == 1)
         for li, L in enumerate(self.layers):
             kc, vc = kv.k[li], kv.v[li]
             if chain and li > 0:
@@ -434,17 +407,10 @@ class LlamaModel:
                 ops.flash_attention(q4, ops.KVLayout.paged(kc, vc, table), Sk=q_offset + M, n_kv_heads=self.nkv,
                                     causal=True, scale=self.scale, q_offset=q_offset, out=attn4)
                 attn = attn4.view(M, self.nq * self.hd)
-            # (the chained o_proj reads bufs.attn: the decode-attention output of the step buffers)
-            d2 = self._chain2_desc(bufs, M, li) if prefill_seq is None and self._chain2_ok(M) else None
-            if d2 is not None:  # chained o_proj -> gate/up (5..16 rows)
-                ops.ext().chain_run(d2[0], 2, d2[1], h)
-                act = bufs.act[:M]
-            else:
-                self._row_parallel(attn, L.o, h)
-                act = bufs.act[:M] if M <= bufs.act.shape[0] else None
-                act = ops.linear_swiglu(h, L.gu, fuse_rms=True, eps=cfg.rms_eps, out=act)
+            self._row_parallel(attn, L.o, h)
+            act = bufs.act[:M] if M <= bufs.act.shape[0] else None
+            act = ops.linear_swiglu(h, L.gu, fuse_rms=True, eps=cfg.rms_eps, out=act)
             self._row_parallel(act, L.down, h)
-        ops.row_quant_handoff(False)
         if n_sel is not None:
             hs = torch.index_select(h, 0, bufs.sel[:n_sel], out=bufs.hidden_sel[:n_sel])
         else:

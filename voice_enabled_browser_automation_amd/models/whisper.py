@@ -299,7 +299,7 @@ class WhisperModel:
     # arrival spread + two-level atomics in uncached memory) costs what a kernel boundary does.
     def _chain_ok(self, M: int) -> bool:
         return (M <= 4 and self.device.type == "cuda" and self.dtype == torch.bfloat16
-                and not getattr(self, "_chain_disabled", False) and ops.env_flag("VWA_CHAIN_ASR", False)
+                and not getattr(self, "_chain_disabled", False) and ops.env_flag("VWA_CHAIN_ASR")
                 and ops.native_available() and all(hasattr(L, "f_qkv") for L in self.dec))
 
     def disable_chain(self) -> None:

@@ -19,11 +19,11 @@ Layout conventions shared by kernels, reference and models:
 from __future__ import annotations
 
 import math
-import os
 from typing import Dict, Optional, Tuple
 
 import torch
 
+from ..utils.env import knob
 from . import reference as ref
 
 _EXT = None
@@ -38,7 +38,7 @@ def ext():
     if _EXT_ERR is not None:
         raise RuntimeError(f"native gfx950 kernel library unavailable: {_EXT_ERR}") from _EXT_ERR
     try:
-        alt = os.environ.get("VWA_KERNEL_SO")  # (A/B experiments: another build of the same library)
+        alt = knob("VWA_KERNEL_SO")  # (A/B experiments: another build of the same library)
         if alt:
             import importlib.machinery
             import importlib.util
@@ -51,28 +51,17 @@ def ext():
         else:
             from . import _vwa_kernels as m  # type: ignore
 
-        impl = os.environ.get("VWA_ATTN_IMPL")
+        # diagnostic overrides (utils/env.py Settings; defaults are the measured-best settings)
+        impl = knob("VWA_ATTN_IMPL")
         if impl:
             m.set_attention_impl(ATTENTION_IMPLS[impl])
-        p8 = os.environ.get("VWA_GEMM_P8")  # 0: 128x128 GEMM only, 1: 256x256 8-phase wherever eligible
+        p8 = knob("VWA_GEMM_P8")  # 0: 128x128 GEMM only, 1: 256x256 8-phase wherever eligible
         if p8 not in (None, ""):
             m.gemm_set_p8(int(p8))
-        nb = os.environ.get("VWA_GEMM_NB")  # stage buffers of few-row (one row block) GEMMs: 4 / 2
-        if nb not in (None, ""):
-            m.gemm_set_nb(int(nb))
-        ga = os.environ.get("VWA_SKINNY_GRID_ADAPT")  # one workgroup per tile up to 2x the grid cap
-        if ga not in (None, ""):
-            m.skinny_set_grid_adapt(int(ga))
-        nt2 = os.environ.get("VWA_SKINNY_NT2_ROWS")  # store/resid/GELU GEMMs: 32-column tiles from this many rows
-        if nt2 not in (None, ""):
-            m.skinny_set_nt2_rows(int(nt2))
-        xsk = os.environ.get("VWA_SKINNY_X_SKEW")  # LDS-staged X rows: 64-B skew every 4 rows (1) / none (0)
+        xsk = knob("VWA_SKINNY_X_SKEW")  # LDS-staged X rows: 64-B skew every 4 rows (1) / none (0)
         if xsk not in (None, ""):
             m.skinny_set_x_skew(int(xsk))
-        xg = os.environ.get("VWA_SKINNY_XG_ROWS")  # <= 16-row streaming GEMM: X streamed from this many rows
-        if xg not in (None, ""):
-            m.skinny_set_xg_rows(int(xg))
-        fill = os.environ.get("VWA_GEMM_SPLIT_FILL")  # split-K until tiles x splits >= this % of CUs
+        fill = knob("VWA_GEMM_SPLIT_FILL")  # split-K until tiles x splits >= this % of CUs
         if fill not in (None, ""):
             m.gemm_set_split_fill(int(fill))
         _EXT = m
@@ -193,10 +182,24 @@ def _fp8_stream_fits(M: int, K: int, nt: int = 1) -> bool:
 _SCALED_MM_OK: Optional[bool] = None
 
 
+def vendor_fallback(what: str) -> None:
+    """Called on every op path that leaves the hand-written kernels for a vendor library (hipBLASLt
+    through torch.matmul / torch._scaled_mm) on a GPU tensor.  VWA_STRICT_NATIVE=1 (the GPU tests,
+    bench.py) turns it into an error, so a new shape landing on a silent fallback is caught; the
+    count is kept either way (``vendor_fallbacks``)."""
+    vendor_fallbacks[what] = vendor_fallbacks.get(what, 0) + 1
+    if knob("VWA_STRICT_NATIVE"):
+        raise RuntimeError(f"strict native mode: {what} would fall back to a vendor library")
+
+
+vendor_fallbacks: Dict[str, int] = {}
+
+
 def _fp8_matmul(x: torch.Tensor, w: "FP8Weight") -> torch.Tensor:
     """x [M, K] bf16 @ W8^T for large M with an UNTILED fp8 weight (tiled ones take gemm_fp8):
     hipBLASLt fp8 GEMM with row-wise scales, or dequantise."""
     global _SCALED_MM_OK
+    vendor_fallback(f"fp8 matmul {tuple(x.shape)} x {tuple(w.shape)}")
     if _SCALED_MM_OK is not False and hasattr(torch, "_scaled_mm"):
         try:
             x8 = torch.empty(x.shape, dtype=torch.float8_e4m3fn, device=x.device)
@@ -274,10 +277,8 @@ class TiledWeight:
 
 
 def _stream_ok(x: torch.Tensor, w) -> bool:
-    """Decode rows the streaming kernel takes with a pre-tiled weight: up to STREAM_MAX_M (64) --
-    above 16 rows with 2 or 4 X row fragments per streamed weight fragment (skinny_stream.hip MT),
-    one persistent launch with the fused epilogue instead of split-K GEMM + reduce launches."""
-    return x.shape[0] <= STREAM_MAX_M and x.shape[1] % 128 == 0 and w.shape[0] % 16 == 0
+    """Decode rows (<= SKINNY_MAX_M) the streaming kernel takes with a pre-tiled weight."""
+    return x.shape[0] <= SKINNY_MAX_M and x.shape[1] % 128 == 0 and w.shape[0] % 16 == 0
 
 
 def plain(w):
@@ -396,26 +397,9 @@ def scratch(device, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
 
 
 GEMM_WS_FLOATS = 32 << 20  # split-K workspace (128 MB per device: 4 f32 slices of a 1k x 4096 output)
-# One-launch split-K (gemm.hip, opt-in VWA_GEMM_ONE_LAUNCH=1): the last slice of each output tile
-# reduces the slabs and runs the epilogue, so a split GEMM is one kernel instead of GEMM +
-# gemm_reduce.  Per-tile arrival counters, zeroed once and reset by each tile's last arriver.
-# Measured NOT faster at 32 decode rows (profiles/r4_gemm_one_launch_ab.md): the tail -- write-through
-# partial stores drained, the ticket, the L2-missing partial loads -- costs about what the reduce
-# launch does (fp8 o / down 26.3 vs 20.2 + 5.2 us).
-GEMM_ONE_LAUNCH = os.environ.get("VWA_GEMM_ONE_LAUNCH", "0") == "1"
-_GEMM_TICKETS: Dict[str, torch.Tensor] = {}
-
-
-def gemm_tickets(device) -> Optional[torch.Tensor]:
-    if not GEMM_ONE_LAUNCH:
-        return None
-    dev = torch.device(device)
-    if dev.type == "cuda" and dev.index is None:
-        dev = torch.device("cuda", torch.cuda.current_device())
-    t = _GEMM_TICKETS.get(str(dev))
-    if t is None:
-        t = _GEMM_TICKETS[str(dev)] = torch.zeros(1 << 14, dtype=torch.int32, device=dev)
-    return t
+# (a one-launch split-K -- the last slice of each tile reducing -- measured no faster at 32 decode
+# rows: the write-through drain + ticket + L2-missing partial loads cost what the reduce launch
+# does, fp8 o / down 26.3 vs 20.2 + 5.2 us, profiles/r4_gemm_one_launch_ab.md; removed in round 5)
 
 
 _GEMM_EPI = {"none": 0, "resid": 1, "swiglu": 2, "gelu": 3}
@@ -434,7 +418,7 @@ def gemm(x: torch.Tensor, w, out: torch.Tensor, *, epi: str = "none", bias: Opti
     tiled = isinstance(w, TiledWeight)
     wt = w.t if tiled else w
     ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
-    E.gemm(x, wt, bias, out, _GEMM_EPI[epi], rstd, residual, tiled, ws, gemm_tickets(x.device))
+    E.gemm(x, wt, bias, out, _GEMM_EPI[epi], rstd, residual, tiled, ws)
     return out
 
 
@@ -442,55 +426,19 @@ def _rows16(t: Optional[torch.Tensor]) -> bool:
     return t is None or (t.stride(-1) == 1 and t.stride(0) % 8 == 0 and t.data_ptr() % 16 == 0)
 
 
-# Row-quantisation hand-off between consecutive W8A8 GEMMs on the same rows (the fp8 decode step
-# of > 16 rows): a GEMM whose split-K reduce can also quantise its output rows (gemm.hip
-# gemm_reduce_rowq_kernel) leaves the e4m3 codes / scales / 1/rms in the next GEMM's input staging
-# buffers, and the next GEMM reading that output skips its quant_fp8_rows launch.  Enabled only
-# around a model's layer loop (models/llama.py), where the hand-off tensor (the residual stream /
-# the SwiGLU output) is written by nothing but those GEMMs; the key is (pointer, shape, row stride).
-_QHAND = {"on": False, "key": None, "eps": None, "n": 0}
-
-
-def row_quant_handoff(enabled: bool) -> None:
-    # opt-in (VWA_ROWQ_HANDOFF=1): measured slower in whole fp8 decode steps (32 rows 5.31 vs 4.97 ms,
-    # profiles/r4_gemm_ab.md) -- the one-workgroup-per-row reduce is latency-bound on the
-    # 14336-wide SwiGLU rows (21 us vs 6 + 5 for the reduce and quant launches)
-    _QHAND.update(on=bool(enabled) and os.environ.get("VWA_ROWQ_HANDOFF", "0") == "1", key=None, eps=None)
-
-
-def _qhand_guard(fn):
-    """A projection that wrote the hand-off tensor by any other path (not gemm_fp8) invalidates it."""
-    import functools
-
-    @functools.wraps(fn)
-    def wrapped(*a, **k):
-        n0 = _QHAND["n"]
-        y = fn(*a, **k)
-        key = _QHAND["key"]
-        if key is not None and _QHAND["n"] == n0 and isinstance(y, torch.Tensor) and y.data_ptr() == key[0]:
-            _QHAND["key"] = None
-        return y
-
-    return wrapped
-
-
-def _qkey(t: torch.Tensor):
-    return (t.data_ptr(), tuple(t.shape), t.stride(0))
-
-
-def _fp8_staging(x: torch.Tensor, K: int, n_out: int = 0):
+def _fp8_staging(x: torch.Tensor, K: int):
     M = x.shape[0]
-    x8 = scratch(x.device, "gemm_x8", M * max(K, n_out), torch.uint8).view(torch.float8_e4m3fn)
+    x8 = scratch(x.device, "gemm_x8", M * K, torch.uint8).view(torch.float8_e4m3fn)
     return x8, scratch(x.device, "gemm_sx", M), scratch(x.device, "gemm_rstd", M)
 
 
 def _fp8_input(x: torch.Tensor, fuse_rms: bool, eps: float):
-    """(x8 [M, K], sx, rstd or None) of x: the hand-off of the GEMM that wrote x, or one row pass."""
+    """(x8 [M, K], sx, rstd or None): x quantised per row by one kernel that also yields the
+    RMSNorm 1/rms.  (Round 4's opt-in hand-off -- the previous GEMM's split-K reduce quantising its
+    output rows -- measured slower in whole fp8 steps, profiles/r4_gemm_ab.md; removed in round 5.)"""
     M, K = x.shape
     x8, sx, rs = _fp8_staging(x, K)
-    if not (_QHAND["on"] and _QHAND["key"] == _qkey(x) and _QHAND["eps"] == eps):
-        E = ext()
-        E.quant_fp8_rows(x, x8[: M * K].view(M, K), sx, rs if fuse_rms else None, eps)
+    ext().quant_fp8_rows(x, x8[: M * K].view(M, K), sx, rs if fuse_rms else None, eps)
     return x8[: M * K].view(M, K), sx, (rs if fuse_rms else None)
 
 
@@ -498,26 +446,12 @@ def gemm_fp8(x: torch.Tensor, w: "FP8Weight", out: torch.Tensor, *, epi: str = "
              bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, fuse_rms: bool = False,
              eps: float = 1e-5) -> torch.Tensor:
     """W8A8 tiled MFMA GEMM (gemm.hip F8) for M > 16 rows: x is quantised per row (amax / 448, one
-    kernel that also yields the RMSNorm 1/rms -- or the previous GEMM's hand-off), the fp8 MFMA runs
-    on the tiled fp8 weight, both scales (and the RMSNorm 1/rms of the unquantised x) apply in the
-    epilogue.  Inside row_quant_handoff: the output rows are quantised for the next GEMM too."""
+    kernel that also yields the RMSNorm 1/rms), the fp8 MFMA runs on the tiled fp8 weight, both
+    scales (and the RMSNorm 1/rms of the unquantised x) apply in the epilogue."""
     E = ext()
-    M, K = x.shape
     x8, sx, rstd = _fp8_input(x, fuse_rms, eps)
     ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
-    tk = gemm_tickets(x.device)
-    # (residual epilogues only: the 4096-wide residual rows reduce + quantise in one pass faster than
-    # the two launches; the 14336-wide SwiGLU rows do not -- profiles/r4_gemm_ab.md)
-    if not _QHAND["on"] or out.dtype != torch.bfloat16 or epi != "resid":
-        E.gemm_fp8(x8, sx, w.w8, w.scale, bias, out, _GEMM_EPI[epi], rstd, residual, ws, tk)
-        return out
-    n_out = out.shape[1]
-    q8, qs, qr = _fp8_staging(x, K, n_out)
-    q8 = q8[: M * n_out].view(M, n_out)
-    # (the output's codes overwrite this GEMM's input codes -- in stream order, after it read them)
-    if not E.gemm_fp8(x8, sx, w.w8, w.scale, bias, out, _GEMM_EPI[epi], rstd, residual, ws, tk, q8, qs, qr, eps):
-        E.quant_fp8_rows(out, q8, qs, qr, eps)  # (no split-K reduce to fold it into)
-    _QHAND.update(key=_qkey(out), eps=eps, n=_QHAND["n"] + 1)
+    E.gemm_fp8(x8, sx, w.w8, w.scale, bias, out, _GEMM_EPI[epi], rstd, residual, ws)
     return out
 
 
@@ -539,14 +473,11 @@ def gemm_ok(x: torch.Tensor, w, out: Optional[torch.Tensor] = None, residual: Op
 # Rows handled by the MFMA streaming (skinny) kernels; above this the hand-written LDS-tiled MFMA
 # GEMM (gemm.hip) takes the step (continuous batching of many sessions, prefill).
 SKINNY_MAX_M = 16
-# Rows the streaming kernel takes with PRE-TILED bf16 weights.  17..64 rows are supported
-# (skinny_stream.hip MT = 2 / 4, X streamed with the weights) but measured slower than the tiled
-# GEMM for whole decode steps (Llama-3-8B, tools/rows_sweep.py, profiles/r4_rows_sweep_*: 32 rows
-# 6.89 vs 5.65 ms, 64 rows 11.0 vs 6.9 ms): opt-in with VWA_STREAM_MAX_M.
-STREAM_MAX_M = max(16, min(64, int(os.environ.get("VWA_STREAM_MAX_M", "16"))))
+# (round 4 built a 17..64-row form of the streaming kernel -- X streamed with the weights, MT = 2 /
+# 4 row fragments -- and measured it slower than the tiled GEMM for whole decode steps, 32 rows
+# 6.89 vs 5.65 ms, 64 rows 11.0 vs 6.9 ms, profiles/r4_rows_sweep_*; removed in round 5.)
 
 
-@_qhand_guard
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, out: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, act: str = "none", fuse_rms: bool = False, eps: float = 1e-5,
            out_dtype: Optional[torch.dtype] = None, ln_c: Optional[torch.Tensor] = None,
@@ -617,6 +548,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     if fp8 and w.tiled:
         w = FP8Weight(w.rows(), w.scale)  # (shapes the tiled kernels reject: dequantising path)
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
+    if not fp8:
+        vendor_fallback(f"linear {tuple(x.shape)} x {tuple(w.shape)}")
     y = _fp8_matmul(xin, w) if fp8 else torch.matmul(xin, w.t())
     if bias is not None or act != "none" or residual is not None:
         if y.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and y.shape[1] % 8 == 0:
@@ -633,7 +566,6 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return out
 
 
-@_qhand_guard
 def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False, eps: float = 1e-5,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
     M = x.shape[0]
@@ -665,6 +597,8 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
     if fp8 and w_gu.tiled:
         w_gu = FP8Weight(w_gu.rows(), w_gu.scale)
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
+    if not fp8:
+        vendor_fallback(f"linear_swiglu {tuple(x.shape)} x {tuple(w_gu.shape)}")
     gu = _fp8_matmul(xin, w_gu) if fp8 else torch.matmul(xin, w_gu.t())
     E.swiglu(gu, out)
     return out
@@ -673,7 +607,7 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
 # > 16-row QKV projections with the rotary + paged-KV write in the tiled GEMM's epilogue (gemm.hip
 # EPI_QKV; with split-K: in the slab reduction) -- no qkv scratch round trip, no rope_kv_write
 # launch.  VWA_GEMM_QKV=0: GEMM -> qkv scratch -> rope_kv_write
-GEMM_QKV_FUSED = os.environ.get("VWA_GEMM_QKV", "1") != "0"
+GEMM_QKV_FUSED = knob("VWA_GEMM_QKV")
 
 
 def _gemm_qkv(x, w, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, rope, positions, slots, q_out, k_cache,
@@ -681,18 +615,17 @@ def _gemm_qkv(x, w, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, rope, 
     E = ext()
     M, K = x.shape
     ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
-    tk = gemm_tickets(x.device)
     common = (n_q_heads, n_kv_heads, head_dim, rope is not None, positions, slots, rope, q_out, k_cache, v_cache)
     if isinstance(w, FP8Weight):
         x8, sx, rstd = _fp8_input(x, fuse_rms, eps)
-        E.gemm_qkv(x8, sx, w.w8, w.scale, bias, rstd, True, ws, tk, *common)
+        E.gemm_qkv(x8, sx, w.w8, w.scale, bias, rstd, True, ws, *common)
         return
     rstd = None
     if fuse_rms:
         rstd = scratch(x.device, "gemm_rstd", M)
         E.row_rstd(x, rstd, eps)
     tiled = isinstance(w, TiledWeight)
-    E.gemm_qkv(x, None, w.t if tiled else w, None, bias, rstd, tiled, ws, tk, *common)
+    E.gemm_qkv(x, None, w.t if tiled else w, None, bias, rstd, tiled, ws, *common)
 
 
 def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Tensor], *, fuse_rms: bool, eps: float,
@@ -756,6 +689,8 @@ def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Te
     if fp8 and w_qkv.tiled:
         w_qkv = FP8Weight(w_qkv.rows(), w_qkv.scale)
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
+    if not fp8:
+        vendor_fallback(f"qkv {tuple(x.shape)} x {tuple(w_qkv.shape)}")
     qkv = _fp8_matmul(xin, w_qkv) if fp8 else torch.matmul(xin, w_qkv.t())
     if bias is not None:
         qkv = qkv + bias
@@ -1112,16 +1047,10 @@ def conv1d_gelu(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], *, 
     return out
 
 
-def env_flag(name: str, default: bool = False) -> bool:
-    v = os.environ.get(name)
-    if v is None:
-        return default
-    return v.strip().lower() in ("1", "true", "yes", "on")
+def env_flag(name: str) -> bool:
+    """A boolean knob (utils/env.py Settings: declared type and default)."""
+    return bool(knob(name))
 
 
-def env_int(name: str, default: int) -> int:
-    v = os.environ.get(name)
-    try:
-        return int(v) if v not in (None, "") else default
-    except ValueError:
-        return default
+def env_int(name: str) -> int:
+    return int(knob(name))

@@ -70,7 +70,7 @@ def build_kernels(force: bool = False, jobs: int = 8) -> str:
     headers = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
     kern_src = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     common = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result",
-              "-I", os.path.join(CSRC)] + os.environ.get("VWA_HIPCC_EXTRA", "").split()  # (experiments)
+              "-I", os.path.join(CSRC)] + os.environ.get("VWA_HIPCC_EXTRA", "").split()  # (utils/env.py Settings documents it; build.py stays import-light)  # (experiments)
     jobs_list = []
     objs = []
     for src in kern_src:

@@ -18,6 +18,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from ..utils.env import knob
 
 
 class OneShotAllReduce:
@@ -70,6 +71,6 @@ class OneShotAllReduce:
 
 def maybe_custom_ar(tp, ctl_group) -> Optional[OneShotAllReduce]:
     """Attach a one-shot all-reduce to a GPU TP context (None on CPU / disabled / TP=1)."""
-    if tp.size <= 1 or not torch.cuda.is_available() or os.environ.get("VWA_CUSTOM_AR", "1") == "0":
+    if tp.size <= 1 or not torch.cuda.is_available() or not knob("VWA_CUSTOM_AR"):
         return None
     return OneShotAllReduce(tp.rank, tp.size, ctl_group)

@@ -24,6 +24,7 @@ from typing import Optional
 
 import torch
 import torch.distributed as dist
+from ..utils.env import knob
 
 
 @dataclass
@@ -34,6 +35,7 @@ class TPContext:
     dp_rank: int = 0
     dp_size: int = 1
     custom_ar: Optional[object] = None  # parallel.custom_ar.OneShotAllReduce (GPU TP groups)
+    ctl: Optional[object] = None  # CPU (gloo) group of this TP group: the serving control plane
 
     @staticmethod
     def single() -> "TPContext":
@@ -77,7 +79,7 @@ def init_distributed(tp_size: Optional[int] = None, backend: Optional[str] = Non
     rank = int(os.environ.get("RANK", "0"))
     if not dist.is_initialized():
         if backend is None:
-            backend = os.environ.get("VWA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+            backend = knob("VWA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if torch.cuda.is_available():
             local = int(os.environ.get("LOCAL_RANK", rank))
             # gloo rehearsal of a multi-rank run on fewer GPUs: ranks share devices round-robin
@@ -88,9 +90,14 @@ def init_distributed(tp_size: Optional[int] = None, backend: Optional[str] = Non
     groups = [dist.new_group(list(range(s, s + tp))) for s in range(0, world, tp)]
     gi = rank // tp
     ctx = TPContext(rank=rank % tp, size=tp, group=groups[gi], dp_rank=gi, dp_size=world // tp)
-    if tp > 1 and torch.cuda.is_available():
-        from .custom_ar import maybe_custom_ar
-
+    if tp > 1:
+        # one gloo group per TP group (every rank takes part in creating every group): the brain's
+        # lockstep control messages (brain/tp_engine.py) and the IPC handle exchange of the custom
+        # all-reduce stay off the GPU and within the group
         ctl = [dist.new_group(list(range(s, s + tp)), backend="gloo") for s in range(0, world, tp)]
-        ctx.custom_ar = maybe_custom_ar(ctx, ctl[gi])
+        ctx.ctl = ctl[gi]
+        if torch.cuda.is_available():
+            from .custom_ar import maybe_custom_ar
+
+            ctx.custom_ar = maybe_custom_ar(ctx, ctl[gi])
     return ctx

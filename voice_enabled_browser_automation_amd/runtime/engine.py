@@ -29,6 +29,7 @@ import torch
 
 from .. import ops
 from .kv_cache import BlockManager, PagedKVCache
+from ..utils.env import knob
 
 # Row buckets of the captured step graphs (VWA_ROW_BUCKETS overrides).  48 between the powers of
 # two: a 44-row step of 32 concurrent sessions (+ jump-forward rows) pays for 48 rows, not 64 --
@@ -36,7 +37,7 @@ from .kv_cache import BlockManager, PagedKVCache
 # streaming GEMMs' X staging makes 8..16-row steps cost ~72 us per row (8: 4.04, 12: 4.36, 16:
 # 4.61 ms bf16, profiles/r4_rows_buckets_8_16.jsonl).  (24 measured the same as 32: the one
 # 128-row GEMM tile and the attention floor dominate there.)
-BUCKETS = tuple(int(b) for b in os.environ.get("VWA_ROW_BUCKETS", "1,2,4,8,12,16,32,48,64").split(","))
+BUCKETS = tuple(int(b) for b in knob("VWA_ROW_BUCKETS").split(","))
 
 
 class TPGroupFailure(RuntimeError):
@@ -57,10 +58,10 @@ _SEQ_UIDS = itertools.count()
 # Decode attention reads the prompt prefix the step's sessions share (the same prefix-cached
 # blocks) once per group of rows across sessions (attention.hip / mq_attention.h cascade);
 # VWA_SHARED_ATTN=0: once per session
-SHARED_ATTN = os.environ.get("VWA_SHARED_ATTN", "1") != "0"
+SHARED_ATTN = knob("VWA_SHARED_ATTN")
 # Batched admission prefill: causal flash attention over [requests x longest suffix] instead of the
 # decode-attention kernel in 64-row slices (VWA_PREFILL_FLASH=0: slices)
-PREFILL_FLASH = os.environ.get("VWA_PREFILL_FLASH", "1") != "0"
+PREFILL_FLASH = knob("VWA_PREFILL_FLASH")
 
 
 @dataclass
@@ -166,7 +167,7 @@ class LLMEngine:
         self.max_model_len = max_model_len
         self.max_seqs = max_seqs
         cfg = model.cfg
-        if kv_blocks is None and kv_gb is None and os.environ.get("VWA_KV_GB", "").strip().lower() == "auto":
+        if kv_blocks is None and kv_gb is None and knob("VWA_KV_GB").strip().lower() == "auto":
             # size the paged KV from the per-GPU HBM plan (runtime/memory_plan.py): what the weights,
             # step buffers and workspaces leave of the 288 GB
             from .memory_plan import plan_memory
@@ -174,7 +175,7 @@ class LLMEngine:
             free, _total = torch.cuda.mem_get_info(self.device) if self.device.type == "cuda" else (0, 0)
             # VWA_SHARED_GB: HBM a co-located service keeps (launch.py sets it when the voice
             # worker's ASR shares this GPU)
-            shared = float(os.environ.get("VWA_SHARED_GB", "0") or 0)
+            shared = knob("VWA_SHARED_GB")
             plan = plan_memory(cfg, model.tp.size, wdtype=getattr(model, "wdtype", "bf16"), block_size=block_size,
                                max_rows=max_rows, max_ctx=max_model_len, shared_gb=shared)
             kv_blocks = plan.kv_blocks
@@ -188,7 +189,7 @@ class LLMEngine:
             self.memory_plan = plan
         if kv_blocks is None:
             if kv_gb is None:
-                kv_gb = float(os.environ.get("VWA_KV_GB", "0") or 0)
+                kv_gb = float(knob("VWA_KV_GB") or 0)
             if kv_gb > 0:
                 kv_blocks = PagedKVCache.blocks_for_budget(kv_gb * 1e9, cfg.n_layers, model.nkv, model.hd, block_size)
             else:
@@ -201,7 +202,7 @@ class LLMEngine:
         self.free_sids = list(range(max_seqs - 1, -1, -1))
         self.seqs: Dict[int, Sequence_] = {}
         if use_graphs is None:
-            use_graphs = ops.env_flag("VWA_HIPGRAPH", True)
+            use_graphs = ops.env_flag("VWA_HIPGRAPH")
         self.use_graphs = bool(use_graphs) and self.device.type == "cuda"
         self.graphs: Dict[Tuple[int, int], Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
         self.graph_pool = None
@@ -539,7 +540,7 @@ class LLMEngine:
         """A chain timeout usually means another kernel held CUs for a while (e.g. the ASR engine
         on another stream of the same GPU): the chained launch is re-armed after 256 steps, then
         after 512, 1024, ... (capped at 65536) if it keeps failing (``VWA_CHAIN_RETRY=0``: never)."""
-        if not ops.env_flag("VWA_CHAIN_RETRY", True) or not hasattr(self.model, "enable_chain"):
+        if not ops.env_flag("VWA_CHAIN_RETRY") or not hasattr(self.model, "enable_chain"):
             return
         self._chain_backoff = min(2 * getattr(self, "_chain_backoff", 128), 1 << 16)
         self._chain_retry_at = self.stats["steps"] + self._chain_backoff

@@ -11,6 +11,7 @@ import gzip
 import json
 import os
 from typing import List, Optional
+from ..utils.env import knob
 
 ASSET_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
 
@@ -79,7 +80,7 @@ def load_tokenizer(kind: str = "llama3") -> Tokenizer:
     from tokenizers import Tokenizer as HFTok
 
     env = {"llama3": "VWA_LLAMA_TOKENIZER", "whisper": "VWA_WHISPER_TOKENIZER", "gpt2": "VWA_GPT2_TOKENIZER"}.get(kind)
-    path = os.environ.get(env) if env else None
+    path = knob(env) if env else None
     if path:
         tok = HFTok.from_file(path)
     elif kind == "gpt2":

@@ -15,13 +15,14 @@ from __future__ import annotations
 import json
 import os
 from typing import Any, Dict, Optional
+from .env import knob
 
 DEFAULT_MAX_BYTES = 2048  # ~600 Llama-3 tokens: the ~1.1k-token prompt stays well inside 4096
 
 
 def max_context_bytes() -> int:
     try:
-        return max(0, int(os.environ.get("VWA_CONTEXT_MAX_BYTES", DEFAULT_MAX_BYTES)))
+        return max(0, knob("VWA_CONTEXT_MAX_BYTES"))
     except ValueError:
         return DEFAULT_MAX_BYTES
 

@@ -31,6 +31,7 @@ from aiohttp import WSMsgType, web
 
 from ..utils.metrics import Metrics
 from .server import VERSION
+from ..utils.env import knob
 
 
 @dataclass
@@ -74,8 +75,8 @@ def build_router(worker_urls: List[str], *, probe_s: Optional[float] = None,
     app = web.Application()
     app["workers"] = [Worker(u.rstrip("/")) for u in worker_urls]
     app["metrics"] = Metrics("voice-router")
-    probe_s = float(os.environ.get("VWA_WATCHDOG_S", "2.0")) if probe_s is None else probe_s
-    max_fails = int(os.environ.get("VWA_WATCHDOG_FAILS", "2")) if max_fails is None else max_fails
+    probe_s = float(knob("VWA_WATCHDOG_S")) if probe_s is None else probe_s
+    max_fails = int(knob("VWA_WATCHDOG_FAILS")) if max_fails is None else max_fails
 
     def pick(exclude: Optional[Worker] = None) -> Optional[Worker]:
         live = [w for w in app["workers"] if w.healthy and w is not exclude]
@@ -225,9 +226,9 @@ def main():
     from ..utils.env import load_dotenv
 
     load_dotenv()
-    port = int(os.environ.get("VOICE_PORT", "7072"))
-    base = int(os.environ.get("VWA_VOICE_BASE_PORT", "7100"))
-    n = int(os.environ.get("VWA_DP", "1"))
+    port = int(knob("VOICE_PORT"))
+    base = int(knob("VWA_VOICE_BASE_PORT"))
+    n = int(knob("VWA_DP"))
     urls = [f"http://127.0.0.1:{base + i}" for i in range(n)]
     print(f"[voice-router] ws://127.0.0.1:{port}/stream -> {json.dumps(urls)}", flush=True)
     web.run_app(build_router(urls), host="127.0.0.1", port=port, print=None)

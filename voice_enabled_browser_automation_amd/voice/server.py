@@ -34,6 +34,7 @@ from aiohttp import WSMsgType, web
 
 from ..utils.context import merge_context
 from ..utils.metrics import Metrics
+from ..utils.env import knob
 
 VERSION = "0.1.0"
 
@@ -58,14 +59,14 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
     # one worker per live session pass: a session's recognition pass blocks its worker inside the
     # recognizer (asr/streaming.py AsrBatcher), whose single scheduler thread batches the passes
     # of all sessions onto the GPU -- so the pool only needs to be as wide as the session count
-    app["asr_pool"] = ThreadPoolExecutor(max_workers=int(os.environ.get("VWA_MAX_SESSIONS", "32")) + 4,
+    app["asr_pool"] = ThreadPoolExecutor(max_workers=knob("VWA_MAX_SESSIONS") + 4,
                                          thread_name_prefix="asr")
     app["asr_factory"] = asr_factory
     app["exec_tasks"] = set()  # executor queues still draining after their connection closed
-    brain_url = brain_url or os.environ.get("BRAIN_URL", "http://127.0.0.1:8090/parse")
-    executor_url = executor_url or os.environ.get("EXECUTOR_URL", "http://127.0.0.1:7081")
+    brain_url = brain_url or knob("BRAIN_URL")
+    executor_url = executor_url or knob("EXECUTOR_URL")
     if debounce_ms is None:
-        debounce_ms = float(os.environ.get("VWA_DEBOUNCE_MS", "1000"))
+        debounce_ms = knob("VWA_DEBOUNCE_MS")
 
     async def on_startup(app_):
         app_["http"] = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=120))
@@ -284,7 +285,7 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
 
 
 def asr_factory_from_env() -> Optional[Callable[[], Any]]:
-    kind = os.environ.get("VWA_ASR_ENGINE", "none")
+    kind = knob("VWA_ASR_ENGINE")
     if kind == "none":
         return None
     import torch
@@ -295,19 +296,19 @@ def asr_factory_from_env() -> Optional[Callable[[], Any]]:
     from ..models.whisper import WhisperModel
     from ..tokenizer import load_tokenizer
 
-    name = os.environ.get("VWA_ASR_MODEL", "whisper-tiny")
+    name = knob("VWA_ASR_MODEL")
     dev = "cuda" if torch.cuda.is_available() else "cpu"
-    wpath = os.environ.get("VWA_ASR_WEIGHTS")
+    wpath = knob("VWA_ASR_WEIGHTS")
     if wpath:
         from ..runtime.weights import LazySafetensors
 
     model = WhisperModel(get_config(name), device=dev, weights=LazySafetensors(wpath) if wpath else None)
     eng = AsrEngine(model, load_tokenizer("whisper"),
-                    max_sessions=int(os.environ.get("VWA_MAX_SESSIONS", "8")))
+                    max_sessions=knob("VWA_MAX_SESSIONS"))
     # VWA_ASR_TOKENS_PER_S: fixed-work transcripts for benchmarks on random-init weights
-    tps = float(os.environ.get("VWA_ASR_TOKENS_PER_S", "0") or 0) or None
+    tps = knob("VWA_ASR_TOKENS_PER_S") or None
     batcher = AsrBatcher(eng, tokens_per_s=tps)
-    every = float(os.environ.get("VWA_PARTIAL_EVERY_S", "1.0"))
+    every = knob("VWA_PARTIAL_EVERY_S")
 
     def factory():
         return StreamingAsrSession(batcher, model_name=name, partial_every_s=every)
@@ -320,7 +321,7 @@ def main():
     from ..utils.env import load_dotenv
 
     load_dotenv()
-    port = int(os.environ.get("VOICE_PORT", "7072"))
+    port = knob("VOICE_PORT")
     print(f"[voice] http/ws listening on http://127.0.0.1:{port}", flush=True)
     # binds all interfaces, as the reference (apps/voice/src/server.ts:80)
     web.run_app(build_app(asr_factory_from_env()), host="0.0.0.0", port=port, print=None)

@@ -4,6 +4,7 @@ from __future__ import annotations
 import os
 
 from aiohttp import web
+from ..utils.env import knob
 
 STATIC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "static")
 
@@ -20,7 +21,7 @@ def build_app() -> web.Application:
 
 
 def main():
-    port = int(os.environ.get("WEB_PORT", "5173"))
+    port = int(knob("WEB_PORT"))
     print(f"[web] http://127.0.0.1:{port}", flush=True)
     web.run_app(build_app(), host="127.0.0.1", port=port, print=None)
 
