@@ -177,4 +177,20 @@ class GPT2Model:
         hs = ops.layernorm(hs, self.lnf_w, self.lnf_b, eps=self.cfg.ln_eps)
         n = hs.shape[0]
         out = bufs.logits_local[:n] if n <= bufs.logits_local.shape[0] else None
+        V = self.lm_head.shape[0]
+        if hs.is_cuda and V % 16:
+            # GPT-2's 50257-token vocabulary is not a multiple of the kernels' 16-column tiles: the
+            # tied head runs zero-padded to the next multiple (built once) into a scratch, and the
+            # real columns are copied out -- no vendor GEMM for the odd shape
+            pad = getattr(self, "_lm_pad", None)
+            if pad is None or pad.device != hs.device:
+                pad = torch.zeros(((V + 15) // 16 * 16, self.lm_head.shape[1]), dtype=self.lm_head.dtype, device=hs.device)
+                pad[:V] = self.lm_head
+                self._lm_pad = pad
+            full = ops.scratch(hs.device, "gpt2_logits", n * pad.shape[0]).view(n, pad.shape[0])
+            ops.linear(hs, pad, out=full, out_dtype=torch.float32, col_mask=col_mask, mask_rows=mask_rows)
+            if out is None:
+                return full[:, :V].contiguous()
+            out.copy_(full[:, :V])
+            return out
         return ops.linear(hs, self.lm_head, out=out, out_dtype=torch.float32, col_mask=col_mask, mask_rows=mask_rows)

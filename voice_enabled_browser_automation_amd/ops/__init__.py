@@ -122,7 +122,10 @@ class FP8Weight:
         self.w8, self.scale, self.tiled = w8, scale, tiled
 
     @staticmethod
-    def quantize(w: torch.Tensor, tiled: bool = False) -> "FP8Weight":
+    def quantize(w: torch.Tensor, tiled: Optional[bool] = None) -> "FP8Weight":
+        """tiled None: the tiled layout on a GPU (the only one its kernels read), row-major on the CPU."""
+        if tiled is None:
+            tiled = w.is_cuda and w.shape[0] % 16 == 0 and w.shape[1] % 128 == 0
         wf = w.float()
         scale = (wf.abs().amax(dim=1) / FP8_MAX).clamp_min(1e-12)
         w8 = (wf / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).contiguous()
@@ -152,7 +155,16 @@ class FP8Weight:
         return 1
 
     def to(self, device) -> "FP8Weight":
-        return FP8Weight(self.w8.to(device), self.scale.to(device), self.tiled)
+        """Moved to a GPU, a row-major weight takes the tiled layout its kernels read (one copy);
+        moved to the CPU, the reference's row-major layout."""
+        dev = torch.device(device)
+        w8 = self.w8
+        N, K = w8.shape
+        if dev.type == "cuda" and not self.tiled and N % 16 == 0 and K % 128 == 0:
+            return FP8Weight(tile_weight_fp8(w8).to(dev), self.scale.to(dev), True)
+        if dev.type == "cpu" and self.tiled:
+            return FP8Weight(untile_weight_fp8(w8.to(dev)), self.scale.to(dev), False)
+        return FP8Weight(w8.to(dev), self.scale.to(dev), self.tiled)
 
 
 def quant_rows_fp8(x: torch.Tensor) -> torch.Tensor:
