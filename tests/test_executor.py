@@ -149,3 +149,16 @@ def test_executor_http_service(tmp_path):
             assert r.headers.get("Access-Control-Allow-Origin") == "http://localhost:5173"
 
     asyncio.run(go())
+
+
+def test_synthesised_selectors_are_escaped():
+    """ids with ':' / '.' (framework markup) and quotes in attribute values
+    give broken selectors when synthesised raw (reference dom-analyzer.ts:78-86); the page script
+    escapes them (CSS.escape, or the same backslash rule without it) -- mirrored in Python."""
+    from voice_enabled_browser_automation_amd.executor.dom_analyzer import ANALYZE_JS, synth_selector
+
+    assert synth_selector("INPUT", {"id": "search:q.1"}) == "#search\\:q\\.1"
+    assert synth_selector("input", {"name": 'a"b'}) == 'input[name="a\\"b"]'
+    assert synth_selector("button", {"data-testid": "go"}) == '[data-testid="go"]'
+    assert synth_selector("A", {}) == "a"
+    assert "CSS.escape" in ANALYZE_JS and "d.selector === 'a'" not in ANALYZE_JS

@@ -13,13 +13,18 @@ from typing import Any, Dict, List, Optional
 
 ANALYZE_JS = r"""
 () => {
+  // ids / attribute values are escaped: an id like "a:b" or "x.y" (frequent in framework-generated
+  // markup) is otherwise a broken selector -- the reference synthesises them raw
+  // (dom-analyzer.ts:78-86)
+  const ident = (s) => (window.CSS && CSS.escape) ? CSS.escape(s) : s.replace(/([^A-Za-z0-9_-])/g, '\\$1');
+  const qv = (s) => s.replace(/\\/g, '\\\\').replace(/"/g, '\\"');
   const sel = (el) => {
-    if (el.id) return '#' + el.id;
+    if (el.id) return '#' + ident(el.id);
     const dt = el.getAttribute('data-testid');
-    if (dt) return `[data-testid="${dt}"]`;
+    if (dt) return `[data-testid="${qv(dt)}"]`;
     const nm = el.getAttribute('name');
     const tag = el.tagName.toLowerCase();
-    if (nm) return `${tag}[name="${nm}"]`;
+    if (nm) return `${tag}[name="${qv(nm)}"]`;
     return tag;
   };
   const attrs = (el) => { const a = {}; for (const x of Array.from(el.attributes)) a[x.name] = x.value; return a; };
@@ -43,9 +48,7 @@ ANALYZE_JS = r"""
   for (const b of Array.from(document.querySelectorAll('button, input[type="button"], input[type="submit"], [role="button"]')))
     if (b.offsetHeight > 0) out.buttons.push(desc(b, 'button'));
   for (const a of Array.from(document.querySelectorAll('a[href]')).slice(0, 500)) {
-    const d = desc(a, 'link');
-    if (d.selector === 'a') d.selector = 'a';
-    if (a.offsetHeight > 0) out.links.push(d);
+    if (a.offsetHeight > 0) out.links.push(desc(a, 'link'));
   }
   for (const f of Array.from(document.querySelectorAll('form'))) {
     const inputs = Array.from(f.querySelectorAll('input, textarea, select')).map((e) => desc(e, e.tagName.toLowerCase() === 'select' ? 'select' : (e.tagName.toLowerCase() === 'textarea' ? 'textarea' : 'input')));
@@ -73,6 +76,26 @@ ANALYZE_JS = r"""
   return out;
 }
 """
+
+
+def css_ident(s: str) -> str:
+    """The selector synthesis' identifier escaping (ANALYZE_JS ``ident`` without CSS.escape):
+    every character outside [A-Za-z0-9_-] backslash-escaped."""
+    return "".join(c if (c.isascii() and (c.isalnum() or c in "_-")) else "\\" + c for c in s)
+
+
+def synth_selector(tag: str, attrs: Dict[str, str]) -> str:
+    """Python mirror of ANALYZE_JS ``sel`` (tests; same order as dom-analyzer.ts:78-86)."""
+    def qv(v: str) -> str:
+        return v.replace("\\", "\\\\").replace('"', '\\"')
+
+    if attrs.get("id"):
+        return "#" + css_ident(attrs["id"])
+    if attrs.get("data-testid"):
+        return f'[data-testid="{qv(attrs["data-testid"])}"]'
+    if attrs.get("name"):
+        return f'{tag.lower()}[name="{qv(attrs["name"])}"]'
+    return tag.lower()
 
 
 class DOMAnalyzer:
