@@ -197,12 +197,39 @@ int device_cus(const Tensor& t) {
   return cus;
 }
 
+// RMS statistics hand-off of the tiled GEMM (GemmParams::ss_*): ss_out (residual epilogue) gets
+// the squares of the output rows added, ss_zero is zeroed (whole tensor), ss_in replaces rstd
+void set_ss(GemmParams& p, int64_t epi, const c10::optional<Tensor>& ss_out, const c10::optional<Tensor>& ss_zero,
+            const c10::optional<Tensor>& ss_in, double eps) {
+  auto chk = [&](const Tensor& t, const char* n) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() >= p.M, n,
+                ": f32 [>= M] contiguous GPU tensor");
+  };
+  if (ss_out.has_value()) {
+    chk(*ss_out, "ss_out");
+    TORCH_CHECK(epi == 1 && !p.y_f32, "ss_out: residual epilogue (bf16 rows) only");
+    p.ss_out = ss_out->data_ptr<float>();
+  }
+  if (ss_zero.has_value()) {
+    chk(*ss_zero, "ss_zero");
+    p.ss_zero = ss_zero->data_ptr<float>();
+    p.ss_zero_n = (int)ss_zero->numel();
+  }
+  if (ss_in.has_value()) {
+    chk(*ss_in, "ss_in");
+    TORCH_CHECK(p.rstd == nullptr, "ss_in replaces rstd");
+    p.ss_in = ss_in->data_ptr<float>();
+    p.ss_eps = (float)eps;
+  }
+}
+
 // LDS-tiled MFMA GEMM (gemm.hip), M > 16 rows.  epi: 0 store (+bias, bf16 / f32 out), 1 residual
 // add (+bias), 2 SwiGLU over interleaved gate/up tiles (y [M, N/2]), 3 GELU (+bias).  rstd: f32
 // [M] per-row RMSNorm scale applied to the product (gammas folded into w).  ws: f32 split-K
 // workspace (the launcher splits K only when the output tiles alone cannot fill the CUs).
 void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi, c10::optional<Tensor> rstd,
-          c10::optional<Tensor> residual, bool w_tiled, c10::optional<Tensor> ws) {
+          c10::optional<Tensor> residual, bool w_tiled, c10::optional<Tensor> ws, c10::optional<Tensor> ss_out,
+          c10::optional<Tensor> ss_zero, c10::optional<Tensor> ss_in, double ss_eps) {
   c10::DeviceGuard g(x.device());
   check_bf16(x, "x");
   check_bf16(w, "w");
@@ -259,21 +286,29 @@ void gemm(Tensor x, Tensor w, c10::optional<Tensor> bias, Tensor y, int64_t epi,
     p.ws_cap = ws->numel();
   }
   p.cus = device_cus(x);
+  set_ss(p, epi, ss_out, ss_zero, ss_in, ss_eps);
   check_rc(vwa_gemm((int)epi, &p, cur_stream(x)), "gemm");
 }
 
-// W8A8 tiled GEMM (gemm.hip, F8): x8 OCP e4m3 [M, K] with per-row scales sx (quant_fp8_rows),
-// w8 the fp8 tiled layout [N, K] with per-row scales sw.
-void gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> bias, Tensor y, int64_t epi,
-              c10::optional<Tensor> rstd, c10::optional<Tensor> residual, c10::optional<Tensor> ws) {
+// fp8 tiled GEMM (gemm.hip): w8 the fp8 tiled layout [N, K] with per-row scales sw, and either
+// x8 OCP e4m3 [M, K] with per-row scales sx (W8A8, quant_fp8_rows) or bf16 rows with sx = None
+// (W8A16: the weights convert to bf16 on the LDS read, no quantised copy of x).
+void gemm_fp8(Tensor x8, c10::optional<Tensor> sx, Tensor w8, Tensor sw, c10::optional<Tensor> bias, Tensor y,
+              int64_t epi, c10::optional<Tensor> rstd, c10::optional<Tensor> residual, c10::optional<Tensor> ws,
+              c10::optional<Tensor> ss_out, c10::optional<Tensor> ss_zero, c10::optional<Tensor> ss_in, double ss_eps) {
   c10::DeviceGuard g(x8.device());
-  TORCH_CHECK(x8.is_cuda() && x8.scalar_type() == at::kFloat8_e4m3fn && x8.dim() == 2 && x8.stride(1) == 1 &&
-                  x8.stride(0) % 16 == 0 && (reinterpret_cast<uintptr_t>(x8.data_ptr()) & 15) == 0,
-              "x8: fp8 e4m3 [M, K] rows 16-byte aligned");
+  if (sx.has_value()) {
+    TORCH_CHECK(x8.is_cuda() && x8.scalar_type() == at::kFloat8_e4m3fn && x8.dim() == 2 && x8.stride(1) == 1 &&
+                    x8.stride(0) % 16 == 0 && (reinterpret_cast<uintptr_t>(x8.data_ptr()) & 15) == 0,
+                "x8: fp8 e4m3 [M, K] rows 16-byte aligned");
+    TORCH_CHECK(sx->is_cuda() && sx->scalar_type() == at::kFloat && sx->numel() >= x8.size(0), "sx f32 [M]");
+  } else {
+    check_bf16(x8, "x");
+    check_contig_rows(x8, "x");
+  }
   TORCH_CHECK(w8.is_cuda() && w8.scalar_type() == at::kFloat8_e4m3fn && w8.is_contiguous() && w8.dim() == 2 &&
                   w8.size(1) == x8.size(1),
               "w8: fp8 e4m3 [N, K] (tiled)");
-  TORCH_CHECK(sx.is_cuda() && sx.scalar_type() == at::kFloat && sx.numel() >= x8.size(0), "sx f32 [M]");
   TORCH_CHECK(sw.is_cuda() && sw.scalar_type() == at::kFloat && sw.numel() == w8.size(0), "sw f32 [N]");
   TORCH_CHECK(epi >= 0 && epi <= 3, "gemm_fp8: bad epilogue");
   GemmParams p{};
@@ -294,7 +329,7 @@ void gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> 
   p.Y = y.data_ptr();
   p.ldy = (int)y.stride(0);
   p.y_f32 = y.scalar_type() == at::kFloat;
-  p.sx = sx.data_ptr<float>();
+  p.sx = sx.has_value() ? sx->data_ptr<float>() : nullptr;
   p.sw = sw.data_ptr<float>();
   if (bias.has_value()) {
     check_bf16(*bias, "bias");
@@ -320,23 +355,34 @@ void gemm_fp8(Tensor x8, Tensor sx, Tensor w8, Tensor sw, c10::optional<Tensor> 
     TORCH_CHECK(ws->is_cuda() && ws->scalar_type() == at::kFloat && ws->is_contiguous(), "ws f32");
     p.ws = ws->data_ptr<float>();
     p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x8), ws->numel(), 1);
+    p.ws_cap = ws->numel();
   }
+  p.cus = device_cus(x8);
+  TORCH_CHECK(!ss_in.has_value() || !sx.has_value(), "ss_in: W8A16 (bf16 x) only");
+  set_ss(p, epi, ss_out, ss_zero, ss_in, ss_eps);
   check_rc(vwa_gemm((int)epi, &p, cur_stream(x8)), "gemm_fp8");
 }
 
 void check_cache(const Tensor& c, const char* name);
 
 // QKV projection on the tiled GEMM with the rotary + paged-KV write in its epilogue (gemm.hip
-// EPI_QKV; > 16 rows): x bf16 (sx null) or fp8 codes x8 with per-row scales sx (W8A8, w fp8 tiled
-// with row scales sw).  Replaces gemm -> qkv scratch -> rope_kv_write.
+// EPI_QKV; > 16 rows): x bf16 (sx null) or fp8 codes x8 with per-row scales sx (W8A8); w bf16 or
+// fp8 tiled with row scales sw (bf16 x + sw: W8A16).  Replaces gemm -> qkv scratch -> rope_kv_write.
 void gemm_qkv(Tensor x, c10::optional<Tensor> sx, Tensor w, c10::optional<Tensor> sw, c10::optional<Tensor> bias,
               c10::optional<Tensor> rstd, bool w_tiled, Tensor ws, int64_t n_q_heads,
               int64_t n_kv_heads, int64_t head_dim, bool use_rope, Tensor positions, Tensor slots,
-              c10::optional<Tensor> rope, Tensor q_out, Tensor k_cache, Tensor v_cache) {
+              c10::optional<Tensor> rope, Tensor q_out, Tensor k_cache, Tensor v_cache, c10::optional<Tensor> ss_in,
+              double ss_eps) {
   c10::DeviceGuard g(x.device());
   const bool f8 = sx.has_value();
   GemmParams p{};
-  if (f8) {
+  if (!f8 && sw.has_value()) {  // W8A16
+    check_bf16(x, "x");
+    check_contig_rows(x, "x");
+    TORCH_CHECK(w.scalar_type() == at::kFloat8_e4m3fn && w_tiled, "W8A16: fp8 tiled w");
+    TORCH_CHECK(sw->scalar_type() == at::kFloat && sw->numel() == w.size(0), "sw f32 [N]");
+    p.sw = sw->data_ptr<float>();
+  } else if (f8) {
     TORCH_CHECK(x.scalar_type() == at::kFloat8_e4m3fn && x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 16 == 0 &&
                     (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0,
                 "x8: fp8 e4m3 [M, K] rows 16-byte aligned");
@@ -397,9 +443,11 @@ void gemm_qkv(Tensor x, c10::optional<Tensor> sx, Tensor w, c10::optional<Tensor
   p.cache_st = k_cache.stride(2);
   TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == at::kFloat && ws.is_contiguous(), "ws f32");
   p.ws = ws.data_ptr<float>();
-  p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws.numel(), f8 ? 1 : 0);
+  p.splits = vwa_gemm_splits(p.M, p.N, p.K, device_cus(x), ws.numel(), p.sw ? 1 : 0);
   p.ws_cap = ws.numel();
   p.cus = device_cus(x);
+  TORCH_CHECK(!ss_in.has_value() || !f8, "ss_in: bf16 x only");
+  set_ss(p, 5, c10::nullopt, c10::nullopt, ss_in, ss_eps);
   check_rc(vwa_gemm(5, &p, cur_stream(x)), "gemm_qkv");
 }
 
@@ -496,6 +544,9 @@ void chain_schedule(ChainParams& cp) {
   // in LDS -- chained layer 103.2-103.6 vs 105.6 us, bench GPU wait 3462-3471 vs 3558 us per step
   cp.xfirst = 1;
   cp.xwait = 1;
+  // o_proj in 32-column tiles: one epilogue per workgroup (1 row 102.3 / 102.1 vs 103.5 / 103.0 us,
+  // 4 rows 107.0 vs 107.5 us per layer, profiles/r5_chain_o_nt2.jsonl)
+  cp.o_nt2 = 1;
   // diagnostic override of the schedule (tools/chain_probe.py A/B runs): "name=value,..."
   if (const char* e = std::getenv("VWA_CHAIN_SCHED")) {
     std::string s(e);
@@ -519,6 +570,7 @@ void chain_schedule(ChainParams& cp) {
         else if (k == "xwait") cp.xwait = v;
         else if (k == "xw_late") cp.xw_late = v;
         else if (k == "poll_free") cp.poll_free = v;
+        else if (k == "o_nt2") cp.o_nt2 = v;
       }
       at = end + 1;
     }
@@ -647,10 +699,10 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   if (lds < 0) return {torch::empty({0}, torch::dtype(torch::kUInt8).device(h.device())), 0};
   Tensor host = torch::empty({(int64_t)sizeof(ChainParams)}, torch::dtype(torch::kUInt8));
   std::memcpy(host.data_ptr(), &cp, sizeof(ChainParams));
-  // (bit 24 of the returned LDS size: the down phase streams X with the weights -- chain_run
-  // launches that instantiation)
+  // (bit 24 of the returned LDS size: the down phase streams X with the weights, bit 25: fp8
+  // weights, bit 26: o_proj in 32-column tiles -- chain_run launches that instantiation)
   return {host.to(h.device()), (int64_t)lds | (cp.n >= 3 && cp.ph[2].xg ? (int64_t)1 << 24 : 0) |
-                                    (s_o.has_value() ? (int64_t)1 << 25 : 0)};
+                                    (s_o.has_value() ? (int64_t)1 << 25 : 0) | (cp.o_nt2 ? (int64_t)1 << 26 : 0)};
 }
 
 // Whisper decoder chains (skinny_stream.hip chain_kernel SEQ 1 / 2): phase i computes
@@ -748,7 +800,7 @@ void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like, int64_t 
   // one workgroup per CU: the barrier needs every workgroup resident
   check_rc(vwa_chain_launch(reinterpret_cast<const ChainParams*>(desc.data_ptr()), (int)seq, (int)n_phases, (int)attn_g,
                             (int)(lds & 0xFFFFFF), chain_grid(like.device().index()), cur_stream(like),
-                            (int)((lds >> 24) & 1), (int)((lds >> 25) & 1)),
+                            (int)((lds >> 24) & 1), (int)((lds >> 25) & 1), (int)((lds >> 26) & 1)),
            "chain");
 }
 
@@ -1245,12 +1297,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("decode_advance", &decode_advance);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
         py::arg("rstd") = py::none(), py::arg("residual") = py::none(), py::arg("w_tiled") = false,
-        py::arg("ws") = py::none());
+        py::arg("ws") = py::none(), py::arg("ss_out") = py::none(), py::arg("ss_zero") = py::none(),
+        py::arg("ss_in") = py::none(), py::arg("ss_eps") = 1e-5);
   m.def("row_rstd", &row_rstd);
-  m.def("gemm_qkv", &gemm_qkv);
+  m.def("gemm_qkv", &gemm_qkv, py::arg("x"), py::arg("sx"), py::arg("w"), py::arg("sw"), py::arg("bias"),
+        py::arg("rstd"), py::arg("w_tiled"), py::arg("ws"), py::arg("n_q_heads"), py::arg("n_kv_heads"),
+        py::arg("head_dim"), py::arg("use_rope"), py::arg("positions"), py::arg("slots"), py::arg("rope"),
+        py::arg("q_out"), py::arg("k_cache"), py::arg("v_cache"), py::arg("ss_in") = py::none(),
+        py::arg("ss_eps") = 1e-5);
   m.def("gemm_fp8", &gemm_fp8, py::arg("x8"), py::arg("sx"), py::arg("w8"), py::arg("sw"), py::arg("bias"),
         py::arg("y"), py::arg("epi"), py::arg("rstd") = py::none(), py::arg("residual") = py::none(),
-        py::arg("ws") = py::none());
+        py::arg("ws") = py::none(), py::arg("ss_out") = py::none(), py::arg("ss_zero") = py::none(),
+        py::arg("ss_in") = py::none(), py::arg("ss_eps") = 1e-5);
   m.def("rmsnorm", &rmsnorm);
   m.def("layernorm", &layernorm);
   m.def("rope_kv_write", &rope_kv_write);

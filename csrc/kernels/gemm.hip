@@ -59,13 +59,19 @@ struct Cfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NW = WM_ * WN_, THREADS = 64 * NW;
   static constexpr int FM = BM / WM / 16, FN = BN / WN / 16;  // MFMA fragments per wave
   static constexpr int A_BYTES = BM * 128, STAGE = BM * 128 + BN * 128;
+  // W8A16 stage: a full k-group -- two bf16 A half images + the fp8 B block of every tile
+  static constexpr int W8STAGE = 2 * BM * 128 + BN * 128;
   static constexpr int NCOL_MAX = BN / WN;
   static constexpr int EPI_LDS = NW * (FM * 16) * (NCOL_MAX * 2 + 16);
   static constexpr int LDS = 2 * STAGE > EPI_LDS ? 2 * STAGE : EPI_LDS;
-  static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0 && (BM / 8) / NW + (BN / 8) / NW == 8,
-                "8 LDS-DMA instructions per thread per stage (the counted vmcnt)");
+  static constexpr int W8LDS = 2 * W8STAGE > EPI_LDS ? 2 * W8STAGE : EPI_LDS;
+  static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0, "whole LDS-DMA instructions per wave");
 };
 using CfgS = Cfg<128, 128, 2, 2>;
+// W8A16 decode tile (<= 64 rows: one row block): 64 x 128, 4 waves of 64 x 32, 32 KB stages (16 KB
+// of fp8 weights each -- the W8A8 kernel's weight bytes per stage: a half-k-group bf16-style stage
+// carried 8 KB and measured 1.25x slower whole decode steps), 2 workgroups per CU
+using CfgW8 = Cfg<64, 128, 1, 4>;
 
 // A-image slot swizzle: chunk c of row r sits at slot c ^ F((r >> 1) & 7).  F makes every
 // ds_read_b128 lane group ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ... : two k-chunk columns g,
@@ -96,11 +102,18 @@ VWA_DEVICE void dma16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, unsigned vo
 // F8 (W8A8): one FULL k-group per stage (16 fp8 = 16 B per chunk): A chunk c = 2 g + s2 holds
 // X8[row][128 kg + 32 g + 16 s2 .. + 16), B the fp8 tiled block [s2][lane][16 B] of the tile
 // (ops.tile_weight_fp8) -- the same stage images as a bf16 half k-group.
-template <class C, bool WT, bool F8>
+// W8 (W8A16, CfgW8): one FULL k-group per stage -- X as the two bf16 half-k-group A images (each as
+// above) and B the fp8 tiled k-group of every tile verbatim ([tile][s2][lane][16 B]: block s2 = h
+// holds the lane's k 32 g + 16 h .. + 16, both sub-steps of half h), converted to bf16 fragments on
+// the LDS read -- no quantised copy of X, half the weight bytes of bf16.
+template <class C, bool WT, bool F8, bool W8 = false>
 VWA_DEVICE void issue_stage(const GemmParams& p, __amdgpu_buffer_rsrc_t rx, __amdgpu_buffer_rsrc_t rw, int bm,
                             int bn, int hs, char* buf) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int kg = F8 ? hs : hs >> 1, h = F8 ? 0 : hs & 1;
+  const int kg = F8 || W8 ? hs : hs >> 1;
+#pragma unroll
+  for (int hh = 0; hh < (W8 ? 2 : 1); ++hh) {  // (W8: both bf16 half images of the k-group)
+  const int ha = W8 ? hh : F8 ? 0 : hs & 1;
 #pragma unroll
   for (int it = 0; it < C::BM / 8 / C::NW; ++it) {
     const int q = it * C::NW + w;  // wave-instruction index: rows 8q .. 8q + 7
@@ -110,10 +123,21 @@ VWA_DEVICE void issue_stage(const GemmParams& p, __amdgpu_buffer_rsrc_t rx, __am
     if constexpr (F8)
       off = (unsigned)((size_t)m * p.ldx + (size_t)kg * BKG + 32 * (c >> 1) + 16 * (c & 1));
     else
-      off = (unsigned)(((size_t)m * p.ldx + (size_t)kg * BKG + 32 * (c >> 1) + 16 * h + 8 * (c & 1)) * 2);
-    dma16(rx, buf + q * 1024, m < p.M ? off : 0xFFFFFFF0u);
+      off = (unsigned)(((size_t)m * p.ldx + (size_t)kg * BKG + 32 * (c >> 1) + 16 * ha + 8 * (c & 1)) * 2);
+    dma16(rx, buf + hh * C::A_BYTES + q * 1024, m < p.M ? off : 0xFFFFFFF0u);
+  }
   }
   const int kgn = p.K / BKG;
+  const int h = F8 || W8 ? 0 : hs & 1;
+  if constexpr (W8) {  // the fp8 blocks of the whole k-group, [tile][s2][lane][16 B]
+#pragma unroll
+    for (int it = 0; it < C::BN / 8 / C::NW; ++it) {
+      const int q = it * C::NW + w, T = (bn >> 4) + (q >> 1);
+      const unsigned off = T * 16 < p.N ? (unsigned)(((size_t)T * kgn + kg) * 2048 + (q & 1) * 1024 + lane * 16) : 0xFFFFFFF0u;
+      dma16(rw, buf + 2 * C::A_BYTES + q * 1024, off);
+    }
+    return;
+  }
 #pragma unroll
   for (int it = 0; it < C::BN / 8 / C::NW; ++it) {
     const int q = it * C::NW + w;  // tile q >> 1, sub-step s' = q & 1
@@ -133,13 +157,44 @@ VWA_DEVICE void issue_stage(const GemmParams& p, __amdgpu_buffer_rsrc_t rx, __am
   }
 }
 
-template <class C, bool F8>
+template <class C, bool F8, bool W8 = false>
 VWA_DEVICE void compute_stage(const char* buf, f32x4 (&acc)[C::FM][C::FN], int wm, int wn) {
   const int l = lane_id();
   const int rl = l & 15, g = l >> 4;
   const char* la = buf + (wm * C::FM * 16 + rl) * 128;
   const char* lb = buf + C::A_BYTES + (wn * C::FN) * 2048 + l * 16;
-  if constexpr (F8) {
+  if constexpr (W8) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+    // 16 e4m3 per lane and tile (both sub-steps of half h), read once; the per-row weight scale is
+    // applied to the finished column in the epilogue
+    uint4 w8[C::FN];
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+      w8[j] = *reinterpret_cast<const uint4*>(buf + 2 * C::A_BYTES + (wn * C::FN + j) * 2048 + h * 1024 + l * 16);
+#pragma unroll
+    for (int sp = 0; sp < 2; ++sp) {
+      bf16x8 a[C::FM], b[C::FN];
+      const int ch = ((2 * g + sp) ^ swz(rl >> 1)) << 4;
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) a[i] = *reinterpret_cast<const bf16x8*>(la + h * C::A_BYTES + i * 16 * 128 + ch);
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        const unsigned d0 = sp ? w8[j].z : w8[j].x, d1 = sp ? w8[j].w : w8[j].y;
+        uint4 bw;
+        bw.x = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d0, 1.0f, false));
+        bw.y = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d0, 1.0f, true));
+        bw.z = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d1, 1.0f, false));
+        bw.w = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d1, 1.0f, true));
+        b[j] = as_bf16x8(bw);
+      }
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16(a[i], b[j], acc[i][j]);
+    }
+    }
+  } else if constexpr (F8) {
     // one 128-deep MX MFMA per fragment pair: lane (row / column, g) supplies the 32 fp8 of
     // k 32 g .. 32 g + 32 -- A chunks 2 g and 2 g + 1 of the swizzled image, B blocks s2 = 0, 1 of
     // the fp8 tiled layout -- each read with one ds_read_b128 (conflict-free, as the bf16 path).
@@ -240,6 +295,13 @@ VWA_DEVICE void p8_mfma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2], const bf16x
 }
 
 VWA_DEVICE float bias_at(const GemmParams& p, int n) { return p.bias ? bf2f(p.bias[n]) : 0.f; }
+
+// per-row RMSNorm scale: rstd[m], or from the handed-off sum of squares (ss_in), or 1
+VWA_DEVICE float row_scale(const GemmParams& p, int m) {
+  if (p.rstd) return p.rstd[m];
+  if (p.ss_in) return rsqrtf(p.ss_in[m] / (float)p.K + p.ss_eps);
+  return 1.f;
+}
 
 template <int EPI>
 VWA_DEVICE void store_out(const GemmParams& p, int m, int n, float v) {
@@ -346,9 +408,10 @@ VWA_DEVICE void sum_items(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int m
 }
 
 // epilogue of one summed item + its stores
+// returns the sum of squares of the stored bf16 values (residual epilogue with ss_out; else 0)
 template <int EPI>
-VWA_DEVICE void finish_item(const GemmParams& p, int m, int c, const float (&a)[8], float (&b)[8]) {
-  const float rs = (p.rstd ? p.rstd[m] : 1.f) * (p.sx ? p.sx[m] : 1.f);
+VWA_DEVICE float finish_item(const GemmParams& p, int m, int c, const float (&a)[8], float (&b)[8]) {
+  const float rs = row_scale(p, m) * (p.sx ? p.sx[m] : 1.f);
   const int n0 = item_src0<EPI>(c), n1 = item_src1<EPI>(c);
   float v[8];
   if constexpr (EPI == EPI_SWIGLU) {
@@ -367,13 +430,13 @@ VWA_DEVICE void finish_item(const GemmParams& p, int m, int c, const float (&a)[
 #pragma unroll
       for (int e = 0; e < 8; ++e) b[e] = b[e] * rs * (p.sw ? p.sw[n1 + e] : 1.f) + bias_at(p, n1 + e);
       qkv_store(p, m, c, v, b);
-      return;
+      return 0.f;
     }
   }
   if (p.y_f32) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) store_out<EPI>(p, m, c + e, v[e]);
-    return;
+    return 0.f;
   }
   if constexpr (kResid<EPI>) {
     float r[8];
@@ -381,22 +444,42 @@ VWA_DEVICE void finish_item(const GemmParams& p, int m, int c, const float (&a)[
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += r[e];
   }
-  *reinterpret_cast<uint4*>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + c) = pack8(v);
+  const uint4 o = pack8(v);
+  *reinterpret_cast<uint4*>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + c) = o;
+  float sq = 0.f;
+  if (kResid<EPI> && p.ss_out) {
+    unpack8(o, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sq += v[e] * v[e];
+  }
+  return sq;
+}
+
+// ss_out[m] += sq summed over the wave's lanes of each row (lanes with m < 0 add nothing): one
+// atomic per row per wave when the wave lies in one row, else one per lane
+VWA_DEVICE void ss_add(float* ss_out, int m, float sq) {
+  const int m0 = __builtin_amdgcn_readfirstlane(m);
+  if (__ballot(m != m0) == 0ull) {
+    sq = wave_sum(sq);
+    if (lane_id() == 0 && m0 >= 0) __hip_atomic_fetch_add(gp(ss_out + m0), sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (m >= 0) {
+    __hip_atomic_fetch_add(gp(ss_out + m), sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 template <int EPI, int AUX>
-VWA_DEVICE void reduce_item(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int m, int c) {
+VWA_DEVICE float reduce_item(const GemmParams& p, __amdgpu_buffer_rsrc_t rws, int m, int c) {
   const int cc[1] = {c};
   const bool ok[1] = {true};
   float a[1][8], b[1][8];
   sum_items<EPI, AUX, 1, 4>(p, rws, m, cc, ok, a, b);
-  finish_item<EPI>(p, m, c, a[0], b[0]);
+  return finish_item<EPI>(p, m, c, a[0], b[0]);
 }
 
 // (round 4's 4-stage variant for one-row-block GEMMs measured slower in whole decode steps -- 128 KB
 // of LDS leaves one workgroup per CU, so split-K grids above 256 workgroups ran in two rounds:
 // fp8 32 rows 4.97 vs 4.36 ms, profiles/r4_gemm_ab.md -- and was removed in round 5)
-template <class C, int EPI, bool WT, bool F8 = false, bool P8 = false>
+template <class C, int EPI, bool WT, bool F8 = false, bool P8 = false, bool W8 = false>
 __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   constexpr int FM = C::FM, FN = C::FN;
@@ -411,6 +494,8 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
   }
   // XCD-aware: logical tile order is column-block major, so consecutive logical tiles (same XCD)
   // share the column block's weight tile in L2
+  if (p.ss_zero && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < p.ss_zero_n; i += C::THREADS) p.ss_zero[i] = 0.f;
   const int lt = xcd_remap((int)(blockIdx.x % tiles), tiles);
   const int bn = (lt / mb) * C::BN, bm = (lt % mb) * C::BM;
   const int KG = p.K / BKG;
@@ -423,11 +508,14 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // pipeline: two LDS buffers, the next stage's DMA in flight during this one's MFMAs; raw
   // barriers with counted vmcnt (a __syncthreads would drain the in-flight DMA)
-  constexpr int SPG = F8 ? 1 : 2;  // stages per k-group
+  constexpr int SPG = F8 || W8 ? 1 : 2;  // stages per k-group
+  constexpr int STG = W8 ? C::W8STAGE : C::STAGE;
+  static_assert(W8 ? 2 * (C::BM / 8 / C::NW) + C::BN / 8 / C::NW == 8 : C::BM / 8 / C::NW + C::BN / 8 / C::NW == 8,
+                "8 LDS-DMA instructions per thread per stage (the counted vmcnt)");
   const int h0 = SPG * kg0, nh = SPG * (kg1 - kg0);
   // X extent: the last row starts at (M-1)*ldx and is K long (rows may overlap: conv views)
   const __amdgpu_buffer_rsrc_t rx = rsrc(p.X, ((size_t)(p.M - 1) * p.ldx + p.K) * (F8 ? 1 : 2));
-  const __amdgpu_buffer_rsrc_t rw = rsrc(p.W, (size_t)p.N * p.K * (F8 ? 1 : 2));
+  const __amdgpu_buffer_rsrc_t rw = rsrc(p.W, (size_t)p.N * p.K * (F8 || W8 ? 1 : 2));
   if constexpr (P8) {
     static_assert(C::BM == 256 && C::BN == 256 && C::NW == 8 && WT && !F8, "8-phase pipeline: CfgP8, tiled bf16");
     const int l = lane_id(), rl = l & 15, g = l >> 4;
@@ -504,16 +592,16 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
     }
     if (wm == 0) asm volatile("s_barrier" ::: "memory");  // (group 1 started one barrier later)
   } else {
-  if (nh > 0) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0, lds);
-  if (nh > 1) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + 1, lds + C::STAGE);
+  if (nh > 0) issue_stage<C, WT, F8, W8>(p, rx, rw, bm, bn, h0, lds);
+  if (nh > 1) issue_stage<C, WT, F8, W8>(p, rx, rw, bm, bn, h0 + 1, lds + STG);
   for (int i = 0; i < nh; ++i) {
     if (i + 1 < nh)
       asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");  // this stage landed everywhere
     else
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-    compute_stage<C, F8>(lds + (i & 1) * C::STAGE, acc, wm, wn);
+    compute_stage<C, F8, W8>(lds + (i & 1) * STG, acc, wm, wn);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave done reading it
-    if (i + 2 < nh) issue_stage<C, WT, F8>(p, rx, rw, bm, bn, h0 + i + 2, lds + (i & 1) * C::STAGE);
+    if (i + 2 < nh) issue_stage<C, WT, F8, W8>(p, rx, rw, bm, bn, h0 + i + 2, lds + (i & 1) * STG);
   }
   }
   const int l = lane_id();
@@ -550,18 +638,20 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) rsv[i][r] = 1.f;
-  if (p.rstd) {
+  if (p.rstd || p.ss_in) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) rsv[i][r] = row0 + i * 16 + r < p.M ? p.rstd[row0 + i * 16 + r] : 1.f;
+      for (int r = 0; r < 4; ++r) rsv[i][r] = row0 + i * 16 + r < p.M ? row_scale(p, row0 + i * 16 + r) : 1.f;
   }
-  // W8A8: acc * sx[m] * sw[n] (SwiGLU: gate / up columns scale before the activation)
-  if constexpr (F8) {
+  // W8A8: acc * sx[m] * sw[n] (SwiGLU: gate / up columns scale before the activation); W8A16: sw only
+  if constexpr (F8 || W8) {
+    if constexpr (F8) {
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) rsv[i][r] *= row0 + i * 16 + r < p.M ? p.sx[row0 + i * 16 + r] : 1.f;
+        for (int r = 0; r < 4; ++r) rsv[i][r] *= row0 + i * 16 + r < p.M ? p.sx[row0 + i * 16 + r] : 1.f;
+    }
 #pragma unroll
     for (int j = 0; j < FN; ++j) cz[j] = col0 + j * 16 < p.N ? p.sw[col0 + j * 16] : 0.f;
   }
@@ -614,8 +704,10 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
   constexpr int CPR = NCOL / 8;  // 16-byte chunks per row
   const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
   const int cbase = EPI == EPI_SWIGLU ? (bn + wn * FN * 16) / 2 : bn + wn * FN * 16;
+  float sqv[ROWS * CPR / 64];  // (ss_out: squares of each stored chunk)
 #pragma unroll
   for (int it = 0; it < ROWS * CPR / 64; ++it) {
+    sqv[it] = 0.f;
     const int idx = it * 64 + l, row = idx / CPR, ch = idx % CPR;
     const int m = bm + wm * ROWS + row, n = cbase + ch * 8;
     if (m >= p.M || n >= ncols) continue;
@@ -634,8 +726,25 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[e] += b[e];
       v = pack8(a);
+      if (p.ss_out) {
+        unpack8(v, a);  // (the stored bf16 values)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sqv[it] += a[e] * a[e];
+      }
     }
     *reinterpret_cast<uint4*>(reinterpret_cast<u16*>(p.Y) + (size_t)m * p.ldy + n) = v;
+  }
+  if (kResid<EPI> && p.ss_out) {  // one atomic per (row, wave): the CPR lanes of a row reduce first
+#pragma unroll
+    for (int it = 0; it < ROWS * CPR / 64; ++it) {
+      const int idx = it * 64 + l, row = idx / CPR, ch = idx % CPR;
+      const int m = bm + wm * ROWS + row;
+      float sq = sqv[it];
+#pragma unroll
+      for (int o = 1; o < CPR; o <<= 1) sq += __shfl_xor(sq, o, 64);  // the CPR lanes of one row
+      if (ch == 0 && m < p.M && cbase < ncols)
+        __hip_atomic_fetch_add(gp(p.ss_out + m), sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -644,9 +753,11 @@ template <int EPI>
 __global__ __launch_bounds__(256) void gemm_reduce_kernel(GemmParams p) {
   const int cpr = (EPI == EPI_SWIGLU ? p.N / 2 : p.N) / 8;
   const int64_t id = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (id >= (int64_t)p.M * cpr) return;
+  const bool ok = id < (int64_t)p.M * cpr;
   const __amdgpu_buffer_rsrc_t rws = rsrc(p.ws, (size_t)p.splits * p.M * p.N * 4);
-  reduce_item<EPI, 0>(p, rws, (int)(id / cpr), (int)(id % cpr) * 8);
+  float sq = 0.f;
+  if (ok) sq = reduce_item<EPI, 0>(p, rws, (int)(id / cpr), (int)(id % cpr) * 8);
+  if (kResid<EPI> && p.ss_out) ss_add(p.ss_out, ok ? (int)(id / cpr) : -1, sq);
 }
 
 // per-row 1/rms of X (the RMSNorm of a projection whose gamma is folded into W)
@@ -671,8 +782,10 @@ int launch_cfg(const GemmParams& p, hipStream_t st) {
   const int tiles = ((p.M + C::BM - 1) / C::BM) * ((p.N + C::BN - 1) / C::BN);
   const dim3 grid(tiles * p.splits * (p.nbatch > 1 ? p.nbatch : 1));
   const int lds = 2 * C::STAGE > C::LDS ? 2 * C::STAGE : C::LDS;  // two stage buffers
-  if (p.sw)
+  if (p.sw && p.sx)
     hipLaunchKernelGGL((gemm_kernel<C, EPI, true, true>), grid, dim3(C::THREADS), lds, st, p);
+  else if (p.sw)  // W8A16: bf16 X, fp8 tiled weights, on its own tile (launch_epi)
+    return -17;
   else if (p.w_tiled)
     hipLaunchKernelGGL((gemm_kernel<C, EPI, true, false>), grid, dim3(C::THREADS), lds, st, p);
   else
@@ -693,6 +806,11 @@ int launch_epi(const GemmParams& p, hipStream_t st, bool p8) {
     const int tiles = ((p.M + 255) / 256) * (p.N / 256);
     hipLaunchKernelGGL((gemm_kernel<CfgP8, EPI, true, false, true>), dim3(tiles * p.splits), dim3(CfgP8::THREADS),
                        CfgP8::LDS, st, p);
+  } else if (p.sw && !p.sx) {  // W8A16
+    using C = CfgW8;
+    const int tiles = ((p.M + C::BM - 1) / C::BM) * ((p.N + C::BN - 1) / C::BN);
+    hipLaunchKernelGGL((gemm_kernel<C, EPI, true, false, false, true>), dim3(tiles * p.splits), dim3(C::THREADS),
+                       C::W8LDS, st, p);
   } else {
     launch_cfg<CfgS, EPI>(p, st);
   }
@@ -729,9 +847,9 @@ extern "C" void vwa_gemm_set_p8(int mode) { g_p8_mode = mode; }
 extern "C" int vwa_gemm(int epi, const GemmParams* pp, hipStream_t st) {
   GemmParams p = *pp;
   if (p.M < 1 || p.N < 16 || p.N % 16 || p.K < BKG || p.K % BKG) return -10;
-  if (p.ldx % (p.sw ? 16 : 8) || (reinterpret_cast<uintptr_t>(p.X) & 15) || (reinterpret_cast<uintptr_t>(p.W) & 15))
+  if (p.ldx % (p.sx ? 16 : 8) || (reinterpret_cast<uintptr_t>(p.X) & 15) || (reinterpret_cast<uintptr_t>(p.W) & 15))
     return -11;
-  if (p.sw && (!p.sx || !p.w_tiled)) return -14;  // W8A8: per-row X scales and the fp8 tiled layout
+  if ((p.sw && !p.w_tiled) || (p.sx && !p.sw)) return -14;  // fp8: the tiled layout; X codes need fp8 weights
   if (epi == EPI_SWIGLU && (p.N % 32 || p.y_f32)) return -12;
   if (epi == EPI_QKV && (p.y_f32 || p.head_dim % 16 || p.N != (p.n_q_heads + 2 * p.n_kv_heads) * p.head_dim ||
                          !p.q_out || !p.k_cache || !p.v_cache || !p.slots || (p.use_rope && (!p.rope || !p.positions))))

@@ -964,9 +964,10 @@ struct ChainShape {
   static constexpr int R = KS == 16 ? 8 : 16;
 };
 
-template <int EPI, int KS = 8, bool XG = false, bool F8 = false>
+// W2: a plain phase in 32-column tiles (the chained o_proj, ChainParams::o_nt2)
+template <int EPI, int KS = 8, bool XG = false, bool F8 = false, bool W2 = false>
 struct PhaseShape {
-  static constexpr int NT = EPI == EPI_SWIGLU ? 2 : 1;
+  static constexpr int NT = (EPI == EPI_SWIGLU || W2) ? 2 : 1;
   // (measured: QKV in half-tile units -- 384 tiles -> 3 units per workgroup, one split tile each --
   // 12.5-13.4 us vs 6.7 median / 11.5 max with whole tiles, also with the split tile processed
   // first and published before the next item's loads under a counted vmcnt)
@@ -975,10 +976,10 @@ struct PhaseShape {
 
 // the phase's first weight item (and with pre2 its second) before the barrier wait: a
 // workgroup that arrives early keeps HBM busy while the grid catches up
-template <int EPI, int KS, int WA, bool XG = false, bool F8 = false, int R>
+template <int EPI, int KS, int WA, bool XG = false, bool F8 = false, bool W2 = false, int R>
 VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[R], uint4 (&wr2)[R], int pre2, int wb0 = 0,
                                   int wn = 0) {
-  using S = PhaseShape<EPI, KS, XG, F8>;
+  using S = PhaseShape<EPI, KS, XG, F8, W2>;
   const PhaseRange r = chain_range<KS>(ph, wb0, wn);
   // (issued before the barrier wait: XG items without their X fragments, chain_phase adds them)
   chain_load<S::NT, S::U, WA, R, XG, F8>(ph.p, ph.nb, wr, 0, r, !XG);
@@ -986,9 +987,9 @@ VWA_DEVICE void chain_issue_first(const ChainPhase& ph, uint4 (&wr)[R], uint4 (&
 }
 
 // one weight item `it` of a phase into wr (the next phase's item 0 / item 1, see chain_kernel)
-template <int EPI, int KS, int WA, bool XG = false, bool F8 = false, int R>
+template <int EPI, int KS, int WA, bool XG = false, bool F8 = false, bool W2 = false, int R>
 VWA_DEVICE void chain_issue_item(const ChainPhase& ph, uint4 (&wr)[R], int it, int wb0 = 0, int wn = 0) {
-  using S = PhaseShape<EPI, KS, XG, F8>;
+  using S = PhaseShape<EPI, KS, XG, F8, W2>;
   const PhaseRange r = chain_range<KS>(ph, wb0, wn);
   chain_load<S::NT, S::U, WA, R, XG, F8>(ph.p, ph.nb, wr, it, r);
 }
@@ -1020,10 +1021,10 @@ VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
 // queued behind weight loads; the other waves issue their item 1 at once (pre2 == 0: one item at
 // the barrier), which streams while the X rows arrive.  hs = items the staging wave has already
 // issued into (X0, X1).
-template <int EPI, int KS, int WA, bool XG = false, bool F8 = false, int R>
+template <int EPI, int KS, int WA, bool XG = false, bool F8 = false, bool W2 = false, int R>
 VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 (&X1)[R], char* smem, int pre2,
                             int hs = 0, int wb0 = 0, int wn = 0, bool has0 = true) {
-  constexpr int NT = PhaseShape<EPI, KS, XG, F8>::NT, U = PhaseShape<EPI, KS, XG, F8>::U;
+  constexpr int NT = PhaseShape<EPI, KS, XG, F8, W2>::NT, U = PhaseShape<EPI, KS, XG, F8, W2>::U;
   const ChainPhase& ph = cp.ph[i];
   const SkinnyParams& p = ph.p;
   const int nb = ph.nb, M = p.M, K = p.K;
@@ -1289,7 +1290,8 @@ struct SeqEpi {
 
 // XG2: phase 2 (the down projection) streams its X fragments with the weights (ChainParams
 // ph[2].xg: more rows than its X fits LDS, 5..16 rows, no attention phase)
-template <int KS, int SEQ, int NPH, int AG, int WA, bool XG2 = false, bool F8 = false>
+// O2: phase 0 (o_proj) in 32-column tiles (ChainParams::o_nt2)
+template <int KS, int SEQ, int NPH, int AG, int WA, bool XG2 = false, bool F8 = false, bool O2 = false>
 __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __restrict__ cpp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ChainParams& cp = *cpp;  // device-resident descriptor
@@ -1350,10 +1352,10 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   // swapping the sets per path measured 120 B of VGPR spills)
   auto issue0 = [&](int pre) {
     if (nx) {
-      chain_issue_item<E0, KS, WA, false, F8>(cp.ph[0], B, 0, ob0, on);
+      chain_issue_item<E0, KS, WA, false, F8, O2>(cp.ph[0], B, 0, ob0, on);
       chain_issue_item<E1, KS, WA, false, F8>(cp.ph[1], A, 0);
     } else {
-      chain_issue_first<E0, KS, WA, false, F8>(cp.ph[0], B, A, pre, ob0, on);
+      chain_issue_first<E0, KS, WA, false, F8, O2>(cp.ph[0], B, A, pre, ob0, on);
     }
   };
   auto preload1 = [&]() {
@@ -1448,7 +1450,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     // wave's item 1 unloaded whenever an attention workgroup also had >= 2 o_proj items -- more
     // attention items than half the grid: several sessions' rows, or a grid cut by
     // VWA_CHAIN_GRID_DIV -- and its MFMAs read stale registers: NaN / wrong o_proj tiles.)
-    chain_phase<E0, KS, WA, false, F8>(cp, 0, B, A, smem, nx ? 1 : pre0, nx ? 2 : 1 + (pre0 ? 1 : 0), ob0, on);
+    chain_phase<E0, KS, WA, false, F8, O2>(cp, 0, B, A, smem, nx ? 1 : pre0, nx ? 2 : 1 + (pre0 ? 1 : 0), ob0, on);
   stamp();
   if (SEQ == 0 && tpr) chain_tp_reduce(cp, 0, e0 + 1, bar, nwg, bar_next);
   gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
@@ -1520,6 +1522,12 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     const SkinnyParams& p = ph.p;
     if (ph.epi != kSeq[cp->seq][i]) return -10;
     ph.nt = (ph.epi == EPI_SWIGLU) ? 2 : 1;
+    // o_nt2: the chained o_proj in 32-column tiles -- one epilogue (cross-wave reduction, residual,
+    // store) per workgroup instead of two at one row (Llama tail with the attention phase, bf16)
+    if (i == 0 && cp->o_nt2) {
+      if (cp->seq == 0 && cp->attn_g > 0 && p.w_scale == nullptr && p.N % 32 == 0) ph.nt = 2;
+      else cp->o_nt2 = 0;
+    }
     // 5..16 rows: only without the attention phase (its row tables hold <= 4 rows), Llama tail; a
     // phase whose X rows do not fit LDS next to the scratch streams X with the weights (xg: the
     // down projection, residual epilogue, pre-tiled weights)
@@ -1602,8 +1610,21 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
 }
 
 extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid,
-                                hipStream_t st, int xg2, int f8) {
+                                hipStream_t st, int xg2, int f8, int o2) {
   if (attn_g) lds = lds > (int)MqLds<128, 8>::bytes ? lds : (int)MqLds<128, 8>::bytes;
+  if (o2) {  // o_proj in 32-column tiles (ChainParams::o_nt2): Llama tail with the attention phase, bf16
+    if (seq != 0 || f8 || xg2 || (n_phases != 3 && n_phases != 4)) return -10;
+    const bool q = n_phases == 4;
+#define VWA_CHAIN_LAUNCH_O2(N, G) \
+  hipLaunchKernelGGL((chain_kernel<8, 0, N, G, 0, false, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp)
+    switch (attn_g) {
+      case 4: if (q) VWA_CHAIN_LAUNCH_O2(4, 4); else VWA_CHAIN_LAUNCH_O2(3, 4); break;
+      case 8: if (q) VWA_CHAIN_LAUNCH_O2(4, 8); else VWA_CHAIN_LAUNCH_O2(3, 8); break;
+      default: return -10;
+    }
+#undef VWA_CHAIN_LAUNCH_O2
+    return (int)hipGetLastError();
+  }
   if (xg2) {  // Llama tail of 5..16 rows: down projection with X from L2, no attention phase
     if (seq != 0 || attn_g != 0 || f8 || (n_phases != 3 && n_phases != 4)) return -10;
     if (n_phases == 4) hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);

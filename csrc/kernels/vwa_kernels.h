@@ -135,6 +135,7 @@ struct ChainParams {
   int xwait;      // no wave issues weights between a barrier's release and its X rows landing in LDS
   int xw_late;    // (xwait) the weights go out after the row scales, not before
   int poll_free;  // wave 0 (the barrier poller) issues nothing ahead of a barrier wait
+  int o_nt2;      // attention launches: phase 0 (o_proj) in 32-column tiles (host request; prepare clears it when unused)
   ChainTP tp;
 };
 
@@ -165,6 +166,11 @@ struct GemmParams {
   const int* positions; const int64_t* slots; const float* rope;
   uint16_t* q_out; int ldq; uint16_t* k_cache; uint16_t* v_cache; int block_size;
   int64_t cache_sb, cache_sh, cache_st;
+  // RMS statistics hand-off (decode steps of > 16 rows, one rank): ss_out -- the residual epilogue
+  // adds the squares of its bf16 output rows into ss_out[m] (the next RMSNorm's statistics, f32
+  // atomics); ss_zero[0, ss_zero_n) is zeroed by workgroup 0 (the other buffer, already consumed);
+  // ss_in -- the per-row scale is rsqrt(ss_in[m] / K + ss_eps) instead of rstd[m] (no row_rstd launch)
+  float* ss_out; float* ss_zero; int ss_zero_n; const float* ss_in; float ss_eps;
 };
 
 struct FlashAttnParams {
@@ -187,7 +193,7 @@ int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipS
 void vwa_skinny_set_x_skew(int skew);  // LDS-staged X rows: 64-B skew every 4 rows (default) or none (0)
 int vwa_chain_prepare(ChainParams* cp, int grid);
 int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid, hipStream_t st,
-                     int xg2 = 0, int f8 = 0);
+                     int xg2 = 0, int f8 = 0, int o2 = 0);
 int vwa_gemm(int epi, const GemmParams* p, hipStream_t st);
 int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats, int f8);
 void vwa_gemm_set_split_fill(int pct);  // split-K while tiles x splits < pct % of the CUs (0: bf16 75, fp8 100)

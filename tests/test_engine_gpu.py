@@ -191,7 +191,17 @@ def test_chained_layer_tail_matches_per_kernel_path(cfg, grid_div, monkeypatch):
         got_a = run(True)
         # 1-row steps there preload gate/up's item 2 into LDS during the attention window
         # (ChainParams::lds_item: the whole 160 KB of LDS)
-        assert any(v[2] == 160 * 1024 for v in model.chain_descs())
+        assert any(v[2] & 0xFFFFFF == 160 * 1024 for v in model.chain_descs())
+        # o_proj in 32-column tiles (ChainParams::o_nt2, one epilogue per workgroup) and in 16
+        for sched, bit in (("o_nt2=1", 1), ("o_nt2=0", 0)):
+            monkeypatch.setenv("VWA_CHAIN_SCHED", sched)
+            model.reset_chains()
+            got_o = run(True)
+            assert any((v[2] >> 26) & 1 == bit for v in model.chain_descs())
+            for a, b in zip(got_o, ref):
+                err = (a - b).abs().max().item()
+                assert math.isfinite(err) and err < 0.02 * (1 + b.abs().max().item()), (sched, err)
+        monkeypatch.delenv("VWA_CHAIN_SCHED")
         monkeypatch.setenv("VWA_CHAIN_ATTN", "0")  # and the separate attention launch
         model.reset_chains()
         got = run(True)

@@ -715,11 +715,13 @@ def test_gemm_qkv_rope_kv_write(M):
         close(a, b, 3e-2)
 
 
-@pytest.mark.parametrize("M", [1, 4, 16, 17, 85, 1011])
+@pytest.mark.parametrize("M", [1, 4, 16, 17, 40, 64, 85, 1011])
 def test_fp8_tiled_weights_w8a8(M):
     """fp8 weights in the fp8 tiled layout (ops.tile_weight_fp8): the W8A8 streaming kernel (<= 16
-    rows) and the W8A8 tiled GEMM (gemm.hip F8, > 16 rows) against the CPU W8A8 emulation, for the
-    store / residual / SwiGLU / QKV epilogues."""
+    rows), the W8A16 tiled GEMM (gemm.hip W8: 17..FP8_A16_ROWS rows, e4m3 tiles converted on the LDS
+    read) and the W8A8 tiled GEMM (gemm.hip F8, more rows) against the CPU emulation of the same
+    rounding, for the store / residual / SwiGLU / QKV epilogues."""
+    assert ops.FP8_A16_ROWS == 64  # (the row classes above)
     K, N = 4096, 1024
     x = rnd(M, K)
     w = rnd(N, K, scale=K ** -0.5)
@@ -923,3 +925,47 @@ def test_decode_attention_shared_prefix(hd, nq, nkv, n_sess, P):
     close(outs[1][:n_real], exp[:n_real], 2e-2)
     assert torch.equal(outs[0], outs[2])
 
+
+
+@pytest.mark.parametrize("M", [17, 40, 85, 600])
+@pytest.mark.parametrize("wdt", ["bf16", "fp8"])
+def test_rms_statistics_handoff(M, wdt):
+    """Many-row residual GEMMs hand the next RMSNorm its row statistics (GemmParams::ss_*): the
+    residual epilogue (direct, or in the split-K reduce) adds the squares of the stored bf16 rows
+    to ss_out and zeroes ss_zero; the consumers (SwiGLU / QKV GEMMs, bf16 and W8A16 -- W8A8 keeps
+    its quantiser's own 1/rms) read rsqrt(ss / K + eps) instead of a row_rstd launch -- equal to
+    the row_rstd path."""
+    d, F = 4096, 1024
+    wrap = (lambda w: ops.FP8Weight.quantize(w)) if wdt == "fp8" else ops.TiledWeight  # noqa: E731
+    wo, wgu = wrap(rnd(d, d, scale=d ** -0.5)), wrap(ops.interleave_gate_up(rnd(F, d, scale=0.02), rnd(F, d, scale=0.02)))
+    x, h0 = rnd(M, d), rnd(M, d)
+    ss = torch.full((2, 4096), 7.0, device=DEV)
+    ss[0].zero_()
+    h = h0.clone()
+    ops.linear(x, wo, out=h, residual=h, ss_out=ss[0], ss_zero=ss[1])
+    assert torch.all(ss[1] == 0)
+    want = h.float().pow(2).sum(-1)
+    close(ss[0, :M], want, 1e-3 * float(want.max()), 1e-4)
+    assert torch.all(ss[0, M:] == 0)
+    h_ref = h0.clone()
+    ops.linear(x, wo, out=h_ref, residual=h_ref)
+    assert torch.equal(h, h_ref)
+    a = ops.linear_swiglu(h, wgu, fuse_rms=True, eps=1e-5, ss_in=ss[0])
+    b = ops.linear_swiglu(h, wgu, fuse_rms=True, eps=1e-5)
+    close(a, b, 1e-2, 1e-2)
+    nq, nkv, hd = 4, 2, 128
+    wq = wrap(ops.permute_qkv_rows(rnd((nq + 2 * nkv) * hd, d, scale=d ** -0.5), nq + 2 * nkv, hd))
+    rope = ops.rope_table(2048, hd, 5e5, device=DEV)
+    pos = torch.arange(M, dtype=torch.int32, device=DEV)
+    slots = torch.arange(M, dtype=torch.int64, device=DEV)
+    outs = []
+    for s_in in (ss[0], None):
+        nb = (M + 15) // 16 + 1
+        kc = torch.zeros(nb, nkv, 16, hd, dtype=BF, device=DEV)
+        vc = torch.zeros_like(kc)
+        q = torch.zeros(M, nq * hd, dtype=BF, device=DEV)
+        ops.qkv_rope_write(h, wq, None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd, rope=rope,
+                           positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc, ss_in=s_in)
+        outs.append((q, kc, vc))
+    for u, v in zip(*outs):
+        close(u, v, 1e-2, 1e-2)

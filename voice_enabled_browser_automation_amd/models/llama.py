@@ -202,10 +202,27 @@ class LlamaModel:
         return sum(t.numel() * t.element_size() for t in ts)
 
     # ------------------------------------------------------------------ forward
-    def _row_parallel(self, x: torch.Tensor, w: torch.Tensor, h: torch.Tensor):
-        """h <- h + x @ w^T summed over TP ranks (one all-reduce, residual folded into rank 0)."""
+    def _rms_stats(self, M: int):
+        """The two RMS-statistics buffers of the per-kernel many-row path (None when the projections
+        run elsewhere: <= 16 rows -- the streaming kernels fuse the RMSNorm themselves -- CPU, or TP,
+        whose row-parallel outputs are partial sums until the all-reduce)."""
+        if M <= ops.SKINNY_MAX_M or self.device.type != "cuda" or self.tp.size > 1 or \
+                not ops.env_flag("VWA_RMS_HANDOFF"):
+            return None
+        if getattr(self, "_ss", None) is None:
+            self._ss = torch.zeros(2, 4096, dtype=torch.float32, device=self.device)
+        if M > self._ss.shape[1]:
+            return None
+        # (the residual GEMMs keep ss[0] zero between forwards; cleared here too, so an interrupted
+        # forward cannot leave partial sums behind)
+        self._ss[0].zero_()
+        return self._ss[0], self._ss[1]
+
+    def _row_parallel(self, x: torch.Tensor, w: torch.Tensor, h: torch.Tensor, ss=None):
+        """h <- h + x @ w^T summed over TP ranks (one all-reduce, residual folded into rank 0).
+        ss = (out, zero): the rows' sums of squares go to ``out``, ``zero`` is cleared (one rank)."""
         if self.tp.size == 1:
-            ops.linear(x, w, out=h, residual=h)
+            ops.linear(x, w, out=h, residual=h, ss_out=ss[0] if ss else None, ss_zero=ss[1] if ss else None)
         else:
             if self.tp.rank == 0:
                 ops.linear(x, w, out=h, residual=h)
@@ -358,6 +375,10 @@ class LlamaModel:
             pf_sid = torch.full((M,), prefill_seq, **i32)
             pf_slices = [(i, min(M, i + 64)) for i in range(0, M, 64)]
             pf_out = torch.empty((M, self.nq * self.hd), dtype=self.dtype, device=self.device)
+        # > 16 rows on one rank (the tiled GEMMs): each residual GEMM hands the sums of squares of the
+        # rows it writes to the next RMSNorm (ss[0]: after o_proj -> gate/up, ss[1]: after down ->
+        # next QKV) and zeroes the other buffer, so no row_rstd launch (GemmParams::ss_*)
+        ss = self._rms_stats(M) if not chain else None
         for li, L in enumerate(self.layers):
             kc, vc = kv.k[li], kv.v[li]
             if chain and li > 0:
@@ -365,7 +386,8 @@ class LlamaModel:
             else:
                 q = ops.qkv_rope_write(h, L.qkv, None, fuse_rms=True, eps=cfg.rms_eps, n_q_heads=self.nq,
                                        n_kv_heads=self.nkv, head_dim=self.hd, rope=self.rope,
-                                       positions=bufs.positions, slots=bufs.slots, q_out=qbuf, k_cache=kc, v_cache=vc)
+                                       positions=bufs.positions, slots=bufs.slots, q_out=qbuf, k_cache=kc, v_cache=vc,
+                                       ss_in=ss[1] if ss is not None and li > 0 else None)
             d = self._chain_desc(bufs, kv, M, li) if chain else None
             if d is not None:
                 # chained layer: [decode attention ->] o_proj -> gate/up -> down [-> next QKV]
@@ -407,10 +429,10 @@ class LlamaModel:
                 ops.flash_attention(q4, ops.KVLayout.paged(kc, vc, table), Sk=q_offset + M, n_kv_heads=self.nkv,
                                     causal=True, scale=self.scale, q_offset=q_offset, out=attn4)
                 attn = attn4.view(M, self.nq * self.hd)
-            self._row_parallel(attn, L.o, h)
+            self._row_parallel(attn, L.o, h, ss and (ss[0], ss[1]))
             act = bufs.act[:M] if M <= bufs.act.shape[0] else None
-            act = ops.linear_swiglu(h, L.gu, fuse_rms=True, eps=cfg.rms_eps, out=act)
-            self._row_parallel(act, L.down, h)
+            act = ops.linear_swiglu(h, L.gu, fuse_rms=True, eps=cfg.rms_eps, out=act, ss_in=ss and ss[0])
+            self._row_parallel(act, L.down, h, ss and (ss[1], ss[0]))
         if n_sel is not None:
             hs = torch.index_select(h, 0, bufs.sel[:n_sel], out=bufs.hidden_sel[:n_sel])
         else:

@@ -176,9 +176,12 @@ def quant_rows_fp8(x: torch.Tensor) -> torch.Tensor:
 
 
 def _ref_w8(x: torch.Tensor, w, fuse_rms: bool, eps: float):
-    """(x, w) for the torch reference: W8A8 emulation when w is fp8 (rms from the unquantised x)."""
+    """(x, w) for the torch reference: the GPU path's rounding when w is fp8 -- W8A16 (x unquantised)
+    for 17..FP8_A16_ROWS rows, W8A8 emulation otherwise (rms from the unquantised x)."""
     if not isinstance(w, FP8Weight):
         return x, w, fuse_rms
+    if SKINNY_MAX_M < x.shape[0] <= FP8_A16_ROWS:
+        return x, w.dequant(), fuse_rms
     xf = x.float()
     if fuse_rms:
         xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
@@ -417,20 +420,29 @@ GEMM_WS_FLOATS = 32 << 20  # split-K workspace (128 MB per device: 4 f32 slices 
 _GEMM_EPI = {"none": 0, "resid": 1, "swiglu": 2, "gelu": 3}
 
 
+def _rstd(x: torch.Tensor, eps: float) -> torch.Tensor:
+    """Per-row 1/rms of x (the RMSNorm of a projection whose gamma is folded into its weight)."""
+    rstd = scratch(x.device, "gemm_rstd", x.shape[0])
+    ext().row_rstd(x, rstd, eps)
+    return rstd
+
+
 def gemm(x: torch.Tensor, w, out: torch.Tensor, *, epi: str = "none", bias: Optional[torch.Tensor] = None,
-         residual: Optional[torch.Tensor] = None, fuse_rms: bool = False, eps: float = 1e-5) -> torch.Tensor:
+         residual: Optional[torch.Tensor] = None, fuse_rms: bool = False, eps: float = 1e-5,
+         ss_out: Optional[torch.Tensor] = None, ss_zero: Optional[torch.Tensor] = None,
+         ss_in: Optional[torch.Tensor] = None) -> torch.Tensor:
     """The hand-written LDS-tiled MFMA GEMM (csrc/kernels/gemm.hip) for M > 16 rows:
     out = epi(rms(x) @ w^T + bias); w a TiledWeight (its single pre-tiled copy) or a row-major bf16
-    [N, K] tensor.  fuse_rms: the per-row 1/rms of x scales the product (gamma folded into w)."""
+    [N, K] tensor.  fuse_rms: the per-row 1/rms of x scales the product (gamma folded into w) --
+    from ``ss_in`` (the rows' sums of squares, handed off by the GEMM that wrote x) when given, else
+    one row_rstd launch.  ss_out / ss_zero (residual epilogue): see GemmParams::ss_*."""
     E = ext()
-    rstd = None
-    if fuse_rms:
-        rstd = scratch(x.device, "gemm_rstd", x.shape[0])
-        E.row_rstd(x, rstd, eps)
+    rstd = _rstd(x, eps) if fuse_rms and ss_in is None else None
     tiled = isinstance(w, TiledWeight)
     wt = w.t if tiled else w
     ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
-    E.gemm(x, wt, bias, out, _GEMM_EPI[epi], rstd, residual, tiled, ws)
+    E.gemm(x, wt, bias, out, _GEMM_EPI[epi], rstd, residual, tiled, ws, ss_out, ss_zero,
+           ss_in if fuse_rms else None, eps)
     return out
 
 
@@ -454,16 +466,29 @@ def _fp8_input(x: torch.Tensor, fuse_rms: bool, eps: float):
     return x8[: M * K].view(M, K), sx, (rs if fuse_rms else None)
 
 
+# fp8 weights, > 16 rows: up to this many rows the tiled GEMM runs W8A16 (bf16 x, the e4m3 tiles
+# converted to bf16 on the LDS read: no per-row quantisation launch -- the decode steps of many
+# sessions are weight-streaming bound), above it W8A8 (the fp8 MFMA: prompt-sized, compute bound)
+FP8_A16_ROWS = knob("VWA_FP8_A16_ROWS")
+
+
 def gemm_fp8(x: torch.Tensor, w: "FP8Weight", out: torch.Tensor, *, epi: str = "none",
              bias: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None, fuse_rms: bool = False,
-             eps: float = 1e-5) -> torch.Tensor:
-    """W8A8 tiled MFMA GEMM (gemm.hip F8) for M > 16 rows: x is quantised per row (amax / 448, one
-    kernel that also yields the RMSNorm 1/rms), the fp8 MFMA runs on the tiled fp8 weight, both
-    scales (and the RMSNorm 1/rms of the unquantised x) apply in the epilogue."""
+             eps: float = 1e-5, ss_out: Optional[torch.Tensor] = None, ss_zero: Optional[torch.Tensor] = None,
+             ss_in: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp8-weight tiled MFMA GEMM (gemm.hip) for M > 16 rows.  <= FP8_A16_ROWS rows: W8A16 (bf16 x,
+    weights converted in-kernel).  More: W8A8 -- x is quantised per row (amax / 448, one kernel that
+    also yields the RMSNorm 1/rms), the fp8 MFMA runs on the tiled fp8 weight.  The scales (and the
+    RMSNorm 1/rms of the unquantised x) apply in the epilogue."""
     E = ext()
-    x8, sx, rstd = _fp8_input(x, fuse_rms, eps)
     ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
-    E.gemm_fp8(x8, sx, w.w8, w.scale, bias, out, _GEMM_EPI[epi], rstd, residual, ws)
+    if x.shape[0] <= FP8_A16_ROWS:
+        E.gemm_fp8(x, None, w.w8, w.scale, bias, out, _GEMM_EPI[epi],
+                   _rstd(x, eps) if fuse_rms and ss_in is None else None, residual, ws, ss_out, ss_zero,
+                   ss_in if fuse_rms else None, eps)
+        return out
+    x8, sx, rstd = _fp8_input(x, fuse_rms, eps)  # (the quantiser yields the 1/rms: ss_in unused)
+    E.gemm_fp8(x8, sx, w.w8, w.scale, bias, out, _GEMM_EPI[epi], rstd, residual, ws, ss_out, ss_zero)
     return out
 
 
@@ -493,7 +518,9 @@ SKINNY_MAX_M = 16
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, *, out: Optional[torch.Tensor] = None,
            residual: Optional[torch.Tensor] = None, act: str = "none", fuse_rms: bool = False, eps: float = 1e-5,
            out_dtype: Optional[torch.dtype] = None, ln_c: Optional[torch.Tensor] = None,
-           col_mask: Optional[torch.Tensor] = None, col_mask_off: int = 0, mask_rows: int = 1) -> torch.Tensor:
+           col_mask: Optional[torch.Tensor] = None, col_mask_off: int = 0, mask_rows: int = 1,
+           ss_out: Optional[torch.Tensor] = None, ss_zero: Optional[torch.Tensor] = None,
+           ss_in: Optional[torch.Tensor] = None) -> torch.Tensor:
     """y = act(rms(x) @ w^T + bias) [+ residual].
 
     GPU: decode rows (<= SKINNY_MAX_M) -> the MFMA streaming GEMM with fused epilogue; more rows
@@ -505,8 +532,28 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     streaming kernel computes only the 16-column tiles with an admissible bit (word col_mask_off
     onward) in one of the first mask_rows rows and leaves the other columns of ``out`` untouched
     -- they must only be read through the same mask.  Other paths compute every column.
+    ss_out / ss_zero / ss_in: the RMS statistics hand-off of the tiled GEMMs (ops.gemm); a path
+    without it honours ss_out / ss_zero with torch ops and computes its own 1/rms.
     """
+    ss = dict(ss_out=ss_out, ss_zero=ss_zero, ss_in=ss_in, used=False)
+    out = _linear_impl(x, w, bias, out, residual, act, fuse_rms, eps, out_dtype, ln_c, col_mask, col_mask_off,
+                       mask_rows, ss)
+    if not ss["used"] and (ss_out is not None or ss_zero is not None):  # (paths without the hand-off)
+        if ss_zero is not None:
+            ss_zero.zero_()
+        if ss_out is not None:
+            ss_out[: x.shape[0]] += out.float().pow(2).sum(-1)
+    return out
+
+
+def _linear_impl(x, w, bias, out, residual, act, fuse_rms, eps, out_dtype, ln_c, col_mask, col_mask_off, mask_rows,
+                 ss):
     M = x.shape[0]
+
+    def ssk():  # the hand-off arguments for the tiled GEMMs (which take them)
+        ss["used"] = True
+        return dict(ss_out=ss["ss_out"], ss_zero=ss["ss_zero"], ss_in=ss["ss_in"])
+
     mk = {}
     if col_mask is not None and residual is None and act == "none" and bias is None and ln_c is None:
         mk = dict(col_mask=col_mask, col_mask_off=col_mask_off, mask_rows=mask_rows)
@@ -527,7 +574,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         if _gpu(x) and gemm_ok(x, w, out, residual) and (act == "none" or residual is None) and \
                 (out.dtype == torch.bfloat16 or (residual is None and act == "none")):
             e = "resid" if residual is not None else ("gelu" if act == "gelu" else "none")
-            return gemm(x, w, out, epi=e, bias=bias, residual=residual, fuse_rms=fuse_rms, eps=eps)
+            return gemm(x, w, out, epi=e, bias=bias, residual=residual, fuse_rms=fuse_rms, eps=eps, **ssk())
         w = w.dense()
     if ln_c is not None:
         if _ln_fold_fits(x, w):
@@ -554,9 +601,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     e = "resid" if residual is not None else ("gelu" if act == "gelu" else "none")
     plain_epi = (act == "none" or residual is None) and (out.dtype == torch.bfloat16 or (residual is None and act == "none"))
     if fp8 and plain_epi and gemm_fp8_ok(x, w, out, residual):
-        return gemm_fp8(x, w, out, epi=e, bias=bias, residual=residual, fuse_rms=fuse_rms, eps=eps)
+        return gemm_fp8(x, w, out, epi=e, bias=bias, residual=residual, fuse_rms=fuse_rms, eps=eps, **ssk())
     if not fp8 and plain_epi and gemm_ok(x, w, out, residual):
-        return gemm(x, w, out, epi=e, bias=bias, residual=residual, fuse_rms=fuse_rms, eps=eps)
+        return gemm(x, w, out, epi=e, bias=bias, residual=residual, fuse_rms=fuse_rms, eps=eps, **ssk())
     if fp8 and w.tiled:
         w = FP8Weight(w.rows(), w.scale)  # (shapes the tiled kernels reject: dequantising path)
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
@@ -579,7 +626,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
 
 
 def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False, eps: float = 1e-5,
-                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  out: Optional[torch.Tensor] = None, ss_in: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(gate) * up of the interleaved gate/up projection (ops.interleave_gate_up); ss_in: the
+    rows' handed-off sums of squares for the fused RMSNorm (tiled GEMM paths, see ops.gemm)."""
     M = x.shape[0]
     F = w_gu.shape[0] // 2
     if out is None:
@@ -589,7 +638,7 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
             ext().skinny_gemm_swiglu(x, w_gu.t, None, out, fuse_rms, eps, None, True)
             return out
         if _gpu(x) and gemm_ok(x, w_gu, out):
-            return gemm(x, w_gu, out, epi="swiglu", fuse_rms=fuse_rms, eps=eps)
+            return gemm(x, w_gu, out, epi="swiglu", fuse_rms=fuse_rms, eps=eps, ss_in=ss_in)
         w_gu = w_gu.dense()
     if not _gpu(x):
         xr, wr, fr = _ref_w8(x, w_gu, fuse_rms, eps)
@@ -603,9 +652,9 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, *, fuse_rms: bool = False
             E.skinny_gemm_swiglu(x, w_gu, None, out, fuse_rms, eps)
         return out
     if fp8 and gemm_fp8_ok(x, w_gu, out):
-        return gemm_fp8(x, w_gu, out, epi="swiglu", fuse_rms=fuse_rms, eps=eps)
+        return gemm_fp8(x, w_gu, out, epi="swiglu", fuse_rms=fuse_rms, eps=eps, ss_in=ss_in)
     if not fp8 and gemm_ok(x, w_gu, out):
-        return gemm(x, w_gu, out, epi="swiglu", fuse_rms=fuse_rms, eps=eps)
+        return gemm(x, w_gu, out, epi="swiglu", fuse_rms=fuse_rms, eps=eps, ss_in=ss_in)
     if fp8 and w_gu.tiled:
         w_gu = FP8Weight(w_gu.rows(), w_gu.scale)
     xin = rmsnorm(x, None, eps=eps) if fuse_rms else x
@@ -623,29 +672,33 @@ GEMM_QKV_FUSED = knob("VWA_GEMM_QKV")
 
 
 def _gemm_qkv(x, w, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, rope, positions, slots, q_out, k_cache,
-              v_cache) -> None:
+              v_cache, ss_in=None) -> None:
     E = ext()
     M, K = x.shape
     ws = scratch(x.device, "gemm_ws", GEMM_WS_FLOATS)
     common = (n_q_heads, n_kv_heads, head_dim, rope is not None, positions, slots, rope, q_out, k_cache, v_cache)
     if isinstance(w, FP8Weight):
+        if M <= FP8_A16_ROWS:  # W8A16 (see gemm_fp8)
+            hand = fuse_rms and ss_in is not None
+            E.gemm_qkv(x, None, w.w8, w.scale, bias, _rstd(x, eps) if fuse_rms and not hand else None, True, ws,
+                       *common, ss_in if hand else None, eps)
+            return
         x8, sx, rstd = _fp8_input(x, fuse_rms, eps)
         E.gemm_qkv(x8, sx, w.w8, w.scale, bias, rstd, True, ws, *common)
         return
-    rstd = None
-    if fuse_rms:
-        rstd = scratch(x.device, "gemm_rstd", M)
-        E.row_rstd(x, rstd, eps)
+    hand = fuse_rms and ss_in is not None
+    rstd = _rstd(x, eps) if fuse_rms and not hand else None
     tiled = isinstance(w, TiledWeight)
-    E.gemm_qkv(x, None, w.t if tiled else w, None, bias, rstd, tiled, ws, *common)
+    E.gemm_qkv(x, None, w.t if tiled else w, None, bias, rstd, tiled, ws, *common, ss_in if hand else None, eps)
 
 
 def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Tensor], *, fuse_rms: bool, eps: float,
                    n_q_heads: int, n_kv_heads: int, head_dim: int, rope: Optional[torch.Tensor],
                    positions: torch.Tensor, slots: torch.Tensor, q_out: torch.Tensor, k_cache: torch.Tensor,
-                   v_cache: torch.Tensor, ln_c: Optional[torch.Tensor] = None) -> torch.Tensor:
+                   v_cache: torch.Tensor, ln_c: Optional[torch.Tensor] = None,
+                   ss_in: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Fused QKV projection + rotary + paged KV write. Returns q_out[:M] (natural layout).
-    ln_c: folded LayerNorm on x (see linear)."""
+    ln_c: folded LayerNorm on x (see linear).  ss_in: handed-off sums of squares (see ops.gemm)."""
     M = x.shape[0]
     if isinstance(w_qkv, TiledWeight):
         if _gpu(x) and _stream_ok(x, w_qkv) and (ln_c is None or _ln_fold_fits(x, w_qkv)):
@@ -656,7 +709,7 @@ def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Te
             x, ln_c = _layernorm_plain(x, eps), None
         if _gpu(x) and gemm_ok(x, w_qkv) and GEMM_QKV_FUSED:
             _gemm_qkv(x, w_qkv, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, rope, positions, slots, q_out,
-                      k_cache, v_cache)
+                      k_cache, v_cache, ss_in)
             return q_out[:M]
         if _gpu(x) and gemm_ok(x, w_qkv):
             qkv = scratch(x.device, "qkv", M * w_qkv.shape[0], torch.bfloat16).view(M, w_qkv.shape[0])
@@ -682,7 +735,7 @@ def qkv_rope_write(x: torch.Tensor, w_qkv: torch.Tensor, bias: Optional[torch.Te
     fp8 = isinstance(w_qkv, FP8Weight)
     if M > SKINNY_MAX_M and (gemm_fp8_ok(x, w_qkv) if fp8 else gemm_ok(x, w_qkv)) and GEMM_QKV_FUSED:
         _gemm_qkv(x, w_qkv, bias, fuse_rms, eps, n_q_heads, n_kv_heads, head_dim, rope, positions, slots, q_out,
-                  k_cache, v_cache)
+                  k_cache, v_cache, ss_in)
         return q_out[:M]
     if M > SKINNY_MAX_M and (gemm_fp8_ok(x, w_qkv) if fp8 else gemm_ok(x, w_qkv)):
         qkv = scratch(x.device, "qkv", M * w_qkv.shape[0], torch.bfloat16).view(M, w_qkv.shape[0])

@@ -114,6 +114,8 @@ class Settings(BaseModel):
     VWA_ROW_BUCKETS: str = Field("1,2,4,8,12,16,32,48,64", description="decode row buckets of the captured graphs")
     VWA_SHARED_ATTN: bool = Field(True, description="decode attention reads a shared prompt prefix once per row group")
     VWA_PREFILL_FLASH: bool = Field(True, description="batched admission prefill through one causal flash launch")
+    VWA_RMS_HANDOFF: bool = Field(True, description="> 16-row steps: residual GEMMs hand the next RMSNorm its row statistics (no row_rstd launches)")
+    VWA_FP8_A16_ROWS: int = Field(64, description="fp8 weights: rows up to which the > 16-row GEMM runs W8A16 (no activation quantisation)")
     VWA_PREFILL_DECODE_ATTN: bool = Field(True, description="cached-prefix prompt suffix through the decode attention")
     VWA_TILED_WEIGHTS: bool = Field(True, description="keep projection weights only in the MFMA-tiled layout")
     VWA_MASKED_HEAD: bool = Field(True, description="LM head computes only the vocab tiles the grammar admits")
