@@ -607,7 +607,8 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                                        c10::optional<Tensor> a_part_ml, c10::optional<Tensor> a_counters,
                                        bool w_tiled, c10::optional<Tensor> a_row_table,
                                        c10::optional<Tensor> s_o, c10::optional<Tensor> s_gu,
-                                       c10::optional<Tensor> s_down, c10::optional<Tensor> s_qkv, int64_t tp_ar) {
+                                       c10::optional<Tensor> s_down, c10::optional<Tensor> s_qkv, int64_t tp_ar,
+                                       c10::optional<Tensor> a_plan, int64_t a_plan_mode) {
   c10::DeviceGuard g(h.device());
   const int64_t M = h.size(0);
   TORCH_CHECK(att.size(0) == M && act.size(0) == M, "row counts differ");
@@ -693,6 +694,15 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
                   "a_row_table must be int32 [>= rows, <= 128 (even)] contiguous");
       cp.attn.row_table = rtab.data_ptr<int>();
       cp.attn.rt_stride = (int)rtab.size(1);
+    }
+    // step plan of the attention partition (mq_attention.h): layer 0 writes it, layers 1.. read it
+    if (a_plan_mode) {
+      TORCH_CHECK(a_plan_mode == 1 || a_plan_mode == 2, "a_plan_mode: 1 write, 2 read");
+      TORCH_CHECK(a_plan.has_value() && a_plan->is_cuda() && a_plan->scalar_type() == at::kInt && a_plan->is_contiguous() &&
+                      a_plan->numel() >= (int64_t)chain_grid(h.device().index()) * 16,
+                  "a_plan must be int32 [>= grid * 16] on the GPU");
+      cp.attn.plan = a_plan->data_ptr<int>();
+      cp.attn.plan_mode = (int)a_plan_mode;
     }
   }
   const int lds = vwa_chain_prepare(&cp, chain_grid(h.device().index()));
@@ -1282,7 +1292,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("a_n_splits") = 0, py::arg("a_part_o") = py::none(), py::arg("a_part_ml") = py::none(),
         py::arg("a_counters") = py::none(), py::arg("w_tiled") = false, py::arg("a_row_table") = py::none(),
         py::arg("s_o") = py::none(), py::arg("s_gu") = py::none(), py::arg("s_down") = py::none(),
-        py::arg("s_qkv") = py::none(), py::arg("tp_ar") = 0);
+        py::arg("s_qkv") = py::none(), py::arg("tp_ar") = 0, py::arg("a_plan") = py::none(), py::arg("a_plan_mode") = 0);
   m.def("set_small_gemm_bytes", &set_small_gemm_bytes);
   m.def("gemm_set_p8", [](int64_t mode) { vwa_gemm_set_p8((int)mode); });
   m.def("skinny_set_x_skew", [](int64_t skew) { vwa_skinny_set_x_skew((int)skew); });

@@ -177,7 +177,28 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   // the launch's start is 8x the requests on the same L2 lines.  (In the first 2.5 KB: the chained
   // launch's idle workgroups LDS-DMA weights above 32 KB while other waves may still read it.)
   int* s_meta = reinterpret_cast<int*>(lds + L::vimg);  // [4][128] row tables | [64] seq ids | [64] contexts
-  if (w == 0) {
+  // ---- step plan (FINE, p.plan_mode 2): the partition depends only on the step's rows and
+  //      contexts, the same for every layer, so the chained launch of layer 0 writes each
+  //      workgroup's item (plan_mode 1) and layers 1.. load it -- with the row tables, in one round
+  //      trip, every wave for itself: no metadata through LDS, no barrier, no ballots before the
+  //      K/V loads.  Entry (16 ints): n_items, n_final, state (0 idle, 1 item, 2 empty chunk, 3 no
+  //      plan: several items per workgroup), kv head, r0, nr, kbeg, kend, nact, slot, rows, -,
+  //      contexts of group rows 0..3.  An entry of another row count is ignored.
+  int2 rt[4];
+  int ev = 0;
+  bool plan = false;
+  if constexpr (FINE) {
+    if (p.plan_mode == 2) {
+      const __amdgpu_buffer_rsrc_t r_pl = __builtin_amdgcn_make_buffer_rsrc(p.plan, (short)0, (bid + 1) * 64, 0x00020000);
+      ev = (int)__builtin_amdgcn_raw_buffer_load_b32(r_pl, (bid * 16 + (lane & 15)) * 4, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        rt[r] = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
+                                             r_rt, 2 * lane < p.rt_stride ? (r * p.rt_stride + 2 * lane) * 4 : 0x7FFFFFF0, 0, 0));
+      plan = __builtin_amdgcn_readlane(ev, 2) != 3 && __builtin_amdgcn_readlane(ev, 10) == p.rows;
+    }
+  }
+  if (w == 0 && !plan) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       *reinterpret_cast<int2*>(s_meta + r * 128 + 2 * lane) = __builtin_bit_cast(
@@ -195,13 +216,14 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
       if (lane < 2) s_meta[640 + lane] = (int)__builtin_amdgcn_raw_buffer_load_b32(r_sh, lane * 4, 0, 0);
     }
   }
-  __syncthreads();
-  stamp(12);  // (diagnostic: step metadata in LDS)
-  int2 rt[4];
+  if (!plan) {
+    __syncthreads();
 #pragma unroll
-  for (int r = 0; r < 4; ++r) rt[r] = *reinterpret_cast<const int2*>(s_meta + r * 128 + 2 * lane);
-  const int sl = lane < p.rows ? s_meta[512 + lane] : -1;
-  const int cl = lane < p.rows ? s_meta[576 + lane] : 0;
+    for (int r = 0; r < 4; ++r) rt[r] = *reinterpret_cast<const int2*>(s_meta + r * 128 + 2 * lane);
+  }
+  stamp(12);  // (diagnostic: step metadata in LDS / the plan entry in registers)
+  const int sl = plan ? -1 : lane < p.rows ? s_meta[512 + lane] : -1;
+  const int cl = plan ? 0 : lane < p.rows ? s_meta[576 + lane] : 0;
   stamp(16);
   const int sp = __shfl(sl, lane > 0 ? lane - 1 : 0, 64);
   const unsigned long long seq_starts = __ballot(lane < p.rows && (lane == 0 || sl != sp));
@@ -233,11 +255,24 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   const int tgt = FINE ? grid : max(1, grid / 2);
   const int n_pc = cascade ? max(1, min(p.n_splits - RG, tgt / max(1, n_groups * nkv) - RG)) : 0;
   const int n_eff = cascade ? n_pc + RG : max(1, min(FINE ? min(p.n_splits, 16) : p.n_splits, tgt / max(1, n_groups * nkv)));
-  const int n_items = n_groups * nkv * n_eff;
+  const int n_items = plan ? __builtin_amdgcn_readlane(ev, 0) : n_groups * nkv * n_eff;
   if (n_items_out) *n_items_out = n_items;
-  if (n_final_out) *n_final_out = n_groups * nkv;
+  if (n_final_out) *n_final_out = plan ? __builtin_amdgcn_readlane(ev, 1) : n_groups * nkv;
   stamp(17);
+  // plan_mode 1: lanes 0..15 of wave 0 write this workgroup's entry (c: the group rows' contexts
+  // in lanes 0..3)
+  const bool multi = n_items > grid;
+  auto write_plan = [&](int st, int kvh, int r0, int nr, int kbeg, int kend, int nact, int slot, int c) {
+    if (!FINE || p.plan_mode != 1 || w != 0) return;
+    const int cr = __shfl(c, lane & 3, 64);
+    const int i = lane & 15;
+    const int v = i == 0 ? n_items : i == 1 ? n_groups * nkv : i == 2 ? (multi ? 3 : st) : i == 3 ? kvh : i == 4 ? r0
+                : i == 5 ? nr : i == 6 ? kbeg : i == 7 ? kend : i == 8 ? nact : i == 9 ? slot : i == 10 ? p.rows
+                : i == 11 ? 0 : cr;
+    if (lane < 16) p.plan[bid * 16 + i] = v;
+  };
   if (bid >= n_items) {
+    write_plan(0, 0, 0, 0, 0, 0, 0, 0, 0);
     on_idle();
     return true;
   }
@@ -251,14 +286,30 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   };
   for (int item = bid; item < n_items; item += grid) {
   if (item == bid) stamp(18);
+  int kvh, r0, nr, CL, kbeg, kend, nact, slot, kv_seq, ctx_n;
+  const int rho = n / G;  // group row of this lane's query column
+  if (plan) {  // (one item per workgroup)
+    if (__builtin_amdgcn_readlane(ev, 2) != 1) continue;  // empty chunk
+    kvh = __builtin_amdgcn_readlane(ev, 3);
+    r0 = __builtin_amdgcn_readlane(ev, 4);
+    nr = __builtin_amdgcn_readlane(ev, 5);
+    kbeg = __builtin_amdgcn_readlane(ev, 6);
+    kend = __builtin_amdgcn_readlane(ev, 7);
+    nact = __builtin_amdgcn_readlane(ev, 8);
+    slot = __builtin_amdgcn_readlane(ev, 9);
+    CL = kend - kbeg;
+    kv_seq = 0;
+    const int c_rho = __shfl(ev, 12 + min(rho, 3), 64);  // (rho differs per lane: a shuffle)
+    ctx_n = rho < nr ? c_rho : 0;
+  } else {
   // item -> (kv head, group, chunk); kv head fastest so a head's workgroups share one XCD (b % 8)
-  const int kvh = item % nkv;
+  kvh = item % nkv;
   const int gi = (item / nkv) % n_groups, chunk = item / (nkv * n_groups);
   const unsigned long long pick = __ballot(((leaders >> lane) & 1ull) && my_rank == gi);
-  const int r0 = __builtin_ctzll(pick);
+  r0 = __builtin_ctzll(pick);
   const unsigned long long later = run_starts & ~((2ull << r0) - 1ull);
   const int run_end = later ? __builtin_ctzll(later) : p.rows;
-  const int nr = min(RG, run_end - r0);  // rows in this group
+  nr = min(RG, run_end - r0);  // rows in this group
   const int seq = __shfl(sl, r0, 64);
   if (item == bid) stamp(11);  // (diagnostic: before the item's barrier)
   __syncthreads();  // the previous item's LDS readers are done
@@ -269,11 +320,11 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) ctxmax = max(ctxmax, __shfl_xor(ctxmax, o, 64));
   if (item == bid) stamp(19);
-  const int rho = n / G;                     // group row of this lane's query column
-  int ctx_n = __shfl(c_own, rho, 64);        // its context (0 for padded columns)
+  ctx_n = __shfl(c_own, rho, 64);  // its context (0 for padded columns)
 
   // ---- this item's chunk of the group's keys (NW waves x CL/NW keys): [kbeg, kend), partial slot
-  int CL, kbeg, kend, nact, slot = chunk, kv_seq = seq;
+  slot = chunk;
+  kv_seq = seq;
   if (cascade && r0 < n_real) {
     // prefix chunks (slots 0 .. npa-1) over [0, P) for every row of the group; then one chunk per
     // sequence run j of the group with keys past P: [P, max ctx of the run), the other runs'
@@ -316,10 +367,15 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
     CL = ((ctxmax + n_eff - 1) / n_eff + kChunk - 1) / kChunk * kChunk;
     if (cascade) CL = (ctxmax + kChunk - 1) / kChunk * kChunk;  // padded rows: one chunk
     kbeg = chunk * CL;
-    if (kbeg >= ctxmax) continue;
+    if (kbeg >= ctxmax) {
+      if (item == bid) write_plan(2, 0, 0, 0, 0, 0, 0, 0, 0);
+      continue;
+    }
     kend = min(ctxmax, kbeg + CL);
     nact = (ctxmax + CL - 1) / CL;
   }
+  if (item == bid) write_plan(cascade ? 3 : 1, kvh, r0, nr, kbeg, kend, nact, slot, c_own);
+  }  // (metadata path)
   // non-FINE: wave w takes the contiguous CL / NW keys from wb; FINE: the chunk's 32-key steps
   // round-robin over the waves (step s of the chunk -> wave s % NW)
   const int wb = FINE ? kbeg : kbeg + w * (CL / kWv);

@@ -69,6 +69,9 @@ struct DecodeAttnParams {
   // session shares), so those rows are grouped RG at a time across sequences for keys < P (one
   // K/V read per group instead of per sequence) and by sequence for their own keys >= P.
   const int* shared;
+  // optional (chained attention): per-workgroup step plan [grid][16] int32 -- plan_mode 1: write it
+  // (layer 0), 2: read it (layers 1..; mq_attention.h), 0: off
+  int* plan; int plan_mode;
 };
 
 // Chained decode GEMM phases in one persistent launch (skinny_stream.hip, vwa_chain): each phase

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--row-major", dest="tiled", action="store_false",
                     help="row-major [N, K] weights instead of the pre-tiled layout (ops.tile_weight)")
     ap.add_argument("--fp8", action="store_true", help="fp8 tiled weights (the W8A16 chain, ops.FP8Weight)")
+    ap.add_argument("--no-plan", action="store_true",
+                    help="(--attn) every launch derives the attention partition itself (no step plan)")
     ap.add_argument("--no-stamps", action="store_true",
                     help="launch without the per-phase stamps (their stores and waits slow the phases slightly)")
     a = ap.parse_args()
@@ -99,9 +101,19 @@ def main():
         for w in Ws:
             w.update({k + "_t": ops.tile_weight(w[k]) for k in ("o", "gu", "down", "qkv")})
     wt = (lambda w, k: w[k + "_t"]) if a.tiled else (lambda w, k: w[k])  # noqa: E731
-    descs = [E.chain_make(h, att, act, wt(w, "o"), wt(w, "gu"), wt(w, "down"), 1e-5, wt(w, "qkv"), nq, nkv, hd, pos, slots, rope, q,
-                          kc, vc, bar, work, None if a.no_stamps else ts, a.bar_mode, **akw, w_tiled=a.tiled, **sc)
-             for w, sc in zip(Ws, sck)]
+    plan = {}
+    if a.attn and not a.no_plan:  # layers 1.. of a step: the plan layer 0 wrote (written once below)
+        plan = dict(a_plan=torch.zeros(1024 * 16, dtype=torch.int32, device=dev), a_plan_mode=2)
+
+    def make(w, sc, pl):
+        return E.chain_make(h, att, act, wt(w, "o"), wt(w, "gu"), wt(w, "down"), 1e-5, wt(w, "qkv"), nq, nkv, hd, pos,
+                            slots, rope, q, kc, vc, bar, work, None if a.no_stamps else ts, a.bar_mode, **akw,
+                            w_tiled=a.tiled, **sc, **pl)
+
+    descs = [make(w, sc, plan) for w, sc in zip(Ws, sck)]
+    if plan:
+        wdesc, wlds = make(Ws[0], sck[0], dict(plan, a_plan_mode=1))
+        E.chain_run(wdesc, 4, wlds, h, ag)
     it = [0]
 
     def chained():
@@ -153,7 +165,7 @@ def main():
             col = col[col > 0]
             if col.numel():
                 extra[nm] = [round(float((col.median() - t0) * 10e-3), 2), round(float((col.max() - t0) * 10e-3), 2)]
-    r = dict(kernel="chain_probe", rows=M, fp8=a.fp8, ctx=a.ctx if a.attn else None, warm_kv=a.warm_kv, n_splits=a.n_splits, kv_tok_major=a.kv_tok_major, bar_mode=a.bar_mode, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
+    r = dict(kernel="chain_probe", rows=M, plan=bool(plan), fp8=a.fp8, ctx=a.ctx if a.attn else None, warm_kv=a.warm_kv, n_splits=a.n_splits, kv_tok_major=a.kv_tok_major, bar_mode=a.bar_mode, tiled=a.tiled, row_table=a.row_table, separate_us=round(t_sep, 2), chained_us=round(t_ch, 2),
              stamps_med_us=[round(x, 2) for x in med], stamps_min_us=[round(x, 2) for x in mn],
              stamps_max_us=[round(x, 2) for x in mx],
              legend=("start,end_attn," if a.attn else "start,") + "end_o,wait_o,end_gu,wait_gu,end_down,wait_down,end_qkv")
@@ -163,6 +175,12 @@ def main():
         isatt = full[:, 9] > 0
         for nm, sel in (("attn_wg", isatt), ("other_wg", ~isatt)):
             if int(sel.sum()):
+                for slot, key in ((12, "meta_landed"), (56, "idle_issued")):
+                    col = full[sel, slot]
+                    col = col[col > t0]
+                    if col.numel():
+                        r[f"{nm}_{key}"] = [round(float((col.median() - t0) * 10e-3), 2),
+                                            round(float((col.max() - t0) * 10e-3), 2)]
                 s = st[sel]
                 r[nm] = dict(n=int(sel.sum()), med=[round(x, 2) for x in s.median(dim=0).values.tolist()],
                              max=[round(x, 2) for x in s.max(dim=0).values.tolist()],

@@ -309,6 +309,12 @@ class LlamaModel:
                      a_sb=lay.sb, a_sh=lay.sh, a_st=lay.st, a_ctx=bufs.ctx_lens, a_seq=bufs.seq_ids,
                      a_scale=self.scale, a_n_splits=ops.decode_n_splits(bufs.max_ctx), a_part_o=bufs.part_o,
                      a_part_ml=bufs.part_ml, a_counters=bufs.attn_cnt, a_row_table=bufs.row_table)
+            if ops.env_flag("VWA_CHAIN_PLAN"):
+                # the attention partition is the same for every layer of a step: layer 0's launch
+                # writes each workgroup's item, layers 1.. read it (mq_attention.h step plan)
+                if getattr(bufs, "attn_plan", None) is None:
+                    bufs.attn_plan = torch.zeros(1024 * 16, dtype=torch.int32, device=self.device)
+                a.update(a_plan=bufs.attn_plan, a_plan_mode=1 if li == 0 else 2)
         f8 = isinstance(L.o, ops.FP8Weight)
         tiled = f8 or isinstance(L.o, ops.TiledWeight)
         wsel = (lambda w: w.w8) if f8 else (lambda w: w.t) if tiled else (lambda w: w)  # noqa: E731

@@ -129,6 +129,7 @@ class Settings(BaseModel):
     VWA_CHAIN_RETRY: bool = Field(True, description="re-arm the chain after a barrier-timeout fallback")
     VWA_CHAIN_ASR: bool = Field(False, description="chained Whisper decoder launches (measured slower; off)")
     VWA_CHAIN_GRID_DIV: Optional[str] = Field(None, description="chained launch on CUs / k workgroups (shared GPU)")
+    VWA_CHAIN_PLAN: bool = Field(True, description="chained attention: layer 0 writes the step's work plan, layers 1.. read it")
     VWA_CHAIN_SCHED: Optional[str] = Field(None, description="DIAGNOSTIC: chained schedule override name=value,...")
     VWA_GEMM_QKV: bool = Field(True, description="> 16-row QKV: rotary + KV write in the tiled GEMM epilogue")
     VWA_GEMM_P8: Optional[str] = Field(None, description="DIAGNOSTIC: 256x256 8-phase GEMM eligibility override")
