@@ -547,6 +547,10 @@ void chain_schedule(ChainParams& cp) {
   // o_proj in 32-column tiles: one epilogue per workgroup (1 row 102.3 / 102.1 vs 103.5 / 103.0 us,
   // 4 rows 107.0 vs 107.5 us per layer, profiles/r5_chain_o_nt2.jsonl)
   cp.o_nt2 = 1;
+  // 5..16 rows: the X-streaming down projection in 32-column tiles, half the X bytes per weight
+  // byte -- 8 / 13 / 16 rows 107.8 / 113.8 / 117.1 vs 110.4 / 119.0 / 125.4 us per layer
+  // (profiles/r5_chain_d_nt2.jsonl)
+  cp.d_nt2 = 1;
   // diagnostic override of the schedule (tools/chain_probe.py A/B runs): "name=value,..."
   if (const char* e = std::getenv("VWA_CHAIN_SCHED")) {
     std::string s(e);
@@ -571,6 +575,7 @@ void chain_schedule(ChainParams& cp) {
         else if (k == "xw_late") cp.xw_late = v;
         else if (k == "poll_free") cp.poll_free = v;
         else if (k == "o_nt2") cp.o_nt2 = v;
+        else if (k == "d_nt2") cp.d_nt2 = v;
       }
       at = end + 1;
     }
@@ -712,6 +717,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   // (bit 24 of the returned LDS size: the down phase streams X with the weights, bit 25: fp8
   // weights, bit 26: o_proj in 32-column tiles -- chain_run launches that instantiation)
   return {host.to(h.device()), (int64_t)lds | (cp.n >= 3 && cp.ph[2].xg ? (int64_t)1 << 24 : 0) |
+                                    (cp.d_nt2 ? (int64_t)1 << 27 : 0) |
                                     (s_o.has_value() ? (int64_t)1 << 25 : 0) | (cp.o_nt2 ? (int64_t)1 << 26 : 0)};
 }
 
@@ -810,7 +816,8 @@ void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like, int64_t 
   // one workgroup per CU: the barrier needs every workgroup resident
   check_rc(vwa_chain_launch(reinterpret_cast<const ChainParams*>(desc.data_ptr()), (int)seq, (int)n_phases, (int)attn_g,
                             (int)(lds & 0xFFFFFF), chain_grid(like.device().index()), cur_stream(like),
-                            (int)((lds >> 24) & 1), (int)((lds >> 25) & 1), (int)((lds >> 26) & 1)),
+                            (int)((lds >> 24) & 1) * (((lds >> 27) & 1) ? 2 : 1), (int)((lds >> 25) & 1),
+                            (int)((lds >> 26) & 1)),
            "chain");
 }
 

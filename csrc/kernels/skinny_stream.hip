@@ -852,7 +852,8 @@ VWA_DEVICE PhaseRange chain_range(const ChainPhase& ph, int wb0 = 0, int wn = 0)
 // fragments in registers (v_cvt_scalef32_pk_bf16_fp8) -- W8A16, half the weight bytes
 template <int NT, int U, int WA, int R, bool XG = false, bool F8 = false>
 VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[R], int it, const PhaseRange& r, bool wx = true) {
-  static_assert(XG ? (NT == 1 && U == 2 && R == 16 && !F8) : NT * U * (F8 ? 2 : 4) == R,
+  // (XG: the weights in registers 0 .. 4 NT U - 1, the X fragments from register 8)
+  static_assert(XG ? (NT * U * 4 <= 8 && 8 + U * 4 <= R && !F8) : NT * U * (F8 ? 2 : 4) == R,
                 "an item fills its register set");
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.W), (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
@@ -906,7 +907,7 @@ VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[R], int it
 // the X fragments (registers 8..15) of an XG item whose weights went out before the barrier wait
 template <int U, int R>
 VWA_DEVICE void chain_load_x(const SkinnyParams& p, int nb, uint4 (&wr)[R], int it, const PhaseRange& r) {
-  static_assert(U == 2 && R == 16, "XG items: 8 weight + 8 X registers");
+  static_assert(8 + U * 4 <= R, "XG items: weight registers 0..7, X fragments from register 8");
   const __amdgpu_buffer_rsrc_t rxg =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.X), (short)0, (int)((size_t)p.M * p.ldx * 2), 0x00020000);
   const int lane = threadIdx.x & 63, nl = lane & 15, g = lane >> 4;
@@ -964,14 +965,16 @@ struct ChainShape {
   static constexpr int R = KS == 16 ? 8 : 16;
 };
 
-// W2: a plain phase in 32-column tiles (the chained o_proj, ChainParams::o_nt2)
+// W2: a plain phase in 32-column tiles (the chained o_proj, ChainParams::o_nt2; the X-streaming
+// down projection, ChainParams::d_nt2: one k-group of two tiles per item, every X fragment feeds
+// both -- half the X bytes per weight byte)
 template <int EPI, int KS = 8, bool XG = false, bool F8 = false, bool W2 = false>
 struct PhaseShape {
   static constexpr int NT = (EPI == EPI_SWIGLU || W2) ? 2 : 1;
   // (measured: QKV in half-tile units -- 384 tiles -> 3 units per workgroup, one split tile each --
   // 12.5-13.4 us vs 6.7 median / 11.5 max with whole tiles, also with the split tile processed
   // first and published before the next item's loads under a counted vmcnt)
-  static constexpr int U = XG ? 2 : ChainShape<KS>::R / 4 / NT * (F8 ? 2 : 1);
+  static constexpr int U = XG ? (W2 ? 1 : 2) : ChainShape<KS>::R / 4 / NT * (F8 ? 2 : 1);
 };
 
 // the phase's first weight item (and with pre2 its second) before the barrier wait: a
@@ -1291,7 +1294,8 @@ struct SeqEpi {
 // XG2: phase 2 (the down projection) streams its X fragments with the weights (ChainParams
 // ph[2].xg: more rows than its X fits LDS, 5..16 rows, no attention phase)
 // O2: phase 0 (o_proj) in 32-column tiles (ChainParams::o_nt2)
-template <int KS, int SEQ, int NPH, int AG, int WA, bool XG2 = false, bool F8 = false, bool O2 = false>
+// D2: the X-streaming down projection (XG2) in 32-column tiles (ChainParams::d_nt2)
+template <int KS, int SEQ, int NPH, int AG, int WA, bool XG2 = false, bool F8 = false, bool O2 = false, bool D2 = false>
 __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __restrict__ cpp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ChainParams& cp = *cpp;  // device-resident descriptor
@@ -1472,7 +1476,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   stamp();
   if constexpr (NPH >= 3) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
-    if ((!stg && prew) || XG2) chain_issue_first<E2, KS, WA, XG2, F8>(cp.ph[2], A, B, preb_of(2));  // (XG2: no staging wave)
+    if ((!stg && prew) || XG2) chain_issue_first<E2, KS, WA, XG2, F8, D2>(cp.ph[2], A, B, preb_of(2));  // (XG2: no staging wave)
     // phase 2's LDS item (down projection): its item 2 streams through the barrier window too
     // (phase 1's LDS use ended at the arrival's __syncthreads; the region lies above phase 2's
     // X rows and scratch, which the staging wave fills after the release)
@@ -1481,7 +1485,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
           cp.ph[2].p, cp.ph[2].nb, chain_range<KS>(cp.ph[2]), 2, smem + cp.lds_item2);
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
-    chain_phase<E2, KS, WA, XG2, F8>(cp, 2, A, B, smem, preb_of(2), 0, 0, 0, prew || XG2);
+    chain_phase<E2, KS, WA, XG2, F8, D2>(cp, 2, A, B, smem, preb_of(2), 0, 0, 0, prew || XG2);
     stamp();
     if (SEQ == 0 && tpr) {
       chain_tp_reduce(cp, 1, e0 + 2, bar, nwg, bar_next);
@@ -1538,17 +1542,19 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     if (i > 0 && f8 != (cp->ph[0].p.w_scale != nullptr)) return -10;
     const int max_rows = (cp->seq == 0 && cp->attn_g == 0 && !f8) ? 16 : 4;
     if (p.M < 1 || p.M > max_rows || p.K % 128 != 0 || p.N % (16 * ph.nt) != 0) return -10;
-    const size_t scratch = (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float);
     const size_t xrows = ((size_t)p.M * (p.K + 8) * 2 + 15) & ~(size_t)15;
     ph.xg = 0;
-    if (xrows + scratch > 160 * 1024) {
+    if (xrows + (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float) > 160 * 1024) {
       if (!(cp->seq == 0 && i == 2 && ph.epi == EPI_RESID && p.w_tiled && p.fuse_rms == 0)) return -10;
       ph.xg = 1;
     }
     // (X streaming has only the attention-less instantiation: a 70B down projection at 3-4 rows
     // -- 28672-wide X rows -- is chained with the decode attention as its own launch instead)
     if (ph.xg && (f8 || cp->attn_g > 0)) return -10;
-    const int U = ph.xg ? 2 : R / 4 / ph.nt * (f8 ? 2 : 1);
+    if (ph.xg && cp->d_nt2 && p.N % 32 == 0) ph.nt = 2;
+    if (i == 2 && !(ph.xg && ph.nt == 2)) cp->d_nt2 = 0;  // (d_nt2 does not apply: the plain instantiation)
+    const size_t scratch = (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float);
+    const int U = ph.xg ? (ph.nt == 2 ? 1 : 2) : R / 4 / ph.nt * (f8 ? 2 : 1);
     if ((size_t)p.N * p.K * 2 >= 0x7FFFFFF0ull || (size_t)p.M * p.ldx * 2 >= 0x7FFFFFF0ull) return -10;
     const int G = p.K / 128;
     const int per_wave = (G + KS - 1) / KS;
@@ -1558,7 +1564,9 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     // a tile may straddle at most two workgroup ranges (two partial slots per tile): every
     // non-empty range (floor or ceil of units / grid units, >= 1) must hold >= nb - 1 units
     const long long min_range = units / grid > 0 ? units / grid : 1;
-    if (ph.nb > 1 && min_range < ph.nb - 1) return -10;
+    // (equal ranges that divide a tile's units also split each tile over exactly two workgroups)
+    const bool aligned = units % grid == 0 && ph.nb % min_range == 0 && ph.nb / min_range <= 2;
+    if (ph.nb > 1 && min_range < ph.nb - 1 && !aligned) return -10;
     if (ntiles > cp->max_tiles || (size_t)ntiles * 2 * p.M * 16 * ph.nt > (size_t)cp->part_floats) return -10;
     const size_t need = (ph.xg ? 0 : xrows) + scratch;  // X rows + scales, means, flag
     if (need > lds) lds = need;
@@ -1627,8 +1635,14 @@ extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, 
   }
   if (xg2) {  // Llama tail of 5..16 rows: down projection with X from L2, no attention phase
     if (seq != 0 || attn_g != 0 || f8 || (n_phases != 3 && n_phases != 4)) return -10;
-    if (n_phases == 4) hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
-    else hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+    if (xg2 == 2) {  // (d_nt2: 32-column down tiles)
+      if (n_phases == 4) hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, 0, true, false, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+      else hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, 0, true, false, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+    } else if (n_phases == 4) {
+      hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+    } else {
+      hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+    }
     return (int)hipGetLastError();
   }
 #define VWA_CHAIN_LAUNCH(S, N, G) \

@@ -139,6 +139,7 @@ struct ChainParams {
   int xw_late;    // (xwait) the weights go out after the row scales, not before
   int poll_free;  // wave 0 (the barrier poller) issues nothing ahead of a barrier wait
   int o_nt2;      // attention launches: phase 0 (o_proj) in 32-column tiles (host request; prepare clears it when unused)
+  int d_nt2;      // 5..16 rows: the X-streaming down projection in 32-column tiles (host request; cleared when unused)
   ChainTP tp;
 };
 

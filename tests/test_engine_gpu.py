@@ -466,11 +466,15 @@ def test_chain_is_rearmed_after_backoff(monkeypatch):
         assert err < 0.02 * (1 + b.abs().max().item()), err
 
 
-def test_chained_layer_tail_5_to_16_rows(monkeypatch):
+@pytest.mark.parametrize("sched", ["", "d_nt2=1", "d_nt2=0"])
+def test_chained_layer_tail_5_to_16_rows(sched, monkeypatch):
     """Steps of 5..16 rows on the chained launch (VWA_CHAIN_MAX_ROWS): no attention phase, the
     down projection streaming its X fragments with the weights (its 14336-wide rows do not fit LDS
-    above 5 rows: ChainPhase::xg) -- against the per-kernel path on 8B-shaped layers."""
+    above 5 rows: ChainPhase::xg), in 16- and 32-column tiles (ChainParams::d_nt2) -- against the
+    per-kernel path on 8B-shaped layers."""
     ops.ext()
+    if sched:
+        monkeypatch.setenv("VWA_CHAIN_SCHED", sched)
     cfg = LlamaConfig(name="t8x", vocab_size=4096, hidden=4096, n_layers=2, n_heads=32, n_kv_heads=8, head_dim=128,
                       ffn=14336, max_pos=2048)
     torch.manual_seed(1)
@@ -497,6 +501,8 @@ def test_chained_layer_tail_5_to_16_rows(monkeypatch):
     assert not model.chain_error()
     descs = [v for v in model.chain_descs() if v is not None]
     assert any((v[2] >> 24) & 1 for v in descs), "no descriptor streams X with the weights"
+    if sched:
+        assert any((v[2] >> 27) & 1 for v in descs) == (sched == "d_nt2=1")
     for a, b in zip(got, ref):
         err = (a - b).abs().max().item()
         assert err < 0.02 * (1 + b.abs().max().item()), err
