@@ -160,7 +160,14 @@ class LLMIntentEngine:
         if forced:
             r.matcher.accept_bytes(forced)
             r.out += forced
-            ftoks = self.tok.encode(forced.decode("ascii"))
+            # the grammar forces a small set of strings (JSON syntax, keys, enum values): their
+            # standalone encodings are cached (a tokenizer call is ~9 us, 1-2 per sampled token)
+            cache = self.__dict__.setdefault("_forced_ids", {})
+            ftoks = cache.get(forced)
+            if ftoks is None:
+                ftoks = self.tok.encode(forced.decode("ascii"))
+                if len(cache) < 8192:
+                    cache[forced] = ftoks
             r.forced += len(ftoks)
             r.feed += ftoks
 
