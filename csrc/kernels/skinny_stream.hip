@@ -933,7 +933,7 @@ VWA_DEVICE void chain_load_x(const SkinnyParams& p, int nb, uint4 (&wr)[R], int 
 // F8: the fp8 tiled item (chain_load F8: two 1 KB loads per k-group, register (nt * U + u) * 2 + s2)
 template <int NT, int U, int WA, bool F8 = false>
 VWA_DEVICE void chain_preload(const SkinnyParams& p, int nb, const PhaseRange& r, int it, char* dst) {
-  static_assert(NT * U == (F8 ? 8 : 4), "an item = 16 loads of 1 KB per wave");
+  static_assert(NT * U * (F8 ? 2 : 4) <= 16, "an item = at most 16 loads of 1 KB per wave (16 KB of LDS)");
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.W), (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
   const unsigned lane = threadIdx.x & 63;
@@ -959,10 +959,12 @@ VWA_DEVICE void chain_preload(const SkinnyParams& p, int nb, const PhaseRange& r
 }
 
 // loads per weight item (register set): 16 with 8 waves per workgroup, 8 with 16 waves (a wave's
-// VGPR budget halves with twice the waves)
-template <int KS>
+// VGPR budget halves with twice the waves).  fp8 (W8A16) items: 8 loads -- with 16 the fp8
+// instantiations ran out of VGPRs at the barrier pre-issue (each new weight register spilled to
+// scratch behind an s_waitcnt vmcnt(0): the item's loads serialised)
+template <int KS, bool F8 = false>
 struct ChainShape {
-  static constexpr int R = KS == 16 ? 8 : 16;
+  static constexpr int R = (KS == 16 || F8) ? 8 : 16;
 };
 
 // W2: a plain phase in 32-column tiles (the chained o_proj, ChainParams::o_nt2; the X-streaming
@@ -974,7 +976,7 @@ struct PhaseShape {
   // (measured: QKV in half-tile units -- 384 tiles -> 3 units per workgroup, one split tile each --
   // 12.5-13.4 us vs 6.7 median / 11.5 max with whole tiles, also with the split tile processed
   // first and published before the next item's loads under a counted vmcnt)
-  static constexpr int U = XG ? (W2 ? 1 : 2) : ChainShape<KS>::R / 4 / NT * (F8 ? 2 : 1);
+  static constexpr int U = XG ? (W2 ? 1 : 2) : ChainShape<KS, F8>::R / 4 / NT * (F8 ? 2 : 1);
 };
 
 // the phase's first weight item (and with pre2 its second) before the barrier wait: a
@@ -1242,7 +1244,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
   auto ldi = [&](uint4 (&wr)[R], int idx) {
     if (idx == 2 && ((i == 1 && cp.lds_item && w < cp.lds_item_waves) ||
                      (i == 2 && cp.lds_item2 && w < cp.lds_item2_waves && !(cp.poll_free && w == 0)))) {  // preloaded (chain_preload)
-      static_assert(R == 16, "LDS item: 16 loads of 1 KB per wave");
+      static_assert(R <= 16, "LDS item: up to 16 loads of 1 KB per wave");
       // this wave's LDS-DMA of the item must have landed (no barrier drains vmcnt any more, and
       // the compiler does not order LDS-DMA writes before these reads)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1318,7 +1320,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
         : "s"(cpp));
     if (junk == 0x9e3779b9u) __builtin_amdgcn_s_sleep(1);
   }
-  uint4 A[ChainShape<KS>::R], B[ChainShape<KS>::R];
+  uint4 A[ChainShape<KS, F8>::R], B[ChainShape<KS, F8>::R];
   // barrier = arrive (stores drained), issue the next phase's first weight item, then wait: the
   // weight stream is in flight while the slowest workgroup finishes
   const int nwg = (int)gridDim.x;
@@ -1554,7 +1556,7 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
     if (ph.xg && cp->d_nt2 && p.N % 32 == 0) ph.nt = 2;
     if (i == 2 && !(ph.xg && ph.nt == 2)) cp->d_nt2 = 0;  // (d_nt2 does not apply: the plain instantiation)
     const size_t scratch = (size_t)(KS * ph.nt * 4 * 64 + 48) * sizeof(float);
-    const int U = ph.xg ? (ph.nt == 2 ? 1 : 2) : R / 4 / ph.nt * (f8 ? 2 : 1);
+    const int U = ph.xg ? (ph.nt == 2 ? 1 : 2) : (f8 ? ChainShape<KS, true>::R : R) / 4 / ph.nt * (f8 ? 2 : 1);
     if ((size_t)p.N * p.K * 2 >= 0x7FFFFFF0ull || (size_t)p.M * p.ldx * 2 >= 0x7FFFFFF0ull) return -10;
     const int G = p.K / 128;
     const int per_wave = (G + KS - 1) / KS;
