@@ -551,6 +551,9 @@ void chain_schedule(ChainParams& cp) {
   // byte -- 8 / 13 / 16 rows 107.8 / 113.8 / 117.1 vs 110.4 / 119.0 / 125.4 us per layer
   // (profiles/r5_chain_d_nt2.jsonl)
   cp.d_nt2 = 1;
+  // the QKV phase's two items go out at the down -> QKV barrier (half the workgroups take two of its
+  // 384 tiles): 100.96 / 100.84 vs 101.38 / 101.57 us (profiles/r5_chain_pre_mask.jsonl)
+  cp.pre_mask = 8;
   // diagnostic override of the schedule (tools/chain_probe.py A/B runs): "name=value,..."
   if (const char* e = std::getenv("VWA_CHAIN_SCHED")) {
     std::string s(e);
