@@ -291,3 +291,29 @@ def test_batched_admission_prefill_matches_serial_prefill():
     eC.prefill_batch([(s, len(s.tokens)) for s in sC[1:3]])  # 60 rows: one step-bucket forward
     for a, b in zip(next_logits(eC, sC[1:3]), want[1:3]):
         assert torch.allclose(a, b, atol=2e-2, rtol=2e-2), (a - b).abs().max()
+
+
+def test_rms_statistics_handoff_paths_without_the_tiled_gemm():
+    """ops.linear's RMS-statistics arguments (GemmParams::ss_*, used by the > 16-row GPU path)
+    keep their meaning on paths without the hand-off: ss_out gets the squares of the stored rows
+    added, ss_zero is cleared, ss_in is ignored (the consumer computes its own 1/rms)."""
+    import voice_enabled_browser_automation_amd.ops as ops
+
+    torch.manual_seed(0)
+    M, K, N = 20, 256, 128
+    x, h = torch.randn(M, K).to(torch.bfloat16), torch.randn(M, N).to(torch.bfloat16)
+    w = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
+    ss = torch.full((2, 64), 3.0)
+    ss[0].zero_()
+    out = h.clone()
+    ops.linear(x, w, out=out, residual=out, ss_out=ss[0], ss_zero=ss[1])
+    assert torch.all(ss[1] == 0)
+    torch.testing.assert_close(ss[0, :M], out.float().pow(2).sum(-1), rtol=1e-5, atol=1e-3)
+    assert torch.all(ss[0, M:] == 0)
+    ref = h.clone()
+    ops.linear(x, w, out=ref, residual=ref)
+    assert torch.equal(out, ref)
+    gu = ops.interleave_gate_up((torch.randn(64, N) * 0.05).to(torch.bfloat16), (torch.randn(64, N) * 0.05).to(torch.bfloat16))
+    a = ops.linear_swiglu(out, gu, fuse_rms=True, eps=1e-5, ss_in=ss[0])
+    b = ops.linear_swiglu(out, gu, fuse_rms=True, eps=1e-5)
+    assert torch.equal(a, b)
