@@ -28,6 +28,7 @@ import os
 import statistics
 import sys
 import time
+import zlib
 
 import numpy as np
 import torch
@@ -242,6 +243,8 @@ def main():
     # lengths), and the ranks of a TP group decode in lockstep
     utterances = [synth_speech(args.audio_s, seed=i) for i in range(8)]
 
+    last = {}
+
     def one(i: int):
         pcm = utterances[i % len(utterances)]
         t0 = time.perf_counter()
@@ -253,6 +256,7 @@ def main():
         out = brain.parse(req)
         ok = safe_parse(ParseResponse, out).success
         t1 = time.perf_counter()
+        last["text"], last["out"] = text, out
         return (t1 - t0) * 1e3, (t_asr - t0) * 1e3, ok
 
     drive_sessions(brain, tp, world, args.warmup, one)
@@ -262,8 +266,10 @@ def main():
         r = one(i)
         stats = dict(brain.last_stats)
         if args.verbose and rank == 0:
+            # (crc32 of the transcript and of the intent JSON: run-to-run reproducibility checks)
             print(json.dumps({"step": i - args.warmup, "latency_ms": round(r[0], 2), "asr_ms": round(r[1], 2),
-                              **stats}), flush=True)
+                              "text_crc": zlib.crc32(str(last.get("text")).encode()),
+                              "out_crc": zlib.crc32(str(last.get("out")).encode()), **stats}), flush=True)
         return r + (stats,)
 
     res_steps, elapsed = drive_sessions(brain, tp, world, args.steps, timed_one, start=args.warmup)

@@ -969,3 +969,4 @@ def test_rms_statistics_handoff(M, wdt):
         outs.append((q, kc, vc))
     for u, v in zip(*outs):
         close(u, v, 1e-2, 1e-2)
+

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tokens", type=int, default=40)
     ap.add_argument("--batch", default="", help="also time transcribe_many over B utterances (comma list)")
+    ap.add_argument("--modes", default="0,1", help="VWA_CHAIN_ASR values to time (0 per-kernel, 1 chained)")
     a = ap.parse_args()
     ops.ext()
     m = WhisperModel(get_config(a.asr), device="cuda", seed=0)
@@ -51,7 +52,7 @@ def main():
         return
     audio = None
     texts = {}
-    for chain in ("0", "1"):
+    for chain in a.modes.split(","):
         os.environ["VWA_CHAIN_ASR"] = chain
         m.reset_chains()
         eng = AsrEngine(m, load_tokenizer("whisper"), max_sessions=2)
@@ -71,7 +72,8 @@ def main():
                               total_ms=round(statistics.median(tot), 2),
                               decode_us_per_token=round(1e3 * statistics.median(dec) / a.tokens, 1),
                               chained=bool(m.chain_descs()))), flush=True)
-    print(json.dumps(dict(tool="asr_timing", same_text=texts["0"] == texts["1"])), flush=True)
+    if len(texts) == 2:
+        print(json.dumps(dict(tool="asr_timing", same_text=texts["0"] == texts["1"])), flush=True)
 
 
 if __name__ == "__main__":
