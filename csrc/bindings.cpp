@@ -202,23 +202,23 @@ int device_cus(const Tensor& t) {
 void set_ss(GemmParams& p, int64_t epi, const c10::optional<Tensor>& ss_out, const c10::optional<Tensor>& ss_zero,
             const c10::optional<Tensor>& ss_in, double eps) {
   auto chk = [&](const Tensor& t, const char* n) {
-    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() >= p.M, n,
-                ": f32 [>= M] contiguous GPU tensor");
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kLong && t.is_contiguous() && t.numel() >= p.M, n,
+                ": int64 [>= M] contiguous GPU tensor (u64 fixed point, 2^-16 units)");
   };
   if (ss_out.has_value()) {
     chk(*ss_out, "ss_out");
     TORCH_CHECK(epi == 1 && !p.y_f32, "ss_out: residual epilogue (bf16 rows) only");
-    p.ss_out = ss_out->data_ptr<float>();
+    p.ss_out = reinterpret_cast<unsigned long long*>(ss_out->data_ptr<int64_t>());
   }
   if (ss_zero.has_value()) {
     chk(*ss_zero, "ss_zero");
-    p.ss_zero = ss_zero->data_ptr<float>();
+    p.ss_zero = reinterpret_cast<unsigned long long*>(ss_zero->data_ptr<int64_t>());
     p.ss_zero_n = (int)ss_zero->numel();
   }
   if (ss_in.has_value()) {
     chk(*ss_in, "ss_in");
     TORCH_CHECK(p.rstd == nullptr, "ss_in replaces rstd");
-    p.ss_in = ss_in->data_ptr<float>();
+    p.ss_in = reinterpret_cast<const unsigned long long*>(ss_in->data_ptr<int64_t>());
     p.ss_eps = (float)eps;
   }
 }

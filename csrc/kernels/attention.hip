@@ -463,7 +463,6 @@ __global__ __launch_bounds__(256 * FlashCfg<D>::NS) void flash_attn_kernel(Flash
 
   // split s: tiles s, s + 2, ...; every split runs the same iteration count (block-wide barriers)
   constexpr int DEPTH = FC::DEPTH;
-  constexpr bool PRE = D == 64;  // all of a tile's LDS fragments in registers at once (D = 128: no room)
   const int iters = (nt + NS - 1) / NS;
   if (split < nt) {
     load_tile(split * kFK, kra, vra);
@@ -481,28 +480,10 @@ __global__ __launch_bounds__(256 * FlashCfg<D>::NS) void flash_attn_kernel(Flash
       const int k0 = t * kFK;
       const unsigned char* kimg = simg + (2 * (it & 1)) * IMG;
       const unsigned char* vimg = kimg + IMG;
-      // ---- every LDS fragment of the tile requested up front (D = 64: 64 VGPRs of K and V^T
-      // fragments), so no MFMA waits on a read issued right before it (the compiler-scheduled
-      // form waited lgkmcnt(0) before each P.V MFMA)
-      uint4 kf[2][NDS];
-      uint2 vf[2][2][NDT][2];
-      if constexpr (PRE) {
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int ds = 0; ds < NDS; ++ds)
-            kf[kk][ds] = *reinterpret_cast<const uint4*>(kimg + FC::off(32 * kk + a_key, 2 * ds + hf));
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-            for (int dt = 0; dt < NDT; ++dt) {
-              const int kr0 = 32 * kk + 16 * ks + v_key, ch = 4 * dt + v_ch;
-              vf[kk][ks][dt][0] = lds_tr16(vimg + FC::off(kr0, ch) + v_sub);
-              vf[kk][ks][dt][1] = lds_tr16(vimg + FC::off(kr0 + 4, ch) + v_sub);
-            }
-      }
+      // (LDS fragments are read next to their MFMAs.  A D = 64 form that requested all of a tile's
+      // K and V^T fragments up front -- 64 VGPRs -- gave results that varied by 1-2 bf16 ulps from
+      // run to run (tools/repro_ops.py: 5 variants in 5 runs of the same inputs) and was no faster
+      // end to end: Whisper-large-v3 encoder 3.14-3.35 vs 3.37-3.52 ms; removed)
       // ---- S^T = K.Q^T
       f32x16 s[2];
 #pragma unroll
@@ -512,7 +493,7 @@ __global__ __launch_bounds__(256 * FlashCfg<D>::NS) void flash_attn_kernel(Flash
         const int row = 32 * kk + a_key;
 #pragma unroll
         for (int ds = 0; ds < NDS; ++ds) {
-          const uint4 a = PRE ? kf[kk][ds] : *reinterpret_cast<const uint4*>(kimg + FC::off(row, 2 * ds + hf));
+          const uint4 a = *reinterpret_cast<const uint4*>(kimg + FC::off(row, 2 * ds + hf));
           s[kk] = mfma32(as_bf16x8(a), qf[ds], s[kk]);
         }
       }
@@ -569,8 +550,8 @@ __global__ __launch_bounds__(256 * FlashCfg<D>::NS) void flash_attn_kernel(Flash
 #pragma unroll
           for (int dt = 0; dt < NDT; ++dt) {
             const int ch = 4 * dt + v_ch;
-            const uint2 lo = PRE ? vf[kk][ks][dt][0] : lds_tr16(vimg + FC::off(kr0, ch) + v_sub);
-            const uint2 hi = PRE ? vf[kk][ks][dt][1] : lds_tr16(vimg + FC::off(kr0 + 4, ch) + v_sub);
+            const uint2 lo = lds_tr16(vimg + FC::off(kr0, ch) + v_sub);
+            const uint2 hi = lds_tr16(vimg + FC::off(kr0 + 4, ch) + v_sub);
             oacc[dt] = mfma32(as_bf16x8(make_uint4(lo.x, lo.y, hi.x, hi.y)), pb[ks], oacc[dt]);
           }
         }

@@ -296,10 +296,16 @@ VWA_DEVICE void p8_mfma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2], const bf16x
 
 VWA_DEVICE float bias_at(const GemmParams& p, int n) { return p.bias ? bf2f(p.bias[n]) : 0.f; }
 
+// RMS statistics hand-off (GemmParams::ss_*): sums of squares in u64 fixed point, 2^-16 units
+constexpr double kSsScale = 65536.0;
+VWA_DEVICE unsigned long long ss_fix(float sq) {
+  return (unsigned long long)fminf(sq * (float)kSsScale, 1.8e19f);  // (>= 0; clamped below 2^64)
+}
+
 // per-row RMSNorm scale: rstd[m], or from the handed-off sum of squares (ss_in), or 1
 VWA_DEVICE float row_scale(const GemmParams& p, int m) {
   if (p.rstd) return p.rstd[m];
-  if (p.ss_in) return rsqrtf(p.ss_in[m] / (float)p.K + p.ss_eps);
+  if (p.ss_in) return rsqrtf((float)((double)p.ss_in[m] * (1.0 / kSsScale)) / (float)p.K + p.ss_eps);
   return 1.f;
 }
 
@@ -457,13 +463,14 @@ VWA_DEVICE float finish_item(const GemmParams& p, int m, int c, const float (&a)
 
 // ss_out[m] += sq summed over the wave's lanes of each row (lanes with m < 0 add nothing): one
 // atomic per row per wave when the wave lies in one row, else one per lane
-VWA_DEVICE void ss_add(float* ss_out, int m, float sq) {
+VWA_DEVICE void ss_add(unsigned long long* ss_out, int m, float sq) {
   const int m0 = __builtin_amdgcn_readfirstlane(m);
   if (__ballot(m != m0) == 0ull) {
     sq = wave_sum(sq);
-    if (lane_id() == 0 && m0 >= 0) __hip_atomic_fetch_add(gp(ss_out + m0), sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane_id() == 0 && m0 >= 0)
+      __hip_atomic_fetch_add(gp(ss_out + m0), ss_fix(sq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else if (m >= 0) {
-    __hip_atomic_fetch_add(gp(ss_out + m), sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(gp(ss_out + m), ss_fix(sq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -495,7 +502,7 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
   // XCD-aware: logical tile order is column-block major, so consecutive logical tiles (same XCD)
   // share the column block's weight tile in L2
   if (p.ss_zero && blockIdx.x == 0)
-    for (int i = threadIdx.x; i < p.ss_zero_n; i += C::THREADS) p.ss_zero[i] = 0.f;
+    for (int i = threadIdx.x; i < p.ss_zero_n; i += C::THREADS) p.ss_zero[i] = 0ull;
   const int lt = xcd_remap((int)(blockIdx.x % tiles), tiles);
   const int bn = (lt / mb) * C::BN, bm = (lt % mb) * C::BM;
   const int KG = p.K / BKG;
@@ -743,7 +750,7 @@ __global__ __launch_bounds__(C::THREADS, C::NW == 4 ? 2 : 1) void gemm_kernel(Ge
 #pragma unroll
       for (int o = 1; o < CPR; o <<= 1) sq += __shfl_xor(sq, o, 64);  // the CPR lanes of one row
       if (ch == 0 && m < p.M && cbase < ncols)
-        __hip_atomic_fetch_add(gp(p.ss_out + m), sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(gp(p.ss_out + m), ss_fix(sq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

@@ -171,10 +171,14 @@ struct GemmParams {
   uint16_t* q_out; int ldq; uint16_t* k_cache; uint16_t* v_cache; int block_size;
   int64_t cache_sb, cache_sh, cache_st;
   // RMS statistics hand-off (decode steps of > 16 rows, one rank): ss_out -- the residual epilogue
-  // adds the squares of its bf16 output rows into ss_out[m] (the next RMSNorm's statistics, f32
-  // atomics); ss_zero[0, ss_zero_n) is zeroed by workgroup 0 (the other buffer, already consumed);
-  // ss_in -- the per-row scale is rsqrt(ss_in[m] / K + ss_eps) instead of rstd[m] (no row_rstd launch)
-  float* ss_out; float* ss_zero; int ss_zero_n; const float* ss_in; float ss_eps;
+  // adds the squares of its bf16 output rows into ss_out[m] (the next RMSNorm's statistics);
+  // ss_zero[0, ss_zero_n) is zeroed by workgroup 0 (the other buffer, already consumed); ss_in --
+  // the per-row scale is rsqrt(ss_in[m] / K + ss_eps) instead of rstd[m] (no row_rstd launch).
+  // The sums are u64 fixed point in units of 2^-16 (kSsScale): integer atomics add in any order
+  // to the same bits, so the statistics -- and every token after them -- are run-to-run
+  // reproducible (f32 atomics were not: tools/repro_check.py)
+  unsigned long long* ss_out; unsigned long long* ss_zero; int ss_zero_n; const unsigned long long* ss_in;
+  float ss_eps;
 };
 
 struct FlashAttnParams {

@@ -645,3 +645,33 @@ def test_batched_admission_prefill_gpu(flash, monkeypatch):
     for a, b in zip(got, want):
         assert torch.isfinite(a).all()
         assert torch.allclose(a, b, atol=3e-2, rtol=3e-2), (a - b).abs().max()
+
+
+def test_intent_parses_and_transcripts_are_reproducible():
+    """Same weights, inputs and sampler seed -> the same bits from two fresh engines: the
+    many-row RMS statistics add as integers (GemmParams::ss_*), every split reduction sums in a
+    fixed order, and the flash-attention form whose results moved by an ulp from run to run is
+    gone (tools/repro_check.py / repro_ops.py found both)."""
+    from voice_enabled_browser_automation_amd.brain.intent_engine import LLMIntentEngine
+    from voice_enabled_browser_automation_amd.models.config import LLAMA_PRESETS
+
+    ops.ext()
+    m = LlamaModel(LLAMA_PRESETS["llama-tiny"], device="cuda", seed=4)
+    texts = ["search wireless earbuds on the first page of results", "scroll down", "sort by price", "go back"]
+    outs = []
+    for _ in range(2):
+        eng = LLMEngine(m, max_seqs=4, max_model_len=2048)
+        eng.capture_all()
+        ie = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=200, temperature=0.1, seed=7)
+        outs.append(ie.parse_many([{"text": t, "context": {}} for t in texts]))
+        m.reset_chains()
+    assert outs[0] == outs[1]
+    w = WhisperModel(get_config("whisper-tiny"), device="cuda", seed=1)
+    asr = AsrEngine(w, load_tokenizer("whisper"), max_sessions=2)
+    g = torch.Generator().manual_seed(3)
+    audio = (torch.randn(16000 * 5, generator=g) * 0.1).to("cuda")
+    mel = w.mel_batch([audio])
+    enc = [w.encode(mel).clone() for _ in range(3)]
+    assert all(torch.equal(enc[0], e) for e in enc[1:])
+    toks = [asr.decode_many([audio], exact_tokens=24)[0] for _ in range(2)]
+    assert toks[0] == toks[1]

@@ -303,12 +303,12 @@ def test_rms_statistics_handoff_paths_without_the_tiled_gemm():
     M, K, N = 20, 256, 128
     x, h = torch.randn(M, K).to(torch.bfloat16), torch.randn(M, N).to(torch.bfloat16)
     w = (torch.randn(N, K) * 0.05).to(torch.bfloat16)
-    ss = torch.full((2, 64), 3.0)
+    ss = torch.full((2, 64), 3, dtype=torch.int64)  # (u64 fixed point, ops.SS_SCALE units)
     ss[0].zero_()
     out = h.clone()
     ops.linear(x, w, out=out, residual=out, ss_out=ss[0], ss_zero=ss[1])
     assert torch.all(ss[1] == 0)
-    torch.testing.assert_close(ss[0, :M], out.float().pow(2).sum(-1), rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(ops.ss_float(ss[0, :M]).float(), out.float().pow(2).sum(-1), rtol=1e-5, atol=1e-3)
     assert torch.all(ss[0, M:] == 0)
     ref = h.clone()
     ops.linear(x, w, out=ref, residual=ref)

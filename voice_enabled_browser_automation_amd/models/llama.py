@@ -210,7 +210,8 @@ class LlamaModel:
                 not ops.env_flag("VWA_RMS_HANDOFF"):
             return None
         if getattr(self, "_ss", None) is None:
-            self._ss = torch.zeros(2, 4096, dtype=torch.float32, device=self.device)
+            # (int64: u64 fixed-point sums, ops.SS_SCALE -- integer atomics keep them reproducible)
+            self._ss = torch.zeros(2, 4096, dtype=torch.int64, device=self.device)
         if M > self._ss.shape[1]:
             return None
         # (the residual GEMMs keep ss[0] zero between forwards; cleared here too, so an interrupted

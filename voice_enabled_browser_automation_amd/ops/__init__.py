@@ -542,8 +542,21 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         if ss_zero is not None:
             ss_zero.zero_()
         if ss_out is not None:
-            ss_out[: x.shape[0]] += out.float().pow(2).sum(-1)
+            ss_out[: x.shape[0]] += ss_fixed(out.float().pow(2).sum(-1))
     return out
+
+
+SS_SCALE = 65536.0  # RMS statistics hand-off: u64 fixed point in 2^-16 units (GemmParams::ss_*)
+
+
+def ss_fixed(sq: torch.Tensor) -> torch.Tensor:
+    """f32 sums of squares -> the hand-off's int64 fixed point (2^-16 units, truncated)."""
+    return (sq.float() * SS_SCALE).clamp(max=1.8e19).to(torch.int64)
+
+
+def ss_float(ss: torch.Tensor) -> torch.Tensor:
+    """The hand-off's fixed-point sums of squares -> f64 values."""
+    return ss.double() / SS_SCALE
 
 
 def _linear_impl(x, w, bias, out, residual, act, fuse_rms, eps, out_dtype, ln_c, col_mask, col_mask_off, mask_rows,
