@@ -62,7 +62,7 @@ void set_small_gemm_bytes(int64_t n) { g_small_bytes = (size_t)(n > 0 ? n : 0); 
 int skinny_ks(const SkinnyParams& p) { return g_ks ? g_ks : (p.K < 2048 && p.M <= 16 ? 4 : 8); }
 
 bool small_gemm(const SkinnyParams& p) {
-  return !p.w_scale && g_small_bytes && p.M <= 16 && ((size_t)p.N * p.K * 2 <= g_small_bytes || p.K < 1024);
+  return !p.w_scale && g_small_bytes && p.M <= 64 && ((size_t)p.N * p.K * 2 <= g_small_bytes || p.K < 1024);
 }
 
 int run_skinny(int epi, const SkinnyParams& p, hipStream_t st) {
@@ -86,7 +86,10 @@ SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<T
   check_contig_rows(x, "x");
   TORCH_CHECK(w.is_contiguous() && w.dim() == 2, "w must be contiguous [N, K]");
   TORCH_CHECK(x.size(1) == w.size(1), "K mismatch: x ", x.sizes(), " w ", w.sizes());
-  TORCH_CHECK(x.size(0) >= 1 && x.size(0) <= 16, "skinny_gemm supports 1..16 rows (more: the tiled GEMM), got ", x.size(0));
+  // (17..64 rows: the one-tile kernel only, small bf16 weights -- ops._small_rows)
+  TORCH_CHECK(x.size(0) >= 1 && x.size(0) <= 64, "skinny_gemm supports 1..64 rows (more: the tiled GEMM), got ", x.size(0));
+  TORCH_CHECK(x.size(0) <= 16 || (!w_scale.has_value() && !w_tiled),
+              "17..64 rows: bf16 row-major weights (the one-tile kernel) only");
   TORCH_CHECK(w.size(1) % 128 == 0, "K must be a multiple of 128");
   if (bias.has_value()) {
     check_bf16(*bias, "bias");
@@ -113,19 +116,20 @@ SkinnyParams base_params(const Tensor& x, const Tensor& w, const c10::optional<T
 // fp8 weights run only on the streaming kernel; a shape it cannot take is an error, never a
 // silent bf16 fallback (the Python layer routes those shapes to the dequantising path).
 int run_skinny_checked(int epi, const SkinnyParams& p, hipStream_t st) {
+  if (p.M > 16) return vwa_skinny_gemm(epi, &p, st);  // (17..64 rows: the one-tile kernel's MT row tiles)
   // pre-tiled weights (bf16 or fp8) exist only for the streaming kernel (a shape it rejects is an error)
   if (p.w_tiled) return vwa_skinny_stream(epi, &p, g_grid_cap, skinny_ks(p), st);
   if (p.w_scale || (p.fuse_rms == 2 && !small_gemm(p))) return vwa_skinny_stream(epi, &p, g_grid_cap, skinny_ks(p), st);
   return run_skinny(epi, p, st);
 }
 
-// Folded LayerNorm (fuse_rms = 2): bf16 weights, <= 16 rows; runs on the streaming kernel, or on
+// Folded LayerNorm (fuse_rms = 2): bf16 weights, <= 16 rows (17..64: the one-tile kernel); runs on the streaming kernel, or on
 // the one-tile kernel for the small GEMMs it takes (run_skinny_checked: small_gemm).
 void set_ln_fold(SkinnyParams& p, const c10::optional<Tensor>& ln_c, int epi) {
   if (!ln_c.has_value()) return;
   TORCH_CHECK(p.w_scale == nullptr, "folded LayerNorm needs bf16 weights");
   TORCH_CHECK(epi != 2, "folded LayerNorm is not supported with the SwiGLU epilogue");
-  TORCH_CHECK(p.M <= 16, "folded LayerNorm takes <= 16 rows");
+  TORCH_CHECK(p.M <= 64, "folded LayerNorm takes <= 64 rows (17..64: the one-tile kernel)");
   TORCH_CHECK(ln_c->is_cuda() && ln_c->scalar_type() == at::kFloat && ln_c->is_contiguous() && ln_c->numel() == p.N,
               "ln_c must be f32 [N]");
   p.fuse_rms = 2;

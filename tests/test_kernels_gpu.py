@@ -115,7 +115,7 @@ def _kv_setup(nq, nkv, hd, blocks=16, bs=16):
     return kc, vc
 
 
-@pytest.mark.parametrize("M", [1, 7, 70])
+@pytest.mark.parametrize("M", [1, 7, 40, 70])
 def test_qkv_rope_write(M, skinny_mode):
     nq, nkv, hd, K = 8, 2, 128, 512
     H = nq + 2 * nkv
@@ -139,11 +139,12 @@ def test_qkv_rope_write(M, skinny_mode):
 
 
 @pytest.mark.parametrize("small_bytes", [0, 4 << 20], ids=["stream", "one_tile"])
-@pytest.mark.parametrize("M", [1, 6, 16, 24])
+@pytest.mark.parametrize("M", [1, 6, 16, 24, 40, 64])
 def test_folded_layernorm_linear_and_qkv(M, small_bytes):
     """LayerNorm folded into the GEMM (mean/rstd from the streamed / staged rows) vs LayerNorm ->
     linear in f32, on the persistent streaming kernel and on the one-tile kernel small weights
-    are routed to (skinny_gemm.hip); 24 rows take the normalise-then-GEMM path.  Inputs carry a
+    are routed to (skinny_gemm.hip; 17..64 rows with small weights: its MT row tiles, one launch,
+    no LayerNorm kernel -- ops._small_rows).  Inputs carry a
     large mean (the residual stream's offset) to exercise the mean * rowsum correction."""
     ops.ext().set_small_gemm_bytes(small_bytes)
     try:

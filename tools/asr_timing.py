@@ -27,8 +27,12 @@ def main():
     ap.add_argument("--tokens", type=int, default=40)
     ap.add_argument("--batch", default="", help="also time transcribe_many over B utterances (comma list)")
     ap.add_argument("--modes", default="0,1", help="VWA_CHAIN_ASR values to time (0 per-kernel, 1 chained)")
+    ap.add_argument("--small-max-m", type=int, default=None,
+                    help="A/B: rows up to which small weights take the one-tile kernel (16: the tiled GEMM above 16)")
     a = ap.parse_args()
     ops.ext()
+    if a.small_max_m is not None:
+        ops.SMALL_MAX_M = a.small_max_m
     m = WhisperModel(get_config(a.asr), device="cuda", seed=0)
     if a.batch:  # concurrent sessions' batched pass (bench.py --concurrent: one per round)
         sizes = [int(x) for x in a.batch.split(",")]

@@ -47,11 +47,14 @@ class WhisperRunner:
         R = max(BUCKETS)
         i32 = dict(dtype=torch.int32, device=dev)
         b = RunnerBuffers()
-        b.tokens = torch.zeros(R, **i32)
-        b.positions = torch.zeros(R, **i32)
-        b.seq_ids = torch.zeros(R, **i32)
-        b.ctx_lens = torch.ones(R, **i32)
-        b.slots = torch.full((R,), -1, dtype=torch.int64, device=dev)
+        # one device block for a step's inputs (tokens | positions | seq_ids | ctx_lens | slots as
+        # int64) and its pinned mirror: ONE host->device copy per step (five separate copies were
+        # 7 % of the 32-session batched decode's GPU time, profiles/r4_asr_tiny_batch32_kernel_stats.md)
+        b.step_in = torch.zeros(6 * R, **i32)
+        b.tokens, b.positions, b.seq_ids, b.ctx_lens = (b.step_in[i * R : (i + 1) * R] for i in range(4))
+        b.slots = b.step_in[4 * R :].view(torch.int64)
+        b.ctx_lens.fill_(1)
+        b.slots.fill_(-1)
         b.block_table = torch.zeros(max_sessions, self.bps, **i32)
         for s in range(max_sessions):
             b.block_table[s] = torch.arange(1 + s * self.bps, 1 + (s + 1) * self.bps, dtype=torch.int32)
@@ -75,8 +78,11 @@ class WhisperRunner:
         b.cross_lens = torch.full((R,), cfg.n_audio_ctx, dtype=torch.int32, device=dev)
         self.b = b
         pin = dev.type == "cuda"
-        self.h_i32 = torch.zeros(4, R, dtype=torch.int32, pin_memory=pin)
-        self.h_slots = torch.full((R,), -1, dtype=torch.int64, pin_memory=pin)
+        self.h_in = torch.zeros(6 * R, dtype=torch.int32, pin_memory=pin)
+        self.h_i32 = self.h_in[: 4 * R].view(4, R)
+        self.h_slots = self.h_in[4 * R :].view(torch.int64)
+        self.h_i32[3].fill_(1)
+        self.h_slots.fill_(-1)
         if use_graphs is None:
             use_graphs = ops.env_flag("VWA_HIPGRAPH")
         self.use_graphs = bool(use_graphs) and dev.type == "cuda"
@@ -121,11 +127,7 @@ class WhisperRunner:
             hi[0, i], hi[1, i], hi[2, i], hi[3, i] = 0, 0, 0, 1
             self.h_slots[i] = -1
         b = self.b
-        b.tokens.copy_(hi[0], non_blocking=True)
-        b.positions.copy_(hi[1], non_blocking=True)
-        b.seq_ids.copy_(hi[2], non_blocking=True)
-        b.ctx_lens.copy_(hi[3], non_blocking=True)
-        b.slots.copy_(self.h_slots, non_blocking=True)
+        b.step_in.copy_(self.h_in, non_blocking=True)
         if self.use_graphs:
             g, out = self.graphs.get(M) or self._capture(M)
             g.replay()
@@ -263,6 +265,11 @@ class AsrEngine:
                 return toks[:n_max]
 
     def set_cross_batch(self, slots: List[int], enc_states: torch.Tensor) -> None:
+        cross = self.runner.b.cross
+        s0 = slots[0]
+        if list(slots) == list(range(s0, s0 + len(slots))):  # a run of slots: projected in place
+            self.model.cross_kv(enc_states, out=[(k[s0 : s0 + len(slots)], v[s0 : s0 + len(slots)]) for k, v in cross])
+            return
         kvs = self.model.cross_kv(enc_states)
         for li, (k, v) in enumerate(kvs):
             for i, slot in enumerate(slots):

@@ -280,16 +280,19 @@ class WhisperModel:
         x = ops.layernorm(x, self.enc_ln_w, self.enc_ln_b, eps=cfg.ln_eps)
         return x.view(B, T, d)
 
-    def cross_kv(self, enc: torch.Tensor):
-        """Per decoder layer cross-attention K/V [B, T, H, hd] (computed once per window)."""
+    def cross_kv(self, enc: torch.Tensor, out=None):
+        """Per decoder layer cross-attention K/V [B, T, H, hd] (computed once per window).
+        out: per layer (k, v) contiguous [B, T, H, hd] destinations (e.g. a run of the decode
+        buffers' session slots) the projections write straight into -- no copies."""
         B, T, d = enc.shape
         x = enc.reshape(B * T, d)
-        out = []
-        for L in self.dec:
-            k = ops.linear(x, L.xk).view(B, T, self.H, self.hd)
-            v = ops.linear(x, L.xv, L.xv_b).view(B, T, self.H, self.hd)
-            out.append((k.contiguous(), v.contiguous()))
-        return out
+        res = []
+        for li, L in enumerate(self.dec):
+            ko, vo = (None, None) if out is None else (out[li][0].view(B * T, d), out[li][1].view(B * T, d))
+            k = ops.linear(x, L.xk, out=ko).view(B, T, self.H, self.hd)
+            v = ops.linear(x, L.xv, L.xv_b, out=vo).view(B, T, self.H, self.hd)
+            res.append((k, v))
+        return res
 
     # ------------------------------------------------------------------ decoder step
     # ---- chained decode launches (skinny_stream.hip chain_kernel SEQ 2 / SEQ 1; M <= 4 rows).

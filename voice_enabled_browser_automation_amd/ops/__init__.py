@@ -371,8 +371,21 @@ def _layernorm_plain(x: torch.Tensor, eps: float) -> torch.Tensor:
 
 
 def _ln_fold_fits(x: torch.Tensor, w) -> bool:
-    return (_gpu(x) and not isinstance(w, FP8Weight) and x.shape[0] <= SKINNY_MAX_M and x.shape[1] % 128 == 0
-            and w.shape[0] % 16 == 0)
+    return (_gpu(x) and not isinstance(w, FP8Weight) and x.shape[1] % 128 == 0 and w.shape[0] % 16 == 0
+            and (x.shape[0] <= SKINNY_MAX_M or _small_rows(x, w)))
+
+
+SMALL_MAX_M = 64         # rows the one-tile kernel (skinny_gemm.hip) takes with small weights
+SMALL_BYTES = 4 << 20    # ... and what "small" is (the library's set_small_gemm_bytes default)
+
+
+def _small_rows(x: torch.Tensor, w) -> bool:
+    """17..64 rows with a small row-major bf16 weight (Whisper-tiny's decoder projections at a
+    batched decode step): ONE launch of the one-tile kernel, with the folded LayerNorm, instead of
+    a LayerNorm launch + the tiled GEMM's split-K pair (profiles/r4_asr_tiny_batch32_kernel_stats.md)."""
+    return (SKINNY_MAX_M < x.shape[0] <= SMALL_MAX_M and isinstance(w, torch.Tensor) and not isinstance(w, TiledWeight)
+            and w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and w.dim() == 2
+            and w.shape[0] * w.shape[1] * 2 <= SMALL_BYTES and x.shape[1] % 128 == 0 and w.shape[0] % 16 == 0)
 
 
 def rope_table(max_pos: int, head_dim: int, theta: float, device=None, scaling: Optional[dict] = None) -> torch.Tensor:
@@ -600,8 +613,8 @@ def _linear_impl(x, w, bias, out, residual, act, fuse_rms, eps, out_dtype, ln_c,
         return ref.linear(xr, wr, bias, out=out, residual=residual, act=act, fuse_rms=fr, eps=eps)
     E = ext()
     fp8 = isinstance(w, FP8Weight)
-    if (M <= SKINNY_MAX_M and x.shape[1] % 128 == 0 and w.shape[0] % 16 == 0
-            and (not fp8 or _fp8_stream_fits(M, x.shape[1]))):
+    if ((M <= SKINNY_MAX_M and x.shape[1] % 128 == 0 and w.shape[0] % 16 == 0
+            and (not fp8 or _fp8_stream_fits(M, x.shape[1]))) or (not fp8 and not mk and _small_rows(x, w))):
         epi = {"none": 0, "gelu": 3}[act]
         if residual is not None:
             assert act == "none"
