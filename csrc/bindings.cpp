@@ -207,7 +207,7 @@ void set_ss(GemmParams& p, int64_t epi, const c10::optional<Tensor>& ss_out, con
             const c10::optional<Tensor>& ss_in, double eps) {
   auto chk = [&](const Tensor& t, const char* n) {
     TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kLong && t.is_contiguous() && t.numel() >= p.M, n,
-                ": int64 [>= M] contiguous GPU tensor (u64 fixed point, 2^-16 units)");
+                ": int64 [>= M] contiguous GPU tensor (u64 fixed point, 2^-24 units)");
   };
   if (ss_out.has_value()) {
     chk(*ss_out, "ss_out");
@@ -817,14 +817,19 @@ Tensor alloc_uncached_i32(int64_t n, Tensor like) {
                           torch::dtype(torch::kInt).device(like.device()));
 }
 
-void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like, int64_t attn_g, int64_t seq) {
+// n_layers > 1: desc holds n_layers consecutive descriptors (torch.cat of chain_make outputs of
+// consecutive layers, same flags) run by ONE launch (skinny_stream.hip chain_kernel MULTI)
+void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like, int64_t attn_g, int64_t seq, int64_t n_layers) {
   c10::DeviceGuard g(like.device());
-  TORCH_CHECK(desc.is_cuda() && desc.numel() == (int64_t)sizeof(ChainParams), "bad chain descriptor");
+  TORCH_CHECK(n_layers >= 1 && desc.is_cuda() && desc.is_contiguous() &&
+                  desc.numel() == n_layers * (int64_t)sizeof(ChainParams) &&
+                  (reinterpret_cast<uintptr_t>(desc.data_ptr()) & 63) == 0,
+              "bad chain descriptor (n_layers x sizeof(ChainParams) bytes, 64-byte aligned)");
   // one workgroup per CU: the barrier needs every workgroup resident
   check_rc(vwa_chain_launch(reinterpret_cast<const ChainParams*>(desc.data_ptr()), (int)seq, (int)n_phases, (int)attn_g,
                             (int)(lds & 0xFFFFFF), chain_grid(like.device().index()), cur_stream(like),
                             (int)((lds >> 24) & 1) * (((lds >> 27) & 1) ? 2 : 1), (int)((lds >> 25) & 1),
-                            (int)((lds >> 26) & 1)),
+                            (int)((lds >> 26) & 1), (int)n_layers),
            "chain");
 }
 
@@ -1239,6 +1244,24 @@ void quant_fp8_rows(Tensor x, Tensor q, Tensor scale, c10::optional<Tensor> rstd
 }
 
 // ---- one-shot all-reduce (opaque state handle as int64)
+// TP preflight (parallel/custom_ar.py): may device `dev` map device `peer`'s memory (xGMI P2P)?
+// -1 when either index is not visible to this process
+int64_t can_access_peer(int64_t dev, int64_t peer) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || dev < 0 || peer < 0 || dev >= n || peer >= n) return -1;
+  if (dev == peer) return 1;
+  int ok = 0;
+  if (hipDeviceCanAccessPeer(&ok, (int)dev, (int)peer) != hipSuccess) return -1;
+  return ok;
+}
+
+// PCI location "domain:bus:device" of a visible device (a stable id across processes' masks)
+std::string pci_id(int64_t dev) {
+  char buf[64] = {0};
+  if (hipDeviceGetPCIBusId(buf, (int)sizeof(buf), (int)dev) != hipSuccess) return "";
+  return std::string(buf);
+}
+
 int64_t ar_create(int64_t rank, int64_t world, int64_t max_elems) {
   void* st = vwa_ar_create((int)rank, (int)world, max_elems);
   TORCH_CHECK(st, "all-reduce buffer allocation failed (world <= 8, max_elems % 512 == 0)");
@@ -1277,6 +1300,8 @@ void ar_destroy(int64_t st) { vwa_ar_destroy(reinterpret_cast<void*>(st)); }
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("quant_fp8_rows", &quant_fp8_rows, py::arg("x"), py::arg("q"), py::arg("scale"),
         py::arg("rstd") = py::none(), py::arg("eps") = 1e-5);
+  m.def("can_access_peer", &can_access_peer);
+  m.def("pci_id", &pci_id);
   m.def("ar_create", &ar_create);
   m.def("ar_handles", &ar_handles);
   m.def("ar_open_peer", &ar_open_peer);
@@ -1316,7 +1341,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("positions"), py::arg("slots"), py::arg("k_cache"), py::arg("v_cache"), py::arg("bar"),
         py::arg("work"), py::arg("bar_mode") = 1, py::arg("w_tiled") = false);
   m.def("chain_run", &chain_run, py::arg("desc"), py::arg("n_phases"), py::arg("lds"), py::arg("like"),
-        py::arg("attn_g") = 0, py::arg("seq") = 0);
+        py::arg("attn_g") = 0, py::arg("seq") = 0, py::arg("n_layers") = 1);
   m.def("alloc_uncached_i32", &alloc_uncached_i32);
   m.def("decode_advance", &decode_advance);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),

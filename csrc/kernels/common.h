@@ -52,11 +52,15 @@ VWA_DEVICE uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, bf16x2_t));
 }
 
-// v_max3_f32 without the canonicalising v_max the compiler puts in front of fmaxf on MFMA results
+// max of three as ONE v_maximum3_f32 (gfx950), visible to the compiler: fmaxf would put a
+// canonicalising v_max in front of every MFMA result, and the inline-asm v_max3_f32 used until
+// round 5 hid its operands from the hazard recognizer -- in the flash kernel's non-masked path it
+// read the last 32x32 MFMA's accumulators 3 SALU instructions after the MFMA (gfx950 needs 12 wait
+// states: the compiler now emits s_nop 11 there), so tmax could see a stale score and the deferred
+// rescale moved from launch to launch.  fmaximum propagates NaN, which no
+// score can be (masked keys are -inf).
 VWA_DEVICE float vmax3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
+  return __builtin_elementwise_maximum(a, __builtin_elementwise_maximum(b, c));
 }
 
 // the value of lane l ^ 32 combined with lane l's: v_permlane32_swap (VALU; no LDS round trip)
@@ -114,6 +118,19 @@ VWA_DEVICE float wave_max(float v) {
 }
 
 VWA_DEVICE int lane_id() { return threadIdx.x & 63; }
+
+// The workitem id through an empty volatile asm: every use is a fresh value, so address math
+// derived from it cannot be hoisted out of an enclosing loop.  The chained decode kernels read
+// their thread ids through this (VWA_TX): in the multi-layer launch (chain_kernel MULTI) LICM
+// otherwise hoisted every lane-derived LDS / weight address of all four phases and the attention
+// out of the layer loop -- 256 VGPRs + 650 B of scratch per lane (round 2's failed 32-layer loop
+// had the same cause).
+VWA_DEVICE int opaque_tid() {
+  int t = (int)__builtin_amdgcn_workitem_id_x();
+  asm volatile("" : "+v"(t));
+  return t;
+}
+#define VWA_TX (::vwa::opaque_tid())
 
 VWA_DEVICE f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);

@@ -296,10 +296,13 @@ VWA_DEVICE void p8_mfma(f32x4 (&acc)[8][4], const bf16x8 (&a)[4][2], const bf16x
 
 VWA_DEVICE float bias_at(const GemmParams& p, int n) { return p.bias ? bf2f(p.bias[n]) : 0.f; }
 
-// RMS statistics hand-off (GemmParams::ss_*): sums of squares in u64 fixed point, 2^-16 units
-constexpr double kSsScale = 65536.0;
+// RMS statistics hand-off (GemmParams::ss_*): sums of squares in u64 fixed point, 2^-24 units,
+// each partial rounded to nearest (truncation biased every atomic add down by up to one unit --
+// visible on small-norm rows).  Headroom: 2^64 / 2^24 ~ 1.1e12 per row sum; one partial is
+// clamped to 9.2e18 so a handful of them cannot wrap the counter.
+constexpr double kSsScale = 16777216.0;
 VWA_DEVICE unsigned long long ss_fix(float sq) {
-  return (unsigned long long)fminf(sq * (float)kSsScale, 1.8e19f);  // (>= 0; clamped below 2^64)
+  return (unsigned long long)fminf(sq * (float)kSsScale + 0.5f, 9.2e18f);  // (>= 0)
 }
 
 // per-row RMSNorm scale: rstd[m], or from the handed-off sum of squares (ss_in), or 1

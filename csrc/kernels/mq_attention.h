@@ -159,7 +159,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   int& s_last = *reinterpret_cast<int*>(lds + L::last);
 
   const int nkv = p.n_kv_heads, nq = p.n_q_heads;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = VWA_TX & 63, w = VWA_TX >> 6;
   const int n = lane & 15, g = lane >> 4;
 
   // ---- row groups of the whole step (<= 64 rows; every wave derives the same answer): runs of
@@ -190,7 +190,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   if constexpr (FINE) {
     if (p.plan_mode == 2) {
       const __amdgpu_buffer_rsrc_t r_pl = __builtin_amdgcn_make_buffer_rsrc(p.plan, (short)0, (bid + 1) * 64, 0x00020000);
-      ev = (int)__builtin_amdgcn_raw_buffer_load_b32(r_pl, (bid * 16 + (lane & 15)) * 4, 0, 0);
+      ev = (int)__builtin_amdgcn_raw_buffer_load_b32(r_pl, (bid * 16 + (lane & 15)) * 4, 0, 16);  // (sc1: written this launch)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         rt[r] = __builtin_bit_cast(int2, __builtin_amdgcn_raw_buffer_load_b64(
@@ -282,7 +282,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
     if (done == nullptr) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(gp(done), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (VWA_TX == 0) __hip_atomic_fetch_add(gp(done), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   for (int item = bid; item < n_items; item += grid) {
   if (item == bid) stamp(18);
@@ -388,11 +388,21 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   bf16x8 qf[NKS];
   auto make_qf = [&]() {
     const float qs = p.scale * 1.4426950408889634f;
-    const u16* qr = p.q + (int64_t)(r0 + min(rho, nr - 1)) * p.ldq + (kvh * G + n % G) * D + 8 * g;
+    const int64_t qo = (int64_t)(r0 + min(rho, nr - 1)) * p.ldq + (kvh * G + n % G) * D + 8 * g;
+    // FINE (the chained launch): Q is written by the QKV phase of the same launch when several
+    // layers run in one launch (chain_kernel MULTI), possibly on another XCD whose L2 line this
+    // XCD may hold from the previous layer's attention: device-scope (sc1) loads
+    const __amdgpu_buffer_rsrc_t r_q = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<u16*>(p.q), (short)0, FINE ? (int)((int64_t)p.rows * p.ldq * 2) : 0, 0x00020000);
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       float f[8];
-      unpack8(ld128(qr + 32 * ks), f);
+      if constexpr (FINE) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r_q, (int)((qo + 32 * ks) * 2), 0, 16);
+        unpack8(make_uint4(v.x, v.y, v.z, v.w), f);
+      } else {
+        unpack8(ld128(p.q + qo + 32 * ks), f);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = rho < nr ? f[j] * qs : 0.f;
       qf[ks] = as_bf16x8(pack8(f));
@@ -538,7 +548,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   __syncthreads();
 
   // ---- merge the waves: thread -> (query column cn, 8-dim chunk dc)
-  const int cn = threadIdx.x >> 4, dc = threadIdx.x & 15;
+  const int cn = VWA_TX >> 4, dc = VWA_TX & 15;
   const int crow = r0 + cn / G, ch = kvh * G + cn % G;
   const bool act = cn / G < nr && dc < NCH;
   const __amdgpu_buffer_rsrc_t r_o = rsrc_f32(p.part_o, (int64_t)p.rows * p.n_splits * nq * D);
@@ -581,7 +591,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
   // ---- ticket (same protocol as the split kernel): drained sc1 stores, then one counter add
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (VWA_TX == 0) {
     int* cnt = p.counters + r0 * nkv + kvh;
     const int ticket = __hip_atomic_fetch_add(gp(cnt), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = (ticket == nact - 1);
@@ -597,7 +607,7 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
     //      other chunk with all of its (<= n_splits / 2) partial loads in flight at once (clamped
     //      indices, zero weight past nact), then the two halves combine through LDS
     constexpr int MAXC = 8;  // chunks per thread: nact <= 2 * MAXC (host: n_splits <= 16)
-    const int pr = threadIdx.x & 255, hf = threadIdx.x >> 8;
+    const int pr = VWA_TX & 255, hf = VWA_TX >> 8;
     const int pcn = pr >> 4, pdc = pr & 15;
     const int prow = r0 + pcn / G, pch = kvh * G + pcn % G;
     const bool pact = pcn / G < nr && pdc < NCH;

@@ -139,13 +139,13 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
     return s;
   };
   auto operands = [&](int o) {
-    if (first && o == (int)threadIdx.x) return pre;
+    if (first && o == VWA_TX) return pre;
     EpiPre e;
     epi_values<EPI, NT, SC1>(p, tile, o, e);
     return e;
   };
   if constexpr (EPI == EPI_SWIGLU) {
-    for (int o = threadIdx.x; o < M * 16; o += KS * 64) {
+    for (int o = VWA_TX; o < M * 16; o += KS * 64) {
       const int m = o >> 4, q = o & 15;
       const EpiPre e = operands(o);
       const float sc = rs[m];
@@ -161,7 +161,7 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
     const int head = n0 / hd;
     const int t = (n0 % hd) >> 4;
     const bool is_v = head >= p.n_q_heads + p.n_kv_heads;
-    for (int o = threadIdx.x; o < M * 16; o += KS * 64) {
+    for (int o = VWA_TX; o < M * 16; o += KS * 64) {
       const int m = o >> 4, q = o & 15;
       const EpiPre e = operands(o);
       const float sc = rs[m];
@@ -192,7 +192,7 @@ VWA_DEVICE void tile_epilogue(const SkinnyParams& p, float* red, const float* rs
       }
     }
   } else {
-    for (int o = threadIdx.x; o < M * 16 * NT; o += KS * 64) {
+    for (int o = VWA_TX; o < M * 16 * NT; o += KS * 64) {
       const int m = o / (16 * NT), nn = o % (16 * NT);
       const int n = n0 + nn;
       const EpiPre e = operands(o);
@@ -231,11 +231,11 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
   float* rs = red + KS * NT * MT * 4 * 64;                // [16 MT] row scales (1/rms, LayerNorm rstd)
   float* mu = rs + 16 * MT;                               // [16 MT] row means (folded LayerNorm)
   const float* mus = (p.fuse_rms == 2) ? mu : nullptr;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = VWA_TX & 63, w = VWA_TX >> 6;
   const int nl = lane & 15, g = lane >> 4;
 
   EpiPre pre;
-  epi_values<EPI, NT>(p, blockIdx.x, threadIdx.x, pre);  // first tile's epilogue operands, early
+  epi_values<EPI, NT>(p, blockIdx.x, VWA_TX, pre);  // first tile's epilogue operands, early
   const int G = K / 128;
   const int gb = (G * w) / KS, ge = (G * (w + 1)) / KS;
   const __amdgpu_buffer_rsrc_t rw =
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_stream_kernel(SkinnyParams p, 
   // ---- stage X rows into LDS
   const int k8 = K / 8;
   if constexpr (!XG) {
-    for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
+    for (int c = VWA_TX; c < M * k8; c += KS * 64) {
       const int m = c / k8, kk = c % k8;
       *reinterpret_cast<uint4*>(xs + xrow(m) + kk * 8) =
           *reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8);
@@ -457,12 +457,12 @@ __global__ __launch_bounds__(KS * 64) void skinny_fp8_kernel(SkinnyParams p, int
   float* red = reinterpret_cast<float*>(smem + xbytes);  // [KS][NT][4][64]
   float* rs = red + KS * NT * 4 * 64;                     // [16] row scale (rms * x-quant scale)
   float* inv = rs + 16;                                    // [16] 1 / x-quant scale
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = VWA_TX & 63, w = VWA_TX >> 6;
   const int nl = lane & 15, g = lane >> 4;
   const int k8 = K / 8;
 
   EpiPre pre;
-  epi_values<EPI, NT>(p, blockIdx.x, threadIdx.x, pre);  // first tile's epilogue operands, early
+  epi_values<EPI, NT>(p, blockIdx.x, VWA_TX, pre);  // first tile's epilogue operands, early
   // ---- per-row statistics (sum of squares for the fused RMSNorm, amax for the fp8 scale)
   for (int m = w; m < 16; m += KS) {
     float sc = 1.f, iv = 1.f;
@@ -490,7 +490,7 @@ __global__ __launch_bounds__(KS * 64) void skinny_fp8_kernel(SkinnyParams p, int
   }
   lds_sync();
   // ---- quantise X rows into LDS (e4m3, 8 values -> 8 bytes)
-  for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
+  for (int c = VWA_TX; c < M * k8; c += KS * 64) {
     const int m = c / k8, kk = c % k8;
     float f[8];
     unpack8(*reinterpret_cast<const uint4*>(p.X + (size_t)m * p.ldx + kk * 8), f);
@@ -655,7 +655,7 @@ VWA_DEVICE unsigned long long bar_sum8(const unsigned long long* bar) {
 // (every completed launch added a multiple of nwg; this workgroup has not arrived yet, so fewer
 // than nwg arrivals of this launch can be counted in it).
 VWA_DEVICE unsigned long long chain_base(const unsigned long long* bar, int nwg, int mode) {
-  if (mode < 4 || threadIdx.x >= 64) return 0;
+  if (mode < 4 || VWA_TX >= 64) return 0;
   const unsigned long long s = bar_sum8(bar);
   return (s / (unsigned long long)nwg) * (unsigned long long)nwg;
 }
@@ -664,13 +664,13 @@ VWA_DEVICE unsigned long long chain_arrive(unsigned long long* bar, int nwg, int
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores are performed
   lds_sync();
   if (mode >= 4) {
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(gp(&bar[16 * (blockIdx.x & 7)]), 1ull, __ATOMIC_RELAXED,
+    if (VWA_TX == 0) __hip_atomic_fetch_add(gp(&bar[16 * (blockIdx.x & 7)]), 1ull, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
     next += (unsigned long long)nwg;
     return next;
   }
   unsigned long long target = 0;
-  if (threadIdx.x == 0) {
+  if (VWA_TX == 0) {
     if (mode == 0) {
       const unsigned long long t = __hip_atomic_fetch_add(gp(&bar[0]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       target = (t / (unsigned long long)nwg + 1ull) * (unsigned long long)nwg;
@@ -694,14 +694,14 @@ VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, i
     return;
   }
   if (mode == 4) {
-    if (threadIdx.x < 64) {
+    if (VWA_TX < 64) {
       const unsigned long long tgt = __builtin_amdgcn_readfirstlane((unsigned)target) |
                                      ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(target >> 32)) << 32);
       int spins = 0;
       while ((long long)(bar_sum8(bar) - tgt) < 0) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > kChainSpinLimit) {
-          if (threadIdx.x == 0) __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (VWA_TX == 0) __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }
@@ -713,7 +713,7 @@ VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, i
     // wave 0 polls with scalar loads (glc: past the scalar cache; bar lives in uncached memory so
     // no L2 copy can be stale): SMEM completes on lgkmcnt, so the poll is not queued behind the
     // next phase's weight loads this wave just issued (vmcnt retires in order)
-    if (threadIdx.x < 64) {
+    if (VWA_TX < 64) {
       const unsigned long long tgt = __builtin_amdgcn_readfirstlane((unsigned)target) |
                                      ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(target >> 32)) << 32);
       const unsigned long long* top = &bar[kBarTop];
@@ -724,7 +724,7 @@ VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, i
         if ((long long)(v - tgt) >= 0) break;
         __builtin_amdgcn_s_sleep(1);
         if (++spins > kChainSpinLimit) {
-          if (threadIdx.x == 0) __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (VWA_TX == 0) __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
         }
       }
@@ -732,7 +732,7 @@ VWA_DEVICE void chain_wait(unsigned long long* bar, unsigned long long target, i
     lds_sync();
     return;
   }
-  if (threadIdx.x == 0) {
+  if (VWA_TX == 0) {
     unsigned long long* w = mode == 0 ? &bar[0] : &bar[kBarTop];
     int spins = 0;
     while ((long long)(__hip_atomic_load(gp(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
@@ -758,10 +758,10 @@ VWA_DEVICE void chain_tp_reduce(const ChainParams& cp, int region, int target, u
   __threadfence_system();
   const unsigned long long gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
   chain_wait(bar, gen, cp.bar_mode);
-  if (blockIdx.x == 0 && (int)threadIdx.x < tp.world)
-    __hip_atomic_store(gp(tp.flag_out[threadIdx.x]), target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if ((int)threadIdx.x < tp.world) {
-    const int* f = tp.flag_in + threadIdx.x;
+  if (blockIdx.x == 0 && VWA_TX < tp.world)
+    __hip_atomic_store(gp(tp.flag_out[VWA_TX]), target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (VWA_TX < tp.world) {
+    const int* f = tp.flag_in + VWA_TX;
     int spins = 0;
     while (__hip_atomic_load(gp(f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target < 0) {
       __builtin_amdgcn_s_sleep(1);
@@ -785,7 +785,7 @@ VWA_DEVICE void chain_tp_reduce(const ChainParams& cp, int region, int target, u
   for (int q = 0; q < kMaxW; ++q)
     rs[q] = __builtin_amdgcn_make_buffer_rsrc(q < tp.world ? tp.stage[q] + (size_t)region * tp.region : tp.stage[0],
                                               (short)0, (int)(tp.region * sizeof(float)), 0x00020000);
-  for (int i = lo + (int)threadIdx.x; i < hi; i += (int)blockDim.x) {
+  for (int i = lo + VWA_TX; i < hi; i += (int)blockDim.x) {
     const int m = (4 * i) / d, c = 4 * i - m * d;
     u32x4 part[kMaxW];
 #pragma unroll
@@ -823,7 +823,7 @@ struct PhaseRange {
 template <int KS>
 VWA_DEVICE PhaseRange chain_range(const ChainPhase& ph, int wb0 = 0, int wn = 0) {
   PhaseRange r;
-  const int w = threadIdx.x >> 6;
+  const int w = VWA_TX >> 6;
   const int G = ph.p.K / 128;
   r.gb = (G * w) / KS;
   r.ge = (G * (w + 1)) / KS;
@@ -859,7 +859,7 @@ VWA_DEVICE void chain_load(const SkinnyParams& p, int nb, uint4 (&wr)[R], int it
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.W), (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rxg =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.X), (short)0, XG ? (int)((size_t)p.M * p.ldx * 2) : 0, 0x00020000);
-  const int lane = threadIdx.x & 63, nl = lane & 15, g = lane >> 4;
+  const int lane = VWA_TX & 63, nl = lane & 15, g = lane >> 4;
   const int unit = r.u0 + it;
   const int tile = unit / nb, b = unit % nb;
 #pragma unroll
@@ -910,7 +910,7 @@ VWA_DEVICE void chain_load_x(const SkinnyParams& p, int nb, uint4 (&wr)[R], int 
   static_assert(8 + U * 4 <= R, "XG items: weight registers 0..7, X fragments from register 8");
   const __amdgpu_buffer_rsrc_t rxg =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.X), (short)0, (int)((size_t)p.M * p.ldx * 2), 0x00020000);
-  const int lane = threadIdx.x & 63, nl = lane & 15, g = lane >> 4;
+  const int lane = VWA_TX & 63, nl = lane & 15, g = lane >> 4;
   const int b = (r.u0 + it) % nb;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -936,8 +936,8 @@ VWA_DEVICE void chain_preload(const SkinnyParams& p, int nb, const PhaseRange& r
   static_assert(NT * U * (F8 ? 2 : 4) <= 16, "an item = at most 16 loads of 1 KB per wave (16 KB of LDS)");
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(p.W), (short)0, (int)((size_t)p.N * p.K * 2), 0x00020000);
-  const unsigned lane = threadIdx.x & 63;
-  char* wd = dst + (threadIdx.x >> 6) * 16384;
+  const unsigned lane = VWA_TX & 63;
+  char* wd = dst + (VWA_TX >> 6) * 16384;
   const int unit = r.u0 + it;
   const int tile = unit / nb, b = unit % nb;
 #pragma unroll
@@ -1002,13 +1002,13 @@ VWA_DEVICE void chain_issue_item(const ChainPhase& ph, uint4 (&wr)[R], int it, i
 // partial tile of a split tile: cross-wave sums of this workgroup's units -> slot (sc1)
 template <int NT, int KS>
 VWA_DEVICE void tile_publish(int M, float* red, f32x4 (&acc)[NT], float* slot) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = VWA_TX & 63, w = VWA_TX >> 6;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[((w * NT + nt) * 4 + i) * 64 + lane] = acc[nt][i];
   lds_sync();
-  for (int o = threadIdx.x; o < M * 16 * NT; o += KS * 64) {
+  for (int o = VWA_TX; o < M * 16 * NT; o += KS * 64) {
     const int m = o / (16 * NT), nn = o % (16 * NT);
     const int nt = nn >> 4, q = nn & 15;
     const int ln = q + 16 * (m >> 2), i = m & 3;
@@ -1041,7 +1041,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
   float* mu = rs + 16;                  // [16] row means (folded LayerNorm)
   int* s_flag = reinterpret_cast<int*>(rs + 32);
   const float* mus = p.fuse_rms == 2 ? mu : nullptr;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = VWA_TX & 63, w = VWA_TX >> 6;
   const int nl = lane & 15, g = lane >> 4;
   const PhaseRange r = chain_range<KS>(ph, wb0, wn);
   const int first_tile = r.u0 / nb;
@@ -1050,7 +1050,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
   // (entry, X staged, row scales, item 0 computed, tile 0 finished, item 1, tile 1 finished)
   auto pst = [&](int k) {
     const int slot = k < 8 ? 22 + 8 * i + k : -1;
-    if (cp.ts && threadIdx.x == 0 && slot >= 0) *gp(cp.ts + blockIdx.x * kTsStride + slot) = __builtin_amdgcn_s_memrealtime();
+    if (cp.ts && VWA_TX == 0 && slot >= 0) *gp(cp.ts + blockIdx.x * kTsStride + slot) = __builtin_amdgcn_s_memrealtime();
   };
   pst(0);
   if constexpr (XG) {  // X fragments of the items issued before the barrier wait (weights only)
@@ -1088,7 +1088,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
   if (!xw) issue_rest();
 
   EpiPre pre;
-  if (r.n_items > 0 && !xw) epi_values<EPI, NT, true>(p, first_tile, threadIdx.x, pre);
+  if (r.n_items > 0 && !xw) epi_values<EPI, NT, true>(p, first_tile, VWA_TX, pre);
   if (stager && xw) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pieces (the staging wave issued nothing else)
   } else if (stager) {
@@ -1113,7 +1113,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   } else if (!xdma && !XG) {
-    for (int c = threadIdx.x; c < M * k8; c += KS * 64) {
+    for (int c = VWA_TX; c < M * k8; c += KS * 64) {
       const int m = c / k8, kk = c % k8;
       const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(((size_t)m * p.ldx + kk * 8) * 2), 0, 16);
       *reinterpret_cast<uint4*>(xs + m * xstride + kk * 8) = make_uint4(v.x, v.y, v.z, v.w);
@@ -1129,7 +1129,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
       if (hs < 1) chain_load<NT, U, WA, R, XG, F8>(p, nb, X0, 0, r);
       if (hs < 2) chain_load<NT, U, WA, R, XG, F8>(p, nb, X1, 1, r);
     }
-    if (r.n_items > 0) epi_values<EPI, NT, true>(p, first_tile, threadIdx.x, pre);
+    if (r.n_items > 0) epi_values<EPI, NT, true>(p, first_tile, VWA_TX, pre);
   };
   if (xw && !cp.xw_late) issue_xw();
   for (int m = w; m < 16; m += KS) {
@@ -1213,7 +1213,7 @@ VWA_DEVICE void chain_phase(const ChainParams& cp, int i, uint4 (&X0)[R], uint4 
     tile_publish<NT, KS>(M, red, acc, slots + mine * per);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_sync();
-    if (threadIdx.x == 0) {
+    if (VWA_TX == 0) {
       const unsigned t = __hip_atomic_fetch_add(gp(&cp.tickets[tile]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = t == 1u;
       if (last) __hip_atomic_store(gp(&cp.tickets[tile]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1297,10 +1297,31 @@ struct SeqEpi {
 // ph[2].xg: more rows than its X fits LDS, 5..16 rows, no attention phase)
 // O2: phase 0 (o_proj) in 32-column tiles (ChainParams::o_nt2)
 // D2: the X-streaming down projection (XG2) in 32-column tiles (ChainParams::d_nt2)
-template <int KS, int SEQ, int NPH, int AG, int WA, bool XG2 = false, bool F8 = false, bool O2 = false, bool D2 = false>
-__global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __restrict__ cpp) {
+// MULTI: ONE launch runs n_layers consecutive layers (descriptors cpp[0 .. n_layers), each a
+// 4-phase Llama tail whose QKV phase feeds the next layer's attention).  Between layers every
+// workgroup arrives at a grid barrier after its QKV tiles; only the workgroups that run an
+// attention item of the next layer wait for it (they read the next layer's Q and newest K/V).  A
+// workgroup the step plan (mq_attention.h, written by layer 0 of this very launch) gives no
+// attention item goes straight on: it issues the next layer's o_proj weights and gate/up LDS item
+// while the slow QKV tiles and the attention are still running -- no kernel boundary, no launch
+// ramp, and the HBM pipe of half the CUs is busy through the QKV tail and the attention front.
+// (Skipping the wait is safe for the ticket barriers: such a workgroup's next arrival happens only
+// after the attention hand-off, which itself needed this barrier complete.)
+template <int KS, int SEQ, int NPH, int AG, int WA, bool XG2 = false, bool F8 = false, bool O2 = false, bool D2 = false,
+          bool MULTI = false>
+__global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __restrict__ cpp, int n_layers) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const ChainParams& cp = *cpp;  // device-resident descriptor
+  static_assert(!MULTI || (SEQ == 0 && NPH == 4 && AG > 0 && !XG2), "multi-layer launch: Llama tails with attention");
+  const int nwg = (int)gridDim.x;
+  unsigned long long* bar = reinterpret_cast<unsigned long long*>(cpp->bar);
+  unsigned long long bar_next = chain_base(bar, nwg, cpp->bar_mode);  // mode >= 4: running target
+  // TP rounds of this launch: e0 + 2 li + 1 (after layer li's o_proj), e0 + 2 li + 2 (after its
+  // down); every workgroup reads e0 before its first arrival, workgroup 0 advances it after each
+  // layer's last round
+  const bool tpr = cpp->tp.world > 1;
+  const int e0 = tpr ? __hip_atomic_load(gp(cpp->tp.epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  for (int li = 0; li < (MULTI ? n_layers : 1); ++li) {
+  const ChainParams& cp = cpp[li];  // device-resident descriptor
   // Warm the scalar cache with the whole descriptor (24 x 64-byte lines) in ONE round trip: the
   // fields are otherwise fetched behind branches and earlier fields' values, a chain of dependent
   // scalar misses (the attention prologue measured ~6 of them before its first vector load)
@@ -1317,23 +1338,20 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
         "s_load_dword %0, %1, 0x540\n\t""s_load_dword %0, %1, 0x580\n\t""s_load_dword %0, %1, 0x5c0\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=&s"(junk)
-        : "s"(cpp));
+        : "s"(cpp + li));
     if (junk == 0x9e3779b9u) __builtin_amdgcn_s_sleep(1);
   }
-  uint4 A[ChainShape<KS, F8>::R], B[ChainShape<KS, F8>::R];
+  // (zeroed per layer: otherwise a path that reads a set before writing it -- only possible for
+  // an all-OOB padding item -- keeps the previous layer's 128 registers live across the layer
+  // loop's back edge and through the attention: spills.  Zeros cost nothing to rematerialise.)
+  uint4 A[ChainShape<KS, F8>::R] = {}, B[ChainShape<KS, F8>::R] = {};
   // barrier = arrive (stores drained), issue the next phase's first weight item, then wait: the
   // weight stream is in flight while the slowest workgroup finishes
-  const int nwg = (int)gridDim.x;
   unsigned long long gen;
-  unsigned long long* bar = reinterpret_cast<unsigned long long*>(cp.bar);
-  unsigned long long bar_next = chain_base(bar, nwg, cp.bar_mode);  // mode >= 4: running target
-  // TP rounds of this launch: e0 + 1 (after o_proj), e0 + 2 (after down); every workgroup reads e0
-  // before its first arrival, workgroup 0 advances it after the last round
-  const bool tpr = cp.tp.world > 1;
-  const int e0 = tpr ? __hip_atomic_load(gp(cp.tp.epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  const int er = e0 + 2 * li;  // this layer's TP round base
   int nts = 0;
   auto stamp = [&]() {
-    if (cp.ts && threadIdx.x == 0) *gp(cp.ts + blockIdx.x * kTsStride + nts) = __builtin_amdgcn_s_memrealtime();
+    if (cp.ts && VWA_TX == 0) *gp(cp.ts + blockIdx.x * kTsStride + nts) = __builtin_amdgcn_s_memrealtime();
     ++nts;
   };
   stamp();
@@ -1381,7 +1399,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                           issue0(pre0);
                                                         }, &n_attn, [&](int k) {
                                                           if ((k == 15 || k == 10) && cp.ts) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                                                          if (cp.ts && threadIdx.x == 0)
+                                                          if (cp.ts && VWA_TX == 0)
                                                             *gp(cp.ts + blockIdx.x * kTsStride + k) = __builtin_amdgcn_s_memrealtime();
                                                         }, done, &n_final);
     if (!idle) setup0(n_attn);
@@ -1391,9 +1409,9 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
       pre0 = 0;
       issue0(0);
     }
-    if (cp.lds_item && (int)(threadIdx.x >> 6) < cp.lds_item_waves) preload1();
+    if (cp.lds_item && (int)(VWA_TX >> 6) < cp.lds_item_waves) preload1();
     if (chain_range<KS>(cp.ph[0], ob0, on).n_items > 0) {
-      if (threadIdx.x < 64) {
+      if (VWA_TX < 64) {
         const unsigned long long tgt = (unsigned long long)n_final;
         int spins = 0;
         while (true) {
@@ -1402,7 +1420,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
           if (v >= tgt) break;
           __builtin_amdgcn_s_sleep(1);
           if (++spins > kChainSpinLimit) {
-            if (threadIdx.x == 0) __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (VWA_TX == 0) __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             break;
           }
         }
@@ -1419,7 +1437,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                           issue0(pre0);
                                                         }, &n_attn, [&](int k) {
                                                           if ((k == 15 || k == 10) && cp.ts) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                                                          if (cp.ts && threadIdx.x == 0)
+                                                          if (cp.ts && VWA_TX == 0)
                                                             *gp(cp.ts + blockIdx.x * kTsStride + k) = __builtin_amdgcn_s_memrealtime();
                                                         });
     if (!idle) setup0(n_attn);
@@ -1433,7 +1451,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     // attention's use of LDS).  Measured (tools/chain_probe.py, 1 row): 101.7-102.0 vs
     // 104.2-104.9 us per layer; issued earlier (idle workgroups at once) its bytes delayed the
     // attention's K/V (+1.7 us), issued inside the o_proj phase they delayed its end (+4.5 us)
-    if (cp.lds_item && (int)(threadIdx.x >> 6) < cp.lds_item_waves) preload1();
+    if (cp.lds_item && (int)(VWA_TX >> 6) < cp.lds_item_waves) preload1();
 
     chain_wait(bar, gen, cp.bar_mode);
    }
@@ -1443,7 +1461,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   }
   // cp.xdma: the staging wave issues nothing at the barriers (chain_phase), the others one item
   // (their second follows right at the release)
-  const bool stg = cp.xdma && (threadIdx.x >> 6) == KS - 1;
+  const bool stg = cp.xdma && (VWA_TX >> 6) == KS - 1;
   const int preb = cp.xdma ? 0 : cp.pre2;
   // per-barrier override (cp.pre_mask bit i): two items issued ahead of phase i even with xdma
   auto preb_of = [&](int i) { return ((cp.pre_mask >> i) & 1) ? 1 : preb; };
@@ -1458,11 +1476,11 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     // VWA_CHAIN_GRID_DIV -- and its MFMAs read stale registers: NaN / wrong o_proj tiles.)
     chain_phase<E0, KS, WA, false, F8, O2>(cp, 0, B, A, smem, nx ? 1 : pre0, nx ? 2 : 1 + (pre0 ? 1 : 0), ob0, on);
   stamp();
-  if (SEQ == 0 && tpr) chain_tp_reduce(cp, 0, e0 + 1, bar, nwg, bar_next);
+  if (SEQ == 0 && tpr) chain_tp_reduce(cp, 0, er + 1, bar, nwg, bar_next);
   gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
   // cp.pre_waves (> 0): only waves below it issue the next phase's items at the barrier; the others
   // issue theirs after the release, behind the X pieces (chain_phase has0 = false)
-  const int wv = (int)(threadIdx.x >> 6);
+  const int wv = (int)(VWA_TX >> 6);
   const bool prew = (cp.pre_waves == 0 || wv < cp.pre_waves) && !(cp.poll_free && wv == 0);
   if (!stg) {
     if (nx) chain_issue_item<E1, KS, WA, false, F8>(cp.ph[1], B, 1);  // phase 1's item 0 is already in A
@@ -1471,7 +1489,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   chain_wait(bar, gen, cp.bar_mode);
   // every attention output was counted and every waiter released before this barrier: reset the
   // count for the next launch (ordered before it by the kernel boundary)
-  if (AG > 0 && cp.attn_flag && blockIdx.x == 0 && threadIdx.x == 0)
+  if (AG > 0 && cp.attn_flag && blockIdx.x == 0 && VWA_TX == 0)
     __hip_atomic_store(gp(&bar[kBarAttnDone]), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp();
   chain_phase<E1, KS, WA, false, F8>(cp, 1, A, B, smem, nx ? 1 : preb_of(1), nx ? 1 : 0, 0, 0, nx || prew);
@@ -1490,9 +1508,9 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     chain_phase<E2, KS, WA, XG2, F8, D2>(cp, 2, A, B, smem, preb_of(2), 0, 0, 0, prew || XG2);
     stamp();
     if (SEQ == 0 && tpr) {
-      chain_tp_reduce(cp, 1, e0 + 2, bar, nwg, bar_next);
-      if (blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(gp(cp.tp.epoch), e0 + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      chain_tp_reduce(cp, 1, er + 2, bar, nwg, bar_next);
+      if (blockIdx.x == 0 && VWA_TX == 0)
+        __hip_atomic_store(gp(cp.tp.epoch), er + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if constexpr (NPH >= 4) {
@@ -1503,6 +1521,25 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     chain_phase<E3, KS, WA, false, F8>(cp, 3, A, B, smem, preb_of(3), 0, 0, 0, prew);
     stamp();
   }
+  if constexpr (MULTI) {
+    if (li + 1 < n_layers) {
+      // layer li -> li + 1: the QKV tiles of every workgroup are stored (the arrival drains them)
+      // before an attention workgroup reads Q / the newest K/V
+      gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
+      const DecodeAttnParams& na = cpp[li + 1].attn;
+      bool skip = false;
+      if (cpp[li + 1].attn_flag && na.plan_mode == 2) {
+        // this workgroup's step-plan entry (state 0 idle / 2 empty chunk: no Q, K or V read)
+        const __amdgpu_buffer_rsrc_t r_pl =
+            __builtin_amdgcn_make_buffer_rsrc(na.plan, (short)0, ((int)blockIdx.x + 1) * 64, 0x00020000);
+        const int ev = (int)__builtin_amdgcn_raw_buffer_load_b32(r_pl, ((int)blockIdx.x * 16 + (VWA_TX & 15)) * 4, 0, 16);
+        const int st = __builtin_amdgcn_readlane(ev, 2), rows = __builtin_amdgcn_readlane(ev, 10);
+        skip = (st == 0 || st == 2) && rows == na.rows;
+      }
+      if (!skip) chain_wait(bar, gen, cp.bar_mode);
+    }
+  }
+  }  // layers
 }
 
 }  // namespace
@@ -1620,13 +1657,26 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
 }
 
 extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid,
-                                hipStream_t st, int xg2, int f8, int o2) {
+                                hipStream_t st, int xg2, int f8, int o2, int n_layers) {
   if (attn_g) lds = lds > (int)MqLds<128, 8>::bytes ? lds : (int)MqLds<128, 8>::bytes;
+  if (n_layers > 1) {  // one launch over n_layers consecutive 4-phase Llama tails (chain_kernel MULTI)
+    if (seq != 0 || n_phases != 4 || xg2 || (attn_g != 4 && attn_g != 8) || (!f8 && !o2) || (f8 && o2)) return -10;
+#define VWA_CHAIN_LAUNCH_MULTI(G, F8_, O2_) \
+  hipLaunchKernelGGL((chain_kernel<8, 0, 4, G, 0, false, F8_, O2_, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp, n_layers)
+    if (attn_g == 4) {
+      if (f8) VWA_CHAIN_LAUNCH_MULTI(4, true, false); else VWA_CHAIN_LAUNCH_MULTI(4, false, true);
+    } else {
+      if (f8) VWA_CHAIN_LAUNCH_MULTI(8, true, false); else VWA_CHAIN_LAUNCH_MULTI(8, false, true);
+    }
+#undef VWA_CHAIN_LAUNCH_MULTI
+    return (int)hipGetLastError();
+  }
+#ifndef VWA_ONLY_MULTI  // (register-budget experiments: compile the multi-layer instantiations alone)
   if (o2) {  // o_proj in 32-column tiles (ChainParams::o_nt2): Llama tail with the attention phase, bf16
     if (seq != 0 || f8 || xg2 || (n_phases != 3 && n_phases != 4)) return -10;
     const bool q = n_phases == 4;
 #define VWA_CHAIN_LAUNCH_O2(N, G) \
-  hipLaunchKernelGGL((chain_kernel<8, 0, N, G, 0, false, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp)
+  hipLaunchKernelGGL((chain_kernel<8, 0, N, G, 0, false, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp, 1)
     switch (attn_g) {
       case 4: if (q) VWA_CHAIN_LAUNCH_O2(4, 4); else VWA_CHAIN_LAUNCH_O2(3, 4); break;
       case 8: if (q) VWA_CHAIN_LAUNCH_O2(4, 8); else VWA_CHAIN_LAUNCH_O2(3, 8); break;
@@ -1638,19 +1688,19 @@ extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, 
   if (xg2) {  // Llama tail of 5..16 rows: down projection with X from L2, no attention phase
     if (seq != 0 || attn_g != 0 || f8 || (n_phases != 3 && n_phases != 4)) return -10;
     if (xg2 == 2) {  // (d_nt2: 32-column down tiles)
-      if (n_phases == 4) hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, 0, true, false, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
-      else hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, 0, true, false, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+      if (n_phases == 4) hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, 0, true, false, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp, 1);
+      else hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, 0, true, false, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp, 1);
     } else if (n_phases == 4) {
-      hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+      hipLaunchKernelGGL((chain_kernel<8, 0, 4, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp, 1);
     } else {
-      hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp);
+      hipLaunchKernelGGL((chain_kernel<8, 0, 3, 0, 0, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp, 1);
     }
     return (int)hipGetLastError();
   }
 #define VWA_CHAIN_LAUNCH(S, N, G) \
-  hipLaunchKernelGGL((chain_kernel<8, S, N, G, 0>), dim3(grid), dim3(8 * 64), lds, st, d_cp)
+  hipLaunchKernelGGL((chain_kernel<8, S, N, G, 0>), dim3(grid), dim3(8 * 64), lds, st, d_cp, 1)
 #define VWA_CHAIN_LAUNCH_F8(N, G) \
-  hipLaunchKernelGGL((chain_kernel<8, 0, N, G, 0, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp)
+  hipLaunchKernelGGL((chain_kernel<8, 0, N, G, 0, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp, 1)
   if (f8) {  // fp8 tiled weights, W8A16 (Llama tail only)
     if (seq != 0 || (n_phases != 3 && n_phases != 4)) return -10;
     const bool q = n_phases == 4;
@@ -1683,6 +1733,9 @@ extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, 
   }
 #undef VWA_CHAIN_LAUNCH
   return (int)hipGetLastError();
+#else
+  return -10;
+#endif
 }
 
 // (round 4's 32-column tiles for the plain epilogues measured slower at
@@ -1718,7 +1771,11 @@ extern "C" void vwa_skinny_set_x_skew(int skew) { g_x_skew = skew == 0 ? 0 : 32;
 extern "C" int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st) {
   if (p->M < 1 || p->M > 16 || p->K % 128 != 0) return -10;
   if ((size_t)p->N * p->K * (p->w_scale ? 1 : 2) >= 0x7FFFFFF0ull) return -10;
+#ifdef VWA_ONLY_MULTI
+  const int r = -10;
+#else
   const int r = (ks == 4) ? dispatch_ks<4>(epi, *p, grid_cap, st) : dispatch_ks<8>(epi, *p, grid_cap, st);
+#endif
   if (r) return r;
   return (int)hipGetLastError();
 }

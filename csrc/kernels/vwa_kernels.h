@@ -98,7 +98,9 @@ struct ChainTP {
   int region;          // floats per region (>= M x hidden)
 };
 
-struct ChainParams {
+// (64-byte aligned: a multi-layer launch indexes an array of them, and each one's scalar-cache
+// warm-up, chain_kernel, covers exactly its 24 lines)
+struct alignas(64) ChainParams {
   ChainPhase ph[kChainMaxPhases];
   int n;
   int seq;                 // 0 Llama tail, 1 Whisper tail, 2 Whisper middle (skinny_stream.hip chain_kernel)
@@ -174,7 +176,7 @@ struct GemmParams {
   // adds the squares of its bf16 output rows into ss_out[m] (the next RMSNorm's statistics);
   // ss_zero[0, ss_zero_n) is zeroed by workgroup 0 (the other buffer, already consumed); ss_in --
   // the per-row scale is rsqrt(ss_in[m] / K + ss_eps) instead of rstd[m] (no row_rstd launch).
-  // The sums are u64 fixed point in units of 2^-16 (kSsScale): integer atomics add in any order
+  // The sums are u64 fixed point in units of 2^-24 (kSsScale): integer atomics add in any order
   // to the same bits, so the statistics -- and every token after them -- are run-to-run
   // reproducible (f32 atomics were not: tools/repro_check.py)
   unsigned long long* ss_out; unsigned long long* ss_zero; int ss_zero_n; const unsigned long long* ss_in;
@@ -200,8 +202,10 @@ int vwa_skinny_gemm(int epi, const SkinnyParams* p, hipStream_t st);
 int vwa_skinny_stream(int epi, const SkinnyParams* p, int grid_cap, int ks, hipStream_t st);
 void vwa_skinny_set_x_skew(int skew);  // LDS-staged X rows: 64-B skew every 4 rows (default) or none (0)
 int vwa_chain_prepare(ChainParams* cp, int grid);
+// n_layers > 1: d_cp is an array of n_layers descriptors of consecutive 4-phase Llama tails with the
+// attention phase, run by ONE launch (skinny_stream.hip chain_kernel MULTI)
 int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid, hipStream_t st,
-                     int xg2 = 0, int f8 = 0, int o2 = 0);
+                     int xg2 = 0, int f8 = 0, int o2 = 0, int n_layers = 1);
 int vwa_gemm(int epi, const GemmParams* p, hipStream_t st);
 int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats, int f8);
 void vwa_gemm_set_split_fill(int pct);  // split-K while tiles x splits < pct % of the CUs (0: bf16 75, fp8 100)

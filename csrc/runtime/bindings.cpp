@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include "grammar.h"
+#include "shm_channel.h"
 
 namespace py = pybind11;
 using namespace vwa;
@@ -52,4 +53,31 @@ PYBIND11_MODULE(_vwa_native, m) {
       .def("min_completion", &Matcher::min_completion)
       .def("canon", [](const Matcher& mt) { return py::bytes(mt.canon()); })
       .def("clone", &Matcher::clone);
+  // TP brain control plane (brain/tp_engine.py): /dev/shm broadcast ring, waits without the GIL
+  py::class_<ShmChannel>(m, "ShmChannel")
+      .def(py::init<const std::string&, int, int64_t, int, bool>(), py::arg("name"), py::arg("n_readers") = 1,
+           py::arg("slot_bytes") = 1 << 20, py::arg("n_slots") = 4, py::arg("create") = false)
+      .def("publish",
+           [](ShmChannel& c, py::bytes b, double timeout_s) {
+             std::string s(b);
+             py::gil_scoped_release rel;
+             return c.publish(s, timeout_s);
+           },
+           py::arg("payload"), py::arg("timeout_s") = 60.0)
+      .def("receive",
+           [](ShmChannel& c, int r, double timeout_s, double dead_s) {
+             std::string s;
+             {
+               py::gil_scoped_release rel;
+               s = c.receive(r, timeout_s, dead_s);
+             }
+             return py::bytes(s);
+           },
+           py::arg("reader"), py::arg("timeout_s") = -1.0, py::arg("dead_s") = 60.0)
+      .def("beat", &ShmChannel::beat)
+      .def("unlink", &ShmChannel::unlink)
+      .def("published", &ShmChannel::published)
+      .def("acked", &ShmChannel::acked)
+      .def_property_readonly("n_readers", &ShmChannel::n_readers)
+      .def_property_readonly("slot_bytes", &ShmChannel::slot_bytes);
 }

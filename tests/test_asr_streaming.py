@@ -227,3 +227,31 @@ def test_vad_threshold_adapts_to_the_noise_floor():
 
     assert len(run(3.0)) == 1
     assert len(run(0.0)) == 0  # (no adaptation: the hiss never ends the utterance)
+
+
+def test_noise_floor_is_capped_and_frozen_inside_utterances():
+    """steady background that creeps up (a TV, soft speech below the threshold) must not
+    walk the adaptive VAD threshold up without bound -- the tracked floor stops at the bootstrap's
+    ceiling (10 x the fixed threshold / noise_mult) and never rises from an utterance's pauses."""
+    import numpy as np
+
+    from voice_enabled_browser_automation_amd.asr.streaming import StreamingAsrSession
+
+    rng = np.random.default_rng(1)
+    s = StreamingAsrSession(_AsyncRec(), partial_every_s=10.0, endpoint_silence_s=0.3, spec_silence_s=0.12,
+                            energy_threshold=100.0, noise_mult=3.0)
+    _feed(s, (rng.standard_normal(int(0.5 * 16000)) * 40).astype(np.int16))  # quiet mic: bootstrap
+    assert 0 < s.noise_floor < 60
+    lvl = 40.0
+    for _ in range(300):  # 30 s of background rising 2 % per 100 ms: it stays "non-speech"
+        lvl *= 1.02
+        _feed(s, (rng.standard_normal(1600) * lvl).astype(np.int16))
+    assert s.noise_floor <= s._floor_cap() + 1e-6 and s._floor_cap() == 10.0 * 100.0 / 3.0
+    # inside an utterance a pause does not raise the floor
+    s2 = StreamingAsrSession(_AsyncRec(), partial_every_s=10.0, endpoint_silence_s=5.0, spec_silence_s=0.0,
+                             energy_threshold=100.0, noise_mult=3.0)
+    _feed(s2, (rng.standard_normal(int(0.5 * 16000)) * 40).astype(np.int16))
+    f0 = s2.noise_floor
+    _feed(s2, _tone(0.5))  # speech
+    _feed(s2, (rng.standard_normal(int(2.0 * 16000)) * 90).astype(np.int16))  # a pause louder than the floor
+    assert s2.speech > 0 and s2.noise_floor <= f0 + 1e-6  # (round 5: +35 % over these 100 frames)

@@ -214,6 +214,55 @@ def test_chained_layer_tail_matches_per_kernel_path(cfg, grid_div, monkeypatch):
         assert err < 0.02 * (1 + b.abs().max().item()), err
 
 
+@pytest.mark.parametrize("cfg,wdtype", [
+    (LlamaConfig(name="t8x4", vocab_size=4096, hidden=4096, n_layers=4, n_heads=32, n_kv_heads=8, head_dim=128,
+                 ffn=14336, max_pos=2048), "bf16"),
+    (LlamaConfig(name="t8x4", vocab_size=4096, hidden=4096, n_layers=4, n_heads=32, n_kv_heads=8, head_dim=128,
+                 ffn=14336, max_pos=2048), "fp8"),
+    (LlamaConfig(name="t70x3", vocab_size=4096, hidden=8192, n_layers=3, n_heads=64, n_kv_heads=8, head_dim=128,
+                 ffn=28672, max_pos=2048), "bf16")],
+    ids=["llama8b-4layers", "llama8b-4layers-fp8", "llama70b-3layers-gqa8"])
+def test_multi_layer_chained_launch_matches_per_layer_launches(cfg, wdtype, monkeypatch):
+    """Layers 0 .. L-2 in ONE chained launch (skinny_stream.hip chain_kernel MULTI: the QKV phase
+    feeds the next layer's attention through an in-launch barrier that only attention workgroups
+    wait on) give the SAME bits as one chained launch per layer, and match the per-kernel path,
+    over steps of 1, 2, 4 and 1 rows and a second session (contexts that differ per row)."""
+    ops.ext()
+    torch.manual_seed(0)
+    toks = torch.randint(0, cfg.vocab_size, (80,)).tolist()
+    model = LlamaModel(cfg, device="cuda", seed=5, wdtype=wdtype)
+    engines = []
+
+    def run(chain: bool, multi: bool):
+        monkeypatch.setenv("VWA_CHAIN", "1" if chain else "0")
+        monkeypatch.setenv("VWA_CHAIN_MULTI", "1" if multi else "0")
+        model.reset_chains()
+        e = LLMEngine(model, max_seqs=2, max_model_len=512, kv_blocks=40, block_size=16)
+        engines.append(e)
+        s = e.new_sequence(toks[:40], use_prefix_cache=False)
+        s2 = e.new_sequence(toks[5:23], use_prefix_cache=False)
+        e.prefill(s)
+        e.prefill(s2)
+        out, i = [], 40
+        for rows in ([(s, toks[40])], [(s, toks[41]), (s2, toks[42])], [(s, t) for t in toks[43:47]],
+                     [(s2, toks[47])], [(s, toks[48])]):
+            out.append(e.run_rows(rows).float().cpu().clone())
+        return out
+
+    ref = run(False, False)
+    per_layer = run(True, False)
+    got = run(True, True)
+    assert not model.chain_error()
+    multis = [v for d in model._chains.values() for k, v in d.items() if k[0] == "multi"]
+    # (70B shapes at 3-4 rows chain the tail without the attention phase: those steps stay per layer)
+    assert any(v is not None and v[3] == cfg.n_layers - 1 for v in multis), "no multi-layer launch"
+    for a, b in zip(got, per_layer):
+        assert torch.equal(a, b), (a - b).abs().max().item()
+    for a, b in zip(got, ref):
+        err = (a - b).abs().max().item()
+        assert math.isfinite(err) and err < 0.03 * (1 + b.abs().max().item()), err
+
+
 @pytest.mark.parametrize("grid_div,max_len", [(1, 256), (8, 512)], ids=["full-grid", "griddiv8"])
 def test_llama70b_shape_chained_layers_match_f32_reference(grid_div, max_len, monkeypatch):
     """Llama-3-70B layer shapes (hidden 8192, 64 q / 8 kv heads -> GQA 8:1, FFN 28672; BASELINE

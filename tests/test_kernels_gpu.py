@@ -993,16 +993,19 @@ def test_rms_statistics_handoff(M, wdt):
 
 @pytest.mark.parametrize("hd", [64, 128])
 @pytest.mark.parametrize("causal", [False, True])
-def test_flash_attention_is_bitwise_reproducible(hd, causal):
-    """The same inputs give the same output bits on every launch (a D = 64 form that read all of a
-    tile's LDS fragments up front varied by 1-2 ulps from run to run and was removed)."""
+@pytest.mark.parametrize("qmul", [1.0, 8.0])
+def test_flash_attention_is_bitwise_reproducible(hd, causal, qmul):
+    """The same inputs give the same output bits on every launch.  qmul = 8: scores scaled x8 (the
+    'extreme' inputs on which round 5's D = 64 kernel still varied by 1-2 ulps -- its inline-asm
+    v_max3 read the last MFMA's accumulators inside the hazard window, common.h vmax3)."""
     T, H = 700, 4
     qkv = rnd(1, T, 3, H, hd)
     q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    q = (q.float() * qmul).to(BF)
     table = torch.zeros(1, 1, dtype=torch.int32, device=DEV)
     outs = [ops.flash_attention(q, ops.KVLayout.contiguous(k, v, table), Sk=T, n_kv_heads=H, causal=causal,
-                                scale=hd ** -0.5).clone() for _ in range(4)]
+                                scale=hd ** -0.5).clone() for _ in range(10)]
     assert all(torch.equal(outs[0], o) for o in outs[1:])
     ref_o = torch.nn.functional.scaled_dot_product_attention(
         q.float().transpose(1, 2), k.float().transpose(1, 2), v.float().transpose(1, 2), is_causal=causal).transpose(1, 2)
-    close(outs[0], ref_o, 2e-2)
+    close(outs[0], ref_o, 2e-2 * qmul)

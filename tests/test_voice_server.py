@@ -327,3 +327,148 @@ def test_local_agreement_commits_stable_prefix():
         assert b[: len(a)] == a
     assert fin[0]["is_final"] and fin[0]["channel"]["alternatives"][0]["transcript"].startswith("1 2")
     assert s.committed == [] and s.stats["committed_tokens"] > 0
+
+
+class ScriptedAsr:
+    """Each binary frame is a command: b"S" speech (re)starts, b"P:<text>" the speculative final
+    pass finished with <text> (the on_speculative callback), b"F:<text>" a final, else nothing."""
+
+    def __init__(self):
+        self.vad_events = False
+        self.on_speculative = None
+
+    def push(self, data):
+        d = bytes(data)
+        if d == b"S":
+            return [{"type": "SpeechStarted", "channel": [0, 1], "timestamp": 0.0}] if self.vad_events else []
+        if d.startswith(b"P:"):
+            if self.on_speculative is not None:
+                self.on_speculative(d[2:].decode())
+            return []
+        if d.startswith(b"F:"):
+            return [results_event(d[2:].decode(), is_final=True, start=0, duration=1.0, model="fake")]
+        return []
+
+    def flush(self):
+        return []
+
+
+def _policy_app(brain_calls, exec_calls, brain_delay=0.0, **kw):
+    async def brain(req):
+        body = await req.json()
+        brain_calls.append(body["text"])
+        await asyncio.sleep(brain_delay)
+        return web.json_response({"version": "1.0", "intents": [
+            {"type": "search", "args": {"query": body["text"]}, "priority": 0, "requires_confirmation": False,
+             "retries": 1}], "context_updates": {}, "confidence": 0.9})
+
+    async def execute(req):
+        exec_calls.append(await req.json())
+        return web.json_response({"session_id": "s", "results": [], "artifacts": {}})
+
+    bapp, eapp = web.Application(), web.Application()
+    bapp.router.add_post("/parse", brain)
+    eapp.router.add_post("/execute", execute)
+    return bapp, eapp
+
+
+def test_pause_inside_a_command_is_not_a_command_boundary():
+    """speech that resumes after an ASR final (a 300-600 ms pause inside a
+    command) holds the pending text -- the brain gets ONE merged command, one intent frame."""
+    brain_calls, exec_calls = [], []
+
+    async def go():
+        bapp, eapp = _policy_app(brain_calls, exec_calls)
+        async with TestServer(bapp) as bs, TestServer(eapp) as es:
+            vapp = build_app(lambda: ScriptedAsr(), brain_url=str(bs.make_url("/parse")),
+                             executor_url=str(es.make_url("")).rstrip("/"), debounce_ms=0, commit_ms=700,
+                             spec_brain=False)
+            async with TestClient(TestServer(vapp)) as c:
+                ws = await c.ws_connect("/stream")
+                await ws.receive()
+                await ws.receive()
+                await ws.send_bytes(b"S")
+                await ws.send_bytes(b"F:search for")      # the ASR endpoint after "search for"
+                await asyncio.sleep(0.2)                  # (inside the 700 ms commit window)
+                await ws.send_bytes(b"S")                 # ... the user goes on
+                await asyncio.sleep(0.6)                  # longer than the window: still held
+                assert brain_calls == []
+                await ws.send_bytes(b"F:wireless earbuds")
+                got = await _recv_types(ws, ["intent"])
+                intents = [g for g in got if g["type"] == "intent"]
+                assert len(intents) == 1 and brain_calls == ["search for wireless earbuds"]
+                await ws.close()
+                m = (await (await c.get("/metrics")).json())["counters"]
+                assert m["commits_held"] == 1 and m["commands"] == 1
+
+    asyncio.run(go())
+
+
+def test_speculative_brain_is_used_only_for_the_committed_text():
+    """VWA_SPEC_BRAIN: the brain starts on the speculative final pass; its answer is delivered when
+    the final confirms the same text (no second call), and dropped when speech resumed."""
+    brain_calls, exec_calls = [], []
+
+    async def go():
+        bapp, eapp = _policy_app(brain_calls, exec_calls, brain_delay=0.3)
+        async with TestServer(bapp) as bs, TestServer(eapp) as es:
+            vapp = build_app(lambda: ScriptedAsr(), brain_url=str(bs.make_url("/parse")),
+                             executor_url=str(es.make_url("")).rstrip("/"), debounce_ms=0, commit_ms=0,
+                             spec_brain=True)
+            async with TestClient(TestServer(vapp)) as c:
+                ws = await c.ws_connect("/stream")
+                await ws.receive()
+                await ws.receive()
+                loop = asyncio.get_running_loop()
+                await ws.send_bytes(b"S")
+                await ws.send_bytes(b"P:scroll down")
+                await asyncio.sleep(0.2)
+                t0 = loop.time()
+                await ws.send_bytes(b"F:scroll down")
+                got = await _recv_types(ws, ["intent"])
+                assert loop.time() - t0 < 0.25, "the final waited for a full brain call"
+                assert brain_calls == ["scroll down"]
+                assert next(g for g in got if g["type"] == "intent")["payload"]["intents"][0]["args"]["query"] == \
+                    "scroll down"
+                # resumed speech after the speculative pass: that answer is never delivered
+                await ws.send_bytes(b"S")
+                await ws.send_bytes(b"P:go")
+                await ws.send_bytes(b"S")
+                await ws.send_bytes(b"F:go back")
+                got = await _recv_types(ws, ["intent"])
+                intents = [g for g in got if g["type"] == "intent"]
+                assert [i["payload"]["intents"][0]["args"]["query"] for i in intents] == ["go back"]
+                assert brain_calls == ["scroll down", "go", "go back"]
+                await ws.close()
+                m = (await (await c.get("/metrics")).json())["counters"]
+                assert m["spec_brain_used"] == 1 and m["spec_brain_dropped"] == 1 and m["commands"] == 2
+
+    asyncio.run(go())
+
+
+def test_disconnect_during_a_brain_call_still_executes_its_safe_intents():
+    """a command whose brain call is in flight when the client disconnects still reaches
+    the executor (the queue's end marker goes in after it, not before)."""
+    brain_calls, exec_calls = [], []
+
+    async def go():
+        bapp, eapp = _policy_app(brain_calls, exec_calls, brain_delay=0.5)
+        async with TestServer(bapp) as bs, TestServer(eapp) as es:
+            vapp = build_app(lambda: ScriptedAsr(), brain_url=str(bs.make_url("/parse")),
+                             executor_url=str(es.make_url("")).rstrip("/"), debounce_ms=0, commit_ms=0,
+                             spec_brain=False)
+            async with TestClient(TestServer(vapp)) as c:
+                ws = await c.ws_connect("/stream")
+                await ws.receive()
+                await ws.receive()
+                await ws.send_bytes(b"F:sort by price")
+                await asyncio.sleep(0.15)  # the brain call is in flight
+                await ws.close()
+                for _ in range(40):
+                    if exec_calls:
+                        break
+                    await asyncio.sleep(0.05)
+                assert brain_calls == ["sort by price"]
+                assert exec_calls and exec_calls[0]["intents"][0]["args"]["query"] == "sort by price"
+
+    asyncio.run(go())

@@ -20,7 +20,9 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)) % torch.cuda.device_count())
-    ar = OneShotAllReduce(rank, world, dist.group.WORLD, max_elems=64 * 4096)
+    ar = OneShotAllReduce(rank, world, dist.group.WORLD, max_elems=64 * 4096)  # (preflight + self-test inside)
+    if os.environ.get("VWA_AR_CHECK_REPORT") and rank == 0:
+        print("PREFLIGHT", ar.peer_report, flush=True)
     ok = True
     for n in (4096, 8 * 4096, 64 * 4096, 1000 * 8):
         torch.manual_seed(100 + n)

@@ -39,6 +39,9 @@ def main():
                     help="(--attn) every launch derives the attention partition itself (no step plan)")
     ap.add_argument("--no-stamps", action="store_true",
                     help="launch without the per-phase stamps (their stores and waits slow the phases slightly)")
+    ap.add_argument("--multi", type=int, default=0,
+                    help="(--attn) also time N layers as ONE launch (chain_kernel MULTI; each layer its own K/V "
+                         "cache, weights rotating over the copies): reports multi_layer_us = launch / N")
     a = ap.parse_args()
     if a.no_wait:
         a.bar_mode = 5 if a.bar_mode >= 4 else 3
@@ -140,6 +143,36 @@ def main():
         ops.qkv_rope_write(h, w["qkv"], None, fuse_rms=True, eps=1e-5, n_q_heads=nq, n_kv_heads=nkv, head_dim=hd,
                            rope=rope, positions=pos, slots=slots, q_out=q, k_cache=kc, v_cache=vc)
 
+    multi_us = None
+    if a.multi > 1 and a.attn:
+        # N layers, layer i on weight copy i % ncopy and its own paged K/V (same table); layer 0
+        # writes the step plan, layers 1.. read it (as the engine's multi-layer launch)
+        mplan = torch.zeros(1024 * 16, dtype=torch.int32, device=dev)
+        kvs = [(torch.randn_like(akw["a_k"]) * 0.5, torch.randn_like(akw["a_v"])) for _ in range(a.multi + 1)]
+        mds = []
+        for li in range(a.multi):
+            w = Ws[li % ncopy]
+            kw = dict(akw, a_k=kvs[li][0], a_v=kvs[li][1])
+            mds.append(E.chain_make(h, att, act, wt(w, "o"), wt(w, "gu"), wt(w, "down"), 1e-5, wt(w, "qkv"), nq, nkv,
+                                    hd, pos, slots, rope, q, kvs[li + 1][0], kvs[li + 1][1], bar, work, None, a.bar_mode,
+                                    **kw, w_tiled=a.tiled, **sck[li % ncopy], a_plan=mplan,
+                                    a_plan_mode=1 if li == 0 else 2))
+        mcat = torch.cat([d[0] for d in mds])
+        mlds = mds[0][1]
+
+        def multi():
+            E.chain_run(mcat, 4, mlds, h, ag, 0, a.multi)
+
+        def per_layer():
+            for d in mds:
+                E.chain_run(d[0], 4, d[1], h, ag)
+
+        multi()
+        torch.cuda.synchronize()
+        assert int(bar.view(torch.int64)[160].item()) == 0, "barrier timeout (multi)"
+        multi_us = timeit(multi) / a.multi
+        per_layer_us = timeit(per_layer) / a.multi
+        assert int(bar.view(torch.int64)[160].item()) == 0, "barrier timeout (multi)"
     chained()  # one launch first: a broken barrier shows up as the error word, not a long run
     torch.cuda.synchronize()
     assert int(bar.view(torch.int64)[160].item()) == 0, "barrier timeout"
@@ -198,6 +231,8 @@ def main():
                         ph[pn] = [round(float((col.median() - t0) * 10e-3), 2), round(float((col.max() - t0) * 10e-3), 2),
                                   int(col.numel())]
                 r[nm + "_phase"] = ph
+    if multi_us is not None:
+        r.update(multi_layers=a.multi, multi_layer_us=round(multi_us, 2), per_layer_launch_us=round(per_layer_us, 2))
     r["env"] = {k: v for k, v in os.environ.items() if k.startswith("VWA_CHAIN")}
     r["layer_us"] = round(float(mx[-1]), 2)
     print(json.dumps(r), flush=True)

@@ -2,7 +2,7 @@
 ``intent`` frame over WS ``/stream``, with the brain and voice services as separate processes on
 the GPU(s) they would get from launch.py and a stub executor.
 
-    python tools/service_bench.py --sessions 1,8 --debounce 0,1000 --chain 1,0 --json out.jsonl
+    python tools/service_bench.py --sessions 1,8 --debounce 0,1000 --commit 0,700 --chain 1,0 --json out.jsonl
 
 Per (chain, debounce, sessions): every session opens ``/stream``, sets the page context, then
 streams utterances of ``--audio-s`` seconds of synthetic speech as 60 ms PCM16 packets paced in
@@ -47,8 +47,36 @@ def free_port() -> int:
     return p
 
 
+def paused_speech(seconds: float, seed: int, max_pause_ms: float = 650.0, rate: int = 16000) -> np.ndarray:
+    """A spoken command with pauses: voiced words of 0.25-0.7 s separated by gaps of 0.1 s to
+    ``max_pause_ms`` (the first two >= 300 ms, i.e. longer than the ASR endpoint -- the pauses a
+    speaker makes inside one command), ending on a word; silence is a low noise floor."""
+    rng = np.random.default_rng(seed)
+    n = int(seconds * rate)
+    out = (rng.standard_normal(n) * 30).astype(np.float64)
+    t, words = 0.0, []
+    while True:
+        w = rng.uniform(0.25, 0.7)
+        if t + w > seconds:
+            break
+        words.append((t, t + w))
+        t += w
+        lo = 0.3 if len(words) <= 2 else 0.1  # the first two gaps are longer than the endpoint
+        g = rng.uniform(lo, max(lo, max_pause_ms / 1000.0))
+        if t + g + 0.25 > seconds:
+            break
+        t += g
+    for a, b in words:
+        i, j = int(a * rate), int(b * rate)
+        seg = synth_speech(b - a, seed=int(rng.integers(1 << 30)), rate=rate)[: j - i].astype(np.float64)
+        out[i : i + len(seg)] += seg
+    end = int(words[-1][1] * rate)
+    return np.clip(out[:end], -32767, 32767).astype(np.int16)
+
+
 def synth_speech(seconds: float, seed: int, rate: int = 16000) -> np.ndarray:
-    """Voiced syllables with short pauses (< the 0.6 s VAD endpoint), as bench.py's generator."""
+    """Continuously voiced syllables (amplitude envelope >= 0.35 everywhere: NO pauses -- one
+    word's signal for paused_speech, or a pause-free utterance)."""
     rng = np.random.default_rng(seed)
     t = np.arange(int(seconds * rate)) / rate
     f0 = 110 + 30 * np.sin(2 * np.pi * 0.3 * t + rng.uniform(0, 6))
@@ -110,7 +138,13 @@ async def start_stub_executor():
     return runner, port
 
 
-async def session(url: str, idx: int, n_utt: int, audio_s: float, out: list) -> None:
+async def session(url: str, idx: int, n_utt: int, audio_s: float, out: list, max_pause_ms: float = 0.0,
+                  gap_s: float = 1.5) -> None:
+    """One microphone: utterances of ``audio_s`` s (``max_pause_ms`` > 0: paused_speech), packets
+    sent at the END of their 60 ms (a packet exists only once it is captured: App.tsx:279-288
+    sends when >= 60 ms have accumulated), ``gap_s`` of silence between utterances.  Per
+    utterance: the first intent frame after the speech end, and every intent frame the utterance
+    produced -- more than one, or one before the speech ended, is a split command."""
     import aiohttp
 
     pkt = 960  # 60 ms at 16 kHz
@@ -118,7 +152,7 @@ async def session(url: str, idx: int, n_utt: int, audio_s: float, out: list) -> 
     async with aiohttp.ClientSession() as s:
         async with s.ws_connect(url, max_msg_size=0) as ws:
             await ws.send_str(json.dumps({"type": "context_update", "payload": {"url": "https://www.bestbuy.com"}}))
-            marks: dict = {}
+            marks: dict = {"intents": [], "finals": []}
             got = asyncio.Event()
 
             async def reader():
@@ -127,41 +161,54 @@ async def session(url: str, idx: int, n_utt: int, audio_s: float, out: list) -> 
                         continue
                     f = json.loads(msg.data)
                     now = time.perf_counter()
-                    if f["type"] == "transcript_final" and "final" not in marks:
-                        marks["final"] = now
+                    if f["type"] == "transcript_final":
+                        marks["finals"].append(now)
                     elif f["type"] == "intent":
-                        marks["intent"] = now
+                        marks["intents"].append(now)
                         marks["valid"] = isinstance(f.get("payload"), dict) and "intents" in f["payload"]
-                        got.set()
+                        if marks.get("t_end") is not None:
+                            got.set()
 
             rd = asyncio.ensure_future(reader())
             t_next = time.perf_counter()
+
+            async def send_paced(chunk: bytes):
+                nonlocal t_next
+                t_next += pkt / 16000
+                await asyncio.sleep(max(0.0, t_next - time.perf_counter()))  # captured, then sent
+                await ws.send_bytes(chunk)
+
             for u in range(n_utt):
-                pcm = synth_speech(audio_s, seed=1000 * idx + u)
-                marks.clear()
+                seed = 1000 * idx + u
+                pcm = paused_speech(audio_s, seed, max_pause_ms) if max_pause_ms > 0 else synth_speech(audio_s, seed)
+                marks.update(intents=[], finals=[], t_end=None, valid=False)
                 got.clear()
                 for i in range(0, len(pcm), pkt):
-                    await ws.send_bytes(pcm[i : i + pkt].tobytes())
-                    t_next += pkt / 16000
-                    await asyncio.sleep(max(0.0, t_next - time.perf_counter()))
-                t_end = time.perf_counter()
+                    await send_paced(pcm[i : i + pkt].tobytes())
+                t_end = time.perf_counter()  # the packet holding the last speech samples is sent
+                marks["t_end"] = t_end
+                if any(t >= t_end for t in marks["intents"]):
+                    got.set()
                 deadline = t_end + 30.0
                 while not got.is_set() and time.perf_counter() < deadline:  # the mic keeps sending silence
-                    await ws.send_bytes(silence)
-                    t_next += pkt / 16000
-                    await asyncio.sleep(max(0.0, t_next - time.perf_counter()))
-                if got.is_set():
-                    fin = marks.get("final", marks["intent"])
+                    await send_paced(silence)
+                for _ in range(int(gap_s / 0.06)):  # silence between utterances (late split intents land here)
+                    await send_paced(silence)
+                after = [t for t in marks["intents"] if t >= t_end]
+                if after:
+                    t_int = after[0]
+                    fins = [t for t in marks["finals"] if t <= t_int]
+                    fin = fins[-1] if fins else t_int
                     out.append({"session": idx, "utt": u, "valid": marks.get("valid", False),
+                                "intent_frames": len(marks["intents"]),
+                                "split": len(marks["intents"]) > 1 or len(after) < len(marks["intents"]),
+                                "finals": len(marks["finals"]),
                                 "speech_end_to_final_ms": (fin - t_end) * 1e3,
-                                "final_to_intent_ms": (marks["intent"] - fin) * 1e3,
-                                "speech_end_to_intent_ms": (marks["intent"] - t_end) * 1e3})
+                                "final_to_intent_ms": (t_int - fin) * 1e3,
+                                "speech_end_to_intent_ms": (t_int - t_end) * 1e3})
                 else:
-                    out.append({"session": idx, "utt": u, "timeout": True})
-                for _ in range(8):  # ~0.5 s of silence between utterances
-                    await ws.send_bytes(silence)
-                    t_next += pkt / 16000
-                    await asyncio.sleep(max(0.0, t_next - time.perf_counter()))
+                    out.append({"session": idx, "utt": u, "timeout": True,
+                                "intent_frames": len(marks["intents"]), "split": bool(marks["intents"])})
             await ws.send_str(json.dumps({"type": "close"}))
             rd.cancel()
 
@@ -188,29 +235,38 @@ async def run_matrix(a) -> list:
                 t0 = time.time()
                 await wait_health(f"http://127.0.0.1:{bport}/health", brain, a.load_timeout)
                 brain_load_s = time.time() - t0
-                for deb in a.debounce:
+                for deb, commit in [(d, c) for d in a.debounce for c in a.commit]:
                     vport = free_port()
                     venv = {"VWA_ASR_ENGINE": a.asr_engine, "VWA_ASR_MODEL": a.asr, "VOICE_PORT": str(vport),
                             "BRAIN_URL": f"http://127.0.0.1:{bport}/parse",
                             "EXECUTOR_URL": f"http://127.0.0.1:{ex_port}", "VWA_DEBOUNCE_MS": deb,
                             "HIP_VISIBLE_DEVICES": a.voice_gpu, "VWA_MAX_SESSIONS": str(max(a.sessions)),
                             "VWA_ASR_TOKENS_PER_S": str(a.asr_tokens_per_s),
-                            "VWA_ENDPOINT_MS": str(a.endpoint_ms), "VWA_SPEC_FINAL_MS": str(a.spec_ms)}
-                    voice = spawn(f"{PKG}.voice.server", venv, os.path.join(logs, f"voice_chain{chain}_deb{deb}.log"))
+                            "VWA_ENDPOINT_MS": str(a.endpoint_ms), "VWA_SPEC_FINAL_MS": str(a.spec_ms),
+                            "VWA_COMMIT_MS": str(commit), "VWA_SPEC_BRAIN": a.spec_brain}
+                    voice = spawn(f"{PKG}.voice.server", venv,
+                                  os.path.join(logs, f"voice_chain{chain}_deb{deb}_commit{commit}.log"))
                     try:
                         await wait_health(f"http://127.0.0.1:{vport}/health", voice, a.load_timeout)
                         url = f"http://127.0.0.1:{vport}/stream"
                         # warm-up: one utterance (graph captures, prefix cache of the prompt head)
-                        await session(url, 99, 1, a.audio_s, [])
+                        await session(url, 99, 1, a.audio_s, [], a.max_pause_ms)
                         for n in a.sessions:
                             out: list = []
                             t0 = time.perf_counter()
-                            await asyncio.gather(*(session(url, i, a.utterances, a.audio_s, out) for i in range(n)))
+                            await asyncio.gather(*(session(url, i, a.utterances, a.audio_s, out, a.max_pause_ms)
+                                                   for i in range(n)))
                             wall = time.perf_counter() - t0
                             ok = [r for r in out if not r.get("timeout")]
                             e2i = [r["speech_end_to_intent_ms"] for r in ok]
-                            rec = {"what": "service_latency", "chain": chain, "debounce_ms": float(deb), "sessions": n,
+                            rec = {"what": "service_latency", "chain": chain, "debounce_ms": float(deb),
+                                   "commit_ms": float(commit), "spec_brain": a.spec_brain, "sessions": n,
+                                   "speech": f"paused (<= {a.max_pause_ms:g} ms gaps)" if a.max_pause_ms > 0
+                                   else "continuous", "packet_timing": "end of packet",
                                    "utterances": len(out), "timeouts": len(out) - len(ok),
+                                   "split_commands": sum(bool(r.get("split")) for r in out),
+                                   "intent_frames": sum(r.get("intent_frames", 0) for r in out),
+                                   "asr_finals_per_utterance": pct([r["finals"] for r in ok], 50),
                                    "valid_intents": f"{sum(r['valid'] for r in ok)}/{len(out)}",
                                    "audio_s": a.audio_s, "asr": a.asr, "llm": a.llm, "dtype": a.dtype,
                                    "endpoint_ms": a.endpoint_ms, "spec_final_ms": a.spec_ms,
@@ -246,6 +302,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sessions", default="1,8")
     ap.add_argument("--debounce", default="0,1000")
+    ap.add_argument("--commit", default="0", help="voice VWA_COMMIT_MS values (silence that ends a command)")
+    ap.add_argument("--spec-brain", default="1", help="voice VWA_SPEC_BRAIN")
+    ap.add_argument("--max-pause-ms", type=float, default=650.0,
+                    help="paused speech: longest pause inside a command (0: continuous speech, round 5's)")
     ap.add_argument("--chain", default="0", help="brain VWA_CHAIN (the single-GPU deployment default: 0)")
     ap.add_argument("--utterances", type=int, default=20, help="utterances per session per point")
     ap.add_argument("--endpoint-ms", type=float, default=knob("VWA_ENDPOINT_MS"))
@@ -264,6 +324,7 @@ def main():
     a = ap.parse_args()
     a.sessions = [int(x) for x in a.sessions.split(",")]
     a.debounce = a.debounce.split(",")
+    a.commit = a.commit.split(",")
     a.chain = a.chain.split(",")
     res = asyncio.run(run_matrix(a))
     if a.json:

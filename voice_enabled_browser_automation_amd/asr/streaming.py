@@ -145,6 +145,13 @@ class StreamingAsrSession:
         self.stats: Dict[str, float] = {"partials": 0, "finals": 0, "asr_ms": 0.0, "passes": 0,
                                         "committed_tokens": 0, "spec_started": 0, "spec_used": 0,
                                         "spec_discarded": 0}
+        # on_speculative(text): called (from the recognizer's thread) when a speculative final pass
+        # finishes while it still covers the utterance -- the voice server starts the brain on it
+        # (voice/server.py: the brain's latency then overlaps the rest of the endpoint wait)
+        self.on_speculative: Optional[Callable[[str], None]] = None
+        # vad_events (Deepgram's live option of that name, off by default there too): push() also
+        # returns {"type": "SpeechStarted"} when speech begins or resumes after a speculative final
+        self.vad_events = False
 
     # ------------------------------------------------------------------ internals
     @property
@@ -180,6 +187,11 @@ class StreamingAsrSession:
             self.noise_floor = max(self.noise_floor, med)
         self._boot = None
 
+    def _floor_cap(self) -> float:
+        """The highest noise floor the VAD tracks: the bootstrap's own ceiling (mult x floor <= 10 x
+        the fixed threshold)."""
+        return 10.0 * self.thresh / self.noise_mult if self.noise_mult > 0.0 else 0.0
+
     def _reset_utterance(self) -> None:
         self.t_offset += self._n / self.rate
         self._n = 0
@@ -198,7 +210,18 @@ class StreamingAsrSession:
         """The final pass, started during the trailing silence (see module docstring)."""
         self.stats["spec_started"] += 1
         self._spec_t0 = time.perf_counter()
-        self._spec = recognize_async(self.rec, self.buf.copy(), self.committed if self.local_agreement else ())
+        fut = recognize_async(self.rec, self.buf.copy(), self.committed if self.local_agreement else ())
+        self._spec = fut
+        if self.on_speculative is not None:
+            fut.add_done_callback(self._spec_ready)
+
+    def _spec_ready(self, fut: Future) -> None:
+        if self._spec is not fut or fut.cancelled() or fut.exception() is not None:
+            return  # (speech resumed meanwhile, or a failed pass: the endpoint runs the final itself)
+        try:
+            self.on_speculative(fut.result().text)
+        except Exception:  # noqa: BLE001  (a listener failure must not break recognition)
+            pass
 
     def _final(self, use_spec: bool = True) -> List[Dict]:
         out: List[Dict] = []
@@ -254,15 +277,26 @@ class StreamingAsrSession:
             rms = float(np.sqrt(np.mean(fr.astype(np.float32) ** 2)))
             self._track_floor(rms)
             if rms >= max(self.thresh, self.noise_mult * self.noise_floor):
+                if self.vad_events and (self.speech == 0 or self._spec is not None):
+                    # Deepgram's VAD event (vad_events): speech begins -- a new utterance, or the
+                    # speaker resumed after a speculative final (the voice server holds / drops
+                    # what it started on the previous words: voice/server.py commit policy)
+                    events.append({"type": "SpeechStarted", "channel": [0, 1],
+                                   "timestamp": round(self.t_offset + self._n / self.rate, 3)})
                 self.speech += len(fr)
                 self.trailing_silence = 0
                 self._drop_spec()  # speech resumed: the speculative final no longer covers the utterance
             else:
                 self.trailing_silence += len(fr)
-                # non-speech frames: the floor falls fast to quieter frames, rises slowly (0.3 % / frame)
+                # non-speech frames: the floor falls fast to quieter frames, rises slowly (0.3 % /
+                # frame) and only between utterances (never from an utterance's own pauses), capped
+                # at the bootstrap's ceiling -- steady soft speech or a TV in the background cannot
+                # walk the threshold up until quiet speakers stop being detected
                 if self.noise_floor > 0.0:
-                    self.noise_floor = (0.8 * self.noise_floor + 0.2 * rms if rms < self.noise_floor
-                                        else min(rms, self.noise_floor * 1.003))
+                    if rms < self.noise_floor:
+                        self.noise_floor = 0.8 * self.noise_floor + 0.2 * rms
+                    elif self.speech == 0:
+                        self.noise_floor = min(rms, self.noise_floor * 1.003, self._floor_cap())
             if self.speech > 0:
                 self.since_partial += len(fr)
             if self.speech >= self.min_speech and self.trailing_silence >= self.endpoint:

@@ -8,8 +8,11 @@ vocab-parallel sampler's partial-maxima exchange) that only match up if all rank
 step.  So:
 
 * rank 0 serves HTTP; ``submit_async`` queues a request (chat messages + a Future);
-* rank 0's scheduler thread, once per iteration, broadcasts over the CPU (gloo) control group the
-  requests it admits in that iteration (possibly none) and a stop flag;
+* rank 0's scheduler thread, once per iteration, sends the other ranks the requests it admits in
+  that iteration (possibly none) and a stop flag -- through a /dev/shm ring (parallel/control.py,
+  csrc/runtime/shm_channel.cpp; one TP group is one node), not a gloo broadcast: the message is on
+  the critical path of every decode iteration (gloo only carries the setup and oversize payloads;
+  ``VWA_TP_CONTROL=gloo`` restores the round-5 broadcast);
 * every rank appends those requests to its own ``LLMIntentEngine`` queue in the same order and
   runs the identical ``step()`` -- batched admission prefill, one ragged forward for all active
   requests, vocab-parallel sampling.  Sampling is deterministic given the step's inputs and the
@@ -77,6 +80,10 @@ class TPIntentEngine:
         self.control_msgs = 0
         self.heartbeats = 0
         self.heartbeat_s = HEARTBEAT_S if heartbeat_s is None else heartbeat_s
+        from ..parallel.control import make_channel
+
+        # collective over the TP group (every rank builds its TPIntentEngine at the same point)
+        self.chan = make_channel(tp.rank, tp.size, self.ctl)
 
     # ------------------------------------------------------------------ shared
     @property
@@ -101,23 +108,16 @@ class TPIntentEngine:
         return out
 
     def _exchange(self, new_msgs: Optional[List[List[dict]]] = None, stop: bool = False):
-        """One control message per iteration: a 2-int header (admission count, stop) over the gloo
-        group, then -- only when something is admitted -- the pickled chat messages.  Rank 0
-        passes its decision; the other ranks receive it.  -> (messages list, stop)."""
-        import torch
-        import torch.distributed as dist
-
-        lead = self.tp.rank == 0
-        hdr = torch.tensor([len(new_msgs or []), int(stop)] if lead else [0, 0], dtype=torch.int64)
-        dist.broadcast(hdr, src=0, group=self.ctl)
+        """One control message per iteration (the admitted chat messages, the stop flag) over the
+        group's control channel.  Rank 0 passes its decision; the other ranks receive it.
+        -> (messages list, stop)."""
+        if self.tp.rank == 0:
+            msg = (list(new_msgs or []), bool(stop))
+            self.chan.send(msg)
+        else:
+            msg = self.chan.recv()
         self.control_msgs += 1
-        n, stop = int(hdr[0]), bool(hdr[1])
-        msgs = list(new_msgs or []) if lead else []
-        if n:
-            box = [msgs if lead else None]
-            dist.broadcast_object_list(box, src=0, group=self.ctl)
-            msgs = box[0]
-        return msgs, stop
+        return msg[0], msg[1]
 
     def _iteration(self, new: List[Tuple[List[dict], Future]]) -> None:
         """Identical on every rank: queue this iteration's admissions, run one scheduler step."""

@@ -559,12 +559,13 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     return out
 
 
-SS_SCALE = 65536.0  # RMS statistics hand-off: u64 fixed point in 2^-16 units (GemmParams::ss_*)
+SS_SCALE = 16777216.0  # RMS statistics hand-off: u64 fixed point in 2^-24 units (GemmParams::ss_*)
 
 
 def ss_fixed(sq: torch.Tensor) -> torch.Tensor:
-    """f32 sums of squares -> the hand-off's int64 fixed point (2^-16 units, truncated)."""
-    return (sq.float() * SS_SCALE).clamp(max=1.8e19).to(torch.int64)
+    """f32 sums of squares -> the hand-off's int64 fixed point (2^-24 units, rounded to nearest as
+    gemm.hip ss_fix does; clamped below the int64 maximum)."""
+    return torch.floor(sq.float() * SS_SCALE + 0.5).clamp(max=9.2e18).to(torch.int64)
 
 
 def ss_float(ss: torch.Tensor) -> torch.Tensor:

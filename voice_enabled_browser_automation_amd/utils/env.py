@@ -93,6 +93,8 @@ class Settings(BaseModel):
     VWA_WATCHDOG_S: float = Field(2.0, description="DP router: health poll period")
     VWA_WATCHDOG_FAILS: int = Field(2, description="DP router: failed polls before a worker is declared dead")
     VWA_TP_HEARTBEAT_S: float = Field(5.0, description="idle TP leader control heartbeat")
+    VWA_TP_CONTROL: str = Field("shm", description="TP brain per-iteration control channel: shm (/dev/shm ring, parallel/control.py) or gloo (broadcast)")
+    VWA_TP_DEAD_S: float = Field(60.0, description="TP worker: the leader counts as dead after this long without a control message or heartbeat (shm channel)")
     VWA_DIST_BACKEND: Optional[str] = Field(None, description="torch.distributed backend override (nccl = RCCL)")
     VWA_CUSTOM_AR: bool = Field(True, description="one-shot IPC all-reduce for small TP messages (else RCCL)")
     VWA_BROWSER_DRIVER: str = Field("auto", description="executor browser driver: auto | cdp | playwright")
@@ -101,6 +103,8 @@ class Settings(BaseModel):
     VWA_GPT2_TOKENIZER: Optional[str] = Field(None, description="tokenizer.json for the GPT-2 brain (bundled otherwise)")
     # ---- voice path (streaming ASR / debounce)
     VWA_DEBOUNCE_MS: float = Field(1000.0, description="final transcript -> brain call debounce (reference: 1000)")
+    VWA_COMMIT_MS: float = Field(0.0, description="voice: silence after the speech end before pending finals are a command (0: the ASR endpoint; speech resuming earlier holds them -- voice/server.py commit policy)")
+    VWA_SPEC_BRAIN: bool = Field(True, description="voice: start the brain on the ASR's speculative final pass (its answer is used only for exactly that text)")
     VWA_ENDPOINT_MS: float = Field(300.0, description="trailing silence that ends an utterance (VAD endpoint)")
     VWA_SPEC_FINAL_MS: float = Field(120.0, description="trailing silence that starts the speculative final pass (0: off)")
     VWA_VAD_THRESHOLD: float = Field(300.0, description="speech frame RMS floor (PCM16 units)")
@@ -130,6 +134,7 @@ class Settings(BaseModel):
     VWA_CHAIN_ASR: bool = Field(False, description="chained Whisper decoder launches (measured slower; off)")
     VWA_CHAIN_GRID_DIV: Optional[str] = Field(None, description="chained launch on CUs / k workgroups (shared GPU)")
     VWA_CHAIN_PLAN: bool = Field(True, description="chained attention: layer 0 writes the step's work plan, layers 1.. read it")
+    VWA_CHAIN_MULTI: bool = Field(True, description="chained decode: layers 0 .. L-2 in ONE launch (skinny_stream.hip chain_kernel MULTI; the last layer, without a next QKV, is its own launch)")
     VWA_CHAIN_SCHED: Optional[str] = Field(None, description="DIAGNOSTIC: chained schedule override name=value,...")
     VWA_GEMM_QKV: bool = Field(True, description="> 16-row QKV: rotary + KV write in the tiled GEMM epilogue")
     VWA_GEMM_P8: Optional[str] = Field(None, description="DIAGNOSTIC: 256x256 8-phase GEMM eligibility override")

@@ -6,6 +6,13 @@ Per connection:
     ``transcript_partial`` / ``transcript_final`` frames carrying Deepgram-shaped payloads;
   * final transcripts are aggregated and debounced (``VWA_DEBOUNCE_MS``, reference fixed 1000 ms:
     :229) before ``POST BRAIN_URL`` {text, context};
+  * commit policy for pauses (the reference only merges finals that land inside its debounce):
+    the recognizer's VAD events (``SpeechStarted``) hold the pending text while the user speaks
+    again -- a pause longer than the ASR endpoint is not a command boundary until ``VWA_COMMIT_MS``
+    of silence have passed since the speech end; the brain is started SPECULATIVELY on the
+    speculative final pass (``VWA_SPEC_BRAIN``), so its latency hides in the endpoint / commit
+    wait, and its answer is used only if the committed text is exactly the text it parsed (and
+    the context did not change meanwhile) -- otherwise it is dropped and the merged text parsed;
   * brain reply -> ``intent`` frame, ``tts`` frame (tts_summary), context merge of
     ``context_updates``, safe/risky split: safe intents go to ``POST EXECUTOR_URL/execute`` with
     the connection's executor session id (``execution_result`` / ``execution_error``), risky
@@ -50,7 +57,8 @@ async def post_json_and_return(session: aiohttp.ClientSession, url: str, body: A
 
 
 def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Optional[str] = None,
-              executor_url: Optional[str] = None, debounce_ms: Optional[float] = None) -> web.Application:
+              executor_url: Optional[str] = None, debounce_ms: Optional[float] = None,
+              commit_ms: Optional[float] = None, spec_brain: Optional[bool] = None) -> web.Application:
     """asr_factory() -> a StreamingAsrSession-like object (push(bytes)->events, flush()->events);
     None = passthrough mode (no recognizer, as the reference without DEEPGRAM_API_KEY)."""
     app = web.Application()
@@ -67,6 +75,10 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
     executor_url = executor_url or knob("EXECUTOR_URL")
     if debounce_ms is None:
         debounce_ms = knob("VWA_DEBOUNCE_MS")
+    commit_ms = knob("VWA_COMMIT_MS") if commit_ms is None else commit_ms
+    spec_brain = knob("VWA_SPEC_BRAIN") if spec_brain is None else spec_brain
+    # the ASR final fires endpoint_ms after the speech end: the commit window's rest comes after it
+    hold_s = max(debounce_ms, commit_ms - knob("VWA_ENDPOINT_MS")) / 1000.0
 
     async def on_startup(app_):
         app_["http"] = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=120))
@@ -99,8 +111,10 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
         m.inc("connections")
         loop = asyncio.get_running_loop()
         # per-utterance span (monotonic): first audio -> final transcript -> brain reply
+        # pending: final text not yet sent to the brain; spec: a speculative brain call {text, ctx,
+        # task}; ctx: context version (a speculative answer is only used for the context it saw)
         st: Dict[str, Any] = {"context": {}, "pending": "", "debounce": None, "session_id": None, "closed": False,
-                              "t_final": None, "t_utt": None}
+                              "t_final": None, "t_utt": None, "spec": None, "ctx": 0, "procs": set()}
         lock = asyncio.Lock()
 
         async def send(obj):
@@ -127,6 +141,9 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
             else:
                 await send({"type": "info", "payload": "deepgram_connected"})
                 await send({"type": "info", "payload": {"state": "open"}})
+                if hasattr(asr, "vad_events"):
+                    asr.vad_events = True
+                    asr.on_speculative = lambda text: loop.call_soon_threadsafe(on_speculative_final, text)
         else:
             await send({"type": "warn", "payload": "no_api_key; running in passthrough"})
 
@@ -167,28 +184,50 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
 
         exec_task = asyncio.ensure_future(exec_worker())
 
-        async def process(combined: str):
+        async def call_brain(text: str):
+            """One /parse call (serialised per connection: context updates apply in order)."""
             async with lock:
                 t0 = time.perf_counter()
                 try:
-                    resp = await post_json_and_return(app["http"], brain_url,
-                                                      {"text": combined, "context": st["context"]})
+                    resp = await post_json_and_return(app["http"], brain_url, {"text": text, "context": st["context"]})
                 except Exception as e:  # noqa: BLE001
                     m.inc("brain_errors")
                     print(f"[voice] brain post failed: {e}", flush=True)
-                    return
+                    return None
+                m.observe("brain_ms", (time.perf_counter() - t0) * 1e3)
+                return resp
+
+        async def process(combined: str):
+            """Commit one command: the speculative answer if it parsed exactly this text under the
+            current context, else a fresh brain call; then deliver it."""
+            sp, st["spec"] = st["spec"], None
+            if sp is not None and sp["text"] == combined and sp["ctx"] == st["ctx"]:
+                resp = await sp["task"]
+                m.inc("spec_brain_used")
+                if resp is None:
+                    resp = await call_brain(combined)
+            else:
+                if sp is not None:
+                    m.inc("spec_brain_dropped")
+                resp = await call_brain(combined)
+            if resp is not None:
+                await deliver(resp)
+
+        async def deliver(resp):
+            async with lock:
                 await send({"type": "intent", "payload": resp})
                 now = time.perf_counter()
+                m.inc("commands")
                 if st["t_final"] is not None:
                     m.observe("final_to_intent_ms", (now - st["t_final"]) * 1e3)
                 if st["t_utt"] is not None:
                     m.observe("utterance_to_intent_ms", (now - st["t_utt"]) * 1e3)
                     st["t_utt"] = None
-                m.observe("brain_ms", (time.perf_counter() - t0) * 1e3)
                 if isinstance(resp, dict) and resp.get("tts_summary"):
                     await send({"type": "tts", "payload": resp["tts_summary"]})
                 if isinstance(resp, dict) and isinstance(resp.get("context_updates"), dict):
                     st["context"] = merge_context(st["context"], resp["context_updates"])
+                    st["ctx"] += 1
                 intents = resp.get("intents") if isinstance(resp, dict) else None
                 if isinstance(intents, list):
                     safe = [i for i in intents if not (isinstance(i, dict) and i.get("requires_confirmation"))]
@@ -201,7 +240,7 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
 
         async def debounced():
             try:
-                await asyncio.sleep(debounce_ms / 1000.0)
+                await asyncio.sleep(hold_s)
             except asyncio.CancelledError:
                 return
             combined = st["pending"].strip()
@@ -210,8 +249,34 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
             if combined:
                 await process(combined)
 
+        def start_debounce():
+            t = asyncio.ensure_future(debounced())
+            st["debounce"] = t
+            st["procs"].add(t)  # (tracked until done: a disconnect lets a committing call finish)
+            t.add_done_callback(st["procs"].discard)
+
+        def on_speculative_final(text: str):
+            """The ASR's speculative final pass finished (the user has been silent for
+            VWA_SPEC_FINAL_MS): parse pending + it now, commit later (process)."""
+            text = (text or "").strip()
+            if not spec_brain or not text or st["closed"]:
+                return
+            cand = f"{st['pending']} {text}" if st["pending"] else text
+            sp = st["spec"]
+            if sp is not None and sp["text"] == cand and sp["ctx"] == st["ctx"]:
+                return
+            m.inc("spec_brain_started")
+            st["spec"] = {"text": cand, "ctx": st["ctx"], "task": asyncio.ensure_future(call_brain(cand))}
+
         async def handle_events(events):
             for ev in events:
+                if ev.get("type") == "SpeechStarted":
+                    # the user speaks (again): nothing pending is a finished command yet
+                    if st["debounce"] is not None:
+                        st["debounce"].cancel()
+                        st["debounce"] = None
+                        m.inc("commits_held")
+                    continue
                 is_final = bool(ev.get("is_final") or (ev.get("channel") or {}).get("is_final"))
                 await send({"type": "transcript_final" if is_final else "transcript_partial", "payload": ev})
                 if not is_final:
@@ -227,7 +292,7 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                 st["pending"] = f"{st['pending']} {text}" if st["pending"] else text
                 if st["debounce"] is not None:
                     st["debounce"].cancel()
-                st["debounce"] = asyncio.ensure_future(debounced())
+                start_debounce()
 
         app["live"] += 1
         try:
@@ -259,6 +324,7 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
                         break
                     if ctl.get("type") == "context_update" and isinstance(ctl.get("payload"), dict):
                         st["context"] = merge_context(st["context"], ctl["payload"])
+                        st["ctx"] += 1
                     elif ctl.get("type") == "flush" and asr is not None:
                         events = await asr_call(asr.flush)
                         await handle_events(events)
@@ -268,14 +334,24 @@ def build_app(asr_factory: Optional[Callable[[], Any]] = None, *, brain_url: Opt
             app["live"] -= 1
             st["closed"] = True
             if st["debounce"] is not None:
-                st["debounce"].cancel()
+                st["debounce"].cancel()  # (still sleeping: a command nobody finished saying)
             if asr is not None and hasattr(asr, "close"):
                 asr.close()
             # queued executions still run (the reference's fire-and-forget promises do); their
-            # frames are dropped once the socket is closed
-            exec_q.put_nowait(None)
-            app["exec_tasks"].add(exec_task)
-            exec_task.add_done_callback(app["exec_tasks"].discard)
+            # frames are dropped once the socket is closed.  A command already committing (its
+            # brain call in flight) still enqueues its safe intents: the sentinel goes in after it
+            # (ADVICE r5 -- enqueued behind the sentinel they were silently dropped)
+            inflight = [t for t in st["procs"] if not t.done()]
+
+            async def close_exec():
+                if inflight:
+                    await asyncio.gather(*inflight, return_exceptions=True)
+                exec_q.put_nowait(None)
+
+            closer = asyncio.ensure_future(close_exec())
+            for t in (closer, exec_task):
+                app["exec_tasks"].add(t)
+                t.add_done_callback(app["exec_tasks"].discard)
         return ws
 
     app.router.add_get("/health", health)
