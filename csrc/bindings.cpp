@@ -558,6 +558,12 @@ void chain_schedule(ChainParams& cp) {
   // the QKV phase's two items go out at the down -> QKV barrier (half the workgroups take two of its
   // 384 tiles): 100.96 / 100.84 vs 101.38 / 101.57 us (profiles/r5_chain_pre_mask.jsonl)
   cp.pre_mask = 8;
+  // round 6: the multi-layer launch's QKV -> next-attention hand-off (grid barrier; per-kv-group
+  // counters and a K/V prefetch measured no better, kept as schedule options) and the attention
+  // workgroups' gate/up item 0 issued during their attention
+  cp.qkv_flags = 0;  // (per-kv-group counters measured 99.5 -> 100.9 us per layer: the barrier stays)
+  cp.kv_prefetch = 0;  // (neutral: 99.47 vs 99.53 us per layer, profiles/r6_chain_multi_variants.jsonl)
+  cp.attn_pre = 1;
   // diagnostic override of the schedule (tools/chain_probe.py A/B runs): "name=value,..."
   if (const char* e = std::getenv("VWA_CHAIN_SCHED")) {
     std::string s(e);
@@ -583,6 +589,9 @@ void chain_schedule(ChainParams& cp) {
         else if (k == "poll_free") cp.poll_free = v;
         else if (k == "o_nt2") cp.o_nt2 = v;
         else if (k == "d_nt2") cp.d_nt2 = v;
+        else if (k == "qkv_flags") cp.qkv_flags = v;
+        else if (k == "kv_pf") cp.kv_prefetch = v;
+        else if (k == "attn_pre") cp.attn_pre = v;
       }
       at = end + 1;
     }
@@ -651,6 +660,7 @@ std::tuple<Tensor, int64_t> chain_make(Tensor h, Tensor att, Tensor act, Tensor 
   cp.n = 3;
   cp.seq = 0;
   chain_schedule(cp);
+  if (bar.numel() < 640) cp.qkv_flags = 0;  // (the per-group QKV counters live up to u64 word 304)
   if (w_qkv.has_value()) {
     TORCH_CHECK(positions.has_value() && slots.has_value() && q_out.has_value() && k_cache.has_value() &&
                     v_cache.has_value(),

@@ -140,11 +140,15 @@ struct NoStamp {
 // done (optional, the chained launch's attention -> o_proj hand-off): after a (row group, kv
 // head)'s final output is stored and drained, one no-return add of 1 to *done -- the consumers
 // wait for *n_final_out of them instead of a grid barrier.
+// on_kv (optional, single-register-set form): called once per wave of a workgroup WITH an item,
+// after the wave's key steps (at once for a wave without one) and before the merge -- the chained
+// launch issues a weight item of a later phase there, so the attention workgroups' memory pipe is
+// not idle through the attention's merge (and, for the waves without a key step, all of it).
 template <int D, int G, int NW, bool SC1OUT, bool DB = true, bool FINE = false, class OnIdle = NoIdle,
-          class Stamp = NoStamp>
+          class Stamp = NoStamp, class OnKv = NoIdle>
 VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid, int bid, OnIdle on_idle = {},
                         int* n_items_out = nullptr, Stamp stamp = {}, unsigned long long* done = nullptr,
-                        int* n_final_out = nullptr) {
+                        int* n_final_out = nullptr, OnKv on_kv = {}) {
   constexpr int kWv = NW;
   constexpr int kChunk = FINE ? kMqStep : NW * kMqStep;  // chunk granularity (keys)
   constexpr int RG = kMqCols / G;          // rows per group
@@ -533,6 +537,10 @@ VWA_DEVICE bool mq_body(const DecodeAttnParams& p, unsigned char* lds, int grid,
       if (item == bid && s == w) stamp(15);  // (diagnostic stamp 15: the wave's first K/V step landed)
       compute_step(wb + s * kMqStep, kA, vA);
     }
+    // (after the wave's key steps: their K/V registers are free -- issued inside the loop the item
+    // kept 64 more VGPRs live through the attention and spilled; a wave without a key step, most
+    // of them at one row, issues at once and streams through the whole attention)
+    if (item == bid) on_kv();
   }
 
   // ---- per-wave (m, l, O) -> LDS; O^T accumulator of lane (n, g): dims 16dt + 4g + i

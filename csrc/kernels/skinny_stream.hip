@@ -625,6 +625,11 @@ constexpr int kChainTpSpinLimit = 1 << 22;
 // arrival to release (four dependent agent-scope round trips).  A flat counter polled with scalar loads
 // on uncached memory (256 same-address atomics) measured 121 us per chained layer vs 99.6 two-level.
 constexpr int kBarTop = 128, kBarErr = 160, kBarAttnDone = 176;
+// multi-layer launch (chain_kernel MULTI): per-kv-group QKV completion counters, u64 words
+// kBarQkv + 16 g (each on its own 128-byte line: eight counters in one line measured 2.4 us per
+// layer slower than the grid barrier -- every atomic and poll of all groups on one line) --
+// monotonic, + (tiles of the group) per QKV phase.  (bar: >= 320 u64 words, ops.chain_buffers)
+constexpr int kBarQkv = 192, kBarQkvStride = 16;
 // diagnostic stamp slots per workgroup (ChainParams::ts): 0..8 phase edges, 9..21 attention,
 // 22..53 in-phase (chain_phase pst)
 constexpr int kTsStride = 64;
@@ -1297,8 +1302,98 @@ struct SeqEpi {
 // ph[2].xg: more rows than its X fits LDS, 5..16 rows, no attention phase)
 // O2: phase 0 (o_proj) in 32-column tiles (ChainParams::o_nt2)
 // D2: the X-streaming down projection (XG2) in 32-column tiles (ChainParams::d_nt2)
+// ---- multi-layer launch: QKV -> next layer's attention, per kv group instead of a grid barrier
+// The QKV phase's 16-column tiles of kv group g are the q heads g G .. g G + G - 1, k head g and v
+// head g ((G + 2) hd / 16 tiles).  A workgroup that finished its QKV tiles (whole tiles: nb == 1)
+// drains its stores and adds 1 per tile to its groups' counters; an attention workgroup waits only
+// for the counter of ITS kv head -- the groups whose tiles finish in the phase's first round start
+// their attention while the second-round tiles still run, and nobody waits for a grid barrier.
+VWA_DEVICE int qkv_group(const SkinnyParams& q, int tile) {
+  const int head = tile * 16 / q.head_dim, G = q.n_q_heads / q.n_kv_heads;
+  return head < q.n_q_heads ? head / G : head < q.n_q_heads + q.n_kv_heads ? head - q.n_q_heads
+                                                                            : head - q.n_q_heads - q.n_kv_heads;
+}
+VWA_DEVICE long long qkv_tiles_per_group(const SkinnyParams& q) {
+  return (long long)(q.n_q_heads / q.n_kv_heads + 2) * q.head_dim / 16;
+}
+
+template <int KS>
+VWA_DEVICE void qkv_signal(const ChainPhase& ph, unsigned long long* bar) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Q / K / V stores are performed
+  lds_sync();
+  const PhaseRange r = chain_range<KS>(ph);
+  if (VWA_TX == 0)
+    for (int it = 0; it < r.n_items; ++it)
+      __hip_atomic_fetch_add(gp(&bar[kBarQkv + kBarQkvStride * qkv_group(ph.p, r.u0 + it)]), 1ull, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wave 0 polls (scalar loads past the scalar cache, uncached words) until every group in
+// [g0, g1) has reached its target; bounded like chain_wait
+VWA_DEVICE void qkv_wait(unsigned long long* bar, const unsigned long long* base, unsigned long long add, int g0, int g1) {
+  if (VWA_TX < 64) {
+    for (int g = g0; g < g1; ++g) {
+      const unsigned long long tgt = base[g] + add;
+      const unsigned long long* w = &bar[kBarQkv + kBarQkvStride * g];
+      int spins = 0;
+      while (true) {
+        unsigned long long v;
+        asm volatile("s_load_dwordx2 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(w) : "memory");
+        if ((long long)(v - tgt) >= 0) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kChainSpinLimit) {
+          if (VWA_TX == 0) __hip_atomic_store(gp(&bar[kBarErr]), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+  }
+  lds_sync();
+}
+
+// K/V prefetch of an attention workgroup's next item while it waits for the QKV counters: the
+// chunk's keys older than the step's rows (never a key this launch writes) pulled into this XCD's
+// L2 by LDS-DMA into a junk line of each wave's own V-image slot (mq_attention.h vimg; the wave's
+// K/V waits order the DMAs before its own V-image writes, and the chain waits vmcnt(0) before any
+// other LDS use of those bytes).  The attention's own K/V loads then hit L2: the cold K/V round
+// trip (~4 us) leaves the critical path.  ev: the workgroup's step-plan entry (lanes:
+// 3 kv head, 4 first row, 6 / 7 key range, 12 context of the group's first row).
+VWA_DEVICE void kv_prefetch(const DecodeAttnParams& a, int ev, unsigned char* lds) {
+  const int kvh = __builtin_amdgcn_readlane(ev, 3), r0 = __builtin_amdgcn_readlane(ev, 4);
+  const int kbeg = __builtin_amdgcn_readlane(ev, 6), kend = __builtin_amdgcn_readlane(ev, 7);
+  const int c0 = __builtin_amdgcn_readlane(ev, 12);
+  const int nk = min(min(kend, c0 - 1) - kbeg, 128);
+  if (nk <= 0 || a.kv.block_size != 16) return;
+  const int tx = VWA_TX, lane = tx & 63, w = tx >> 6;
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(a.kv.k), (short)0, 0x7FFFFFF0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<u16*>(a.kv.v), (short)0, 0x7FFFFFF0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(a.row_table), (short)0,
+                                                                     (r0 + 1) * a.rt_stride * 4, 0x00020000);
+  auto* dst = (__attribute__((address_space(3))) void*)(lds + w * kMqStep * 256);
+  // 16-byte pieces: 16 per 256-byte key row; piece q of the chunk -> key kbeg + q / 16; a wave
+  // takes pieces w * 64 + lane + 512 i (i < 4: nk <= 128 keys), all table loads first
+  int blk[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = w * 64 + lane + 512 * i, key = kbeg + q / 16;
+    blk[i] = (int)__builtin_amdgcn_raw_buffer_load_b32(rt, q < nk * 16 ? (r0 * a.rt_stride + key / 16) * 4 : 0x7FFFFFF0,
+                                                       0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = w * 64 + lane + 512 * i, key = kbeg + q / 16;
+    if (512 * i + w * 64 >= nk * 16) break;  // wave-uniform
+    const long long e = (long long)blk[i] * a.kv.stride_block + (long long)kvh * a.kv.stride_head +
+                        (long long)(key & 15) * a.kv.stride_tok;
+    const unsigned off = q < nk * 16 ? (unsigned)(e * 2 + (q & 15) * 16) : 0x7FFFFFF0u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, dst, 16, off, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, dst, 16, off, 0, 0, 0);
+  }
+}
+
 // MULTI: ONE launch runs n_layers consecutive layers (descriptors cpp[0 .. n_layers), each a
-// 4-phase Llama tail whose QKV phase feeds the next layer's attention).  Between layers every
+// 4-phase Llama tail whose QKV phase feeds the next layer's attention; the last may be the
+// model's last layer, a 3-phase tail).  Between layers every
 // workgroup arrives at a grid barrier after its QKV tiles; only the workgroups that run an
 // attention item of the next layer wait for it (they read the next layer's Q and newest K/V).  A
 // workgroup the step plan (mq_attention.h, written by layer 0 of this very launch) gives no
@@ -1320,12 +1415,30 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   // layer's last round
   const bool tpr = cpp->tp.world > 1;
   const int e0 = tpr ? __hip_atomic_load(gp(cpp->tp.epoch), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  // MULTI: the per-kv-group QKV counters' values before this launch (whole phases only: read
+  // before this workgroup's first arrival, and no QKV phase of this launch starts before every
+  // workgroup arrived three times); hand-off by group only with whole QKV tiles per workgroup
+  unsigned long long qkv_base[8] = {};
+  const bool qsig = MULTI && cpp->qkv_flags && cpp->bar_mode == 2 && cpp->ph[3].nb == 1 &&
+                    cpp->ph[3].p.n_kv_heads <= 8 && cpp->attn_flag;  // (uncached words, scalar polls)
+  if constexpr (MULTI) {
+    if (qsig && VWA_TX < 64) {
+      const unsigned long long tpg = (unsigned long long)qkv_tiles_per_group(cpp->ph[3].p);
+      for (int g = 0; g < cpp->ph[3].p.n_kv_heads; ++g) {
+        const unsigned long long v = __hip_atomic_load(gp(&bar[kBarQkv + kBarQkvStride * g]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        qkv_base[g] = v / tpg * tpg;
+      }
+    }
+  }
+  bool pf_prev = false, pf_next = false;  // (MULTI) the previous layer's end issued K/V prefetch DMAs
   for (int li = 0; li < (MULTI ? n_layers : 1); ++li) {
+  pf_prev = pf_next;
+  pf_next = false;
   const ChainParams& cp = cpp[li];  // device-resident descriptor
-  // Warm the scalar cache with the whole descriptor (24 x 64-byte lines) in ONE round trip: the
+  // Warm the scalar cache with the whole descriptor (25 x 64-byte lines) in ONE round trip: the
   // fields are otherwise fetched behind branches and earlier fields' values, a chain of dependent
   // scalar misses (the attention prologue measured ~6 of them before its first vector load)
-  static_assert(sizeof(ChainParams) <= 24 * 64, "descriptor warm-up covers 24 lines");
+  static_assert(sizeof(ChainParams) <= 25 * 64, "descriptor warm-up covers 25 lines");
   {
     // (non-volatile, no memory clobber: a volatile block counts as a memory write and turns every
     // later descriptor read into a vector load; the never-true test keeps it alive)
@@ -1335,7 +1448,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
         "s_load_dword %0, %1, 0x200\n\t""s_load_dword %0, %1, 0x240\n\t""s_load_dword %0, %1, 0x280\n\t""s_load_dword %0, %1, 0x2c0\n\t"
         "s_load_dword %0, %1, 0x300\n\t""s_load_dword %0, %1, 0x340\n\t""s_load_dword %0, %1, 0x380\n\t""s_load_dword %0, %1, 0x3c0\n\t"
         "s_load_dword %0, %1, 0x400\n\t""s_load_dword %0, %1, 0x440\n\t""s_load_dword %0, %1, 0x480\n\t""s_load_dword %0, %1, 0x4c0\n\t""s_load_dword %0, %1, 0x500\n\t"
-        "s_load_dword %0, %1, 0x540\n\t""s_load_dword %0, %1, 0x580\n\t""s_load_dword %0, %1, 0x5c0\n\t"
+        "s_load_dword %0, %1, 0x540\n\t""s_load_dword %0, %1, 0x580\n\t""s_load_dword %0, %1, 0x5c0\n\t""s_load_dword %0, %1, 0x600\n\t"
         "s_waitcnt lgkmcnt(0)"
         : "=&s"(junk)
         : "s"(cpp + li));
@@ -1366,6 +1479,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   // k-batch) never uses register set B, so B carries phase 1's first item from the start: it
   // streams during the attention phase / the launch ramp, when HBM would otherwise idle.
   bool nx = false;
+  bool apre = false;  // (cp.attn_pre) phase 1's item 0 was issued into A during this workgroup's attention
   auto setup0 = [&](int n_attn) {
     const bool sub = cp.osub && n_attn > 0 && n_attn <= nwg / 2;
     ob0 = sub ? n_attn : 0;
@@ -1401,9 +1515,23 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
                                                           if ((k == 15 || k == 10) && cp.ts) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                                                           if (cp.ts && VWA_TX == 0)
                                                             *gp(cp.ts + blockIdx.x * kTsStride + k) = __builtin_amdgcn_s_memrealtime();
-                                                        }, done, &n_final);
+                                                        }, done, &n_final, [&]() {
+                                                          // cp.attn_pre: an attention workgroup without o_proj
+                                                          // units (osub) streams gate/up's item 0 into A through
+                                                          // its attention's merge (fp8 items only: the bf16 item's
+                                                          // 64 VGPRs next to the merge's spilled 124 B per lane)
+                                                          if constexpr (F8) {
+                                                            if (cp.attn_pre && cp.osub && n_attn > 0 && n_attn <= nwg / 2 &&
+                                                                (int)blockIdx.x < n_attn) {
+                                                              chain_issue_item<E1, KS, WA, false, F8>(cp.ph[1], A, 0);
+                                                              apre = true;
+                                                            }
+                                                          }
+                                                        });
     if (!idle) setup0(n_attn);
     stamp();
+    // (MULTI: this wave's K/V prefetch DMAs, kv_prefetch, have landed before any LDS reuse)
+    if (MULTI && !idle && pf_prev) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_sync();  // the attention's LDS readers are done (idle workgroups: the metadata's)
     if (!idle) {
       pre0 = 0;
@@ -1482,8 +1610,9 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   // issue theirs after the release, behind the X pieces (chain_phase has0 = false)
   const int wv = (int)(VWA_TX >> 6);
   const bool prew = (cp.pre_waves == 0 || wv < cp.pre_waves) && !(cp.poll_free && wv == 0);
+  const bool nx1 = nx || apre;  // phase 1's item 0 already in A (o_proj's free set, or the attention window)
   if (!stg) {
-    if (nx) chain_issue_item<E1, KS, WA, false, F8>(cp.ph[1], B, 1);  // phase 1's item 0 is already in A
+    if (nx1) chain_issue_item<E1, KS, WA, false, F8>(cp.ph[1], B, 1);  // phase 1's item 0 is already in A
     else if (prew) chain_issue_first<E1, KS, WA, false, F8>(cp.ph[1], A, B, preb_of(1));
   }
   chain_wait(bar, gen, cp.bar_mode);
@@ -1492,7 +1621,7 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
   if (AG > 0 && cp.attn_flag && blockIdx.x == 0 && VWA_TX == 0)
     __hip_atomic_store(gp(&bar[kBarAttnDone]), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   stamp();
-  chain_phase<E1, KS, WA, false, F8>(cp, 1, A, B, smem, nx ? 1 : preb_of(1), nx ? 1 : 0, 0, 0, nx || prew);
+  chain_phase<E1, KS, WA, false, F8>(cp, 1, A, B, smem, nx1 ? 1 : preb_of(1), nx1 ? 1 : 0, 0, 0, nx1 || prew);
   stamp();
   if constexpr (NPH >= 3) {
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
@@ -1514,29 +1643,44 @@ __global__ __launch_bounds__(KS * 64) void chain_kernel(const ChainParams* __res
     }
   }
   if constexpr (NPH >= 4) {
+   if (!MULTI || cp.n >= 4) {  // (MULTI: the model's last layer has no next QKV phase)
     gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
     if (!stg && prew) chain_issue_first<E3, KS, WA, false, F8>(cp.ph[3], A, B, preb_of(3));
     chain_wait(bar, gen, cp.bar_mode);
     stamp();
     chain_phase<E3, KS, WA, false, F8>(cp, 3, A, B, smem, preb_of(3), 0, 0, 0, prew);
     stamp();
+   }
   }
   if constexpr (MULTI) {
     if (li + 1 < n_layers) {
-      // layer li -> li + 1: the QKV tiles of every workgroup are stored (the arrival drains them)
-      // before an attention workgroup reads Q / the newest K/V
-      gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
+      // layer li -> li + 1: an attention workgroup of layer li + 1 reads Q / the newest K/V only
+      // once the QKV tiles of its kv group are stored (qsig: per-group counters; else a barrier)
+      if (qsig) qkv_signal<KS>(cp.ph[3], bar);
+      else gen = chain_arrive(bar, nwg, cp.bar_mode, bar_next);
       const DecodeAttnParams& na = cpp[li + 1].attn;
-      bool skip = false;
+      int st = 3, ev = 0;
       if (cpp[li + 1].attn_flag && na.plan_mode == 2) {
         // this workgroup's step-plan entry (state 0 idle / 2 empty chunk: no Q, K or V read)
         const __amdgpu_buffer_rsrc_t r_pl =
             __builtin_amdgcn_make_buffer_rsrc(na.plan, (short)0, ((int)blockIdx.x + 1) * 64, 0x00020000);
-        const int ev = (int)__builtin_amdgcn_raw_buffer_load_b32(r_pl, ((int)blockIdx.x * 16 + (VWA_TX & 15)) * 4, 0, 16);
-        const int st = __builtin_amdgcn_readlane(ev, 2), rows = __builtin_amdgcn_readlane(ev, 10);
-        skip = (st == 0 || st == 2) && rows == na.rows;
+        ev = (int)__builtin_amdgcn_raw_buffer_load_b32(r_pl, ((int)blockIdx.x * 16 + (VWA_TX & 15)) * 4, 0, 16);
+        st = __builtin_amdgcn_readlane(ev, 10) == na.rows ? __builtin_amdgcn_readlane(ev, 2) : 3;
       }
-      if (!skip) chain_wait(bar, gen, cp.bar_mode);
+      if (st != 0 && st != 2) {  // (idle / empty-chunk workgroups go straight on: no wait at all)
+        if (st == 1 && cp.kv_prefetch) {
+          kv_prefetch(na, ev, reinterpret_cast<unsigned char*>(smem));
+          pf_next = true;
+        }
+        if (!qsig) {
+          chain_wait(bar, gen, cp.bar_mode);
+        } else {
+          const int kvh = __builtin_amdgcn_readlane(ev, 3);
+          const unsigned long long add = (unsigned long long)qkv_tiles_per_group(cp.ph[3].p) * (unsigned long long)(li + 1);
+          if (st == 1) qkv_wait(bar, qkv_base, add, kvh, kvh + 1);
+          else qkv_wait(bar, qkv_base, add, 0, cp.ph[3].p.n_kv_heads);  // (no plan: every group)
+        }
+      }
     }
   }
   }  // layers
@@ -1659,7 +1803,7 @@ extern "C" int vwa_chain_prepare(ChainParams* cp, int grid) {
 extern "C" int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid,
                                 hipStream_t st, int xg2, int f8, int o2, int n_layers) {
   if (attn_g) lds = lds > (int)MqLds<128, 8>::bytes ? lds : (int)MqLds<128, 8>::bytes;
-  if (n_layers > 1) {  // one launch over n_layers consecutive 4-phase Llama tails (chain_kernel MULTI)
+  if (n_layers > 1) {  // one launch over n_layers consecutive Llama tails (chain_kernel MULTI)
     if (seq != 0 || n_phases != 4 || xg2 || (attn_g != 4 && attn_g != 8) || (!f8 && !o2) || (f8 && o2)) return -10;
 #define VWA_CHAIN_LAUNCH_MULTI(G, F8_, O2_) \
   hipLaunchKernelGGL((chain_kernel<8, 0, 4, G, 0, false, F8_, O2_, false, true>), dim3(grid), dim3(8 * 64), lds, st, d_cp, n_layers)

@@ -99,7 +99,7 @@ struct ChainTP {
 };
 
 // (64-byte aligned: a multi-layer launch indexes an array of them, and each one's scalar-cache
-// warm-up, chain_kernel, covers exactly its 24 lines)
+// warm-up, chain_kernel, covers exactly its 25 lines)
 struct alignas(64) ChainParams {
   ChainPhase ph[kChainMaxPhases];
   int n;
@@ -142,6 +142,9 @@ struct alignas(64) ChainParams {
   int poll_free;  // wave 0 (the barrier poller) issues nothing ahead of a barrier wait
   int o_nt2;      // attention launches: phase 0 (o_proj) in 32-column tiles (host request; prepare clears it when unused)
   int d_nt2;      // 5..16 rows: the X-streaming down projection in 32-column tiles (host request; cleared when unused)
+  int kv_prefetch;  // multi-layer launch: attention workgroups pull their next item's old K/V into L2 while they wait
+  int qkv_flags;    // multi-layer launch: QKV -> next attention by per-kv-group tile counters (0: grid barrier)
+  int attn_pre;     // attention workgroups (no o_proj units) issue gate/up's item 0 during their attention
   ChainTP tp;
 };
 

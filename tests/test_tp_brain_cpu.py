@@ -197,6 +197,39 @@ def test_plan_gpus_maps_through_the_parent_mask():
     assert p == {"brain": ["6"], "voice": ["6"], "shared": True}
     assert shared_gpu_env({})["VWA_CHAIN"] == "0"
     assert shared_gpu_env({"VWA_SHARED_CHAIN": "1"})["VWA_CHAIN"] == "1"
+    # round 6: with a busy word the brain keeps the chain and gates it on the ASR's activity
+    g = shared_gpu_env({}, "/dev/shm/vwa_asr_busy_test")
+    assert g["VWA_CHAIN"] == "1" and g["VWA_ASR_BUSY_FILE"] == "/dev/shm/vwa_asr_busy_test"
+    assert "VWA_ASR_BUSY_FILE" not in shared_gpu_env({"VWA_SHARED_CHAIN": "0"}, "/dev/shm/x")
+
+
+def test_asr_busy_flag_gates_the_chained_launch(tmp_path):
+    """utils/busy_flag.py: the ASR batcher's passes mark the shared word busy (with a hold after
+    the last one); the brain engine's chain_gate reads it before every step."""
+    import numpy as np
+
+    from voice_enabled_browser_automation_amd.runtime.engine import LLMEngine
+    from voice_enabled_browser_automation_amd.utils.busy_flag import BusyFlag
+
+    path = str(tmp_path / "busy")
+    w, r = BusyFlag(path, create=True), BusyFlag(path)
+    assert not r.busy(0.0)
+    w.enter()
+    assert r.busy(0.0)
+    w.leave()
+    assert not r.busy(0.0) and r.busy(10_000.0)  # within the hold
+    m = LlamaModel(TINY, device="cpu", seed=1)
+    e = LLMEngine(m, max_seqs=1, max_model_len=256, kv_blocks=40)
+    e.chain_gate = lambda: r.busy(0.0)
+    s = e.new_sequence([1, 2, 3, 4], use_prefix_cache=False)
+    e.prefill(s)
+    w.enter()
+    a = e.run_rows([(s, 5)])
+    assert e.stats["gated_steps"] == 1 and m._chain_gated
+    w.leave()
+    b = e.run_rows([(s, 6)])
+    assert e.stats["gated_steps"] == 1 and not m._chain_gated
+    assert np.isfinite(a.numpy()).all() and np.isfinite(b.numpy()).all()
 
 
 def test_brain_health_reports_a_failed_tp_group():

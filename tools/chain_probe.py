@@ -59,8 +59,8 @@ def main():
     pos = torch.arange(M, dtype=torch.int32, device=dev)
     slots = torch.arange(M, dtype=torch.int64, device=dev)
     rope = ops.rope_table(4096, hd, 5e5, device=dev)
-    bar = E.alloc_uncached_i32(512, torch.empty(1, device=dev)) if a.bar_mode >= 2 else \
-        torch.zeros(512, dtype=torch.int32, device=dev)
+    bar = E.alloc_uncached_i32(1024, torch.empty(1, device=dev)) if a.bar_mode >= 2 else \
+        torch.zeros(1024, dtype=torch.int32, device=dev)
     ts = torch.zeros(1024 * 64, dtype=torch.int64, device=dev)  # 64 stamp slots per workgroup
     work = torch.zeros(1 << 20, dtype=torch.int32, device=dev)
     akw, ag = {}, 0

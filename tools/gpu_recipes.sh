@@ -14,6 +14,7 @@
 #              sharing the one GPU (gloo control plane)
 #   rows       decode step vs rows per step + batched admission prefill (tools/rows_sweep.py)
 #   service    speech end -> intent through the services (tools/service_bench.py)
+#   service6   the same with paused speech, end-of-packet timing, commit windows 0 / 700 ms, chain gate
 #   asr        Whisper-tiny / large-v3 decode timing + kernel trace (tools/asr_timing.py)
 #   frontend   ASR front-end kernel bench + counters (tools/bench_frontend.py, pmc_frontend.py)
 TPR="python -u -m torch.distributed.run --nnodes=1 --master-addr=127.0.0.1"
@@ -51,6 +52,11 @@ for r in "$@"; do
       done ;;
     rows) add rows_sweep 400 "python -u tools/rows_sweep.py --json gpurun_out/rows_sweep.jsonl" ;;
     service) add service_bench 1100 "python -u tools/service_bench.py --json gpurun_out/service_bench.jsonl" ;;
+    service6)  # round 6: paused speech, end-of-packet timing, commit window, chain gated on the ASR
+      add svc_tiny 1100 "python -u tools/service_bench.py --sessions 1,8 --debounce 0 --commit 0,700 --chain gate --utterances 16 --json gpurun_out/svc_tiny.jsonl"
+      add svc_tiny_par 600 "python -u tools/service_bench.py --sessions 1 --debounce 1000 --commit 0 --chain gate --utterances 12 --json gpurun_out/svc_tiny.jsonl"
+      add svc_tiny_pk 600 "python -u tools/service_bench.py --sessions 1 --debounce 0 --commit 0 --chain 0 --utterances 12 --json gpurun_out/svc_tiny.jsonl"
+      add svc_large 1100 "python -u tools/service_bench.py --asr whisper-large-v3 --sessions 1,8 --debounce 0 --commit 0,700 --chain gate --utterances 16 --json gpurun_out/svc_large.jsonl" ;;
     asr)
       add asr_tiny 200 "python -u tools/asr_timing.py --asr whisper-tiny"
       add asr_large 300 "python -u tools/asr_timing.py --asr whisper-large-v3 --reps 5"

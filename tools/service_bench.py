@@ -227,9 +227,14 @@ async def run_matrix(a) -> list:
     try:
         for chain in a.chain:
             bport = free_port()
+            # chain "gate": the shared-GPU deployment of launch.py (round 6) -- the chained launch
+            # only while the ASR batcher's busy word is clear (utils/busy_flag.py)
+            busy = f"/dev/shm/vwa_bench_busy_{os.getpid()}" if chain == "gate" else ""
             benv = {"VWA_BRAIN_ENGINE": a.brain_engine, "VWA_LLM_MODEL": a.llm, "BRAIN_PORT": str(bport),
-                    "VWA_CHAIN": chain, "HIP_VISIBLE_DEVICES": a.brain_gpu, "VWA_MAX_SESSIONS": str(max(a.sessions)),
-                    "VWA_DTYPE": a.dtype, "VWA_SHARED_GB": "24"}
+                    "VWA_CHAIN": "1" if chain == "gate" else chain, "HIP_VISIBLE_DEVICES": a.brain_gpu,
+                    "VWA_MAX_SESSIONS": str(max(a.sessions)), "VWA_DTYPE": a.dtype, "VWA_SHARED_GB": "24"}
+            if busy:
+                benv["VWA_ASR_BUSY_FILE"] = busy
             brain = spawn(f"{PKG}.brain.server", benv, os.path.join(logs, f"brain_chain{chain}.log"))
             try:
                 t0 = time.time()
@@ -244,6 +249,8 @@ async def run_matrix(a) -> list:
                             "VWA_ASR_TOKENS_PER_S": str(a.asr_tokens_per_s),
                             "VWA_ENDPOINT_MS": str(a.endpoint_ms), "VWA_SPEC_FINAL_MS": str(a.spec_ms),
                             "VWA_COMMIT_MS": str(commit), "VWA_SPEC_BRAIN": a.spec_brain}
+                    if busy:
+                        venv["VWA_ASR_BUSY_FILE"] = busy
                     voice = spawn(f"{PKG}.voice.server", venv,
                                   os.path.join(logs, f"voice_chain{chain}_deb{deb}_commit{commit}.log"))
                     try:
@@ -283,6 +290,7 @@ async def run_matrix(a) -> list:
                             rec["brain_chain_fallbacks"] = eng.get("chain_fallbacks", 0)
                             rec["brain_rows_per_iteration"] = eng.get("rows_per_iteration")
                             rec["brain_chained_steps"] = eng.get("chained_steps", 0)
+                            rec["brain_gated_steps"] = eng.get("gated_steps", 0)
                             rec["brain_steps"] = eng.get("steps", 0)
                             rec["brain_host_ms"] = eng.get("host_ms")
                             print(json.dumps(rec), flush=True)
@@ -306,7 +314,8 @@ def main():
     ap.add_argument("--spec-brain", default="1", help="voice VWA_SPEC_BRAIN")
     ap.add_argument("--max-pause-ms", type=float, default=650.0,
                     help="paused speech: longest pause inside a command (0: continuous speech, round 5's)")
-    ap.add_argument("--chain", default="0", help="brain VWA_CHAIN (the single-GPU deployment default: 0)")
+    ap.add_argument("--chain", default="gate",
+                    help="brain VWA_CHAIN: 1, 0, or gate (the single-GPU deployment: chained while the ASR is idle)")
     ap.add_argument("--utterances", type=int, default=20, help="utterances per session per point")
     ap.add_argument("--endpoint-ms", type=float, default=knob("VWA_ENDPOINT_MS"))
     ap.add_argument("--spec-ms", type=float, default=knob("VWA_SPEC_FINAL_MS"))

@@ -359,6 +359,11 @@ class AsrBatcher:
         self._cv = threading.Condition()
         self._stop = False
         self.stats = {"batches": 0, "passes": 0, "max_batch": 0, "gpu_ms": 0.0}
+        # shared-GPU deployment: the brain reads this to keep its persistent chained decode launch
+        # off the GPU while recognition runs (utils/busy_flag.py; launch.py sets the path)
+        from ..utils.busy_flag import from_env
+
+        self.busy = from_env(create=True)
         dev = getattr(asr_engine.model, "device", None)
         self._cuda_index = None
         if dev is not None and getattr(dev, "type", "cpu") == "cuda":
@@ -403,6 +408,8 @@ class AsrBatcher:
                     return
                 batch, self._q = self._q[: self.max_batch], self._q[self.max_batch :]
             t0 = time.perf_counter()
+            if self.busy is not None:
+                self.busy.enter()
             try:
                 audios = [self.eng.pcm_to_audio(p) for p, _, _ in batch]
                 kw = dict(max_tokens=self.max_tokens)
@@ -417,6 +424,9 @@ class AsrBatcher:
                 for _, _, fut in batch:
                     if not fut.done():
                         fut.set_exception(e)
+            finally:
+                if self.busy is not None:
+                    self.busy.leave()
             n = len(batch)
             self.stats["batches"] += 1
             self.stats["passes"] += n

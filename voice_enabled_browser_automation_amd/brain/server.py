@@ -161,6 +161,12 @@ def build_llm_engine(model_name: Optional[str] = None, device: Optional[str] = N
     model = load_llm(name, device=dev, tp=tp, seed=seed, weights_path=wpath,
                      wdtype=knob("VWA_DTYPE"))
     eng = LLMEngine(model, max_seqs=sessions, max_model_len=4096)
+    from ..utils.busy_flag import from_env
+
+    flag = from_env(create=True)  # shared-GPU deployment: no chained launch while the ASR runs
+    if flag is not None and tp.size == 1:
+        hold = knob("VWA_ASR_BUSY_HOLD_MS")
+        eng.chain_gate = lambda: flag.busy(hold)
     eng.capture_all()
     ie = LLMIntentEngine(eng, load_tokenizer("llama3"), budget_chars=budget, chat_format=llama3_chat)
     return TPIntentEngine(ie, tp) if tp.size > 1 else ie

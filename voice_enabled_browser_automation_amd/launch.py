@@ -8,8 +8,8 @@ GPU placement on one node (plan_gpus): the brain (LLM) takes GPUs 0..TP-1 and th
 (ASR) every remaining GPU, one voice worker per GPU behind the session router (session DP);
 VWA_BRAIN_GPUS / VWA_VOICE_GPUS (comma lists) override.  With VWA_TP>1 the brain is launched
 through torch.distributed.run with one process per GPU.  When only one GPU is visible the two
-share it (shared_gpu_env: per-kernel decode launches beside the ASR -- measured faster than the
-chained launch there).  The brain is restartable: a TP group that loses lockstep exits and is started again in fresh
+share it (shared_gpu_env: the brain uses the chained decode launch only while the ASR is idle --
+a busy word in /dev/shm).  The brain is restartable: a TP group that loses lockstep exits and is started again in fresh
 processes while the other services keep serving (Supervisor).
 """
 from __future__ import annotations
@@ -145,17 +145,22 @@ def _parent_visible() -> str:
     return os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("CUDA_VISIBLE_DEVICES") or ""
 
 
-def shared_gpu_env(env) -> dict:
-    """Brain settings when it shares its GPU with a voice worker.  Per-kernel decode launches by
-    default: under live streaming-ASR load the chained launch's persistent workgroups wait for the
-    ASR kernels to drain from their CUs, and the step measured 3.72-3.76 ms of GPU wait vs
-    3.61-3.62 ms per-kernel (tools/service_bench.py, two alternating runs each,
-    profiles/r4_service_chain_ab.jsonl; a first round-4 run had measured the chain ahead).
-    VWA_SHARED_CHAIN=1 keeps the chain (bounded waits, fallback + re-arm in runtime/engine.py);
-    VWA_SHARED_CHAIN_GRID_DIV=k gives it CUs/k workgroups."""
-    out = {"VWA_CHAIN": env.get("VWA_CHAIN", env.get("VWA_SHARED_CHAIN", "0")),
+def shared_gpu_env(env, busy_file: str = "") -> dict:
+    """Brain settings when it shares its GPU with a voice worker.  Under live streaming-ASR load the
+    chained launch's persistent workgroups wait for the ASR kernels to drain from their CUs (the
+    step measured 3.72-3.76 ms of GPU wait vs 3.61-3.62 ms per-kernel, tools/service_bench.py,
+    profiles/r4_service_chain_ab.jsonl), but with the recognizer idle -- one session whose user
+    stopped speaking -- the chain is ~10 % faster.  So (round 6) the two share a busy word
+    (``busy_file``, utils/busy_flag.py: the ASR batcher marks its passes) and the brain picks the
+    launch form per step (runtime/engine.py chain_gate).  VWA_SHARED_CHAIN=0 forces per-kernel
+    launches (round 5's default), =1 the chain always; VWA_SHARED_CHAIN_GRID_DIV=k gives it CUs/k
+    workgroups."""
+    mode = env.get("VWA_SHARED_CHAIN", "gate" if busy_file else "0")
+    out = {"VWA_CHAIN": env.get("VWA_CHAIN", "0" if mode == "0" else "1"),
            # HBM the voice worker's ASR keeps (the brain's auto KV sizing leaves it free)
            "VWA_SHARED_GB": env.get("VWA_SHARED_GB", "24")}
+    if mode == "gate" and busy_file:
+        out["VWA_ASR_BUSY_FILE"] = busy_file
     div = env.get("VWA_SHARED_CHAIN_GRID_DIV")
     if div:
         out["VWA_CHAIN_GRID_DIV"] = div
@@ -177,8 +182,12 @@ def main():
                      parent_visible=_parent_visible())
     voice_gpus = plan["voice"]
     benv = {"HIP_VISIBLE_DEVICES": ",".join(plan["brain"])}
+    venv = {}
     if plan["shared"]:
-        benv.update(shared_gpu_env(os.environ))
+        busy = f"/dev/shm/vwa_asr_busy_{os.getpid()}"
+        benv.update(shared_gpu_env(os.environ, busy))
+        if benv.get("VWA_ASR_BUSY_FILE"):
+            venv["VWA_ASR_BUSY_FILE"] = busy
     sup = Supervisor(max_restarts=knob("VWA_BRAIN_MAX_RESTARTS"))
     sup.add("brain", f"{PKG}.brain.server", benv, tp, restartable=True)
     if len(voice_gpus) > 1:
@@ -188,7 +197,7 @@ def main():
             sup.add(f"voice{i}", f"{PKG}.voice.server", {"HIP_VISIBLE_DEVICES": g, "VOICE_PORT": str(base + i)})
         sup.add("router", f"{PKG}.voice.router", {"VWA_DP": str(len(voice_gpus))})
     else:
-        sup.add("voice", f"{PKG}.voice.server", {"HIP_VISIBLE_DEVICES": voice_gpus[0] if voice_gpus else "0"})
+        sup.add("voice", f"{PKG}.voice.server", {"HIP_VISIBLE_DEVICES": voice_gpus[0] if voice_gpus else "0", **venv})
     sup.add("executor", f"{PKG}.executor.server", {})
     sup.add("web", f"{PKG}.web.server", {})
 

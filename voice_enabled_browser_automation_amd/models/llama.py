@@ -241,6 +241,7 @@ class LlamaModel:
         tp_ok = self.tp.size == 1 or (getattr(self.tp, "custom_ar", None) is not None and ops.env_flag("VWA_CHAIN_TP"))
         return (M <= ops.env_int("VWA_CHAIN_MAX_ROWS") and tp_ok and (self.wdtype == "bf16" or fp8_ok)
                 and self.device.type == "cuda" and not getattr(self, "_chain_disabled", False)
+                and not getattr(self, "_chain_gated", False)
                 and ops.env_flag("VWA_CHAIN") and ops.native_available())
 
     def _chain_any(self, M: int) -> bool:
@@ -342,23 +343,24 @@ class LlamaModel:
         return cache[key]
 
     def _chain_multi(self, bufs, kv, M: int):
-        """(descriptors, lds, attn_g, n) of ONE launch over layers 0 .. n-1 = L-2 (every one a
-        4-phase tail with the attention phase; skinny_stream.hip chain_kernel MULTI), or None when
-        some layer cannot take it (its own chained / per-kernel launch then).  The descriptors are
-        the per-layer ones (_chain_desc) concatenated into one device array; layer 0's writes the
-        attention step plan that layers 1.. of the same launch read, so a plan can never be stale
-        (a per-layer launch whose layer 0 dropped its attention phase would have left
-        layers 1.. reading an older step's entry)."""
-        n = len(self.layers) - 1
-        if n < 2 or not ops.env_flag("VWA_CHAIN_MULTI") or self.tp.size > 1 and not ops.env_flag("VWA_CHAIN_TP"):
+        """(descriptors, lds, attn_g, n) of ONE launch over all n = L layers (4-phase tails with the
+        attention phase, the last one a 3-phase tail; skinny_stream.hip chain_kernel MULTI), or None
+        when some layer cannot take it (per-layer chained / per-kernel launches then).  The
+        descriptors are the per-layer ones (_chain_desc) concatenated into one device array; layer
+        0's writes the attention step plan that layers 1.. of the same launch read, so a plan can
+        never be stale (a per-layer launch whose layer 0 dropped its attention phase would
+        have left layers 1.. reading an older step's entry)."""
+        n = len(self.layers)
+        if n < 3 or not ops.env_flag("VWA_CHAIN_MULTI") or self.tp.size > 1 and not ops.env_flag("VWA_CHAIN_TP"):
             return None
         cache = self._chains.setdefault(bufs, {}) if isinstance(getattr(self, "_chains", None), weakref.WeakKeyDictionary) else None
-        key = ("multi", M, tuple(kv.k[li].data_ptr() for li in range(n + 1)),
-               tuple(kv.v[li].data_ptr() for li in range(n + 1)), bufs.max_ctx)
+        key = ("multi", M, tuple(kv.k[li].data_ptr() for li in range(n)),
+               tuple(kv.v[li].data_ptr() for li in range(n)), bufs.max_ctx)
         if cache is not None and key in cache:
             return cache[key]
         ds = [self._chain_desc(bufs, kv, M, li) for li in range(n)]
-        ok = all(d is not None and d[1] == 4 and d[3] > 0 for d in ds) and len({(d[2], d[3]) for d in ds}) == 1
+        ok = (all(d is not None and d[3] > 0 for d in ds) and all(d[1] == 4 for d in ds[:-1]) and ds[-1][1] == 3
+              and len({(d[2], d[3]) for d in ds}) == 1)
         lds = ds[0][2] if ok else 0
         # the instantiations: o_proj in 32-column tiles (bf16) or fp8 weights, no X streaming
         ok = ok and not (lds >> 24) & 1 and ((lds >> 25) & 1) != ((lds >> 26) & 1)
@@ -411,7 +413,7 @@ class LlamaModel:
         # rows it writes to the next RMSNorm (ss[0]: after o_proj -> gate/up, ss[1]: after down ->
         # next QKV) and zeroes the other buffer, so no row_rstd launch (GemmParams::ss_*)
         ss = self._rms_stats(M) if not chain else None
-        # layers 0 .. L-2 as ONE chained launch when every one of them can take it
+        # every layer as ONE chained launch when each of them can take it
         multi = self._chain_multi(bufs, kv, M) if chain else None
         for li, L in enumerate(self.layers):
             kc, vc = kv.k[li], kv.v[li]

@@ -879,9 +879,13 @@ def chain_buffers(device):
     memory + vector polls (bar_mode 1) if the uncached allocation is unavailable; work = split-tile
     tickets + partial slots.  One set per model: launches sharing a set must be stream-ordered."""
     try:
-        bar, mode = ext().alloc_uncached_i32(512, torch.empty(1, device=device)), 2
+        bar, mode = ext().alloc_uncached_i32(1024, torch.empty(1, device=device)), 2
+        # VWA_CHAIN_BAR_MODE=4: no-return arrivals on the 8 group counters, waiters poll their sum
+        # (one scalar round trip) -- the last arrival is not two dependent atomics away from release
+        if knob("VWA_CHAIN_BAR_MODE") == 4:
+            mode = 4
     except RuntimeError:
-        bar, mode = torch.zeros(512, dtype=torch.int32, device=device), 1
+        bar, mode = torch.zeros(1024, dtype=torch.int32, device=device), 1
     return bar, mode, torch.zeros(1 << 20, dtype=torch.int32, device=device)
 
 

@@ -204,7 +204,11 @@ class LLMEngine:
         if use_graphs is None:
             use_graphs = ops.env_flag("VWA_HIPGRAPH")
         self.use_graphs = bool(use_graphs) and self.device.type == "cuda"
-        self.graphs: Dict[Tuple[int, int], Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
+        self.graphs: Dict[Tuple[int, int, bool], Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
+        # chain_gate() -> True: this step must not use the persistent chained launch (the GPU is
+        # shared with a busy ASR worker, utils/busy_flag.py); graphs are kept per launch form
+        self.chain_gate = None
+        self._gated = False
         self.graph_pool = None
         self.stats = dict(steps=0, rows=0, prefill_tokens=0, cached_tokens=0, graph_replays=0)
         self._last_step = None  # (rows, logits_for, n_computed before) of a chained step, for recover_step
@@ -307,8 +311,8 @@ class LLMEngine:
             self.graph_pool = torch.cuda.graph_pool_handle()
         with torch.cuda.graph(g, pool=self.graph_pool):
             out = self._forward_rows(M, L, upload_meta=True)
-        self.graphs[(M, L)] = (g, out)
-        return self.graphs[(M, L)]
+        self.graphs[(M, L, self._gated)] = (g, out)
+        return self.graphs[(M, L, self._gated)]
 
     def capture_all(self, buckets: Sequence[int] = BUCKETS, logit_buckets: Sequence[int] = (1,)) -> None:
         """Capture the (row bucket, logit-row bucket) graphs up front; others are captured on
@@ -320,7 +324,7 @@ class LLMEngine:
             if M > self.bufs.max_rows:
                 continue
             for L in tuple(logit_buckets) + (M,):
-                if L <= M and (M, L) not in self.graphs:
+                if L <= M and (M, L, self._gated) not in self.graphs:
                     self._capture(M, L)
         torch.cuda.synchronize()
 
@@ -398,13 +402,17 @@ class LLMEngine:
         b.upload(M, meta=not self.use_graphs)  # the step graphs copy the metadata themselves
         if rtab is not None and not self.use_graphs:
             b.row_table[:M].copy_(b.h_row_table[:M], non_blocking=True)
+        if self.chain_gate is not None:
+            self._gated = bool(self.chain_gate())
+            self.model._chain_gated = self._gated
+            self.stats["gated_steps"] = self.stats.get("gated_steps", 0) + int(self._gated)
         chained = self._uses_chain(M)
         if chained:
             self.stats["chained_steps"] = self.stats.get("chained_steps", 0) + 1
         self._last_step = (list(rows), logits_for, {sid: self.seqs[sid].n_computed for sid in pending}) \
             if chained else None
         if self.use_graphs:
-            g, hs = self.graphs.get((M, L)) or self._capture(M, L)
+            g, hs = self.graphs.get((M, L, self._gated)) or self._capture(M, L)
             g.replay()
             self.stats["graph_replays"] += 1
         else:

@@ -105,6 +105,8 @@ class Settings(BaseModel):
     VWA_DEBOUNCE_MS: float = Field(1000.0, description="final transcript -> brain call debounce (reference: 1000)")
     VWA_COMMIT_MS: float = Field(0.0, description="voice: silence after the speech end before pending finals are a command (0: the ASR endpoint; speech resuming earlier holds them -- voice/server.py commit policy)")
     VWA_SPEC_BRAIN: bool = Field(True, description="voice: start the brain on the ASR's speculative final pass (its answer is used only for exactly that text)")
+    VWA_ASR_BUSY_FILE: Optional[str] = Field(None, description="/dev/shm word the voice worker's ASR batcher marks busy while recognition runs (shared-GPU deployment: the brain's decode uses the chained launch only while it is idle; launch.py sets it)")
+    VWA_ASR_BUSY_HOLD_MS: float = Field(20.0, description="brain: keep the per-kernel decode form this long after the last ASR pass ended")
     VWA_ENDPOINT_MS: float = Field(300.0, description="trailing silence that ends an utterance (VAD endpoint)")
     VWA_SPEC_FINAL_MS: float = Field(120.0, description="trailing silence that starts the speculative final pass (0: off)")
     VWA_VAD_THRESHOLD: float = Field(300.0, description="speech frame RMS floor (PCM16 units)")
@@ -134,7 +136,8 @@ class Settings(BaseModel):
     VWA_CHAIN_ASR: bool = Field(False, description="chained Whisper decoder launches (measured slower; off)")
     VWA_CHAIN_GRID_DIV: Optional[str] = Field(None, description="chained launch on CUs / k workgroups (shared GPU)")
     VWA_CHAIN_PLAN: bool = Field(True, description="chained attention: layer 0 writes the step's work plan, layers 1.. read it")
-    VWA_CHAIN_MULTI: bool = Field(True, description="chained decode: layers 0 .. L-2 in ONE launch (skinny_stream.hip chain_kernel MULTI; the last layer, without a next QKV, is its own launch)")
+    VWA_CHAIN_MULTI: bool = Field(True, description="chained decode: all layers in ONE launch (skinny_stream.hip chain_kernel MULTI)")
+    VWA_CHAIN_BAR_MODE: int = Field(2, description="chained launches' grid barrier: 2 two-level tickets + scalar polls (default), 4 no-return arrivals + polled sum of the 8 group counters")
     VWA_CHAIN_SCHED: Optional[str] = Field(None, description="DIAGNOSTIC: chained schedule override name=value,...")
     VWA_GEMM_QKV: bool = Field(True, description="> 16-row QKV: rotary + KV write in the tiled GEMM epilogue")
     VWA_GEMM_P8: Optional[str] = Field(None, description="DIAGNOSTIC: 256x256 8-phase GEMM eligibility override")
