@@ -1,3 +1,4 @@
+#include <mutex>
 // PyTorch bindings for the gfx950 kernel library.
 //
 // Every entry point validates shapes/dtypes/devices on the host BEFORE launching (a bad
@@ -558,12 +559,13 @@ void chain_schedule(ChainParams& cp) {
   // the QKV phase's two items go out at the down -> QKV barrier (half the workgroups take two of its
   // 384 tiles): 100.96 / 100.84 vs 101.38 / 101.57 us (profiles/r5_chain_pre_mask.jsonl)
   cp.pre_mask = 8;
-  // round 6: the multi-layer launch's QKV -> next-attention hand-off (grid barrier; per-kv-group
-  // counters and a K/V prefetch measured no better, kept as schedule options) and the attention
-  // workgroups' gate/up item 0 issued during their attention
+  // round 6 schedule options, all measured no better than the defaults: the
+  // multi-layer launch's QKV -> next-attention hand-off by per-kv-group counters instead of the
+  // grid barrier, a K/V prefetch while the attention workgroups wait, and (fp8) gate/up's item 0
+  // issued by the attention workgroups during their attention
   cp.qkv_flags = 0;  // (per-kv-group counters measured 99.5 -> 100.9 us per layer: the barrier stays)
   cp.kv_prefetch = 0;  // (neutral: 99.47 vs 99.53 us per layer, profiles/r6_chain_multi_variants.jsonl)
-  cp.attn_pre = 1;
+  cp.attn_pre = 0;  // (fp8 chain: 2503.7 vs 2471.6 us GPU wait per step with it, bench.py --dtype fp8)
   // diagnostic override of the schedule (tools/chain_probe.py A/B runs): "name=value,..."
   if (const char* e = std::getenv("VWA_CHAIN_SCHED")) {
     std::string s(e);
@@ -817,14 +819,27 @@ void decode_advance(Tensor tokens, Tensor positions, Tensor ctx_lens, Tensor slo
 }
 
 // Device memory the L2 does not cache (hipDeviceMallocUncached): chain barrier words polled with
-// scalar loads.  Returned as an int32 tensor that frees the allocation with hipFree.
+// scalar loads.  Returned as an int32 tensor whose deleter DEFERS the hipFree to the next
+// allocation: the tensor may die in a garbage collection that runs inside another model's graph
+// capture, where a hipFree is not permitted (seen: the whole process aborted in the GC of an
+// earlier test's model during the next test's capture).
+static std::mutex g_uncached_mu;
+static std::vector<void*> g_uncached_pending;
+
 Tensor alloc_uncached_i32(int64_t n, Tensor like) {
   c10::DeviceGuard g(like.device());
+  {
+    std::lock_guard<std::mutex> lk(g_uncached_mu);
+    for (void* p : g_uncached_pending) (void)hipFree(p);
+    g_uncached_pending.clear();
+  }
   void* ptr = nullptr;
   TORCH_CHECK(hipExtMallocWithFlags(&ptr, (size_t)n * 4, hipDeviceMallocUncached) == hipSuccess, "uncached malloc");
   TORCH_CHECK(hipMemset(ptr, 0, (size_t)n * 4) == hipSuccess, "memset");
-  return torch::from_blob(ptr, {n}, [](void* p) { (void)hipFree(p); },
-                          torch::dtype(torch::kInt).device(like.device()));
+  return torch::from_blob(ptr, {n}, [](void* p) {
+        std::lock_guard<std::mutex> lk(g_uncached_mu);
+        g_uncached_pending.push_back(p);
+      }, torch::dtype(torch::kInt).device(like.device()));
 }
 
 // n_layers > 1: desc holds n_layers consecutive descriptors (torch.cat of chain_make outputs of
