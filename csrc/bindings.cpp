@@ -858,6 +858,93 @@ void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like, int64_t 
            "chain");
 }
 
+// Persistent Whisper decoder (whisper_dec.hip): per-layer descriptors from a flat list of 22
+// tensors per layer -- (W, bias, ln_c) of qkv, out-proj, cross query, cross out-proj, fc1, fc2
+// (pre-tiled bf16 weights; bias / ln_c may be None), then k_cache, v_cache, cross K, cross V.
+Tensor wdec_layers(std::vector<c10::optional<Tensor>> flat, int64_t n_layers, Tensor like) {
+  constexpr int kPer = 3 * kWdGemms + 4;
+  TORCH_CHECK(n_layers >= 1 && (int64_t)flat.size() == n_layers * kPer, "wdec_layers: 22 entries per layer");
+  auto ptr = [&](int64_t i, bool need) -> void* {
+    const auto& t = flat[(size_t)i];
+    if (!t.has_value()) {
+      TORCH_CHECK(!need, "wdec_layers: entry ", i, " is required");
+      return nullptr;
+    }
+    TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->device() == like.device(), "wdec_layers: entry ", i,
+                " must be a contiguous tensor on the model's GPU");
+    return t->data_ptr();
+  };
+  Tensor host = torch::zeros({n_layers * (int64_t)sizeof(WdecLayer)}, torch::dtype(torch::kUInt8));
+  auto* L = reinterpret_cast<WdecLayer*>(host.data_ptr());
+  for (int64_t li = 0; li < n_layers; ++li) {
+    const int64_t b = li * kPer;
+    for (int g = 0; g < kWdGemms; ++g) {
+      const auto& w = flat[(size_t)(b + 3 * g)];
+      TORCH_CHECK(w.has_value() && w->scalar_type() == at::kBFloat16, "wdec_layers: bf16 weights");
+      L[li].g[g].W = static_cast<const uint16_t*>(ptr(b + 3 * g, true));
+      L[li].g[g].bias = static_cast<const uint16_t*>(ptr(b + 3 * g + 1, false));
+      const auto& c = flat[(size_t)(b + 3 * g + 2)];
+      TORCH_CHECK(!c.has_value() || c->scalar_type() == at::kFloat, "wdec_layers: ln_c f32");
+      L[li].g[g].ln_c = static_cast<const float*>(ptr(b + 3 * g + 2, false));
+    }
+    L[li].k_cache = static_cast<uint16_t*>(ptr(b + 18, true));
+    L[li].v_cache = static_cast<uint16_t*>(ptr(b + 19, true));
+    L[li].xk = static_cast<const uint16_t*>(ptr(b + 20, true));
+    L[li].xv = static_cast<const uint16_t*>(ptr(b + 21, true));
+  }
+  return host.to(like.device());
+}
+
+// bufs: x0, x1, q, att, f, xpart, seq_ids, ctx_lens, slots, block_table, cross_table, cnt
+// ints: n_layers, d, H, ffn, T, block_size, bt_stride, nch, ch_len, sessions, grid
+void wdec_run(Tensor layers, Tensor roles, std::vector<Tensor> bufs, std::vector<int64_t> ints, double eps,
+              double scale, std::vector<int64_t> n_prod) {
+  TORCH_CHECK(bufs.size() == 12 && ints.size() == 11 && n_prod.size() == kWdLevels, "wdec_run: argument counts");
+  const Tensor& like = bufs[0];
+  c10::DeviceGuard g(like.device());
+  const int64_t grid = ints[10];
+  TORCH_CHECK(layers.is_cuda() && layers.numel() == ints[0] * (int64_t)sizeof(WdecLayer), "wdec_run: layers");
+  TORCH_CHECK(roles.is_cuda() && roles.scalar_type() == at::kInt && roles.is_contiguous() &&
+                  roles.numel() == grid * kWdRole, "wdec_run: roles [grid, 32] int32");
+  for (int i = 0; i < 5; ++i) check_bf16(bufs[(size_t)i], "wdec_run activation");
+  WdecParams p{};
+  p.layers = reinterpret_cast<const WdecLayer*>(layers.data_ptr());
+  p.n_layers = (int)ints[0];
+  p.roles = roles.data_ptr<int>();
+  p.d = (int)ints[1];
+  p.H = (int)ints[2];
+  p.ffn = (int)ints[3];
+  p.T = (int)ints[4];
+  p.block_size = (int)ints[5];
+  p.bt_stride = (int)ints[6];
+  p.nch = (int)ints[7];
+  p.ch_len = (int)ints[8];
+  p.sessions = (int)ints[9];
+  p.eps = (float)eps;
+  p.scale = (float)scale;
+  auto bf = [&](int i) { return reinterpret_cast<uint16_t*>(bufs[(size_t)i].data_ptr()); };
+  p.x0 = bf(0);
+  p.x1 = bf(1);
+  p.q = bf(2);
+  p.att = bf(3);
+  p.f = bf(4);
+  TORCH_CHECK(bufs[5].scalar_type() == at::kFloat && bufs[5].numel() >= (int64_t)p.H * p.nch * 66, "wdec_run: xpart");
+  p.xpart = bufs[5].data_ptr<float>();
+  p.seq_ids = bufs[6].data_ptr<int>();
+  p.ctx_lens = bufs[7].data_ptr<int>();
+  TORCH_CHECK(bufs[8].scalar_type() == at::kLong, "wdec_run: slots int64");
+  p.slots = bufs[8].data_ptr<int64_t>();
+  p.block_table = bufs[9].data_ptr<int>();
+  p.cross_table = bufs[10].data_ptr<int>();
+  TORCH_CHECK(bufs[11].numel() >= 2 * 1025, "wdec_run: counter words (uncached, >= 1025 u64)");
+  p.cnt = reinterpret_cast<unsigned long long*>(bufs[11].data_ptr());
+  for (int l = 0; l < kWdLevels; ++l) {
+    TORCH_CHECK(n_prod[(size_t)l] > 0, "wdec_run: every level needs a producer");
+    p.n_prod[l] = (int)n_prod[(size_t)l];
+  }
+  check_rc(vwa_wdec_launch(&p, (int)grid, cur_stream(like)), "wdec");
+}
+
 void rmsnorm(Tensor x, c10::optional<Tensor> residual, c10::optional<Tensor> residual_out, c10::optional<Tensor> w,
              Tensor y, double eps) {
   c10::DeviceGuard g(x.device());
@@ -1368,6 +1455,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("chain_run", &chain_run, py::arg("desc"), py::arg("n_phases"), py::arg("lds"), py::arg("like"),
         py::arg("attn_g") = 0, py::arg("seq") = 0, py::arg("n_layers") = 1);
   m.def("alloc_uncached_i32", &alloc_uncached_i32);
+  m.def("device_cus", [](Tensor like) { return (int64_t)device_cus(like); });
+  m.def("wdec_layers", &wdec_layers, py::arg("flat"), py::arg("n_layers"), py::arg("like"));
+  m.def("wdec_run", &wdec_run, py::arg("layers"), py::arg("roles"), py::arg("bufs"), py::arg("ints"), py::arg("eps"),
+        py::arg("scale"), py::arg("n_prod"));
   m.def("decode_advance", &decode_advance);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
         py::arg("rstd") = py::none(), py::arg("residual") = py::none(), py::arg("w_tiled") = false,

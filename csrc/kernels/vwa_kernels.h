@@ -198,6 +198,34 @@ struct FlashAttnParams {
   float scale;
 };
 
+// Persistent Whisper decoder step (whisper_dec.hip wdec_kernel): ONE launch runs every decoder
+// layer of a one-row decode step -- eight dependent levels per layer (self-attention QKV, self-
+// attention, out-proj, cross query, cross-attention, cross out-proj, fc1, fc2) -- with each
+// workgroup's share of a layer's weights held in registers from the previous layer on.
+enum { kWdLevels = 8, kWdGemms = 6, kWdRole = 32 };
+struct WdecGemm {
+  const uint16_t* W;      // pre-tiled bf16 [N / 16][K / 128][4 KB] (ops.tile_weight)
+  const uint16_t* bias;   // [N] or null
+  const float* ln_c;      // folded LayerNorm column sums [N] (ops.fold_layernorm) or null
+};
+struct WdecLayer {
+  WdecGemm g[kWdGemms];                    // qkv, out-proj, cross query, cross out-proj, fc1, fc2
+  uint16_t* k_cache; uint16_t* v_cache;    // self-attention cache [blocks][H][block_size][64]
+  const uint16_t* xk; const uint16_t* xv;  // cross-attention K / V [sessions][T][H][64]
+};
+struct WdecParams {
+  const WdecLayer* layers; int n_layers;
+  const int* roles;                   // [grid][kWdRole] (models/whisper.py wdec_roles)
+  int d, H, ffn, T, block_size, bt_stride, nch, ch_len, sessions;
+  float eps, scale;
+  uint16_t* x0; uint16_t* x1;         // hidden row ping-pong (x0: the embedding; result in x[n_layers & 1])
+  uint16_t* q; uint16_t* att; uint16_t* f;
+  float* xpart;                       // cross-attention partials [H][nch][2 + 64]
+  const int* seq_ids; const int* ctx_lens; const int64_t* slots; const int* block_table; const int* cross_table;
+  unsigned long long* cnt;            // uncached: level counters [8 levels][8 groups] at 128-byte stride, err word at [1024]
+  int n_prod[kWdLevels];              // workgroups that complete each level (per layer)
+};
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -209,6 +237,8 @@ int vwa_chain_prepare(ChainParams* cp, int grid);
 // attention phase, run by ONE launch (skinny_stream.hip chain_kernel MULTI)
 int vwa_chain_launch(const ChainParams* d_cp, int seq, int n_phases, int attn_g, int lds, int grid, hipStream_t st,
                      int xg2 = 0, int f8 = 0, int o2 = 0, int n_layers = 1);
+// -10: a shape / role table the kernel does not take (the caller keeps per-kernel launches)
+int vwa_wdec_launch(const WdecParams* p, int grid, hipStream_t st);
 int vwa_gemm(int epi, const GemmParams* p, hipStream_t st);
 int vwa_gemm_splits(int M, int N, int K, int cus, int64_t ws_floats, int f8);
 void vwa_gemm_set_split_fill(int pct);  // split-K while tiles x splits < pct % of the CUs (0: bf16 75, fp8 100)

@@ -113,3 +113,28 @@ def test_conv_padded_path_matches_plain_on_cpu():
     xv[:, :, :80] = x
     padded = ops.conv1d_gelu(xv, ops.pad_conv_weight(w, cp), b, stride=1, padded=True)
     assert torch.allclose(plain.float(), padded.float(), atol=2e-2)
+
+
+def test_wdec_roles_cover_every_tile_once():
+    """Role table of the persistent whisper-large decoder (whisper_dec.hip): every tile of every
+    projection on exactly one workgroup (fc2 tiles as four parts in slots 1..4), at most 5 slots,
+    every slot refilled at a level its workgroup works at, producer counts = the work masks."""
+    from voice_enabled_browser_automation_amd.models.whisper import wdec_roles
+
+    d, H, ffn, nch = 1280, 20, 5120, 4
+    R, n_prod = wdec_roles(256, d, H, ffn, nch)
+    kind, tile, part, rel, work = R[:, 0:5], R[:, 5:10], R[:, 10:15], R[:, 15:20], R[:, 23]
+    want = {0: 3 * d // 16, 2: d // 16, 3: d // 16, 5: d // 16, 6: ffn // 16, 7: d // 16}
+    for lvl, n in want.items():
+        seen = sorted((int(tile[w, s]), int(part[w, s])) for w in range(256) for s in range(5) if kind[w, s] == lvl)
+        parts = 4 if lvl == 7 else 1
+        assert seen == [(t, p) for t in range(n) for p in range(parts)], lvl
+    for w in range(256):
+        for s in range(5):
+            if kind[w, s] >= 0:
+                assert (work[w] >> rel[w, s]) & 1, (w, s)  # the refill fires at a level this workgroup runs
+        fc2 = [s for s in range(5) if kind[w, s] == 7]
+        assert fc2 in ([], [1, 2, 3, 4])
+    assert sorted(R[:, 20][R[:, 20] >= 0].tolist()) == list(range(H))
+    assert sorted(R[:, 21][R[:, 21] >= 0].tolist()) == list(range(H * nch))
+    assert n_prod == [int(((work >> lvl) & 1).sum()) for lvl in range(8)] and min(n_prod) > 0

@@ -460,6 +460,77 @@ def test_whisper_chained_decoder_matches_per_kernel_path(name, monkeypatch):
         assert err < 0.02 * (1 + b.abs().max().item()), err
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_whisper_persistent_decoder_matches_per_kernel_path(graphs, monkeypatch):
+    """The persistent whisper-large decoder step (whisper_dec.hip: every layer in ONE launch,
+    weights a layer ahead in registers, counter hand-offs) against the per-kernel path on the same
+    weights, caches and cross K/V: one row per step, two sessions, contexts up to 70 keys (several
+    KV blocks), 4 decoder layers; replayed from a hipGraph too."""
+    import dataclasses
+
+    from voice_enabled_browser_automation_amd.asr.engine import WhisperRunner
+
+    ops.ext()
+    cfg = dataclasses.replace(get_config("whisper-large-v3"), n_enc_layers=1, n_dec_layers=4)
+    m = WhisperModel(cfg, device="cuda", seed=3)
+    assert m.dec_tiled
+    torch.manual_seed(4)
+    enc = [torch.randn(1, cfg.n_audio_ctx, cfg.d_model, device="cuda").to(torch.bfloat16) for _ in range(2)]
+    runners = []
+
+    def run(persist: bool):
+        monkeypatch.setenv("VWA_ASR_PERSIST", "1" if persist else "0")
+        r = WhisperRunner(m, max_sessions=2, use_graphs=graphs)
+        runners.append(r)
+        r.set_cross(0, enc[0])
+        r.set_cross(1, enc[1])
+        out = []
+        for p in range(70):
+            for s in (0, 1):
+                lg = r.step([(s, (13 * p + 5 * s) % 1000, p)])
+                if p % 9 == 0 or p == 69:
+                    out.append(lg.float().cpu().clone())
+        return out
+
+    ref = run(False)
+    got = run(True)
+    assert m._wdec and not m.chain_error()
+    for i, (a, b) in enumerate(zip(got, ref)):
+        err = (a - b).abs().max().item()
+        assert err < 0.02 * (1 + b.abs().max().item()), (i, err)
+
+
+def test_wdec_counters_survive_launch_sequences(monkeypatch):
+    """Counter bases across many launches of the persistent decoder (monotonic counters, no reset):
+    200 steps in a row keep matching the per-kernel path at the end."""
+    import dataclasses
+
+    from voice_enabled_browser_automation_amd.asr.engine import WhisperRunner
+
+    ops.ext()
+    cfg = dataclasses.replace(get_config("whisper-large-v3"), n_enc_layers=1, n_dec_layers=2)
+    m = WhisperModel(cfg, device="cuda", seed=8)
+    torch.manual_seed(5)
+    enc = torch.randn(1, cfg.n_audio_ctx, cfg.d_model, device="cuda").to(torch.bfloat16)
+    runners = []
+
+    def run(persist: bool):
+        monkeypatch.setenv("VWA_ASR_PERSIST", "1" if persist else "0")
+        r = WhisperRunner(m, max_sessions=1, use_graphs=True)
+        runners.append(r)
+        r.set_cross(0, enc)
+        for _ in range(50):  # the same position again and again: 200 launches
+            for p in range(4):
+                lg = r.step([(0, (7 * p) % 1000, p)])
+        return lg.float().cpu().clone()
+
+    ref = run(False)
+    got = run(True)
+    assert not m.chain_error()
+    err = (got - ref).abs().max().item()
+    assert err < 0.02 * (1 + ref.abs().max().item()), err
+
+
 @pytest.mark.parametrize("chain", [False, True])
 def test_whisper_tiled_decoder_matches_row_major(chain, monkeypatch):
     """Decode-step weights in the pre-tiled layout (large models: WhisperModel._tile_decoder; the

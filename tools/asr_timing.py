@@ -26,7 +26,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tokens", type=int, default=40)
     ap.add_argument("--batch", default="", help="also time transcribe_many over B utterances (comma list)")
-    ap.add_argument("--modes", default="0,1", help="VWA_CHAIN_ASR values to time (0 per-kernel, 1 chained)")
+    ap.add_argument("--modes", default="0,p",
+                    help="decoder forms to time: 0 per-kernel, 1 chained launches (VWA_CHAIN_ASR), p the persistent "
+                         "one-launch decoder (VWA_ASR_PERSIST, whisper-large)")
     ap.add_argument("--small-max-m", type=int, default=None,
                     help="A/B: rows up to which small weights take the one-tile kernel (16: the tiled GEMM above 16)")
     a = ap.parse_args()
@@ -57,7 +59,8 @@ def main():
     audio = None
     texts = {}
     for chain in a.modes.split(","):
-        os.environ["VWA_CHAIN_ASR"] = chain
+        os.environ["VWA_CHAIN_ASR"] = "1" if chain == "1" else "0"
+        os.environ["VWA_ASR_PERSIST"] = "1" if chain == "p" else "0"
         m.reset_chains()
         eng = AsrEngine(m, load_tokenizer("whisper"), max_sessions=2)
         audio = eng.pcm_to_audio(synth_speech(10.0, seed=100))
@@ -71,13 +74,15 @@ def main():
             enc.append(s["encode_ms"])
             dec.append(s["decode_ms"])
             tot.append(s["total_ms"])
-        print(json.dumps(dict(tool="asr_timing", asr=a.asr, chain=chain == "1", tokens=a.tokens,
+        print(json.dumps(dict(tool="asr_timing", asr=a.asr, chain=chain == "1", persistent=chain == "p",
+                              persistent_used=bool(getattr(m, "_wdec", None)), tokens=a.tokens,
                               encode_ms=round(statistics.median(enc), 2), decode_ms=round(statistics.median(dec), 2),
                               total_ms=round(statistics.median(tot), 2),
                               decode_us_per_token=round(1e3 * statistics.median(dec) / a.tokens, 1),
                               chained=bool(m.chain_descs()))), flush=True)
-    if len(texts) == 2:
-        print(json.dumps(dict(tool="asr_timing", same_text=texts["0"] == texts["1"])), flush=True)
+    if len(texts) >= 2:
+        print(json.dumps(dict(tool="asr_timing", same_text=len(set(texts.values())) == 1,
+                              modes=list(texts), error=bool(m.chain_error()))), flush=True)
 
 
 if __name__ == "__main__":

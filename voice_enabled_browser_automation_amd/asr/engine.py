@@ -88,6 +88,7 @@ class WhisperRunner:
         self.use_graphs = bool(use_graphs) and dev.type == "cuda"
         self.graphs: Dict[int, Tuple[torch.cuda.CUDAGraph, torch.Tensor]] = {}
         self.pool = None
+        self._copy_done: Optional["torch.cuda.Event"] = None  # the last step's staging copy (step())
 
     def set_cross(self, slot: int, enc_states: torch.Tensor) -> None:
         """Compute this session's cross-attention K/V from encoder states [1, T, d]."""
@@ -118,6 +119,12 @@ class WhisperRunner:
         """rows: (session slot, token, position). Returns f32 logits [len(rows), vocab_padded]."""
         n = len(rows)
         M = next(bk for bk in BUCKETS if bk >= n)
+        if self._copy_done is not None:
+            # the previous step's pinned -> device copy may still be queued behind its forward:
+            # rewriting the pinned rows before it ran would feed that step the NEXT step's tokens /
+            # positions / slots (back-to-back step() calls with no host sync in between; the
+            # one-launch decoder leaves the host far ahead of the GPU)
+            self._copy_done.synchronize()
         hi = self.h_i32
         for i, (slot, tok, pos) in enumerate(rows):
             hi[0, i], hi[1, i], hi[2, i], hi[3, i] = tok, pos, slot, pos + 1
@@ -128,6 +135,10 @@ class WhisperRunner:
             self.h_slots[i] = -1
         b = self.b
         b.step_in.copy_(self.h_in, non_blocking=True)
+        if self.device.type == "cuda":
+            if self._copy_done is None:
+                self._copy_done = torch.cuda.Event()
+            self._copy_done.record()
         if self.use_graphs:
             g, out = self.graphs.get(M) or self._capture(M)
             g.replay()

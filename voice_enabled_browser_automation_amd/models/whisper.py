@@ -27,6 +27,79 @@ from .config import WhisperConfig
 from .llama import move_model  # noqa: F401  (re-export)
 
 
+WDEC_LEVELS = ("qkv", "self_attn", "o", "xq", "cross_attn", "xo", "fc1", "fc2")
+
+
+def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
+    """Role table of the persistent Whisper decoder (csrc/kernels/whisper_dec.hip): per workgroup
+    32 ints -- slot kinds (level index or -1), tiles, parts, reload levels, self-attention head,
+    cross-attention item, the level after which the next layer's cross K/V chunk is prefetched, and
+    the mask of levels it completes -- plus the producer count of each level.
+
+    Every layer's weights are spread so each workgroup holds at most 5 slots of 5 loads per wave
+    (one 16-column tile of a K = d projection per slot; an fc2 tile, K = 4 d, takes slots 1..4):
+    fc2 tiles on workgroups [0, d/16), QKV tiles on the last 3 d / 16, the out / cross projections
+    and fc1 in the free slots of the rest.  A slot is refilled right after the level that used it
+    (its next use is a layer later); workgroups that run the self-attention refill after it, so the
+    attention's loads do not queue behind 40-200 KB of weights.  Cross-attention items (head, key
+    chunk) go to the fc2 workgroups, idle from the QKV level to fc2."""
+    import numpy as np
+
+    assert ffn == 4 * d and d % 256 == 0
+    n_qkv, n_d, n_ff = 3 * d // 16, d // 16, ffn // 16
+    n_x = H * nch
+    if nwg < max(n_qkv, n_d + 16, n_x, H) or n_d > nwg:
+        raise ValueError(f"wdec_roles: {nwg} workgroups cannot hold the decoder's tiles")
+    R = np.full((nwg, 32), -1, dtype=np.int32)
+    R[:, 10:15] = 0
+    kind, tile, part, rel = R[:, 0:5], R[:, 5:10], R[:, 10:15], R[:, 15:20]
+    LQ, LS, LO, LXQ, LX, LXO, L1, L2 = range(8)
+    for t in range(n_d):  # fc2: slots 1..4 of workgroup t
+        kind[t, 1:5], tile[t, 1:5], part[t, 1:5] = L2, t, np.arange(4)
+    q0 = nwg - n_qkv
+    for t in range(n_qkv):
+        kind[q0 + t, 0], tile[q0 + t, 0] = LQ, t
+    R[:H, 20] = np.arange(H)
+    R[:n_x, 21] = np.arange(n_x)
+    R[:n_x, 22] = LX
+    free = [(s, w) for s in range(1, 5) for w in range(nwg) if kind[w, s] < 0 and w >= n_d]
+    free.sort()
+    fi = 0
+    for lvl, n in ((LO, n_d), (LXQ, n_d), (LXO, n_d), (L1, n_ff)):
+        for t in range(n):
+            if fi >= len(free):
+                raise ValueError("wdec_roles: not enough free slots")
+            s, w = free[fi]
+            fi += 1
+            kind[w, s], tile[w, s] = lvl, t
+    for w in range(nwg):
+        sat = R[w, 20] >= 0
+        for s in range(5):
+            k = kind[w, s]
+            if k < 0:
+                continue
+            if k == L2:  # refilled at the workgroup's first level of the next layer
+                rel[w, s] = LS if sat else (LQ if kind[w, 0] == LQ else L2)
+            elif k == LQ and sat:
+                rel[w, s] = LS
+            else:
+                rel[w, s] = k
+    work = np.zeros(nwg, dtype=np.int64)
+    for w in range(nwg):
+        m = 0
+        for s in range(5):
+            if kind[w, s] >= 0:
+                m |= 1 << int(kind[w, s])
+        if R[w, 20] >= 0:
+            m |= 1 << LS
+        if R[w, 21] >= 0:
+            m |= 1 << LX
+        work[w] = m
+    R[:, 23] = work
+    n_prod = [int(((work >> lvl) & 1).sum()) for lvl in range(8)]
+    return R, n_prod
+
+
 def sinusoids(length: int, channels: int, max_timescale: float = 10000.0) -> torch.Tensor:
     inc = math.log(max_timescale) / (channels // 2 - 1)
     inv = torch.exp(-inc * torch.arange(channels // 2, dtype=torch.float32))
@@ -307,6 +380,7 @@ class WhisperModel:
 
     def disable_chain(self) -> None:
         self._chain_disabled = True
+        self._wdec_disabled = True  # (a timed-out persistent launch: its counters are out of step)
         self.reset_chains()
 
     def reset_chains(self) -> None:
@@ -321,6 +395,9 @@ class WhisperModel:
 
     def chain_error(self) -> bool:
         w = self.chain_error_word()
+        if w is not None and int(w.item()) != 0:
+            return True
+        w = self.wdec_error_word()
         return bool(w is not None and int(w.item()) != 0)
 
     def _chain_descs(self, bufs, M: int, li: int):
@@ -360,16 +437,75 @@ class WhisperModel:
                       (tail[0], len(E), tail[1]) if tail[0].numel() else None)
         return cache[key]
 
+    # ---- persistent decoder (csrc/kernels/whisper_dec.hip wdec_kernel): a one-row step of the
+    # whisper-large family (d 1280, ffn 5120, head_dim 64, pre-tiled decoder weights) as ONE launch
+    # over every decoder layer; each workgroup's weight tiles stay in its registers a layer ahead.
+    def _wdec_ok(self, M: int) -> bool:
+        cfg = self.cfg
+        return (M == 1 and self.device.type == "cuda" and self.dec_tiled and cfg.d_model == 1280
+                and cfg.ffn == 4 * cfg.d_model and self.hd == 64 and cfg.n_dec_layers >= 2
+                and not getattr(self, "_wdec_disabled", False) and ops.env_flag("VWA_ASR_PERSIST")
+                and ops.native_available())
+
+    def _wdec_state(self, bufs):
+        """(layer descriptors, roles, n_prod, counters, partials, grid) for these buffers, built once
+        (the descriptors embed raw pointers of the buffers and the weights)."""
+        if not isinstance(getattr(self, "_wdec", None), weakref.WeakKeyDictionary):
+            self._wdec = weakref.WeakKeyDictionary()
+        st = self._wdec.get(bufs)
+        if st is not None:
+            return st
+        cfg = self.cfg
+        E = ops.ext()
+        grid = int(E.device_cus(bufs.hidden))  # one workgroup per CU, all resident
+        nch = 4
+        roles, n_prod = wdec_roles(grid, cfg.d_model, self.H, cfg.ffn, nch)
+        wt = lambda t: t.t if isinstance(t, ops.TiledWeight) else t  # noqa: E731
+        flat = []
+        for li, L in enumerate(self.dec):
+            (wq, bq, cq), (wx, bx, cx), (w1, b1, c1) = L.f_qkv, L.f_xq, L.f_fc1
+            flat += [wt(wq), bq, cq, wt(L.o), L.o_b, None, wt(wx), bx, cx, wt(L.xo), L.xo_b, None,
+                     wt(w1), b1, c1, wt(L.fc2), L.fc2_b, None,
+                     bufs.k_cache[li], bufs.v_cache[li], bufs.cross[li][0], bufs.cross[li][1]]
+        layers = E.wdec_layers(flat, len(self.dec), bufs.hidden)
+        cnt = E.alloc_uncached_i32(4096, bufs.hidden)
+        xpart = torch.zeros(self.H * nch * 66, dtype=torch.float32, device=self.device)
+        T = bufs.cross[0][0].shape[1]
+        st = dict(layers=layers, roles=torch.from_numpy(roles).to(self.device), n_prod=n_prod, cnt=cnt, xpart=xpart,
+                  ints=[len(self.dec), cfg.d_model, self.H, cfg.ffn, T, bufs.k_cache.shape[3],
+                        bufs.block_table.shape[1], nch, -(-T // nch), bufs.cross[0][0].shape[0], grid])
+        self._wdec[bufs] = st
+        return st
+
+    def wdec_error_word(self):
+        st = next(iter(getattr(self, "_wdec", {}).values()), None) if getattr(self, "_wdec", None) else None
+        return None if st is None else st["cnt"].view(torch.int64)[1024:1025]
+
+    def _wdec_step(self, bufs) -> torch.Tensor:
+        """Every decoder layer of a one-row step (the embedding is in bufs.hidden[0]); returns the
+        final hidden row."""
+        st = self._wdec_state(bufs)
+        ops.ext().wdec_run(st["layers"], st["roles"],
+                           [bufs.hidden, bufs.h, bufs.q, bufs.att, bufs.f, st["xpart"], bufs.seq_ids, bufs.ctx_lens,
+                            bufs.slots, bufs.block_table, bufs.cross_table, st["cnt"]],
+                           st["ints"], self.cfg.ln_eps, self.hd ** -0.5, st["n_prod"])
+        return (bufs.hidden if len(self.dec) % 2 == 0 else bufs.h)[:1]
+
     def decode_step(self, bufs, M: int) -> torch.Tensor:
         """M token rows (bufs: tokens/positions/slots/seq_ids/ctx_lens + self cache + cross K/V).
         Returns f32 logits [M, vocab].  Eight launches per layer; with VWA_CHAIN_ASR=1 and M <= 4
         four (self-attention, chained out-proj -> cross query, cross-attention, chained out-proj
-        -> MLP -> next QKV)."""
+        -> MLP -> next QKV); one row of whisper-large with VWA_ASR_PERSIST: ONE launch for every
+        layer (whisper_dec.hip)."""
         cfg = self.cfg
         d = cfg.d_model
         x = bufs.hidden[:M]
         ops.embedding(bufs.tokens, self.tok_emb, pos_table=self.pos_emb, positions=bufs.positions, out=x, rows=M)
         eps = cfg.ln_eps
+        if self._wdec_ok(M):
+            x = self._wdec_step(bufs)
+            w, b, c = self.f_lm
+            return ops.linear(x, w, b, out=bufs.logits[:M], eps=eps, ln_c=c)
         chain = self._chain_ok(M)
         qkv_done = False
         for li, L in enumerate(self.dec):
