@@ -898,7 +898,7 @@ Tensor wdec_layers(std::vector<c10::optional<Tensor>> flat, int64_t n_layers, Te
 // bufs: x0, x1, q, att, f, xpart, seq_ids, ctx_lens, slots, block_table, cross_table, cnt
 // ints: n_layers, d, H, ffn, T, block_size, bt_stride, nch, ch_len, sessions, grid
 void wdec_run(Tensor layers, Tensor roles, std::vector<Tensor> bufs, std::vector<int64_t> ints, double eps,
-              double scale, std::vector<int64_t> n_prod) {
+              double scale, std::vector<int64_t> n_prod, c10::optional<Tensor> ts, int64_t opt) {
   TORCH_CHECK(bufs.size() == 12 && ints.size() == 11 && n_prod.size() == kWdLevels, "wdec_run: argument counts");
   const Tensor& like = bufs[0];
   c10::DeviceGuard g(like.device());
@@ -942,6 +942,12 @@ void wdec_run(Tensor layers, Tensor roles, std::vector<Tensor> bufs, std::vector
     TORCH_CHECK(n_prod[(size_t)l] > 0, "wdec_run: every level needs a producer");
     p.n_prod[l] = (int)n_prod[(size_t)l];
   }
+  if (ts.has_value()) {
+    TORCH_CHECK(ts->is_cuda() && ts->scalar_type() == at::kLong && ts->numel() >= grid * ints[0] * kWdLevels * 4,
+                "wdec_run: ts int64 [grid * n_layers * 8 * 4]");
+    p.ts = reinterpret_cast<unsigned long long*>(ts->data_ptr());
+  }
+  p.opt[0] = (int)opt;
   check_rc(vwa_wdec_launch(&p, (int)grid, cur_stream(like)), "wdec");
 }
 
@@ -1458,7 +1464,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("device_cus", [](Tensor like) { return (int64_t)device_cus(like); });
   m.def("wdec_layers", &wdec_layers, py::arg("flat"), py::arg("n_layers"), py::arg("like"));
   m.def("wdec_run", &wdec_run, py::arg("layers"), py::arg("roles"), py::arg("bufs"), py::arg("ints"), py::arg("eps"),
-        py::arg("scale"), py::arg("n_prod"));
+        py::arg("scale"), py::arg("n_prod"), py::arg("ts") = py::none(), py::arg("opt") = 0);
   m.def("decode_advance", &decode_advance);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
         py::arg("rstd") = py::none(), py::arg("residual") = py::none(), py::arg("w_tiled") = false,

@@ -224,6 +224,8 @@ struct WdecParams {
   const int* seq_ids; const int* ctx_lens; const int64_t* slots; const int* block_table; const int* cross_table;
   unsigned long long* cnt;            // uncached: level counters [8 levels][8 groups] at 128-byte stride, err word at [1024]
   int n_prod[kWdLevels];              // workgroups that complete each level (per layer)
+  unsigned long long* ts;             // diagnostic stamps [grid][n_layers * 8][4] (tools/wdec_probe.py) or null
+  int opt[4];                         // schedule options (whisper_dec.hip kOpt*)
 };
 
 #ifdef __cplusplus

@@ -4,11 +4,9 @@
 // Why: the per-kernel decoder runs eight dependent launches per
 // layer, each ~5-9 us of fixed latency (dispatch, X staging, the first weight bytes, reduce,
 // epilogue) for 0.3-13 MB of weights -- 2.3 ms per token for ~1.6 GB, 7x off the HBM roofline.
-// Here the eight levels of a layer are separated only by completion counters, and a workgroup's
-// share of the NEXT use of each of its weight tiles is already in its registers: a level's
-// critical path is the counter hand-off, the activation row (a few KB from L2 / MALL) and a few
-// MFMAs -- the weight bytes stream in the background (each slot is refilled right after the level
-// that consumed it, a full layer ahead of its next use).
+// Here a workgroup's share of the NEXT use of each of its weight tiles is already in its registers
+// (refilled right after the level that consumed it), so a level's critical path is the hand-off of
+// the activation row (a few KB through the MALL) and a few MFMAs.
 //
 // Levels of layer li (reference call site this replaces: /root/reference/apps/voice/src/
 // deepgram.ts:36-45, the hosted recogniser):
@@ -22,17 +20,21 @@
 //   6 FC1      f = GELU(LN2(x2) . W1^T + b1)                      (320 tiles)
 //   7 FC2      x3 = x2 + f . W2^T + b2                            (80 tiles, K = 5120)
 // LayerNorms are folded into the weights (ops.fold_layernorm: y = rstd (x.Wg - mean c) + b'), the
-// mean / rstd come from the staged row.  Hand-off: a producer workgroup drains its stores and adds
-// 1 (no return) to its level's counter of its XCD group; consumers poll the sum of the eight group
-// counters with scalar loads (uncached words: the poll does not queue behind vector loads).
-// Counters are monotonic: a launch adds n_prod[level] x n_layers to each, so every workgroup
-// derives the launch's base from the value it reads at its start.
+// mean / rstd come from the staged row.
 //
+// Hand-off: a producer workgroup drains its stores and adds 1 (no return) to its level's counter of
+// its XCD group; consumers poll the sum of the eight group counters with scalar loads (uncached
+// words: the poll does not queue behind vector loads).  Counters are monotonic: a launch adds
+// n_prod[level] x n_layers to each, so every workgroup derives the launch's base from the value it
+// reads at its start.  (Measured and not kept: values tagged with their (launch, layer, level) and
+// the counter add issued without the store drain -- consumers then re-polled for the same store
+// latency and the cross merge polled word by word: 38.2 vs 36.5 us per layer, tools/wdec_probe.py.)
+
 // Weight slots: 5 slots x 5 loads of 1 KB per wave (100 VGPRs).  A 16-column tile of a K = 1280
 // projection is 40 load-slices (k-group, 32-k slice) of the pre-tiled layout; wave w takes slices
 // w, w + 8, ... -- 5 per wave = one slot.  An fc2 tile (K = 5120) is 20 per wave = slots 1..4.
 // The role table (models/whisper.py wdec_roles) gives each workgroup its slots (level, tile, part,
-// reload level), its self-attention head and its cross-attention item.
+// refill level), its self-attention head and its cross-attention item.
 #include "common.h"
 #include "vwa_kernels.h"
 
@@ -46,19 +48,19 @@ enum { LV_QKV = 0, LV_SATT, LV_O, LV_XQ, LV_XATT, LV_XO, LV_FC1, LV_FC2 };
 enum { R_KIND = 0, R_TILE = 5, R_PART = 10, R_RELOAD = 15, R_SATT = 20, R_XATT = 21, R_XPRE = 22, R_WORK = 23 };
 // LDS layout (bytes)
 constexpr int L_XS = 0;          // bf16 activation row (<= 5120)
-constexpr int L_RED = 10368;     // f32 [8][16] cross-wave partial sums of a tile / reductions
-constexpr int L_STAT = 10880;    // f32 [16]: mean, rstd, row max / sum
-constexpr int L_W8 = 10944;      // f32 [2][8] per-wave reduction values
-constexpr int L_QF = 11008;      // f32 [64] query head
-constexpr int L_P = 11264;       // f32 [512] attention weights
-constexpr int L_OW = 13312;      // f32 [8][64] per-wave attention outputs
-constexpr int L_VA = 15360;      // int [512] self-attention V row offsets (elements)
+constexpr int L_RED = 10368;     // f32 [8][32] cross-wave partial sums of a level's <= 2 tiles
+constexpr int L_STAT = 11392;    // f32 [16]: mean, rstd
+constexpr int L_W8 = 11456;      // f32 [2][8] per-wave reduction values
+constexpr int L_QF = 11520;      // f32 [64] query head
+constexpr int L_P = 11776;       // f32 [512] attention weights
+constexpr int L_OW = 13824;      // f32 [8][64] per-wave attention outputs
+constexpr int L_VA = 15872;      // int [512] self-attention K / V row offsets (elements)
 constexpr int L_KV = 65536;      // cross-attention K chunk [<= 384][64] bf16, V chunk at + 48 KB
 constexpr int L_KVV = 49152;
 constexpr int kLds = 163840;
 constexpr int kMaxChunk = 384;
-constexpr int kSpinLimit = 1 << 18;  // ~0.3 s: a non-resident workgroup ends the launch, not the GPU
-constexpr int kErrWord = 1024;
+constexpr int kSpinLimit = 1 << 17;  // bounded polls: a non-resident producer ends the launch, not the GPU
+constexpr int kErrWord = 1024;       // (WdecParams::cnt u64 index of the error flag)
 
 VWA_DEVICE int gemm_of(int lvl) {
   return lvl == LV_QKV ? 0 : lvl == LV_O ? 1 : lvl == LV_XQ ? 2 : lvl == LV_XO ? 3 : lvl == LV_FC1 ? 4 : 5;
@@ -69,7 +71,7 @@ VWA_DEVICE __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long long bytes) {
                                            0x00020000);
 }
 
-// sc1 (device-coherent) 16-byte load of data another workgroup wrote in this launch
+// sc1 (device-coherent) loads / stores of data crossing workgroups inside the launch
 VWA_DEVICE uint4 ld_sc1_b128(__amdgpu_buffer_rsrc_t r, unsigned off) {
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
   return make_uint4(v.x, v.y, v.z, v.w);
@@ -78,6 +80,10 @@ VWA_DEVICE float ldf_sc1(const float* p) { return __hip_atomic_load(gp(p), __ATO
 VWA_DEVICE void stf_sc1(float* p, float v) { __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 VWA_DEVICE u16 ldh_sc1(const u16* p) { return __hip_atomic_load(gp(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 VWA_DEVICE void sth_sc1(u16* p, u16 v) { __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+VWA_DEVICE void set_err(const WdecParams& p) {
+  __hip_atomic_store(gp(p.cnt + kErrWord), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // sum of a level's eight group counters in one scalar round trip (glc: past the scalar cache)
 VWA_DEVICE unsigned long long cnt_sum8(const unsigned long long* c) {
@@ -101,7 +107,7 @@ VWA_DEVICE unsigned long long cnt_sum8(const unsigned long long* c) {
 VWA_DEVICE unsigned long long* lvl_cnt(const WdecParams& p, int lvl) { return p.cnt + (size_t)lvl * 8 * 16; }
 
 // wave 0 polls until the level's counters reach target; bounded (a timed-out spin sets the error
-// word and goes on: that step's results are invalid, the host falls back to per-kernel launches)
+// word: that step's results are invalid, the host falls back to per-kernel launches)
 VWA_DEVICE void wd_wait(const WdecParams& p, int lvl, unsigned long long target) {
   if (VWA_TX < 64) {
     const unsigned long long* c = lvl_cnt(p, lvl);
@@ -112,7 +118,7 @@ VWA_DEVICE void wd_wait(const WdecParams& p, int lvl, unsigned long long target)
       if ((spins & 255) == 255 && __hip_atomic_load(gp(p.cnt + kErrWord), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
         break;
       if (++spins > kSpinLimit) {
-        if (VWA_TX == 0) __hip_atomic_store(gp(p.cnt + kErrWord), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (VWA_TX == 0) set_err(p);
         break;
       }
     }
@@ -120,13 +126,21 @@ VWA_DEVICE void wd_wait(const WdecParams& p, int lvl, unsigned long long target)
   lds_sync();
 }
 
-// this workgroup completed level lvl: every wave's stores are performed (the caller's vmcnt(0)),
-// then one no-return add on the group counter
+// this workgroup completed level lvl: every wave's stores are performed, then one no-return add on
+// the group counter
 VWA_DEVICE void wd_arrive(const WdecParams& p, int lvl) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_sync();
   if (VWA_TX == 0)
     __hip_atomic_fetch_add(gp(lvl_cnt(p, lvl) + 16 * (blockIdx.x & 7)), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// diagnostic stamp k of (layer, level) (tools/wdec_probe.py): 0 entry, 1 released, 2 row staged
+// (attention levels: softmax done), 3 completed
+VWA_DEVICE void wd_stamp(const WdecParams& p, int li, int lvl, int k) {
+  if (p.ts && VWA_TX == 0)
+    *gp(p.ts + ((size_t)blockIdx.x * p.n_layers * kWdLevels + (size_t)li * kWdLevels + lvl) * 4 + k) =
+        __builtin_amdgcn_s_memrealtime();
 }
 
 VWA_DEVICE int n_cols(const WdecParams& p, int lvl) {
@@ -177,7 +191,10 @@ VWA_DEVICE void wd_kv_prefetch(const WdecParams& p, int li, int item, char* lds)
     const bool isv = r >= n8;
     const int rr = isv ? r - n8 : r;
     const int kk = rr * 8 + (lane >> 3);
-    const unsigned off = kk < nk ? (unsigned)(((((long long)sess * p.T + k0 + kk) * p.H + h) * 64 + (lane & 7) * 8) * 2)
+    // K rows XOR-swizzled by 16-byte chunk (LDS slot j of key kk holds chunk j ^ (kk & 7)): the
+    // key-per-thread dot products read 8 different bank groups per 8 lanes instead of one
+    const int chunk = isv ? (lane & 7) : ((lane & 7) ^ (kk & 7));
+    const unsigned off = kk < nk ? (unsigned)(((((long long)sess * p.T + k0 + kk) * p.H + h) * 64 + chunk * 8) * 2)
                                  : 0x7FFFFFF0u;
     auto* dst = (__attribute__((address_space(3))) void*)(lds + L_KV + (isv ? L_KVV : 0) + rr * 1024);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(isv ? rv : rk, dst, 16, off, 0, 0, 0);
@@ -193,7 +210,6 @@ VWA_DEVICE float blk_max(char* lds, float v) {
   float m = w8[0];
 #pragma unroll
   for (int i = 1; i < 8; ++i) m = fmaxf(m, w8[i]);
-  lds_sync();
   return m;
 }
 VWA_DEVICE float blk_sum(char* lds, float v) {
@@ -204,7 +220,6 @@ VWA_DEVICE float blk_sum(char* lds, float v) {
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) s += w8[i];
-  lds_sync();
   return s;
 }
 
@@ -223,12 +238,13 @@ VWA_DEVICE void wd_q_to_lds(const WdecParams& p, int h, char* lds) {
 }
 
 // softmax over the thread-per-key scores s (keys t < nk, others -inf): returns (max, sum); P[t] in LDS
+// (w8 max slots [0, 8) and sum slots [8, 16) are distinct: no barrier between the two reductions)
 VWA_DEVICE float2 wd_softmax(char* lds, float s, bool valid) {
   float* P = reinterpret_cast<float*>(lds + L_P);
   const float m = blk_max(lds, valid ? s : -INFINITY);
   const float e = valid ? __expf(s - m) : 0.f;
   P[VWA_TX] = e;
-  const float l = blk_sum(lds, e);  // (its barriers publish P)
+  const float l = blk_sum(lds, e);  // (its barrier publishes P)
   return make_float2(m, l);
 }
 
@@ -246,26 +262,51 @@ VWA_DEVICE float wd_ow_sum(char* lds, float o) {
   return s;
 }
 
-// level 1: self-attention of head h over the row's context (<= 512 keys: one thread per key)
-VWA_DEVICE void wd_self_attn(const WdecParams& p, int li, int h, char* lds) {
-  const WdecLayer& L = p.layers[li];
-  const int tx = VWA_TX, lane = tx & 63, w = tx >> 6;
+// level 1: self-attention of head h over the row's context (<= 512 keys: one thread per key).
+// The key rows' addresses are resolved ahead of the release (wd_self_attn_pre); after it q, the K
+// rows and the first 8 V elements per lane are issued together -- one round trip (the newest key
+// was written by this layer's QKV level).
+VWA_DEVICE void wd_self_attn_pre(const WdecParams& p, int h, char* lds) {
+  const int tx = VWA_TX;
   const int seq = p.seq_ids[0], ctx = min(p.ctx_lens[0], kT);
   const int bs = p.block_size;
   int* va = reinterpret_cast<int*>(lds + L_VA);
-  const float* qf = reinterpret_cast<const float*>(lds + L_QF);
-  wd_q_to_lds(p, h, lds);
-  const long long cache_bytes = 0x7FFFFFF0ll;
-  const __amdgpu_buffer_rsrc_t rk = rsrc_of(L.k_cache, cache_bytes), rv = rsrc_of(L.v_cache, cache_bytes);
-  float s = -INFINITY;
-  const bool valid = tx < ctx;
-  if (valid) {
+  if (tx < ctx) {
     const int blk = p.block_table[seq * p.bt_stride + tx / bs];
-    const int e0 = ((blk * p.H + h) * bs + tx % bs) * 64;  // element offset of key tx's row
-    va[tx] = e0;
-    uint4 kr[8];
+    va[tx] = ((blk * p.H + h) * bs + tx % bs) * 64;  // element offset of key tx's row
+  }
+  lds_sync();
+}
+
+VWA_DEVICE void wd_self_attn(const WdecParams& p, int li, int h, char* lds) {
+  const WdecLayer& L = p.layers[li];
+  const int tx = VWA_TX, lane = tx & 63, w = tx >> 6;
+  const int ctx = min(p.ctx_lens[0], kT);
+  const int* va = reinterpret_cast<const int*>(lds + L_VA);
+  float* qf = reinterpret_cast<float*>(lds + L_QF);
+  const __amdgpu_buffer_rsrc_t rk = rsrc_of(L.k_cache, 0x7FFFFFF0ll), rv = rsrc_of(L.v_cache, 0x7FFFFFF0ll);
+  uint4 qv = make_uint4(0, 0, 0, 0);
+  if (tx < 8) qv = ld_sc1_b128(rsrc_of(p.q, (long long)p.d * 2), (unsigned)((h * 64 + tx * 8) * 2));
+  uint4 kr[8];
+  const bool valid = tx < ctx;
+  const int e0 = valid ? va[tx] : 0;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) kr[c] = ld_sc1_b128(rk, (unsigned)(e0 * 2 + c * 16));
+  for (int c = 0; c < 8; ++c) kr[c] = valid ? ld_sc1_b128(rk, (unsigned)(e0 * 2 + c * 16)) : make_uint4(0, 0, 0, 0);
+  float vv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int t = w + 8 * i;
+    vv[i] = t < ctx ? bf2f((u16)__builtin_amdgcn_raw_buffer_load_b16(rv, (int)((va[t] + lane) * 2), 0, 16)) : 0.f;
+  }
+  if (tx < 8) {
+    float f[8];
+    unpack8(qv, f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qf[tx * 8 + e] = f[e];
+  }
+  lds_sync();
+  float s = -INFINITY;
+  if (valid) {
     float acc = 0.f;
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -276,11 +317,16 @@ VWA_DEVICE void wd_self_attn(const WdecParams& p, int li, int h, char* lds) {
     }
     s = acc * p.scale;
   }
-  const float2 ml = wd_softmax(lds, s, valid);  // (publishes va too)
+  const float2 ml = wd_softmax(lds, s, valid);
+  wd_stamp(p, li, LV_SATT, 2);
   const float* P = reinterpret_cast<const float*>(lds + L_P);
   float o = 0.f;
-  for (int t0 = w; t0 < ctx; t0 += 64) {  // 8 keys per wave per batch, loads first
-    float vv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int t = w + 8 * i;
+    if (t < ctx) o += P[t] * vv[i];
+  }
+  for (int t0 = w + 64; t0 < ctx; t0 += 64) {  // (contexts beyond 64 keys: 8 keys per wave per batch)
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int t = t0 + 8 * i;
@@ -297,7 +343,7 @@ VWA_DEVICE void wd_self_attn(const WdecParams& p, int li, int h, char* lds) {
 }
 
 // level 4: cross-attention partial of (head, chunk) from the prefetched K / V chunk in LDS
-VWA_DEVICE void wd_cross_attn(const WdecParams& p, int item, char* lds) {
+VWA_DEVICE void wd_cross_attn(const WdecParams& p, int li, int item, char* lds) {
   const int h = item / p.nch, ch = item % p.nch;
   const int k0 = ch * p.ch_len, nk = min(p.ch_len, p.T - k0);
   const int tx = VWA_TX, lane = tx & 63, w = tx >> 6;
@@ -313,16 +359,29 @@ VWA_DEVICE void wd_cross_attn(const WdecParams& p, int item, char* lds) {
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       float f[8];
-      unpack8(*reinterpret_cast<const uint4*>(kl + tx * 64 + c * 8), f);
+      unpack8(*reinterpret_cast<const uint4*>(kl + tx * 64 + ((c ^ (tx & 7)) * 8)), f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc += qf[c * 8 + e] * f[e];
     }
     s = acc * p.scale;
   }
   const float2 ml = wd_softmax(lds, s, valid);
+  wd_stamp(p, li, LV_XATT, 2);
   const float* P = reinterpret_cast<const float*>(lds + L_P);
-  float o = 0.f;
-  for (int t = w; t < nk; t += 8) o += P[t] * bf2f(vl[t * 64 + lane]);
+  // 8 keys per wave per batch, every LDS read of a batch issued before its FMAs
+  float oa[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int t0 = w; t0 < nk; t0 += 64) {
+    float pv[8], vv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int t = min(t0 + 8 * i, nk - 1);
+      pv[i] = t0 + 8 * i < nk ? P[t] : 0.f;
+      vv[i] = bf2f(vl[t * 64 + lane]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) oa[i] += pv[i] * vv[i];
+  }
+  const float o = ((oa[0] + oa[1]) + (oa[2] + oa[3])) + ((oa[4] + oa[5]) + (oa[6] + oa[7]));
   const float tot = wd_ow_sum(lds, o);
   float* part = p.xpart + (size_t)(h * p.nch + ch) * 66;
   if (tx < 64) stf_sc1(part + 2 + tx, tot);
@@ -332,10 +391,10 @@ VWA_DEVICE void wd_cross_attn(const WdecParams& p, int item, char* lds) {
   }
 }
 
-// X staging of a GEMM level: the activation row (bf16, written earlier in this launch) -> LDS;
-// LayerNorm levels also get the row's mean / rstd (from the staged values)
-VWA_DEVICE void wd_stage(const WdecParams& p, int lvl, const u16* x, char* lds, bool ln) {
-  const int K = k_of(p, lvl), n8 = K >> 3;
+// X staging of a GEMM level: the activation row (bf16, written earlier in this launch or, for layer
+// 0, the embedding) -> LDS; LayerNorm levels also get the row's mean / rstd (from the staged values)
+VWA_DEVICE void wd_stage(const WdecParams& p, int K, const u16* x, char* lds, bool ln) {
+  const int n8 = K >> 3;
   const int tx = VWA_TX;
   u16* xs = reinterpret_cast<u16*>(lds + L_XS);
   const __amdgpu_buffer_rsrc_t r = rsrc_of(x, (long long)K * 2);
@@ -351,20 +410,31 @@ VWA_DEVICE void wd_stage(const WdecParams& p, int lvl, const u16* x, char* lds, 
     const int c = tx + i * kT;
     if (c < n8) {
       *reinterpret_cast<uint4*>(xs + c * 8) = v[i];
-      if (ln) {
-        float f[8];
-        unpack8(v[i], f);
+      float f[8];
+      unpack8(v[i], f);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          s += f[e];
-          s2 += f[e] * f[e];
-        }
+      for (int e = 0; e < 8; ++e) {
+        s += f[e];
+        s2 += f[e] * f[e];
       }
     }
   }
-  if (ln) {
+  if (ln) {  // one block reduction of (sum, sum of squares)
+    float* w8 = reinterpret_cast<float*>(lds + L_W8);
+    s = wave_sum(s);
+    s2 = wave_sum(s2);
+    if ((tx & 63) == 0) {
+      w8[tx >> 6] = s;
+      w8[8 + (tx >> 6)] = s2;
+    }
+    lds_sync();
+    float ts = 0.f, ts2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      ts += w8[i];
+      ts2 += w8[8 + i];
+    }
     float* st = reinterpret_cast<float*>(lds + L_STAT);
-    const float ts = blk_sum(lds, s), ts2 = blk_sum(lds, s2);
     if (tx == 0) {
       const float mean = ts / (float)K;
       st[0] = mean;
@@ -375,66 +445,76 @@ VWA_DEVICE void wd_stage(const WdecParams& p, int lvl, const u16* x, char* lds, 
 }
 
 // X staging of the cross out-projection: the attention row merged from the (head, chunk)
-// partials (chunk order fixed: the same bits whoever finished last)
+// partials (chunk order fixed: the same bits whoever finished last); every partial load of the
+// thread's columns issued before any is used
 VWA_DEVICE void wd_stage_merge(const WdecParams& p, char* lds) {
   u16* xs = reinterpret_cast<u16*>(lds + L_XS);
   const int tx = VWA_TX, nch = p.nch;
-  for (int c = tx; c < p.d; c += kT) {
-    const int h = c >> 6, dd = c & 63;
+  constexpr int kC = 3;  // columns per thread (d <= 1536 with 512 threads)
+  float m[kC][4], l[kC][4], o[kC][4];
+#pragma unroll
+  for (int i = 0; i < kC; ++i) {
+    const int c = min(tx + i * kT, p.d - 1), h = c >> 6, dd = c & 63;
     const float* base = p.xpart + (size_t)h * nch * 66;
-    float m[8], l[8], o[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      if (k < nch) {
-        m[k] = ldf_sc1(base + k * 66);
-        l[k] = ldf_sc1(base + k * 66 + 1);
-        o[k] = ldf_sc1(base + k * 66 + 2 + dd);
-      }
+    for (int k = 0; k < 4; ++k) {
+      const int kk = min(k, nch - 1);
+      m[i][k] = ldf_sc1(base + kk * 66);
+      l[i][k] = ldf_sc1(base + kk * 66 + 1);
+      o[i][k] = ldf_sc1(base + kk * 66 + 2 + dd);
     }
-    float mx = m[0];
+  }
 #pragma unroll
-    for (int k = 1; k < 8; ++k)
-      if (k < nch) mx = fmaxf(mx, m[k]);
+  for (int i = 0; i < kC; ++i) {
+    const int c = tx + i * kT;
+    if (c >= p.d) continue;
+    float mx = m[i][0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+      if (k < nch) mx = fmaxf(mx, m[i][k]);
     float num = 0.f, den = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
+    for (int k = 0; k < 4; ++k)
       if (k < nch) {
-        const float e = __expf(m[k] - mx);
-        num += e * o[k];
-        den += e * l[k];
+        const float e = __expf(m[i][k] - mx);
+        num += e * o[i][k];
+        den += e * l[i][k];
       }
     xs[c] = f2bf(num / den);
   }
   lds_sync();
 }
 
-// cross-wave sum of a tile's 16 columns + the level's epilogue (threads 0..15 store)
-VWA_DEVICE void wd_epilogue(const WdecParams& p, int li, int lvl, int tile, f32x4& acc, char* lds,
-                            const u16* xres, u16* xout) {
+// cross-wave sums of the level's (<= 2) tiles in ONE LDS round + the epilogue: thread t < 16 nt
+// finishes column t & 15 of tile t >> 4 (a second tile costs no second barrier pair); eb / ec /
+// er: that column's bias, folded-LayerNorm column sum and residual, loaded ahead
+VWA_DEVICE void wd_epilogue(const WdecParams& p, int li, int lvl, int tl0, int tl1, int nt, const f32x4& acc0,
+                            const f32x4& acc1, char* lds, u16* xout, float eb, float ec, float er) {
   float* red = reinterpret_cast<float*>(lds + L_RED);
   const float* st = reinterpret_cast<const float*>(lds + L_STAT);
   const int tx = VWA_TX, lane = tx & 63, w = tx >> 6;
-  if (lane < 16) red[w * 16 + lane] = acc[0];
-  acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (lane < 16) {
+    red[w * 32 + lane] = acc0[0];
+    red[w * 32 + 16 + lane] = acc1[0];
+  }
   lds_sync();
-  if (tx < 16) {
-    const WdecGemm& g = p.layers[li].g[gemm_of(lvl)];
-    const int n = tile * 16 + tx;
+  if (tx < 16 * nt) {
+    const int tile = tx < 16 ? tl0 : tl1, q = tx & 15;
+    const int n = tile * 16 + q;
     float v = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < 8; ++ww) v += red[ww * 16 + tx];
-    if (g.ln_c) v = (v - st[0] * g.ln_c[n]) * st[1];
-    if (g.bias) v += bf2f(g.bias[n]);
+    for (int ww = 0; ww < 8; ++ww) v += red[ww * 32 + tx];
+    if (lvl == LV_QKV || lvl == LV_XQ || lvl == LV_FC1) v = (v - st[0] * ec) * st[1];
+    v += eb;
     if (lvl == LV_FC1) v = gelu_erf(v);
     if (lvl == LV_O || lvl == LV_XO || lvl == LV_FC2) {
-      v += bf2f(ldh_sc1(xres + n));
-      sth_sc1(xout + n, f2bf(v));
+      sth_sc1(xout + n, f2bf(v + er));
     } else if (lvl == LV_FC1) {
       sth_sc1(p.f + n, f2bf(v));
     } else if (lvl == LV_XQ) {
       sth_sc1(p.q + n, f2bf(v));
     } else {  // QKV: rows permuted per head (ops.permute_qkv_rows: rotary pairs c, c ^ 8)
-      const int n0 = tile * 16, head = n0 >> 6, t4 = (n0 & 63) >> 4, q = tx;
+      const int n0 = tile * 16, head = n0 >> 6, t4 = (n0 & 63) >> 4;
       const int dd = q < 8 ? 8 * t4 + q : 32 + 8 * t4 + q - 8;
       const u16 out = f2bf(v);
       if (head < p.H) {
@@ -452,8 +532,11 @@ VWA_DEVICE void wd_epilogue(const WdecParams& p, int li, int lvl, int tile, f32x
       }
     }
   }
-  lds_sync();  // (red is reused by the next tile)
 }
+
+// schedule options (WdecParams::opt[0] bits; 0 = the defaults below)
+constexpr int kOptNoEpiPre = 1;    // load the epilogue operands after the row (not ahead of it)
+constexpr int kOptNoSattnPre = 2;  // self-attention resolves its key addresses after its inputs landed
 
 __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -467,8 +550,9 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
     rl[s] = rr[R_RELOAD + s];
   }
   const int sattn = rr[R_SATT], xattn = rr[R_XATT], xpre = rr[R_XPRE], work = rr[R_WORK];
-  if (work == 0) return;
   const int NL = p.n_layers;
+  const int opt = p.opt[0];
+  if (work == 0) return;
   // launch bases of the level counters (see the header comment)
   unsigned long long* bases = reinterpret_cast<unsigned long long*>(lds + L_RED);  // (before any tile)
   if (VWA_TX < 64) {
@@ -488,7 +572,7 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
   }
   lds_sync();
   uint4 wr[kSlots][kLps];
-  // initial slot loads: slots refilled after their use (reload level >= level) hold layer 0 now
+  // initial slot loads: slots refilled after their use (refill level >= level) hold layer 0 now
 #pragma unroll
   for (int s = 0; s < kSlots; ++s) {
 #pragma unroll
@@ -498,38 +582,77 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
   if (xattn >= 0 && xpre >= LV_XATT) wd_kv_prefetch(p, 0, xattn, lds);
 
   for (int li = 0; li < NL; ++li) {
-    uint16_t* xc = (li & 1) ? p.x1 : p.x0;  // this layer's input row
-    uint16_t* xo = (li & 1) ? p.x0 : p.x1;
+    u16* xc = (li & 1) ? p.x1 : p.x0;  // this layer's input row
+    u16* xo = (li & 1) ? p.x0 : p.x1;
     for (int lvl = 0; lvl < kWdLevels; ++lvl) {
       if (!((work >> lvl) & 1)) continue;
-      // inputs: the previous level of this layer (or the last level of the previous layer)
+      wd_stamp(p, li, lvl, 0);
+      const bool gemm = lvl != LV_SATT && lvl != LV_XATT;
+      // ahead of the inputs: the epilogue's bias / LayerNorm column sums (<= 2 tiles per level),
+      // the self-attention's key addresses
+      float eb = 0.f, ec = 0.f, er = 0.f;  // (thread t < 16 nt: column t & 15 of tile t >> 4)
+      int tl[2] = {0, 0};
+      int nt = 0;
+      auto epi_ops = [&]() {
+        if (VWA_TX < 16 * nt) {
+          const WdecGemm& g = p.layers[li].g[gemm_of(lvl)];
+          const int n = (VWA_TX < 16 ? tl[0] : tl[1]) * 16 + (VWA_TX & 15);
+          if (g.bias) eb = bf2f(gld(g.bias + n));
+          if (g.ln_c) ec = gld(g.ln_c + n);
+        }
+      };
+      if (gemm) {
+#pragma unroll
+        for (int s = 0; s < kSlots; ++s) {
+          const bool last = kind[s] == lvl && (s == kSlots - 1 || kind[s + 1] != lvl || tile[s + 1] != tile[s]);
+          if (last) {  // (selects, not a dynamic index: a private array would live in scratch)
+            tl[1] = nt == 1 ? tile[s] : tl[1];
+            tl[0] = nt == 0 ? tile[s] : tl[0];
+            nt = nt < 2 ? nt + 1 : nt;
+          }
+        }
+        if (!(opt & kOptNoEpiPre)) epi_ops();
+      } else if (lvl == LV_SATT && !(opt & kOptNoSattnPre)) {
+        wd_self_attn_pre(p, sattn, lds);
+      }
+      // release: the previous level of this layer (or the last level of the previous layer)
       if (li > 0 || lvl > 0) {
         const int pl = lvl > 0 ? lvl - 1 : kWdLevels - 1, pli = lvl > 0 ? li : li - 1;
         wd_wait(p, pl, base[pl] + (unsigned long long)p.n_prod[pl] * (unsigned long long)(pli + 1));
       }
+      wd_stamp(p, li, lvl, 1);
       if (lvl == LV_SATT) {
+        if (opt & kOptNoSattnPre) wd_self_attn_pre(p, sattn, lds);
         wd_self_attn(p, li, sattn, lds);
       } else if (lvl == LV_XATT) {
-        wd_cross_attn(p, xattn, lds);
+        wd_cross_attn(p, li, xattn, lds);
       } else {
         // activation row + residual of this level
-        const u16* xin = lvl == LV_QKV ? xc : lvl == LV_O ? p.att : lvl == LV_XQ ? xo : lvl == LV_FC1 ? xc
-                       : lvl == LV_FC2 ? p.f : nullptr;
+        const u16* xin = lvl == LV_QKV ? xc : lvl == LV_O ? p.att : lvl == LV_XQ ? xo : lvl == LV_FC1 ? xc : p.f;
         const u16* xres = lvl == LV_O ? xc : lvl == LV_XO ? xo : xc;
         u16* xout = lvl == LV_O ? xo : lvl == LV_XO ? xc : xo;
+        const bool resid = lvl == LV_O || lvl == LV_XO || lvl == LV_FC2;
+        if (resid && VWA_TX < 16 * nt)  // (in the same round trip as the row)
+          er = bf2f(ldh_sc1(xres + (VWA_TX < 16 ? tl[0] : tl[1]) * 16 + (VWA_TX & 15)));
         if (lvl == LV_XO) wd_stage_merge(p, lds);
-        else wd_stage(p, lvl, xin, lds, lvl == LV_QKV || lvl == LV_XQ || lvl == LV_FC1);
-        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+        else wd_stage(p, k_of(p, lvl), xin, lds, lvl == LV_QKV || lvl == LV_XQ || lvl == LV_FC1);
+        wd_stamp(p, li, lvl, 2);
+        if (opt & kOptNoEpiPre) epi_ops();
+        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+        int j = 0;  // tiles finished before this slot
 #pragma unroll
         for (int s = 0; s < kSlots; ++s) {
           if (kind[s] != lvl) continue;
-          wd_mma(lds, part[s], wr[s], acc);
+          if (j == 0) wd_mma(lds, part[s], wr[s], acc0);
+          else wd_mma(lds, part[s], wr[s], acc1);
           const bool last = s == kSlots - 1 || kind[s + 1] != lvl || tile[s + 1] != tile[s];
-          if (last) wd_epilogue(p, li, lvl, tile[s], acc, lds, xres, xout);
+          if (last) ++j;
         }
+        wd_epilogue(p, li, lvl, tl[0], tl[1], nt, acc0, acc1, lds, xout, eb, ec, er);
       }
       wd_arrive(p, lvl);
-      // refills a layer ahead (after the arrival: its vmcnt(0) must not wait for them)
+      wd_stamp(p, li, lvl, 3);
+      // refills a layer ahead
 #pragma unroll
       for (int s = 0; s < kSlots; ++s) {
         if (kind[s] >= 0 && rl[s] == lvl) {
@@ -539,10 +662,7 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
       }
       if (xattn >= 0 && xpre == lvl) {
         const int lt = xpre < LV_XATT ? li : li + 1;
-        if (lt < NL) {
-          if (lvl == LV_XATT) lds_sync();  // (every wave done reading the chunk)
-          wd_kv_prefetch(p, lt, xattn, lds);
-        }
+        if (lt < NL) wd_kv_prefetch(p, lt, xattn, lds);
       }
     }
   }
@@ -553,7 +673,7 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
 
 extern "C" int vwa_wdec_launch(const WdecParams* p, int grid, hipStream_t st) {
   if (p->d != 1280 || p->ffn != 4 * p->d || p->H * 64 != p->d || p->n_layers < 2 || p->ch_len > kMaxChunk ||
-      p->ch_len * p->nch < p->T || p->nch > 8 || grid < 1)
+      p->ch_len * p->nch < p->T || p->nch > 4 || p->d > 3 * kT || grid < 1)
     return -10;
   hipLaunchKernelGGL(wdec_kernel, dim3(grid), dim3(kT), kLds, st, *p);
   return (int)hipGetLastError();

@@ -72,18 +72,6 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
             s, w = free[fi]
             fi += 1
             kind[w, s], tile[w, s] = lvl, t
-    for w in range(nwg):
-        sat = R[w, 20] >= 0
-        for s in range(5):
-            k = kind[w, s]
-            if k < 0:
-                continue
-            if k == L2:  # refilled at the workgroup's first level of the next layer
-                rel[w, s] = LS if sat else (LQ if kind[w, 0] == LQ else L2)
-            elif k == LQ and sat:
-                rel[w, s] = LS
-            else:
-                rel[w, s] = k
     work = np.zeros(nwg, dtype=np.int64)
     for w in range(nwg):
         m = 0
@@ -95,6 +83,25 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
         if R[w, 21] >= 0:
             m |= 1 << LX
         work[w] = m
+    # refill points: a slot may be refilled after ANY level its workgroup runs (after its use: the
+    # next layer's tile; before it: this layer's).  The refill's bytes share the CU's in-order
+    # memory queue with the next level's activation loads, so each slot goes to the level with the
+    # longest run of idle levels behind it (measured: a 40 KB refill right before the next level's
+    # X staging held that staging ~1.6 us), spreading slots over equally good points
+    for w in range(nwg):
+        W = [lv for lv in range(8) if (work[w] >> lv) & 1]
+        gap = {lv: ((W[(i + 1) % len(W)] - lv - 1) % 8) + (8 if len(W) == 1 else 0) for i, lv in enumerate(W)}
+        load = {lv: 0 for lv in W}
+        if R[w, 21] >= 0:
+            load[LX] += 96  # the cross K / V chunk (KB) issued after the cross-attention
+        for s in range(5):
+            k = kind[w, s]
+            if k < 0:
+                continue
+            kb = 40
+            best = max(W, key=lambda lv: (gap[lv] - load[lv] / 80.0, lv == k))
+            rel[w, s] = best
+            load[best] += kb
     R[:, 23] = work
     n_prod = [int(((work >> lvl) & 1).sum()) for lvl in range(8)]
     return R, n_prod
@@ -488,7 +495,8 @@ class WhisperModel:
         ops.ext().wdec_run(st["layers"], st["roles"],
                            [bufs.hidden, bufs.h, bufs.q, bufs.att, bufs.f, st["xpart"], bufs.seq_ids, bufs.ctx_lens,
                             bufs.slots, bufs.block_table, bufs.cross_table, st["cnt"]],
-                           st["ints"], self.cfg.ln_eps, self.hd ** -0.5, st["n_prod"])
+                           st["ints"], self.cfg.ln_eps, self.hd ** -0.5, st["n_prod"], st.get("ts"),
+                           int(st.get("opt", 0)))
         return (bufs.hidden if len(self.dec) % 2 == 0 else bufs.h)[:1]
 
     def decode_step(self, bufs, M: int) -> torch.Tensor:
