@@ -201,6 +201,12 @@ def test_plan_gpus_maps_through_the_parent_mask():
     g = shared_gpu_env({}, "/dev/shm/vwa_asr_busy_test")
     assert g["VWA_CHAIN"] == "1" and g["VWA_ASR_BUSY_FILE"] == "/dev/shm/vwa_asr_busy_test"
     assert "VWA_ASR_BUSY_FILE" not in shared_gpu_env({"VWA_SHARED_CHAIN": "0"}, "/dev/shm/x")
+    # the ASR's persistent decoder only beside a brain that never runs its persistent launch
+    from voice_enabled_browser_automation_amd.launch import shared_voice_env
+
+    assert shared_voice_env({}, g)["VWA_ASR_PERSIST"] == "0"
+    assert shared_voice_env({}, shared_gpu_env({"VWA_SHARED_CHAIN": "0"}))["VWA_ASR_PERSIST"] == "1"
+    assert shared_voice_env({"VWA_ASR_PERSIST": "1"}, g)["VWA_ASR_PERSIST"] == "1"
 
 
 def test_asr_busy_flag_gates_the_chained_launch(tmp_path):

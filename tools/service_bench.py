@@ -251,6 +251,10 @@ async def run_matrix(a) -> list:
                             "VWA_COMMIT_MS": str(commit), "VWA_SPEC_BRAIN": a.spec_brain}
                     if busy:
                         venv["VWA_ASR_BUSY_FILE"] = busy
+                    if a.brain_gpu == a.voice_gpu:  # (launch.py's shared-GPU rule for the ASR)
+                        from voice_enabled_browser_automation_amd.launch import shared_voice_env
+
+                        venv.update(shared_voice_env(os.environ, benv))
                     voice = spawn(f"{PKG}.voice.server", venv,
                                   os.path.join(logs, f"voice_chain{chain}_deb{deb}_commit{commit}.log"))
                     try:

@@ -69,6 +69,7 @@ def main():
         rows.append(ts.view(grid, L, 8, 4).cpu())
     err = m.chain_error()
     res = {lv: dict(handoff=[], stage=[], body=[], span=[]) for lv in WDEC_LEVELS}
+    late = {lv: {} for lv in WDEC_LEVELS}  # workgroup -> completion minus the level's median, per layer
     for t in rows:
         t = t.double() / 100.0  # 100 MHz -> us
         done_prev = None
@@ -78,8 +79,13 @@ def main():
                 act = s[:, 3] > 0
                 if not act.any():
                     continue
+                ids = act.nonzero().flatten().tolist()
                 s = s[act]
                 rel, stg, dn = s[:, 1], s[:, 2], s[:, 3]
+                if li > 0:
+                    med = float(dn.median())
+                    for wg, v in zip(ids, dn.tolist()):
+                        late[name].setdefault(wg, []).append(v - med)
                 if done_prev is not None and li > 0:
                     res[name]["handoff"].append(float(rel.min() - done_prev))
                     res[name]["span"].append(float(dn.max() - done_prev))
@@ -94,6 +100,9 @@ def main():
     for name, d in res.items():
         out[name] = {k: round(statistics.median(v), 2) for k, v in d.items() if v}
     out["layer_span_us"] = round(sum(out[n].get("span", 0) for n in WDEC_LEVELS), 2)
+    for name in WDEC_LEVELS:  # the workgroups that finish a level latest (median lateness, us)
+        lw = sorted(((statistics.median(v), wg) for wg, v in late[name].items()), reverse=True)[:4]
+        out[name]["late"] = [[wg, round(v, 2)] for v, wg in lw]
     print(json.dumps(out), flush=True)
     if a.json:
         with open(a.json, "a") as f:

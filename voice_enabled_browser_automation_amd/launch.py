@@ -167,6 +167,16 @@ def shared_gpu_env(env, busy_file: str = "") -> dict:
     return out
 
 
+def shared_voice_env(env, brain_env: dict) -> dict:
+    """Voice-worker settings on a GPU shared with the brain.  The persistent Whisper-large decoder
+    (VWA_ASR_PERSIST, whisper_dec.hip) and the brain's chained launch are both one-workgroup-per-CU
+    persistent kernels from different processes: if their workgroup dispatch interleaved, each
+    would wait for workgroups the other holds until its bounded spins gave up.  So the ASR keeps
+    per-kernel launches whenever the brain may chain (an explicit VWA_ASR_PERSIST wins)."""
+    brain_chains = brain_env.get("VWA_CHAIN", "1") != "0"
+    return {"VWA_ASR_PERSIST": env.get("VWA_ASR_PERSIST", "0" if brain_chains else "1")}
+
+
 def _visible_gpus() -> int:
     try:
         import torch  # device_count() reads the device list without initialising the HIP runtime
@@ -188,6 +198,7 @@ def main():
         benv.update(shared_gpu_env(os.environ, busy))
         if benv.get("VWA_ASR_BUSY_FILE"):
             venv["VWA_ASR_BUSY_FILE"] = busy
+        venv.update(shared_voice_env(os.environ, benv))
     sup = Supervisor(max_restarts=knob("VWA_BRAIN_MAX_RESTARTS"))
     sup.add("brain", f"{PKG}.brain.server", benv, tp, restartable=True)
     if len(voice_gpus) > 1:

@@ -475,7 +475,7 @@ class WhisperModel:
                      wt(w1), b1, c1, wt(L.fc2), L.fc2_b, None,
                      bufs.k_cache[li], bufs.v_cache[li], bufs.cross[li][0], bufs.cross[li][1]]
         layers = E.wdec_layers(flat, len(self.dec), bufs.hidden)
-        cnt = E.alloc_uncached_i32(4096, bufs.hidden)
+        cnt = E.alloc_uncached_i32(4096, bufs.hidden)  # level counters [8][8] x 128 B + error word
         xpart = torch.zeros(self.H * nch * 66, dtype=torch.float32, device=self.device)
         T = bufs.cross[0][0].shape[1]
         st = dict(layers=layers, roles=torch.from_numpy(roles).to(self.device), n_prod=n_prod, cnt=cnt, xpart=xpart,
