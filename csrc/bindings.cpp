@@ -858,12 +858,12 @@ void chain_run(Tensor desc, int64_t n_phases, int64_t lds, Tensor like, int64_t 
            "chain");
 }
 
-// Persistent Whisper decoder (whisper_dec.hip): per-layer descriptors from a flat list of 22
-// tensors per layer -- (W, bias, ln_c) of qkv, out-proj, cross query, cross out-proj, fc1, fc2
-// (pre-tiled bf16 weights; bias / ln_c may be None), then k_cache, v_cache, cross K, cross V.
+// Persistent Whisper decoder (whisper_dec.hip): per-layer descriptors from a flat list of
+// 3 kWdGemms + 4 tensors per layer -- (W, bias, ln_c) of each WdecLayer::g (pre-tiled bf16 weights;
+// bias / ln_c may be None), then k_cache, v_cache, cross K, cross V.
 Tensor wdec_layers(std::vector<c10::optional<Tensor>> flat, int64_t n_layers, Tensor like) {
   constexpr int kPer = 3 * kWdGemms + 4;
-  TORCH_CHECK(n_layers >= 1 && (int64_t)flat.size() == n_layers * kPer, "wdec_layers: 22 entries per layer");
+  TORCH_CHECK(n_layers >= 1 && (int64_t)flat.size() == n_layers * kPer, "wdec_layers: 3 kWdGemms + 4 entries per layer");
   auto ptr = [&](int64_t i, bool need) -> void* {
     const auto& t = flat[(size_t)i];
     if (!t.has_value()) {
@@ -887,10 +887,11 @@ Tensor wdec_layers(std::vector<c10::optional<Tensor>> flat, int64_t n_layers, Te
       TORCH_CHECK(!c.has_value() || c->scalar_type() == at::kFloat, "wdec_layers: ln_c f32");
       L[li].g[g].ln_c = static_cast<const float*>(ptr(b + 3 * g + 2, false));
     }
-    L[li].k_cache = static_cast<uint16_t*>(ptr(b + 18, true));
-    L[li].v_cache = static_cast<uint16_t*>(ptr(b + 19, true));
-    L[li].xk = static_cast<const uint16_t*>(ptr(b + 20, true));
-    L[li].xv = static_cast<const uint16_t*>(ptr(b + 21, true));
+    constexpr int c0 = 3 * kWdGemms;
+    L[li].k_cache = static_cast<uint16_t*>(ptr(b + c0, true));
+    L[li].v_cache = static_cast<uint16_t*>(ptr(b + c0 + 1, true));
+    L[li].xk = static_cast<const uint16_t*>(ptr(b + c0 + 2, true));
+    L[li].xv = static_cast<const uint16_t*>(ptr(b + c0 + 3, true));
   }
   return host.to(like.device());
 }
@@ -928,7 +929,8 @@ void wdec_run(Tensor layers, Tensor roles, std::vector<Tensor> bufs, std::vector
   p.q = bf(2);
   p.att = bf(3);
   p.f = bf(4);
-  TORCH_CHECK(bufs[5].scalar_type() == at::kFloat && bufs[5].numel() >= (int64_t)p.H * p.nch * 66, "wdec_run: xpart");
+  TORCH_CHECK(bufs[5].scalar_type() == at::kFloat && bufs[5].numel() >= (int64_t)p.H * p.nch * 66 + 2 * p.d,
+              "wdec_run: xpart (cross partials + the cross query's two f32 halves)");
   p.xpart = bufs[5].data_ptr<float>();
   p.seq_ids = bufs[6].data_ptr<int>();
   p.ctx_lens = bufs[7].data_ptr<int>();

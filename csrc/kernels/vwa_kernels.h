@@ -199,17 +199,21 @@ struct FlashAttnParams {
 };
 
 // Persistent Whisper decoder step (whisper_dec.hip wdec_kernel): ONE launch runs every decoder
-// layer of a one-row decode step -- eight dependent levels per layer (self-attention QKV, self-
-// attention, out-proj, cross query, cross-attention, cross out-proj, fc1, fc2) -- with each
-// workgroup's share of a layer's weights held in registers from the previous layer on.
-enum { kWdLevels = 8, kWdGemms = 6, kWdRole = 32 };
+// layer of a one-row decode step -- seven dependent levels per layer (self-attention QKV, self-
+// attention, out-proj + cross-query pre-activation, cross-attention, cross out-proj, fc1, fc2) plus
+// one off the critical path (the layer input's share of the cross query), with each workgroup's
+// share of a layer's weights held in registers from the previous layer on.
+enum { kWdLevels = 8, kWdGemms = 7, kWdRole = 32 };
 struct WdecGemm {
   const uint16_t* W;      // pre-tiled bf16 [N / 16][K / 128][4 KB] (ops.tile_weight)
   const uint16_t* bias;   // [N] or null
   const float* ln_c;      // folded LayerNorm column sums [N] (ops.fold_layernorm) or null
 };
 struct WdecLayer {
-  WdecGemm g[kWdGemms];                    // qkv, out-proj, cross query, cross out-proj, fc1, fc2
+  // qkv, out-proj, cross query (LayerNorm gamma folded; bias = its product with the out-proj bias,
+  // ln_c = its column sums), cross out-proj, fc1, fc2, cross query x out-proj (bias = the folded
+  // cross-query bias, applied after the LayerNorm)
+  WdecGemm g[kWdGemms];
   uint16_t* k_cache; uint16_t* v_cache;    // self-attention cache [blocks][H][block_size][64]
   const uint16_t* xk; const uint16_t* xv;  // cross-attention K / V [sessions][T][H][64]
 };

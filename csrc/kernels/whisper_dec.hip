@@ -11,16 +11,22 @@
 // Levels of layer li (reference call site this replaces: /root/reference/apps/voice/src/
 // deepgram.ts:36-45, the hosted recogniser):
 //   0 QKV      LN1(x) . Wqkv^T + b -> q, self K / V cache row   (240 column tiles of 16)
-//   1 SATT     self-attention of the row, one workgroup per head -> att
-//   2 O        x1 = x + att . Wo^T + b                            (80 tiles)
-//   3 XQ       LNx(x1) . Wxq^T + b -> q                           (80 tiles)
-//   4 XATT     cross-attention partials, (head, key chunk) per workgroup, K / V chunk prefetched
-//              into LDS by LDS-DMA a layer ahead
+//   1 XQX      x . Wxq^T -> xqa (f32)                             (80 tiles; off the critical path)
+//   2 SATT     self-attention of the row, one workgroup per head -> att
+//   3 OXQ      x1 = x + att . Wo^T + bo                           (80 tiles)
+//              att . (Wxq Wo)^T + Wxq bo -> xqb (f32)             (80 tiles, same staged row)
+//   4 XATT     q = LNx(x1) . Wxq^T + b from xqa + xqb and x1's mean / rstd, then the cross-
+//              attention partials, (head, key chunk) per workgroup, K / V chunk prefetched into
+//              LDS by LDS-DMA a layer ahead
 //   5 XO       x2 = x1 + merge(partials) . Wxo^T + b              (80 tiles; the merge is the X staging)
 //   6 FC1      f = GELU(LN2(x2) . W1^T + b1)                      (320 tiles)
 //   7 FC2      x3 = x2 + f . W2^T + b2                            (80 tiles, K = 5120)
 // LayerNorms are folded into the weights (ops.fold_layernorm: y = rstd (x.Wg - mean c) + b'), the
-// mean / rstd come from the staged row.
+// mean / rstd come from the staged row.  The cross query needs x1 = x + att Wo^T + bo, so by
+// linearity x1 Wg^T = x Wg^T + att (Wg Wo)^T + Wg bo: its x part runs while the self-attention
+// does (level 1, the row QKV staged) and its att part beside the out-projection -- one dependent
+// level per layer fewer than out-proj -> cross query -> cross-attention (the x1 rounding to bf16
+// is the only difference; the extra 3.3 MB per layer fits the register slots).
 //
 // Hand-off: a producer workgroup drains its stores and adds 1 (no return) to its level's counter of
 // its XCD group; consumers poll the sum of the eight group counters with scalar loads (uncached
@@ -43,7 +49,9 @@ using namespace vwa;
 
 constexpr int kT = 512;           // threads (8 waves, K split over the waves)
 constexpr int kSlots = 5, kLps = 5;
-enum { LV_QKV = 0, LV_SATT, LV_O, LV_XQ, LV_XATT, LV_XO, LV_FC1, LV_FC2 };
+enum { LV_QKV = 0, LV_XQX, LV_SATT, LV_OXQ, LV_XATT, LV_XO, LV_FC1, LV_FC2 };
+// gemm ids (WdecLayer::g; a slot's kind): the level of each
+enum { G_QKV = 0, G_O, G_XQ, G_XO, G_FC1, G_FC2, G_XQO };
 // role row layout (kWdRole ints per workgroup)
 enum { R_KIND = 0, R_TILE = 5, R_PART = 10, R_RELOAD = 15, R_SATT = 20, R_XATT = 21, R_XPRE = 22, R_WORK = 23 };
 // LDS layout (bytes)
@@ -62,8 +70,9 @@ constexpr int kMaxChunk = 384;
 constexpr int kSpinLimit = 1 << 17;  // bounded polls: a non-resident producer ends the launch, not the GPU
 constexpr int kErrWord = 1024;       // (WdecParams::cnt u64 index of the error flag)
 
-VWA_DEVICE int gemm_of(int lvl) {
-  return lvl == LV_QKV ? 0 : lvl == LV_O ? 1 : lvl == LV_XQ ? 2 : lvl == LV_XO ? 3 : lvl == LV_FC1 ? 4 : 5;
+VWA_DEVICE int level_of(int gm) {
+  return gm == G_QKV ? LV_QKV : gm == G_XQ ? LV_XQX : gm == G_O || gm == G_XQO ? LV_OXQ : gm == G_XO ? LV_XO
+       : gm == G_FC1 ? LV_FC1 : LV_FC2;
 }
 
 VWA_DEVICE __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long long bytes) {
@@ -143,16 +152,19 @@ VWA_DEVICE void wd_stamp(const WdecParams& p, int li, int lvl, int k) {
         __builtin_amdgcn_s_memrealtime();
 }
 
-VWA_DEVICE int n_cols(const WdecParams& p, int lvl) {
-  return lvl == LV_QKV ? 3 * p.d : lvl == LV_FC1 ? p.ffn : p.d;
+VWA_DEVICE int n_cols(const WdecParams& p, int gm) {
+  return gm == G_QKV ? 3 * p.d : gm == G_FC1 ? p.ffn : p.d;
 }
-VWA_DEVICE int k_of(const WdecParams& p, int lvl) { return lvl == LV_FC2 ? p.ffn : p.d; }
+VWA_DEVICE int k_of(const WdecParams& p, int gm) { return gm == G_FC2 ? p.ffn : p.d; }
 
-// slot load: part `part` (5 load-slices per wave) of tile `tile` of level lvl's weight, layer li
-VWA_DEVICE void wd_load(const WdecParams& p, int li, int lvl, int tile, int part, uint4 (&wr)[kLps]) {
-  const WdecGemm& g = p.layers[li].g[gemm_of(lvl)];
-  const int K = k_of(p, lvl), G = K >> 7;
-  const __amdgpu_buffer_rsrc_t r = rsrc_of(g.W, (long long)n_cols(p, lvl) * K * 2);
+// the cross query's f32 pre-activation halves (x part, att part) behind the cross partials
+VWA_DEVICE float* xq_buf(const WdecParams& p) { return p.xpart + (size_t)p.H * p.nch * 66; }
+
+// slot load: part `part` (5 load-slices per wave) of tile `tile` of gemm gm's weight, layer li
+VWA_DEVICE void wd_load(const WdecParams& p, int li, int gm, int tile, int part, uint4 (&wr)[kLps]) {
+  const WdecGemm& g = p.layers[li].g[gm];
+  const int K = k_of(p, gm), G = K >> 7;
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(g.W, (long long)n_cols(p, gm) * K * 2);
   const int tx = VWA_TX, lane = tx & 63, w = tx >> 6;
 #pragma unroll
   for (int j = 0; j < kLps; ++j) {
@@ -223,16 +235,45 @@ VWA_DEVICE float blk_sum(char* lds, float v) {
   return s;
 }
 
-// q head h (bf16, written this launch) -> LDS f32 [64]
-VWA_DEVICE void wd_q_to_lds(const WdecParams& p, int h, char* lds) {
+// cross query head h -> LDS f32 [64]: q = rstd1 (xqa + xqb - mean1 c) + b' (rounded to bf16 like
+// the per-kernel path's q), mean1 / rstd1 of the row x1 (written this layer); qc / qb: c and b' of
+// column h 64 + tx, loaded ahead of the release.  The loads go out after the K / V chunk DMAs, so
+// the vmcnt wait also covers those (the barrier then publishes every wave's chunk).
+VWA_DEVICE void wd_xq_to_lds(const WdecParams& p, const u16* x1, int h, char* lds, float qc, float qb) {
   float* qf = reinterpret_cast<float*>(lds + L_QF);
-  const int tx = VWA_TX;
-  if (tx < 8) {
-    const uint4 v = ld_sc1_b128(rsrc_of(p.q, (long long)p.d * 2), (unsigned)((h * 64 + tx * 8) * 2));
-    float f[8];
-    unpack8(v, f);
+  float* w8 = reinterpret_cast<float*>(lds + L_W8);
+  const int tx = VWA_TX, n8 = p.d >> 3;
+  const float* xq = xq_buf(p);
+  float a = 0.f, b = 0.f;
+  if (tx < 64) {
+    a = ldf_sc1(xq + h * 64 + tx);
+    b = ldf_sc1(xq + p.d + h * 64 + tx);
+  }
+  const uint4 v = tx < n8 ? ld_sc1_b128(rsrc_of(x1, (long long)p.d * 2), (unsigned)tx * 16u) : make_uint4(0, 0, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float f[8], s = 0.f, s2 = 0.f;
+  unpack8(v, f);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) qf[tx * 8 + e] = f[e];
+  for (int e = 0; e < 8; ++e) {
+    s += f[e];
+    s2 += f[e] * f[e];
+  }
+  s = wave_sum(s);
+  s2 = wave_sum(s2);
+  if ((tx & 63) == 0) {
+    w8[tx >> 6] = s;
+    w8[8 + (tx >> 6)] = s2;
+  }
+  lds_sync();
+  if (tx < 64) {
+    float ts = 0.f, ts2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      ts += w8[i];
+      ts2 += w8[8 + i];
+    }
+    const float mean = ts / (float)p.d, rstd = rsqrtf(fmaxf(ts2 / (float)p.d - mean * mean, 0.f) + p.eps);
+    qf[tx] = bf2f(f2bf((a + b - mean * qc) * rstd + qb));
   }
   lds_sync();
 }
@@ -343,12 +384,11 @@ VWA_DEVICE void wd_self_attn(const WdecParams& p, int li, int h, char* lds) {
 }
 
 // level 4: cross-attention partial of (head, chunk) from the prefetched K / V chunk in LDS
-VWA_DEVICE void wd_cross_attn(const WdecParams& p, int li, int item, char* lds) {
+VWA_DEVICE void wd_cross_attn(const WdecParams& p, int li, int item, const u16* x1, char* lds, float qc, float qb) {
   const int h = item / p.nch, ch = item % p.nch;
   const int k0 = ch * p.ch_len, nk = min(p.ch_len, p.T - k0);
   const int tx = VWA_TX, lane = tx & 63, w = tx >> 6;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's K / V DMAs have landed
-  wd_q_to_lds(p, h, lds);                            // (its barrier: every wave's DMAs)
+  wd_xq_to_lds(p, x1, h, lds, qc, qb);
   const float* qf = reinterpret_cast<const float*>(lds + L_QF);
   const u16* kl = reinterpret_cast<const u16*>(lds + L_KV);
   const u16* vl = reinterpret_cast<const u16*>(lds + L_KV + L_KVV);
@@ -486,9 +526,9 @@ VWA_DEVICE void wd_stage_merge(const WdecParams& p, char* lds) {
 }
 
 // cross-wave sums of the level's (<= 2) tiles in ONE LDS round + the epilogue: thread t < 16 nt
-// finishes column t & 15 of tile t >> 4 (a second tile costs no second barrier pair); eb / ec /
-// er: that column's bias, folded-LayerNorm column sum and residual, loaded ahead
-VWA_DEVICE void wd_epilogue(const WdecParams& p, int li, int lvl, int tl0, int tl1, int nt, const f32x4& acc0,
+// finishes column t & 15 of tile t >> 4 (gemm gm, a second tile costs no second barrier pair);
+// eb / ec / er: that column's bias, folded-LayerNorm column sum and residual, loaded ahead
+VWA_DEVICE void wd_epilogue(const WdecParams& p, int li, int g0, int g1, int tl0, int tl1, int nt, const f32x4& acc0,
                             const f32x4& acc1, char* lds, u16* xout, float eb, float ec, float er) {
   float* red = reinterpret_cast<float*>(lds + L_RED);
   const float* st = reinterpret_cast<const float*>(lds + L_STAT);
@@ -499,20 +539,20 @@ VWA_DEVICE void wd_epilogue(const WdecParams& p, int li, int lvl, int tl0, int t
   }
   lds_sync();
   if (tx < 16 * nt) {
-    const int tile = tx < 16 ? tl0 : tl1, q = tx & 15;
+    const int tile = tx < 16 ? tl0 : tl1, gm = tx < 16 ? g0 : g1, q = tx & 15;
     const int n = tile * 16 + q;
     float v = 0.f;
 #pragma unroll
     for (int ww = 0; ww < 8; ++ww) v += red[ww * 32 + tx];
-    if (lvl == LV_QKV || lvl == LV_XQ || lvl == LV_FC1) v = (v - st[0] * ec) * st[1];
+    if (gm == G_QKV || gm == G_FC1) v = (v - st[0] * ec) * st[1];
     v += eb;
-    if (lvl == LV_FC1) v = gelu_erf(v);
-    if (lvl == LV_O || lvl == LV_XO || lvl == LV_FC2) {
+    if (gm == G_FC1) v = gelu_erf(v);
+    if (gm == G_O || gm == G_XO || gm == G_FC2) {
       sth_sc1(xout + n, f2bf(v + er));
-    } else if (lvl == LV_FC1) {
+    } else if (gm == G_FC1) {
       sth_sc1(p.f + n, f2bf(v));
-    } else if (lvl == LV_XQ) {
-      sth_sc1(p.q + n, f2bf(v));
+    } else if (gm == G_XQ || gm == G_XQO) {
+      stf_sc1(xq_buf(p) + (gm == G_XQ ? 0 : p.d) + n, v);
     } else {  // QKV: rows permuted per head (ops.permute_qkv_rows: rotary pairs c, c ^ 8)
       const int n0 = tile * 16, head = n0 >> 6, t4 = (n0 & 63) >> 4;
       const int dd = q < 8 ? 8 * t4 + q : 32 + 8 * t4 + q - 8;
@@ -541,10 +581,11 @@ constexpr int kOptNoSattnPre = 2;  // self-attention resolves its key addresses 
 __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int* rr = p.roles + (size_t)blockIdx.x * kWdRole;
-  int kind[kSlots], tile[kSlots], part[kSlots], rl[kSlots];
+  int kind[kSlots], klv[kSlots], tile[kSlots], part[kSlots], rl[kSlots];
 #pragma unroll
   for (int s = 0; s < kSlots; ++s) {
-    kind[s] = rr[R_KIND + s];
+    kind[s] = rr[R_KIND + s];  // gemm id or -1
+    klv[s] = kind[s] >= 0 ? level_of(kind[s]) : -1;
     tile[s] = rr[R_TILE + s];
     part[s] = rr[R_PART + s];
     rl[s] = rr[R_RELOAD + s];
@@ -571,13 +612,15 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
               ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) << 32);
   }
   lds_sync();
+  // the level's counter target after layer pli
+  auto target = [&](int l, int pli) { return base[l] + (unsigned long long)p.n_prod[l] * (unsigned long long)(pli + 1); };
   uint4 wr[kSlots][kLps];
   // initial slot loads: slots refilled after their use (refill level >= level) hold layer 0 now
 #pragma unroll
   for (int s = 0; s < kSlots; ++s) {
 #pragma unroll
     for (int j = 0; j < kLps; ++j) wr[s][j] = make_uint4(0, 0, 0, 0);
-    if (kind[s] >= 0 && rl[s] >= kind[s]) wd_load(p, 0, kind[s], tile[s], part[s], wr[s]);
+    if (kind[s] >= 0 && rl[s] >= klv[s]) wd_load(p, 0, kind[s], tile[s], part[s], wr[s]);
   }
   if (xattn >= 0 && xpre >= LV_XATT) wd_kv_prefetch(p, 0, xattn, lds);
 
@@ -589,66 +632,79 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
       wd_stamp(p, li, lvl, 0);
       const bool gemm = lvl != LV_SATT && lvl != LV_XATT;
       // ahead of the inputs: the epilogue's bias / LayerNorm column sums (<= 2 tiles per level),
-      // the self-attention's key addresses
+      // the self-attention's key addresses, the cross query's column sums and bias
       float eb = 0.f, ec = 0.f, er = 0.f;  // (thread t < 16 nt: column t & 15 of tile t >> 4)
-      int tl[2] = {0, 0};
+      int tl[2] = {0, 0}, tg[2] = {0, 0};
       int nt = 0;
       auto epi_ops = [&]() {
         if (VWA_TX < 16 * nt) {
-          const WdecGemm& g = p.layers[li].g[gemm_of(lvl)];
+          const int gm = VWA_TX < 16 ? tg[0] : tg[1];
+          const WdecGemm& g = p.layers[li].g[gm];
           const int n = (VWA_TX < 16 ? tl[0] : tl[1]) * 16 + (VWA_TX & 15);
-          if (g.bias) eb = bf2f(gld(g.bias + n));
-          if (g.ln_c) ec = gld(g.ln_c + n);
+          if (g.bias && gm != G_XQ) eb = bf2f(gld(g.bias + n));
+          if (g.ln_c && (gm == G_QKV || gm == G_FC1)) ec = gld(g.ln_c + n);
         }
       };
       if (gemm) {
 #pragma unroll
         for (int s = 0; s < kSlots; ++s) {
-          const bool last = kind[s] == lvl && (s == kSlots - 1 || kind[s + 1] != lvl || tile[s + 1] != tile[s]);
+          const bool last = klv[s] == lvl && (s == kSlots - 1 || kind[s + 1] != kind[s] || tile[s + 1] != tile[s]);
           if (last) {  // (selects, not a dynamic index: a private array would live in scratch)
             tl[1] = nt == 1 ? tile[s] : tl[1];
+            tg[1] = nt == 1 ? kind[s] : tg[1];
             tl[0] = nt == 0 ? tile[s] : tl[0];
+            tg[0] = nt == 0 ? kind[s] : tg[0];
             nt = nt < 2 ? nt + 1 : nt;
           }
         }
         if (!(opt & kOptNoEpiPre)) epi_ops();
       } else if (lvl == LV_SATT && !(opt & kOptNoSattnPre)) {
         wd_self_attn_pre(p, sattn, lds);
+      } else if (lvl == LV_XATT && VWA_TX < 64) {
+        const WdecGemm& g = p.layers[li].g[G_XQ];
+        const int n = (xattn / p.nch) * 64 + VWA_TX;
+        ec = gld(g.ln_c + n);
+        eb = bf2f(gld(g.bias + n));
       }
-      // release: the previous level of this layer (or the last level of the previous layer)
-      if (li > 0 || lvl > 0) {
-        const int pl = lvl > 0 ? lvl - 1 : kWdLevels - 1, pli = lvl > 0 ? li : li - 1;
-        wd_wait(p, pl, base[pl] + (unsigned long long)p.n_prod[pl] * (unsigned long long)(pli + 1));
+      // release: the level's producer level (the x part of the cross query needs only the layer
+      // input: nothing when this workgroup just ran the QKV level; the cross-attention also needs it)
+      if (lvl == LV_XATT) wd_wait(p, LV_XQX, target(LV_XQX, li));
+      if (lvl == LV_QKV || (lvl == LV_XQX && !(work & 1))) {
+        if (li > 0) wd_wait(p, LV_FC2, target(LV_FC2, li - 1));
+      } else if (lvl != LV_XQX) {
+        const int pl = lvl == LV_SATT ? LV_QKV : lvl - 1;
+        wd_wait(p, pl, target(pl, li));
       }
       wd_stamp(p, li, lvl, 1);
       if (lvl == LV_SATT) {
         if (opt & kOptNoSattnPre) wd_self_attn_pre(p, sattn, lds);
         wd_self_attn(p, li, sattn, lds);
       } else if (lvl == LV_XATT) {
-        wd_cross_attn(p, li, xattn, lds);
+        wd_cross_attn(p, li, xattn, xo, lds, ec, eb);
       } else {
         // activation row + residual of this level
-        const u16* xin = lvl == LV_QKV ? xc : lvl == LV_O ? p.att : lvl == LV_XQ ? xo : lvl == LV_FC1 ? xc : p.f;
-        const u16* xres = lvl == LV_O ? xc : lvl == LV_XO ? xo : xc;
-        u16* xout = lvl == LV_O ? xo : lvl == LV_XO ? xc : xo;
-        const bool resid = lvl == LV_O || lvl == LV_XO || lvl == LV_FC2;
+        const u16* xin = lvl == LV_OXQ ? p.att : lvl == LV_FC2 ? p.f : xc;
+        const u16* xres = lvl == LV_XO ? xo : xc;
+        u16* xout = lvl == LV_XO ? xc : xo;
+        const bool resid = lvl == LV_OXQ || lvl == LV_XO || lvl == LV_FC2;
         if (resid && VWA_TX < 16 * nt)  // (in the same round trip as the row)
           er = bf2f(ldh_sc1(xres + (VWA_TX < 16 ? tl[0] : tl[1]) * 16 + (VWA_TX & 15)));
         if (lvl == LV_XO) wd_stage_merge(p, lds);
-        else wd_stage(p, k_of(p, lvl), xin, lds, lvl == LV_QKV || lvl == LV_XQ || lvl == LV_FC1);
+        else if (!(lvl == LV_XQX && (work & 1)))  // (after the QKV level the row is staged already)
+          wd_stage(p, k_of(p, lvl == LV_FC2 ? G_FC2 : G_O), xin, lds, lvl == LV_QKV || lvl == LV_FC1);
         wd_stamp(p, li, lvl, 2);
         if (opt & kOptNoEpiPre) epi_ops();
         f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
         int j = 0;  // tiles finished before this slot
 #pragma unroll
         for (int s = 0; s < kSlots; ++s) {
-          if (kind[s] != lvl) continue;
+          if (klv[s] != lvl) continue;
           if (j == 0) wd_mma(lds, part[s], wr[s], acc0);
           else wd_mma(lds, part[s], wr[s], acc1);
-          const bool last = s == kSlots - 1 || kind[s + 1] != lvl || tile[s + 1] != tile[s];
+          const bool last = s == kSlots - 1 || kind[s + 1] != kind[s] || tile[s + 1] != tile[s];
           if (last) ++j;
         }
-        wd_epilogue(p, li, lvl, tl[0], tl[1], nt, acc0, acc1, lds, xout, eb, ec, er);
+        wd_epilogue(p, li, tg[0], tg[1], tl[0], tl[1], nt, acc0, acc1, lds, xout, eb, ec, er);
       }
       wd_arrive(p, lvl);
       wd_stamp(p, li, lvl, 3);
@@ -656,7 +712,7 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
 #pragma unroll
       for (int s = 0; s < kSlots; ++s) {
         if (kind[s] >= 0 && rl[s] == lvl) {
-          const int lt = rl[s] < kind[s] ? li : li + 1;
+          const int lt = rl[s] < klv[s] ? li : li + 1;
           if (lt < NL) wd_load(p, lt, kind[s], tile[s], part[s], wr[s]);
         }
       }

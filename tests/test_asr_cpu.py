@@ -117,24 +117,31 @@ def test_conv_padded_path_matches_plain_on_cpu():
 
 def test_wdec_roles_cover_every_tile_once():
     """Role table of the persistent whisper-large decoder (whisper_dec.hip): every tile of every
-    projection on exactly one workgroup (fc2 tiles as four parts in slots 1..4), at most 5 slots,
-    every slot refilled at a level its workgroup works at, producer counts = the work masks."""
-    from voice_enabled_browser_automation_amd.models.whisper import wdec_roles
+    projection (kinds = gemm ids, WDEC_GEMMS) on exactly one workgroup (fc2 tiles as four parts in
+    slots 1..4), at most 5 slots and 2 tiles of a level per workgroup, the x part of the cross query
+    on QKV workgroups, every slot refilled at a level its workgroup works at, producer counts = the
+    work masks."""
+    from voice_enabled_browser_automation_amd.models.whisper import WDEC_GEMM_LEVEL, wdec_roles
 
     d, H, ffn, nch = 1280, 20, 5120, 4
     R, n_prod = wdec_roles(256, d, H, ffn, nch)
     kind, tile, part, rel, work = R[:, 0:5], R[:, 5:10], R[:, 10:15], R[:, 15:20], R[:, 23]
-    want = {0: 3 * d // 16, 2: d // 16, 3: d // 16, 5: d // 16, 6: ffn // 16, 7: d // 16}
-    for lvl, n in want.items():
-        seen = sorted((int(tile[w, s]), int(part[w, s])) for w in range(256) for s in range(5) if kind[w, s] == lvl)
-        parts = 4 if lvl == 7 else 1
-        assert seen == [(t, p) for t in range(n) for p in range(parts)], lvl
+    want = {0: 3 * d // 16, 1: d // 16, 2: d // 16, 3: d // 16, 4: ffn // 16, 5: d // 16, 6: d // 16}
+    for gm, n in want.items():
+        seen = sorted((int(tile[w, s]), int(part[w, s])) for w in range(256) for s in range(5) if kind[w, s] == gm)
+        parts = 4 if gm == 5 else 1
+        assert seen == [(t, p) for t in range(n) for p in range(parts)], gm
     for w in range(256):
         for s in range(5):
             if kind[w, s] >= 0:
                 assert (work[w] >> rel[w, s]) & 1, (w, s)  # the refill fires at a level this workgroup runs
-        fc2 = [s for s in range(5) if kind[w, s] == 7]
+                assert (work[w] >> WDEC_GEMM_LEVEL[kind[w, s]]) & 1
+        fc2 = [s for s in range(5) if kind[w, s] == 5]
         assert fc2 in ([], [1, 2, 3, 4])
+        lv = [WDEC_GEMM_LEVEL[k] for k in kind[w] if 0 <= k != 5]
+        assert all(lv.count(x) <= 2 for x in lv), w
+        if 2 in kind[w]:
+            assert kind[w, 0] == 0 and R[w, 20] < 0  # its row is staged by the QKV level
     assert sorted(R[:, 20][R[:, 20] >= 0].tolist()) == list(range(H))
     assert sorted(R[:, 21][R[:, 21] >= 0].tolist()) == list(range(H * nch))
     assert n_prod == [int(((work >> lvl) & 1).sum()) for lvl in range(8)] and min(n_prod) > 0

@@ -7,7 +7,8 @@ workgroups that run it --
   body       staged (or release) -> completion (stamp 3): MFMAs, reduce, epilogue, store drain
   span       previous level's last completion -> this level's last completion
 
-reported as the median over layers 1..L-1 (layer 0 carries the launch ramp), plus the whole
+(the x part of the cross query, level xq_x, runs beside the chain: body only) reported as the
+median over layers 1..L-1 (layer 0 carries the launch ramp), plus the whole
 launch time from the host and the decode us/token of the same model.
 
     python tools/wdec_probe.py [--layers 32] [--steps 20] [--opt 0] [--json out.jsonl]
@@ -86,7 +87,8 @@ def main():
                     med = float(dn.median())
                     for wg, v in zip(ids, dn.tolist()):
                         late[name].setdefault(wg, []).append(v - med)
-                if done_prev is not None and li > 0:
+                off = name == "xq_x"  # (off the critical path: not part of the level chain)
+                if done_prev is not None and li > 0 and not off:
                     res[name]["handoff"].append(float(rel.min() - done_prev))
                     res[name]["span"].append(float(dn.max() - done_prev))
                 if (stg > 0).all():  # (attention levels: stamp 2 = softmax done)
@@ -94,12 +96,13 @@ def main():
                     res[name]["body"].append(float((dn - stg).median()))
                 else:
                     res[name]["body"].append(float((dn - rel).median()))
-                done_prev = float(dn.max())
+                if not off:
+                    done_prev = float(dn.max())
     out = dict(tool="wdec_probe", layers=L, opt=a.opt, grid=grid, step_us=round(step_us, 1),
                per_layer_us=round(step_us / L, 2), error=bool(err))
     for name, d in res.items():
         out[name] = {k: round(statistics.median(v), 2) for k, v in d.items() if v}
-    out["layer_span_us"] = round(sum(out[n].get("span", 0) for n in WDEC_LEVELS), 2)
+    out["layer_span_us"] = round(sum(out[n].get("span", 0) for n in WDEC_LEVELS if n != "xq_x"), 2)
     for name in WDEC_LEVELS:  # the workgroups that finish a level latest (median lateness, us)
         lw = sorted(((statistics.median(v), wg) for wg, v in late[name].items()), reverse=True)[:4]
         out[name]["late"] = [[wg, round(v, 2)] for v, wg in lw]

@@ -27,22 +27,27 @@ from .config import WhisperConfig
 from .llama import move_model  # noqa: F401  (re-export)
 
 
-WDEC_LEVELS = ("qkv", "self_attn", "o", "xq", "cross_attn", "xo", "fc1", "fc2")
+WDEC_LEVELS = ("qkv", "xq_x", "self_attn", "o_xq", "cross_attn", "xo", "fc1", "fc2")
+# gemm ids of the persistent decoder (whisper_dec.hip G_*; WdecLayer::g order) and their levels
+WDEC_GEMMS = ("qkv", "o", "xq", "xo", "fc1", "fc2", "xq_o")
+WDEC_GEMM_LEVEL = (0, 3, 1, 5, 6, 7, 3)
 
 
 def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
     """Role table of the persistent Whisper decoder (csrc/kernels/whisper_dec.hip): per workgroup
-    32 ints -- slot kinds (level index or -1), tiles, parts, reload levels, self-attention head,
-    cross-attention item, the level after which the next layer's cross K/V chunk is prefetched, and
-    the mask of levels it completes -- plus the producer count of each level.
+    32 ints -- slot kinds (gemm id, WDEC_GEMMS, or -1), tiles, parts, refill levels, self-attention
+    head, cross-attention item, the level after which the next layer's cross K/V chunk is
+    prefetched, and the mask of levels it completes -- plus the producer count of each level.
 
     Every layer's weights are spread so each workgroup holds at most 5 slots of 5 loads per wave
     (one 16-column tile of a K = d projection per slot; an fc2 tile, K = 4 d, takes slots 1..4):
     fc2 tiles on workgroups [0, d/16), QKV tiles on the last 3 d / 16, the out / cross projections
-    and fc1 in the free slots of the rest.  A slot is refilled right after the level that used it
-    (its next use is a layer later); workgroups that run the self-attention refill after it, so the
-    attention's loads do not queue behind 40-200 KB of weights.  Cross-attention items (head, key
-    chunk) go to the fc2 workgroups, idle from the QKV level to fc2."""
+    and fc1 in the free slots of the rest (at most 2 tiles of a level per workgroup: the epilogue
+    finishes 2 in one round), the x part of the cross query last -- on QKV workgroups, which have
+    its row staged.  A slot is refilled right after the level that used it (its next use is a
+    layer later); workgroups that run the self-attention refill after it, so the attention's loads
+    do not queue behind 40-200 KB of weights.  Cross-attention items (head, key chunk) go to the
+    fc2 workgroups, idle from the QKV level to fc2."""
     import numpy as np
 
     assert ffn == 4 * d and d % 256 == 0
@@ -53,31 +58,38 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
     R = np.full((nwg, 32), -1, dtype=np.int32)
     R[:, 10:15] = 0
     kind, tile, part, rel = R[:, 0:5], R[:, 5:10], R[:, 10:15], R[:, 15:20]
-    LQ, LS, LO, LXQ, LX, LXO, L1, L2 = range(8)
+    GQ, GO, GXQ, GXO, G1, G2, GXQO = range(7)
+    LQ, LXQX, LS, LOXQ, LX = 0, 1, 2, 3, 4
+    lvl_of = WDEC_GEMM_LEVEL
     for t in range(n_d):  # fc2: slots 1..4 of workgroup t
-        kind[t, 1:5], tile[t, 1:5], part[t, 1:5] = L2, t, np.arange(4)
+        kind[t, 1:5], tile[t, 1:5], part[t, 1:5] = G2, t, np.arange(4)
     q0 = nwg - n_qkv
     for t in range(n_qkv):
-        kind[q0 + t, 0], tile[q0 + t, 0] = LQ, t
+        kind[q0 + t, 0], tile[q0 + t, 0] = GQ, t
     R[:H, 20] = np.arange(H)
     R[:n_x, 21] = np.arange(n_x)
     R[:n_x, 22] = LX
     free = [(s, w) for s in range(1, 5) for w in range(nwg) if kind[w, s] < 0 and w >= n_d]
     free.sort()
     fi = 0
-    for lvl, n in ((LO, n_d), (LXQ, n_d), (LXO, n_d), (L1, n_ff)):
+    for gm, n in ((GO, n_d), (GXQO, n_d), (GXO, n_d), (G1, n_ff), (GXQ, n_d)):
         for t in range(n):
+            while fi < len(free) and (
+                    sum(1 for s in range(5) if kind[free[fi][1], s] >= 0
+                        and lvl_of[kind[free[fi][1], s]] == lvl_of[gm]) >= 2
+                    or (gm == GXQ and (kind[free[fi][1], 0] != GQ or R[free[fi][1], 20] >= 0))):
+                fi += 1
             if fi >= len(free):
                 raise ValueError("wdec_roles: not enough free slots")
             s, w = free[fi]
             fi += 1
-            kind[w, s], tile[w, s] = lvl, t
+            kind[w, s], tile[w, s] = gm, t
     work = np.zeros(nwg, dtype=np.int64)
     for w in range(nwg):
         m = 0
         for s in range(5):
             if kind[w, s] >= 0:
-                m |= 1 << int(kind[w, s])
+                m |= 1 << lvl_of[kind[w, s]]
         if R[w, 20] >= 0:
             m |= 1 << LS
         if R[w, 21] >= 0:
@@ -87,11 +99,16 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
     # next layer's tile; before it: this layer's).  The refill's bytes share the CU's in-order
     # memory queue with the next level's activation loads, so each slot goes to the level with the
     # longest run of idle levels behind it (measured: a 40 KB refill right before the next level's
-    # X staging held that staging ~1.6 us), spreading slots over equally good points
+    # X staging held that staging ~1.6 us), spreading slots over equally good points.  (The x part
+    # of the cross query is off the critical path: it counts as no gap.)
+    crit = [lv for lv in range(8) if lv != LXQX]
     for w in range(nwg):
-        W = [lv for lv in range(8) if (work[w] >> lv) & 1]
-        gap = {lv: ((W[(i + 1) % len(W)] - lv - 1) % 8) + (8 if len(W) == 1 else 0) for i, lv in enumerate(W)}
-        load = {lv: 0 for lv in W}
+        W = [lv for lv in crit if (work[w] >> lv) & 1]
+        pos = {lv: crit.index(lv) for lv in W}
+        gap = {lv: ((pos[W[(i + 1) % len(W)]] - pos[lv] - 1) % 7) + (7 if len(W) == 1 else 0) for i, lv in enumerate(W)}
+        if (work[w] >> LXQX) & 1:
+            gap[LXQX] = -1
+        load = {lv: 0 for lv in gap}
         if R[w, 21] >= 0:
             load[LX] += 96  # the cross K / V chunk (KB) issued after the cross-attention
         for s in range(5):
@@ -99,7 +116,7 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
             if k < 0:
                 continue
             kb = 40
-            best = max(W, key=lambda lv: (gap[lv] - load[lv] / 80.0, lv == k))
+            best = max(gap, key=lambda lv: (gap[lv] - load[lv] / 80.0, lv == lvl_of[k]))
             rel[w, s] = best
             load[best] += kb
     R[:, 23] = work
@@ -471,18 +488,31 @@ class WhisperModel:
         flat = []
         for li, L in enumerate(self.dec):
             (wq, bq, cq), (wx, bx, cx), (w1, b1, c1) = L.f_qkv, L.f_xq, L.f_fc1
+            wxo, bxo = self._wdec_xq_o(L)
             flat += [wt(wq), bq, cq, wt(L.o), L.o_b, None, wt(wx), bx, cx, wt(L.xo), L.xo_b, None,
-                     wt(w1), b1, c1, wt(L.fc2), L.fc2_b, None,
+                     wt(w1), b1, c1, wt(L.fc2), L.fc2_b, None, wt(wxo), bxo, None,
                      bufs.k_cache[li], bufs.v_cache[li], bufs.cross[li][0], bufs.cross[li][1]]
         layers = E.wdec_layers(flat, len(self.dec), bufs.hidden)
         cnt = E.alloc_uncached_i32(4096, bufs.hidden)  # level counters [8][8] x 128 B + error word
-        xpart = torch.zeros(self.H * nch * 66, dtype=torch.float32, device=self.device)
+        xpart = torch.zeros(self.H * nch * 66 + 2 * cfg.d_model, dtype=torch.float32, device=self.device)
         T = bufs.cross[0][0].shape[1]
         st = dict(layers=layers, roles=torch.from_numpy(roles).to(self.device), n_prod=n_prod, cnt=cnt, xpart=xpart,
                   ints=[len(self.dec), cfg.d_model, self.H, cfg.ffn, T, bufs.k_cache.shape[3],
                         bufs.block_table.shape[1], nch, -(-T // nch), bufs.cross[0][0].shape[0], grid])
         self._wdec[bufs] = st
         return st
+
+    def _wdec_xq_o(self, L):
+        """The cross query's att part (whisper_dec.hip level OXQ): Wg Wo (pre-tiled bf16) and
+        Wg bo, Wg = the LayerNorm-folded cross-query weight -- x1 Wg^T = x Wg^T + att (Wg Wo)^T +
+        Wg bo.  Built once per layer (3.3 MB each), in f32 then rounded."""
+        if getattr(L, "_xq_o", None) is None:
+            dense = lambda t: (t.dense() if isinstance(t, ops.TiledWeight) else t).float()  # noqa: E731
+            wg, wo = dense(L.f_xq[0]), dense(L.o)
+            w = (wg @ wo).to(torch.bfloat16)
+            b = (wg @ L.o_b.float()).to(torch.bfloat16) if L.o_b is not None else None
+            L._xq_o = (ops.TiledWeight(w), b)
+        return L._xq_o
 
     def wdec_error_word(self):
         st = next(iter(getattr(self, "_wdec", {}).values()), None) if getattr(self, "_wdec", None) else None
