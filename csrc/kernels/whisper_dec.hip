@@ -15,9 +15,9 @@
 //   2 SATT     self-attention of the row, one workgroup per head -> att
 //   3 OXQ      x1 = x + att . Wo^T + bo                           (80 tiles)
 //              att . (Wxq Wo)^T + Wxq bo -> xqb (f32)             (80 tiles, same staged row)
-//   4 XATT     q = LNx(x1) . Wxq^T + b from xqa + xqb and x1's mean / rstd, then the cross-
-//              attention partials, (head, key chunk) per workgroup, K / V chunk prefetched into
-//              LDS by LDS-DMA a layer ahead
+//   4 XATT     q = LNx(x1) . Wxq^T + b from xqa + xqb and x1's mean / rstd (the out-proj tiles'
+//              sums), then the cross-attention partials, (head, key chunk) per workgroup, K / V
+//              chunk prefetched into LDS by LDS-DMA a layer ahead
 //   5 XO       x2 = x1 + merge(partials) . Wxo^T + b              (80 tiles; the merge is the X staging)
 //   6 FC1      f = GELU(LN2(x2) . W1^T + b1)                      (320 tiles)
 //   7 FC2      x3 = x2 + f . W2^T + b2                            (80 tiles, K = 5120)
@@ -236,45 +236,33 @@ VWA_DEVICE float blk_sum(char* lds, float v) {
 }
 
 // cross query head h -> LDS f32 [64]: q = rstd1 (xqa + xqb - mean1 c) + b' (rounded to bf16 like
-// the per-kernel path's q), mean1 / rstd1 of the row x1 (written this layer); qc / qb: c and b' of
-// column h 64 + tx, loaded ahead of the release.  The loads go out after the K / V chunk DMAs, so
-// the vmcnt wait also covers those (the barrier then publishes every wave's chunk).
-VWA_DEVICE void wd_xq_to_lds(const WdecParams& p, const u16* x1, int h, char* lds, float qc, float qb) {
+// the per-kernel path's q), mean1 / rstd1 of x1 from the out-projection tiles' (sum, sum of
+// squares) -- wave 0 alone (lane: column h 64 + lane, tiles lane and lane + 64), no cross-wave
+// round; qc / qb: c and b' of the lane's column, loaded ahead of the release.  The loads go out
+// after the K / V chunk DMAs, so every wave's vmcnt wait also covers those (the barrier then
+// publishes every wave's chunk).
+VWA_DEVICE void wd_xq_to_lds(const WdecParams& p, int h, char* lds, float qc, float qb) {
   float* qf = reinterpret_cast<float*>(lds + L_QF);
-  float* w8 = reinterpret_cast<float*>(lds + L_W8);
-  const int tx = VWA_TX, n8 = p.d >> 3;
+  const int tx = VWA_TX, nt = p.d >> 4;
   const float* xq = xq_buf(p);
-  float a = 0.f, b = 0.f;
   if (tx < 64) {
-    a = ldf_sc1(xq + h * 64 + tx);
-    b = ldf_sc1(xq + p.d + h * 64 + tx);
-  }
-  const uint4 v = tx < n8 ? ld_sc1_b128(rsrc_of(x1, (long long)p.d * 2), (unsigned)tx * 16u) : make_uint4(0, 0, 0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  float f[8], s = 0.f, s2 = 0.f;
-  unpack8(v, f);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    s += f[e];
-    s2 += f[e] * f[e];
-  }
-  s = wave_sum(s);
-  s2 = wave_sum(s2);
-  if ((tx & 63) == 0) {
-    w8[tx >> 6] = s;
-    w8[8 + (tx >> 6)] = s2;
-  }
-  lds_sync();
-  if (tx < 64) {
-    float ts = 0.f, ts2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      ts += w8[i];
-      ts2 += w8[8 + i];
+    const float a = ldf_sc1(xq + h * 64 + tx), b = ldf_sc1(xq + p.d + h * 64 + tx);
+    const float* st2 = xq + 2 * p.d;
+    float s = 0.f, s2 = 0.f;
+    if (tx < nt) {
+      s = ldf_sc1(st2 + 2 * tx);
+      s2 = ldf_sc1(st2 + 2 * tx + 1);
     }
-    const float mean = ts / (float)p.d, rstd = rsqrtf(fmaxf(ts2 / (float)p.d - mean * mean, 0.f) + p.eps);
+    if (tx + 64 < nt) {
+      s += ldf_sc1(st2 + 2 * (tx + 64));
+      s2 += ldf_sc1(st2 + 2 * (tx + 64) + 1);
+    }
+    s = wave_sum(s);
+    s2 = wave_sum(s2);
+    const float mean = s / (float)p.d, rstd = rsqrtf(fmaxf(s2 / (float)p.d - mean * mean, 0.f) + p.eps);
     qf[tx] = bf2f(f2bf((a + b - mean * qc) * rstd + qb));
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   lds_sync();
 }
 
@@ -383,12 +371,13 @@ VWA_DEVICE void wd_self_attn(const WdecParams& p, int li, int h, char* lds) {
   if (tx < 64) sth_sc1(p.att + h * 64 + tx, f2bf(tot / ml.y));
 }
 
-// level 4: cross-attention partial of (head, chunk) from the prefetched K / V chunk in LDS
-VWA_DEVICE void wd_cross_attn(const WdecParams& p, int li, int item, const u16* x1, char* lds, float qc, float qb) {
+// level 4: cross query of head h, then the cross-attention partial of (head, chunk) from the
+// prefetched K / V chunk in LDS
+VWA_DEVICE void wd_cross_attn(const WdecParams& p, int li, int item, char* lds, float qc, float qb) {
   const int h = item / p.nch, ch = item % p.nch;
   const int k0 = ch * p.ch_len, nk = min(p.ch_len, p.T - k0);
   const int tx = VWA_TX, lane = tx & 63, w = tx >> 6;
-  wd_xq_to_lds(p, x1, h, lds, qc, qb);
+  wd_xq_to_lds(p, h, lds, qc, qb);
   const float* qf = reinterpret_cast<const float*>(lds + L_QF);
   const u16* kl = reinterpret_cast<const u16*>(lds + L_KV);
   const u16* vl = reinterpret_cast<const u16*>(lds + L_KV + L_KVV);
@@ -548,7 +537,21 @@ VWA_DEVICE void wd_epilogue(const WdecParams& p, int li, int g0, int g1, int tl0
     v += eb;
     if (gm == G_FC1) v = gelu_erf(v);
     if (gm == G_O || gm == G_XO || gm == G_FC2) {
-      sth_sc1(xout + n, f2bf(v + er));
+      const u16 o = f2bf(v + er);
+      sth_sc1(xout + n, o);
+      if (gm == G_O) {  // the tile's (sum, sum of squares) of x1: the cross query's LayerNorm stats
+        float a = bf2f(o), b = a * a;
+#pragma unroll
+        for (int m = 8; m > 0; m >>= 1) {
+          a += __shfl_xor(a, m, 64);
+          b += __shfl_xor(b, m, 64);
+        }
+        if (q == 0) {
+          float* st2 = xq_buf(p) + 2 * p.d + 2 * tile;
+          stf_sc1(st2, a);
+          stf_sc1(st2 + 1, b);
+        }
+      }
     } else if (gm == G_FC1) {
       sth_sc1(p.f + n, f2bf(v));
     } else if (gm == G_XQ || gm == G_XQO) {
@@ -577,6 +580,7 @@ VWA_DEVICE void wd_epilogue(const WdecParams& p, int li, int g0, int g1, int tl0
 // schedule options (WdecParams::opt[0] bits; 0 = the defaults below)
 constexpr int kOptNoEpiPre = 1;    // load the epilogue operands after the row (not ahead of it)
 constexpr int kOptNoSattnPre = 2;  // self-attention resolves its key addresses after its inputs landed
+constexpr int kOptXqxIdle = 4;     // (diagnostic, wrong results) the x part of the cross query does no work
 
 __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -676,11 +680,12 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
         wd_wait(p, pl, target(pl, li));
       }
       wd_stamp(p, li, lvl, 1);
-      if (lvl == LV_SATT) {
+      if (lvl == LV_XQX && (opt & kOptXqxIdle)) {
+      } else if (lvl == LV_SATT) {
         if (opt & kOptNoSattnPre) wd_self_attn_pre(p, sattn, lds);
         wd_self_attn(p, li, sattn, lds);
       } else if (lvl == LV_XATT) {
-        wd_cross_attn(p, li, xattn, xo, lds, ec, eb);
+        wd_cross_attn(p, li, xattn, lds, ec, eb);
       } else {
         // activation row + residual of this level
         const u16* xin = lvl == LV_OXQ ? p.att : lvl == LV_FC2 ? p.f : xc;

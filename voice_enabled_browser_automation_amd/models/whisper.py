@@ -47,7 +47,8 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
     its row staged.  A slot is refilled right after the level that used it (its next use is a
     layer later); workgroups that run the self-attention refill after it, so the attention's loads
     do not queue behind 40-200 KB of weights.  Cross-attention items (head, key chunk) go to the
-    fc2 workgroups, idle from the QKV level to fc2."""
+    fc2 workgroups, idle from the QKV level to fc2; self-attention heads to workgroups with idle
+    levels after it."""
     import numpy as np
 
     assert ffn == 4 * d and d % 256 == 0
@@ -66,7 +67,11 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
     q0 = nwg - n_qkv
     for t in range(n_qkv):
         kind[q0 + t, 0], tile[q0 + t, 0] = GQ, t
-    R[:H, 20] = np.arange(H)
+    # self-attention heads: on the fc2-only workgroups [0, q0) first, then on the last ones
+    # (QKV + cross out-proj + fc1: two idle levels after the attention for their refills) -- not
+    # on fc2 + QKV workgroups, whose 5 slots and cross item leave no idle level for theirs
+    sat = list(range(min(H, q0))) + list(range(nwg - 1, nwg - 1 - max(0, H - q0), -1))
+    R[sat, 20] = np.arange(H)
     R[:n_x, 21] = np.arange(n_x)
     R[:n_x, 22] = LX
     free = [(s, w) for s in range(1, 5) for w in range(nwg) if kind[w, s] < 0 and w >= n_d]
@@ -116,7 +121,13 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
             if k < 0:
                 continue
             kb = 40
-            best = max(gap, key=lambda lv: (gap[lv] - load[lv] / 80.0, lv == lvl_of[k]))
+            # (a level right before this workgroup's next one is the last resort: its refill
+            # holds that level's row loads -- measured 1.2 us late QKV on WGs 16..19)
+            # (the x part of the cross query runs right after the QKV level: its slot is never
+            # refilled there -- that would load THIS layer's tile behind every QKV refill)
+            cand = [lv for lv in gap if not (lvl_of[k] == LXQX and lv < LXQX)]
+            best = max(cand, key=lambda lv: (gap[lv] - load[lv] / 80.0 - (0.5 if gap[lv] == 0 else 0.0),
+                                             lv == lvl_of[k]))
             rel[w, s] = best
             load[best] += kb
     R[:, 23] = work
@@ -494,7 +505,7 @@ class WhisperModel:
                      bufs.k_cache[li], bufs.v_cache[li], bufs.cross[li][0], bufs.cross[li][1]]
         layers = E.wdec_layers(flat, len(self.dec), bufs.hidden)
         cnt = E.alloc_uncached_i32(4096, bufs.hidden)  # level counters [8][8] x 128 B + error word
-        xpart = torch.zeros(self.H * nch * 66 + 2 * cfg.d_model, dtype=torch.float32, device=self.device)
+        xpart = torch.zeros(self.H * nch * 66 + 3 * cfg.d_model, dtype=torch.float32, device=self.device)
         T = bufs.cross[0][0].shape[1]
         st = dict(layers=layers, roles=torch.from_numpy(roles).to(self.device), n_prod=n_prod, cnt=cnt, xpart=xpart,
                   ints=[len(self.dec), cfg.d_model, self.H, cfg.ffn, T, bufs.k_cache.shape[3],
