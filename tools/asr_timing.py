@@ -1,7 +1,11 @@
 """Whisper transcription time split (encoder / decoder) with and without the chained decoder
 launches (models/whisper.py, skinny_stream.hip chain_kernel SEQ 1/2), fixed 40-token work on the
 bench's synthetic 10 s utterance.  One JSON line per mode.
-python tools/asr_timing.py [--asr whisper-large-v3] [--reps 10]"""
+python tools/asr_timing.py [--asr whisper-large-v3] [--reps 10]
+
+decode_us_per_token = host time from the encoder's launch to the last token / tokens (includes the
+encoder and cross K/V projections still running after their launch); decode_gpu_us_per_token = the
+decoder's stream time (4-token prompt step + the token loop, CUDA events) / tokens."""
 import argparse
 import json
 import os
@@ -66,7 +70,7 @@ def main():
         audio = eng.pcm_to_audio(synth_speech(10.0, seed=100))
         for _ in range(2):
             eng.transcribe(audio, exact_tokens=a.tokens)
-        enc, dec, tot = [], [], []
+        enc, dec, tot, dgpu = [], [], [], []
         for _ in range(a.reps):
             torch.cuda.synchronize()
             texts[chain] = eng.transcribe(audio, exact_tokens=a.tokens)
@@ -74,11 +78,17 @@ def main():
             enc.append(s["encode_ms"])
             dec.append(s["decode_ms"])
             tot.append(s["total_ms"])
+            if s.get("decode_gpu_ms") is not None:
+                dgpu.append(s["decode_gpu_ms"])
         print(json.dumps(dict(tool="asr_timing", asr=a.asr, chain=chain == "1", persistent=chain == "p",
                               persistent_used=bool(getattr(m, "_wdec", None)), tokens=a.tokens,
                               encode_ms=round(statistics.median(enc), 2), decode_ms=round(statistics.median(dec), 2),
                               total_ms=round(statistics.median(tot), 2),
                               decode_us_per_token=round(1e3 * statistics.median(dec) / a.tokens, 1),
+                              # the decoder's own stream time (prompt step + token loop), from events:
+                              # decode_ms starts when the encoder is LAUNCHED, so it also holds the
+                              # encoder / cross K/V tail still running then
+                              decode_gpu_us_per_token=round(1e3 * statistics.median(dgpu) / a.tokens, 1) if dgpu else None,
                               chained=bool(m.chain_descs()))), flush=True)
     if len(texts) >= 2:
         print(json.dumps(dict(tool="asr_timing", same_text=len(set(texts.values())) == 1,

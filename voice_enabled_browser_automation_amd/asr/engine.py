@@ -335,6 +335,13 @@ class AsrEngine:
             enc = m.encode(mel)
             self.set_cross_batch(slots, enc)
             t_enc = time.perf_counter()
+            # GPU-side decode time (prompt step + token loop): the host stamps above are taken when
+            # the encoder and the cross K/V projections are LAUNCHED, so decode_ms also holds
+            # whatever of them was still running; events bracket the decoder's own stream time
+            ev = None
+            if m.device.type == "cuda":
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             logits = self._prompt_logits(slots, prompts)
             outs: List[List[int]] = [[] for _ in range(B)]
             live = list(range(B))
@@ -361,8 +368,14 @@ class AsrEngine:
             if self._chain_failed():  # results of a timed-out chained launch are invalid: redo
                 retry = True
             t_end = time.perf_counter()
+            dec_gpu = None
+            if ev is not None:
+                ev[1].record()
+                ev[1].synchronize()  # (the tokens were read back: the stream is already there)
+                dec_gpu = ev[0].elapsed_time(ev[1])
             self.last_stats = dict(encode_ms=(t_enc - t0) * 1e3, decode_ms=(t_end - t_enc) * 1e3,
-                                   total_ms=(t_end - t0) * 1e3, tokens=sum(len(o) for o in outs), batch=B,
+                                   decode_gpu_ms=dec_gpu, total_ms=(t_end - t0) * 1e3,
+                                   tokens=sum(len(o) for o in outs), batch=B,
                                    prefix_tokens=sum(len(p) - len(self.prompt) for p in prompts))
             if not retry:
                 return outs
