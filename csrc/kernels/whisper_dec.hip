@@ -75,9 +75,23 @@ VWA_DEVICE int level_of(int gm) {
        : gm == G_FC1 ? LV_FC1 : LV_FC2;
 }
 
+// Wave-uniform values through readfirstlane.  The per-layer descriptors are read with VECTOR loads
+// (the kernel stores to global memory, so the compiler cannot prove them unclobbered for scalar
+// loads): a buffer resource built from such a pointer lives in VGPRs, and every buffer load through
+// it became a waterfall loop -- readfirstlane / compare / exec loop with a vmcnt(0) per iteration,
+// i.e. each 1 KB weight load of a refill and each self-attention V load waited for every load
+// before it (60 such loads in the ISA).  Every pointer and size here is uniform by construction.
+VWA_DEVICE int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+template <class T>
+VWA_DEVICE T* uni(T* p) {
+  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return reinterpret_cast<T*>(((unsigned long long)hi << 32) | lo);
+}
+
 VWA_DEVICE __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long long bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(bytes < 0x7FFFFFF0ll ? bytes : 0x7FFFFFF0ll),
-                                           0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(uni(const_cast<void*>(p)), (short)0,
+                                           uni((int)(bytes < 0x7FFFFFF0ll ? bytes : 0x7FFFFFF0ll)), 0x00020000);
 }
 
 // sc1 (device-coherent) loads / stores of data crossing workgroups inside the launch
@@ -197,7 +211,7 @@ VWA_DEVICE void wd_kv_prefetch(const WdecParams& p, int li, int item, char* lds)
   const WdecLayer& L = p.layers[li];
   const long long bytes = (long long)p.sessions * p.T * p.H * 64 * 2;
   const __amdgpu_buffer_rsrc_t rk = rsrc_of(L.xk, bytes), rv = rsrc_of(L.xv, bytes);
-  const int tx = VWA_TX, lane = tx & 63, w = tx >> 6;
+  const int tx = VWA_TX, lane = tx & 63, w = uni(tx >> 6);  // (uniform: the K / V select stays scalar)
   const int n8 = (nk + 7) >> 3;  // 1 KB instructions (8 keys of 128 B) per tensor
   for (int r = w; r < 2 * n8; r += 8) {
     const bool isv = r >= n8;
@@ -587,14 +601,14 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
   const int* rr = p.roles + (size_t)blockIdx.x * kWdRole;
   int kind[kSlots], klv[kSlots], tile[kSlots], part[kSlots], rl[kSlots];
 #pragma unroll
-  for (int s = 0; s < kSlots; ++s) {
-    kind[s] = rr[R_KIND + s];  // gemm id or -1
+  for (int s = 0; s < kSlots; ++s) {  // (uniform: scalar branches and offsets)
+    kind[s] = uni(rr[R_KIND + s]);  // gemm id or -1
     klv[s] = kind[s] >= 0 ? level_of(kind[s]) : -1;
-    tile[s] = rr[R_TILE + s];
-    part[s] = rr[R_PART + s];
-    rl[s] = rr[R_RELOAD + s];
+    tile[s] = uni(rr[R_TILE + s]);
+    part[s] = uni(rr[R_PART + s]);
+    rl[s] = uni(rr[R_RELOAD + s]);
   }
-  const int sattn = rr[R_SATT], xattn = rr[R_XATT], xpre = rr[R_XPRE], work = rr[R_WORK];
+  const int sattn = uni(rr[R_SATT]), xattn = uni(rr[R_XATT]), xpre = uni(rr[R_XPRE]), work = uni(rr[R_WORK]);
   const int NL = p.n_layers;
   const int opt = p.opt[0];
   if (work == 0) return;

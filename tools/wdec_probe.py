@@ -36,9 +36,14 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--opt", type=int, default=0)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--role-opts", default="", help="role-plan variant, e.g. att_pen=1,sat=tail")
     a = ap.parse_args()
     ops.ext()
     os.environ["VWA_ASR_PERSIST"] = "1"
+    from voice_enabled_browser_automation_amd.models import whisper as W
+    for kv in filter(None, a.role_opts.split(",")):
+        k, v = kv.split("=")
+        W.WDEC_ROLE_OPTS[k] = float(v) if k != "sat" else v
     cfg = dataclasses.replace(get_config("whisper-large-v3"), n_enc_layers=1, n_dec_layers=a.layers)
     m = WhisperModel(cfg, device="cuda", seed=0, tile_decoder=True)
     torch.manual_seed(0)
@@ -98,7 +103,7 @@ def main():
                     res[name]["body"].append(float((dn - rel).median()))
                 if not off:
                     done_prev = float(dn.max())
-    out = dict(tool="wdec_probe", layers=L, opt=a.opt, grid=grid, step_us=round(step_us, 1),
+    out = dict(tool="wdec_probe", layers=L, opt=a.opt, role_opts=a.role_opts, grid=grid, step_us=round(step_us, 1),
                per_layer_us=round(step_us / L, 2), error=bool(err))
     for name, d in res.items():
         out[name] = {k: round(statistics.median(v), 2) for k, v in d.items() if v}

@@ -33,6 +33,12 @@ WDEC_GEMMS = ("qkv", "o", "xq", "xo", "fc1", "fc2", "xq_o")
 WDEC_GEMM_LEVEL = (0, 3, 1, 5, 6, 7, 3)
 
 
+# role-plan variants for A/B probes (tools/wdec_probe.py --role-opts): att_pen = penalty for a
+# refill right before this workgroup's next attention level; sat = "fc2" (self-attention heads on
+# the fc2-only workgroups first) or "tail" (on the last workgroups)
+WDEC_ROLE_OPTS: dict = {}
+
+
 def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
     """Role table of the persistent Whisper decoder (csrc/kernels/whisper_dec.hip): per workgroup
     32 ints -- slot kinds (gemm id, WDEC_GEMMS, or -1), tiles, parts, refill levels, self-attention
@@ -70,7 +76,11 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
     # self-attention heads: on the fc2-only workgroups [0, q0) first, then on the last ones
     # (QKV + cross out-proj + fc1: two idle levels after the attention for their refills) -- not
     # on fc2 + QKV workgroups, whose 5 slots and cross item leave no idle level for theirs
-    sat = list(range(min(H, q0))) + list(range(nwg - 1, nwg - 1 - max(0, H - q0), -1))
+    opts = WDEC_ROLE_OPTS
+    if opts.get("sat", "fc2") == "tail":
+        sat = list(range(nwg - 1, nwg - 1 - H, -1))
+    else:
+        sat = list(range(min(H, q0))) + list(range(nwg - 1, nwg - 1 - max(0, H - q0), -1))
     R[sat, 20] = np.arange(H)
     R[:n_x, 21] = np.arange(n_x)
     R[:n_x, 22] = LX
@@ -111,6 +121,8 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
         W = [lv for lv in crit if (work[w] >> lv) & 1]
         pos = {lv: crit.index(lv) for lv in W}
         gap = {lv: ((pos[W[(i + 1) % len(W)]] - pos[lv] - 1) % 7) + (7 if len(W) == 1 else 0) for i, lv in enumerate(W)}
+        nxt = {lv: W[(i + 1) % len(W)] for i, lv in enumerate(W)}
+        att_pen = {lv: (opts.get("att_pen", 0.0) if nxt[lv] in (LS, LX) else 0.0) for lv in W}
         if (work[w] >> LXQX) & 1:
             gap[LXQX] = -1
         load = {lv: 0 for lv in gap}
@@ -126,8 +138,8 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
             # (the x part of the cross query runs right after the QKV level: its slot is never
             # refilled there -- that would load THIS layer's tile behind every QKV refill)
             cand = [lv for lv in gap if not (lvl_of[k] == LXQX and lv < LXQX)]
-            best = max(cand, key=lambda lv: (gap[lv] - load[lv] / 80.0 - (0.5 if gap[lv] == 0 else 0.0),
-                                             lv == lvl_of[k]))
+            best = max(cand, key=lambda lv: (gap[lv] - load[lv] / 80.0 - (0.5 if gap[lv] == 0 else 0.0)
+                                             - att_pen.get(lv, 0.0), lv == lvl_of[k]))
             rel[w, s] = best
             load[best] += kb
     R[:, 23] = work
