@@ -898,8 +898,10 @@ Tensor wdec_layers(std::vector<c10::optional<Tensor>> flat, int64_t n_layers, Te
 
 // bufs: x0, x1, q, att, f, xpart, seq_ids, ctx_lens, slots, block_table, cross_table, cnt
 // ints: n_layers, d, H, ffn, T, block_size, bt_stride, nch, ch_len, sessions, grid
+// lm (optional): [W pre-tiled bf16 [V, d], bias bf16 [V] or None-as-empty, column sums f32 [V], logits f32 [>= V]]
 void wdec_run(Tensor layers, Tensor roles, std::vector<Tensor> bufs, std::vector<int64_t> ints, double eps,
-              double scale, std::vector<int64_t> n_prod, c10::optional<Tensor> ts, int64_t opt) {
+              double scale, std::vector<int64_t> n_prod, c10::optional<Tensor> ts, int64_t opt,
+              c10::optional<std::vector<Tensor>> lm) {
   TORCH_CHECK(bufs.size() == 12 && ints.size() == 11 && n_prod.size() == kWdLevels, "wdec_run: argument counts");
   const Tensor& like = bufs[0];
   c10::DeviceGuard g(like.device());
@@ -950,6 +952,26 @@ void wdec_run(Tensor layers, Tensor roles, std::vector<Tensor> bufs, std::vector
     p.ts = reinterpret_cast<unsigned long long*>(ts->data_ptr());
   }
   p.opt[0] = (int)opt;
+  if (lm.has_value()) {
+    const std::vector<Tensor>& L = *lm;
+    TORCH_CHECK(L.size() == 4, "wdec_run: lm = [W, bias, ln_c, logits]");
+    check_bf16(L[0], "wdec_run lm W");
+    TORCH_CHECK(L[0].dim() == 2 && L[0].size(1) == p.d && L[0].size(0) % 16 == 0 && L[0].is_contiguous(),
+                "wdec_run: lm W [V % 16 == 0, d] (pre-tiled)");
+    const int64_t V = L[0].size(0);
+    TORCH_CHECK(L[2].scalar_type() == at::kFloat && L[2].numel() == V && L[2].is_cuda(), "wdec_run: lm ln_c f32 [V]");
+    TORCH_CHECK(L[3].scalar_type() == at::kFloat && L[3].is_contiguous() && L[3].numel() >= V && L[3].is_cuda(),
+                "wdec_run: logits f32 [>= V]");
+    p.lm_W = reinterpret_cast<const uint16_t*>(L[0].data_ptr());
+    if (L[1].numel()) {
+      check_bf16(L[1], "wdec_run lm bias");
+      TORCH_CHECK(L[1].numel() == V, "wdec_run: lm bias [V]");
+      p.lm_b = reinterpret_cast<const uint16_t*>(L[1].data_ptr());
+    }
+    p.lm_c = L[2].data_ptr<float>();
+    p.logits = L[3].data_ptr<float>();
+    p.n_vocab = (int)V;
+  }
   check_rc(vwa_wdec_launch(&p, (int)grid, cur_stream(like)), "wdec");
 }
 
@@ -1466,7 +1488,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("device_cus", [](Tensor like) { return (int64_t)device_cus(like); });
   m.def("wdec_layers", &wdec_layers, py::arg("flat"), py::arg("n_layers"), py::arg("like"));
   m.def("wdec_run", &wdec_run, py::arg("layers"), py::arg("roles"), py::arg("bufs"), py::arg("ints"), py::arg("eps"),
-        py::arg("scale"), py::arg("n_prod"), py::arg("ts") = py::none(), py::arg("opt") = 0);
+        py::arg("scale"), py::arg("n_prod"), py::arg("ts") = py::none(), py::arg("opt") = 0, py::arg("lm") = py::none());
   m.def("decode_advance", &decode_advance);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
         py::arg("rstd") = py::none(), py::arg("residual") = py::none(), py::arg("w_tiled") = false,

@@ -230,6 +230,9 @@ struct WdecParams {
   int n_prod[kWdLevels];              // workgroups that complete each level (per layer)
   unsigned long long* ts;             // diagnostic stamps [grid][n_layers * 8][4] (tools/wdec_probe.py) or null
   int opt[4];                         // schedule options (whisper_dec.hip kOpt*)
+  // optional LM head after the last layer (lm_W null: none): folded final LayerNorm, pre-tiled
+  // [n_vocab][d] bf16, bias [n_vocab], column sums [n_vocab] -> f32 logits row [n_vocab]
+  const uint16_t* lm_W; const uint16_t* lm_b; const float* lm_c; float* logits; int n_vocab;
 };
 
 #ifdef __cplusplus

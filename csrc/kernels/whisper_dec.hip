@@ -189,6 +189,20 @@ VWA_DEVICE void wd_load(const WdecParams& p, int li, int gm, int tile, int part,
   }
 }
 
+// slot load of a tile of an explicit K = d weight (the LM head): all 40 slices, 5 per wave
+VWA_DEVICE void wd_load_w(const u16* W, int n_cols, int K, int tile, uint4 (&wr)[kLps]) {
+  const int G = K >> 7;
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(W, (long long)n_cols * K * 2);
+  const int tx = VWA_TX, lane = tx & 63, w = tx >> 6;
+#pragma unroll
+  for (int j = 0; j < kLps; ++j) {
+    const int sl = w + 8 * j, kg = sl >> 2, s4 = sl & 3;
+    const unsigned off = ((unsigned)(tile * G + kg) * 4u + (unsigned)s4) * 1024u + (unsigned)lane * 16u;
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    wr[j] = make_uint4(v.x, v.y, v.z, v.w);
+  }
+}
+
 // the MFMAs of one slot: acc (row 0 = lanes 0..15, element 0) += X . W over the slot's slices
 VWA_DEVICE void wd_mma(const char* lds, int part, const uint4 (&wr)[kLps], f32x4& acc) {
   const int tx = VWA_TX, lane = tx & 63, w = tx >> 6, nl = lane & 15, g = lane >> 4;
@@ -591,6 +605,27 @@ VWA_DEVICE void wd_epilogue(const WdecParams& p, int li, int g0, int g1, int tl0
   }
 }
 
+// LM head epilogue of (<= 2) tiles in one LDS round: thread t < 16 nt finishes column t & 15 of
+// tile t >> 4 (lc / lb: that column's folded-LayerNorm column sum and bias, loaded with the tile)
+VWA_DEVICE void wd_lm_epilogue(const WdecParams& p, int tl0, int tl1, int nt, const f32x4& acc0, const f32x4& acc1,
+                               char* lds, float lc, float lb) {
+  float* red = reinterpret_cast<float*>(lds + L_RED);
+  const float* st = reinterpret_cast<const float*>(lds + L_STAT);
+  const int tx = VWA_TX, lane = tx & 63, w = tx >> 6;
+  if (lane < 16) {
+    red[w * 32 + lane] = acc0[0];
+    red[w * 32 + 16 + lane] = acc1[0];
+  }
+  lds_sync();
+  if (tx < 16 * nt) {
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) v += red[ww * 32 + tx];
+    p.logits[(tx < 16 ? tl0 : tl1) * 16 + (tx & 15)] = (v - st[0] * lc) * st[1] + lb;
+  }
+  lds_sync();  // (red is rewritten by the next round)
+}
+
 // schedule options (WdecParams::opt[0] bits; 0 = the defaults below)
 constexpr int kOptNoEpiPre = 1;    // load the epilogue operands after the row (not ahead of it)
 constexpr int kOptNoSattnPre = 2;  // self-attention resolves its key addresses after its inputs landed
@@ -611,7 +646,7 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
   const int sattn = uni(rr[R_SATT]), xattn = uni(rr[R_XATT]), xpre = uni(rr[R_XPRE]), work = uni(rr[R_WORK]);
   const int NL = p.n_layers;
   const int opt = p.opt[0];
-  if (work == 0) return;
+  if (work == 0 && !p.lm_W) return;
   // launch bases of the level counters (see the header comment)
   unsigned long long* bases = reinterpret_cast<unsigned long long*>(lds + L_RED);  // (before any tile)
   if (VWA_TX < 64) {
@@ -738,6 +773,50 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
       if (xattn >= 0 && xpre == lvl) {
         const int lt = xpre < LV_XATT ? li : li + 1;
         if (lt < NL) wd_kv_prefetch(p, lt, xattn, lds);
+      }
+    }
+  }
+  if (p.lm_W) {
+    // LM head: tiles blockIdx.x + j grid of the padded vocabulary, a 5-slot ring; the first five
+    // tiles' weights go out BEFORE the wait for the last layer's fc2 (weights never depend on the
+    // activations), the rest stream behind them -- no separate launch, no launch gap
+    const int G = (int)gridDim.x, NTv = p.n_vocab >> 4, b0 = (int)blockIdx.x;
+    const int ntw = b0 < NTv ? (NTv - 1 - b0) / G + 1 : 0;
+    const int tx = VWA_TX, q = tx & 15;
+    float lc[kSlots], lb[kSlots];  // (threads < 32: column q of the slot's tile)
+    auto issue = [&](int s, int j) {
+      if (j < ntw) {
+        const int t = b0 + j * G;
+        wd_load_w(p.lm_W, p.n_vocab, p.d, t, wr[s]);
+        if (tx < 32) {
+          lc[s] = gld(p.lm_c + t * 16 + q);
+          lb[s] = p.lm_b ? bf2f(gld(p.lm_b + t * 16 + q)) : 0.f;
+        }
+      }
+    };
+#pragma unroll
+    for (int s = 0; s < kSlots; ++s) issue(s, s);
+    wd_wait(p, LV_FC2, base[LV_FC2] + (unsigned long long)p.n_prod[LV_FC2] * (unsigned long long)NL);
+    wd_stage(p, p.d, ((NL - 1) & 1) ? p.x0 : p.x1, lds, true);
+    for (int j0 = 0; j0 < ntw; j0 += kSlots) {
+#pragma unroll
+      for (int s = 0; s < kSlots; s += 2) {
+        const int ja = j0 + s, jb = j0 + s + 1;
+        if (ja >= ntw) break;  // (uniform)
+        const bool two = s + 1 < kSlots && jb < ntw;
+        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+        wd_mma(lds, 0, wr[s], acc0);
+        const float c0 = lc[s], bb0 = lb[s];
+        float c1 = 0.f, bb1 = 0.f;
+        if (s + 1 < kSlots) {
+          if (two) wd_mma(lds, 0, wr[s + 1], acc1);
+          c1 = lc[s + 1];
+          bb1 = lb[s + 1];
+        }
+        issue(s, ja + kSlots);  // (the slot's registers are free once its MFMAs were issued)
+        if (s + 1 < kSlots && two) issue(s + 1, jb + kSlots);
+        wd_lm_epilogue(p, b0 + ja * G, b0 + jb * G, two ? 2 : 1, acc0, acc1, lds, tx < 16 ? c0 : c1,
+                       tx < 16 ? bb0 : bb1);
       }
     }
   }

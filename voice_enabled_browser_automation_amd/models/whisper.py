@@ -542,15 +542,20 @@ class WhisperModel:
         return None if st is None else st["cnt"].view(torch.int64)[1024:1025]
 
     def _wdec_step(self, bufs) -> torch.Tensor:
-        """Every decoder layer of a one-row step (the embedding is in bufs.hidden[0]); returns the
-        final hidden row."""
+        """Every decoder layer of a one-row step (the embedding is in bufs.hidden[0]) and the LM
+        head (folded final LayerNorm) in the same launch; returns the f32 logits row [1, V]."""
         st = self._wdec_state(bufs)
+        w, b, c = self.f_lm
+        wt = w.t if isinstance(w, ops.TiledWeight) else w
+        lm = [wt, b if b is not None else st.setdefault("no_bias", torch.empty(0, dtype=torch.bfloat16,
+                                                                                  device=self.device)),
+              c, bufs.logits[0]]
         ops.ext().wdec_run(st["layers"], st["roles"],
                            [bufs.hidden, bufs.h, bufs.q, bufs.att, bufs.f, st["xpart"], bufs.seq_ids, bufs.ctx_lens,
                             bufs.slots, bufs.block_table, bufs.cross_table, st["cnt"]],
                            st["ints"], self.cfg.ln_eps, self.hd ** -0.5, st["n_prod"], st.get("ts"),
-                           int(st.get("opt", 0)))
-        return (bufs.hidden if len(self.dec) % 2 == 0 else bufs.h)[:1]
+                           int(st.get("opt", 0)), lm)
+        return bufs.logits[:1]
 
     def decode_step(self, bufs, M: int) -> torch.Tensor:
         """M token rows (bufs: tokens/positions/slots/seq_ids/ctx_lens + self cache + cross K/V).
@@ -564,9 +569,7 @@ class WhisperModel:
         ops.embedding(bufs.tokens, self.tok_emb, pos_table=self.pos_emb, positions=bufs.positions, out=x, rows=M)
         eps = cfg.ln_eps
         if self._wdec_ok(M):
-            x = self._wdec_step(bufs)
-            w, b, c = self.f_lm
-            return ops.linear(x, w, b, out=bufs.logits[:M], eps=eps, ln_c=c)
+            return self._wdec_step(bufs)  # (the LM head is the launch's last level)
         chain = self._chain_ok(M)
         qkv_done = False
         for li, L in enumerate(self.dec):
