@@ -901,7 +901,8 @@ Tensor wdec_layers(std::vector<c10::optional<Tensor>> flat, int64_t n_layers, Te
 // lm (optional): [W pre-tiled bf16 [V, d], bias bf16 [V] or None-as-empty, column sums f32 [V], logits f32 [>= V]]
 void wdec_run(Tensor layers, Tensor roles, std::vector<Tensor> bufs, std::vector<int64_t> ints, double eps,
               double scale, std::vector<int64_t> n_prod, c10::optional<Tensor> ts, int64_t opt,
-              c10::optional<std::vector<Tensor>> lm) {
+              c10::optional<std::vector<Tensor>> lm, c10::optional<std::vector<Tensor>> emb,
+              c10::optional<std::vector<Tensor>> smp, int64_t loop_base_block) {
   TORCH_CHECK(bufs.size() == 12 && ints.size() == 11 && n_prod.size() == kWdLevels, "wdec_run: argument counts");
   const Tensor& like = bufs[0];
   c10::DeviceGuard g(like.device());
@@ -971,6 +972,48 @@ void wdec_run(Tensor layers, Tensor roles, std::vector<Tensor> bufs, std::vector
     p.lm_c = L[2].data_ptr<float>();
     p.logits = L[3].data_ptr<float>();
     p.n_vocab = (int)V;
+  }
+  // emb (optional): [tok_emb bf16 [rows, d], pos_emb bf16 [>= max position + 1, d], tokens int32, positions int32]
+  if (emb.has_value()) {
+    const std::vector<Tensor>& Em = *emb;
+    TORCH_CHECK(Em.size() == 4, "wdec_run: emb = [tok_emb, pos_emb, tokens, positions]");
+    check_bf16(Em[0], "wdec_run tok_emb");
+    check_bf16(Em[1], "wdec_run pos_emb");
+    TORCH_CHECK(Em[0].dim() == 2 && Em[0].size(1) == p.d && Em[0].is_contiguous() && Em[1].dim() == 2 &&
+                    Em[1].size(1) == p.d && Em[1].is_contiguous(),
+                "wdec_run: embedding tables [rows, d] contiguous");
+    TORCH_CHECK(Em[2].scalar_type() == at::kInt && Em[3].scalar_type() == at::kInt && Em[2].is_cuda() && Em[3].is_cuda(),
+                "wdec_run: tokens / positions int32");
+    TORCH_CHECK(p.block_size > 0 && Em[1].size(0) >= (int64_t)p.bt_stride * p.block_size,
+                "wdec_run: the position table covers every KV position");
+    p.tok_emb = reinterpret_cast<const uint16_t*>(Em[0].data_ptr());
+    p.pos_emb = reinterpret_cast<const uint16_t*>(Em[1].data_ptr());
+    p.tokens = Em[2].data_ptr<int>();
+    p.positions = Em[3].data_ptr<int>();
+    p.emb_rows = (int)Em[0].size(0);
+  }
+  // smp (optional, needs lm): [mask u32-as-int32 [>= V / 32], out_tok int32, step int32, part f32 [2 grid],
+  //   loop_out int32, loop_cnt int32, adv_tokens, adv_positions, adv_ctx int32, adv_slots int64]
+  if (smp.has_value()) {
+    const std::vector<Tensor>& S = *smp;
+    TORCH_CHECK(S.size() == 10 && p.lm_W, "wdec_run: smp = 10 tensors, with the LM head");
+    TORCH_CHECK(S[0].scalar_type() == at::kInt && S[0].numel() * 32 >= p.n_vocab, "wdec_run: sampler mask words");
+    TORCH_CHECK(S[3].scalar_type() == at::kFloat && S[3].numel() >= 2 * grid, "wdec_run: sampler partials f32 [2 grid]");
+    for (int i : {1, 2, 4, 5, 6, 7, 8}) TORCH_CHECK(S[(size_t)i].scalar_type() == at::kInt && S[(size_t)i].is_cuda(), "wdec_run: int32 loop state");
+    TORCH_CHECK(S[9].scalar_type() == at::kLong && S[9].is_cuda(), "wdec_run: slots int64");
+    p.smp_mask = reinterpret_cast<const uint32_t*>(S[0].data_ptr());
+    p.smp_tok = S[1].data_ptr<int>();
+    p.smp_step = S[2].data_ptr<int>();
+    p.smp_part = S[3].data_ptr<float>();
+    p.loop_out = S[4].data_ptr<int>();
+    p.loop_max = (int)S[4].numel();
+    p.loop_cnt = S[5].data_ptr<int>();
+    p.adv_tokens = S[6].data_ptr<int>();
+    p.adv_positions = S[7].data_ptr<int>();
+    p.adv_ctx = S[8].data_ptr<int>();
+    p.adv_slots = S[9].data_ptr<int64_t>();
+    p.loop_base_block = (int)loop_base_block;
+    TORCH_CHECK(bufs[11].numel() >= 2 * 1280, "wdec_run: counter words hold the sampler counters (u64 1152..1279)");
   }
   check_rc(vwa_wdec_launch(&p, (int)grid, cur_stream(like)), "wdec");
 }
@@ -1488,7 +1531,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("device_cus", [](Tensor like) { return (int64_t)device_cus(like); });
   m.def("wdec_layers", &wdec_layers, py::arg("flat"), py::arg("n_layers"), py::arg("like"));
   m.def("wdec_run", &wdec_run, py::arg("layers"), py::arg("roles"), py::arg("bufs"), py::arg("ints"), py::arg("eps"),
-        py::arg("scale"), py::arg("n_prod"), py::arg("ts") = py::none(), py::arg("opt") = 0, py::arg("lm") = py::none());
+        py::arg("scale"), py::arg("n_prod"), py::arg("ts") = py::none(), py::arg("opt") = 0, py::arg("lm") = py::none(),
+        py::arg("emb") = py::none(), py::arg("smp") = py::none(), py::arg("loop_base_block") = 0);
   m.def("decode_advance", &decode_advance);
   m.def("gemm", &gemm, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("y"), py::arg("epi"),
         py::arg("rstd") = py::none(), py::arg("residual") = py::none(), py::arg("w_tiled") = false,

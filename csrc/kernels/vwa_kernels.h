@@ -233,6 +233,15 @@ struct WdecParams {
   // optional LM head after the last layer (lm_W null: none): folded final LayerNorm, pre-tiled
   // [n_vocab][d] bf16, bias [n_vocab], column sums [n_vocab] -> f32 logits row [n_vocab]
   const uint16_t* lm_W; const uint16_t* lm_b; const float* lm_c; float* logits; int n_vocab;
+  // optional: the step's embedding from the tables (tok_emb null: x0 holds it already) -- row
+  // tokens[0] of tok_emb [emb_rows][d] (ids outside give zeros) + row positions[0] of pos_emb
+  const uint16_t* tok_emb; const uint16_t* pos_emb; const int* tokens; const int* positions; int emb_rows;
+  // optional (needs the LM head): greedy masked argmax of the logits (smp_mask: one bit per token,
+  // the sampler's; -1 when no token is admissible) and the device-loop advance (asr/engine.py):
+  // token -> smp_tok, loop_out[loop_cnt++], adv_tokens[0]; position / context / KV slot move on
+  const uint32_t* smp_mask; int* smp_tok; int* smp_step; float* smp_part; int* loop_out; int* loop_cnt;
+  int loop_max, loop_base_block;
+  int* adv_tokens; int* adv_positions; int* adv_ctx; int64_t* adv_slots;
 };
 
 #ifdef __cplusplus

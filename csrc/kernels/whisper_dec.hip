@@ -69,6 +69,7 @@ constexpr int kLds = 163840;
 constexpr int kMaxChunk = 384;
 constexpr int kSpinLimit = 1 << 17;  // bounded polls: a non-resident producer ends the launch, not the GPU
 constexpr int kErrWord = 1024;       // (WdecParams::cnt u64 index of the error flag)
+constexpr int kSmpCnt = 1152;       // (u64 index: the fused sampler's arrival counters, 8 groups x 128 B, monotonic)
 
 VWA_DEVICE int level_of(int gm) {
   return gm == G_QKV ? LV_QKV : gm == G_XQ ? LV_XQX : gm == G_O || gm == G_XQO ? LV_OXQ : gm == G_XO ? LV_XO
@@ -98,6 +99,9 @@ VWA_DEVICE __amdgpu_buffer_rsrc_t rsrc_of(const void* p, long long bytes) {
 VWA_DEVICE uint4 ld_sc1_b128(__amdgpu_buffer_rsrc_t r, unsigned off) {
   const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
   return make_uint4(v.x, v.y, v.z, v.w);
+}
+VWA_DEVICE void st_sc1_b128(__amdgpu_buffer_rsrc_t r, unsigned off, const uint4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, r, (int)off, 0, 16);
 }
 VWA_DEVICE float ldf_sc1(const float* p) { return __hip_atomic_load(gp(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 VWA_DEVICE void stf_sc1(float* p, float v) { __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
@@ -450,16 +454,44 @@ VWA_DEVICE void wd_cross_attn(const WdecParams& p, int li, int item, char* lds, 
 
 // X staging of a GEMM level: the activation row (bf16, written earlier in this launch or, for layer
 // 0, the embedding) -> LDS; LayerNorm levels also get the row's mean / rstd (from the staged values)
-VWA_DEVICE void wd_stage(const WdecParams& p, int K, const u16* x, char* lds, bool ln) {
+// emb (layer 0 with WdecParams::tok_emb): the row is the step's embedding, built here from the
+// tables (embedding_kernel's arithmetic: f32 sum of the two bf16 rows, one rounding); emb_store:
+// this workgroup also writes it to x (the layer's residual / input row for every later level)
+VWA_DEVICE void wd_stage(const WdecParams& p, int K, const u16* x, char* lds, bool ln, bool emb = false,
+                         bool emb_store = false) {
   const int n8 = K >> 3;
   const int tx = VWA_TX;
   u16* xs = reinterpret_cast<u16*>(lds + L_XS);
   const __amdgpu_buffer_rsrc_t r = rsrc_of(x, (long long)K * 2);
   uint4 v[2];
+  if (emb) {
+    const int id = uni(p.tokens[0]), pos = uni(p.positions[0]);
+    const bool in = id >= 0 && id < p.emb_rows;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int c = tx + i * kT;
-    v[i] = c < n8 ? ld_sc1_b128(r, (unsigned)c * 16u) : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < 2; ++i) {
+      const int c = tx + i * kT;
+      v[i] = make_uint4(0, 0, 0, 0);
+      if (c < n8) {
+        float a[8], b[8];
+        if (in) {
+          unpack8(*reinterpret_cast<const uint4*>(p.tok_emb + (size_t)id * K + c * 8), a);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] = 0.f;
+        }
+        unpack8(*reinterpret_cast<const uint4*>(p.pos_emb + (size_t)pos * K + c * 8), b);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += b[e];
+        v[i] = pack8(a);
+        if (emb_store) st_sc1_b128(r, (unsigned)c * 16u, v[i]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tx + i * kT;
+      v[i] = c < n8 ? ld_sc1_b128(r, (unsigned)c * 16u) : make_uint4(0, 0, 0, 0);
+    }
   }
   float s = 0.f, s2 = 0.f;
 #pragma unroll
@@ -607,8 +639,15 @@ VWA_DEVICE void wd_epilogue(const WdecParams& p, int li, int g0, int g1, int tl0
 
 // LM head epilogue of (<= 2) tiles in one LDS round: thread t < 16 nt finishes column t & 15 of
 // tile t >> 4 (lc / lb: that column's folded-LayerNorm column sum and bias, loaded with the tile)
+VWA_DEVICE void argmax_merge(float& bv, int& bi, float v, int i) {
+  if (v > bv || (v == bv && i < bi)) {  // (sample.hip's order: the lowest id on ties)
+    bv = v;
+    bi = i;
+  }
+}
+
 VWA_DEVICE void wd_lm_epilogue(const WdecParams& p, int tl0, int tl1, int nt, const f32x4& acc0, const f32x4& acc1,
-                               char* lds, float lc, float lb) {
+                               char* lds, float lc, float lb, int mk, float& bv, int& bi) {
   float* red = reinterpret_cast<float*>(lds + L_RED);
   const float* st = reinterpret_cast<const float*>(lds + L_STAT);
   const int tx = VWA_TX, lane = tx & 63, w = tx >> 6;
@@ -621,7 +660,10 @@ VWA_DEVICE void wd_lm_epilogue(const WdecParams& p, int tl0, int tl1, int nt, co
     float v = 0.f;
 #pragma unroll
     for (int ww = 0; ww < 8; ++ww) v += red[ww * 32 + tx];
-    p.logits[(tx < 16 ? tl0 : tl1) * 16 + (tx & 15)] = (v - st[0] * lc) * st[1] + lb;
+    const int n = (tx < 16 ? tl0 : tl1) * 16 + (tx & 15);
+    const float lg = (v - st[0] * lc) * st[1] + lb;
+    p.logits[n] = lg;
+    if (mk) argmax_merge(bv, bi, lg, n);
   }
   lds_sync();  // (red is rewritten by the next round)
 }
@@ -665,6 +707,13 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
               ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) << 32);
   }
   lds_sync();
+  // (the fused sampler's arrival counters: base of this launch, read by workgroup 0's wave 0 --
+  // before any workgroup can arrive there, which needs every level, workgroup 0's included)
+  unsigned long long smp_base = 0;
+  if (p.smp_mask && blockIdx.x == 0 && VWA_TX < 64) {
+    const unsigned long long inc = (unsigned long long)gridDim.x;
+    smp_base = cnt_sum8(p.cnt + kSmpCnt) / inc * inc;
+  }
   // the level's counter target after layer pli
   auto target = [&](int l, int pli) { return base[l] + (unsigned long long)p.n_prod[l] * (unsigned long long)(pli + 1); };
   uint4 wr[kSlots][kLps];
@@ -743,9 +792,15 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
         const bool resid = lvl == LV_OXQ || lvl == LV_XO || lvl == LV_FC2;
         if (resid && VWA_TX < 16 * nt)  // (in the same round trip as the row)
           er = bf2f(ldh_sc1(xres + (VWA_TX < 16 ? tl[0] : tl[1]) * 16 + (VWA_TX & 15)));
-        if (lvl == LV_XO) wd_stage_merge(p, lds);
-        else if (!(lvl == LV_XQX && (work & 1)))  // (after the QKV level the row is staged already)
-          wd_stage(p, k_of(p, lvl == LV_FC2 ? G_FC2 : G_O), xin, lds, lvl == LV_QKV || lvl == LV_FC1);
+        if (lvl == LV_XO) {
+          wd_stage_merge(p, lds);
+        } else if (!(lvl == LV_XQX && (work & 1))) {  // (after the QKV level the row is staged already)
+          // layer 0 with the tables: the QKV / cross-query-x levels build the embedding row
+          // themselves; the workgroup of QKV tile 0 stores it for the residual reads
+          const bool emb = p.tok_emb && li == 0 && (lvl == LV_QKV || lvl == LV_XQX);
+          wd_stage(p, k_of(p, lvl == LV_FC2 ? G_FC2 : G_O), xin, lds, lvl == LV_QKV || lvl == LV_FC1, emb,
+                   emb && lvl == LV_QKV && kind[0] == G_QKV && tile[0] == 0);
+        }
         wd_stamp(p, li, lvl, 2);
         if (opt & kOptNoEpiPre) epi_ops();
         f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
@@ -784,13 +839,18 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
     const int ntw = b0 < NTv ? (NTv - 1 - b0) / G + 1 : 0;
     const int tx = VWA_TX, q = tx & 15;
     float lc[kSlots], lb[kSlots];  // (threads < 32: column q of the slot's tile)
+    int mk[kSlots];                 // (its sampler mask bit)
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
     auto issue = [&](int s, int j) {
       if (j < ntw) {
         const int t = b0 + j * G;
         wd_load_w(p.lm_W, p.n_vocab, p.d, t, wr[s]);
         if (tx < 32) {
-          lc[s] = gld(p.lm_c + t * 16 + q);
-          lb[s] = p.lm_b ? bf2f(gld(p.lm_b + t * 16 + q)) : 0.f;
+          const int n = t * 16 + q;
+          lc[s] = gld(p.lm_c + n);
+          lb[s] = p.lm_b ? bf2f(gld(p.lm_b + n)) : 0.f;
+          mk[s] = p.smp_mask ? (int)((gld(p.smp_mask + (n >> 5)) >> (n & 31)) & 1u) : 0;
         }
       }
     };
@@ -807,16 +867,71 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
         f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
         wd_mma(lds, 0, wr[s], acc0);
         const float c0 = lc[s], bb0 = lb[s];
+        const int m0 = mk[s];
         float c1 = 0.f, bb1 = 0.f;
+        int m1 = 0;
         if (s + 1 < kSlots) {
           if (two) wd_mma(lds, 0, wr[s + 1], acc1);
           c1 = lc[s + 1];
           bb1 = lb[s + 1];
+          m1 = mk[s + 1];
         }
         issue(s, ja + kSlots);  // (the slot's registers are free once its MFMAs were issued)
         if (s + 1 < kSlots && two) issue(s + 1, jb + kSlots);
         wd_lm_epilogue(p, b0 + ja * G, b0 + jb * G, two ? 2 : 1, acc0, acc1, lds, tx < 16 ? c0 : c1,
-                       tx < 16 ? bb0 : bb1);
+                       tx < 16 ? bb0 : bb1, tx < 16 ? m0 : m1, bv, bi);
+      }
+    }
+    if (p.smp_mask) {
+      // greedy sample: the workgroup's best (wave 0, lanes < 32 hold columns) -> a partial; the
+      // last workgroup to arrive merges the grid's partials and advances the device loop
+      if (tx < 64) {
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) {
+          const float ov = __shfl_xor(bv, m, 64);
+          const int oi = __shfl_xor(bi, m, 64);
+          argmax_merge(bv, bi, ov, oi);
+        }
+      }
+      // (arrival as the levels do it: no-return adds spread over 8 group counters, workgroup 0
+      // polls their sum -- one returning ticket on one word from 256 workgroups measured ~15 us)
+      if (tx == 0) {
+        stf_sc1(p.smp_part + 2 * b0, bv);
+        stf_sc1(p.smp_part + 2 * b0 + 1, __int_as_float(bi));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(gp(p.cnt + kSmpCnt + 16 * (b0 & 7)), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (b0 == 0 && tx < 64) {
+        int spins = 0;
+        while ((long long)(cnt_sum8(p.cnt + kSmpCnt) - (smp_base + (unsigned long long)G)) < 0) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > kSpinLimit) {
+            if (tx == 0) set_err(p);
+            break;
+          }
+        }
+        float v = -INFINITY;
+        int ix = 0x7fffffff;
+        for (int k = tx; k < G; k += 64) argmax_merge(v, ix, ldf_sc1(p.smp_part + 2 * k), __float_as_int(ldf_sc1(p.smp_part + 2 * k + 1)));
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) {
+          const float ov = __shfl_xor(v, m, 64);
+          const int oi = __shfl_xor(ix, m, 64);
+          argmax_merge(v, ix, ov, oi);
+        }
+        if (tx == 0) {  // (decode_advance_kernel's arithmetic)
+          const int tok = v == -INFINITY ? -1 : ix;
+          p.smp_tok[0] = tok;
+          p.smp_step[0] += 1;
+          const int c = p.loop_cnt[0];
+          if (c < p.loop_max) p.loop_out[c] = tok;
+          p.loop_cnt[0] = c + 1;
+          p.adv_tokens[0] = tok;
+          const int pos = p.adv_positions[0] + 1;
+          p.adv_positions[0] = pos;
+          p.adv_ctx[0] = pos + 1;
+          p.adv_slots[0] = (int64_t)(p.loop_base_block + pos / p.block_size) * p.block_size + pos % p.block_size;
+        }
       }
     }
   }

@@ -500,6 +500,33 @@ def test_whisper_persistent_decoder_matches_per_kernel_path(graphs, monkeypatch)
         assert err < 0.02 * (1 + b.abs().max().item()), (i, err)
 
 
+def test_whisper_persistent_device_loop_is_one_launch_and_matches(monkeypatch):
+    """The device-resident greedy loop (asr/engine.py) with the persistent decoder: each step is ONE
+    launch (embedding from the tables, every layer, LM head, masked argmax, advance) and gives the
+    per-kernel loop's tokens; 4 decoder layers, two utterances decoded back to back."""
+    import dataclasses
+
+    from voice_enabled_browser_automation_amd.asr.engine import AsrEngine
+    from voice_enabled_browser_automation_amd.tokenizer import load_tokenizer
+
+    ops.ext()
+    cfg = dataclasses.replace(get_config("whisper-large-v3"), n_enc_layers=1, n_dec_layers=4)
+    m = WhisperModel(cfg, device="cuda", seed=11)
+    torch.manual_seed(12)
+    audios = [torch.randn(16000 * 3, device="cuda") * 0.1 for _ in range(2)]
+    outs = {}
+    for persist in ("0", "1"):
+        monkeypatch.setenv("VWA_ASR_PERSIST", persist)
+        eng = AsrEngine(m, load_tokenizer("whisper"), max_sessions=2)
+        outs[persist] = [eng.decode_many([a], exact_tokens=24)[0] for a in audios]
+        if persist == "1":
+            assert m._wdec and not m.chain_error()
+            # the loop graph of one step holds a single kernel launch
+            st = next(iter(m._wdec.values()))
+            assert "smp_part" in st
+    assert outs["1"] == outs["0"], (outs["0"], outs["1"])
+
+
 def test_wdec_counters_survive_launch_sequences(monkeypatch):
     """Counter bases across many launches of the persistent decoder (monotonic counters, no reset):
     200 steps in a row keep matching the per-kernel path at the end."""

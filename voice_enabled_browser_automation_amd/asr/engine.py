@@ -200,6 +200,12 @@ class AsrEngine:
     def _loop_step(self, slot: int, allow_eot: bool) -> None:
         r = self.runner
         b = r.b
+        # whisper-large persistent decoder: embedding, layers, LM head, argmax and advance are ONE
+        # launch (models/whisper.py wdec_loop_step)
+        if self.model.wdec_loop_step(
+                b, self.mask_text_eot if allow_eot else self.mask_text, self.d_tok, self.d_step, self.loop_out,
+                self.loop_cnt, 1 + slot * r.bps):
+            return
         logits = r._fwd(1)
         self._advance(logits, slot, allow_eot)
 

@@ -541,21 +541,45 @@ class WhisperModel:
         st = next(iter(getattr(self, "_wdec", {}).values()), None) if getattr(self, "_wdec", None) else None
         return None if st is None else st["cnt"].view(torch.int64)[1024:1025]
 
-    def _wdec_step(self, bufs) -> torch.Tensor:
-        """Every decoder layer of a one-row step (the embedding is in bufs.hidden[0]) and the LM
-        head (folded final LayerNorm) in the same launch; returns the f32 logits row [1, V]."""
+    def _wdec_emb_ok(self, bufs) -> bool:
+        """The launch builds the step's embedding row itself (layer 0): the position table covers
+        every KV position of a session."""
+        return self.pos_emb.shape[0] >= bufs.block_table.shape[1] * bufs.k_cache.shape[3]
+
+    def _wdec_step(self, bufs, smp: Optional[list] = None, base_block: int = 0) -> torch.Tensor:
+        """Every decoder layer of a one-row step and the LM head (folded final LayerNorm) in ONE
+        launch -- with the embedding of bufs.tokens[0] / bufs.positions[0] built by layer 0
+        (_wdec_emb_ok; else it must be in bufs.hidden[0]) and, with ``smp`` (the device loop,
+        asr/engine.py), the greedy masked argmax + the loop advance as its last step.  Returns the
+        f32 logits row [1, V]."""
         st = self._wdec_state(bufs)
         w, b, c = self.f_lm
         wt = w.t if isinstance(w, ops.TiledWeight) else w
         lm = [wt, b if b is not None else st.setdefault("no_bias", torch.empty(0, dtype=torch.bfloat16,
                                                                                   device=self.device)),
               c, bufs.logits[0]]
+        emb = [self.tok_emb, self.pos_emb, bufs.tokens, bufs.positions] if self._wdec_emb_ok(bufs) else None
         ops.ext().wdec_run(st["layers"], st["roles"],
                            [bufs.hidden, bufs.h, bufs.q, bufs.att, bufs.f, st["xpart"], bufs.seq_ids, bufs.ctx_lens,
                             bufs.slots, bufs.block_table, bufs.cross_table, st["cnt"]],
                            st["ints"], self.cfg.ln_eps, self.hd ** -0.5, st["n_prod"], st.get("ts"),
-                           int(st.get("opt", 0)), lm)
+                           int(st.get("opt", 0)), lm, emb, smp, base_block)
         return bufs.logits[:1]
+
+    def wdec_loop_step(self, bufs, mask: torch.Tensor, tok: torch.Tensor, step: torch.Tensor, out: torch.Tensor,
+                       cnt: torch.Tensor, base_block: int) -> bool:
+        """One device-loop decode step (asr/engine.py _loop_step) as ONE launch: layers, LM head,
+        greedy masked argmax, advance.  False when the persistent decoder does not take this step
+        (the caller runs the separate launches)."""
+        if not (self._wdec_ok(1) and self._wdec_emb_ok(bufs)):
+            return False
+        st = self._wdec_state(bufs)
+        part = st.get("smp_part")
+        if part is None:
+            part = st["smp_part"] = torch.zeros(2 * st["ints"][10], dtype=torch.float32, device=self.device)
+        self._wdec_step(bufs, [mask.view(torch.int32).reshape(-1), tok, step, part, out, cnt, bufs.tokens,
+                               bufs.positions, bufs.ctx_lens, bufs.slots], base_block)
+        return True
 
     def decode_step(self, bufs, M: int) -> torch.Tensor:
         """M token rows (bufs: tokens/positions/slots/seq_ids/ctx_lens + self cache + cross K/V).
@@ -566,10 +590,13 @@ class WhisperModel:
         cfg = self.cfg
         d = cfg.d_model
         x = bufs.hidden[:M]
-        ops.embedding(bufs.tokens, self.tok_emb, pos_table=self.pos_emb, positions=bufs.positions, out=x, rows=M)
         eps = cfg.ln_eps
-        if self._wdec_ok(M):
-            return self._wdec_step(bufs)  # (the LM head is the launch's last level)
+        if self._wdec_ok(M):  # (embedding, every layer and the LM head in one launch)
+            if not self._wdec_emb_ok(bufs):
+                ops.embedding(bufs.tokens, self.tok_emb, pos_table=self.pos_emb, positions=bufs.positions, out=x,
+                              rows=M)
+            return self._wdec_step(bufs)
+        ops.embedding(bufs.tokens, self.tok_emb, pos_table=self.pos_emb, positions=bufs.positions, out=x, rows=M)
         chain = self._chain_ok(M)
         qkv_done = False
         for li, L in enumerate(self.dec):
