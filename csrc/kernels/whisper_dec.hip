@@ -1,5 +1,5 @@
-// Persistent Whisper decoder step (whisper-large family: d = 1280, ffn = 4 d, head_dim 64), one
-// row: ONE launch for every decoder layer.
+// Persistent Whisper decoder step (any Whisper width: d a multiple of 128 up to 1536, ffn = 4 d,
+// head_dim 64 -- tiny 384 .. large 1280), one row: ONE launch for every decoder layer.
 //
 // Why: the per-kernel decoder runs eight dependent launches per
 // layer, each ~5-9 us of fixed latency (dispatch, X staging, the first weight bytes, reduce,
@@ -38,7 +38,8 @@
 
 // Weight slots: 5 slots x 5 loads of 1 KB per wave (100 VGPRs).  A 16-column tile of a K = 1280
 // projection is 40 load-slices (k-group, 32-k slice) of the pre-tiled layout; wave w takes slices
-// w, w + 8, ... -- 5 per wave = one slot.  An fc2 tile (K = 5120) is 20 per wave = slots 1..4.
+// w, w + 8, ... -- 5 per wave = one slot (narrower models: K / 32 < 40 slices, the rest of the slot
+// reads nothing).  An fc2 tile (K = 4 d) is ceil(d / 320) slots: 4 for large, 2 for tiny.
 // The role table (models/whisper.py wdec_roles) gives each workgroup its slots (level, tile, part,
 // refill level), its self-attention head and its cross-attention item.
 #include "common.h"
@@ -187,13 +188,15 @@ VWA_DEVICE void wd_load(const WdecParams& p, int li, int gm, int tile, int part,
 #pragma unroll
   for (int j = 0; j < kLps; ++j) {
     const int sl = w + 8 * (part * kLps + j), kg = sl >> 2, s4 = sl & 3;
-    const unsigned off = ((unsigned)(tile * G + kg) * 4u + (unsigned)s4) * 1024u + (unsigned)lane * 16u;
+    // (slices past the tile's 4 K / 128: out of the buffer -> zeros, no traffic; d < 1280)
+    const unsigned off = sl < 4 * G ? ((unsigned)(tile * G + kg) * 4u + (unsigned)s4) * 1024u + (unsigned)lane * 16u
+                                    : 0x7FFFFFF0u;
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
     wr[j] = make_uint4(v.x, v.y, v.z, v.w);
   }
 }
 
-// slot load of a tile of an explicit K = d weight (the LM head): all 40 slices, 5 per wave
+// slot load of a tile of an explicit K = d weight (the LM head): all 4 d / 128 <= 40 slices, 5 per wave
 VWA_DEVICE void wd_load_w(const u16* W, int n_cols, int K, int tile, uint4 (&wr)[kLps]) {
   const int G = K >> 7;
   const __amdgpu_buffer_rsrc_t r = rsrc_of(W, (long long)n_cols * K * 2);
@@ -201,21 +204,23 @@ VWA_DEVICE void wd_load_w(const u16* W, int n_cols, int K, int tile, uint4 (&wr)
 #pragma unroll
   for (int j = 0; j < kLps; ++j) {
     const int sl = w + 8 * j, kg = sl >> 2, s4 = sl & 3;
-    const unsigned off = ((unsigned)(tile * G + kg) * 4u + (unsigned)s4) * 1024u + (unsigned)lane * 16u;
+    const unsigned off = sl < 4 * G ? ((unsigned)(tile * G + kg) * 4u + (unsigned)s4) * 1024u + (unsigned)lane * 16u
+                                    : 0x7FFFFFF0u;
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
     wr[j] = make_uint4(v.x, v.y, v.z, v.w);
   }
 }
 
 // the MFMAs of one slot: acc (row 0 = lanes 0..15, element 0) += X . W over the slot's slices
-VWA_DEVICE void wd_mma(const char* lds, int part, const uint4 (&wr)[kLps], f32x4& acc) {
+// (nsl: the tile's slices, 4 K / 128 -- the row past K is not read)
+VWA_DEVICE void wd_mma(const char* lds, int part, const uint4 (&wr)[kLps], f32x4& acc, int nsl) {
   const int tx = VWA_TX, lane = tx & 63, w = tx >> 6, nl = lane & 15, g = lane >> 4;
   const u16* xs = reinterpret_cast<const u16*>(lds + L_XS);
 #pragma unroll
   for (int j = 0; j < kLps; ++j) {
     const int sl = w + 8 * (part * kLps + j), kg = sl >> 2, s4 = sl & 3;
     uint4 a = make_uint4(0, 0, 0, 0);
-    if (nl == 0) a = *reinterpret_cast<const uint4*>(xs + kg * 128 + 32 * g + 8 * s4);
+    if (nl == 0 && sl < nsl) a = *reinterpret_cast<const uint4*>(xs + kg * 128 + 32 * g + 8 * s4);
     acc = mfma16(as_bf16x8(a), as_bf16x8(wr[j]), acc);
   }
 }
@@ -808,8 +813,9 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
 #pragma unroll
         for (int s = 0; s < kSlots; ++s) {
           if (klv[s] != lvl) continue;
-          if (j == 0) wd_mma(lds, part[s], wr[s], acc0);
-          else wd_mma(lds, part[s], wr[s], acc1);
+          const int nsl = k_of(p, kind[s]) >> 5;
+          if (j == 0) wd_mma(lds, part[s], wr[s], acc0, nsl);
+          else wd_mma(lds, part[s], wr[s], acc1, nsl);
           const bool last = s == kSlots - 1 || kind[s + 1] != kind[s] || tile[s + 1] != tile[s];
           if (last) ++j;
         }
@@ -865,13 +871,13 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
         if (ja >= ntw) break;  // (uniform)
         const bool two = s + 1 < kSlots && jb < ntw;
         f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-        wd_mma(lds, 0, wr[s], acc0);
+        wd_mma(lds, 0, wr[s], acc0, p.d >> 5);
         const float c0 = lc[s], bb0 = lb[s];
         const int m0 = mk[s];
         float c1 = 0.f, bb1 = 0.f;
         int m1 = 0;
         if (s + 1 < kSlots) {
-          if (two) wd_mma(lds, 0, wr[s + 1], acc1);
+          if (two) wd_mma(lds, 0, wr[s + 1], acc1, p.d >> 5);
           c1 = lc[s + 1];
           bb1 = lb[s + 1];
           m1 = mk[s + 1];
@@ -941,8 +947,10 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
 }  // namespace
 
 extern "C" int vwa_wdec_launch(const WdecParams* p, int grid, hipStream_t st) {
-  if (p->d != 1280 || p->ffn != 4 * p->d || p->H * 64 != p->d || p->n_layers < 2 || p->ch_len > kMaxChunk ||
-      p->ch_len * p->nch < p->T || p->nch > 4 || p->d > 3 * kT || grid < 1)
+  // (whisper tiny .. large: d a multiple of 128 up to 1536 -- the merge stages <= 3 columns per
+  // thread, a tile <= 40 slices of the K = d slots; ffn = 4 d staged by <= 2 x 16 B per thread)
+  if (p->d % 128 != 0 || p->d > 3 * kT || p->ffn != 4 * p->d || p->ffn > 2 * kT * 8 || p->H * 64 != p->d ||
+      p->n_layers < 2 || p->ch_len > kMaxChunk || p->ch_len * p->nch < p->T || p->nch > 4 || grid < 1)
     return -10;
   hipLaunchKernelGGL(wdec_kernel, dim3(grid), dim3(kT), kLds, st, *p);
   return (int)hipGetLastError();

@@ -460,8 +460,9 @@ def test_whisper_chained_decoder_matches_per_kernel_path(name, monkeypatch):
         assert err < 0.02 * (1 + b.abs().max().item()), err
 
 
-@pytest.mark.parametrize("graphs", [False, True])
-def test_whisper_persistent_decoder_matches_per_kernel_path(graphs, monkeypatch):
+@pytest.mark.parametrize("graphs,model", [(False, "whisper-large-v3"), (True, "whisper-large-v3"),
+                                          (True, "whisper-tiny")])
+def test_whisper_persistent_decoder_matches_per_kernel_path(graphs, model, monkeypatch):
     """The persistent whisper-large decoder step (whisper_dec.hip: every layer in ONE launch,
     weights a layer ahead in registers, counter hand-offs) against the per-kernel path on the same
     weights, caches and cross K/V: one row per step, two sessions, contexts up to 70 keys (several
@@ -471,9 +472,9 @@ def test_whisper_persistent_decoder_matches_per_kernel_path(graphs, monkeypatch)
     from voice_enabled_browser_automation_amd.asr.engine import WhisperRunner
 
     ops.ext()
-    cfg = dataclasses.replace(get_config("whisper-large-v3"), n_enc_layers=1, n_dec_layers=4)
+    cfg = dataclasses.replace(get_config(model), n_enc_layers=1, n_dec_layers=4)
     m = WhisperModel(cfg, device="cuda", seed=3)
-    assert m.dec_tiled
+    assert m.dec_tiled == (model == "whisper-large-v3")  # (tiny: the kernel gets tiled copies)
     torch.manual_seed(4)
     enc = [torch.randn(1, cfg.n_audio_ctx, cfg.d_model, device="cuda").to(torch.bfloat16) for _ in range(2)]
     runners = []
@@ -500,7 +501,8 @@ def test_whisper_persistent_decoder_matches_per_kernel_path(graphs, monkeypatch)
         assert err < 0.02 * (1 + b.abs().max().item()), (i, err)
 
 
-def test_whisper_persistent_device_loop_is_one_launch_and_matches(monkeypatch):
+@pytest.mark.parametrize("model", ["whisper-large-v3", "whisper-tiny"])
+def test_whisper_persistent_device_loop_is_one_launch_and_matches(model, monkeypatch):
     """The device-resident greedy loop (asr/engine.py) with the persistent decoder: each step is ONE
     launch (embedding from the tables, every layer, LM head, masked argmax, advance) and gives the
     per-kernel loop's tokens; 4 decoder layers, two utterances decoded back to back."""
@@ -510,7 +512,7 @@ def test_whisper_persistent_device_loop_is_one_launch_and_matches(monkeypatch):
     from voice_enabled_browser_automation_amd.tokenizer import load_tokenizer
 
     ops.ext()
-    cfg = dataclasses.replace(get_config("whisper-large-v3"), n_enc_layers=1, n_dec_layers=4)
+    cfg = dataclasses.replace(get_config(model), n_enc_layers=1, n_dec_layers=4)
     m = WhisperModel(cfg, device="cuda", seed=11)
     torch.manual_seed(12)
     audios = [torch.randn(16000 * 3, device="cuda") * 0.1 for _ in range(2)]

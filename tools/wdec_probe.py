@@ -32,7 +32,8 @@ from voice_enabled_browser_automation_amd.models.whisper import WDEC_LEVELS, Whi
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--asr", default="whisper-large-v3")
+    ap.add_argument("--layers", type=int, default=None)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--opt", type=int, default=0)
     ap.add_argument("--json", default=None)
@@ -44,7 +45,9 @@ def main():
     for kv in filter(None, a.role_opts.split(",")):
         k, v = kv.split("=")
         W.WDEC_ROLE_OPTS[k] = float(v) if k != "sat" else v
-    cfg = dataclasses.replace(get_config("whisper-large-v3"), n_enc_layers=1, n_dec_layers=a.layers)
+    base = get_config(a.asr)
+    a.layers = a.layers or base.n_dec_layers
+    cfg = dataclasses.replace(base, n_enc_layers=1, n_dec_layers=a.layers)
     m = WhisperModel(cfg, device="cuda", seed=0, tile_decoder=True)
     torch.manual_seed(0)
     enc = torch.randn(1, cfg.n_audio_ctx, cfg.d_model, device="cuda").to(torch.bfloat16)
@@ -103,7 +106,7 @@ def main():
                     res[name]["body"].append(float((dn - rel).median()))
                 if not off:
                     done_prev = float(dn.max())
-    out = dict(tool="wdec_probe", layers=L, opt=a.opt, role_opts=a.role_opts, grid=grid, step_us=round(step_us, 1),
+    out = dict(tool="wdec_probe", asr=a.asr, layers=L, opt=a.opt, role_opts=a.role_opts, grid=grid, step_us=round(step_us, 1),
                per_layer_us=round(step_us / L, 2), error=bool(err))
     for name, d in res.items():
         out[name] = {k: round(statistics.median(v), 2) for k, v in d.items() if v}

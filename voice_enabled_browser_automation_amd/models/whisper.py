@@ -46,7 +46,8 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
     prefetched, and the mask of levels it completes -- plus the producer count of each level.
 
     Every layer's weights are spread so each workgroup holds at most 5 slots of 5 loads per wave
-    (one 16-column tile of a K = d projection per slot; an fc2 tile, K = 4 d, takes slots 1..4):
+    (one 16-column tile of a K = d projection per slot; an fc2 tile, K = 4 d, takes slots 1..P,
+    P = ceil(d / 320): 4 for whisper-large, 2 for tiny):
     fc2 tiles on workgroups [0, d/16), QKV tiles on the last 3 d / 16, the out / cross projections
     and fc1 in the free slots of the rest (at most 2 tiles of a level per workgroup: the epilogue
     finishes 2 in one round), the x part of the cross query last -- on QKV workgroups, which have
@@ -57,8 +58,9 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
     levels after it."""
     import numpy as np
 
-    assert ffn == 4 * d and d % 256 == 0
+    assert ffn == 4 * d and d % 128 == 0 and d <= 1536
     n_qkv, n_d, n_ff = 3 * d // 16, d // 16, ffn // 16
+    n_p2 = -(-(ffn // 32) // 40)  # slots per fc2 tile (40 slices of 32 k each)
     n_x = H * nch
     if nwg < max(n_qkv, n_d + 16, n_x, H) or n_d > nwg:
         raise ValueError(f"wdec_roles: {nwg} workgroups cannot hold the decoder's tiles")
@@ -68,8 +70,8 @@ def wdec_roles(nwg: int, d: int, H: int, ffn: int, nch: int):
     GQ, GO, GXQ, GXO, G1, G2, GXQO = range(7)
     LQ, LXQX, LS, LOXQ, LX = 0, 1, 2, 3, 4
     lvl_of = WDEC_GEMM_LEVEL
-    for t in range(n_d):  # fc2: slots 1..4 of workgroup t
-        kind[t, 1:5], tile[t, 1:5], part[t, 1:5] = G2, t, np.arange(4)
+    for t in range(n_d):  # fc2: slots 1..n_p2 of workgroup t
+        kind[t, 1:1 + n_p2], tile[t, 1:1 + n_p2], part[t, 1:1 + n_p2] = G2, t, np.arange(n_p2)
     q0 = nwg - n_qkv
     for t in range(n_qkv):
         kind[q0 + t, 0], tile[q0 + t, 0] = GQ, t
@@ -485,11 +487,11 @@ class WhisperModel:
         return cache[key]
 
     # ---- persistent decoder (csrc/kernels/whisper_dec.hip wdec_kernel): a one-row step of the
-    # whisper-large family (d 1280, ffn 5120, head_dim 64, pre-tiled decoder weights) as ONE launch
+    # Whisper model (tiny .. large: d a multiple of 128 up to 1536, ffn 4 d, head_dim 64) as ONE launch
     # over every decoder layer; each workgroup's weight tiles stay in its registers a layer ahead.
     def _wdec_ok(self, M: int) -> bool:
         cfg = self.cfg
-        return (M == 1 and self.device.type == "cuda" and self.dec_tiled and cfg.d_model == 1280
+        return (M == 1 and self.device.type == "cuda" and cfg.d_model % 128 == 0 and cfg.d_model <= 1536
                 and cfg.ffn == 4 * cfg.d_model and self.hd == 64 and cfg.n_dec_layers >= 2
                 and not getattr(self, "_wdec_disabled", False) and ops.env_flag("VWA_ASR_PERSIST")
                 and ops.native_available())
@@ -507,7 +509,16 @@ class WhisperModel:
         grid = int(E.device_cus(bufs.hidden))  # one workgroup per CU, all resident
         nch = 4
         roles, n_prod = wdec_roles(grid, cfg.d_model, self.H, cfg.ffn, nch)
-        wt = lambda t: t.t if isinstance(t, ops.TiledWeight) else t  # noqa: E731
+        # the kernel reads pre-tiled weights: a model whose decoder stays row-major (small models:
+        # _tile_decoder only above 256 MB) gets tiled copies for it here, kept alive in the state
+        keep = []
+
+        def wt(t):
+            if isinstance(t, ops.TiledWeight):
+                return t.t
+            keep.append(ops.tile_weight(t))
+            return keep[-1]
+
         flat = []
         for li, L in enumerate(self.dec):
             (wq, bq, cq), (wx, bx, cx), (w1, b1, c1) = L.f_qkv, L.f_xq, L.f_fc1
@@ -519,7 +530,9 @@ class WhisperModel:
         cnt = E.alloc_uncached_i32(4096, bufs.hidden)  # level counters [8][8] x 128 B + error word
         xpart = torch.zeros(self.H * nch * 66 + 3 * cfg.d_model, dtype=torch.float32, device=self.device)
         T = bufs.cross[0][0].shape[1]
+        w_lm = wt(self.f_lm[0])
         st = dict(layers=layers, roles=torch.from_numpy(roles).to(self.device), n_prod=n_prod, cnt=cnt, xpart=xpart,
+                  keep=keep, lm_w=w_lm,
                   ints=[len(self.dec), cfg.d_model, self.H, cfg.ffn, T, bufs.k_cache.shape[3],
                         bufs.block_table.shape[1], nch, -(-T // nch), bufs.cross[0][0].shape[0], grid])
         self._wdec[bufs] = st
@@ -553,9 +566,8 @@ class WhisperModel:
         asr/engine.py), the greedy masked argmax + the loop advance as its last step.  Returns the
         f32 logits row [1, V]."""
         st = self._wdec_state(bufs)
-        w, b, c = self.f_lm
-        wt = w.t if isinstance(w, ops.TiledWeight) else w
-        lm = [wt, b if b is not None else st.setdefault("no_bias", torch.empty(0, dtype=torch.bfloat16,
+        _, b, c = self.f_lm
+        lm = [st["lm_w"], b if b is not None else st.setdefault("no_bias", torch.empty(0, dtype=torch.bfloat16,
                                                                                   device=self.device)),
               c, bufs.logits[0]]
         emb = [self.tok_emb, self.pos_emb, bufs.tokens, bufs.positions] if self._wdec_emb_ok(bufs) else None
