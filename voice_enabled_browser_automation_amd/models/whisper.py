@@ -508,7 +508,11 @@ class WhisperModel:
         E = ops.ext()
         grid = int(E.device_cus(bufs.hidden))  # one workgroup per CU, all resident
         nch = 4
-        roles, n_prod = wdec_roles(grid, cfg.d_model, self.H, cfg.ffn, nch)
+        try:
+            roles, n_prod = wdec_roles(grid, cfg.d_model, self.H, cfg.ffn, nch)
+        except ValueError:  # (a partitioned device with too few CUs for the tiles: per-kernel launches)
+            self._wdec_disabled = True
+            return None
         # the kernel reads pre-tiled weights: a model whose decoder stays row-major (small models:
         # _tile_decoder only above 256 MB) gets tiled copies for it here, kept alive in the state
         keep = []
@@ -583,7 +587,7 @@ class WhisperModel:
         """One device-loop decode step (asr/engine.py _loop_step) as ONE launch: layers, LM head,
         greedy masked argmax, advance.  False when the persistent decoder does not take this step
         (the caller runs the separate launches)."""
-        if not (self._wdec_ok(1) and self._wdec_emb_ok(bufs)):
+        if not (self._wdec_ok(1) and self._wdec_emb_ok(bufs) and self._wdec_state(bufs) is not None):
             return False
         st = self._wdec_state(bufs)
         part = st.get("smp_part")
@@ -603,7 +607,7 @@ class WhisperModel:
         d = cfg.d_model
         x = bufs.hidden[:M]
         eps = cfg.ln_eps
-        if self._wdec_ok(M):  # (embedding, every layer and the LM head in one launch)
+        if self._wdec_ok(M) and self._wdec_state(bufs) is not None:  # (embedding, layers, LM head: one launch)
             if not self._wdec_emb_ok(bufs):
                 ops.embedding(bufs.tokens, self.tok_emb, pos_table=self.pos_emb, positions=bufs.positions, out=x,
                               rows=M)
