@@ -44,7 +44,7 @@ def main():
     from voice_enabled_browser_automation_amd.models import whisper as W
     for kv in filter(None, a.role_opts.split(",")):
         k, v = kv.split("=")
-        W.WDEC_ROLE_OPTS[k] = float(v) if k != "sat" else v
+        W.WDEC_ROLE_OPTS[k] = v if k == "sat" else float(v)
     base = get_config(a.asr)
     a.layers = a.layers or base.n_dec_layers
     cfg = dataclasses.replace(base, n_enc_layers=1, n_dec_layers=a.layers)
