@@ -768,8 +768,8 @@ def test_fp8_chained_layer_is_w8a16(cfg, monkeypatch):
         assert err < 0.02 * (1 + b.abs().max().item()), err
 
 
-@pytest.mark.parametrize("flash,tail_lens", [("1", (40, 33, 27, 85, 60)), ("0", (40, 33, 27, 85, 60)), ("1", (85,))])
-def test_batched_admission_prefill_gpu(flash, tail_lens, monkeypatch):
+@pytest.mark.parametrize("flash", ["1", "0"])
+def test_batched_admission_prefill_gpu(flash, monkeypatch):
     """GPU batched admission prefill (runtime/engine.py prefill_batch, > 64 ragged rows): the
     per-request runs' causal attention as ONE batched flash launch per layer (VWA_PREFILL_FLASH=1,
     the default) or the decode kernel over 64-row slices -- the same K/V, hence the same next-token
@@ -780,7 +780,7 @@ def test_batched_admission_prefill_gpu(flash, tail_lens, monkeypatch):
     torch.manual_seed(0)
     m = LlamaModel(CFG, device="cuda", seed=3)
     head = torch.randint(0, 4096, (200,)).tolist()
-    tails = [torch.randint(0, 4096, (n,)).tolist() for n in tail_lens]  # (85,): one request, B = 1 flash
+    tails = [torch.randint(0, 4096, (n,)).tolist() for n in (40, 33, 27, 85, 60)]
 
     def make():
         e = LLMEngine(m, max_seqs=6, max_model_len=512, kv_blocks=200, block_size=16)
@@ -800,7 +800,7 @@ def test_batched_admission_prefill_gpu(flash, tail_lens, monkeypatch):
     calls = []
     orig = ops.flash_attention_runs
     monkeypatch.setattr(ops, "flash_attention_runs", lambda *a, **k: calls.append(1) or orig(*a, **k))
-    eB.prefill_batch([(s, len(s.tokens)) for s in sB])  # 245 (or 85) suffix rows behind the cached head
+    eB.prefill_batch([(s, len(s.tokens)) for s in sB])  # 245 suffix rows behind the cached head
     assert bool(calls) == (flash == "1")
     got = next_logits(eB, sB)
     for a, b in zip(got, want):

@@ -654,9 +654,7 @@ class LLMEngine:
                 runs[-1][2] += 1
             else:
                 runs.append([sid, i, 1, pos])
-        # (one run too: a single request's prompt suffix behind its cached prefix -- the decode
-        # kernel would read the whole cached context once per 4-row group, 22 times for 85 rows)
-        if not runs or len({r[0] for r in runs}) != len(runs):
+        if len(runs) < 2 or len({r[0] for r in runs}) != len(runs):
             return None
         B, S = len(runs), max(r[2] for r in runs)
         if B * S > 2 * len(sids):  # one long run among short ones: mostly padding queries -- slices
