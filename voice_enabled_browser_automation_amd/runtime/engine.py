@@ -654,6 +654,9 @@ class LLMEngine:
                 runs[-1][2] += 1
             else:
                 runs.append([sid, i, 1, pos])
+        # (one run -- a single request's suffix -- keeps the decode kernel's key-split slices:
+        # the batched flash launch then has 32 workgroups for the whole GPU, 41 vs 35 us per
+        # layer on the headline's 85-row suffix, profiles/r6_prefill_flash_b1_rejected.md)
         if len(runs) < 2 or len({r[0] for r in runs}) != len(runs):
             return None
         B, S = len(runs), max(r[2] for r in runs)
