@@ -932,7 +932,7 @@ void wdec_run(Tensor layers, Tensor roles, std::vector<Tensor> bufs, std::vector
   p.q = bf(2);
   p.att = bf(3);
   p.f = bf(4);
-  TORCH_CHECK(bufs[5].scalar_type() == at::kFloat && bufs[5].numel() >= (int64_t)p.H * p.nch * 66 + 3 * p.d,
+  TORCH_CHECK(bufs[5].scalar_type() == at::kFloat && bufs[5].numel() >= (int64_t)p.H * p.nch * 68 + 3 * p.d,
               "wdec_run: xpart (cross partials + the cross query's two f32 halves + x1 tile sums)");
   p.xpart = bufs[5].data_ptr<float>();
   p.seq_ids = bufs[6].data_ptr<int>();

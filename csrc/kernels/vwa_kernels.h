@@ -224,7 +224,7 @@ struct WdecParams {
   float eps, scale;
   uint16_t* x0; uint16_t* x1;         // hidden row ping-pong (x0: the embedding; result in x[n_layers & 1])
   uint16_t* q; uint16_t* att; uint16_t* f;
-  float* xpart;                       // cross-attention partials [H][nch][2 + 64]
+  float* xpart;                       // cross-attention partials [H][nch][4 + 64] (max, sum, -, -, out)
   const int* seq_ids; const int* ctx_lens; const int64_t* slots; const int* block_table; const int* cross_table;
   unsigned long long* cnt;            // uncached: level counters [8 levels][8 groups] at 128-byte stride, err word at [1024]
   int n_prod[kWdLevels];              // workgroups that complete each level (per layer)

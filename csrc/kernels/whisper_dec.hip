@@ -177,7 +177,9 @@ VWA_DEVICE int n_cols(const WdecParams& p, int gm) {
 VWA_DEVICE int k_of(const WdecParams& p, int gm) { return gm == G_FC2 ? p.ffn : p.d; }
 
 // the cross query's f32 pre-activation halves (x part, att part) behind the cross partials
-VWA_DEVICE float* xq_buf(const WdecParams& p) { return p.xpart + (size_t)p.H * p.nch * 66; }
+// cross-attention partial of (head, chunk): [max, sum, -, -, out[64]] -- 16-byte aligned rows
+constexpr int kPart = 68;
+VWA_DEVICE float* xq_buf(const WdecParams& p) { return p.xpart + (size_t)p.H * p.nch * kPart; }
 
 // slot load: part `part` (5 load-slices per wave) of tile `tile` of gemm gm's weight, layer li
 VWA_DEVICE void wd_load(const WdecParams& p, int li, int gm, int tile, int part, uint4 (&wr)[kLps]) {
@@ -449,8 +451,8 @@ VWA_DEVICE void wd_cross_attn(const WdecParams& p, int li, int item, char* lds, 
   }
   const float o = ((oa[0] + oa[1]) + (oa[2] + oa[3])) + ((oa[4] + oa[5]) + (oa[6] + oa[7]));
   const float tot = wd_ow_sum(lds, o);
-  float* part = p.xpart + (size_t)(h * p.nch + ch) * 66;
-  if (tx < 64) stf_sc1(part + 2 + tx, tot);
+  float* part = p.xpart + (size_t)(h * p.nch + ch) * kPart;
+  if (tx < 64) stf_sc1(part + 4 + tx, tot);
   if (tx == 0) {
     stf_sc1(part, ml.x);
     stf_sc1(part + 1, ml.y);
@@ -539,42 +541,44 @@ VWA_DEVICE void wd_stage(const WdecParams& p, int K, const u16* x, char* lds, bo
 }
 
 // X staging of the cross out-projection: the attention row merged from the (head, chunk)
-// partials (chunk order fixed: the same bits whoever finished last); every partial load of the
-// thread's columns issued before any is used
+// partials (chunk order fixed: the same bits whoever finished last).  A thread merges 4
+// consecutive columns of one head: per chunk one 8-byte (max, sum) and one 16-byte output load,
+// all issued before any is used (was 12 scalar loads per column, 3 columns per thread)
 VWA_DEVICE void wd_stage_merge(const WdecParams& p, char* lds) {
   u16* xs = reinterpret_cast<u16*>(lds + L_XS);
   const int tx = VWA_TX, nch = p.nch;
-  constexpr int kC = 3;  // columns per thread (d <= 1536 with 512 threads)
-  float m[kC][4], l[kC][4], o[kC][4];
+  const int c0 = 4 * min(tx, (p.d >> 2) - 1), h = c0 >> 6, dd = c0 & 63;
+  const __amdgpu_buffer_rsrc_t r = rsrc_of(p.xpart, (long long)p.H * nch * kPart * 4);
+  u32x2 ml[4];
+  u32x4 ov[4];
 #pragma unroll
-  for (int i = 0; i < kC; ++i) {
-    const int c = min(tx + i * kT, p.d - 1), h = c >> 6, dd = c & 63;
-    const float* base = p.xpart + (size_t)h * nch * 66;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int kk = min(k, nch - 1);
-      m[i][k] = ldf_sc1(base + kk * 66);
-      l[i][k] = ldf_sc1(base + kk * 66 + 1);
-      o[i][k] = ldf_sc1(base + kk * 66 + 2 + dd);
-    }
+  for (int k = 0; k < 4; ++k) {
+    const int kk = min(k, nch - 1);
+    const unsigned base = (unsigned)((h * nch + kk) * kPart) * 4u;
+    ml[k] = __builtin_amdgcn_raw_buffer_load_b64(r, (int)base, 0, 16);
+    ov[k] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(base + 16u + (unsigned)dd * 4u), 0, 16);
   }
-#pragma unroll
-  for (int i = 0; i < kC; ++i) {
-    const int c = tx + i * kT;
-    if (c >= p.d) continue;
-    float mx = m[i][0];
+  if (tx < (p.d >> 2)) {
+    float mx = __uint_as_float(ml[0].x);
 #pragma unroll
     for (int k = 1; k < 4; ++k)
-      if (k < nch) mx = fmaxf(mx, m[i][k]);
-    float num = 0.f, den = 0.f;
+      if (k < nch) mx = fmaxf(mx, __uint_as_float(ml[k].x));
+    float num[4] = {0.f, 0.f, 0.f, 0.f}, den = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (k < nch) {
-        const float e = __expf(m[i][k] - mx);
-        num += e * o[i][k];
-        den += e * l[i][k];
+        const float e = __expf(__uint_as_float(ml[k].x) - mx);
+        den += e * __uint_as_float(ml[k].y);
+        num[0] += e * __uint_as_float(ov[k].x);
+        num[1] += e * __uint_as_float(ov[k].y);
+        num[2] += e * __uint_as_float(ov[k].z);
+        num[3] += e * __uint_as_float(ov[k].w);
       }
-    xs[c] = f2bf(num / den);
+    const float inv = 1.f / den;
+    uint2 pk;
+    pk.x = (unsigned)f2bf(num[0] * inv) | ((unsigned)f2bf(num[1] * inv) << 16);
+    pk.y = (unsigned)f2bf(num[2] * inv) | ((unsigned)f2bf(num[3] * inv) << 16);
+    *reinterpret_cast<uint2*>(xs + c0) = pk;
   }
   lds_sync();
 }

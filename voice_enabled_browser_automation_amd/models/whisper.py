@@ -534,7 +534,7 @@ class WhisperModel:
                      bufs.k_cache[li], bufs.v_cache[li], bufs.cross[li][0], bufs.cross[li][1]]
         layers = E.wdec_layers(flat, len(self.dec), bufs.hidden)
         cnt = E.alloc_uncached_i32(4096, bufs.hidden)  # level counters [8][8] x 128 B + error word
-        xpart = torch.zeros(self.H * nch * 66 + 3 * cfg.d_model, dtype=torch.float32, device=self.device)
+        xpart = torch.zeros(self.H * nch * 68 + 3 * cfg.d_model, dtype=torch.float32, device=self.device)
         T = bufs.cross[0][0].shape[1]
         w_lm = wt(self.f_lm[0])
         st = dict(layers=layers, roles=torch.from_numpy(roles).to(self.device), n_prod=n_prod, cnt=cnt, xpart=xpart,
