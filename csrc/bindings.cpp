@@ -941,7 +941,8 @@ void wdec_run(Tensor layers, Tensor roles, std::vector<Tensor> bufs, std::vector
   p.slots = bufs[8].data_ptr<int64_t>();
   p.block_table = bufs[9].data_ptr<int>();
   p.cross_table = bufs[10].data_ptr<int>();
-  TORCH_CHECK(bufs[11].numel() >= 2 * 1025, "wdec_run: counter words (uncached, >= 1025 u64)");
+  TORCH_CHECK(bufs[11].numel() >= 2 * (1280 + 16 * ints[2]),
+              "wdec_run: counter words (uncached: levels, error word, sampler, per-head QKV counters)");
   p.cnt = reinterpret_cast<unsigned long long*>(bufs[11].data_ptr());
   for (int l = 0; l < kWdLevels; ++l) {
     TORCH_CHECK(n_prod[(size_t)l] > 0, "wdec_run: every level needs a producer");

@@ -70,6 +70,7 @@ constexpr int kLds = 163840;
 constexpr int kMaxChunk = 384;
 constexpr int kSpinLimit = 1 << 17;  // bounded polls: a non-resident producer ends the launch, not the GPU
 constexpr int kErrWord = 1024;       // (WdecParams::cnt u64 index of the error flag)
+constexpr int kHeadCnt = 1280;      // (u64 index: per-head QKV completion counters, 128 B apart, <= 48 heads)
 constexpr int kSmpCnt = 1152;       // (u64 index: the fused sampler's arrival counters, 8 groups x 128 B, monotonic)
 
 VWA_DEVICE int level_of(int gm) {
@@ -161,6 +162,34 @@ VWA_DEVICE void wd_arrive(const WdecParams& p, int lvl) {
   lds_sync();
   if (VWA_TX == 0)
     __hip_atomic_fetch_add(gp(lvl_cnt(p, lvl) + 16 * (blockIdx.x & 7)), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// QKV -> self-attention by head: the workgroup of QKV tile t adds 1 to the counter of head
+// (t / 4) mod H (its 16 columns are 16 of that head's 64 q, k or v dims); the attention of head h
+// waits for its 12 tiles only, not for all 3 d / 16
+VWA_DEVICE unsigned long long* head_cnt(const WdecParams& p, int h) { return p.cnt + kHeadCnt + 16 * h; }
+VWA_DEVICE void wd_arrive_head(const WdecParams& p, int tile) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_sync();
+  if (VWA_TX == 0)
+    __hip_atomic_fetch_add(gp(head_cnt(p, (tile >> 2) % p.H)), 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+VWA_DEVICE void wd_wait_head(const WdecParams& p, int h, unsigned long long target) {
+  if (VWA_TX < 64) {
+    const unsigned long long* c = head_cnt(p, h);
+    int spins = 0;
+    while (true) {
+      unsigned long long v;
+      asm volatile("s_load_dwordx2 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(c) : "memory");
+      if ((long long)(v - target) >= 0) break;
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > kSpinLimit) {
+        if (VWA_TX == 0) set_err(p);
+        break;
+      }
+    }
+  }
+  lds_sync();
 }
 
 // diagnostic stamp k of (layer, level) (tools/wdec_probe.py): 0 entry, 1 released, 2 row staged
@@ -681,6 +710,7 @@ VWA_DEVICE void wd_lm_epilogue(const WdecParams& p, int tl0, int tl1, int nt, co
 constexpr int kOptNoEpiPre = 1;    // load the epilogue operands after the row (not ahead of it)
 constexpr int kOptNoSattnPre = 2;  // self-attention resolves its key addresses after its inputs landed
 constexpr int kOptXqxIdle = 4;     // (diagnostic, wrong results) the x part of the cross query does no work
+constexpr int kOptQkvLevel = 8;    // QKV -> self-attention through the whole level's counters, not per head
 
 __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -718,6 +748,16 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
   lds_sync();
   // (the fused sampler's arrival counters: base of this launch, read by workgroup 0's wave 0 --
   // before any workgroup can arrive there, which needs every level, workgroup 0's included)
+  // (the self-attention head's counter: 12 tiles per layer, n_layers per launch)
+  unsigned long long hbase = 0;
+  const bool by_head = !(opt & kOptQkvLevel);
+  if (by_head && sattn >= 0 && VWA_TX < 64) {
+    const unsigned long long inc = 12ull * (unsigned long long)NL;
+    unsigned long long v;
+    const unsigned long long* c = head_cnt(p, sattn);
+    asm volatile("s_load_dwordx2 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(c) : "memory");
+    hbase = v / inc * inc;
+  }
   unsigned long long smp_base = 0;
   if (p.smp_mask && blockIdx.x == 0 && VWA_TX < 64) {
     const unsigned long long inc = (unsigned long long)gridDim.x;
@@ -782,6 +822,8 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
       if (lvl == LV_XATT) wd_wait(p, LV_XQX, target(LV_XQX, li));
       if (lvl == LV_QKV || (lvl == LV_XQX && !(work & 1))) {
         if (li > 0) wd_wait(p, LV_FC2, target(LV_FC2, li - 1));
+      } else if (lvl == LV_SATT && by_head) {
+        wd_wait_head(p, sattn, hbase + 12ull * (unsigned long long)(li + 1));
       } else if (lvl != LV_XQX) {
         const int pl = lvl == LV_SATT ? LV_QKV : lvl - 1;
         wd_wait(p, pl, target(pl, li));
@@ -825,7 +867,8 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
         }
         wd_epilogue(p, li, tg[0], tg[1], tl[0], tl[1], nt, acc0, acc1, lds, xout, eb, ec, er);
       }
-      wd_arrive(p, lvl);
+      if (lvl == LV_QKV && by_head) wd_arrive_head(p, tile[0]);  // (the QKV tile sits in slot 0)
+      else wd_arrive(p, lvl);
       wd_stamp(p, li, lvl, 3);
       // refills a layer ahead
 #pragma unroll
