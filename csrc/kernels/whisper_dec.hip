@@ -710,7 +710,8 @@ VWA_DEVICE void wd_lm_epilogue(const WdecParams& p, int tl0, int tl1, int nt, co
 constexpr int kOptNoEpiPre = 1;    // load the epilogue operands after the row (not ahead of it)
 constexpr int kOptNoSattnPre = 2;  // self-attention resolves its key addresses after its inputs landed
 constexpr int kOptXqxIdle = 4;     // (diagnostic, wrong results) the x part of the cross query does no work
-constexpr int kOptQkvLevel = 8;    // QKV -> self-attention through the whole level's counters, not per head
+constexpr int kOptQkvByHead = 8;   // (opt-in) QKV -> self-attention through per-head counters: ~8 us per
+                                   // launch faster, but one GPU-test mismatch on a box was not explained
 
 __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -750,7 +751,7 @@ __global__ __launch_bounds__(kT) void wdec_kernel(WdecParams p) {
   // before any workgroup can arrive there, which needs every level, workgroup 0's included)
   // (the self-attention head's counter: 12 tiles per layer, n_layers per launch)
   unsigned long long hbase = 0;
-  const bool by_head = !(opt & kOptQkvLevel);
+  const bool by_head = (opt & kOptQkvByHead) != 0;
   if (by_head && sattn >= 0 && VWA_TX < 64) {
     const unsigned long long inc = 12ull * (unsigned long long)NL;
     unsigned long long v;

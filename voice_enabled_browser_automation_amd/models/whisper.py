@@ -581,7 +581,7 @@ class WhisperModel:
                            [bufs.hidden, bufs.h, bufs.q, bufs.att, bufs.f, st["xpart"], bufs.seq_ids, bufs.ctx_lens,
                             bufs.slots, bufs.block_table, bufs.cross_table, st["cnt"]],
                            st["ints"], self.cfg.ln_eps, self.hd ** -0.5, st["n_prod"], st.get("ts"),
-                           int(st.get("opt", 0)), lm, emb, smp, base_block)
+                           int(st.get("opt", ops.env_int("VWA_WDEC_OPT"))), lm, emb, smp, base_block)
         return bufs.logits[:1]
 
     def wdec_loop_step(self, bufs, mask: torch.Tensor, tok: torch.Tensor, step: torch.Tensor, out: torch.Tensor,
