@@ -1,5 +1,8 @@
 // Persistent Whisper decoder step (any Whisper width: d a multiple of 128 up to 1536, ffn = 4 d,
-// head_dim 64 -- tiny 384 .. large 1280), one row: ONE launch for every decoder layer.
+// head_dim 64 -- tiny 384 .. large 1280), one row: ONE launch for the whole token step -- the
+// embedding (layer 0 builds it from the tables), every decoder layer, the LM head (a last level
+// streaming the vocabulary tiles through the slots) and, in the device loop, the greedy masked
+// argmax + the loop advance (workgroup 0 merges the workgroups' partials).
 //
 // Why: the per-kernel decoder runs eight dependent launches per
 // layer, each ~5-9 us of fixed latency (dispatch, X staging, the first weight bytes, reduce,
@@ -21,6 +24,7 @@
 //   5 XO       x2 = x1 + merge(partials) . Wxo^T + b              (80 tiles; the merge is the X staging)
 //   6 FC1      f = GELU(LN2(x2) . W1^T + b1)                      (320 tiles)
 //   7 FC2      x3 = x2 + f . W2^T + b2                            (80 tiles, K = 5120)
+// (tile counts for whisper-large; QKV -> SATT optionally through per-head counters, kOptQkvByHead)
 // LayerNorms are folded into the weights (ops.fold_layernorm: y = rstd (x.Wg - mean c) + b'), the
 // mean / rstd come from the staged row.  The cross query needs x1 = x + att Wo^T + bo, so by
 // linearity x1 Wg^T = x Wg^T + att (Wg Wo)^T + Wg bo: its x part runs while the self-attention
