@@ -446,8 +446,11 @@ class WhisperModel:
         w = self.chain_error_word()
         if w is not None and int(w.item()) != 0:
             return True
-        w = self.wdec_error_word()
-        return bool(w is not None and int(w.item()) != 0)
+        # every persistent-decoder state (one per runner's buffers) has its own error word
+        for st in list(getattr(self, "_wdec", {}).values()) if getattr(self, "_wdec", None) else []:
+            if st is not None and int(st["cnt"].view(torch.int64)[1024].item()) != 0:
+                return True
+        return False
 
     def _chain_descs(self, bufs, M: int, li: int):
         """Layer li's two chained launches for these buffers, built on first use:
@@ -556,8 +559,12 @@ class WhisperModel:
             L._xq_o = (ops.TiledWeight(w), b)
         return L._xq_o
 
-    def wdec_error_word(self):
-        st = next(iter(getattr(self, "_wdec", {}).values()), None) if getattr(self, "_wdec", None) else None
+    def wdec_error_word(self, bufs=None):
+        """The error word of the persistent decoder's state for ``bufs`` (default: the first one)."""
+        d = getattr(self, "_wdec", None)
+        if not d:
+            return None
+        st = d.get(bufs) if bufs is not None else next(iter(d.values()), None)
         return None if st is None else st["cnt"].view(torch.int64)[1024:1025]
 
     def _wdec_emb_ok(self, bufs) -> bool:
