@@ -135,7 +135,7 @@ class Settings(BaseModel):
     VWA_CHAIN_RETRY: bool = Field(True, description="re-arm the chain after a barrier-timeout fallback")
     VWA_CHAIN_ASR: bool = Field(False, description="chained Whisper decoder launches (measured slower; off)")
     VWA_WDEC_OPT: int = Field(0, description="diagnostic: schedule option bits of the persistent Whisper decoder (whisper_dec.hip kOpt*; 0 = the measured defaults)")
-    VWA_ASR_PERSIST: bool = Field(True, description="one-row Whisper-large decode steps as ONE persistent launch over every decoder layer (csrc/kernels/whisper_dec.hip); needs every CU free: off when the GPU is shared with a persistent brain launch")
+    VWA_ASR_PERSIST: bool = Field(True, description="one-row Whisper decode steps (every width, tiny .. large) as ONE persistent launch: embedding, every decoder layer, LM head and, in the device loop, argmax + advance (csrc/kernels/whisper_dec.hip); needs every CU free: off when the GPU is shared with a persistent brain launch")
     VWA_CHAIN_GRID_DIV: Optional[str] = Field(None, description="chained launch on CUs / k workgroups (shared GPU)")
     VWA_CHAIN_PLAN: bool = Field(True, description="chained attention: layer 0 writes the step's work plan, layers 1.. read it")
     VWA_CHAIN_MULTI: bool = Field(True, description="chained decode: all layers in ONE launch (skinny_stream.hip chain_kernel MULTI)")
