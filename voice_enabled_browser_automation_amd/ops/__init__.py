@@ -427,7 +427,10 @@ def scratch(device, name: str, numel: int, dtype=torch.float32) -> torch.Tensor:
 GEMM_WS_FLOATS = 32 << 20  # split-K workspace (128 MB per device: 4 f32 slices of a 1k x 4096 output)
 # (a one-launch split-K -- the last slice of each tile reducing -- measured no faster at 32 decode
 # rows: the write-through drain + ticket + L2-missing partial loads cost what the reduce launch
-# does, fp8 o / down 26.3 vs 20.2 + 5.2 us, profiles/r4_gemm_one_launch_ab.md; removed in round 5)
+# does, fp8 o / down 26.3 vs 20.2 + 5.2 us, profiles/r4_gemm_one_launch_ab.md; removed in round 5.
+# Round 6: the reduce loading all 8 slabs of an 8-way split in ONE batch instead of two batches of
+# 4 -- same bits -- measured 0.3-1.6 % slower whole steps at 32-64 rows, fp8 and bf16,
+# profiles/r6_reduce_one_batch_rejected_*.jsonl; not kept)
 
 
 _GEMM_EPI = {"none": 0, "resid": 1, "swiglu": 2, "gelu": 3}
